@@ -1,0 +1,200 @@
+"""Headline benchmark (BASELINE.json metric "bins/sec (NxN matrix)").
+
+A step = one TADpole()-equivalent pipeline over one synthetic N0 x N0 Hi-C
+matrix already resident in HBM: NA->0 + symmetrise, bad-column mask, Pearson
+correlation, PCA to max_pcs, CONISS sweep over every PC prefix, broken stick,
+Calinski-Harabasz, parameter choice, TAD coordinates of every significant level.
+Workload = BASELINE.json configs[1] (C2: synthetic 2000 x 2000, max_pcs=200).
+
+Multi-GPU: one process per GPU (torch.distributed.run); each rank processes its
+own matrix (independent chromosomes): weak scaling, no
+data-path collective.  value = bins of all ranks / max-over-ranks time.
+
+Extra fields: "roofline" for the dominant kernel (HIP events inside the
+library, same stream), "cpu_baseline" (the CPU oracle on this host, rank 0),
+"parity" (rank 0's TAD boundaries vs the oracle on the same matrix).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+FP64_MFMA_PEAK_TFLOPS = 78.6     # MI355X FP64 matrix, dense (AMD spec)
+HBM_PEAK_GBS = 8000.0            # MI355X HBM3E (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n0", type=int, default=2000)
+    ap.add_argument("--max-pcs", type=int, default=200)
+    ap.add_argument("--min-clusters", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-reps", type=int, default=3)
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+    torch.cuda.set_device(local)
+
+    import tadpole_amd as tp
+    from tadpole_amd import _lib
+    from tadpole_amd.api import _assemble
+    from tadpole_amd.synth import SEED_BASE, synth_hic
+
+    L = _lib.load()
+    n0 = args.n0
+    seed = SEED_BASE + 2 + 1000 * rank
+    host = synth_hic(n0, seed)
+    dev_m = torch.from_numpy(host).to(f"cuda:{local}")
+    stream = torch.cuda.current_stream()
+
+    k_cap = max(1, min(args.max_pcs, n0))
+    w_cap = n0
+    bufs = dict(bad=np.zeros(n0, np.int32), good=np.zeros(n0, np.int32),
+                nclu=np.zeros(k_cap, np.int32), scores=np.zeros(k_cap * w_cap),
+                merge=np.zeros(2 * (n0 - 1), np.int32), height=np.zeros(n0 - 1),
+                boundary=np.zeros(n0 - 1, np.int32), timings=np.zeros(16))
+    I = ctypes.c_int
+
+    def step(want_timings: bool):
+        b = bufs
+        outs = [I(0) for _ in range(6)]
+        n_good, k, w, n_pcs, n_clusters, st = outs
+        L.tp_pipeline_dev(ctypes.c_void_p(dev_m.data_ptr()), ctypes.byref(I(n0)), ctypes.byref(I(args.max_pcs)),
+                          ctypes.byref(I(args.min_clusters)), ctypes.byref(ctypes.c_double(0.01)),
+                          ctypes.byref(I(_lib.TP_FLAG_ROW_MAJOR)), ctypes.byref(I(local)),
+                          ctypes.c_void_p(stream.cuda_stream), ctypes.byref(I(k_cap)), ctypes.byref(I(w_cap)),
+                          _lib.ip(b["bad"]), ctypes.byref(n_good), _lib.ip(b["good"]), ctypes.byref(k),
+                          _lib.ip(b["nclu"]), _lib.dp(b["scores"]), ctypes.byref(w), ctypes.byref(n_pcs),
+                          ctypes.byref(n_clusters), _lib.ip(b["merge"]), _lib.dp(b["height"]),
+                          _lib.ip(b["boundary"]), _lib.dp(b["timings"]) if want_timings else None,
+                          ctypes.byref(st))
+        _lib.check(st)
+        n = n_good.value
+        kk, ww = k.value, w.value
+        res = dict(bad=b["bad"].astype(bool), good=b["good"][:n].copy(), k=kk, w=ww,
+                   scores=b["scores"][:kk * ww].reshape(ww, kk).T.copy(), n_pcs=n_pcs.value,
+                   n_clusters=n_clusters.value,
+                   merge=b["merge"][:2 * (n - 1)].reshape(2, n - 1).T.copy(), height=b["height"][:n - 1].copy(),
+                   boundary=b["boundary"][:n - 1].copy(), timings=b["timings"].copy())
+        return _assemble(res, np.flatnonzero(res["bad"]) + 1)
+
+    for _ in range(args.warmup):
+        step(False)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    last = None
+    for _ in range(args.steps):
+        last = step(False)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # one more instrumented step for the per-kernel breakdown (not in `value`)
+    prof = step(True)
+    tm = prof.timings_ms
+    n = int(tm[14])
+    k = int(tm[15])
+
+    if rank == 0:
+        value = n0 * world * args.steps / elapsed
+        # ---- roofline of the dominant kernel
+        kern = {
+            "xtx_gemm": (tm[5], "mfma", 1, float(n) ** 3),                      # N^3 (symmetric half)
+            "xcxc_gemm": (tm[6], "mfma", 1, float(n) ** 3),
+            "gq_gemm": (tm[7], "mfma", max(1, int(tm[8])), 2.0 * n * n * int(tm[12]) if tm[12] else 0.0),
+            "coniss": (tm[9], "hbm", 1, 40.0 * (n - 1) * k * (k + 1) / 2.0),    # bytes: 5 sum vectors/merge
+            "ch": (tm[10], "hbm", 1, 16.0 * n * k * k),                         # bytes: 2 passes/tree
+        }
+        dom = max(kern, key=lambda q: kern[q][0])
+        ms_tot, bound, launches, per_launch = kern[dom]
+        avg_ms = ms_tot / launches
+        if bound == "mfma":
+            achieved = per_launch / (avg_ms * 1e-3) / 1e12
+            peak, unit = FP64_MFMA_PEAK_TFLOPS, "TFLOP/s"
+        else:
+            achieved = per_launch / (avg_ms * 1e-3) / 1e9
+            peak, unit = HBM_PEAK_GBS, "GB/s"
+        roof = {"kernel": dom, "bound": bound, "achieved": round(achieved, 3), "peak": peak, "unit": unit,
+                "frac": round(achieved / peak, 5), "traffic": None, "avg_launch_ms": round(avg_ms, 4),
+                "launches_per_step": launches,
+                "breakdown_ms": {q: round(kern[q][0], 4) for q in kern},
+                "stages_ms": {"mask": round(tm[0], 3), "cor": round(tm[1], 3), "pca": round(tm[2], 3),
+                              "sweep": round(tm[3], 3), "total": round(tm[4], 3)},
+                "pca": {"iters": int(tm[11]), "block": int(tm[12]), "resid": float(tm[13])}}
+        out = {"metric": "bins/sec (NxN matrix) at 1/2/4/8 GPUs; TAD boundary bit-match vs R ref",
+               "value": round(value, 2), "unit": "bins/s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+               "data": "synthetic (SURVEY.md §8(d) Hi-C generator, seed 20261015+2+1000*rank)",
+               "config": {"workload": f"C2: synthetic {n0}x{n0} Hi-C matrix per GPU, max_pcs={args.max_pcs}",
+                          "n0": n0, "n_good": n, "k": k, "max_pcs": args.max_pcs,
+                          "parallelism": f"one matrix per GPU x{world}"},
+               "roofline": roof}
+        if not args.no_cpu_baseline:
+            sys.path.insert(0, os.path.join(HERE, "oracle"))
+            import tadpole_oracle as O
+            threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+            t1 = time.perf_counter()
+            ref = None
+            for _ in range(args.cpu_reps):
+                ref = O.tadpole(host, max_pcs=args.max_pcs, min_clusters=args.min_clusters, nthreads=threads)
+            cpu_s = (time.perf_counter() - t1) / args.cpu_reps
+            out["cpu_baseline"] = {"value": round(n0 / cpu_s, 2), "unit": "bins/s", "cores": threads,
+                                   "kind": "port",
+                                   "sample": f"{args.cpu_reps} full C2 pipelines (numpy LAPACK SVD + C sweep, "
+                                             f"OpenMP over PC prefixes), {cpu_s:.3f} s each"}
+            same = (last.n_pcs == ref.n_pcs and last.optimal_n_clusters == ref.optimal_n_clusters
+                    and set(last.clusters) == {str(q) for q in ref.clusters}
+                    and all(np.array_equal(last.clusters[str(q)], v) for q, v in ref.clusters.items()))
+            a, b = last.scores, ref.scores
+            fin = ~np.isnan(b)
+            rel = float(np.max(np.abs(a[fin] - b[fin]) / np.abs(b[fin]))) if a.shape == b.shape else None
+            out["parity"] = {"boundaries_match_oracle": bool(same), "n_pcs": [last.n_pcs, ref.n_pcs],
+                             "n_clusters": [last.optimal_n_clusters, ref.optimal_n_clusters],
+                             "ch_max_rel_err": rel}
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    L.tp_shutdown()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,164 @@
+/*
+ * tadpole_hip.h — C ABI of libtadpole_hip.so, the MI355X (gfx950) engine for
+ * TADpole's per-matrix hot path.
+ *
+ * The reference (3DGenomes/TADpole, R) has no FFI of its own: its seam is the R
+ * function body R/TADpole.R:444-460, which these entry points replace
+ *
+ *   load_mat mask        R/TADpole.R:19-20,35-37,88-89   -> tp_mask
+ *   sparse_cor + NaN->0  R/TADpole.R:94-100,448-449       -> tp_cor
+ *   prcomp(cor, rank.)   R/TADpole.R:452-453              -> tp_pca
+ *   find_params          R/TADpole.R:102-140,456          -> tp_sweep
+ *   chclust(dist(pcs))   R/TADpole.R:108,459-460          -> tp_coniss
+ *   dist(pcs)            R/TADpole.R:108,460              -> tp_dist
+ *   calinhara(x, cutree) R/TADpole.R:117-120              -> tp_ch
+ *   the whole seam       R/TADpole.R:348-349,444-468      -> tp_pipeline
+ *
+ * Calling convention (so R's .C() can bind every entry without R headers, and
+ * Python ctypes in the tests): every argument is a pointer; matrices are
+ * column-major unless a layout flag says otherwise; logical = int; the caller
+ * allocates every output; 1-based indices only where R would see them (merge
+ * matrix, n_pcs, n_clusters).  NA in double outputs is R's NA_real_ bit
+ * pattern (0x7FF00000000007A2), so R reads NA, not NaN.
+ *
+ * Status: every entry writes *status (0 = TP_OK).  On failure the message is
+ * available from tp_last_error / tp_last_error_r (per thread).  A missing GPU
+ * or HIP runtime is an error (TP_ERR_HIP): there is no CPU fallback.
+ *
+ * Device pointers: the *_dev variants take device-resident inputs (e.g. from a
+ * torch tensor) and a hipStream_t (as void*, NULL = the library stream of that
+ * device); their outputs are host pointers unless named d_*.
+ */
+#ifndef TADPOLE_HIP_H
+#define TADPOLE_HIP_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+    TP_OK = 0,
+    TP_ERR_ARG = 1,         /* bad sizes / arguments                              */
+    TP_ERR_HIP = 2,         /* HIP runtime / device failure                       */
+    TP_ERR_NO_BSTICK = 3,   /* a tree has no broken-stick level: R errors in
+                               rep(NA, n_cluster) at R/TADpole.R:115            */
+    TP_ERR_CAPACITY = 4,    /* an output array is too small (see *_cap args)     */
+    TP_ERR_NUMERIC = 5,     /* PCA did not converge / non-finite scores          */
+    TP_ERR_UNSUPPORTED = 6  /* size beyond what this build handles               */
+};
+
+/* flags for tp_pipeline / tp_mask */
+#define TP_FLAG_ROW_MAJOR   1   /* input matrix buffer is row-major (numpy C order) */
+#define TP_FLAG_CLEAN       2   /* input is already NA-free and symmetric          */
+#define TP_FLAG_NO_MASK     4   /* keep every bin: the per-arm matrices of
+                                   R/TADpole.R:362 are correlated as given        */
+
+/* ---------------------------------------------------------------- runtime */
+int  tp_version(void);                          /* ABI version, 1                */
+int  tp_device_count(void);                     /* HIP devices visible (>=0)     */
+void tp_shutdown(void);                         /* free every device context     */
+int  tp_last_error(char *buf, int len);         /* ctypes form                   */
+void tp_last_error_r(char **buf, int *len);     /* R .C form                     */
+
+/* ------------------------------------------------------------------- mask */
+/* R/TADpole.R:19-20 (NA->0, forceSymmetric(uplo='U')), :35-37 (rowMeans, diag==0,
+ * quantile type 7 at bad_frac), :88-89 (subset).  M: n0 x n0.  Outputs:
+ * bad[n0] (logical), rowmean[n0] (may be NULL), *n_good, good_idx[n0] (1-based
+ * original indices of kept bins, first *n_good entries valid). */
+void tp_mask(const double *M, const int *n0, const double *bad_frac,
+             const int *flags, const int *device, int *bad, double *rowmean,
+             int *n_good, int *good_idx, int *status);
+
+/* -------------------------------------------------------------------- cor */
+/* sparse_cor(x)$cor with NaN -> 0 (R/TADpole.R:94-100,449).  X: n x n
+ * symmetric (column-major), cor: n x n. */
+void tp_cor(const double *X, const int *n, const int *device, double *cor,
+            int *status);
+
+/* -------------------------------------------------------------------- pca */
+/* prcomp(C, rank. = k)$x (R/TADpole.R:452-453): P = (C - 1 colMeans(C)') V_k,
+ * V_k the top-k right singular vectors.  C: n x n symmetric.  P: n x k.
+ * sdev (length k, may be NULL) = singular values / sqrt(n-1) as prcomp. */
+void tp_pca(const double *C, const int *n, const int *k, const int *device,
+            double *P, double *sdev, int *status);
+
+/* ------------------------------------------------------------------ sweep */
+/* find_params (R/TADpole.R:102-140) on scores P (n x k, column-major):
+ * for i = 1..k: CONISS on P[,1:i], broken stick -> n_cluster[i-1], CH on all k
+ * columns for n = min(min_clusters, n_cluster)..n_cluster.
+ * scores: k x w_cap column-major (NA where R has NA), *w = max n_cluster,
+ * *n_pcs / *n_clusters = which.max(rowMeans(scores, na.rm=TRUE)) / which.max
+ * of that row (1-based).  merge (2 x (n-1) ints, R merge matrix column-major)
+ * and height (n-1) describe the tree of n_pcs (the dendrogram R re-computes
+ * at R/TADpole.R:459-460); either may be NULL. */
+void tp_sweep(const double *P, const int *n, const int *k,
+              const int *min_clusters, const int *device, const int *w_cap,
+              int *n_cluster, double *scores, int *w, int *n_pcs,
+              int *n_clusters, int *merge, double *height, int *status);
+
+/* ----------------------------------------------------------------- coniss */
+/* rioja::chclust(dist(P), method="coniss") (R/TADpole.R:108): P n x ncols.
+ * merge: (n-1) x 2 column-major hclust encoding (negative = singleton),
+ * height (n-1): cumulative total within-cluster dispersion.
+ * boundary (n-1, may be NULL): 1-based index of the first bin of the right
+ * cluster of each merge (the boundary it removes). */
+void tp_coniss(const double *P, const int *n, const int *ncols,
+               const int *device, int *merge, double *height, int *boundary,
+               int *status);
+
+/* ------------------------------------------------------------------- dist */
+/* stats::dist(P) euclidean, R's accumulation order: d has n(n-1)/2 entries,
+ * lower triangle by columns (the R "dist" vector). */
+void tp_dist(const double *P, const int *n, const int *ncols,
+             const int *device, double *d, int *status);
+
+/* --------------------------------------------------------------------- ch */
+/* fpc::calinhara(P, labels, cn) (R/TADpole.R:119) for contiguous labels
+ * 1..cn (as cutree gives on a constrained tree).  P n x k. */
+void tp_ch(const double *P, const int *n, const int *k, const int *labels,
+           const int *cn, const int *device, double *ch, int *status);
+
+/* --------------------------------------------------------------- pipeline */
+/* The whole seam: mask -> cor -> pca -> sweep -> tree of n_pcs.
+ * M: n0 x n0 raw matrix (NA allowed unless TP_FLAG_CLEAN).
+ * Outputs (caller-allocated):
+ *   bad[n0], *n_good, good_idx[n0] (1-based original indices)
+ *   *k = min(max_pcs, n_good), n_cluster[k_cap], scores[k_cap * w_cap]
+ *   (k x w column-major, leading dimension *k), *w
+ *   *n_pcs, *n_clusters (1-based), merge[2*(n0-1)] and height[n0-1] of the
+ *   final tree (first n_good-1 rows valid), boundary[n0-1] (1-based, may be
+ *   NULL), timings_ms[16] (may be NULL; when given, HIP events time:
+ *   [0] mask+subset [1] cor [2] pca [3] sweep [4] total (ms), kernels
+ *   [5] X'X GEMM [6] Xc'Xc GEMM [7] sum of G*Q GEMMs [8] their count
+ *   [9] CONISS [10] CH, and [11] PCA iterations [12] block [13] residual
+ *   [14] n_good [15] k). */
+void tp_pipeline(const double *M, const int *n0, const int *max_pcs,
+                 const int *min_clusters, const double *bad_frac,
+                 const int *flags, const int *device, const int *k_cap,
+                 const int *w_cap, int *bad, int *n_good, int *good_idx,
+                 int *k, int *n_cluster, double *scores, int *w, int *n_pcs,
+                 int *n_clusters, int *merge, double *height, int *boundary,
+                 double *timings_ms, int *status);
+
+/* Same, input already on the device (d_M, n0 x n0, may be overwritten when
+ * TP_FLAG_CLEAN is not set) and work queued on `stream` (hipStream_t). */
+void tp_pipeline_dev(const double *d_M, const int *n0, const int *max_pcs,
+                     const int *min_clusters, const double *bad_frac,
+                     const int *flags, const int *device, void *stream,
+                     const int *k_cap, const int *w_cap, int *bad,
+                     int *n_good, int *good_idx, int *k, int *n_cluster,
+                     double *scores, int *w, int *n_pcs, int *n_clusters,
+                     int *merge, double *height, int *boundary,
+                     double *timings_ms, int *status);
+
+/* Device-resident stage entry points for tests and benches (d_* = device). */
+void tp_sweep_dev(const double *d_P, const int *n, const int *k,
+                  const int *min_clusters, const int *device, void *stream,
+                  const int *w_cap, int *n_cluster, double *scores, int *w,
+                  int *mrg_a_all, int *mrg_b_all, double *cost_all,
+                  double *height_all, int *status);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TADPOLE_HIP_H */

@@ -1,0 +1,120 @@
+"""ctypes binding of libtadpole_hip.so (include/tadpole_hip.h).
+
+The library is the product: there is no CPU path behind it.  Loading fails
+loudly when the shared object is missing; calls fail with TadpoleError when no
+HIP device is present.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libtadpole_hip.so")
+
+TP_OK, TP_ERR_ARG, TP_ERR_HIP, TP_ERR_NO_BSTICK, TP_ERR_CAPACITY, TP_ERR_NUMERIC, TP_ERR_UNSUPPORTED = range(7)
+TP_FLAG_ROW_MAJOR = 1
+TP_FLAG_CLEAN = 2
+TP_FLAG_NO_MASK = 4
+
+#: every symbol include/tadpole_hip.h declares
+EXPORTS = (
+    "tp_version", "tp_device_count", "tp_shutdown", "tp_last_error", "tp_last_error_r",
+    "tp_mask", "tp_cor", "tp_pca", "tp_sweep", "tp_coniss", "tp_dist", "tp_ch",
+    "tp_pipeline", "tp_pipeline_dev", "tp_sweep_dev",
+)
+
+
+class TadpoleError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"[status {status}] {msg}")
+        self.status = status
+
+
+_lib = None
+
+_I = ctypes.POINTER(ctypes.c_int)
+_D = ctypes.POINTER(ctypes.c_double)
+_V = ctypes.c_void_p
+
+
+def load() -> ctypes.CDLL:
+    """Load libtadpole_hip.so.
+
+    One HIP runtime per process: torch-ROCm bundles its own libamdhip64.so.7
+    (same SONAME as /opt/rocm's).  Importing torch first makes our DT_NEEDED
+    entries bind to the runtime torch already mapped, so device pointers and
+    streams from torch tensors are valid in the library.  Without torch (R,
+    plain C) the library binds to /opt/rocm.
+    """
+    global _lib
+    if _lib is not None:
+        return _lib
+    try:
+        import torch  # noqa: F401  (maps torch's HIP runtime before ours)
+    except ImportError:
+        pass
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(make -C tadpole_amd/csrc).  There is no CPU fallback.")
+    L = ctypes.CDLL(LIB_PATH)
+    L.tp_version.restype = ctypes.c_int
+    L.tp_device_count.restype = ctypes.c_int
+    L.tp_last_error.restype = ctypes.c_int
+    L.tp_last_error.argtypes = [ctypes.c_char_p, ctypes.c_int]
+    L.tp_mask.argtypes = [_D, _I, _D, _I, _I, _I, _D, _I, _I, _I]
+    L.tp_cor.argtypes = [_D, _I, _I, _D, _I]
+    L.tp_pca.argtypes = [_D, _I, _I, _I, _D, _D, _I]
+    L.tp_sweep.argtypes = [_D, _I, _I, _I, _I, _I, _I, _D, _I, _I, _I, _I, _D, _I]
+    L.tp_coniss.argtypes = [_D, _I, _I, _I, _I, _D, _I, _I]
+    L.tp_dist.argtypes = [_D, _I, _I, _I, _D, _I]
+    L.tp_ch.argtypes = [_D, _I, _I, _I, _I, _I, _D, _I]
+    L.tp_pipeline.argtypes = [_D, _I, _I, _I, _D, _I, _I, _I, _I, _I, _I, _I, _I, _I, _D, _I, _I, _I,
+                              _I, _D, _I, _D, _I]
+    L.tp_pipeline_dev.argtypes = [_V, _I, _I, _I, _D, _I, _I, _V, _I, _I, _I, _I, _I, _I, _I, _D, _I,
+                                  _I, _I, _I, _D, _I, _D, _I]
+    L.tp_sweep_dev.argtypes = [_V, _I, _I, _I, _I, _V, _I, _I, _D, _I, _I, _I, _D, _D, _I]
+    _lib = L
+    return L
+
+
+def last_error() -> str:
+    L = load()
+    buf = ctypes.create_string_buffer(1024)
+    L.tp_last_error(buf, 1024)
+    return buf.value.decode(errors="replace")
+
+
+def check(status: ctypes.c_int):
+    if status.value != TP_OK:
+        raise TadpoleError(status.value, last_error())
+
+
+def ip(x):
+    """int* to a scalar c_int or an int32 ndarray (None -> NULL)."""
+    if x is None:
+        return None
+    if isinstance(x, ctypes.c_int):
+        return ctypes.pointer(x)
+    assert x.dtype == np.int32 and x.flags["C_CONTIGUOUS"] or x.flags["F_CONTIGUOUS"]
+    return x.ctypes.data_as(_I)
+
+
+def dp(x):
+    if x is None:
+        return None
+    if isinstance(x, ctypes.c_double):
+        return ctypes.pointer(x)
+    assert x.dtype == np.float64
+    return x.ctypes.data_as(_D)
+
+
+def cint(v: int) -> ctypes.c_int:
+    return ctypes.c_int(int(v))
+
+
+def cdbl(v: float) -> ctypes.c_double:
+    return ctypes.c_double(float(v))

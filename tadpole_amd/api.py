@@ -1,0 +1,431 @@
+"""Host-side mirror of the reference R API (NAMESPACE:3-8): ``TADpole``,
+``load_mat``, ``diffT``, ``random_bed`` and the ``tadpole`` result object.
+
+The numeric hot path (mask, correlation, PCA, CONISS sweep, broken stick,
+Calinski-Harabasz) runs in ``libtadpole_hip.so`` on the GPU; this module does
+what the R host code does around it: file parsing, the NA-padded result
+assembly, cutree, bad-column re-insertion and ``fix_values`` (R/TADpole.R:
+470-510), the centromere arm split (R/TADpole.R:58-85, 351-442), and diffT.
+Plots (``load_mat``'s levelplot/histogram, ``plot_hierarchy``, ``CH_map``) are
+out of scope: they draw, they do not compute.
+"""
+from __future__ import annotations
+
+import ctypes
+import struct
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import TadpoleError, cdbl, cint, dp, ip
+
+NA_BITS = 0x7FF00000000007A2
+NA_REAL = struct.unpack("<d", struct.pack("<Q", NA_BITS))[0]
+
+
+def is_na(x) -> np.ndarray:
+    """R ``is.na`` on a score matrix: NA and NaN."""
+    return np.isnan(np.asarray(x, np.float64))
+
+
+def is_r_na(x) -> np.ndarray:
+    """True only where the value carries R's NA_real_ bits (not NaN)."""
+    return np.asarray(x, np.float64).view(np.uint64) == np.uint64(NA_BITS)
+
+
+# ------------------------------------------------------------------ objects
+
+@dataclass
+class Chclust:
+    """``rioja::chclust`` object (class c("chclust", "hclust")): what
+    ``plot_hierarchy`` feeds to ``cutree`` / ``ggdendro::dendro_data``."""
+    merge: np.ndarray            # (n-1) x 2 int, hclust encoding
+    height: np.ndarray           # n-1 cumulative total dispersion
+    order: np.ndarray            # 1..n
+    labels: List[str]            # original bin indices
+    boundary: np.ndarray         # 1-based first bin (in 1..n) of the right cluster per merge
+    method: str = "coniss"
+    dist_method: str = "euclidean"
+    call: str = "rioja::chclust(d = dist(pcs))"
+
+    @property
+    def n(self) -> int:
+        return len(self.order)
+
+    def cutree(self, k: int) -> np.ndarray:
+        """``stats::cutree(tree, k)``: labels 1..k in observation order."""
+        n = self.n
+        lab = np.ones(n, np.int64)
+        if k > 1:
+            b = np.sort(self.boundary[n - k:] - 1)
+            lab[b] += 1
+            lab = np.cumsum(lab) - np.arange(n)
+        return lab
+
+    def __repr__(self):
+        return (f"\nCall:\n{self.call}\n\nCluster method   : {self.method}\n"
+                f"Distance         : {self.dist_method}\nNumber of objects: {self.n}\n")
+
+
+@dataclass
+class Tadpole:
+    """The ``tadpole`` list of R/TADpole.R:463-468 (plus ``merging_arms`` /
+    per-arm ``p``, ``q`` entries when ``centromere_search`` is on)."""
+    n_pcs: Optional[int] = None
+    optimal_n_clusters: Optional[int] = None
+    dendro: Optional[Chclust] = None
+    clusters: Dict[str, np.ndarray] = field(default_factory=dict)   # "k" -> (m x 2) start, end
+    scores: Optional[np.ndarray] = None                             # k x w, NA = R NA bits
+    merging_arms: Optional[np.ndarray] = None
+    p: Optional["Tadpole"] = None
+    q: Optional["Tadpole"] = None
+    bad_columns: Optional[np.ndarray] = None                        # 1-based original indices
+    timings_ms: Optional[np.ndarray] = None
+
+    def __getitem__(self, key):
+        return getattr(self, key)
+
+    # R's cluster slot name on the arm branch is `cluster` (R/TADpole.R:407)
+    @property
+    def cluster(self):
+        return self.clusters
+
+
+# --------------------------------------------------------------- load_mat
+
+def read_matrix(mat_file) -> np.ndarray:
+    """``bigmemory::read.big.matrix(sep='\\t', type='double')`` (R/TADpole.R:17):
+    a headerless tab-separated numeric matrix; "NA"/"NaN" become NaN."""
+    import pandas as pd
+    df = pd.read_csv(mat_file, sep="\t", header=None, dtype=np.float64,
+                     na_values=["NA", "NaN", "nan", ""], keep_default_na=True, engine="c")
+    return np.ascontiguousarray(df.to_numpy(dtype=np.float64))
+
+
+def _as_matrix(mat) -> np.ndarray:
+    if isinstance(mat, (str, bytes)) or hasattr(mat, "__fspath__"):
+        return read_matrix(mat)
+    m = np.asarray(mat, dtype=np.float64)
+    if m.ndim != 2 or m.shape[0] != m.shape[1]:
+        raise ValueError("the interaction matrix must be square")
+    return m
+
+
+def _layout(m: np.ndarray):
+    if m.flags["F_CONTIGUOUS"] and not m.flags["C_CONTIGUOUS"]:
+        return m, 0
+    return np.ascontiguousarray(m), _lib.TP_FLAG_ROW_MAJOR
+
+
+def clean_symmetrize(m: np.ndarray) -> np.ndarray:
+    """R/TADpole.R:19-20 on the host (used for the arm split and for load_mat's
+    return value; the pipeline does the same on the device)."""
+    out = np.array(m, dtype=np.float64, copy=True)
+    out[np.isnan(out)] = 0.0
+    iu = np.triu_indices(out.shape[0], 1)
+    out.T[iu] = out[iu]
+    return out
+
+
+def mask(mat, bad_frac: float = 0.01, device: int = 0):
+    """GPU bad-column mask (R/TADpole.R:35-37).  Returns (bad bool[N0],
+    rowMeans, good 1-based indices)."""
+    L = _lib.load()
+    m, flags = _layout(_as_matrix(mat))
+    n0 = m.shape[0]
+    bad = np.zeros(n0, np.int32)
+    rm = np.zeros(n0)
+    good = np.zeros(n0, np.int32)
+    ng = cint(0)
+    st = cint(0)
+    L.tp_mask(dp(m), ctypes.byref(cint(n0)), ctypes.byref(cdbl(bad_frac)), ctypes.byref(cint(flags)),
+              ctypes.byref(cint(device)), ip(bad), dp(rm), ctypes.byref(ng), ip(good), ctypes.byref(st))
+    _lib.check(st)
+    return bad.astype(bool), rm, good[:ng.value].copy()
+
+
+class Mat(np.ndarray):
+    """ndarray with R's ``attr(mat, 'bad_columns')`` and its row names (the
+    1-based original bin index of every row)."""
+    bad_columns: np.ndarray
+    names: np.ndarray
+
+    def __new__(cls, arr, bad_columns, names):
+        obj = np.asarray(arr).view(cls)
+        obj.bad_columns = np.asarray(bad_columns, np.int64)
+        obj.names = np.asarray(names, np.int64)
+        return obj
+
+    def __array_finalize__(self, obj):
+        self.bad_columns = getattr(obj, "bad_columns", np.zeros(0, np.int64))
+        self.names = getattr(obj, "names", np.zeros(0, np.int64))
+
+
+def _runs(idx: np.ndarray) -> List[np.ndarray]:
+    """``split(idx, cumsum(seq_along(idx) %in% (which(diff(idx) > 1) + 1)))``."""
+    if idx.size == 0:
+        return []
+    cut = np.flatnonzero(np.diff(idx) > 1) + 1
+    return np.split(idx, cut)
+
+
+def load_mat(mat_file, chr=None, start=None, end=None, resol=None, bad_frac: float = 0.01,
+             centromere_search: bool = False, device: int = 0):
+    """``load_mat`` (R/TADpole.R:15-92) without its plots.
+
+    Returns the masked matrix (``Mat`` with ``bad_columns``) or, with
+    ``centromere_search``, ``{"p": Mat, "q": Mat, "centromere": ndarray}``,
+    bug-compatible with the reference (q-arm bad columns removed with original
+    indices, R/TADpole.R:78-80; a plain matrix when the longest bad run touches
+    an end, R/TADpole.R:66-70)."""
+    raw = _as_matrix(mat_file)
+    bad, _, good = mask(raw, bad_frac, device)
+    m = clean_symmetrize(raw)
+    n0 = m.shape[0]
+    bad_idx = np.flatnonzero(bad) + 1
+    if bad.any() and centromere_search:
+        runs = _runs(bad_idx)
+        longest = runs[int(np.argmax([len(r) for r in runs]))]
+        cs, ce = int(longest[0]), int(longest[-1])
+        if cs == 1 or ce == n0:
+            return Mat(m[np.ix_(good - 1, good - 1)], bad_idx, good)
+        idx_p = np.arange(1, cs)
+        idx_q = np.arange(ce + 1, n0 + 1)
+        bad_p = bad_idx[bad_idx < cs]
+        bad_q = bad_idx[bad_idx > ce]
+        keep_p = _r_negative_keep(len(idx_p), bad_p)
+        keep_q = _r_negative_keep(len(idx_q), bad_q)
+        sel_p, sel_q = idx_p[keep_p] - 1, idx_q[keep_q] - 1
+        return {"p": Mat(m[np.ix_(sel_p, sel_p)], bad_p, sel_p + 1),
+                "q": Mat(m[np.ix_(sel_q, sel_q)], bad_q, sel_q + 1),
+                "centromere": np.arange(cs, ce + 1)}
+    return Mat(m[np.ix_(good - 1, good - 1)], bad_idx, good)
+
+
+def _r_negative_keep(n: int, neg: np.ndarray) -> np.ndarray:
+    """Positions kept by R's ``x[-neg]`` on length n: negative subscripts are
+    positions (the reference passes original bin indices here, R/TADpole.R:80),
+    and out-of-range ones are silently ignored."""
+    if neg.size == 0:
+        return np.arange(n)
+    drop = neg[(neg >= 1) & (neg <= n)] - 1
+    return np.setdiff1d(np.arange(n), drop)
+
+
+# ---------------------------------------------------------------- pipeline
+
+def _pipeline(m: np.ndarray, max_pcs: int, min_clusters: int, bad_frac: float, flags: int,
+              device: int):
+    L = _lib.load()
+    m, lay = _layout(m)
+    flags |= lay
+    n0 = m.shape[0]
+    k_cap = max(1, min(max_pcs, n0))
+    w_cap = max(1, n0)
+    bad = np.zeros(n0, np.int32)
+    good = np.zeros(n0, np.int32)
+    nclu = np.zeros(k_cap, np.int32)
+    scores = np.zeros(k_cap * w_cap)
+    merge = np.zeros(2 * max(1, n0 - 1), np.int32)
+    height = np.zeros(max(1, n0 - 1))
+    boundary = np.zeros(max(1, n0 - 1), np.int32)
+    timings = np.zeros(16)
+    out = [cint(0) for _ in range(6)]
+    n_good, k, w, n_pcs, n_clusters, st = out
+    L.tp_pipeline(dp(m), ctypes.byref(cint(n0)), ctypes.byref(cint(max_pcs)), ctypes.byref(cint(min_clusters)),
+                  ctypes.byref(cdbl(bad_frac)), ctypes.byref(cint(flags)), ctypes.byref(cint(device)),
+                  ctypes.byref(cint(k_cap)), ctypes.byref(cint(w_cap)), ip(bad), ctypes.byref(n_good),
+                  ip(good), ctypes.byref(k), ip(nclu), dp(scores), ctypes.byref(w), ctypes.byref(n_pcs),
+                  ctypes.byref(n_clusters), ip(merge), dp(height), ip(boundary), dp(timings),
+                  ctypes.byref(st))
+    _lib.check(st)
+    n = n_good.value
+    kk, ww = k.value, w.value
+    sc = scores[:kk * ww].reshape(ww, kk).T.copy()
+    return dict(bad=bad.astype(bool), good=good[:n].copy(), k=kk, w=ww, n_cluster=nclu[:kk].copy(),
+                scores=sc, n_pcs=n_pcs.value, n_clusters=n_clusters.value,
+                merge=merge[:2 * (n - 1)].reshape(2, n - 1).T.copy(), height=height[:n - 1].copy(),
+                boundary=boundary[:n - 1].copy(), timings=timings)
+
+
+def rle(x):
+    x = np.asarray(x)
+    if x.size == 0:
+        return np.zeros(0, np.int64), x
+    cut = np.flatnonzero(x[1:] != x[:-1]) + 1
+    starts = np.concatenate([[0], cut])
+    return np.diff(np.concatenate([starts, [x.size]])), x[starts]
+
+
+def fix_values(lengths, values):
+    """``fix_values`` (R/TADpole.R:503-510)."""
+    values = np.array(values, copy=True)
+    for i in np.flatnonzero(values == 0):
+        if i == 0 or i == len(values) - 1:
+            continue
+        if values[i - 1] == values[i + 1]:
+            values[i] = values[i - 1]
+    return lengths, values
+
+
+def _fixed_clusters(labels_good, good_idx1, bad_idx1):
+    """R/TADpole.R:474-483: c(good, bad=0), order by numeric name, fix_values,
+    inverse.rle.  Returns (vector over all bins in original order, names)."""
+    names = np.concatenate([good_idx1, bad_idx1]).astype(np.float64)
+    vals = np.concatenate([np.asarray(labels_good, np.float64), np.zeros(len(bad_idx1))])
+    order = np.argsort(names, kind="stable")
+    lens, v = fix_values(*rle(vals[order]))
+    return np.repeat(v, lens), names[order]
+
+
+def _coords(fixed):
+    """R/TADpole.R:485-488: runs of the fixed vector -> (start, end), 0-runs dropped."""
+    lens, v = rle(fixed)
+    eb = np.cumsum(lens)
+    start = np.concatenate([[1], eb[:-1] + 1])
+    keep = v != 0
+    return np.stack([start[keep], eb[keep]], axis=1).astype(np.int64)
+
+
+def _assemble(res, bad_idx1, arm_mode: bool = False) -> Tadpole:
+    n = len(res["good"])
+    dendro = Chclust(merge=res["merge"], height=res["height"], order=np.arange(1, n + 1),
+                     labels=[str(int(g)) for g in res["good"]], boundary=res["boundary"])
+    t = Tadpole(n_pcs=res["n_pcs"], optimal_n_clusters=res["n_clusters"], dendro=dendro,
+                scores=res["scores"], bad_columns=bad_idx1, timings_ms=res["timings"])
+    row = res["scores"][res["n_pcs"] - 1]
+    good1 = res["good"]
+    for kk in np.flatnonzero(~np.isnan(row)) + 1:
+        lab = dendro.cutree(int(kk))
+        if bad_idx1 is not None:
+            fixed, _ = _fixed_clusters(lab, good1, bad_idx1)
+            t.clusters[str(int(kk))] = _coords(fixed)
+        else:
+            eb = np.cumsum(np.bincount(lab)[1:])
+            t.clusters[str(int(kk))] = np.stack([np.concatenate([[1], eb[:-1] + 1]), eb], axis=1)
+    return t
+
+
+def TADpole(mat_file, max_pcs: int = 200, min_clusters: int = 2, bad_frac: float = 0.01,
+            chr=None, start=None, end=None, resol=None, centromere_search: bool = False,
+            device: int = 0) -> Tadpole:
+    """``TADpole()`` (R/TADpole.R:344-501).  ``mat_file`` may be a path to a
+    tab-separated matrix or an in-memory square array."""
+    raw = _as_matrix(mat_file)
+    if not centromere_search:
+        res = _pipeline(raw, max_pcs, min_clusters, bad_frac, 0, device)
+        bad_idx1 = np.flatnonzero(res["bad"]) + 1
+        return _assemble(res, bad_idx1)
+    mat = load_mat(raw, bad_frac=bad_frac, centromere_search=True, device=device)
+    if not isinstance(mat, dict):
+        # R/TADpole.R:356: `mat$centromer` on a matrix is an error in R
+        raise TypeError("$ operator is invalid for atomic vectors (no centromere split: the longest "
+                        "bad run touches an end of the matrix; R/TADpole.R:66-70,356)")
+    return _tadpole_arms(mat, max_pcs, min_clusters, device)
+
+
+def _tadpole_arms(mat, max_pcs, min_clusters, device) -> Tadpole:
+    """R/TADpole.R:351-442 (arm loop and arm merge), bug-compatible."""
+    tad = Tadpole()
+    centromer = mat["centromere"]
+    fixed_arms: List[np.ndarray] = []
+    for arm in ("p", "q"):
+        am = mat[arm]
+        bad_cols = am.bad_columns
+        res = _pipeline(np.asarray(am), max_pcs, min_clusters, 0.0,
+                        _lib.TP_FLAG_CLEAN | _lib.TP_FLAG_NO_MASK, device)
+        names = am.names.astype(np.int32)   # rownames inherited from the full matrix
+        res["good"] = names
+        sub = _assemble_arm(res, bad_cols)
+        setattr(tad, arm, sub)
+        lab = sub.dendro.cutree(sub.optimal_n_clusters)
+        if bad_cols is not None and len(bad_cols):
+            fixed, _ = _fixed_clusters(lab, names, np.asarray(bad_cols))
+        else:
+            order = np.argsort(names.astype(np.float64), kind="stable")
+            lens, v = fix_values(*rle(np.asarray(lab, np.float64)[order]))
+            fixed = np.repeat(v, lens)
+        fixed_arms.append(fixed)
+        fixed_arms.append(np.zeros(len(centromer)))
+    allv = np.concatenate(fixed_arms)
+    allv = allv[: len(allv) - len(centromer)]
+    tad.merging_arms = _coords(allv)
+    return tad
+
+
+def _assemble_arm(res, bad_cols) -> Tadpole:
+    t = _assemble(res, np.asarray(bad_cols) if bad_cols is not None and len(bad_cols) else None)
+    return t
+
+
+# ------------------------------------------------------------------ diffT
+
+def _bed_rows(bed):
+    if hasattr(bed, "itertuples"):
+        return [(r[1], int(r[2]), int(r[3])) for r in bed.itertuples()]
+    return [(r[0], int(r[1]), int(r[2])) for r in bed]
+
+
+def bin_index(bed, size: int) -> np.ndarray:
+    """``bin_index`` (R/DiffT.R:1-9)."""
+    rows = _bed_rows(bed)
+    out = np.zeros(size, np.int64)
+    first = rows[0][1]
+    for t, (_, s, e) in enumerate(rows, start=1):
+        lo, hi = s - first, e - first
+        if hi >= lo:
+            out[lo:hi + 1] = t
+        else:  # R's seq(s, e) counts down when e < s
+            out[hi:lo + 1] = t
+    return out
+
+
+def diffT(bed_x, bed_y) -> np.ndarray:
+    """``diffT`` (R/DiffT.R:19-50), O(L) instead of R's O(L^2) loop; identical
+    integer counts, so the normalised profile is identical."""
+    rx, ry = _bed_rows(bed_x), _bed_rows(bed_y)
+    if len(rx) != len(ry):
+        raise ValueError("Both calls must have the same number of TADs.")
+    sx, sy = rx[0][1], ry[0][1]
+    ex, ey = rx[-1][2], ry[-1][2]
+    tx = bin_index(rx, ex - sx + 1)
+    ty = bin_index(ry, ey - sy + 1)
+    tx = np.concatenate([np.ones(max(0, sx - sy), np.int64), tx, np.full(max(0, ey - ex), tx.max())])
+    ty = np.concatenate([np.ones(max(0, sy - sx), np.int64), ty, np.full(max(0, ex - ey), ty.max())])
+    if len(tx) != len(ty):
+        raise ValueError("length(tad_x) == length(tad_y) is not TRUE")
+    # count_b = #{c : (tx[c]==tx[b]) xor (ty[c]==ty[b])} for nonzero ids
+    _, ix, cx = np.unique(tx, return_inverse=True, return_counts=True)
+    _, iy, cy = np.unique(ty, return_inverse=True, return_counts=True)
+    pair = ix.astype(np.int64) * (iy.max() + 1) + iy
+    _, ip_, cp = np.unique(pair, return_inverse=True, return_counts=True)
+    A, B, AB = cx[ix], cy[iy], cp[ip_]
+    L_ = len(tx)
+    scores = A + B - 2 * AB
+    zx, zy = tx == 0, ty == 0
+    scores = np.where(zx & ~zy, B, scores)      # x all TRUE: xor = !y
+    scores = np.where(~zx & zy, A, scores)      # y all TRUE: xor = !x
+    scores = np.where(zx & zy, 0, scores)
+    del L_
+    s = np.cumsum(scores)
+    if scores.max() == 0:
+        return s
+    return s / s.max()
+
+
+def random_bed(bed, bad_columns=None, rng=None):
+    """``random_bed`` (R/DiffT.R:61-73): same construction, numpy RNG."""
+    rows = _bed_rows(bed)
+    rng = np.random.default_rng(rng)
+    start, end = rows[0][1], rows[-1][2]
+    size = end - start + 1
+    bins = np.arange(start, end + 1)
+    if bad_columns is not None:
+        bins = np.delete(bins, np.asarray(bad_columns, np.int64) - 1)
+    borders = np.sort(rng.choice(bins[1:], len(rows) - 1, replace=False))
+    import pandas as pd
+    return pd.DataFrame({"chrom": [r[0] for r in rows],
+                         "start": np.concatenate([[start], borders - 1]),
+                         "end": np.concatenate([borders - 2, [start + size - 1]])})

@@ -1,0 +1,674 @@
+// C ABI of libtadpole_hip.so (include/tadpole_hip.h): device contexts, stage
+// orchestration, and the host-side tail of find_params (R/TADpole.R:125-135:
+// NA-padded score matrix, rowMeans(na.rm=TRUE) in long double as R does, first
+// which.max) plus the hclust merge encoding of the chosen tree.
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/tadpole_hip.h"
+#include "tp_internal.h"
+
+namespace tp {
+
+static thread_local std::string g_err;
+
+void fail(int status, const std::string &msg) { throw Error{status, msg}; }
+
+void hip_check(hipError_t e, const char *what, const char *file, int line) {
+    if (e != hipSuccess) {
+        char b[512];
+        snprintf(b, sizeof b, "HIP error %d (%s) at %s:%d: %s", (int)e, hipGetErrorString(e), file, line, what);
+        fail(TP_ERR_HIP, b);
+    }
+}
+
+void *DevBuf::get(size_t b) {
+    if (b == 0) b = 8;
+    if (b > bytes) {
+        if (p) TP_HIP(hipFree(p));
+        p = nullptr;
+        size_t nb = std::max(b, bytes + bytes / 4);
+        TP_HIP(hipMalloc(&p, nb));
+        bytes = nb;
+    }
+    return p;
+}
+void DevBuf::release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+}
+
+void *Ctx::pinned(size_t b) {
+    if (b > host_pinned_bytes) {
+        if (host_pinned) TP_HIP(hipHostFree(host_pinned));
+        host_pinned = nullptr;
+        TP_HIP(hipHostMalloc(&host_pinned, b, hipHostMallocDefault));
+        host_pinned_bytes = b;
+    }
+    return host_pinned;
+}
+
+static hipEvent_t next_event(Ctx &c) {
+    if (c.evnext == c.evpool.size()) {
+        hipEvent_t e;
+        TP_HIP(hipEventCreate(&e));
+        c.evpool.push_back(e);
+    }
+    return c.evpool[c.evnext++];
+}
+void kprof_begin(Ctx &c, int cls) {
+    if (!c.prof) return;
+    c.open_cls = cls;
+    c.open_ev = next_event(c);
+    TP_HIP(hipEventRecord(c.open_ev, c.cur));
+}
+void kprof_end(Ctx &c, int cls) {
+    if (!c.prof || c.open_cls != cls) return;
+    hipEvent_t e = next_event(c);
+    TP_HIP(hipEventRecord(e, c.cur));
+    c.recs.push_back({cls, c.open_ev, e});
+    c.open_cls = -1;
+}
+void kprof_collect(Ctx &c, double *ms, int *cnt) {
+    for (int q = 0; q < K_NCLASS; ++q) { ms[q] = 0; cnt[q] = 0; }
+    for (auto &r : c.recs) {
+        TP_HIP(hipEventSynchronize(r.b));
+        float t = 0;
+        TP_HIP(hipEventElapsedTime(&t, r.a, r.b));
+        ms[r.cls] += t;
+        cnt[r.cls] += 1;
+    }
+    c.recs.clear();
+    c.evnext = 0;
+}
+
+static std::mutex g_mu;
+static Ctx *g_ctx[64] = {nullptr};
+
+Ctx &ctx_for(int device) {
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev <= 0) fail(TP_ERR_HIP, "no HIP device available (libtadpole_hip has no CPU path)");
+    if (device < 0 || device >= ndev || device >= 64) fail(TP_ERR_ARG, "device index out of range");
+    std::lock_guard<std::mutex> lk(g_mu);
+    TP_HIP(hipSetDevice(device));
+    if (!g_ctx[device]) {
+        Ctx *c = new Ctx();
+        c->device = device;
+        TP_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        g_ctx[device] = c;
+    }
+    g_ctx[device]->cur = g_ctx[device]->stream;
+    return *g_ctx[device];
+}
+
+void ctx_shutdown_all() {
+    std::lock_guard<std::mutex> lk(g_mu);
+    blas_shutdown_all();
+    for (int d = 0; d < 64; ++d) {
+        Ctx *c = g_ctx[d];
+        if (!c) continue;
+        (void)hipSetDevice(d);
+        (void)hipStreamSynchronize(c->stream);
+        for (auto &b : c->buf) b.release();
+        c->pinned_flag.release();
+        if (c->host_pinned) (void)hipHostFree(c->host_pinned);
+        (void)hipStreamDestroy(c->stream);
+        delete c;
+        g_ctx[d] = nullptr;
+    }
+}
+
+// ---------------------------------------------------------- host helpers
+// R/TADpole.R:134-135: which.max(rowMeans(scores, na.rm = TRUE)) and
+// which.max(scores[n_PCs, ]); rowMeans sums in LDOUBLE (R array.c).
+static void select_params(const double *scores, int k, int w, int *n_pcs, int *n_clusters) {
+    int best = -1;
+    double bestv = 0.0;
+    for (int i = 0; i < k; ++i) {
+        long double s = 0.0L;
+        int cnt = 0;
+        for (int j = 0; j < w; ++j) {
+            double v = scores[(size_t)i + (size_t)j * k];
+            if (std::isnan(v)) continue;
+            s += v;
+            ++cnt;
+        }
+        if (cnt == 0) continue;                    // NaN row mean: skipped by which.max
+        double mean = (double)(s / cnt);
+        if (std::isnan(mean)) continue;
+        if (best < 0 || mean > bestv) { best = i; bestv = mean; }
+    }
+    if (best < 0) fail(TP_ERR_NUMERIC, "no finite Calinski-Harabasz row mean (which.max is empty)");
+    int bj = -1;
+    double bv = 0.0;
+    for (int j = 0; j < w; ++j) {
+        double v = scores[(size_t)best + (size_t)j * k];
+        if (std::isnan(v)) continue;
+        if (bj < 0 || v > bv) { bj = j; bv = v; }
+    }
+    *n_pcs = best + 1;
+    *n_clusters = bj + 1;
+}
+
+// hclust merge encoding of a constrained tree: row s = (left id, right id),
+// singleton = -(bin), cluster formed at step t = t.  Column-major (n-1) x 2.
+static void encode_merge(const int *mrg_a, const int *mrg_b, int n, int *merge) {
+    std::vector<int> id(n);
+    for (int p = 0; p < n; ++p) id[p] = -(p + 1);
+    for (int s = 0; s < n - 1; ++s) {
+        int a = mrg_a[s], b = mrg_b[s];
+        merge[s] = id[a];
+        merge[s + (n - 1)] = id[b];
+        id[a] = s + 1;
+    }
+}
+
+struct Timer {
+    hipEvent_t ev[8];
+    int n = 0;
+    bool on;
+    hipStream_t s;
+    Timer(bool enable, hipStream_t st) : on(enable), s(st) {
+        if (on) for (auto &e : ev) TP_HIP(hipEventCreate(&e));
+    }
+    void mark() {
+        if (on && n < 8) TP_HIP(hipEventRecord(ev[n++], s));
+    }
+    void read(double *out) {
+        if (!on || !out) return;
+        TP_HIP(hipEventSynchronize(ev[n - 1]));
+        for (int t = 1; t < n; ++t) {
+            float ms = 0;
+            TP_HIP(hipEventElapsedTime(&ms, ev[t - 1], ev[t]));
+            out[t - 1] = ms;
+        }
+        float tot = 0;
+        TP_HIP(hipEventElapsedTime(&tot, ev[0], ev[n - 1]));
+        out[4] = tot;
+    }
+    ~Timer() {
+        if (on) for (auto &e : ev) (void)hipEventDestroy(e);
+    }
+};
+
+// ------------------------------------------------------------- sweep host
+struct SweepOut {
+    int w = 0, n_pcs = 0, n_clusters = 0;
+};
+
+// Runs the sweep for trees 1..k on device scores Pt (n x k row-major), copies
+// n_cluster and the NA-padded scores to the host, selects (n_pcs, n_clusters)
+// and fetches the merge record / heights of tree n_pcs.
+static SweepOut run_sweep(Ctx &c, const double *d_Pt, int n, int k, int min_clusters, int w_cap_host,
+                          int *n_cluster, double *scores, int *merge, double *height, int *boundary,
+                          std::vector<int> *all_a = nullptr, std::vector<int> *all_b = nullptr,
+                          std::vector<double> *all_cost = nullptr, std::vector<double> *all_h = nullptr) {
+    hipStream_t s = c.cur;
+    SweepDev sd{};
+    sd.Pt = d_Pt;
+    sd.n = n;
+    sd.ldp = k;
+    sd.k = k;
+    sd.tree0 = 0;
+    sd.ntrees = k;
+    sd.min_clusters = min_clusters;
+    sd.sums = c.buf[S_SWEEP].as<double>(sweep_sums_doubles(n, 0, k));
+    const size_t rec = (size_t)k * (n - 1);
+    char *recbuf = c.buf[S_SWEEP2].as<char>(rec * (4 + 4 + 8 + 8) + 256);
+    sd.mrg_a = (int *)recbuf;
+    sd.mrg_b = sd.mrg_a + rec;
+    sd.cost = (double *)(((uintptr_t)(sd.mrg_b + rec) + 15) & ~(uintptr_t)15);
+    sd.height = sd.cost + rec;
+    sd.w_cap = std::max(1, n - 1);
+    sd.seg_cap = std::min(sd.w_cap, 1024);
+    char *sc = c.buf[S_SCORES].as<char>((size_t)k * sd.w_cap * 8 + (size_t)k * 4 + 64);
+    sd.scores = (double *)sc;
+    sd.n_cluster = (int *)(sd.scores + (size_t)k * sd.w_cap);
+    sd.seg = c.buf[S_PARTIAL].as<double>((size_t)k * sd.seg_cap * (k + 1));
+    sd.iseg = c.buf[S_MISC].as<int>((size_t)k * (2 * sd.seg_cap + 2) + 64) + 64;
+    sd.err = c.buf[S_MISC].as<int>(64);
+    sd.trS = (double *)(c.buf[S_NGOOD].as<char>(64)) + 2;
+    TP_HIP(hipMemsetAsync(sd.err, 0, sizeof(int), s));
+    launch_sweep(sd, s, &c);
+    std::vector<int> h_nc(k);
+    int h_err = 0;
+    TP_HIP(hipMemcpyAsync(h_nc.data(), sd.n_cluster, k * sizeof(int), hipMemcpyDeviceToHost, s));
+    TP_HIP(hipMemcpyAsync(&h_err, sd.err, sizeof(int), hipMemcpyDeviceToHost, s));
+    TP_HIP(hipStreamSynchronize(s));
+    for (int i = 0; i < k; ++i)
+        if (h_nc[i] < 1)
+            fail(TP_ERR_NO_BSTICK, "no broken-stick level is significant for PC prefix " + std::to_string(i + 1) +
+                                       " (R: invalid 'times' argument at R/TADpole.R:115)");
+    if (h_err) fail(TP_ERR_UNSUPPORTED, "a broken-stick cut exceeds the CH kernel's segment capacity");
+    SweepOut o;
+    o.w = *std::max_element(h_nc.begin(), h_nc.end());
+    if (o.w > w_cap_host) fail(TP_ERR_CAPACITY, "scores capacity (w_cap) too small: need " + std::to_string(o.w));
+    if (n_cluster) memcpy(n_cluster, h_nc.data(), k * sizeof(int));
+    std::vector<double> h_sc((size_t)k * o.w);
+    TP_HIP(hipMemcpyAsync(h_sc.data(), sd.scores, h_sc.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+    TP_HIP(hipStreamSynchronize(s));
+    if (scores) memcpy(scores, h_sc.data(), h_sc.size() * sizeof(double));
+    select_params(h_sc.data(), k, o.w, &o.n_pcs, &o.n_clusters);
+    const int t = o.n_pcs - 1;
+    std::vector<int> ma(n - 1), mb(n - 1);
+    std::vector<double> he(n - 1);
+    TP_HIP(hipMemcpyAsync(ma.data(), sd.mrg_a + (size_t)t * (n - 1), (n - 1) * sizeof(int), hipMemcpyDeviceToHost, s));
+    TP_HIP(hipMemcpyAsync(mb.data(), sd.mrg_b + (size_t)t * (n - 1), (n - 1) * sizeof(int), hipMemcpyDeviceToHost, s));
+    TP_HIP(hipMemcpyAsync(he.data(), sd.height + (size_t)t * (n - 1), (n - 1) * sizeof(double),
+                          hipMemcpyDeviceToHost, s));
+    if (all_a) {
+        all_a->resize(rec); all_b->resize(rec); all_cost->resize(rec); all_h->resize(rec);
+        TP_HIP(hipMemcpyAsync(all_a->data(), sd.mrg_a, rec * 4, hipMemcpyDeviceToHost, s));
+        TP_HIP(hipMemcpyAsync(all_b->data(), sd.mrg_b, rec * 4, hipMemcpyDeviceToHost, s));
+        TP_HIP(hipMemcpyAsync(all_cost->data(), sd.cost, rec * 8, hipMemcpyDeviceToHost, s));
+        TP_HIP(hipMemcpyAsync(all_h->data(), sd.height, rec * 8, hipMemcpyDeviceToHost, s));
+    }
+    TP_HIP(hipStreamSynchronize(s));
+    if (merge) encode_merge(ma.data(), mb.data(), n, merge);
+    if (height) memcpy(height, he.data(), (n - 1) * sizeof(double));
+    if (boundary)
+        for (int q = 0; q < n - 1; ++q) boundary[q] = mb[q] + 1;
+    return o;
+}
+
+// ------------------------------------------------------------ pipeline
+struct PipeOut {
+    int n_good = 0, k = 0;
+    SweepOut sw;
+};
+
+static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_clusters, double bad_frac, int flags,
+                            int k_cap, int w_cap, int *bad, int *good_idx, int *n_cluster, double *scores,
+                            int *merge, double *height, int *boundary, double *timings) {
+    hipStream_t s = c.cur;
+    if (n0 < 1) fail(TP_ERR_ARG, "empty matrix");
+    if (max_pcs < 1) fail(TP_ERR_ARG, "max_pcs must be >= 1");
+    if (!(bad_frac >= 0.0 && bad_frac <= 1.0)) fail(TP_ERR_ARG, "bad_frac must be in [0, 1]");
+    Timer tm(timings != nullptr, s);
+    c.prof = timings != nullptr;
+    c.recs.clear();
+    c.evnext = 0;
+    tm.mark();
+    // ---- load_mat cleaning + mask + subset (R/TADpole.R:19-20,35-37,88-89)
+    if (!(flags & TP_FLAG_CLEAN)) launch_clean_symmetrize(d_M, n0, !(flags & TP_FLAG_ROW_MAJOR), s);
+    double *rm = c.buf[S_ROWMEAN].as<double>(n0);
+    double *dg = c.buf[S_DIAG].as<double>(n0);
+    int *d_bad = c.buf[S_BAD].as<int>(n0);
+    int *d_good = c.buf[S_GOOD].as<int>(n0);
+    int *d_ng = (int *)c.buf[S_NGOOD].as<char>(64);
+    int n = 0;
+    if (flags & TP_FLAG_NO_MASK) {
+        std::vector<int> iota(n0);
+        for (int q = 0; q < n0; ++q) iota[q] = q;
+        TP_HIP(hipMemcpyAsync(d_good, iota.data(), n0 * sizeof(int), hipMemcpyHostToDevice, s));
+        TP_HIP(hipMemsetAsync(d_bad, 0, n0 * sizeof(int), s));
+        TP_HIP(hipStreamSynchronize(s));
+        n = n0;
+    } else {
+        launch_rowmean_diag(d_M, n0, rm, dg, s);
+        const double qindex = 1.0 + (double)(n0 - 1) * bad_frac;
+        launch_mask_select(rm, dg, n0, bad_frac, qindex, d_bad, d_good, d_ng, s);
+        TP_HIP(hipMemcpyAsync(&n, d_ng, sizeof(int), hipMemcpyDeviceToHost, s));
+        TP_HIP(hipStreamSynchronize(s));
+    }
+    if (bad) TP_HIP(hipMemcpyAsync(bad, d_bad, n0 * sizeof(int), hipMemcpyDeviceToHost, s));
+    if (good_idx) TP_HIP(hipMemcpyAsync(good_idx, d_good, n * sizeof(int), hipMemcpyDeviceToHost, s));
+    PipeOut o;
+    o.n_good = n;
+    if (n < 3) fail(TP_ERR_NO_BSTICK, "fewer than 3 good bins after masking");
+    double *X = c.buf[S_X].as<double>((size_t)n * n);
+    double *m = c.buf[S_COLMEAN].as<double>(n);
+    launch_gather_colmean(d_M, n0, d_good, n, X, m, s);
+    tm.mark();
+    // ---- sparse_cor (R/TADpole.R:94-100,448-449)
+    double *S = c.buf[S_S].as<double>((size_t)n * n);
+    double *C = c.buf[S_C].as<double>((size_t)n * n);
+    {
+        GemmArgs g{n, n, n, X, n, true, X, n, S, n};
+        g.sym_upper = true;
+        kprof_begin(c, K_COR_GEMM);
+        gemm_f64(g, c.buf[S_PARTIAL], s);
+        kprof_end(c, K_COR_GEMM);
+    }
+    launch_cor_epilogue(S, m, n, C, s);
+    tm.mark();
+    // ---- prcomp (R/TADpole.R:452-453)
+    const int k = std::min(max_pcs, n);
+    o.k = k;
+    if (k > k_cap) fail(TP_ERR_CAPACITY, "k_cap smaller than min(max_pcs, n_good)");
+    double *P = c.buf[S_P].as<double>((size_t)n * k);
+    double *Pt = c.buf[S_PT].as<double>((size_t)n * k);
+    PcaStats ps = pca_dev(c, C, n, k, P, Pt, nullptr);
+    tm.mark();
+    // ---- find_params + final tree (R/TADpole.R:456-460)
+    o.sw = run_sweep(c, Pt, n, k, min_clusters, w_cap, n_cluster, scores, merge, height, boundary);
+    tm.mark();
+    if (good_idx)
+        for (int q = 0; q < n; ++q) good_idx[q] += 1;
+    if (timings) {
+        double t[8] = {0};
+        tm.read(t);
+        for (int q = 0; q < 5; ++q) timings[q] = t[q];
+        double kms[K_NCLASS];
+        int kcnt[K_NCLASS];
+        kprof_collect(c, kms, kcnt);
+        timings[5] = kms[K_COR_GEMM];
+        timings[6] = kms[K_G_GEMM];
+        timings[7] = kms[K_GQ_GEMM];
+        timings[8] = kcnt[K_GQ_GEMM];
+        timings[9] = kms[K_CONISS];
+        timings[10] = kms[K_CH];
+        timings[11] = ps.iters;
+        timings[12] = ps.block;
+        timings[13] = ps.resid;
+        timings[14] = n;
+        timings[15] = k;
+    }
+    c.prof = false;
+    return o;
+}
+
+template <class F> static void guarded(int *status, F &&f) {
+    try {
+        f();
+        if (status) *status = TP_OK;
+    } catch (const Error &e) {
+        g_err = e.msg;
+        if (status) *status = e.status;
+    } catch (const std::exception &e) {
+        g_err = e.what();
+        if (status) *status = TP_ERR_HIP;
+    } catch (...) {
+        g_err = "unknown error";
+        if (status) *status = TP_ERR_HIP;
+    }
+}
+
+static int dev_of(const int *device) { return device ? *device : 0; }
+
+}  // namespace tp
+
+using namespace tp;
+
+extern "C" {
+
+int tp_version(void) { return 1; }
+
+int tp_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+void tp_shutdown(void) { ctx_shutdown_all(); }
+
+int tp_last_error(char *buf, int len) {
+    if (!buf || len <= 0) return (int)g_err.size();
+    snprintf(buf, (size_t)len, "%s", g_err.c_str());
+    return (int)g_err.size();
+}
+
+void tp_last_error_r(char **buf, int *len) {
+    if (buf && buf[0] && len && *len > 0) snprintf(buf[0], (size_t)*len, "%s", g_err.c_str());
+}
+
+void tp_mask(const double *M, const int *n0, const double *bad_frac, const int *flags, const int *device, int *bad,
+             double *rowmean, int *n_good, int *good_idx, int *status) {
+    guarded(status, [&] {
+        if (!M || !n0 || *n0 < 1) fail(TP_ERR_ARG, "bad matrix");
+        Ctx &c = ctx_for(dev_of(device));
+        hipStream_t s = c.cur;
+        const int N0 = *n0;
+        const int fl = flags ? *flags : 0;
+        double *dM = c.buf[S_M].as<double>((size_t)N0 * N0);
+        TP_HIP(hipMemcpyAsync(dM, M, (size_t)N0 * N0 * 8, hipMemcpyHostToDevice, s));
+        if (!(fl & TP_FLAG_CLEAN)) launch_clean_symmetrize(dM, N0, !(fl & TP_FLAG_ROW_MAJOR), s);
+        double *rm = c.buf[S_ROWMEAN].as<double>(N0);
+        double *dg = c.buf[S_DIAG].as<double>(N0);
+        int *d_bad = c.buf[S_BAD].as<int>(N0);
+        int *d_good = c.buf[S_GOOD].as<int>(N0);
+        int *d_ng = (int *)c.buf[S_NGOOD].as<char>(64);
+        launch_rowmean_diag(dM, N0, rm, dg, s);
+        const double bf = bad_frac ? *bad_frac : 0.01;
+        launch_mask_select(rm, dg, N0, bf, 1.0 + (double)(N0 - 1) * bf, d_bad, d_good, d_ng, s);
+        int ng = 0;
+        TP_HIP(hipMemcpyAsync(&ng, d_ng, 4, hipMemcpyDeviceToHost, s));
+        if (bad) TP_HIP(hipMemcpyAsync(bad, d_bad, N0 * 4, hipMemcpyDeviceToHost, s));
+        if (rowmean) TP_HIP(hipMemcpyAsync(rowmean, rm, N0 * 8, hipMemcpyDeviceToHost, s));
+        if (good_idx) TP_HIP(hipMemcpyAsync(good_idx, d_good, N0 * 4, hipMemcpyDeviceToHost, s));
+        TP_HIP(hipStreamSynchronize(s));
+        if (n_good) *n_good = ng;
+        if (good_idx)
+            for (int q = 0; q < ng; ++q) good_idx[q] += 1;
+    });
+}
+
+void tp_cor(const double *X, const int *n, const int *device, double *cor, int *status) {
+    guarded(status, [&] {
+        if (!X || !n || *n < 2 || !cor) fail(TP_ERR_ARG, "bad arguments");
+        Ctx &c = ctx_for(dev_of(device));
+        hipStream_t s = c.cur;
+        const int N = *n;
+        double *dX = c.buf[S_X].as<double>((size_t)N * N);
+        TP_HIP(hipMemcpyAsync(dX, X, (size_t)N * N * 8, hipMemcpyHostToDevice, s));
+        double *m = c.buf[S_COLMEAN].as<double>(N);
+        launch_colmean(dX, N, N, m, s);
+        double *S = c.buf[S_S].as<double>((size_t)N * N);
+        double *C = c.buf[S_C].as<double>((size_t)N * N);
+        GemmArgs g{N, N, N, dX, N, true, dX, N, S, N};
+        g.sym_upper = true;
+        gemm_f64(g, c.buf[S_PARTIAL], s);
+        launch_cor_epilogue(S, m, N, C, s);
+        TP_HIP(hipMemcpyAsync(cor, C, (size_t)N * N * 8, hipMemcpyDeviceToHost, s));
+        TP_HIP(hipStreamSynchronize(s));
+    });
+}
+
+void tp_pca(const double *C, const int *n, const int *k, const int *device, double *P, double *sdev, int *status) {
+    guarded(status, [&] {
+        if (!C || !n || !k || *n < 2 || *k < 1 || *k > *n || !P) fail(TP_ERR_ARG, "bad arguments");
+        Ctx &c = ctx_for(dev_of(device));
+        hipStream_t s = c.cur;
+        const int N = *n, K = *k;
+        double *dC = c.buf[S_C].as<double>((size_t)N * N);
+        TP_HIP(hipMemcpyAsync(dC, C, (size_t)N * N * 8, hipMemcpyHostToDevice, s));
+        double *dP = c.buf[S_P].as<double>((size_t)N * K);
+        pca_dev(c, dC, N, K, dP, nullptr, sdev);
+        TP_HIP(hipMemcpyAsync(P, dP, (size_t)N * K * 8, hipMemcpyDeviceToHost, s));
+        TP_HIP(hipStreamSynchronize(s));
+    });
+}
+
+void tp_sweep(const double *P, const int *n, const int *k, const int *min_clusters, const int *device,
+              const int *w_cap, int *n_cluster, double *scores, int *w, int *n_pcs, int *n_clusters, int *merge,
+              double *height, int *status) {
+    guarded(status, [&] {
+        if (!P || !n || !k || *n < 3 || *k < 1 || !w_cap) fail(TP_ERR_ARG, "bad arguments");
+        Ctx &c = ctx_for(dev_of(device));
+        hipStream_t s = c.cur;
+        const int N = *n, K = *k;
+        double *dP = c.buf[S_P].as<double>((size_t)N * K);
+        double *dPt = c.buf[S_PT].as<double>((size_t)N * K);
+        TP_HIP(hipMemcpyAsync(dP, P, (size_t)N * K * 8, hipMemcpyHostToDevice, s));
+        launch_transpose(dP, N, K, N, dPt, K, s);
+        SweepOut o = run_sweep(c, dPt, N, K, min_clusters ? *min_clusters : 2, *w_cap, n_cluster, scores, merge,
+                               height, nullptr);
+        if (w) *w = o.w;
+        if (n_pcs) *n_pcs = o.n_pcs;
+        if (n_clusters) *n_clusters = o.n_clusters;
+    });
+}
+
+void tp_sweep_dev(const double *d_P, const int *n, const int *k, const int *min_clusters, const int *device,
+                  void *stream, const int *w_cap, int *n_cluster, double *scores, int *w, int *mrg_a_all,
+                  int *mrg_b_all, double *cost_all, double *height_all, int *status) {
+    guarded(status, [&] {
+        if (!d_P || !n || !k || *n < 3 || *k < 1 || !w_cap) fail(TP_ERR_ARG, "bad arguments");
+        Ctx &c = ctx_for(dev_of(device));
+        if (stream) c.cur = (hipStream_t)stream;
+        hipStream_t s = c.cur;
+        const int N = *n, K = *k;
+        double *dPt = c.buf[S_PT].as<double>((size_t)N * K);
+        launch_transpose(d_P, N, K, N, dPt, K, s);
+        std::vector<int> A, B;
+        std::vector<double> Co, H;
+        bool want = mrg_a_all || mrg_b_all || cost_all || height_all;
+        SweepOut o = run_sweep(c, dPt, N, K, min_clusters ? *min_clusters : 2, *w_cap, n_cluster, scores, nullptr,
+                               nullptr, nullptr, want ? &A : nullptr, want ? &B : nullptr, want ? &Co : nullptr,
+                               want ? &H : nullptr);
+        if (w) *w = o.w;
+        if (want) {
+            if (mrg_a_all) memcpy(mrg_a_all, A.data(), A.size() * 4);
+            if (mrg_b_all) memcpy(mrg_b_all, B.data(), B.size() * 4);
+            if (cost_all) memcpy(cost_all, Co.data(), Co.size() * 8);
+            if (height_all) memcpy(height_all, H.data(), H.size() * 8);
+        }
+    });
+}
+
+void tp_coniss(const double *P, const int *n, const int *ncols, const int *device, int *merge, double *height,
+               int *boundary, int *status) {
+    guarded(status, [&] {
+        if (!P || !n || !ncols || *n < 2 || *ncols < 1 || *ncols > 256) fail(TP_ERR_ARG, "bad arguments");
+        Ctx &c = ctx_for(dev_of(device));
+        hipStream_t s = c.cur;
+        const int N = *n, K = *ncols;
+        double *dP = c.buf[S_P].as<double>((size_t)N * K);
+        double *dPt = c.buf[S_PT].as<double>((size_t)N * K);
+        TP_HIP(hipMemcpyAsync(dP, P, (size_t)N * K * 8, hipMemcpyHostToDevice, s));
+        launch_transpose(dP, N, K, N, dPt, K, s);
+        SweepDev sd{};
+        sd.Pt = dPt;
+        sd.n = N;
+        sd.ldp = K;
+        sd.k = K;
+        sd.tree0 = K - 1;
+        sd.ntrees = 1;
+        sd.min_clusters = 2;
+        sd.sums = c.buf[S_SWEEP].as<double>(sweep_sums_doubles(N, K - 1, 1));
+        char *recbuf = c.buf[S_SWEEP2].as<char>((size_t)(N - 1) * 24 + 256);
+        sd.mrg_a = (int *)recbuf;
+        sd.mrg_b = sd.mrg_a + (N - 1);
+        sd.cost = (double *)(((uintptr_t)(sd.mrg_b + (N - 1)) + 15) & ~(uintptr_t)15);
+        sd.height = sd.cost + (N - 1);
+        sd.n_cluster = c.buf[S_MISC].as<int>(64);
+        sd.w_cap = std::max(1, N - 1);
+        // CONISS only (the CH half needs a broken-stick cut; not wanted here)
+        launch_coniss_only(sd, s);
+        std::vector<int> ma(N - 1), mb(N - 1);
+        std::vector<double> he(N - 1);
+        TP_HIP(hipMemcpyAsync(ma.data(), sd.mrg_a, (N - 1) * 4, hipMemcpyDeviceToHost, s));
+        TP_HIP(hipMemcpyAsync(mb.data(), sd.mrg_b, (N - 1) * 4, hipMemcpyDeviceToHost, s));
+        TP_HIP(hipMemcpyAsync(he.data(), sd.height, (N - 1) * 8, hipMemcpyDeviceToHost, s));
+        TP_HIP(hipStreamSynchronize(s));
+        if (merge) encode_merge(ma.data(), mb.data(), N, merge);
+        if (height) memcpy(height, he.data(), (N - 1) * 8);
+        if (boundary)
+            for (int q = 0; q < N - 1; ++q) boundary[q] = mb[q] + 1;
+    });
+}
+
+void tp_dist(const double *P, const int *n, const int *ncols, const int *device, double *d, int *status) {
+    guarded(status, [&] {
+        if (!P || !n || !ncols || *n < 2 || *ncols < 1 || !d) fail(TP_ERR_ARG, "bad arguments");
+        Ctx &c = ctx_for(dev_of(device));
+        hipStream_t s = c.cur;
+        const int N = *n, K = *ncols;
+        double *dP = c.buf[S_P].as<double>((size_t)N * K);
+        size_t nd = (size_t)N * (N - 1) / 2;
+        double *dd = c.buf[S_S].as<double>(nd);
+        TP_HIP(hipMemcpyAsync(dP, P, (size_t)N * K * 8, hipMemcpyHostToDevice, s));
+        launch_dist(dP, N, N, K, dd, s);
+        TP_HIP(hipMemcpyAsync(d, dd, nd * 8, hipMemcpyDeviceToHost, s));
+        TP_HIP(hipStreamSynchronize(s));
+    });
+}
+
+void tp_ch(const double *P, const int *n, const int *k, const int *labels, const int *cn, const int *device,
+           double *ch, int *status) {
+    guarded(status, [&] {
+        if (!P || !n || !k || !labels || !cn || *n < 2 || *k < 1 || *k > 256 || *cn < 1 || !ch)
+            fail(TP_ERR_ARG, "bad arguments");
+        const int N = *n, K = *k, CN = *cn;
+        std::vector<int> bnd(CN + 1);
+        bnd[0] = 0;
+        int g = 0;
+        if (labels[0] != 1) fail(TP_ERR_ARG, "labels must be contiguous 1..cn in order");
+        for (int a = 1; a < N; ++a) {
+            if (labels[a] == labels[a - 1]) continue;
+            if (labels[a] != labels[a - 1] + 1) fail(TP_ERR_ARG, "labels must be contiguous 1..cn in order");
+            bnd[++g] = a;
+        }
+        if (g + 1 != CN) fail(TP_ERR_ARG, "cn does not match the number of label runs");
+        bnd[CN] = N;
+        Ctx &c = ctx_for(dev_of(device));
+        hipStream_t s = c.cur;
+        double *dP = c.buf[S_P].as<double>((size_t)N * K);
+        double *dPt = c.buf[S_PT].as<double>((size_t)N * K);
+        int *dB = c.buf[S_GOOD].as<int>(CN + 1);
+        double *seg = c.buf[S_PARTIAL].as<double>(CN + 8);
+        double *out = c.buf[S_SMALL].as<double>(8);
+        TP_HIP(hipMemcpyAsync(dP, P, (size_t)N * K * 8, hipMemcpyHostToDevice, s));
+        TP_HIP(hipMemcpyAsync(dB, bnd.data(), (CN + 1) * 4, hipMemcpyHostToDevice, s));
+        launch_transpose(dP, N, K, N, dPt, K, s);
+        launch_ch_only(dPt, N, K, K, dB, CN, seg, out, s);
+        TP_HIP(hipMemcpyAsync(ch, out, 8, hipMemcpyDeviceToHost, s));
+        TP_HIP(hipStreamSynchronize(s));
+    });
+}
+
+static void pipeline_common(double *dM, const int *n0, const int *max_pcs, const int *min_clusters,
+                            const double *bad_frac, const int *flags, Ctx &c, const int *k_cap, const int *w_cap,
+                            int *bad, int *n_good, int *good_idx, int *k, int *n_cluster, double *scores, int *w,
+                            int *n_pcs, int *n_clusters, int *merge, double *height, int *boundary,
+                            double *timings_ms) {
+    PipeOut o = pipeline_dev(c, dM, *n0, max_pcs ? *max_pcs : 200, min_clusters ? *min_clusters : 2,
+                             bad_frac ? *bad_frac : 0.01, flags ? *flags : 0, k_cap ? *k_cap : 0,
+                             w_cap ? *w_cap : 0, bad, good_idx, n_cluster, scores, merge, height, boundary,
+                             timings_ms);
+    if (n_good) *n_good = o.n_good;
+    if (k) *k = o.k;
+    if (w) *w = o.sw.w;
+    if (n_pcs) *n_pcs = o.sw.n_pcs;
+    if (n_clusters) *n_clusters = o.sw.n_clusters;
+}
+
+void tp_pipeline(const double *M, const int *n0, const int *max_pcs, const int *min_clusters,
+                 const double *bad_frac, const int *flags, const int *device, const int *k_cap, const int *w_cap,
+                 int *bad, int *n_good, int *good_idx, int *k, int *n_cluster, double *scores, int *w, int *n_pcs,
+                 int *n_clusters, int *merge, double *height, int *boundary, double *timings_ms, int *status) {
+    guarded(status, [&] {
+        if (!M || !n0 || *n0 < 1) fail(TP_ERR_ARG, "bad matrix");
+        Ctx &c = ctx_for(dev_of(device));
+        const size_t bytes = (size_t)(*n0) * (*n0) * 8;
+        double *dM = c.buf[S_M].as<double>((size_t)(*n0) * (*n0));
+        TP_HIP(hipMemcpyAsync(dM, M, bytes, hipMemcpyHostToDevice, c.cur));
+        pipeline_common(dM, n0, max_pcs, min_clusters, bad_frac, flags, c, k_cap, w_cap, bad, n_good, good_idx, k,
+                        n_cluster, scores, w, n_pcs, n_clusters, merge, height, boundary, timings_ms);
+    });
+}
+
+void tp_pipeline_dev(const double *d_M, const int *n0, const int *max_pcs, const int *min_clusters,
+                     const double *bad_frac, const int *flags, const int *device, void *stream, const int *k_cap,
+                     const int *w_cap, int *bad, int *n_good, int *good_idx, int *k, int *n_cluster, double *scores,
+                     int *w, int *n_pcs, int *n_clusters, int *merge, double *height, int *boundary,
+                     double *timings_ms, int *status) {
+    guarded(status, [&] {
+        if (!d_M || !n0 || *n0 < 1) fail(TP_ERR_ARG, "bad matrix");
+        Ctx &c = ctx_for(dev_of(device));
+        if (stream) c.cur = (hipStream_t)stream;
+        pipeline_common(const_cast<double *>(d_M), n0, max_pcs, min_clusters, bad_frac, flags, c, k_cap, w_cap,
+                        bad, n_good, good_idx, k, n_cluster, scores, w, n_pcs, n_clusters, merge, height, boundary,
+                        timings_ms);
+    });
+}
+
+}  // extern "C"

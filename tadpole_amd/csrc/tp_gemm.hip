@@ -1,0 +1,207 @@
+// fp64 GEMM on the CDNA4 matrix cores (v_mfma_f64_16x16x4_f64).
+//
+// Used for every O(N^3) / O(N^2 k) product of the path:
+//   S = X'X            crossprod in sparse_cor        R/TADpole.R:96   (sym_upper)
+//   G = Xc'Xc          normal matrix of prcomp's SVD  R/TADpole.R:453  (sym_upper)
+//   Z = G Q            PCA subspace iteration
+//   P = Xc V_k         prcomp scores x %*% rotation   R/TADpole.R:453
+//
+// Tile: 64x64 per workgroup, BK = 16, 256 threads = 4 waves in a 2x2 grid, each
+// wave 32x32 = 2x2 MFMA tiles.  Operands are staged k-contiguous in LDS
+// ([row][BK+2]: the +2 pad makes the 16-row x 2-k fragment read of ds_read_b64
+// conflict-free), next tile prefetched into registers during the MFMAs.
+// fp64 MFMA layout (cdna_hip_programming.md §3): A lane l = A[l&15][k=l>>4],
+// B lane l = B[k=l>>4][l&15], D lane l reg r = D[(l>>4) + 4r][l&15].
+#include "tp_common.cuh"
+#include "tp_internal.h"
+
+namespace tp {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+constexpr int BM = 64, BN = 64, BK = 16, LDK = BK + 2;
+
+template <bool TA>
+__device__ __forceinline__ void load_a(double (&ra)[4], const double *A, int lda, int M, int K, int i0, int k0) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        int idx = t + 256 * p;
+        int row, kk;
+        if (TA) { row = idx >> 4; kk = idx & 15; }   // k contiguous in memory
+        else    { kk = idx >> 6; row = idx & 63; }   // i contiguous in memory
+        int i = i0 + row, k = k0 + kk;
+        ra[p] = (i < M && k < K) ? (TA ? A[(size_t)k + (size_t)i * lda] : A[(size_t)i + (size_t)k * lda]) : 0.0;
+    }
+}
+template <bool TA>
+__device__ __forceinline__ void store_a(double (*As)[LDK], const double (&ra)[4]) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        int idx = t + 256 * p;
+        int row, kk;
+        if (TA) { row = idx >> 4; kk = idx & 15; }
+        else    { kk = idx >> 6; row = idx & 63; }
+        As[row][kk] = ra[p];
+    }
+}
+__device__ __forceinline__ void load_b(double (&rb)[4], const double *B, int ldb, int N, int K, int j0, int k0) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        int idx = t + 256 * p;
+        int col = idx >> 4, kk = idx & 15;
+        int j = j0 + col, k = k0 + kk;
+        rb[p] = (j < N && k < K) ? B[(size_t)k + (size_t)j * ldb] : 0.0;
+    }
+}
+__device__ __forceinline__ void store_b(double (*Bs)[LDK], const double (&rb)[4]) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        int idx = t + 256 * p;
+        Bs[idx >> 4][idx & 15] = rb[p];
+    }
+}
+
+template <bool TA>
+__global__ void __launch_bounds__(256) k_gemm_f64(int M, int N, int K, const double *__restrict__ A, int lda,
+                                                  const double *__restrict__ B, int ldb, double *__restrict__ C,
+                                                  int ldc, int store_t, int sym, int tiles_n, int kchunk,
+                                                  size_t part_stride) {
+    __shared__ double As[2][BM][LDK];
+    __shared__ double Bs[2][BN][LDK];
+    int bm, bn;
+    if (sym) {  // linear id -> (bm <= bn)
+        int id = blockIdx.x;
+        bm = 0;
+        while (id >= tiles_n - bm) { id -= tiles_n - bm; ++bm; }
+        bn = bm + id;
+    } else {
+        bm = blockIdx.x % ((M + BM - 1) / BM);
+        bn = blockIdx.x / ((M + BM - 1) / BM);
+    }
+    const int i0 = bm * BM, j0 = bn * BN;
+    const int kbeg = blockIdx.z * kchunk;
+    const int kend = min(K, kbeg + kchunk);
+    C += part_stride * blockIdx.z;
+
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int wm = (w & 1) * 32, wn = (w >> 1) * 32;
+    const int fr = lane & 15, fk = lane >> 4;
+
+    d4 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = (d4){0.0, 0.0, 0.0, 0.0};
+
+    double ra[4], rb[4];
+    int buf = 0;
+    if (kbeg < kend) {
+        load_a<TA>(ra, A, lda, M, kend, i0, kbeg);
+        load_b(rb, B, ldb, N, kend, j0, kbeg);
+        store_a<TA>(As[0], ra);
+        store_b(Bs[0], rb);
+    }
+    __syncthreads();
+    for (int k0 = kbeg; k0 < kend; k0 += BK) {
+        const bool more = k0 + BK < kend;
+        if (more) {
+            load_a<TA>(ra, A, lda, M, kend, i0, k0 + BK);
+            load_b(rb, B, ldb, N, kend, j0, k0 + BK);
+        }
+#pragma unroll
+        for (int kk = 0; kk < BK; kk += 4) {
+            double af[2], bf[2];
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                af[t] = As[buf][wm + t * 16 + fr][kk + fk];
+                bf[t] = Bs[buf][wn + t * 16 + fr][kk + fk];
+            }
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[a], bf[b], acc[a][b], 0, 0, 0);
+        }
+        if (more) {
+            store_a<TA>(As[buf ^ 1], ra);
+            store_b(Bs[buf ^ 1], rb);
+        }
+        __syncthreads();
+        buf ^= 1;
+    }
+    // epilogue
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                int i = i0 + wm + a * 16 + fk + 4 * r;
+                int j = j0 + wn + b * 16 + fr;
+                if (i >= M || j >= N) continue;
+                double v = acc[a][b][r];
+                if (sym) {
+                    if (i > j) continue;
+                    C[(size_t)i + (size_t)j * ldc] = v;
+                    C[(size_t)j + (size_t)i * ldc] = v;
+                } else if (store_t) {
+                    C[(size_t)j + (size_t)i * ldc] = v;
+                } else {
+                    C[(size_t)i + (size_t)j * ldc] = v;
+                }
+            }
+}
+
+// Fixed-order split-K reduction: C = sum_{z=0..S-1} part[z] (column-major M x N).
+__global__ void __launch_bounds__(256) k_splitk_reduce(const double *part, size_t stride, int S, int M, int N,
+                                                       double *C, int ldc, int store_t) {
+    size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (size_t)M * N) return;
+    int i = (int)(idx % M), j = (int)(idx / M);
+    double v = part[idx];
+    for (int z = 1; z < S; ++z) v = v + part[idx + z * stride];
+    if (store_t) C[(size_t)j + (size_t)i * ldc] = v;
+    else C[(size_t)i + (size_t)j * ldc] = v;
+}
+
+void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s) {
+    if (g.M <= 0 || g.N <= 0) return;
+    if (g.sym_upper && g.M != g.N) fail(TP_ERR_ARG, "sym_upper GEMM needs a square output");
+    const int tm = (g.M + BM - 1) / BM, tn = (g.N + BN - 1) / BN;
+    long nblk = g.sym_upper ? (long)tn * (tn + 1) / 2 : (long)tm * tn;
+    int S = g.splitk < 1 ? 1 : g.splitk;
+    int kchunk = ((g.K + S - 1) / S + BK - 1) / BK * BK;
+    if (kchunk < BK) kchunk = BK;
+    S = (g.K + kchunk - 1) / kchunk;
+    if (S < 1) S = 1;
+    dim3 grid((unsigned)nblk, 1, (unsigned)S);
+    double *out = g.C;
+    int ldo = g.ldc;
+    int st = g.store_t;
+    size_t pstride = 0;
+    if (S > 1) {
+        pstride = (size_t)g.M * g.N;
+        out = work.as<double>(pstride * S);
+        ldo = g.M;
+        st = 0;
+    }
+    if (g.trans_a)
+        hipLaunchKernelGGL(k_gemm_f64<true>, grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb, out, ldo,
+                           st, (int)g.sym_upper, tn, kchunk, pstride);
+    else
+        hipLaunchKernelGGL(k_gemm_f64<false>, grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb, out,
+                           ldo, st, (int)g.sym_upper, tn, kchunk, pstride);
+    TP_HIP(hipGetLastError());
+    if (S > 1) {
+        size_t tot = (size_t)g.M * g.N;
+        hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, out, pstride, S,
+                           g.M, g.N, g.C, g.ldc, (int)g.store_t);
+        TP_HIP(hipGetLastError());
+    }
+}
+
+}  // namespace tp

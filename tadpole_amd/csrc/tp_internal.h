@@ -1,0 +1,137 @@
+// Internal declarations shared by the HIP translation units of libtadpole_hip.
+// Nothing here is part of the C ABI (include/tadpole_hip.h is).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstddef>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/tadpole_hip.h"
+
+namespace tp {
+
+constexpr uint64_t kRNaBits = 0x7FF00000000007A2ULL;  // R NA_real_
+constexpr uint64_t kRNanBits = 0x7FF8000000000000ULL; // R NaN
+
+struct Error {
+    int status;
+    std::string msg;
+};
+
+[[noreturn]] void fail(int status, const std::string &msg);
+void hip_check(hipError_t e, const char *what, const char *file, int line);
+#define TP_HIP(x) ::tp::hip_check((x), #x, __FILE__, __LINE__)
+
+// Growable device scratch buffer.
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+    void *get(size_t b);
+    template <class T> T *as(size_t count) { return static_cast<T *>(get(count * sizeof(T))); }
+    void release();
+};
+
+// Kernel classes timed with HIP events when a caller asks for timings.
+enum KClass { K_COR_GEMM = 0, K_G_GEMM, K_GQ_GEMM, K_CONISS, K_CH, K_NCLASS };
+
+// Per-device state: one stream, named scratch buffers.
+struct Ctx {
+    bool prof = false;                  // record per-kernel events this call
+    std::vector<hipEvent_t> evpool;
+    size_t evnext = 0;
+    struct Rec { int cls; hipEvent_t a, b; };
+    std::vector<Rec> recs;
+    int open_cls = -1;
+    hipEvent_t open_ev = nullptr;
+    int device = 0;
+    hipStream_t stream = nullptr;   // library stream
+    hipStream_t cur = nullptr;      // stream used by the current call
+    DevBuf buf[24];
+    DevBuf pinned_flag;
+    void *host_pinned = nullptr;    // small pinned staging area
+    size_t host_pinned_bytes = 0;
+    void *pinned(size_t b);
+};
+
+Ctx &ctx_for(int device);
+void kprof_begin(Ctx &c, int cls);
+void kprof_end(Ctx &c, int cls);
+void kprof_collect(Ctx &c, double *ms_per_class, int *count_per_class);
+void ctx_shutdown_all();
+
+// Scratch slots (indices into Ctx::buf) so stages can share one context.
+enum Slot {
+    S_M = 0, S_ROWMEAN, S_DIAG, S_BAD, S_GOOD, S_NGOOD, S_X, S_COLMEAN,
+    S_S, S_C, S_XC, S_XCT, S_G, S_Q, S_Z, S_W, S_SMALL, S_P, S_PT,
+    S_SWEEP, S_SWEEP2, S_SCORES, S_PARTIAL, S_MISC
+};
+
+// ---------------------------------------------------------------- kernels
+// mask / correlation / centering  (tp_prep.hip)
+void launch_clean_symmetrize(double *d_M, int n0, bool src_upper, hipStream_t s);
+void launch_rowmean_diag(const double *d_M, int n0, double *d_rowmean, double *d_diag,
+                         hipStream_t s);
+void launch_mask_select(const double *d_rowmean, const double *d_diag, int n0,
+                        double bad_frac, double qindex, int *d_bad, int *d_good,
+                        int *d_ngood, hipStream_t s);
+void launch_gather_colmean(const double *d_M, int n0, const int *d_good, int n,
+                           double *d_X, double *d_colmean, hipStream_t s);
+void launch_colmean(const double *d_A, int n, int ld, double *d_mean, hipStream_t s);
+void launch_cor_epilogue(const double *d_S, const double *d_m, int n, double *d_C,
+                         hipStream_t s);
+void launch_center(const double *d_C, const double *d_mean, int n, double *d_Xc,
+                   double *d_XcT, hipStream_t s);
+
+// fp64 MFMA GEMM (tp_gemm.hip).  C[i,j] = sum_k A'(i,k) B(k,j); A' = A^T when
+// trans_a (A stored K x M col-major), else A (M x K col-major).  B: K x N
+// col-major.  C: M x N col-major (ldc) or, if store_t, C^T (C[j + i*ldc]).
+// sym_upper: compute tiles with row-block <= col-block only and mirror them.
+// splitk > 1: partial sums in workspace, reduced in a fixed order.
+struct GemmArgs {
+    int M, N, K;
+    const double *A; int lda; bool trans_a;
+    const double *B; int ldb;
+    double *C; int ldc;
+    bool store_t = false;
+    bool sym_upper = false;
+    int splitk = 1;
+};
+void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s);
+
+// sweep (tp_sweep.hip)
+struct SweepDev {
+    const double *Pt;   // n x ldp row-major PC scores
+    int n, ldp, k;      // k = columns used by CH (all PCs)
+    int tree0 = 0;      // trees tree0+1 .. tree0+ntrees (grid = ntrees)
+    int ntrees = 0;
+    int min_clusters;
+    double *sums;       // per-tree cluster sums, see sweep_sums_doubles
+    int *mrg_a, *mrg_b; // k x (n-1)
+    double *cost, *height;
+    int *n_cluster;     // ntrees
+    double *scores;     // ntrees x w_cap, column-major (ld ntrees)
+    int w_cap;
+    double *seg;        // CH scratch: k trees x seg_cap x (k + 1) doubles
+    int *iseg;          // CH scratch: k trees x (2 seg_cap + 2) ints
+    int seg_cap;        // max cut size the CH kernel handles
+    double *trS;        // 1
+    int *err;           // device flag: 1 = a cut exceeded seg_cap / w_cap
+};
+size_t sweep_sums_doubles(int n, int tree0, int ntrees);
+void blas_shutdown_all();
+void launch_sweep(const SweepDev &sd, hipStream_t s, Ctx *prof = nullptr);
+void launch_coniss_only(const SweepDev &sd, hipStream_t s);
+void launch_ch_only(const double *d_Pt, int n, int ldp, int k, const int *d_bnd,
+                    int cn, double *d_seg, double *d_out, hipStream_t s);
+void launch_dist(const double *d_P, int n, int ldp, int ncols, double *d_d, hipStream_t s);
+void launch_transpose(const double *d_A, int rows, int cols, int lda, double *d_T, int ldt,
+                      hipStream_t s);
+
+// PCA (tp_pca.cpp): P (n x k col-major, ld n) and Pt (n x k row-major) from C.
+struct PcaStats { int iters = 0; double resid = 0; double rate = 0; int block = 0; };
+PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d_Pt,
+                 double *h_sdev);
+
+}  // namespace tp

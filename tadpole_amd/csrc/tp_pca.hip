@@ -1,0 +1,261 @@
+// prcomp(cor, rank. = k)$x  (R/TADpole.R:452-453) on the GPU.
+//
+// R computes a FULL thin SVD of the column-centred N x N matrix (LAPACK gesdd)
+// and keeps k = min(max_pcs, N) right singular vectors.  Here:
+//   Xc = C - 1 colMeans(C)'                       (centring, tp_prep.hip)
+//   G  = Xc' Xc                                   (fp64 MFMA GEMM, symmetric)
+//   block subspace iteration on G, block b = k + oversampling, CholQR2
+//   orthonormalisation, Rayleigh-Ritz at the end (b x b eigensolve)
+//   P  = Xc V_k                                   (fp64 MFMA GEMM)
+// Only span(V_1..V_i) matters downstream (distances and CH are invariant to
+// sign and to rotations inside the top-i space), and the iteration stops when
+// every Ritz pair j <= k has ||G v - theta v|| <= tol * theta_1.
+// When N <= b the Ritz problem is G itself (exact full eigendecomposition).
+#include <rocblas/rocblas.h>
+#include <rocsolver/rocsolver.h>
+
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "tp_common.cuh"
+#include "tp_internal.h"
+
+namespace tp {
+
+static void rb_check(rocblas_status st, const char *what) {
+    if (st != rocblas_status_success) fail(TP_ERR_HIP, std::string("rocBLAS/rocSOLVER failure in ") + what);
+}
+
+struct Blas {
+    rocblas_handle h = nullptr;
+    int dev = -1;
+};
+static Blas g_blas[64];
+
+static rocblas_handle blas_for(Ctx &c) {
+    Blas &b = g_blas[c.device];
+    if (!b.h) {
+        rb_check(rocblas_create_handle(&b.h), "rocblas_create_handle");
+        b.dev = c.device;
+    }
+    rb_check(rocblas_set_stream(b.h, c.cur), "rocblas_set_stream");
+    return b.h;
+}
+
+void blas_shutdown_all() {
+    for (auto &b : g_blas)
+        if (b.h) {
+            (void)hipSetDevice(b.dev);
+            rocblas_destroy_handle(b.h);
+            b.h = nullptr;
+        }
+}
+
+// deterministic pseudo-random start block, uniform in (-1, 1)
+__global__ void k_rand_block(double *Q, int n, int b, uint64_t seed) {
+    size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (size_t)n * b) return;
+    uint64_t z = seed + 0x9E3779B97F4A7C15ULL * (idx + 1);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    z = z ^ (z >> 31);
+    Q[idx] = ((double)(z >> 11) * (1.0 / 9007199254740992.0)) * 2.0 - 1.0;
+}
+
+// W <- (W + W')/2 and W_jj += rel * max_j W_jj   (single workgroup)
+__global__ void __launch_bounds__(1024) k_sym_shift(double *W, int b, double rel) {
+    __shared__ double red[1024];
+    double mx = 0.0;
+    for (int j = threadIdx.x; j < b; j += blockDim.x) mx = fmax(mx, W[(size_t)j * b + j]);
+    red[threadIdx.x] = mx;
+    __syncthreads();
+    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+        if (threadIdx.x < o) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + o]);
+        __syncthreads();
+    }
+    const double s = rel * red[0];
+    for (size_t t = threadIdx.x; t < (size_t)b * b; t += blockDim.x) {
+        int i = (int)(t % b), j = (int)(t / b);
+        if (i < j) {
+            double v = 0.5 * (W[t] + W[(size_t)i * b + j]);
+            W[t] = v;
+            W[(size_t)i * b + j] = v;
+        }
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < b; j += blockDim.x) W[(size_t)j * b + j] += s;
+}
+
+// Wk[:, j] = W[:, b-1-j], j < k  (eigenvectors in descending eigenvalue order)
+__global__ void k_select_rev(const double *W, int b, int k, double *Wk) {
+    size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (size_t)b * k) return;
+    int i = (int)(idx % b), j = (int)(idx / b);
+    Wk[idx] = W[(size_t)(b - 1 - j) * b + i];
+}
+
+// resid[j] = || Y[:, j] - theta_j V[:, j] ||_2  (one wave per column)
+__global__ void __launch_bounds__(256) k_resid(const double *Y, const double *V, const double *theta_asc, int n, int b,
+                                               int k, double *resid) {
+    int lane = threadIdx.x & 63;
+    int j = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (j >= k) return;
+    double th = theta_asc[b - 1 - j];
+    double acc = 0.0;
+    for (int a = lane; a < n; a += 64) {
+        double r = Y[(size_t)j * n + a] - th * V[(size_t)j * n + a];
+        acc = fma(r, r, acc);
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) resid[j] = sqrt(acc);
+}
+
+static void orth_cholqr(Ctx &c, rocblas_handle h, double *Z, int n, int b, double *W, int *d_info, int passes,
+                        double first_shift) {
+    for (int p = 0; p < passes; ++p) {
+        GemmArgs g{b, b, n, Z, n, true, Z, n, W, b};
+        g.sym_upper = true;
+        g.splitk = std::max(1, std::min(16, n / 256));
+        gemm_f64(g, c.buf[S_PARTIAL], c.cur);
+        hipLaunchKernelGGL(k_sym_shift, dim3(1), dim3(1024), 0, c.cur, W, b, p == 0 ? first_shift : 0.0);
+        TP_HIP(hipGetLastError());
+        rb_check(rocsolver_dpotrf(h, rocblas_fill_upper, b, W, b, d_info), "dpotrf");
+        const double one = 1.0;
+        rb_check(rocblas_dtrsm(h, rocblas_side_right, rocblas_fill_upper, rocblas_operation_none,
+                               rocblas_diagonal_non_unit, n, b, &one, W, b, Z, n),
+                 "dtrsm");
+    }
+}
+
+PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d_Pt, double *h_sdev) {
+    PcaStats st;
+    hipStream_t s = c.cur;
+    rocblas_handle h = blas_for(c);
+    rb_check(rocblas_set_pointer_mode(h, rocblas_pointer_mode_host), "pointer mode");
+    double *mean = c.buf[S_COLMEAN].as<double>(n);
+    double *Xc = c.buf[S_XC].as<double>((size_t)n * n);
+    double *XcT = c.buf[S_XCT].as<double>((size_t)n * n);
+    double *G = c.buf[S_G].as<double>((size_t)n * n);
+    launch_colmean(d_C, n, n, mean, s);
+    launch_center(d_C, mean, n, Xc, XcT, s);
+    {
+        GemmArgs g{n, n, n, Xc, n, true, Xc, n, G, n};
+        g.sym_upper = true;
+        kprof_begin(c, K_G_GEMM);
+        gemm_f64(g, c.buf[S_PARTIAL], s);
+        kprof_end(c, K_G_GEMM);
+    }
+    int *d_info = c.buf[S_MISC].as<int>(64);
+    const int over = std::max(32, k / 4);
+    int b = std::min(n, ((k + over + 31) / 32) * 32);
+    st.block = b;
+    double *V = c.buf[S_W].as<double>((size_t)n * k);       // n x k, descending
+    double *theta = c.buf[S_SMALL].as<double>((size_t)std::max(n, b) + 64);
+    double *Wsm = nullptr;
+    std::vector<double> h_theta;
+    if (b >= n) {
+        // exact: eigendecomposition of G itself
+        b = n;
+        double *E = c.buf[S_Z].as<double>((size_t)n * n);
+        TP_HIP(hipMemcpyAsync(E, G, (size_t)n * n * sizeof(double), hipMemcpyDeviceToDevice, s));
+        double *offbuf = c.buf[S_Q].as<double>((size_t)n + 64);
+        rb_check(rocsolver_dsyevd(h, rocblas_evect_original, rocblas_fill_upper, n, E, n, theta, offbuf, d_info),
+                 "dsyevd");
+        size_t tot = (size_t)n * k;
+        hipLaunchKernelGGL(k_select_rev, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, E, n, k, V);
+        TP_HIP(hipGetLastError());
+        h_theta.resize(n);
+        TP_HIP(hipMemcpyAsync(h_theta.data(), theta, n * sizeof(double), hipMemcpyDeviceToHost, s));
+        TP_HIP(hipStreamSynchronize(s));
+        st.iters = 0;
+    } else {
+        double *Q = c.buf[S_Q].as<double>((size_t)n * b);
+        double *Z = c.buf[S_Z].as<double>((size_t)n * b);
+        Wsm = c.buf[S_SMALL].as<double>((size_t)b * b + 2 * b + 64);
+        theta = Wsm + (size_t)b * b;
+        double *offd = theta + b;
+        double *resid = c.buf[S_MISC].as<double>(64 + k) + 64;
+        d_info = c.buf[S_MISC].as<int>(64);
+        const size_t nb = (size_t)n * b;
+        hipLaunchKernelGGL(k_rand_block, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, s, Q, n, b,
+                           0x5EEDULL + (uint64_t)n);
+        TP_HIP(hipGetLastError());
+        orth_cholqr(c, h, Q, n, b, Wsm, d_info, 3, 1e-13);
+        const double target = 1e-12;
+        int done = 0, chunk = 12;
+        const int max_iter = 400;
+        std::vector<double> h_res(k);
+        h_theta.resize(b);
+        for (int round = 0; round < 8; ++round) {
+            for (int it = 0; it < chunk; ++it) {
+                GemmArgs g{n, b, n, G, n, true, Q, n, Z, n};
+                kprof_begin(c, K_GQ_GEMM);
+                gemm_f64(g, c.buf[S_PARTIAL], s);
+                kprof_end(c, K_GQ_GEMM);
+                orth_cholqr(c, h, Z, n, b, Wsm, d_info, 2, 1e-13);
+                std::swap(Q, Z);
+            }
+            done += chunk;
+            // Rayleigh-Ritz: H = Q' G Q, eigen-decompose, rotate Q
+            {
+                GemmArgs g{n, b, n, G, n, true, Q, n, Z, n};
+                gemm_f64(g, c.buf[S_PARTIAL], s);
+                GemmArgs hq{b, b, n, Q, n, true, Z, n, Wsm, b};
+                hq.splitk = std::max(1, std::min(16, n / 256));
+                gemm_f64(hq, c.buf[S_PARTIAL], s);
+                hipLaunchKernelGGL(k_sym_shift, dim3(1), dim3(1024), 0, s, Wsm, b, 0.0);
+                rb_check(rocsolver_dsyevd(h, rocblas_evect_original, rocblas_fill_upper, b, Wsm, b, theta, offd,
+                                          d_info),
+                         "dsyevd(RR)");
+                // rotate the whole block: Z = Q * W(desc order), keep as new Q
+                size_t tot = (size_t)b * b;
+                double *Wall = c.buf[S_SWEEP].as<double>(tot);
+                hipLaunchKernelGGL(k_select_rev, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, Wsm, b, b,
+                                   Wall);
+                GemmArgs rq{n, b, b, Q, n, false, Wall, b, Z, n};
+                gemm_f64(rq, c.buf[S_PARTIAL], s);
+                std::swap(Q, Z);
+                // residuals of the top k: Y = G V - V theta
+                GemmArgs gy{n, k, n, G, n, true, Q, n, Z, n};
+                gemm_f64(gy, c.buf[S_PARTIAL], s);
+                hipLaunchKernelGGL(k_resid, dim3((k + 3) / 4), dim3(256), 0, s, Z, Q, theta, n, b, k, resid);
+                TP_HIP(hipGetLastError());
+                TP_HIP(hipMemcpyAsync(h_res.data(), resid, k * sizeof(double), hipMemcpyDeviceToHost, s));
+                TP_HIP(hipMemcpyAsync(h_theta.data(), theta, b * sizeof(double), hipMemcpyDeviceToHost, s));
+                TP_HIP(hipStreamSynchronize(s));
+            }
+            const double th1 = std::fabs(h_theta[b - 1]);
+            double worst = 0.0;
+            for (int j = 0; j < k; ++j) worst = std::max(worst, h_res[j] / (th1 > 0 ? th1 : 1.0));
+            st.resid = worst;
+            const double thk = h_theta[b - k], thb = h_theta[0];
+            const double rho = (thk > 0 && thb > 0) ? thb / thk : 0.9;
+            st.rate = rho;
+            if (!(worst > target) || done >= max_iter) break;
+            double need = std::log(target / worst) / std::log(std::max(1e-3, std::min(rho, 0.999)));
+            chunk = std::max(4, std::min(max_iter - done, (int)std::ceil(need) + 2));
+        }
+        st.iters = done;
+        if (!(st.resid <= 1e-8)) fail(TP_ERR_NUMERIC, "PCA subspace iteration did not converge");
+        TP_HIP(hipMemcpyAsync(V, Q, (size_t)n * k * sizeof(double), hipMemcpyDeviceToDevice, s));
+    }
+    // scores P = Xc V  (= XcT' V): n x k column-major; Pt row-major
+    {
+        GemmArgs g{n, k, n, XcT, n, true, V, n, d_P, n};
+        gemm_f64(g, c.buf[S_PARTIAL], s);
+    }
+    if (d_Pt) launch_transpose(d_P, n, k, n, d_Pt, k, s);
+    if (h_sdev) {
+        // prcomp sdev = d / sqrt(max(1, n-1)), d = singular values of Xc = sqrt(eig(G))
+        std::vector<double> th = h_theta;
+        int bb = (int)th.size();
+        for (int j = 0; j < k; ++j) {
+            double e = th[bb - 1 - j];
+            h_sdev[j] = std::sqrt(std::max(0.0, e)) / std::sqrt((double)std::max(1, n - 1));
+        }
+    }
+    return st;
+}
+
+}  // namespace tp

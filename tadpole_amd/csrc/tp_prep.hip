@@ -1,0 +1,290 @@
+// Pre-processing kernels: load_mat cleaning + bad-column mask + subset
+// (R/TADpole.R:19-20,35-37,88-89), the sparse_cor epilogue
+// (R/TADpole.R:94-100,449) and prcomp's column centring (R/TADpole.R:453).
+// All of these are HBM-streaming passes over an N x N fp64 matrix.
+#include "tp_common.cuh"
+#include "tp_internal.h"
+
+namespace tp {
+
+// ------------------------------------------------ NA -> 0, forceSymmetric(U)
+// Treat the buffer as column-major B(r,c) = buf[r + c*n0].  The matrix's upper
+// triangle is B's upper triangle for column-major input, B's lower for
+// row-major input (src_upper = false).  One 64x64 tile pair per workgroup.
+__global__ void __launch_bounds__(256) k_clean_symmetrize(double *M, int n0, int nb, bool src_upper) {
+    __shared__ double t[64][65];
+    // linear block id -> (bi <= bj)
+    int id = blockIdx.x;
+    int bi = 0;
+    while (id >= nb - bi) { id -= nb - bi; ++bi; }
+    int bj = bi + id;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    // source tile rows/cols (buffer coordinates)
+    int sr0 = src_upper ? bi * 64 : bj * 64;
+    int sc0 = src_upper ? bj * 64 : bi * 64;
+    for (int y = ty; y < 64; y += 4) {
+        int r = sr0 + tx, c = sc0 + y;
+        double v = 0.0;
+        if (r < n0 && c < n0) {
+            v = M[(size_t)r + (size_t)c * n0];
+            if (isnan(v)) v = 0.0;
+        }
+        t[tx][y] = v;
+    }
+    __syncthreads();
+    if (bi != bj) {
+        for (int y = ty; y < 64; y += 4) {
+            int r = sr0 + tx, c = sc0 + y;
+            if (r < n0 && c < n0) M[(size_t)r + (size_t)c * n0] = t[tx][y];
+            // mirrored tile: B(sc0 + tx, sr0 + y) = t[y][tx]
+            int r2 = sc0 + tx, c2 = sr0 + y;
+            if (r2 < n0 && c2 < n0) M[(size_t)r2 + (size_t)c2 * n0] = t[y][tx];
+        }
+    } else {
+        for (int y = ty; y < 64; y += 4) {
+            int r = sr0 + tx, c = sc0 + y;
+            if (r < n0 && c < n0) {
+                bool from_here = src_upper ? (tx <= y) : (tx >= y);
+                M[(size_t)r + (size_t)c * n0] = from_here ? t[tx][y] : t[y][tx];
+            }
+        }
+    }
+}
+
+void launch_clean_symmetrize(double *d_M, int n0, bool src_upper, hipStream_t s) {
+    int nb = (n0 + 63) / 64;
+    long nblk = (long)nb * (nb + 1) / 2;
+    hipLaunchKernelGGL(k_clean_symmetrize, dim3((unsigned)nblk), dim3(256), 0, s, d_M, n0, nb, src_upper);
+    TP_HIP(hipGetLastError());
+}
+
+// ------------------------------------------ rowMeans (long double in R) + diag
+// The matrix is symmetric here, so row a is column a (contiguous).  One wave
+// per column; double-double accumulation stands in for R's LDOUBLE.
+__global__ void __launch_bounds__(256) k_rowmean_diag(const double *M, int n0, double *rm, double *dg) {
+    int lane = threadIdx.x & 63;
+    int a = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (a >= n0) return;
+    const double *col = M + (size_t)a * n0;
+    double hi = 0.0, lo = 0.0;
+    for (int r = lane; r < n0; r += 64) dd_add_d(hi, lo, col[r]);
+    wave_dd_sum(hi, lo);
+    if (lane == 0) {
+        rm[a] = dd_div_d(hi, lo, (double)n0);
+        if (dg) dg[a] = col[a];
+    }
+}
+
+void launch_rowmean_diag(const double *d_M, int n0, double *d_rowmean, double *d_diag, hipStream_t s) {
+    hipLaunchKernelGGL(k_rowmean_diag, dim3((n0 + 3) / 4), dim3(256), 0, s, d_M, n0, d_rowmean, d_diag);
+    TP_HIP(hipGetLastError());
+}
+
+// ------------------------------------- quantile type 7 + bad mask + compaction
+// One 1024-thread workgroup.  Order statistics by MSB-first radix select on
+// order-preserving 64-bit keys, then R's type-7 interpolation, then the mask
+// bad = diag == 0 | r < q and an order-preserving compaction of good bins.
+__device__ uint64_t radix_select(const double *r, int n, int rank, unsigned *hist, uint64_t *bcast) {
+    uint64_t prefix = 0, pmask = 0;
+    for (int shift = 56; shift >= 0; shift -= 8) {
+        for (int b = threadIdx.x; b < 256; b += blockDim.x) hist[b] = 0;
+        __syncthreads();
+        for (int i = threadIdx.x; i < n; i += blockDim.x) {
+            uint64_t key = dkey(r[i]);
+            if ((key & pmask) == prefix) atomicAdd(&hist[(key >> shift) & 255], 1u);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned cum = 0;
+            int d = 0;
+            for (; d < 256; ++d) {
+                if (cum + hist[d] > (unsigned)rank) break;
+                cum += hist[d];
+            }
+            rank -= (int)cum;
+            bcast[0] = prefix | ((uint64_t)d << shift);
+            bcast[1] = (uint64_t)rank;
+        }
+        __syncthreads();
+        prefix = bcast[0];
+        rank = (int)bcast[1];
+        pmask |= (uint64_t)255 << shift;
+        __syncthreads();
+    }
+    return prefix;
+}
+
+__global__ void __launch_bounds__(1024) k_mask_select(const double *r, const double *dg, int n0, double bad_frac,
+                                                      double qindex, int *bad, int *good, int *ngood) {
+    __shared__ unsigned hist[256];
+    __shared__ uint64_t bcast[2];
+    __shared__ unsigned long long umin;
+    __shared__ unsigned cnt_le;
+    __shared__ int scan[1024];
+    __shared__ double qsh;
+    const bool use_q = bad_frac != 0.0;
+    if (use_q) {
+        int lo = (int)floor(qindex), hi = (int)ceil(qindex);
+        uint64_t klo = radix_select(r, n0, lo - 1, hist, bcast);
+        double xlo = dkey_inv(klo), xhi = xlo;
+        if (hi != lo) {
+            if (threadIdx.x == 0) { umin = ~0ULL; cnt_le = 0; }
+            __syncthreads();
+            unsigned c = 0;
+            unsigned long long mn = ~0ULL;
+            for (int i = threadIdx.x; i < n0; i += blockDim.x) {
+                uint64_t key = dkey(r[i]);
+                if (key <= klo) ++c;
+                else if (key < mn) mn = key;
+            }
+            atomicAdd(&cnt_le, c);
+            atomicMin(&umin, mn);
+            __syncthreads();
+            if (cnt_le <= (unsigned)(hi - 1)) xhi = dkey_inv(umin);
+        }
+        if (threadIdx.x == 0) {
+            double q = xlo;
+            if (qindex > (double)lo && xhi != q) {
+                double h = qindex - (double)lo;
+                q = (1.0 - h) * q + h * xhi;
+            }
+            qsh = q;
+        }
+        __syncthreads();
+    }
+    const double q = use_q ? qsh : 0.0;
+    // chunked, order-preserving compaction
+    const int T = blockDim.x;
+    const int chunk = (n0 + T - 1) / T;
+    const int b0 = threadIdx.x * chunk, b1 = min(n0, b0 + chunk);
+    int c = 0;
+    for (int a = b0; a < b1; ++a) {
+        int isbad = (dg[a] == 0.0) || (use_q && r[a] < q);
+        bad[a] = isbad;
+        c += !isbad;
+    }
+    scan[threadIdx.x] = c;
+    __syncthreads();
+    for (int off = 1; off < T; off <<= 1) {
+        int v = threadIdx.x >= off ? scan[threadIdx.x - off] : 0;
+        __syncthreads();
+        scan[threadIdx.x] += v;
+        __syncthreads();
+    }
+    int pos = scan[threadIdx.x] - c;
+    for (int a = b0; a < b1; ++a)
+        if (!bad[a]) good[pos++] = a;
+    if (threadIdx.x == T - 1) *ngood = scan[T - 1];
+}
+
+void launch_mask_select(const double *d_rowmean, const double *d_diag, int n0, double bad_frac, double qindex,
+                        int *d_bad, int *d_good, int *d_ngood, hipStream_t s) {
+    hipLaunchKernelGGL(k_mask_select, dim3(1), dim3(1024), 0, s, d_rowmean, d_diag, n0, bad_frac, qindex, d_bad,
+                       d_good, d_ngood);
+    TP_HIP(hipGetLastError());
+}
+
+// --------------------------------------- X = M[good, good] + colMeans(X) (dd)
+__global__ void __launch_bounds__(256) k_gather_colmean(const double *M, int n0, const int *good, int n, double *X,
+                                                        double *cm) {
+    int lane = threadIdx.x & 63;
+    int j = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (j >= n) return;
+    const double *src = M + (size_t)good[j] * n0;
+    double *dst = X + (size_t)j * n;
+    double hi = 0.0, lo = 0.0;
+    for (int a = lane; a < n; a += 64) {
+        double v = src[good[a]];
+        dst[a] = v;
+        dd_add_d(hi, lo, v);
+    }
+    wave_dd_sum(hi, lo);
+    if (lane == 0 && cm) cm[j] = dd_div_d(hi, lo, (double)n);
+}
+
+void launch_gather_colmean(const double *d_M, int n0, const int *d_good, int n, double *d_X, double *d_colmean,
+                           hipStream_t s) {
+    hipLaunchKernelGGL(k_gather_colmean, dim3((n + 3) / 4), dim3(256), 0, s, d_M, n0, d_good, n, d_X, d_colmean);
+    TP_HIP(hipGetLastError());
+}
+
+__global__ void __launch_bounds__(256) k_colmean(const double *A, int n, int ld, double *cm) {
+    int lane = threadIdx.x & 63;
+    int j = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (j >= n) return;
+    const double *src = A + (size_t)j * ld;
+    double hi = 0.0, lo = 0.0;
+    for (int a = lane; a < n; a += 64) dd_add_d(hi, lo, src[a]);
+    wave_dd_sum(hi, lo);
+    if (lane == 0) cm[j] = dd_div_d(hi, lo, (double)n);
+}
+
+void launch_colmean(const double *d_A, int n, int ld, double *d_mean, hipStream_t s) {
+    hipLaunchKernelGGL(k_colmean, dim3((n + 3) / 4), dim3(256), 0, s, d_A, n, ld, d_mean);
+    TP_HIP(hipGetLastError());
+}
+
+// ------------------------------------------------- sparse_cor epilogue (R order)
+// cov = (S - n * (m m')) / (n - 1); cor = cov / (sd sd'), sd = sqrt(diag(cov));
+// NaN -> 0 (R/TADpole.R:96-98,449).  Rounding order as R evaluates it.
+__global__ void __launch_bounds__(256) k_cor_epilogue(const double *S, const double *m, int n, double *C) {
+    size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    size_t tot = (size_t)n * n;
+    if (idx >= tot) return;
+    int i = (int)(idx % n), j = (int)(idx / n);
+    const double fn = (double)n, fn1 = (double)(n - 1);
+    double cij = (S[idx] - fn * (m[i] * m[j])) / fn1;
+    double cii = (S[(size_t)i * n + i] - fn * (m[i] * m[i])) / fn1;
+    double cjj = (S[(size_t)j * n + j] - fn * (m[j] * m[j])) / fn1;
+    double v = cij / (sqrt(cii) * sqrt(cjj));
+    if (isnan(v)) v = 0.0;
+    C[idx] = v;
+}
+
+void launch_cor_epilogue(const double *d_S, const double *d_m, int n, double *d_C, hipStream_t s) {
+    size_t tot = (size_t)n * n;
+    hipLaunchKernelGGL(k_cor_epilogue, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, d_S, d_m, n, d_C);
+    TP_HIP(hipGetLastError());
+}
+
+// ------------------------------------------------ prcomp centring (scale(x, TRUE))
+// Xc = C - 1 mean'  and its transpose XcT = C - mean 1' (C symmetric).
+__global__ void __launch_bounds__(256) k_center(const double *C, const double *mean, int n, double *Xc, double *XcT) {
+    size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    size_t tot = (size_t)n * n;
+    if (idx >= tot) return;
+    int a = (int)(idx % n), i = (int)(idx / n);
+    double c = C[idx];
+    Xc[idx] = c - mean[i];
+    if (XcT) XcT[idx] = c - mean[a];
+}
+
+void launch_center(const double *d_C, const double *d_mean, int n, double *d_Xc, double *d_XcT, hipStream_t s) {
+    size_t tot = (size_t)n * n;
+    hipLaunchKernelGGL(k_center, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, d_C, d_mean, n, d_Xc, d_XcT);
+    TP_HIP(hipGetLastError());
+}
+
+// --------------------------------------------------------------- transpose
+__global__ void __launch_bounds__(256) k_transpose(const double *A, int rows, int cols, int lda, double *T, int ldt) {
+    __shared__ double t[32][33];
+    int r0 = blockIdx.x * 32, c0 = blockIdx.y * 32;
+    int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+    for (int y = ty; y < 32; y += 8) {
+        int r = r0 + tx, c = c0 + y;
+        t[y][tx] = (r < rows && c < cols) ? A[(size_t)r + (size_t)c * lda] : 0.0;
+    }
+    __syncthreads();
+    for (int y = ty; y < 32; y += 8) {
+        int c = c0 + tx, r = r0 + y;
+        if (r < rows && c < cols) T[(size_t)c + (size_t)r * ldt] = t[tx][y];
+    }
+}
+
+void launch_transpose(const double *d_A, int rows, int cols, int lda, double *d_T, int ldt, hipStream_t s) {
+    dim3 g((rows + 31) / 32, (cols + 31) / 32);
+    hipLaunchKernelGGL(k_transpose, g, dim3(256), 0, s, d_A, rows, cols, lda, d_T, ldt);
+    TP_HIP(hipGetLastError());
+}
+
+}  // namespace tp

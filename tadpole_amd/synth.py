@@ -1,0 +1,92 @@
+"""Seeded synthetic Hi-C matrices.
+
+The reference ships no matrix for its own example (``README.md:65-68`` names
+``inst/extdata/raw_chr18_300_500_30kb.tsv``, which is absent), so every test and
+bench input is generated here:
+
+* TAD sizes ~ U{10..60} bins, grouped into meta-TADs of 3-6 TADs;
+* ``E_ij = 1000 (1+|i-j|)^-1 (1 + 2[same TAD] + [same meta-TAD])``;
+* ``M_ij ~ Poisson(E_ij)`` for ``i <= j``, mirrored (upper wins);
+* ``zero_frac`` of the bins zeroed (row and column), i.e. bad via ``diag == 0``;
+* optionally a zero run at ``[0.4875 N0, 0.572 N0)`` standing in for a centromere.
+
+Seeds follow the survey: ``20261015 + config index``.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+SEED_BASE = 20261015
+
+#: Config shapes of BASELINE.json (index -> raw bins).  C4/C5 are described in
+#: SURVEY.md §8; C4 uses the hg19 chromosome sizes at 25 kb.
+CONFIG_BINS = {1: 200, 2: 2000, 3: 7808, 5: 49851}
+
+#: hg19 chromosome lengths (bp) for the whole-genome config C4 (@25 kb).
+HG19_BP = {
+    "chr1": 249250621, "chr2": 243199373, "chr3": 198022430, "chr4": 191154276,
+    "chr5": 180915260, "chr6": 171115067, "chr7": 159138663, "chr8": 146364022,
+    "chr9": 141213431, "chr10": 135534747, "chr11": 135006516, "chr12": 133851895,
+    "chr13": 115169878, "chr14": 107349540, "chr15": 102531392, "chr16": 90354753,
+    "chr17": 81195210, "chr18": 78077248, "chr19": 59128983, "chr20": 63025520,
+    "chr21": 48129895, "chr22": 51304566, "chrX": 155270560,
+}
+
+
+def tad_layout(n0: int, rng: np.random.Generator):
+    """Per-bin TAD and meta-TAD ids."""
+    tad = np.empty(n0, np.int64)
+    meta = np.empty(n0, np.int64)
+    pos = t = m = 0
+    while pos < n0:
+        for _ in range(int(rng.integers(3, 7))):
+            if pos >= n0:
+                break
+            e = min(n0, pos + int(rng.integers(10, 61)))
+            tad[pos:e] = t
+            meta[pos:e] = m
+            pos = e
+            t += 1
+        m += 1
+    return tad, meta
+
+
+def synth_hic(n0: int, seed: int, zero_frac: float = 0.005,
+              centromere: bool = False, dtype=np.float64) -> np.ndarray:
+    """Symmetric n0 x n0 synthetic contact matrix (C-contiguous)."""
+    rng = np.random.default_rng(seed)
+    tad, meta = tad_layout(n0, rng)
+    out = np.empty((n0, n0), dtype=dtype)
+    # Row blocks keep the peak memory at a few rows of n0 at a time.
+    blk = max(1, min(n0, (1 << 24) // max(n0, 1)))
+    idx = np.arange(n0)
+    for r0 in range(0, n0, blk):
+        r1 = min(n0, r0 + blk)
+        i = idx[r0:r1, None]
+        e = 1000.0 / (1.0 + np.abs(i - idx[None, :]))
+        e = e * (1.0 + 2.0 * (tad[r0:r1, None] == tad[None, :])
+                 + 1.0 * (meta[r0:r1, None] == meta[None, :]))
+        e[idx[None, :] < i] = 0.0          # draw the upper triangle only
+        out[r0:r1] = rng.poisson(e)
+    iu = np.tril_indices(n0, -1)
+    out[iu] = out.T[iu]                    # mirror: upper wins
+    nz = max(1, int(round(zero_frac * n0))) if zero_frac > 0 else 0
+    if nz:
+        z = rng.choice(n0, nz, replace=False)
+        out[z, :] = 0
+        out[:, z] = 0
+    if centromere:
+        a, b = int(0.4875 * n0), int(0.572 * n0)
+        out[a:b, :] = 0
+        out[:, a:b] = 0
+    return out
+
+
+def config_matrix(config: int, **kw) -> np.ndarray:
+    return synth_hic(CONFIG_BINS[config], SEED_BASE + config,
+                     centromere=(config == 5), **kw)
+
+
+def genome_bins(resol: int = 25000):
+    """Bins per chromosome for C4 (whole genome @resol)."""
+    return {c: -(-bp // resol) for c, bp in HG19_BP.items()}

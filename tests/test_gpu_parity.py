@@ -1,0 +1,246 @@
+"""GPU parity: every stage through the C ABI of libtadpole_hip.so against the
+CPU oracle (oracle/), at sizes the oracle finishes in seconds.
+
+Bars: bit-exact for indices (mask, merge order, boundaries, n_cluster,
+n_pcs/n_clusters, TAD coordinates) and for the canonical-order sweep floats
+(heights, CH scores given identical PC scores); R's dist order bit-exact;
+correlation / PCA (different algorithm from LAPACK) within the tolerances
+written in each test; end-to-end CH within 1e-6 relative (north_star).
+"""
+import numpy as np
+import pytest
+
+import gpu_helpers as G
+import tadpole_oracle as O
+from tadpole_amd.synth import synth_hic
+
+pytestmark = pytest.mark.gpu
+
+
+def _pcs(n0, seed, k=200):
+    m = synth_hic(n0, seed)
+    r = O.tadpole(m, max_pcs=k)
+    return r.pcs
+
+
+# ------------------------------------------------------------------ mask
+
+@pytest.mark.parametrize("n0,seed", [(200, 1), (333, 2), (1000, 3)])
+def test_mask_integer_counts(gpu, n0, seed):
+    m = synth_hic(n0, seed)
+    bad, rm, good = G.mask(m)
+    obad, orm, _ = O.bad_mask(O.clean_symmetrize(m), 0.01)
+    assert np.array_equal(bad, obad)
+    assert np.array_equal(rm, orm)            # integer sums: exact
+    assert np.array_equal(good, np.flatnonzero(~obad))
+
+
+@pytest.mark.parametrize("frac", [0.0, 0.01, 0.05, 0.3, 1.0])
+def test_mask_real_values_nan_and_asymmetric(gpu, frac):
+    rng = np.random.default_rng(7)
+    n0 = 257
+    m = rng.gamma(2.0, 3.0, (n0, n0))          # asymmetric on purpose: upper must win
+    m[rng.random((n0, n0)) < 0.01] = np.nan
+    m[5, 5] = 0.0
+    bad, rm, good = G.mask(m, frac)
+    cm = O.clean_symmetrize(m)
+    obad, orm, _ = O.bad_mask(cm, frac)
+    assert np.array_equal(bad, obad)
+    np.testing.assert_allclose(rm, orm, rtol=2e-16, atol=0)
+    # column-major buffer of the same matrix gives the same answer
+    bad2, _, _ = G.mask(np.asfortranarray(m), frac, flags=0)
+    assert np.array_equal(bad2, obad)
+
+
+def test_mask_ties_and_all_equal(gpu):
+    m = np.ones((64, 64))
+    bad, _, _ = G.mask(m, 0.01)
+    assert not bad.any()                       # r < q is false for ties
+    m[:, 3] = m[3, :] = 0.5
+    bad, _, _ = G.mask(m, 0.01)
+    obad, _, _ = O.bad_mask(O.clean_symmetrize(m), 0.01)
+    assert np.array_equal(bad, obad)
+
+
+# ------------------------------------------------------------------- cor
+
+@pytest.mark.parametrize("n", [64, 198, 515])
+def test_cor(gpu, n):
+    m = synth_hic(n + 3, 11 + n)
+    obad, _, _ = O.bad_mask(O.clean_symmetrize(m), 0.01)
+    g = np.flatnonzero(~obad)
+    x = O.clean_symmetrize(m)[np.ix_(g, g)]
+    c = G.cor(x)
+    oc = O.sparse_cor(x)
+    assert np.array_equal(c, c.T)              # exactly symmetric, as dsyrk + copy
+    np.testing.assert_allclose(c, oc, rtol=0, atol=5e-12)
+
+
+def test_cor_constant_column_nan_to_zero(gpu):
+    rng = np.random.default_rng(3)
+    x = rng.random((40, 40))
+    x = x + x.T
+    x[:, 7] = 2.0
+    x[7, :] = 2.0
+    c = G.cor(x)
+    oc = O.sparse_cor(x)
+    assert np.all(c[7, :] == 0) or np.allclose(c[7, :], oc[7, :], atol=1e-12)
+    np.testing.assert_allclose(c, oc, atol=1e-10)
+
+
+# ------------------------------------------------------------------- pca
+
+def _proj(p, i):
+    q, _ = np.linalg.qr(p[:, :i])
+    return q @ q.T
+
+
+@pytest.mark.parametrize("n0,k", [(120, 120), (200, 200), (700, 200)])
+def test_pca_scores(gpu, n0, k):
+    m = synth_hic(n0, 40 + n0)
+    cm = O.clean_symmetrize(m)
+    obad, _, _ = O.bad_mask(cm, 0.01)
+    g = np.flatnonzero(~obad)
+    c = O.sparse_cor(cm[np.ix_(g, g)])
+    kk = min(k, len(g))
+    p, sd = G.pca(c, kk)
+    op = O.prcomp_x(c, kk)
+    # column signs are arbitrary (irrelevant downstream); compare |columns|
+    s = np.sign(np.sum(p * op, axis=0))
+    s[s == 0] = 1
+    scale = np.abs(op).max()
+    # well separated leading components: elementwise
+    np.testing.assert_allclose(p[:, :20] * s[:20], op[:, :20], atol=1e-9 * scale)
+    # every prefix subspace the sweep uses (distances only see span(P[:, :i]))
+    sv = np.linalg.svd(op, compute_uv=False)
+    for i in (1, 5, 20, kk // 2, kk):
+        if i < kk and sv[i - 1] / max(sv[i], 1e-300) < 1.0 + 1e-6:
+            continue                           # degenerate prefix: not defined by the reference either
+        assert np.abs(_proj(p, i) - _proj(op, i)).max() < 1e-7, i
+
+
+# ---------------------------------------------------------- coniss / dist
+
+@pytest.mark.parametrize("n,c,seed", [(2, 1, 0), (3, 1, 1), (50, 1, 2), (97, 7, 3), (300, 64, 4), (300, 65, 5),
+                                      (400, 200, 6), (513, 256, 7)])
+def test_coniss_bit_exact(gpu, n, c, seed):
+    rng = np.random.default_rng(seed)
+    p = rng.standard_normal((n, c)) * rng.random(c)[None, :] * 10
+    merge, h, bnd = G.coniss(p)
+    ma, mb, co, he = O.coniss(p)
+    assert np.array_equal(bnd, mb)
+    assert np.array_equal(h, he)               # canonical order: bit-identical
+    # hclust encoding is consistent with the boundary order
+    assert merge.shape == (n - 1, 2)
+
+
+def test_coniss_ties_leftmost(gpu):
+    p = np.repeat(np.arange(6.0), 2)[:, None]  # equal adjacent pairs everywhere
+    _, h, bnd = G.coniss(p)
+    _, mb, _, he = O.coniss(p)
+    assert np.array_equal(bnd, mb)
+    assert np.array_equal(h, he)
+
+
+def test_coniss_matches_distance_matrix_definition(gpu):
+    rng = np.random.default_rng(9)
+    p = rng.standard_normal((80, 5))
+    _, h, bnd = G.coniss(p)
+    mb, he = O.coniss_bruteforce(p)
+    assert np.array_equal(bnd, mb)
+    np.testing.assert_allclose(h, he, rtol=1e-10)
+
+
+@pytest.mark.parametrize("n,c", [(2, 1), (33, 3), (300, 20)])
+def test_dist_r_order_bit_exact(gpu, n, c):
+    from scipy.spatial.distance import pdist
+    rng = np.random.default_rng(n)
+    p = rng.standard_normal((n, c))
+    d = G.dist(p)
+    assert np.array_equal(d, O.dist_r(p))
+    np.testing.assert_allclose(d, pdist(p), rtol=1e-13)
+
+
+# -------------------------------------------------------------------- ch
+
+def test_ch_single(gpu):
+    from sklearn.metrics import calinski_harabasz_score
+    rng = np.random.default_rng(5)
+    p = rng.standard_normal((150, 30))
+    lab = np.repeat(np.arange(1, 7), 25)
+    v = G.ch(p, lab)
+    np.testing.assert_allclose(v, calinski_harabasz_score(p, lab), rtol=1e-12)
+    assert np.isnan(G.ch(p, np.ones(150, np.int32)))   # cn = 1: 0/0 as in fpc
+
+
+# ----------------------------------------------------------------- sweep
+
+@pytest.mark.parametrize("n0,k,seed", [(200, 200, 20261016), (420, 60, 12), (700, 200, 13)])
+def test_sweep_bit_exact(gpu, n0, k, seed):
+    p = _pcs(n0, seed, k)
+    got = G.sweep_dev(p)
+    ref = O.sweep(p)
+    assert np.array_equal(got["n_cluster"], ref.n_cluster)
+    assert np.array_equal(got["mrg_b"], ref.mrg_b)
+    assert np.array_equal(got["mrg_a"], ref.mrg_a)
+    assert np.array_equal(got["height"], ref.height)
+    a, b = got["scores"], ref.scores
+    assert a.shape == b.shape
+    assert np.array_equal(a.view(np.uint64), b.view(np.uint64))   # incl. NA bit patterns
+
+
+def test_sweep_selection_and_bstick_r_faithful(gpu):
+    p = _pcs(300, 21)
+    got = G.sweep(p)
+    ref = O.sweep(p)
+    ld = O.sweep(p, bstick="ld")                # R's long double cumsum decides the same
+    assert np.array_equal(ref.n_cluster, ld.n_cluster)
+    assert (got["n_pcs"], got["n_clusters"]) == O.select_params(ref.scores)
+
+
+@pytest.mark.parametrize("mc", [1, 2, 5, 50])
+def test_sweep_min_clusters(gpu, mc):
+    p = _pcs(250, 22, 40)
+    got = G.sweep_dev(p, min_clusters=mc)
+    ref = O.sweep(p, min_clusters=mc)
+    assert np.array_equal(got["scores"].view(np.uint64), ref.scores.view(np.uint64))
+
+
+# -------------------------------------------------------------- pipeline
+
+@pytest.mark.parametrize("n0,seed,max_pcs", [(200, 20261016, 200), (150, 5, 200), (600, 6, 200),
+                                              (900, 7, 50), (64, 8, 10)])
+def test_pipeline_end_to_end(gpu, n0, seed, max_pcs):
+    import tadpole_amd as tp
+    m = synth_hic(n0, seed)
+    got = tp.TADpole(m, max_pcs=max_pcs)
+    ref = O.tadpole(m, max_pcs=max_pcs)
+    assert got.n_pcs == ref.n_pcs
+    assert got.optimal_n_clusters == ref.optimal_n_clusters
+    assert set(got.clusters) == {str(q) for q in ref.clusters}
+    for q, v in ref.clusters.items():
+        assert np.array_equal(got.clusters[str(q)], v), q
+    assert np.array_equal(got.bad_columns, np.flatnonzero(ref.bad) + 1)
+    a, b = got.scores, ref.scores
+    assert a.shape == b.shape
+    fin = ~np.isnan(b)
+    assert np.array_equal(np.isnan(a), ~fin)
+    assert np.max(np.abs(a[fin] - b[fin]) / np.abs(b[fin])) < 1e-6
+    np.testing.assert_allclose(got.dendro.height, ref.height, rtol=1e-8)
+
+
+def test_pipeline_file_input_and_nan(gpu, tmp_path):
+    import tadpole_amd as tp
+    m = synth_hic(180, 31).astype(float)
+    m[3, 100] = np.nan
+    f = tmp_path / "m.tsv"
+    np.savetxt(f, m, delimiter="\t", fmt="%.17g")
+    got = tp.TADpole(str(f))
+    ref = O.tadpole(m)
+    assert (got.n_pcs, got.optimal_n_clusters) == (ref.n_pcs, ref.optimal_n_clusters)
+
+
+def test_pipeline_errors(gpu):
+    import tadpole_amd as tp
+    with pytest.raises(tp.TadpoleError):
+        tp.TADpole(np.zeros((10, 10)))         # everything bad
