@@ -15,6 +15,8 @@
 #include "tp_common.cuh"
 #include "tp_internal.h"
 
+#include <algorithm>
+
 namespace tp {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
@@ -173,7 +175,13 @@ void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s) {
     if (g.sym_upper && g.M != g.N) fail(TP_ERR_ARG, "sym_upper GEMM needs a square output");
     const int tm = (g.M + BM - 1) / BM, tn = (g.N + BN - 1) / BN;
     long nblk = g.sym_upper ? (long)tn * (tn + 1) / 2 : (long)tm * tn;
-    int S = g.splitk < 1 ? 1 : g.splitk;
+    int S = g.splitk;
+    if (S < 1) {
+        // auto: fill the 256 CUs when the output has few tiles and K is long
+        S = 1;
+        if (nblk < 192 && g.K >= 512) S = (int)std::min<long>(8, std::max<long>(1, (384 + nblk - 1) / nblk));
+        S = std::min(S, std::max(1, g.K / 128));
+    }
     int kchunk = ((g.K + S - 1) / S + BK - 1) / BK * BK;
     if (kchunk < BK) kchunk = BK;
     S = (g.K + kchunk - 1) / kchunk;

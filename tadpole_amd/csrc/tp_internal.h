@@ -96,9 +96,10 @@ struct GemmArgs {
     double *C; int ldc;
     bool store_t = false;
     bool sym_upper = false;
-    int splitk = 1;
+    int splitk = 1;     // 0 = choose from the tile count
 };
 void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s);
+void launch_chol_inv(double *d_W, double *d_X, int b, double rel, int *d_info, hipStream_t s);
 
 // sweep (tp_sweep.hip)
 struct SweepDev {

@@ -63,30 +63,6 @@ __global__ void k_rand_block(double *Q, int n, int b, uint64_t seed) {
     Q[idx] = ((double)(z >> 11) * (1.0 / 9007199254740992.0)) * 2.0 - 1.0;
 }
 
-// W <- (W + W')/2 and W_jj += rel * max_j W_jj   (single workgroup)
-__global__ void __launch_bounds__(1024) k_sym_shift(double *W, int b, double rel) {
-    __shared__ double red[1024];
-    double mx = 0.0;
-    for (int j = threadIdx.x; j < b; j += blockDim.x) mx = fmax(mx, W[(size_t)j * b + j]);
-    red[threadIdx.x] = mx;
-    __syncthreads();
-    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
-        if (threadIdx.x < o) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + o]);
-        __syncthreads();
-    }
-    const double s = rel * red[0];
-    for (size_t t = threadIdx.x; t < (size_t)b * b; t += blockDim.x) {
-        int i = (int)(t % b), j = (int)(t / b);
-        if (i < j) {
-            double v = 0.5 * (W[t] + W[(size_t)i * b + j]);
-            W[t] = v;
-            W[(size_t)i * b + j] = v;
-        }
-    }
-    __syncthreads();
-    for (int j = threadIdx.x; j < b; j += blockDim.x) W[(size_t)j * b + j] += s;
-}
-
 // Wk[:, j] = W[:, b-1-j], j < k  (eigenvectors in descending eigenvalue order)
 __global__ void k_select_rev(const double *W, int b, int k, double *Wk) {
     size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -111,28 +87,34 @@ __global__ void __launch_bounds__(256) k_resid(const double *Y, const double *V,
     if (lane == 0) resid[j] = sqrt(acc);
 }
 
-static void orth_cholqr(Ctx &c, rocblas_handle h, double *Z, int n, int b, double *W, int *d_info, int passes,
-                        double first_shift) {
+// Q = orth(Z): W = Z'Z (symmetric GEMM), U = chol(W + s I), X = U^{-1}
+// (one workgroup), Q = Z X.  `passes` CholQR passes (Q feeds the next pass).
+static void orth_cholqr(Ctx &c, double *Z, double *Qout, double *Tmp, int n, int b, double *W, double *X,
+                        int *d_info, int passes, double shift) {
+    double *src = Z;
     for (int p = 0; p < passes; ++p) {
-        GemmArgs g{b, b, n, Z, n, true, Z, n, W, b};
+        GemmArgs g{b, b, n, src, n, true, src, n, W, b};
         g.sym_upper = true;
-        g.splitk = std::max(1, std::min(16, n / 256));
+        g.splitk = std::max(1, std::min(32, n / 128));
         gemm_f64(g, c.buf[S_PARTIAL], c.cur);
-        hipLaunchKernelGGL(k_sym_shift, dim3(1), dim3(1024), 0, c.cur, W, b, p == 0 ? first_shift : 0.0);
-        TP_HIP(hipGetLastError());
-        rb_check(rocsolver_dpotrf(h, rocblas_fill_upper, b, W, b, d_info), "dpotrf");
-        const double one = 1.0;
-        rb_check(rocblas_dtrsm(h, rocblas_side_right, rocblas_fill_upper, rocblas_operation_none,
-                               rocblas_diagonal_non_unit, n, b, &one, W, b, Z, n),
-                 "dtrsm");
+        launch_chol_inv(W, X, b, p == 0 ? shift : 0.0, d_info, c.cur);
+        double *dst = ((passes - 1 - p) % 2 == 0) ? Qout : Tmp;   // last pass lands in Qout
+        GemmArgs q{n, b, b, src, n, false, X, b, dst, n};
+        q.splitk = 0;
+        gemm_f64(q, c.buf[S_PARTIAL], c.cur);
+        src = dst;
     }
+}
+
+// |U_jj| of the last Cholesky (upper triangle of W) -> host, ascending index j
+__global__ void k_diag(const double *W, int b, double *d) {
+    int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < b) d[j] = fabs(W[(size_t)j * b + j]);
 }
 
 PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d_Pt, double *h_sdev) {
     PcaStats st;
     hipStream_t s = c.cur;
-    rocblas_handle h = blas_for(c);
-    rb_check(rocblas_set_pointer_mode(h, rocblas_pointer_mode_host), "pointer mode");
     double *mean = c.buf[S_COLMEAN].as<double>(n);
     double *Xc = c.buf[S_XC].as<double>((size_t)n * n);
     double *XcT = c.buf[S_XCT].as<double>((size_t)n * n);
@@ -146,17 +128,17 @@ PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d
         gemm_f64(g, c.buf[S_PARTIAL], s);
         kprof_end(c, K_G_GEMM);
     }
-    int *d_info = c.buf[S_MISC].as<int>(64);
     const int over = std::max(32, k / 4);
     int b = std::min(n, ((k + over + 31) / 32) * 32);
     st.block = b;
     double *V = c.buf[S_W].as<double>((size_t)n * k);       // n x k, descending
-    double *theta = c.buf[S_SMALL].as<double>((size_t)std::max(n, b) + 64);
-    double *Wsm = nullptr;
     std::vector<double> h_theta;
     if (b >= n) {
-        // exact: eigendecomposition of G itself
+        // exact: eigendecomposition of G itself (small n)
+        rocblas_handle h = blas_for(c);
         b = n;
+        int *d_info = c.buf[S_MISC].as<int>(64);
+        double *theta = c.buf[S_SMALL].as<double>((size_t)n + 64);
         double *E = c.buf[S_Z].as<double>((size_t)n * n);
         TP_HIP(hipMemcpyAsync(E, G, (size_t)n * n * sizeof(double), hipMemcpyDeviceToDevice, s));
         double *offbuf = c.buf[S_Q].as<double>((size_t)n + 64);
@@ -172,69 +154,93 @@ PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d
     } else {
         double *Q = c.buf[S_Q].as<double>((size_t)n * b);
         double *Z = c.buf[S_Z].as<double>((size_t)n * b);
-        Wsm = c.buf[S_SMALL].as<double>((size_t)b * b + 2 * b + 64);
-        theta = Wsm + (size_t)b * b;
+        double *T = c.buf[S_SWEEP].as<double>((size_t)n * b);
+        double *Wsm = c.buf[S_SMALL].as<double>((size_t)2 * b * b + 2 * b + 64);
+        double *Xinv = Wsm + (size_t)b * b;
+        double *theta = Xinv + (size_t)b * b;
         double *offd = theta + b;
-        double *resid = c.buf[S_MISC].as<double>(64 + k) + 64;
-        d_info = c.buf[S_MISC].as<int>(64);
+        double *resid = c.buf[S_MISC].as<double>(64 + k + b) + 64;
+        int *d_info = c.buf[S_MISC].as<int>(64);
         const size_t nb = (size_t)n * b;
-        hipLaunchKernelGGL(k_rand_block, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, s, Q, n, b,
+        hipLaunchKernelGGL(k_rand_block, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, s, Z, n, b,
                            0x5EEDULL + (uint64_t)n);
         TP_HIP(hipGetLastError());
-        orth_cholqr(c, h, Q, n, b, Wsm, d_info, 3, 1e-13);
-        const double target = 1e-12;
-        int done = 0, chunk = 12;
-        const int max_iter = 400;
-        std::vector<double> h_res(k);
-        h_theta.resize(b);
-        for (int round = 0; round < 8; ++round) {
-            for (int it = 0; it < chunk; ++it) {
+        orth_cholqr(c, Z, Q, T, n, b, Wsm, Xinv, d_info, 3, 1e-13);
+        auto iterate = [&](int count) {
+            for (int it = 0; it < count; ++it) {
                 GemmArgs g{n, b, n, G, n, true, Q, n, Z, n};
+                g.splitk = 0;
                 kprof_begin(c, K_GQ_GEMM);
                 gemm_f64(g, c.buf[S_PARTIAL], s);
                 kprof_end(c, K_GQ_GEMM);
-                orth_cholqr(c, h, Z, n, b, Wsm, d_info, 2, 1e-13);
-                std::swap(Q, Z);
+                orth_cholqr(c, Z, Q, T, n, b, Wsm, Xinv, d_info, 1, 1e-14);
             }
-            done += chunk;
-            // Rayleigh-Ritz: H = Q' G Q, eigen-decompose, rotate Q
-            {
-                GemmArgs g{n, b, n, G, n, true, Q, n, Z, n};
-                gemm_f64(g, c.buf[S_PARTIAL], s);
-                GemmArgs hq{b, b, n, Q, n, true, Z, n, Wsm, b};
-                hq.splitk = std::max(1, std::min(16, n / 256));
-                gemm_f64(hq, c.buf[S_PARTIAL], s);
-                hipLaunchKernelGGL(k_sym_shift, dim3(1), dim3(1024), 0, s, Wsm, b, 0.0);
-                rb_check(rocsolver_dsyevd(h, rocblas_evect_original, rocblas_fill_upper, b, Wsm, b, theta, offd,
-                                          d_info),
-                         "dsyevd(RR)");
-                // rotate the whole block: Z = Q * W(desc order), keep as new Q
-                size_t tot = (size_t)b * b;
-                double *Wall = c.buf[S_SWEEP].as<double>(tot);
-                hipLaunchKernelGGL(k_select_rev, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, Wsm, b, b,
-                                   Wall);
-                GemmArgs rq{n, b, b, Q, n, false, Wall, b, Z, n};
-                gemm_f64(rq, c.buf[S_PARTIAL], s);
-                std::swap(Q, Z);
-                // residuals of the top k: Y = G V - V theta
-                GemmArgs gy{n, k, n, G, n, true, Q, n, Z, n};
-                gemm_f64(gy, c.buf[S_PARTIAL], s);
-                hipLaunchKernelGGL(k_resid, dim3((k + 3) / 4), dim3(256), 0, s, Z, Q, theta, n, b, k, resid);
-                TP_HIP(hipGetLastError());
-                TP_HIP(hipMemcpyAsync(h_res.data(), resid, k * sizeof(double), hipMemcpyDeviceToHost, s));
-                TP_HIP(hipMemcpyAsync(h_theta.data(), theta, b * sizeof(double), hipMemcpyDeviceToHost, s));
-                TP_HIP(hipStreamSynchronize(s));
-            }
+        };
+        const double target = 1e-12;
+        const int max_iter = 400;
+        // phase 1: a few iterations, then read the convergence rate off the
+        // Cholesky diagonal (|U_jj| -> lambda_j in orthogonal iteration)
+        int done = 6;
+        iterate(done);
+        {
+            std::vector<double> dg(b);
+            hipLaunchKernelGGL(k_diag, dim3((b + 255) / 256), dim3(256), 0, s, Wsm, b, resid);
+            TP_HIP(hipMemcpyAsync(dg.data(), resid, b * sizeof(double), hipMemcpyDeviceToHost, s));
+            TP_HIP(hipStreamSynchronize(s));
+            double lk = dg[k - 1], lb = dg[b - 1];
+            double rho = (lk > 0 && lb > 0) ? std::min(0.98, std::max(1e-3, lb / lk)) : 0.9;
+            st.rate = rho;
+            int need = (int)std::ceil(std::log(target) / std::log(rho)) + 2;
+            int more = std::max(0, std::min(max_iter - done, need - done));
+            iterate(more);
+            done += more;
+        }
+        std::vector<double> h_res(k);
+        h_theta.resize(b);
+        rocblas_handle h = blas_for(c);
+        for (int round = 0; round < 6; ++round) {
+            // Rayleigh-Ritz: orthonormalise tightly, H = Q'GQ, eigen-decompose, rotate
+            GemmArgs g{n, b, n, G, n, true, Q, n, Z, n};
+            g.splitk = 0;
+            gemm_f64(g, c.buf[S_PARTIAL], s);
+            orth_cholqr(c, Z, Q, T, n, b, Wsm, Xinv, d_info, 2, 1e-14);
+            GemmArgs g2{n, b, n, G, n, true, Q, n, Z, n};
+            g2.splitk = 0;
+            gemm_f64(g2, c.buf[S_PARTIAL], s);
+            GemmArgs hq{b, b, n, Q, n, true, Z, n, Wsm, b};
+            hq.sym_upper = true;
+            hq.splitk = std::max(1, std::min(32, n / 128));
+            gemm_f64(hq, c.buf[S_PARTIAL], s);
+            rb_check(rocsolver_dsyevd(h, rocblas_evect_original, rocblas_fill_upper, b, Wsm, b, theta, offd,
+                                      d_info),
+                     "dsyevd(RR)");
+            size_t tot = (size_t)b * b;
+            hipLaunchKernelGGL(k_select_rev, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, Wsm, b, b, Xinv);
+            GemmArgs rq{n, b, b, Q, n, false, Xinv, b, Z, n};
+            rq.splitk = 0;
+            gemm_f64(rq, c.buf[S_PARTIAL], s);
+            std::swap(Q, Z);
+            // residuals of the top k Ritz pairs: ||G v - theta v||
+            GemmArgs gy{n, k, n, G, n, true, Q, n, Z, n};
+            gy.splitk = 0;
+            gemm_f64(gy, c.buf[S_PARTIAL], s);
+            hipLaunchKernelGGL(k_resid, dim3((k + 3) / 4), dim3(256), 0, s, Z, Q, theta, n, b, k, resid);
+            TP_HIP(hipGetLastError());
+            TP_HIP(hipMemcpyAsync(h_res.data(), resid, k * sizeof(double), hipMemcpyDeviceToHost, s));
+            TP_HIP(hipMemcpyAsync(h_theta.data(), theta, b * sizeof(double), hipMemcpyDeviceToHost, s));
+            TP_HIP(hipStreamSynchronize(s));
             const double th1 = std::fabs(h_theta[b - 1]);
             double worst = 0.0;
             for (int j = 0; j < k; ++j) worst = std::max(worst, h_res[j] / (th1 > 0 ? th1 : 1.0));
             st.resid = worst;
             const double thk = h_theta[b - k], thb = h_theta[0];
-            const double rho = (thk > 0 && thb > 0) ? thb / thk : 0.9;
+            const double rho = (thk > 0 && thb > 0) ? std::min(0.98, std::max(1e-3, thb / thk)) : 0.9;
             st.rate = rho;
-            if (!(worst > target) || done >= max_iter) break;
-            double need = std::log(target / worst) / std::log(std::max(1e-3, std::min(rho, 0.999)));
-            chunk = std::max(4, std::min(max_iter - done, (int)std::ceil(need) + 2));
+            if (!(worst > target * 10) || done >= max_iter) break;
+            int need = (int)std::ceil(std::log(target / worst) / std::log(rho)) + 2;
+            int more = std::max(2, std::min(max_iter - done, need));
+            iterate(more);
+            done += more;
         }
         st.iters = done;
         if (!(st.resid <= 1e-8)) fail(TP_ERR_NUMERIC, "PCA subspace iteration did not converge");
@@ -243,15 +249,15 @@ PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d
     // scores P = Xc V  (= XcT' V): n x k column-major; Pt row-major
     {
         GemmArgs g{n, k, n, XcT, n, true, V, n, d_P, n};
+        g.splitk = 0;
         gemm_f64(g, c.buf[S_PARTIAL], s);
     }
     if (d_Pt) launch_transpose(d_P, n, k, n, d_Pt, k, s);
     if (h_sdev) {
         // prcomp sdev = d / sqrt(max(1, n-1)), d = singular values of Xc = sqrt(eig(G))
-        std::vector<double> th = h_theta;
-        int bb = (int)th.size();
+        int bb = (int)h_theta.size();
         for (int j = 0; j < k; ++j) {
-            double e = th[bb - 1 - j];
+            double e = h_theta[bb - 1 - j];
             h_sdev[j] = std::sqrt(std::max(0.0, e)) / std::sqrt((double)std::max(1, n - 1));
         }
     }
