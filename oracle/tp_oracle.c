@@ -60,10 +60,12 @@ static double butterfly64(double *part) {
 
 /*
  * Ward increment of merging adjacent clusters A (na rows, column sums SA) and
- * B: |A||B|/(|A|+|B|) * ||SA/na - SB/nb||^2 over the first ncols columns.
+ * B: |A||B|/(|A|+|B|) * ||SA/na - SB/nb||^2 over the first ncols columns,
+ * evaluated division-free as sum_j (SA_j nb - SB_j na)^2 / (na nb (na+nb)).
  * This is CONISS's "increase in total dispersion" (Grimm 1987; rioja chclust
- * called at R/TADpole.R:108,374,460).  Canonical order: lane l accumulates
- * j = l, l+64, ... with fma(d, d, acc); xor butterfly; times the weight.
+ * called at R/TADpole.R:108,374,460).  Canonical order: e_j = SA_j*nb - SB_j*na
+ * (two rounded products, one subtraction); lane l accumulates j = l, l+64, ...
+ * with fma(e, e, acc); xor butterfly; one division by na*nb*(na+nb).
  */
 double tpo_ward(const double *SA, int na, const double *SB, int nb, int ncols) {
     double part[LANES];
@@ -71,14 +73,15 @@ double tpo_ward(const double *SA, int na, const double *SB, int nb, int ncols) {
     for (int l = 0; l < LANES; ++l) {
         double acc = 0.0;
         for (int j = l; j < ncols; j += LANES) {
-            double d = SA[j] / fa - SB[j] / fb;
-            acc = fma(d, d, acc);
+            double t1 = SA[j] * fb;
+            double t2 = SB[j] * fa;
+            double e = t1 - t2;
+            acc = fma(e, e, acc);
         }
         part[l] = acc;
     }
     double tot = butterfly64(part);
-    double w = (fa * fb) / (fa + fb);
-    return w * tot;
+    return tot / (fa * fb * (fa + fb));
 }
 
 static inline double nan2inf(double x) { return isnan(x) ? INFINITY : x; }

@@ -236,6 +236,7 @@ static SweepOut run_sweep(Ctx &c, const double *d_Pt, int n, int k, int min_clus
     sd.iseg = c.buf[S_MISC].as<int>((size_t)k * (2 * sd.seg_cap + 2) + 64) + 64;
     sd.err = c.buf[S_MISC].as<int>(64);
     sd.trS = (double *)(c.buf[S_NGOOD].as<char>(64)) + 2;
+    sd.cost0 = c.buf[S_SMALL].as<double>(sweep_cost0_doubles(n, k));
     TP_HIP(hipMemsetAsync(sd.err, 0, sizeof(int), s));
     launch_sweep(sd, s, &c);
     std::vector<int> h_nc(k);
@@ -560,6 +561,7 @@ void tp_coniss(const double *P, const int *n, const int *ncols, const int *devic
         sd.cost = (double *)(((uintptr_t)(sd.mrg_b + (N - 1)) + 15) & ~(uintptr_t)15);
         sd.height = sd.cost + (N - 1);
         sd.n_cluster = c.buf[S_MISC].as<int>(64);
+        sd.cost0 = c.buf[S_SMALL].as<double>(sweep_cost0_doubles(N, 1));
         sd.w_cap = std::max(1, N - 1);
         // CONISS only (the CH half needs a broken-stick cut; not wanted here)
         launch_coniss_only(sd, s);
@@ -668,6 +670,109 @@ void tp_pipeline_dev(const double *d_M, const int *n0, const int *max_pcs, const
         pipeline_common(const_cast<double *>(d_M), n0, max_pcs, min_clusters, bad_frac, flags, c, k_cap, w_cap,
                         bad, n_good, good_idx, k, n_cluster, scores, w, n_pcs, n_clusters, merge, height, boundary,
                         timings_ms);
+    });
+}
+
+
+/* ---- diagnostics (not part of include/tadpole_hip.h) -------------------- */
+
+/* k_chol + k_trsm_ru on a b x b SPD matrix W: U (upper) and Q = Z U^{-1}
+ * for Z = identity (so Q = U^{-1}); mean ms of `reps` (chol, trsm). */
+void tp_debug_chol(const double *W, const int *b, const double *rel, const int *reps, double *U, double *Xinv,
+                   double *ms, int *status) {
+    guarded(status, [&] {
+        Ctx &c = ctx_for(0);
+        hipStream_t s = c.cur;
+        const int B = *b;
+        double *dW = c.buf[S_SMALL].as<double>((size_t)3 * B * B + B);
+        double *dI = dW + (size_t)B * B;
+        double *dX = dI + (size_t)B * B;
+        double *rd = dX + (size_t)B * B;
+        int *info = c.buf[S_MISC].as<int>(64);
+        std::vector<double> eye((size_t)B * B, 0.0);
+        for (int q = 0; q < B; ++q) eye[(size_t)q * B + q] = 1.0;
+        TP_HIP(hipMemcpyAsync(dI, eye.data(), (size_t)B * B * 8, hipMemcpyHostToDevice, s));
+        hipEvent_t e0, e1, e2;
+        TP_HIP(hipEventCreate(&e0));
+        TP_HIP(hipEventCreate(&e1));
+        TP_HIP(hipEventCreate(&e2));
+        float t1 = 0, t2 = 0;
+        for (int r = 0; r < *reps; ++r) {
+            TP_HIP(hipMemcpyAsync(dW, W, (size_t)B * B * 8, hipMemcpyHostToDevice, s));
+            TP_HIP(hipEventRecord(e0, s));
+            launch_chol(dW, rd, B, *rel, info, s);
+            TP_HIP(hipEventRecord(e1, s));
+            launch_trsm_ru(dI, B, B, dW, rd, dX, s);
+            TP_HIP(hipEventRecord(e2, s));
+            TP_HIP(hipEventSynchronize(e2));
+            float a = 0, bb = 0;
+            TP_HIP(hipEventElapsedTime(&a, e0, e1));
+            TP_HIP(hipEventElapsedTime(&bb, e1, e2));
+            t1 += a;
+            t2 += bb;
+        }
+        // one stamped run: cycles of (a) diag factor, (b) panel solve, (c) trailing, prologue
+        long long *dst = (long long *)c.buf[S_MISC].as<char>(1024) + 32;
+        TP_HIP(hipMemcpyAsync(dW, W, (size_t)B * B * 8, hipMemcpyHostToDevice, s));
+        launch_chol_stamped(dW, rd, B, *rel, info, dst, s);
+        long long hst[4];
+        TP_HIP(hipMemcpyAsync(hst, dst, 32, hipMemcpyDeviceToHost, s));
+        TP_HIP(hipStreamSynchronize(s));
+        for (int q = 0; q < 4; ++q) ms[2 + q] = (double)hst[q];
+        TP_HIP(hipMemcpyAsync(U, dW, (size_t)B * B * 8, hipMemcpyDeviceToHost, s));
+        TP_HIP(hipMemcpyAsync(Xinv, dX, (size_t)B * B * 8, hipMemcpyDeviceToHost, s));
+        TP_HIP(hipStreamSynchronize(s));
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        (void)hipEventDestroy(e2);
+        ms[0] = t1 / *reps;
+        ms[1] = t2 / *reps;
+    });
+}
+
+/* stamped CONISS for trees 1..k on P (n x k col-major): stamps[k * 8]
+ * (cycles per phase: argmin, loads, costs, update, init, bstick), kernel ms. */
+void tp_debug_coniss_stamps(const double *P, const int *n, const int *k, long long *stamps, double *ms,
+                            int *status) {
+    guarded(status, [&] {
+        Ctx &c = ctx_for(0);
+        hipStream_t s = c.cur;
+        const int N = *n, K = *k;
+        double *dP = c.buf[S_P].as<double>((size_t)N * K);
+        double *dPt = c.buf[S_PT].as<double>((size_t)N * K);
+        TP_HIP(hipMemcpyAsync(dP, P, (size_t)N * K * 8, hipMemcpyHostToDevice, s));
+        launch_transpose(dP, N, K, N, dPt, K, s);
+        SweepDev sd{};
+        sd.Pt = dPt;
+        sd.n = N;
+        sd.ldp = K;
+        sd.k = K;
+        sd.tree0 = 0;
+        sd.ntrees = K;
+        sd.sums = c.buf[S_SWEEP].as<double>(sweep_sums_doubles(N, 0, K));
+        const size_t rec = (size_t)K * (N - 1);
+        char *recbuf = c.buf[S_SWEEP2].as<char>(rec * 24 + 256);
+        sd.mrg_a = (int *)recbuf;
+        sd.mrg_b = sd.mrg_a + rec;
+        sd.cost = (double *)(((uintptr_t)(sd.mrg_b + rec) + 15) & ~(uintptr_t)15);
+        sd.height = sd.cost + rec;
+        sd.n_cluster = c.buf[S_MISC].as<int>(K + 64);
+        long long *dst = (long long *)c.buf[S_SCORES].as<char>((size_t)K * 8 * 8);
+        sd.stamps = dst;
+        sd.cost0 = c.buf[S_SMALL].as<double>(sweep_cost0_doubles(N, K));
+        hipEvent_t e0, e1;
+        TP_HIP(hipEventCreate(&e0));
+        TP_HIP(hipEventCreate(&e1));
+        TP_HIP(hipEventRecord(e0, s));
+        launch_coniss_stamped(sd, s);
+        TP_HIP(hipEventRecord(e1, s));
+        TP_HIP(hipEventSynchronize(e1));
+        float t = 0;
+        TP_HIP(hipEventElapsedTime(&t, e0, e1));
+        *ms = t;
+        TP_HIP(hipMemcpy(stamps, dst, (size_t)K * 8 * 8, hipMemcpyDeviceToHost));
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
     });
 }
 

@@ -99,7 +99,11 @@ struct GemmArgs {
     int splitk = 1;     // 0 = choose from the tile count
 };
 void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s);
-void launch_chol_inv(double *d_W, double *d_X, int b, double rel, int *d_info, hipStream_t s);
+void launch_chol(double *d_W, double *d_rdiag, int b, double rel, int *d_info, hipStream_t s);
+void launch_chol_stamped(double *d_W, double *d_rdiag, int b, double rel, int *d_info, long long *d_st,
+                         hipStream_t s);
+void launch_trsm_ru(const double *d_Z, int n, int b, const double *d_U, const double *d_rdiag, double *d_Q,
+                    hipStream_t s);
 
 // sweep (tp_sweep.hip)
 struct SweepDev {
@@ -119,11 +123,15 @@ struct SweepDev {
     int seg_cap;        // max cut size the CH kernel handles
     double *trS;        // 1
     int *err;           // device flag: 1 = a cut exceeded seg_cap / w_cap
+    long long *stamps = nullptr;   // diagnostic builds only (k_coniss_t<true>)
+    double *cost0 = nullptr;       // ntrees x roundup(n, 64) initial costs (scratch)
 };
+inline size_t sweep_cost0_doubles(int n, int ntrees) { return (size_t)ntrees * ((n + 63) / 64) * 64; }
 size_t sweep_sums_doubles(int n, int tree0, int ntrees);
 void blas_shutdown_all();
 void launch_sweep(const SweepDev &sd, hipStream_t s, Ctx *prof = nullptr);
 void launch_coniss_only(const SweepDev &sd, hipStream_t s);
+void launch_coniss_stamped(const SweepDev &sd, hipStream_t s);
 void launch_ch_only(const double *d_Pt, int n, int ldp, int k, const int *d_bnd,
                     int cn, double *d_seg, double *d_out, hipStream_t s);
 void launch_dist(const double *d_P, int n, int ldp, int ncols, double *d_d, hipStream_t s);

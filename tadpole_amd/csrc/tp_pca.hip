@@ -87,8 +87,8 @@ __global__ void __launch_bounds__(256) k_resid(const double *Y, const double *V,
     if (lane == 0) resid[j] = sqrt(acc);
 }
 
-// Q = orth(Z): W = Z'Z (symmetric GEMM), U = chol(W + s I), X = U^{-1}
-// (one workgroup), Q = Z X.  `passes` CholQR passes (Q feeds the next pass).
+// Q = orth(Z): W = Z'Z (symmetric GEMM), U = chol(W + s I) (one workgroup),
+// Q = Z U^{-1} (row-block TRSM).  `passes` CholQR passes.  X holds 1/diag(U).
 static void orth_cholqr(Ctx &c, double *Z, double *Qout, double *Tmp, int n, int b, double *W, double *X,
                         int *d_info, int passes, double shift) {
     double *src = Z;
@@ -97,13 +97,21 @@ static void orth_cholqr(Ctx &c, double *Z, double *Qout, double *Tmp, int n, int
         g.sym_upper = true;
         g.splitk = std::max(1, std::min(32, n / 128));
         gemm_f64(g, c.buf[S_PARTIAL], c.cur);
-        launch_chol_inv(W, X, b, p == 0 ? shift : 0.0, d_info, c.cur);
+        launch_chol(W, X, b, p == 0 ? shift : 0.0, d_info, c.cur);
         double *dst = ((passes - 1 - p) % 2 == 0) ? Qout : Tmp;   // last pass lands in Qout
-        GemmArgs q{n, b, b, src, n, false, X, b, dst, n};
-        q.splitk = 0;
-        gemm_f64(q, c.buf[S_PARTIAL], c.cur);
+        launch_trsm_ru(src, n, b, W, X, dst, c.cur);
         src = dst;
     }
+}
+
+// Chebyshev three-term step: Y = alpha * GY + beta * Yc + gamma * Yp (n x b)
+__global__ void k_cheb(double *Y, const double *GY, const double *Yc, const double *Yp, size_t cnt, double alpha,
+                       double beta, double gamma) {
+    size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= cnt) return;
+    double v = alpha * GY[t] + beta * Yc[t];
+    if (Yp) v = v + gamma * Yp[t];
+    Y[t] = v;
 }
 
 // |U_jj| of the last Cholesky (upper triangle of W) -> host, ascending index j
@@ -166,34 +174,84 @@ PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d
                            0x5EEDULL + (uint64_t)n);
         TP_HIP(hipGetLastError());
         orth_cholqr(c, Z, Q, T, n, b, Wsm, Xinv, d_info, 3, 1e-13);
-        auto iterate = [&](int count) {
+        double *Yb = c.buf[S_SWEEP2].as<double>((size_t)n * b);   // 4th block buffer (sweep scratch later)
+        auto gemm_gq = [&](const double *Yin, double *Out) {
+            GemmArgs g{n, b, n, G, n, true, Yin, n, Out, n};
+            g.splitk = 0;
+            kprof_begin(c, K_GQ_GEMM);
+            gemm_f64(g, c.buf[S_PARTIAL], s);
+            kprof_end(c, K_GQ_GEMM);
+        };
+        auto iterate = [&](int count) {   // plain subspace iteration
             for (int it = 0; it < count; ++it) {
-                GemmArgs g{n, b, n, G, n, true, Q, n, Z, n};
-                g.splitk = 0;
-                kprof_begin(c, K_GQ_GEMM);
-                gemm_f64(g, c.buf[S_PARTIAL], s);
-                kprof_end(c, K_GQ_GEMM);
+                gemm_gq(Q, Z);
                 orth_cholqr(c, Z, Q, T, n, b, Wsm, Xinv, d_info, 1, 1e-14);
             }
         };
+        // Chebyshev filter of degree m on [0, cut]: Q <- orth(T_m((G - e)/h) Q),
+        // e = h = cut / 2 (scaled three-term recurrence), then CholQR
+        auto cheb_block = [&](int m, double cut) {
+            const double e = 0.5 * cut, hh = 0.5 * cut;
+            const size_t cnt = (size_t)n * b;
+            const unsigned grid = (unsigned)((cnt + 255) / 256);
+            double *prev = Q, *cur = T, *gy = Z, *nxt = Yb;
+            gemm_gq(Q, gy);
+            hipLaunchKernelGGL(k_cheb, dim3(grid), dim3(256), 0, s, cur, gy, Q, (const double *)nullptr, cnt,
+                               1.0 / hh, -e / hh, 0.0);
+            for (int j = 1; j < m; ++j) {
+                gemm_gq(cur, gy);
+                hipLaunchKernelGGL(k_cheb, dim3(grid), dim3(256), 0, s, nxt, gy, cur, prev, cnt, 2.0 / hh,
+                                   -2.0 * e / hh, -1.0);
+                double *old = prev;
+                prev = cur;
+                cur = nxt;
+                nxt = old;
+            }
+            TP_HIP(hipGetLastError());
+            // cur holds Y_m; orthonormalise into Q (the CholQR temp must differ)
+            double *tmp = (cur == T) ? Yb : T;
+            if (cur == Q) {   // never: Q is Y_0 and m >= 1, but keep the buffers distinct
+                TP_HIP(hipMemcpyAsync(tmp, cur, cnt * sizeof(double), hipMemcpyDeviceToDevice, s));
+                cur = tmp;
+                tmp = (cur == T) ? Yb : T;
+            }
+            orth_cholqr(c, cur, Q, tmp, n, b, Wsm, Xinv, d_info, 1, 1e-14);
+        };
         const double target = 1e-12;
-        const int max_iter = 400;
-        // phase 1: a few iterations, then read the convergence rate off the
+        const int max_deg = 600;
+        // phase 1: a few plain iterations, then read the spectrum estimate off the
         // Cholesky diagonal (|U_jj| -> lambda_j in orthogonal iteration)
-        int done = 6;
+        int done = 4;
         iterate(done);
+        double cut = 0.0, gk = 2.0;
+        int mdeg = 1;
         {
             std::vector<double> dg(b);
             hipLaunchKernelGGL(k_diag, dim3((b + 255) / 256), dim3(256), 0, s, Wsm, b, resid);
             TP_HIP(hipMemcpyAsync(dg.data(), resid, b * sizeof(double), hipMemcpyDeviceToHost, s));
             TP_HIP(hipStreamSynchronize(s));
-            double lk = dg[k - 1], lb = dg[b - 1];
-            double rho = (lk > 0 && lb > 0) ? std::min(0.98, std::max(1e-3, lb / lk)) : 0.9;
-            st.rate = rho;
-            int need = (int)std::ceil(std::log(target) / std::log(rho)) + 2;
-            int more = std::max(0, std::min(max_iter - done, need - done));
-            iterate(more);
-            done += more;
+            const double l1 = dg[0], lk = dg[k - 1], lb = dg[b - 1];
+            cut = lb;
+            if (cut > 0 && lk > cut && l1 >= lk) {
+                const double x1 = 2.0 * l1 / cut - 1.0, xk = 2.0 * lk / cut - 1.0;
+                const double g1 = x1 + std::sqrt(x1 * x1 - 1.0);
+                gk = xk + std::sqrt(xk * xk - 1.0);
+                // keep the filtered block CholQR-conditionable: (g1/gk)^m <= 1e6
+                mdeg = (int)std::floor(std::log(1e6) / std::log(std::max(g1 / gk, 1.0001)));
+                mdeg = std::max(1, std::min(8, mdeg));
+            } else {
+                cut = 0.0;
+            }
+            st.rate = gk > 1 ? 1.0 / gk : 0.9;
+            int need = (int)std::ceil(std::log(1.0 / target) / std::log(std::max(gk, 1.0005))) + 2;
+            need = std::min(need, max_deg);
+            if (cut > 0) {
+                for (int deg = 0; deg < need; deg += mdeg) cheb_block(mdeg, cut);
+                done += need;
+            } else {
+                iterate(need);
+                done += need;
+            }
         }
         std::vector<double> h_res(k);
         h_theta.resize(b);
@@ -236,10 +294,16 @@ PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d
             const double thk = h_theta[b - k], thb = h_theta[0];
             const double rho = (thk > 0 && thb > 0) ? std::min(0.98, std::max(1e-3, thb / thk)) : 0.9;
             st.rate = rho;
-            if (!(worst > target * 10) || done >= max_iter) break;
+            if (!(worst > target * 10) || done >= max_deg) break;
             int need = (int)std::ceil(std::log(target / worst) / std::log(rho)) + 2;
-            int more = std::max(2, std::min(max_iter - done, need));
-            iterate(more);
+            int more = std::max(2, std::min(max_deg - done, need));
+            if (cut > 0) {
+                // Ritz values bound the spectrum better now: cut at theta_b
+                cut = std::max(cut, thb);
+                for (int deg = 0; deg < more; deg += mdeg) cheb_block(mdeg, cut);
+            } else {
+                iterate(more);
+            }
             done += more;
         }
         st.iters = done;

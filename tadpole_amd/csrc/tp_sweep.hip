@@ -27,13 +27,27 @@ constexpr int KMAXSLOT = 4;   // columns per lane: k <= 256
 __device__ __forceinline__ bool key_less(double v1, int i1, double v2, int i2) {
     return v1 < v2 || (v1 == v2 && i1 < i2);
 }
+template <int CTRL> __device__ __forceinline__ void amin_step(double &v, int &idx) {
+    double v2 = dpp_d<CTRL>(v);
+    int i2 = dpp_i<CTRL>(idx);
+    if (key_less(v2, i2, v, idx)) { v = v2; idx = i2; }
+}
+// lexicographic (value, index) minimum over the wave; every lane gets it
 __device__ __forceinline__ void wave_argmin(double &v, int &idx) {
+    amin_step<0xB1>(v, idx);
+    amin_step<0x4E>(v, idx);
+    amin_step<0x141>(v, idx);
+    amin_step<0x140>(v, idx);
+    double bv = readlane_d(v, 0);
+    int bi = __builtin_amdgcn_readlane(idx, 0);
 #pragma unroll
-    for (int m = 1; m < 64; m <<= 1) {
-        double v2 = __shfl_xor(v, m, 64);
-        int i2 = __shfl_xor(idx, m, 64);
-        if (key_less(v2, i2, v, idx)) { v = v2; idx = i2; }
+    for (int r = 16; r < 64; r += 16) {
+        double v2 = readlane_d(v, r);
+        int i2 = __builtin_amdgcn_readlane(idx, r);
+        if (key_less(v2, i2, bv, bi)) { bv = v2; bi = i2; }
     }
+    v = bv;
+    idx = bi;
 }
 
 // pairwise tree over 64 leaves = the xor butterfly's summation tree
@@ -54,157 +68,245 @@ size_t sweep_sums_doubles(int n, int tree0, int ntrees) { return sums_off(n, tre
 
 __device__ __forceinline__ double nan2inf(double x) { return isnan(x) ? __longlong_as_double(0x7FF0000000000000LL) : x; }
 
-__global__ void __launch_bounds__(64) k_coniss(SweepDev sd) {
-    extern __shared__ double lds[];
+// STAMPS: diagnostic build accumulating s_memtime cycles per merge phase into
+// sd.stamps[tree * 8 + phase] (0 argmin, 1 links + sum loads, 2 costs,
+// 3 LDS update + refresh, 4 init, 5 bstick).  The product launches STAMPS=false.
+//
+// Argmin without index keys: candidate costs are never NaN (NaN -> +inf) and a
+// non-candidate position holds NaN, which v_min ignores.  The smallest value is
+// found with a DPP min-reduction; the leftmost position holding it is the
+// lowest set bit of a ballot (positions ascend with lane and block), which is
+// exactly the oracle's (value, position) lexicographic rule.  Block minima are
+// values only (NaN = block has no candidate).
+//
+// Synchronisation: the workgroup is one wave.  Every lane writes the same value
+// to each shared LDS word it updates, so no barrier is needed in the loop.
+
+__device__ __forceinline__ double wave_min(double v) {   // ignores NaN lanes
+    v = fmin(v, dpp_d<0xB1>(v));
+    v = fmin(v, dpp_d<0x4E>(v));
+    v = fmin(v, dpp_d<0x141>(v));
+    v = fmin(v, dpp_d<0x140>(v));
+    double r0 = readlane_d(v, 0), r1 = readlane_d(v, 16), r2 = readlane_d(v, 32), r3 = readlane_d(v, 48);
+    return fmin(fmin(r0, r1), fmin(r2, r3));
+}
+
+// two canonical wave sums interleaved (independent chains, same bits as wave_sum)
+__device__ __forceinline__ void wave_sum2(double &u, double &v) {
+    u = u + dpp_d<0xB1>(u);
+    v = v + dpp_d<0xB1>(v);
+    u = u + dpp_d<0x4E>(u);
+    v = v + dpp_d<0x4E>(v);
+    u = u + dpp_d<0x141>(u);
+    v = v + dpp_d<0x141>(v);
+    u = u + dpp_d<0x140>(u);
+    v = v + dpp_d<0x140>(v);
+    double u0 = readlane_d(u, 0), u1 = readlane_d(u, 16), u2 = readlane_d(u, 32), u3 = readlane_d(u, 48);
+    double v0 = readlane_d(v, 0), v1 = readlane_d(v, 16), v2 = readlane_d(v, 32), v3 = readlane_d(v, 48);
+    u = (u0 + u1) + (u2 + u3);
+    v = (v0 + v1) + (v2 + v3);
+}
+
+__device__ __forceinline__ double ward_part(const double (&sa)[KMAXSLOT], double fa, const double (&sb)[KMAXSLOT],
+                                            double fb, int lane, int ncols) {
+    double acc = 0.0;
+#pragma unroll
+    for (int t = 0; t < KMAXSLOT; ++t)
+        if (lane + 64 * t < ncols) {
+            double t1 = sa[t] * fb;
+            double t2 = sb[t] * fa;
+            double e = t1 - t2;
+            acc = fma(e, e, acc);
+        }
+    return acc;
+}
+
+// ---- seeding: every tree's cluster-sum slab starts as the first i columns of
+// the scores, and the initial adjacent (singleton) costs are e_j = x_j - y_j,
+// cost = tot / 2 (canonical order).  One wave per (tree, 64 positions).
+__global__ void __launch_bounds__(64) k_seed(SweepDev sd, double *cost0) {
     const int n = sd.n, ldp = sd.ldp;
+    const int ti = blockIdx.x, i = sd.tree0 + ti + 1;
+    const int lane = threadIdx.x;
+    double *S = sd.sums + sums_off(n, sd.tree0, i);
+    double *c0 = cost0 + (size_t)ti * ((n + 63) / 64) * 64;
+    const int p0 = blockIdx.y * 64;
+    const double QNAN = __longlong_as_double(0x7FF8000000000000LL);
+    double x[KMAXSLOT], y[KMAXSLOT];
+    {
+        const int p = p0;
+#pragma unroll
+        for (int t = 0; t < KMAXSLOT; ++t) {
+            const int j = lane + 64 * t;
+            y[t] = (p < n && j < i) ? sd.Pt[(size_t)p * ldp + j] : 0.0;
+        }
+    }
+    double mycost = QNAN;
+    for (int q = 0; q < 64; ++q) {
+        const int p = p0 + q;
+        if (p >= n) break;
+#pragma unroll
+        for (int t = 0; t < KMAXSLOT; ++t) {
+            x[t] = y[t];
+            const int j = lane + 64 * t;
+            if (j < i) S[(size_t)p * i + j] = x[t];
+            y[t] = (p + 1 < n && j < i) ? sd.Pt[(size_t)(p + 1) * ldp + j] : 0.0;
+        }
+        if (p + 1 < n) {
+            double acc = 0.0;
+#pragma unroll
+            for (int t = 0; t < KMAXSLOT; ++t)
+                if (lane + 64 * t < i) {
+                    double e = x[t] - y[t];
+                    acc = fma(e, e, acc);
+                }
+            double tot = wave_sum(acc);
+            if (lane == q) mycost = nan2inf(tot / 2.0);
+        }
+    }
+    c0[p0 + lane] = mycost;
+}
+
+constexpr int BSLOT = 4;   // block minima per lane (registers): n <= 64 * 64 * BSLOT
+
+template <bool STAMPS>
+__global__ void __launch_bounds__(64) k_coniss_t(SweepDev sd, const double *cost0) {
+    long long st_acc[6] = {0, 0, 0, 0, 0, 0};
+    long long st_t0 = STAMPS ? (long long)__builtin_amdgcn_s_memtime() : 0;
+#define TP_STAMP(ph)                                                      \
+    if (STAMPS) {                                                         \
+        long long _t = (long long)__builtin_amdgcn_s_memtime();           \
+        st_acc[ph] += _t - st_t0;                                         \
+        st_t0 = _t;                                                       \
+    }
+    extern __shared__ double lds[];
+    const int n = sd.n;
     const int ti = blockIdx.x;                 // tree slot
     const int i = sd.tree0 + ti + 1;           // PC prefix length
     const int lane = threadIdx.x;
     const int nbk = (n + 63) / 64;
-    const double INF = __longlong_as_double(0x7FF0000000000000LL);
     const double QNAN = __longlong_as_double(0x7FF8000000000000LL);
-    double *cost = lds;                      // n
-    double *bmv = cost + n;                  // nbk
-    int *bmi = (int *)(bmv + nbk);           // nbk
-    int *link = bmi + nbk + (nbk & 1);       // n
-    const double *Pt = sd.Pt;
+    double *cost = lds;                        // nbk*64: NaN = not a candidate
+    int *link = (int *)(cost + nbk * 64);      // n: cluster start <-> end
+    int *rn = link + n;                        // n: end of the right neighbour (at cluster starts)
     double *S = sd.sums + sums_off(n, sd.tree0, i);
     int *mrg_a = sd.mrg_a + (size_t)ti * (n - 1);
     int *mrg_b = sd.mrg_b + (size_t)ti * (n - 1);
     double *mcost = sd.cost + (size_t)ti * (n - 1);
     double *height = sd.height + (size_t)ti * (n - 1);
+    const double *c0 = cost0 + (size_t)ti * nbk * 64;
 
-    // ---- initial adjacent costs (singletons: weight 1/2), lane-serial canonical tree
-    for (int p = lane; p < n; p += 64) {
-        link[p] = p;
-        if (p < n - 1) {
-            const double *x = Pt + (size_t)p * ldp;
-            const double *y = x + ldp;
-            auto leaf = [&](int m) {
-                double acc = 0.0;
+    double bmr[BSLOT];
 #pragma unroll
-                for (int t = 0; t < KMAXSLOT; ++t) {
-                    int j = m + 64 * t;
-                    if (j < i) {
-                        double d = x[j] - y[j];
-                        acc = fma(d, d, acc);
-                    }
-                }
-                return acc;
-            };
-            double tot = PTree<64>::run(leaf, 0);
-            cost[p] = nan2inf(0.5 * tot);
-        } else {
-            cost[p] = QNAN;   // no right neighbour: not a candidate
+    for (int q = 0; q < BSLOT; ++q) bmr[q] = QNAN;
+    for (int bk = 0; bk < nbk; ++bk) {
+        const int p = bk * 64 + lane;
+        const double cp = c0[p];
+        cost[p] = cp;
+        if (p < n) {
+            link[p] = p;
+            rn[p] = p + 1 < n ? p + 1 : -1;
+        }
+        const double m = wave_min(cp);
+        if (lane == (bk & 63)) {
+#pragma unroll
+            for (int q = 0; q < BSLOT; ++q)
+                if (q == (bk >> 6)) bmr[q] = m;
         }
     }
     __syncthreads();
-    for (int b = 0; b < nbk; ++b) {
-        int p = b * 64 + lane;
-        double v = INF;
-        int idx = p + n;
-        if (p < n && !isnan(cost[p])) { v = cost[p]; idx = p; }
-        wave_argmin(v, idx);
-        if (lane == 0) { bmv[b] = v; bmi[b] = idx; }
-    }
-    __syncthreads();
+    TP_STAMP(4);
 
     double h = 0.0;
     for (int s = 0; s < n - 1; ++s) {
-        // ---- global argmin over block minima
-        double v = INF;
-        int idx = 0x7FFFFFFF;
-        for (int b = lane; b < nbk; b += 64)
-            if (key_less(bmv[b], bmi[b], v, idx)) { v = bmv[b]; idx = bmi[b]; }
-        wave_argmin(v, idx);
-        const int a = idx;                // a candidate always exists here
+        // ---- global argmin: smallest block minimum, leftmost block, leftmost lane
+        double gv = bmr[0];
+#pragma unroll
+        for (int q = 1; q < BSLOT; ++q) gv = fmin(gv, bmr[q]);
+        const double vmin = wave_min(gv);
+        int blk = 0;
+#pragma unroll
+        for (int q = BSLOT - 1; q >= 0; --q) {
+            const unsigned long long m = __ballot(bmr[q] == vmin);
+            if (m) blk = 64 * q + (int)__builtin_ctzll(m);
+        }
+        const unsigned long long mp = __ballot(cost[blk * 64 + lane] == vmin);
+        const int a = blk * 64 + (int)__builtin_ctzll(mp);
+        TP_STAMP(0);
         const int ea = link[a];
-        const int b = ea + 1;
-        const int eb = link[b];
+        const int eb = rn[a];
         const int ls = a > 0 ? link[a - 1] : -1;
+        const int b = ea + 1;
         const int r = eb + 1 < n ? eb + 1 : -1;
-        const int er = r >= 0 ? link[r] : -1;
-        const double c = cost[a];
-        const int na = ea - a + 1, nbb = eb - b + 1, nm = na + nbb;
-        const int nl = ls >= 0 ? a - ls : 0, nr = r >= 0 ? er - r + 1 : 0;
-        // ---- cluster sums (singletons straight from the scores)
+        // ---- cluster sums (addresses need only a, ls, b, r)
         double sa[KMAXSLOT], sb[KMAXSLOT], sl[KMAXSLOT], sr[KMAXSLOT];
+        const double *pa = S + (size_t)a * i, *pb = S + (size_t)b * i;
+        const double *pl = S + (size_t)(ls >= 0 ? ls : a) * i, *pr = S + (size_t)(r >= 0 ? r : a) * i;
 #pragma unroll
         for (int t = 0; t < KMAXSLOT; ++t) {
-            int j = lane + 64 * t;
-            sa[t] = sb[t] = sl[t] = sr[t] = 0.0;
-            if (j < i) {
-                sa[t] = na == 1 ? Pt[(size_t)a * ldp + j] : S[(size_t)a * i + j];
-                sb[t] = nbb == 1 ? Pt[(size_t)b * ldp + j] : S[(size_t)b * i + j];
-                if (ls >= 0) sl[t] = nl == 1 ? Pt[(size_t)ls * ldp + j] : S[(size_t)ls * i + j];
-                if (r >= 0) sr[t] = nr == 1 ? Pt[(size_t)r * ldp + j] : S[(size_t)r * i + j];
-            }
+            const int j = lane + 64 * t;
+            const bool ok = j < i;
+            const int jj = ok ? j : 0;
+            sa[t] = ok ? pa[jj] : 0.0;
+            sb[t] = ok ? pb[jj] : 0.0;
+            sl[t] = ok ? pl[jj] : 0.0;
+            sr[t] = ok ? pr[jj] : 0.0;
         }
+        const int er = r >= 0 ? rn[b] : -1;
+        const double c = vmin;
+        const int na = ea - a + 1, nbb = eb - b + 1, nm = na + nbb;
+        const int nl = ls >= 0 ? a - ls : 0, nr = r >= 0 ? er - r + 1 : 0;
         double sm[KMAXSLOT];
+        if (STAMPS) {   // force the loads to land before the stamp
+            double z = 0.0;
+#pragma unroll
+            for (int t = 0; t < KMAXSLOT; ++t) z += sa[t] + sb[t] + sl[t] + sr[t];
+            if (z == 12345.678) sd.stamps[0] = 1;
+        }
+        TP_STAMP(1);
 #pragma unroll
         for (int t = 0; t < KMAXSLOT; ++t) {
             sm[t] = sa[t] + sb[t];
-            int j = lane + 64 * t;
+            const int j = lane + 64 * t;
             if (j < i) S[(size_t)a * i + j] = sm[t];
         }
-        // ---- the two new adjacent costs
-        const double fm = (double)nm;
-        double cl = QNAN, cr = QNAN;
-        if (ls >= 0) {
-            const double fl = (double)nl;
-            double acc = 0.0;
-#pragma unroll
-            for (int t = 0; t < KMAXSLOT; ++t)
-                if (lane + 64 * t < i) {
-                    double d = sl[t] / fl - sm[t] / fm;
-                    acc = fma(d, d, acc);
-                }
-            double tot = wave_sum(acc);
-            cl = nan2inf(((fl * fm) / (fl + fm)) * tot);
-        }
-        if (r >= 0) {
-            const double fr = (double)nr;
-            double acc = 0.0;
-#pragma unroll
-            for (int t = 0; t < KMAXSLOT; ++t)
-                if (lane + 64 * t < i) {
-                    double d = sm[t] / fm - sr[t] / fr;
-                    acc = fma(d, d, acc);
-                }
-            double tot = wave_sum(acc);
-            cr = nan2inf(((fm * fr) / (fm + fr)) * tot);
-        }
+        // ---- the two new adjacent costs (division-free Ward form), paired
+        const double fm = (double)nm, fl = (double)nl, fr = (double)nr;
+        double ul = ward_part(sl, fl, sm, fm, lane, i);
+        double ur = ward_part(sm, fm, sr, fr, lane, i);
+        wave_sum2(ul, ur);
+        const double cl = ls >= 0 ? nan2inf(ul / (fl * fm * (fl + fm))) : QNAN;
+        const double cr = r >= 0 ? nan2inf(ur / (fm * fr * (fm + fr))) : QNAN;
         h = h + c;
+        TP_STAMP(2);
         if (lane == 0) {
             mrg_a[s] = a;
             mrg_b[s] = b;
             mcost[s] = c;
             height[s] = h;
-            link[a] = eb;
-            link[eb] = a;
-            cost[b] = QNAN;
-            cost[a] = cr;                 // QNAN when there is no right neighbour
-            if (ls >= 0) cost[ls] = cl;
         }
-        __syncthreads();
-        // ---- refresh the block minima that changed
-        const int b1 = a >> 6, b2 = b >> 6, b3 = ls >= 0 ? (ls >> 6) : b1;
-        int blks[3] = {b1, b2 != b1 ? b2 : -1, (b3 != b1 && b3 != b2) ? b3 : -1};
+        // every lane writes the same values (no barrier needed, see above)
+        link[a] = eb;
+        link[eb] = a;
+        rn[a] = er;
+        cost[b] = QNAN;
+        cost[a] = cr;                     // QNAN when there is no right neighbour
+        if (ls >= 0) {
+            cost[ls] = cl;
+            rn[ls] = eb;
+        }
+        // ---- block minima of the touched blocks (a's, b's, ls's)
+        const int ba = a >> 6, bb = b >> 6, bl = ls >= 0 ? (ls >> 6) : ba;
+        const double ma = wave_min(cost[ba * 64 + lane]);
+        const double mb = bb != ba ? wave_min(cost[bb * 64 + lane]) : ma;
+        const double ml = (bl != ba && bl != bb) ? wave_min(cost[bl * 64 + lane]) : ma;
 #pragma unroll
-        for (int q = 0; q < 3; ++q) {
-            const int bk = blks[q];
-            if (bk < 0) continue;
-            int p = bk * 64 + lane;
-            double vv = INF;
-            int ii = p + n;
-            if (p < n) {
-                double cp = cost[p];
-                if (!isnan(cp)) { vv = cp; ii = p; }
-            }
-            wave_argmin(vv, ii);
-            if (lane == 0) { bmv[bk] = vv; bmi[bk] = ii; }
+        for (int q = 0; q < BSLOT; ++q) {
+            if (lane == (ba & 63) && q == (ba >> 6)) bmr[q] = ma;
+            if (bb != ba && lane == (bb & 63) && q == (bb >> 6)) bmr[q] = mb;
+            if (bl != ba && bl != bb && lane == (bl & 63) && q == (bl >> 6)) bmr[q] = ml;
         }
-        __syncthreads();
+        TP_STAMP(3);
     }
 
     // ---- broken stick (rioja bstick.chclust, vegan bstick.default) on heights
@@ -231,28 +333,76 @@ __global__ void __launch_bounds__(64) k_coniss(SweepDev sd) {
         }
         sd.n_cluster[ti] = ncl;
     }
+    TP_STAMP(5);
+    if (STAMPS && lane == 0)
+        for (int q = 0; q < 6; ++q) sd.stamps[(size_t)ti * 8 + q] = st_acc[q];
+#undef TP_STAMP
 }
+template __global__ void k_coniss_t<false>(SweepDev, const double *);
+template __global__ void k_coniss_t<true>(SweepDev, const double *);
+#define k_coniss k_coniss_t<false>
 
 // ------------------------------------------------------------ CH over cuts
 // canonical segment statistics of rows s..e, by one wave (see tpo_seg_ss)
 __device__ double seg_ss_wave(const double *Pt, int ldp, int k, int s, int e, double *sumout, int lane) {
     const double fn = (double)(e - s + 1);
-    double part = 0.0;
+    bool ok[KMAXSLOT];
+    int jj[KMAXSLOT];
 #pragma unroll
     for (int t = 0; t < KMAXSLOT; ++t) {
-        int j = lane + 64 * t;
-        if (j >= k) break;
-        double sj = 0.0;
-        for (int a = s; a <= e; ++a) sj = sj + Pt[(size_t)a * ldp + j];
-        if (sumout) sumout[j] = sj;
-        double mj = sj / fn;
-        double ss = 0.0;
-        for (int a = s; a <= e; ++a) {
-            double d = Pt[(size_t)a * ldp + j] - mj;
-            ss = fma(d, d, ss);
-        }
-        part = part + ss;
+        jj[t] = lane + 64 * t;
+        ok[t] = jj[t] < k;
+        if (!ok[t]) jj[t] = 0;   // safe address, value unused
     }
+    // pass 1: column sums, sequential over rows per column; 4 rows per step
+    // so 16 independent loads are in flight
+    double sj[KMAXSLOT] = {0.0, 0.0, 0.0, 0.0};
+    int a = s;
+    for (; a + 3 <= e; a += 4) {
+        double x[4][KMAXSLOT];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int t = 0; t < KMAXSLOT; ++t) x[r][t] = Pt[(size_t)(a + r) * ldp + jj[t]];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int t = 0; t < KMAXSLOT; ++t) sj[t] = sj[t] + x[r][t];
+    }
+    for (; a <= e; ++a)
+#pragma unroll
+        for (int t = 0; t < KMAXSLOT; ++t) sj[t] = sj[t] + Pt[(size_t)a * ldp + jj[t]];
+    double mj[KMAXSLOT], ss[KMAXSLOT] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int t = 0; t < KMAXSLOT; ++t) {
+        mj[t] = sj[t] / fn;
+        if (sumout && ok[t]) sumout[jj[t]] = sj[t];
+    }
+    a = s;
+    for (; a + 3 <= e; a += 4) {
+        double x[4][KMAXSLOT];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int t = 0; t < KMAXSLOT; ++t) x[r][t] = Pt[(size_t)(a + r) * ldp + jj[t]];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int t = 0; t < KMAXSLOT; ++t) {
+                double d = x[r][t] - mj[t];
+                ss[t] = fma(d, d, ss[t]);
+            }
+    }
+    for (; a <= e; ++a)
+#pragma unroll
+        for (int t = 0; t < KMAXSLOT; ++t) {
+            double d = Pt[(size_t)a * ldp + jj[t]] - mj[t];
+            ss[t] = fma(d, d, ss[t]);
+        }
+    double part = 0.0;
+#pragma unroll
+    for (int t = 0; t < KMAXSLOT; ++t)
+        if (ok[t]) part = part + ss[t];
     return wave_sum(part);
 }
 
@@ -311,7 +461,7 @@ __global__ void __launch_bounds__(256) k_ch(SweepDev sd) {
         int gb = -1;
         for (int g = lane; g < nc; g += 64)
             if (alive[g] && segs[g] == b) gb = g;
-        for (int o = 1; o < 64; o <<= 1) gb = max(gb, __shfl_xor(gb, o, 64));
+        for (int o = 1; o < 64; o <<= 1) gb = max(gb, __shfl_xor(gb, o, 64));   // once per level
         int ga = gb - 1;
         while (ga >= 0 && !alive[ga]) --ga;
         int nx = gb + 1;
@@ -325,12 +475,14 @@ __global__ void __launch_bounds__(256) k_ch(SweepDev sd) {
         for (int t = 0; t < KMAXSLOT; ++t) {
             int j = lane + 64 * t;
             if (j < k) {
-                double d = SA[j] / fa - SB[j] / fb;
-                acc = fma(d, d, acc);
+                double t1 = SA[j] * fb;
+                double t2 = SB[j] * fa;
+                double e = t1 - t2;
+                acc = fma(e, e, acc);
             }
         }
         double tot = wave_sum(acc);
-        trW = trW + ((fa * fb) / (fa + fb)) * tot;
+        trW = trW + tot / (fa * fb * (fa + fb));
 #pragma unroll
         for (int t = 0; t < KMAXSLOT; ++t) {
             int j = lane + 64 * t;
@@ -352,16 +504,36 @@ __global__ void k_fill(double *p, size_t cnt, double v) {
 }
 
 static size_t coniss_lds_bytes(int n) {
-    int nbk = (n + 63) / 64;
-    return (size_t)n * 8 + (size_t)nbk * 12 + 8 + (size_t)n * 4 + 16;
+    size_t nbk = (n + 63) / 64;
+    return nbk * 64 * 8 + (size_t)n * 8 + 16;
+}
+
+// seed kernel + CONISS (cost0 = initial adjacent costs, ntrees x nbk*64)
+static void run_coniss(const SweepDev &sd, hipStream_t s, bool stamped, Ctx *prof) {
+    const int nbk = (sd.n + 63) / 64;
+    double *cost0 = sd.cost0;
+    hipLaunchKernelGGL(k_seed, dim3(sd.ntrees, nbk), dim3(64), 0, s, sd, cost0);
+    TP_HIP(hipGetLastError());
+    size_t lds = coniss_lds_bytes(sd.n);
+    if (stamped) {
+        TP_HIP(hipFuncSetAttribute((const void *)k_coniss_t<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)lds));
+        hipLaunchKernelGGL(k_coniss_t<true>, dim3(sd.ntrees), dim3(64), lds, s, sd, (const double *)cost0);
+    } else {
+        TP_HIP(hipFuncSetAttribute((const void *)k_coniss, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        if (prof) kprof_begin(*prof, K_CONISS);
+        hipLaunchKernelGGL(k_coniss, dim3(sd.ntrees), dim3(64), lds, s, sd, (const double *)cost0);
+        if (prof) kprof_end(*prof, K_CONISS);
+    }
+    TP_HIP(hipGetLastError());
 }
 
 void launch_sweep(const SweepDev &sd, hipStream_t s, Ctx *prof) {
     if (sd.k > 64 * KMAXSLOT) fail(TP_ERR_UNSUPPORTED, "max_pcs > 256 is not supported by this build");
     if (sd.n < 3) fail(TP_ERR_NO_BSTICK, "fewer than 3 good bins: no broken-stick level");
     size_t lds = coniss_lds_bytes(sd.n);
-    if (lds > 160 * 1024) fail(TP_ERR_UNSUPPORTED, "matrix too large for the LDS-resident CONISS (n > ~13000)");
-    TP_HIP(hipFuncSetAttribute((const void *)k_coniss, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    if (lds > 160 * 1024 || sd.n > 64 * 64 * BSLOT)
+        fail(TP_ERR_UNSUPPORTED, "matrix too large for the LDS-resident CONISS (n > 13600)");
     if (sd.ntrees < 1 || sd.tree0 < 0 || sd.tree0 + sd.ntrees > sd.k) fail(TP_ERR_ARG, "bad tree range");
     size_t cnt = (size_t)sd.ntrees * sd.w_cap;
     double na;
@@ -373,23 +545,21 @@ void launch_sweep(const SweepDev &sd, hipStream_t s, Ctx *prof) {
     TP_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_trS, dim3(1), dim3(64), 0, s, sd.Pt, sd.n, sd.ldp, sd.k, sd.trS);
     TP_HIP(hipGetLastError());
-    if (prof) kprof_begin(*prof, K_CONISS);
-    hipLaunchKernelGGL(k_coniss, dim3(sd.ntrees), dim3(64), lds, s, sd);
-    TP_HIP(hipGetLastError());
-    if (prof) kprof_end(*prof, K_CONISS);
+    run_coniss(sd, s, false, prof);
     if (prof) kprof_begin(*prof, K_CH);
     hipLaunchKernelGGL(k_ch, dim3(sd.ntrees), dim3(256), 0, s, sd);
     TP_HIP(hipGetLastError());
     if (prof) kprof_end(*prof, K_CH);
 }
 
+void launch_coniss_stamped(const SweepDev &sd, hipStream_t s) { run_coniss(sd, s, true, nullptr); }
+
 void launch_coniss_only(const SweepDev &sd, hipStream_t s) {
     if (sd.tree0 + sd.ntrees > 64 * KMAXSLOT) fail(TP_ERR_UNSUPPORTED, "more than 256 columns");
     size_t lds = coniss_lds_bytes(sd.n);
-    if (lds > 160 * 1024) fail(TP_ERR_UNSUPPORTED, "matrix too large for the LDS-resident CONISS (n > ~13000)");
-    TP_HIP(hipFuncSetAttribute((const void *)k_coniss, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(k_coniss, dim3(sd.ntrees), dim3(64), lds, s, sd);
-    TP_HIP(hipGetLastError());
+    if (lds > 160 * 1024 || sd.n > 64 * 64 * BSLOT)
+        fail(TP_ERR_UNSUPPORTED, "matrix too large for the LDS-resident CONISS (n > 13600)");
+    run_coniss(sd, s, false, nullptr);
 }
 
 // ------------------------------------------- single calinhara (tp_ch entry)

@@ -1,0 +1,65 @@
+"""GPU diagnostics: k_chol_inv accuracy + time, and per-phase cycle stamps of
+the CONISS merge loop (tp_debug_* entries of libtadpole_hip.so)."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+from tadpole_amd import _lib  # noqa: E402
+
+L = _lib.load()
+B = ctypes.byref
+D = ctypes.POINTER(ctypes.c_double)
+
+
+def chol(b=256, cond=1e6):
+    rng = np.random.default_rng(0)
+    q, _ = np.linalg.qr(rng.standard_normal((b, b)))
+    ev = np.logspace(0, -np.log10(cond), b)
+    W = np.asfortranarray((q * ev) @ q.T)
+    U = np.zeros((b, b), order="F"); X = np.zeros((b, b), order="F")
+    ms = np.zeros(8); st = ctypes.c_int(0)
+    L.tp_debug_chol(W.ctypes.data_as(D), B(ctypes.c_int(b)), B(ctypes.c_double(0.0)), B(ctypes.c_int(5)),
+                    U.ctypes.data_as(D), X.ctypes.data_as(D), ms.ctypes.data_as(D), B(st))
+    _lib.check(st)
+    Uu = np.triu(U)
+    e1 = np.abs(Uu.T @ Uu - W).max() / np.abs(W).max()
+    e2 = np.abs(X @ Uu - np.eye(b)).max()
+    print(f"chol b={b} cond={cond:.0e}: chol {ms[0]:.3f} ms, trsm(I) {ms[1]:.3f} ms  "
+          f"|U'U-W|/|W|={e1:.2e}  |XU-I|={e2:.2e}\n    cycles: diag {ms[2]:.0f} panel {ms[3]:.0f} "
+          f"trailing {ms[4]:.0f} prologue {ms[5]:.0f}", flush=True)
+
+
+def coniss(n0=2000, k=200):
+    import tadpole_oracle as O
+    from tadpole_amd.synth import synth_hic
+    m = synth_hic(n0, 20261017)
+    cm = O.clean_symmetrize(m)
+    bad, _, _ = O.bad_mask(cm, 0.01)
+    g = np.flatnonzero(~bad)
+    p = np.asfortranarray(O.prcomp_x(O.sparse_cor(cm[np.ix_(g, g)]), k))
+    n = p.shape[0]
+    stamps = np.zeros(k * 8, np.int64)
+    ms = ctypes.c_double(0); st = ctypes.c_int(0)
+    L.tp_debug_coniss_stamps(p.ctypes.data_as(D), B(ctypes.c_int(n)), B(ctypes.c_int(k)),
+                             stamps.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)), B(ms), B(st))
+    _lib.check(st)
+    s = stamps.reshape(k, 8)[:, :6].astype(float)
+    names = ["argmin", "links+loads", "costs", "update+refresh", "init", "bstick"]
+    print(f"coniss n={n} k={k}: kernel {ms.value:.3f} ms", flush=True)
+    for i in (0, 63, 127, k - 1):
+        tot = s[i].sum()
+        print(f"  tree {i+1:3d}: total {tot/1e6:.2f} Mcyc; per merge " +
+              ", ".join(f"{nm} {s[i, j]/(n-1):.0f}" for j, nm in enumerate(names[:4])) +
+              f"; init {s[i,4]/1e3:.0f} kcyc, bstick {s[i,5]/1e3:.0f} kcyc", flush=True)
+
+
+if __name__ == "__main__":
+    chol(256, 1e3)
+    chol(256, 1e10)
+    chol(480, 1e6)
+    coniss()
