@@ -11,6 +11,9 @@
 #include <string>
 #include <vector>
 
+#include <rocblas/rocblas.h>
+#include <rocsolver/rocsolver.h>
+
 #include "../../include/tadpole_hip.h"
 #include "tp_internal.h"
 
@@ -773,6 +776,53 @@ void tp_debug_coniss_stamps(const double *P, const int *n, const int *k, long lo
         TP_HIP(hipMemcpy(stamps, dst, (size_t)K * 8 * 8, hipMemcpyDeviceToHost));
         (void)hipEventDestroy(e0);
         (void)hipEventDestroy(e1);
+    });
+}
+
+
+/* rocSOLVER symmetric eigensolvers on a b x b matrix: ms[0] syevd, ms[1]
+ * syevj, ms[2] syevdj; ev_out (b x 3) eigenvalues of each. */
+void tp_debug_eig(const double *H, const int *b, double *ms, double *ev_out, int *status) {
+    guarded(status, [&] {
+        Ctx &c = ctx_for(0);
+        hipStream_t s = c.cur;
+        const int B = *b;
+        rocblas_handle h;
+        if (rocblas_create_handle(&h) != rocblas_status_success) fail(TP_ERR_HIP, "handle");
+        (void)rocblas_set_stream(h, s);
+        double *dA = c.buf[S_SMALL].as<double>((size_t)B * B + 4 * B + 64);
+        double *dW = dA + (size_t)B * B, *dE = dW + B, *dRes = dE + B;
+        int *info = c.buf[S_MISC].as<int>(64);
+        int *nsw = info + 8;
+        hipEvent_t e0, e1;
+        TP_HIP(hipEventCreate(&e0));
+        TP_HIP(hipEventCreate(&e1));
+        for (int which = 0; which < 3; ++which) {
+            float best = 1e30f;
+            for (int rep = 0; rep < 3; ++rep) {
+                TP_HIP(hipMemcpyAsync(dA, H, (size_t)B * B * 8, hipMemcpyHostToDevice, s));
+                TP_HIP(hipEventRecord(e0, s));
+                rocblas_status st = rocblas_status_success;
+                if (which == 0)
+                    st = rocsolver_dsyevd(h, rocblas_evect_original, rocblas_fill_upper, B, dA, B, dW, dE, info);
+                else if (which == 1)
+                    st = rocsolver_dsyevj(h, rocblas_esort_ascending, rocblas_evect_original, rocblas_fill_upper, B,
+                                          dA, B, 1e-14, dRes, 20, nsw, dW, info);
+                else if (which == 2)
+                    st = rocsolver_dsyevdj(h, rocblas_evect_original, rocblas_fill_upper, B, dA, B, dW, info);
+                TP_HIP(hipEventRecord(e1, s));
+                TP_HIP(hipEventSynchronize(e1));
+                if (st != rocblas_status_success) { best = -1; break; }
+                float t = 0;
+                TP_HIP(hipEventElapsedTime(&t, e0, e1));
+                best = std::min(best, t);
+            }
+            ms[which] = best;
+            TP_HIP(hipMemcpy(ev_out + (size_t)which * B, dW, B * 8, hipMemcpyDeviceToHost));
+        }
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        (void)rocblas_destroy_handle(h);
     });
 }
 

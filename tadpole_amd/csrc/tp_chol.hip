@@ -30,8 +30,10 @@ __global__ void __launch_bounds__(NT) k_chol_t(double *W, double *rdiag, int b, 
         st_acc[ph] += _t - st_t0;                                         \
         st_t0 = _t;                                                       \
     }
-    __shared__ double D[NB][NB + 1];       // diagonal block
-    __shared__ double P[NB][BMAX + 1];     // panel U[o:o+32, o+32:b]
+    __shared__ double D[NB][NB + 1];       // factored diagonal block U_pp
+    __shared__ double rd[NB];              // 1 / diag(U_pp)
+    __shared__ double prow[NB];            // pivot row broadcast (wave 0)
+    __shared__ double P[NB][BMAX + 8];     // panel U[o:o+32, o+32:b]
     __shared__ double red[32];
     const int t = threadIdx.x;
     const int T = b / NB;
@@ -51,56 +53,59 @@ __global__ void __launch_bounds__(NT) k_chol_t(double *W, double *rdiag, int b, 
     const double shift = rel * red[0];
     for (int j = t; j < b; j += NT) W[(size_t)j * b + j] += shift;
     __syncthreads();
-
     TP_STAMP(3);
+
     for (int p = 0; p < T; ++p) {
         const int o = p * NB;
-        // (a) diagonal block -> LDS, unblocked upper Cholesky by wave 0
-        for (int e = t; e < NB * NB; e += NT) {
-            const int r = e & 31, c = e >> 5;
-            D[r][c] = (r <= c) ? W[(size_t)(o + c) * b + o + r] : 0.0;
-        }
-        __syncthreads();
+        // (a) 32 x 32 diagonal block by wave 0: lane l owns row r = l & 31 at
+        //     columns c = (l >> 5) + 2m, m < 16, in registers; the pivot row is
+        //     broadcast through LDS (one wave barrier per step)
         if (t < 64) {
+            const int r = t & 31, cp = t >> 5;
+            double d[16];
+#pragma unroll
+            for (int m = 0; m < 16; ++m) {
+                const int c = cp + 2 * m;
+                d[m] = (c >= r) ? W[(size_t)(o + c) * b + o + r] : 0.0;
+            }
+            // Entries left of the diagonal (c < r) carry garbage after the
+            // first steps; they are never read for c < j and never stored.
             for (int j = 0; j < NB; ++j) {
-                double d = D[j][j];
-                if (!(d > 0.0)) {
+                if (r == j) {
+#pragma unroll
+                    for (int m = 0; m < 16; ++m) prow[cp + 2 * m] = d[m];
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                double dj = prow[j];
+                if (!(dj > 0.0)) {
                     if (t == 0) atomicOr(info, 1);
-                    d = 1e-300;
+                    dj = 1e-300;
                 }
-                const double piv = sqrt(d);
-                // scale row j (one division per lane), then the trailing update
-                if (t >= j && t < NB) D[j][t] = (t == j) ? piv : D[j][t] / piv;
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                // 1/sqrt(dj): hardware estimate + one Newton step (<= 1-2 ulp:
+                // fine for an orthonormalisation the next pass cleans up)
+                double rp = __builtin_amdgcn_rsq(dj);
+                rp = rp * fma(-0.5 * dj * rp, rp, 1.5);
+                const double f = (r > j) ? prow[r] * (rp * rp) : 0.0;   // U(j,r) / piv, 0: no-op
+                const double sc = (r == j) ? rp : 1.0;           // row j: D[j][c] / piv
+#pragma unroll
+                for (int m = 0; m < 16; ++m) d[m] = fma(-f, prow[cp + 2 * m], d[m]) * sc;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                 __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                {
-                    const int r = t & 31;            // fixed per lane
-                    const double djr = D[j][r];
-                    double dv[16], djc[16];
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            }
 #pragma unroll
-                    for (int m = 0; m < 16; ++m) {   // c = (t >> 5) + 2m
-                        const int c = (t >> 5) + 2 * m;
-                        dv[m] = D[r][c];
-                        djc[m] = D[j][c];
-                    }
-#pragma unroll
-                    for (int m = 0; m < 16; ++m) {
-                        const int c = (t >> 5) + 2 * m;
-                        if (r > j && c >= r) D[r][c] = dv[m] - djr * djc[m];
-                    }
+            for (int m = 0; m < 16; ++m) {
+                const int c = cp + 2 * m;
+                D[r][c] = (c >= r) ? d[m] : 0.0;
+                if (c >= r) W[(size_t)(o + c) * b + o + r] = d[m];
+                if (c == r) {
+                    rd[r] = 1.0 / d[m];
+                    rdiag[o + r] = 1.0 / d[m];
                 }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
         }
-        __syncthreads();
-        for (int e = t; e < NB * NB; e += NT) {
-            const int r = e & 31, c = e >> 5;
-            if (r <= c) W[(size_t)(o + c) * b + o + r] = D[r][c];
-        }
-        if (t < NB) rdiag[o + t] = 1.0 / D[t][t];
         __syncthreads();
         TP_STAMP(0);
         // (b) panel U_pj = U_pp^{-T} W_pj, one thread per column, in registers
@@ -112,7 +117,7 @@ __global__ void __launch_bounds__(NT) k_chol_t(double *W, double *rdiag, int b, 
             for (int r = 0; r < NB; ++r) v[r] = W[(size_t)col * b + o + r];
 #pragma unroll
             for (int q = 0; q < NB; ++q) {
-                v[q] = v[q] / D[q][q];
+                v[q] = v[q] * rd[q];
 #pragma unroll
                 for (int r = q + 1; r < NB; ++r) v[r] = v[r] - D[q][r] * v[q];
                 __builtin_amdgcn_sched_barrier(0);
@@ -125,46 +130,54 @@ __global__ void __launch_bounds__(NT) k_chol_t(double *W, double *rdiag, int b, 
         }
         __syncthreads();
         TP_STAMP(1);
-        // (c) trailing update W[i, l] -= sum_r P[r][i] P[r][l], i, l < ncol,
-        //     64x64 macro tiles on and above the diagonal, 4x4 per thread
-        const int mt = ncol / 64 + ((ncol & 63) ? 1 : 0);
-        const int ngrp = NT / 256, grp = t >> 8, lt = t & 255, tx = lt & 15, ty = lt >> 4;
-        int tile = 0;
-        for (int ti = 0; ti < mt; ++ti)
-            for (int tl = ti; tl < mt; ++tl, ++tile) {
-                if ((tile % ngrp) != grp) continue;
-                const int i0 = ti * 64, l0 = tl * 64;
-                double acc[4][4];
+        // (c) trailing update W[i, l] -= sum_r P[r][i] P[r][l] over the upper
+        //     triangle, one 8x8 register tile per thread
+        const int mt = (ncol + 7) / 8;
+        const int ntile = mt * (mt + 1) / 2;
+        for (int tile = t; tile < ntile; tile += NT) {
+            int ti = 0, rem = tile;
+            while (rem >= mt - ti) { rem -= mt - ti; ++ti; }
+            const int tl = ti + rem;
+            const int i0 = ti * 8, l0 = tl * 8;
+            double acc[8][8];
 #pragma unroll
-                for (int u = 0; u < 4; ++u)
+            for (int u = 0; u < 8; ++u)
 #pragma unroll
-                    for (int v = 0; v < 4; ++v) acc[u][v] = 0.0;
-                for (int r = 0; r < NB; ++r) {
-                    double ai[4], al[4];
+                for (int v = 0; v < 8; ++v) acc[u][v] = 0.0;
+            for (int r = 0; r < NB; ++r) {
+                double ai[8], al[8];
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        int ii = i0 + tx + 16 * u, ll = l0 + ty + 16 * u;
-                        ai[u] = ii < ncol ? P[r][ii] : 0.0;
-                        al[u] = ll < ncol ? P[r][ll] : 0.0;
-                    }
-#pragma unroll
-                    for (int u = 0; u < 4; ++u)
-#pragma unroll
-                        for (int v = 0; v < 4; ++v) acc[u][v] = fma(ai[u], al[v], acc[u][v]);
+                for (int u = 0; u < 8; ++u) {
+                    ai[u] = P[r][i0 + u];   // P padded: columns >= ncol read stale / zero, unused
+                    al[u] = P[r][l0 + u];
                 }
 #pragma unroll
-                for (int v = 0; v < 4; ++v) {
-                    const int ll = l0 + ty + 16 * v;
-                    if (ll >= ncol) continue;
+                for (int u = 0; u < 8; ++u)
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const int ii = i0 + tx + 16 * u;
-                        if (ii >= ncol) continue;
-                        size_t idx = (size_t)(o + NB + ll) * b + o + NB + ii;
-                        W[idx] = W[idx] - acc[u][v];
-                    }
-                }
+                    for (int v = 0; v < 8; ++v) acc[u][v] = fma(ai[u], al[v], acc[u][v]);
             }
+            // RMW in two halves of 32 (clamped-address loads batched, then
+            // predicated stores) to stay within the register budget
+#pragma unroll
+            for (int hv = 0; hv < 8; hv += 4) {
+                double w[8][4];
+#pragma unroll
+                for (int v = 0; v < 4; ++v)
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const int ll = min(l0 + hv + v, ncol - 1), ii = min(i0 + u, ncol - 1);
+                        w[u][v] = W[(size_t)(o + NB + ll) * b + o + NB + ii];
+                    }
+#pragma unroll
+                for (int v = 0; v < 4; ++v)
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const int ll = l0 + hv + v, ii = i0 + u;
+                        if (ll < ncol && ii <= ll)
+                            W[(size_t)(o + NB + ll) * b + o + NB + ii] = w[u][v] - acc[u][hv + v];
+                    }
+            }
+        }
         __syncthreads();
         TP_STAMP(2);
     }

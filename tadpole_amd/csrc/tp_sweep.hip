@@ -406,9 +406,53 @@ __device__ double seg_ss_wave(const double *Pt, int ldp, int k, int s, int e, do
     return wave_sum(part);
 }
 
-__global__ void __launch_bounds__(64) k_trS(const double *Pt, int n, int ldp, int k, double *out) {
-    double v = seg_ss_wave(Pt, ldp, k, 0, n - 1, nullptr, threadIdx.x);
-    if (threadIdx.x == 0) *out = v;
+// tr(S) over all rows: wave w owns column slot t = w (columns 64w + lane);
+// per column the canonical sequential sums, combined in slot order through LDS
+// exactly as seg_ss_wave's `part` (same bits).
+__global__ void __launch_bounds__(256) k_trS(const double *Pt, int n, int ldp, int k, double *out) {
+    __shared__ double ssl[KMAXSLOT][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int j = lane + 64 * w;
+    const bool ok = j < k;
+    const int jj = ok ? j : 0;
+    const double fn = (double)n;
+    double sj = 0.0;
+    int a = 0;
+    for (; a + 7 < n; a += 8) {
+        double x[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) x[r] = Pt[(size_t)(a + r) * ldp + jj];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) sj = sj + x[r];
+    }
+    for (; a < n; ++a) sj = sj + Pt[(size_t)a * ldp + jj];
+    const double mj = sj / fn;
+    double ss = 0.0;
+    a = 0;
+    for (; a + 7 < n; a += 8) {
+        double x[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) x[r] = Pt[(size_t)(a + r) * ldp + jj];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            double d = x[r] - mj;
+            ss = fma(d, d, ss);
+        }
+    }
+    for (; a < n; ++a) {
+        double d = Pt[(size_t)a * ldp + jj] - mj;
+        ss = fma(d, d, ss);
+    }
+    ssl[w][lane] = ss;
+    __syncthreads();
+    if (w == 0) {
+        double part = 0.0;
+#pragma unroll
+        for (int t = 0; t < KMAXSLOT; ++t)
+            if (lane + 64 * t < k) part = part + ssl[t][lane];
+        double v = wave_sum(part);
+        if (lane == 0) *out = v;
+    }
 }
 
 __global__ void __launch_bounds__(256) k_ch(SweepDev sd) {
@@ -543,7 +587,7 @@ void launch_sweep(const SweepDev &sd, hipStream_t s, Ctx *prof) {
     }
     hipLaunchKernelGGL(k_fill, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, sd.scores, cnt, na);
     TP_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_trS, dim3(1), dim3(64), 0, s, sd.Pt, sd.n, sd.ldp, sd.k, sd.trS);
+    hipLaunchKernelGGL(k_trS, dim3(1), dim3(256), 0, s, sd.Pt, sd.n, sd.ldp, sd.k, sd.trS);
     TP_HIP(hipGetLastError());
     run_coniss(sd, s, false, prof);
     if (prof) kprof_begin(*prof, K_CH);

@@ -58,7 +58,23 @@ def coniss(n0=2000, k=200):
               f"; init {s[i,4]/1e3:.0f} kcyc, bstick {s[i,5]/1e3:.0f} kcyc", flush=True)
 
 
+def eig(b=256):
+    rng = np.random.default_rng(1)
+    q, _ = np.linalg.qr(rng.standard_normal((b, b)))
+    ev = np.sort(rng.gamma(1.0, 1.0, b))[::-1] ** 4
+    H = (q * ev) @ q.T
+    H = np.asfortranarray((H + H.T) / 2)
+    ms = np.zeros(4); out = np.zeros(4 * b); st = ctypes.c_int(0)
+    L.tp_debug_eig(H.ctypes.data_as(D), B(ctypes.c_int(b)), ms.ctypes.data_as(D), out.ctypes.data_as(D), B(st))
+    _lib.check(st)
+    ref = np.sort(ev)
+    for w, name in enumerate(["syevd", "syevj", "syevdj"]):
+        got = np.sort(out[w * b:(w + 1) * b])
+        print(f"eig {name} b={b}: {ms[w]:.3f} ms  max|dev|/max={np.abs(got-ref).max()/ref.max():.2e}", flush=True)
+
+
 if __name__ == "__main__":
+    eig(256)
     chol(256, 1e3)
     chol(256, 1e10)
     chol(480, 1e6)
