@@ -32,6 +32,26 @@ FP64_MFMA_PEAK_TFLOPS = 78.6     # MI355X FP64 matrix, dense (AMD spec)
 HBM_PEAK_GBS = 8000.0            # MI355X HBM3E (MI355X_MICROARCH.md)
 
 
+def _pmc_traffic(kernel_class, n0, k):
+    """HBM bytes per launch of the dominant kernel from the newest committed
+    PMC summary (profiles/*_traffic.json, written by tools/prof_summary.py from
+    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench) for
+    the same workload.  GEMM classes share one kernel symbol: no per-class
+    figure, so null."""
+    import glob
+    names = {"coniss": "tp::k_coniss_t<false>", "ch": "tp::k_ch"}
+    if kernel_class not in names:
+        return None, None
+    for path in sorted(glob.glob(os.path.join(HERE, "profiles", "*_traffic.json")), reverse=True):
+        try:
+            t = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if t.get("n0") == n0 and t.get("k") == k and names[kernel_class] in t.get("kernels", {}):
+            return round(t["kernels"][names[kernel_class]]["hbm_bytes"]), os.path.relpath(path, HERE)
+    return None, None
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -147,8 +167,10 @@ def main():
         else:
             achieved = per_launch / (avg_ms * 1e-3) / 1e9
             peak, unit = HBM_PEAK_GBS, "GB/s"
+        traffic, tsrc = _pmc_traffic(dom, n0, k)
         roof = {"kernel": dom, "bound": bound, "achieved": round(achieved, 3), "peak": peak, "unit": unit,
-                "frac": round(achieved / peak, 5), "traffic": None, "avg_launch_ms": round(avg_ms, 4),
+                "frac": round(achieved / peak, 5), "traffic": traffic, "traffic_source": tsrc,
+                "algorithmic_per_launch": per_launch, "avg_launch_ms": round(avg_ms, 4),
                 "launches_per_step": launches,
                 "breakdown_ms": {q: round(kern[q][0], 4) for q in kern},
                 "stages_ms": {"mask": round(tm[0], 3), "cor": round(tm[1], 3), "pca": round(tm[2], 3),

@@ -289,17 +289,57 @@ def _coords(fixed):
     return np.stack([start[keep], eb[keep]], axis=1).astype(np.int64)
 
 
+def _level_coords(boundary, n, kk, pos):
+    """TAD coordinates of the cut into ``kk`` clusters (R/TADpole.R:470-488).
+
+    The cut's segments are runs of good bins in good order; a run of bad bins
+    (value 0 after ``c(good, bad)`` + ``order``) between two bins of the same
+    segment is filled by ``fix_values`` and one between two segments stays 0,
+    so every TAD spans from its first to its last good bin: (start, end) =
+    (pos[first], pos[last]) with ``pos`` the 1-based rank of each good bin in
+    the name-sorted union of good and bad bins."""
+    out = np.empty((kk, 2), np.int64)
+    out[0, 0] = pos[0]
+    out[kk - 1, 1] = pos[n - 1]
+    if kk > 1:
+        b = np.sort(boundary[n - kk:]) - 1
+        out[1:, 0] = pos[b]
+        out[:-1, 1] = pos[b - 1]
+    return out
+
+
 def _assemble(res, bad_idx1, arm_mode: bool = False) -> Tadpole:
     n = len(res["good"])
+    good1 = np.asarray(res["good"])
     dendro = Chclust(merge=res["merge"], height=res["height"], order=np.arange(1, n + 1),
-                     labels=[str(int(g)) for g in res["good"]], boundary=res["boundary"])
+                     labels=good1.astype(np.int64).astype(str).tolist(), boundary=res["boundary"])
     t = Tadpole(n_pcs=res["n_pcs"], optimal_n_clusters=res["n_clusters"], dendro=dendro,
                 scores=res["scores"], bad_columns=bad_idx1, timings_ms=res["timings"])
     row = res["scores"][res["n_pcs"] - 1]
-    good1 = res["good"]
-    for kk in np.flatnonzero(~np.isnan(row)) + 1:
+    levels = np.flatnonzero(~np.isnan(row)) + 1
+    if bad_idx1 is None or len(bad_idx1) == 0:
+        pos = np.arange(1, n + 1, dtype=np.int64)
+    else:
+        names = np.concatenate([good1, np.asarray(bad_idx1)]).astype(np.float64)
+        if not np.all(np.diff(good1.astype(np.float64)) > 0):
+            return _assemble_rle(t, dendro, levels, good1, bad_idx1)
+        order = np.argsort(names, kind="stable")
+        rank = np.empty(len(names), np.int64)
+        rank[order] = np.arange(1, len(names) + 1)
+        pos = rank[:n]
+    bnd = np.asarray(res["boundary"], np.int64)
+    for kk in levels:
+        t.clusters[str(int(kk))] = _level_coords(bnd, n, int(kk), pos)
+    return t
+
+
+def _assemble_rle(t, dendro, levels, good1, bad_idx1) -> Tadpole:
+    """Literal R/TADpole.R:470-488 (cutree, c(good, bad), order, rle,
+    fix_values, inverse.rle, runs): used when the good names are not
+    ascending, and by the tests as the reference for ``_level_coords``."""
+    for kk in levels:
         lab = dendro.cutree(int(kk))
-        if bad_idx1 is not None:
+        if bad_idx1 is not None and len(bad_idx1):
             fixed, _ = _fixed_clusters(lab, good1, bad_idx1)
             t.clusters[str(int(kk))] = _coords(fixed)
         else:

@@ -3,8 +3,11 @@
 //     W = U'U) for b <= 480, blocked by 32: diagonal block factored by one wave
 //     in LDS, panel solved in registers, trailing matrix updated in global
 //     memory (L2-resident) by 64x64 macro tiles with 4x4 register micro tiles.
-//     Also writes rdiag[j] = 1 / U_jj.  The shift s = rel * max(diag) keeps
-//     ill-conditioned blocks positive definite (shifted CholQR).
+//     Also writes rdiag[j] = 1 / U_jj.  W is Jacobi-scaled to unit diagonal
+//     first (so columns of very different norm -- a Chebyshev-filtered block --
+//     factor as well as the normalised block), and the shift s = rel on that
+//     unit diagonal keeps ill-conditioned blocks positive definite (shifted
+//     CholQR).
 //   k_trsm_ru: Q = Z U^{-1} (right, upper), one workgroup per 16 rows of Z,
 //     16-column blocks of U staged in LDS; spreads the O(n b^2) solve over
 //     n/16 workgroups.
@@ -34,24 +37,26 @@ __global__ void __launch_bounds__(NT) k_chol_t(double *W, double *rdiag, int b, 
     __shared__ double rd[NB];              // 1 / diag(U_pp)
     __shared__ double prow[NB];            // pivot row broadcast (wave 0)
     __shared__ double P[NB][BMAX + 8];     // panel U[o:o+32, o+32:b]
-    __shared__ double red[32];
+    __shared__ double scl[BMAX];           // diag(W)^-1/2
     const int t = threadIdx.x;
     const int T = b / NB;
-    // ---- shift: s = rel * max diag
-    double mx = 0.0;
-    for (int j = t; j < b; j += NT) mx = fmax(mx, W[(size_t)j * b + j]);
-    for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
-    if ((t & 63) == 0) red[t >> 6] = mx;
-    __syncthreads();
-    if (t == 0) {
-        double m = 0.0;
-        for (int q = 0; q < NT / 64; ++q) m = fmax(m, red[q]);
-        red[0] = m;
-        *info = 0;
+    // ---- Jacobi scaling (van der Sluis): factor W' = S W S, S = diag(W)^-1/2,
+    //      so the filtered block's column-norm spread does not reach the pivots;
+    //      shift s = rel on the unit diagonal.  U = U' S^-1 at the end.
+    for (int j = t; j < b; j += NT) {
+        const double dj = W[(size_t)j * b + j];
+        scl[j] = dj > 0.0 ? 1.0 / sqrt(dj) : 1.0;
     }
+    if (t == 0) *info = 0;
     __syncthreads();
-    const double shift = rel * red[0];
-    for (int j = t; j < b; j += NT) W[(size_t)j * b + j] += shift;
+    for (int col = t >> 6; col < b; col += NT / 64) {
+        const double sc = scl[col];
+        for (int r = t & 63; r <= col; r += 64) {
+            double v = W[(size_t)col * b + r] * (scl[r] * sc);
+            if (r == col) v += rel;
+            W[(size_t)col * b + r] = v;
+        }
+    }
     __syncthreads();
     TP_STAMP(3);
 
@@ -102,7 +107,6 @@ __global__ void __launch_bounds__(NT) k_chol_t(double *W, double *rdiag, int b, 
                 if (c >= r) W[(size_t)(o + c) * b + o + r] = d[m];
                 if (c == r) {
                     rd[r] = 1.0 / d[m];
-                    rdiag[o + r] = 1.0 / d[m];
                 }
             }
         }
@@ -181,6 +185,16 @@ __global__ void __launch_bounds__(NT) k_chol_t(double *W, double *rdiag, int b, 
         __syncthreads();
         TP_STAMP(2);
     }
+    // ---- undo the scaling: U = U' S^-1, rdiag = 1 / diag(U)
+    for (int col = t >> 6; col < b; col += NT / 64) {
+        const double isc = 1.0 / scl[col];
+        for (int r = t & 63; r <= col; r += 64) {
+            const double v = W[(size_t)col * b + r] * isc;
+            W[(size_t)col * b + r] = v;
+            if (r == col) rdiag[col] = 1.0 / v;
+        }
+    }
+    TP_STAMP(3);
     if (STAMPS && t == 0)
         for (int q = 0; q < 4; ++q) stamps[q] = st_acc[q];
 #undef TP_STAMP

@@ -139,7 +139,7 @@ void launch_transpose(const double *d_A, int rows, int cols, int lda, double *d_
                       hipStream_t s);
 
 // PCA (tp_pca.cpp): P (n x k col-major, ld n) and Pt (n x k row-major) from C.
-struct PcaStats { int iters = 0; double resid = 0; double rate = 0; int block = 0; };
+struct PcaStats { int iters = 0; double resid = 0; double rate = 0; int block = 0; int blocks = 0; };
 PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d_Pt,
                  double *h_sdev);
 

@@ -170,10 +170,11 @@ PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d
         double *resid = c.buf[S_MISC].as<double>(64 + k + b) + 64;
         int *d_info = c.buf[S_MISC].as<int>(64);
         const size_t nb = (size_t)n * b;
-        hipLaunchKernelGGL(k_rand_block, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, s, Z, n, b,
+        // random start block (well conditioned: the first iteration's CholQR
+        // orthonormalises G Q0 directly)
+        hipLaunchKernelGGL(k_rand_block, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, s, Q, n, b,
                            0x5EEDULL + (uint64_t)n);
         TP_HIP(hipGetLastError());
-        orth_cholqr(c, Z, Q, T, n, b, Wsm, Xinv, d_info, 3, 1e-13);
         double *Yb = c.buf[S_SWEEP2].as<double>((size_t)n * b);   // 4th block buffer (sweep scratch later)
         auto gemm_gq = [&](const double *Yin, double *Out) {
             GemmArgs g{n, b, n, G, n, true, Yin, n, Out, n};
@@ -223,7 +224,7 @@ PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d
         // Cholesky diagonal (|U_jj| -> lambda_j in orthogonal iteration)
         int done = 4;
         iterate(done);
-        double cut = 0.0, gk = 2.0;
+        double cut = 0.0, gk = 2.0, g1cap = 10.0;
         int mdeg = 1;
         {
             std::vector<double> dg(b);
@@ -236,6 +237,7 @@ PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d
                 const double x1 = 2.0 * l1 / cut - 1.0, xk = 2.0 * lk / cut - 1.0;
                 const double g1 = x1 + std::sqrt(x1 * x1 - 1.0);
                 gk = xk + std::sqrt(xk * xk - 1.0);
+                g1cap = g1;
                 // keep the filtered block CholQR-conditionable: (g1/gk)^m <= 1e6
                 mdeg = (int)std::floor(std::log(1e6) / std::log(std::max(g1 / gk, 1.0001)));
                 mdeg = std::max(1, std::min(8, mdeg));
@@ -246,7 +248,19 @@ PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d
             int need = (int)std::ceil(std::log(1.0 / target) / std::log(std::max(gk, 1.0005))) + 2;
             need = std::min(need, max_deg);
             if (cut > 0) {
-                for (int deg = 0; deg < need; deg += mdeg) cheb_block(mdeg, cut);
+                // Block degrees double: after total degree D the j-th column's
+                // components along the larger eigenvectors l < j have shrunk
+                // by (g_j/g_l)^D, so a block of degree D + mdeg amplifies them
+                // no more than the first block of degree mdeg did.  Capped so
+                // T_m(lambda_1) stays far from overflow in the Gram matrix.
+                const int mcap = std::max(1, std::min(24, (int)std::floor(100.0 / std::log10(std::max(g1cap, 10.0)))));
+                int deg = 0;
+                while (deg < need) {
+                    const int m = std::min({need - deg, std::max(mdeg, deg + mdeg), mcap});
+                    cheb_block(m, cut);
+                    deg += m;
+                    ++st.blocks;
+                }
                 done += need;
             } else {
                 iterate(need);
@@ -258,10 +272,10 @@ PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d
         rocblas_handle h = blas_for(c);
         for (int round = 0; round < 6; ++round) {
             // Rayleigh-Ritz: orthonormalise tightly, H = Q'GQ, eigen-decompose, rotate
-            GemmArgs g{n, b, n, G, n, true, Q, n, Z, n};
-            g.splitk = 0;
-            gemm_f64(g, c.buf[S_PARTIAL], s);
-            orth_cholqr(c, Z, Q, T, n, b, Wsm, Xinv, d_info, 2, 1e-14);
+            // Q is orthonormal to ~kappa^2 eps after the last one-pass CholQR:
+            // one more pass on Q itself restores eps-orthonormality
+            orth_cholqr(c, Q, Z, T, n, b, Wsm, Xinv, d_info, 1, 1e-14);
+            std::swap(Q, Z);
             GemmArgs g2{n, b, n, G, n, true, Q, n, Z, n};
             g2.splitk = 0;
             gemm_f64(g2, c.buf[S_PARTIAL], s);

@@ -69,8 +69,9 @@ size_t sweep_sums_doubles(int n, int tree0, int ntrees) { return sums_off(n, tre
 __device__ __forceinline__ double nan2inf(double x) { return isnan(x) ? __longlong_as_double(0x7FF0000000000000LL) : x; }
 
 // STAMPS: diagnostic build accumulating s_memtime cycles per merge phase into
-// sd.stamps[tree * 8 + phase] (0 argmin, 1 links + sum loads, 2 costs,
-// 3 LDS update + refresh, 4 init, 5 bstick).  The product launches STAMPS=false.
+// sd.stamps[tree * 8 + phase] (0 mask + refresh + speculative argmin,
+// 1 links + merged sums, 2 prefetch + costs, 3 choice of the next merge,
+// 4 init, 5 bstick).  The product launches STAMPS=false.
 //
 // Argmin without index keys: candidate costs are never NaN (NaN -> +inf) and a
 // non-candidate position holds NaN, which v_min ignores.  The smallest value is
@@ -217,13 +218,9 @@ __global__ void __launch_bounds__(64) k_coniss_t(SweepDev sd, const double *cost
     __syncthreads();
     TP_STAMP(4);
 
-    double h = 0.0;
-    for (int s = 0; s < n - 1; ++s) {
-        // ---- global argmin: smallest block minimum, leftmost block, leftmost lane
-        double gv = bmr[0];
-#pragma unroll
-        for (int q = 1; q < BSLOT; ++q) gv = fmin(gv, bmr[q]);
-        const double vmin = wave_min(gv);
+    // ---- the first merge: global argmin, then its four cluster rows
+    auto argmin_pos = [&](double vmin) -> int {   // leftmost position holding vmin (-1: none)
+        if (isnan(vmin)) return -1;
         int blk = 0;
 #pragma unroll
         for (int q = BSLOT - 1; q >= 0; --q) {
@@ -231,45 +228,106 @@ __global__ void __launch_bounds__(64) k_coniss_t(SweepDev sd, const double *cost
             if (m) blk = 64 * q + (int)__builtin_ctzll(m);
         }
         const unsigned long long mp = __ballot(cost[blk * 64 + lane] == vmin);
-        const int a = blk * 64 + (int)__builtin_ctzll(mp);
-        TP_STAMP(0);
+        return blk * 64 + (int)__builtin_ctzll(mp);
+    };
+    auto load_row = [&](double (&dst)[KMAXSLOT], int start) {
+        const double *pr = S + (size_t)start * i;
+#pragma unroll
+        for (int t = 0; t < KMAXSLOT; ++t) {
+            const int j = lane + 64 * t;
+            dst[t] = j < i ? pr[j] : 0.0;
+        }
+    };
+    double gv0 = bmr[0];
+#pragma unroll
+    for (int q = 1; q < BSLOT; ++q) gv0 = fmin(gv0, bmr[q]);
+    double c = wave_min(gv0);
+    int a = argmin_pos(c);
+    double sa[KMAXSLOT], sb[KMAXSLOT], sl[KMAXSLOT], sr[KMAXSLOT];
+    {
+        const int ea = link[a], eb = rn[a];
+        const int ls = a > 0 ? link[a - 1] : -1;
+        const int r = eb + 1 < n ? eb + 1 : -1;
+        load_row(sa, a);
+        load_row(sb, ea + 1);
+        load_row(sl, ls >= 0 ? ls : a);
+        load_row(sr, r >= 0 ? r : a);
+    }
+    TP_STAMP(4);
+
+    // Speculative prefetch.  After merge s (pair a|b -> m at a) the next merge is
+    // one of exactly three: the smallest cost among positions this merge does
+    // not touch (a2; found while merge s is in flight, with ls/a/b masked out),
+    // ls|m (new cost cl) or m|r (new cost cr).  The rows each of them needs are
+    // loaded during merge s, so no merge waits on HBM for its own operands:
+    //   a2:   rows a2, b2, ls2, r2 (any of them that is m comes from registers)
+    //   ls|m: sl, sm, row(ll), sr        m|r: sm, sr, sl, row(rr)
+    double h = 0.0;
+    for (int s = 0; s < n - 1; ++s) {
         const int ea = link[a];
         const int eb = rn[a];
         const int ls = a > 0 ? link[a - 1] : -1;
         const int b = ea + 1;
         const int r = eb + 1 < n ? eb + 1 : -1;
-        // ---- cluster sums (addresses need only a, ls, b, r)
-        double sa[KMAXSLOT], sb[KMAXSLOT], sl[KMAXSLOT], sr[KMAXSLOT];
-        const double *pa = S + (size_t)a * i, *pb = S + (size_t)b * i;
-        const double *pl = S + (size_t)(ls >= 0 ? ls : a) * i, *pr = S + (size_t)(r >= 0 ? r : a) * i;
-#pragma unroll
-        for (int t = 0; t < KMAXSLOT; ++t) {
-            const int j = lane + 64 * t;
-            const bool ok = j < i;
-            const int jj = ok ? j : 0;
-            sa[t] = ok ? pa[jj] : 0.0;
-            sb[t] = ok ? pb[jj] : 0.0;
-            sl[t] = ok ? pl[jj] : 0.0;
-            sr[t] = ok ? pr[jj] : 0.0;
-        }
         const int er = r >= 0 ? rn[b] : -1;
-        const double c = vmin;
         const int na = ea - a + 1, nbb = eb - b + 1, nm = na + nbb;
         const int nl = ls >= 0 ? a - ls : 0, nr = r >= 0 ? er - r + 1 : 0;
         double sm[KMAXSLOT];
-        if (STAMPS) {   // force the loads to land before the stamp
-            double z = 0.0;
-#pragma unroll
-            for (int t = 0; t < KMAXSLOT; ++t) z += sa[t] + sb[t] + sl[t] + sr[t];
-            if (z == 12345.678) sd.stamps[0] = 1;
-        }
-        TP_STAMP(1);
 #pragma unroll
         for (int t = 0; t < KMAXSLOT; ++t) {
             sm[t] = sa[t] + sb[t];
             const int j = lane + 64 * t;
             if (j < i) S[(size_t)a * i + j] = sm[t];
         }
+        if (lane == 0) {
+            mrg_a[s] = a;
+            mrg_b[s] = b;
+            mcost[s] = c;
+        }
+        TP_STAMP(1);
+        // ---- structure update; ls, a, b masked out of the cost array
+        link[a] = eb;
+        link[eb] = a;
+        rn[a] = er;
+        cost[b] = QNAN;
+        cost[a] = QNAN;
+        if (ls >= 0) {
+            cost[ls] = QNAN;
+            rn[ls] = eb;
+        }
+        const int ba = a >> 6, bb = b >> 6, bl = ls >= 0 ? (ls >> 6) : ba;
+        {
+            const double ma = wave_min(cost[ba * 64 + lane]);
+            const double mb = bb != ba ? wave_min(cost[bb * 64 + lane]) : ma;
+            const double ml = (bl != ba && bl != bb) ? wave_min(cost[bl * 64 + lane]) : ma;
+#pragma unroll
+            for (int q = 0; q < BSLOT; ++q) {
+                if (lane == (ba & 63) && q == (ba >> 6)) bmr[q] = ma;
+                if (bb != ba && lane == (bb & 63) && q == (bb >> 6)) bmr[q] = mb;
+                if (bl != ba && bl != bb && lane == (bl & 63) && q == (bl >> 6)) bmr[q] = ml;
+            }
+        }
+        double gv = bmr[0];
+#pragma unroll
+        for (int q = 1; q < BSLOT; ++q) gv = fmin(gv, bmr[q]);
+        const double v2 = wave_min(gv);
+        const int a2 = argmin_pos(v2);
+        TP_STAMP(0);
+        // ---- prefetch the candidates' rows (post-merge links)
+        const int a2s = a2 >= 0 ? a2 : a;
+        const int b2 = link[a2s] + 1;
+        const int ls2 = a2s > 0 ? link[a2s - 1] : -1;
+        const int e2 = rn[a2s];
+        const int r2 = (e2 >= 0 && e2 + 1 < n) ? e2 + 1 : -1;
+        const int ll = ls > 0 ? link[ls - 1] : -1;
+        const int rr = (r >= 0 && er + 1 < n) ? er + 1 : -1;
+        double pa[KMAXSLOT], pb[KMAXSLOT], pl[KMAXSLOT], pr[KMAXSLOT], pll[KMAXSLOT], prr[KMAXSLOT];
+        load_row(pa, a2s);
+        load_row(pb, b2 < n ? b2 : a);
+        load_row(pl, ls2 >= 0 ? ls2 : a);
+        load_row(pr, r2 >= 0 ? r2 : a);
+        load_row(pll, ll >= 0 ? ll : a);
+        load_row(prr, rr >= 0 ? rr : a);
         // ---- the two new adjacent costs (division-free Ward form), paired
         const double fm = (double)nm, fl = (double)nl, fr = (double)nr;
         double ul = ward_part(sl, fl, sm, fm, lane, i);
@@ -278,34 +336,46 @@ __global__ void __launch_bounds__(64) k_coniss_t(SweepDev sd, const double *cost
         const double cl = ls >= 0 ? nan2inf(ul / (fl * fm * (fl + fm))) : QNAN;
         const double cr = r >= 0 ? nan2inf(ur / (fm * fr * (fm + fr))) : QNAN;
         h = h + c;
+        if (lane == 0) height[s] = h;
         TP_STAMP(2);
-        if (lane == 0) {
-            mrg_a[s] = a;
-            mrg_b[s] = b;
-            mcost[s] = c;
-            height[s] = h;
-        }
-        // every lane writes the same values (no barrier needed, see above)
-        link[a] = eb;
-        link[eb] = a;
-        rn[a] = er;
-        cost[b] = QNAN;
         cost[a] = cr;                     // QNAN when there is no right neighbour
-        if (ls >= 0) {
-            cost[ls] = cl;
-            rn[ls] = eb;
-        }
-        // ---- block minima of the touched blocks (a's, b's, ls's)
-        const int ba = a >> 6, bb = b >> 6, bl = ls >= 0 ? (ls >> 6) : ba;
-        const double ma = wave_min(cost[ba * 64 + lane]);
-        const double mb = bb != ba ? wave_min(cost[bb * 64 + lane]) : ma;
-        const double ml = (bl != ba && bl != bb) ? wave_min(cost[bl * 64 + lane]) : ma;
+        if (ls >= 0) cost[ls] = cl;
 #pragma unroll
         for (int q = 0; q < BSLOT; ++q) {
-            if (lane == (ba & 63) && q == (ba >> 6)) bmr[q] = ma;
-            if (bb != ba && lane == (bb & 63) && q == (bb >> 6)) bmr[q] = mb;
-            if (bl != ba && bl != bb && lane == (bl & 63) && q == (bl >> 6)) bmr[q] = ml;
+            if (lane == (ba & 63) && q == (ba >> 6)) bmr[q] = fmin(bmr[q], cr);
+            if (ls >= 0 && lane == (bl & 63) && q == (bl >> 6)) bmr[q] = fmin(bmr[q], cl);
         }
+        // ---- next merge: lexicographic (cost, position) minimum of the three
+        double nv = v2;
+        int np = a2;
+        int which = 0;
+        if (ls >= 0 && (np < 0 || cl < nv || (cl == nv && ls < np))) { nv = cl; np = ls; which = 1; }
+        if (r >= 0 && (np < 0 || cr < nv || (cr == nv && a < np))) { nv = cr; np = a; which = 2; }
+        if (which == 0) {
+#pragma unroll
+            for (int t = 0; t < KMAXSLOT; ++t) {
+                sa[t] = pa[t];
+                sb[t] = pb[t];
+                sl[t] = ls2 == a ? sm[t] : pl[t];
+                sr[t] = r2 == a ? sm[t] : pr[t];
+            }
+        } else if (which == 1) {   // ls | m
+#pragma unroll
+            for (int t = 0; t < KMAXSLOT; ++t) {
+                sa[t] = sl[t];
+                sb[t] = sm[t];
+                sl[t] = pll[t];
+            }
+        } else {                   // m | r
+#pragma unroll
+            for (int t = 0; t < KMAXSLOT; ++t) {
+                sa[t] = sm[t];
+                sb[t] = sr[t];
+                sr[t] = prr[t];
+            }
+        }
+        a = np;
+        c = nv;
         TP_STAMP(3);
     }
 

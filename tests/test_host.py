@@ -46,6 +46,35 @@ def test_assembly_matches_oracle_on_golden(name):
     assert t.dendro.labels == [str(x) for x in good1]
 
 
+@pytest.mark.parametrize("seed", range(12))
+def test_vectorised_assembly_equals_literal_rle(seed):
+    # api._level_coords (one slice per level) against the literal cutree + c(good,
+    # bad) + order + rle + fix_values + runs of R/TADpole.R:470-488, with bad runs
+    # at both ends, adjacent bad runs and arm-style names (not 1..n0)
+    rng = np.random.default_rng(100 + seed)
+    n0 = int(rng.integers(5, 120))
+    bad = rng.random(n0) < rng.choice([0.0, 0.1, 0.4])
+    if seed % 3 == 0:
+        bad[:2] = True
+        bad[-3:] = True
+    if bad.sum() > n0 - 3:
+        bad[: n0 - 3] = False
+    names = np.arange(1, n0 + 1) + (0 if seed % 2 else 500)
+    good1, bad1 = names[~bad], names[bad]
+    n = len(good1)
+    mb = rng.permutation(np.arange(1, n))
+    scores = np.full((3, n - 1), np.nan)
+    scores[1, rng.choice(n - 1, size=min(n - 1, 7), replace=False)] = 1.0
+    res = dict(good=good1, merge=np.zeros((n - 1, 2), np.int32), height=np.arange(n - 1, dtype=float),
+               boundary=mb + 1, n_pcs=2, n_clusters=2, scores=scores, timings=np.zeros(16))
+    for b in (bad1, None):
+        fast = api._assemble(res, b)
+        slow = api._assemble_rle(api.Tadpole(), fast.dendro, np.flatnonzero(~np.isnan(scores[1])) + 1, good1, b)
+        assert set(fast.clusters) == set(slow.clusters)
+        for q in fast.clusters:
+            assert np.array_equal(fast.clusters[q], slow.clusters[q]), (q, b is None)
+
+
 def test_assembly_without_bad_columns_branch():
     # R/TADpole.R:490-494 (table(good_clusters)) equals the bad-column branch
     n = 30

@@ -1,0 +1,80 @@
+"""Summarise a gpu_prof.sh run (rocprofv3 CSVs under gpurun_out/) into
+profiles/<tag>_kernel_stats.csv (copy), profiles/<tag>_summary.md and
+profiles/<tag>_traffic.json (per-launch HBM bytes from the two PMC passes).
+
+Traffic per the MI355X guide: FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950
+FETCH_SIZE reads half the bytes of a wide coalesced stream, so
+hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (raw values are kept too).
+
+usage: python tools/prof_summary.py <tag> [steps_per_run]
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "gpurun_out")
+
+# bench.py kernel class -> rocprof kernel-name prefix
+CLASSES = {"coniss": "void tp::k_coniss_t<false>", "ch": "tp::k_ch(", "gq_gemm": "void tp::k_gemm_f64<true>",
+           "xtx_gemm": "void tp::k_gemm_f64<true>", "xcxc_gemm": "void tp::k_gemm_f64<true>"}
+
+
+def short(name):
+    return name.split("(")[0].replace("void ", "")[:90]
+
+
+def main():
+    tag = sys.argv[1]
+    bench = json.load(open(os.path.join(OUT, "prof_bench.json")))
+    steps = bench["steps"] + bench["warmup"] + 1          # timed + warmup + instrumented step
+    stats = list(csv.DictReader(open(os.path.join(OUT, "prof", "run_kernel_stats.csv"))))
+    shutil.copy(os.path.join(OUT, "prof", "run_kernel_stats.csv"),
+                os.path.join(ROOT, "profiles", f"{tag}_kernel_stats.csv"))
+    tot = sum(float(r["TotalDurationNs"]) for r in stats)
+    lines = [f"# {tag}: rocprofv3 --kernel-trace --stats, `python bench.py --steps {bench['steps']} "
+             f"--warmup {bench['warmup']} --no-cpu-baseline` ({steps} pipelines, C2 2000x2000, max_pcs=200)",
+             "", f"bench line of the profiled run: value {bench['value']} bins/s, "
+                 f"{bench['ms_per_step']} ms/step (profiler attached)", "",
+             "| kernel | calls/pipeline | ms/pipeline | avg us | % |", "|---|---|---|---|---|"]
+    for r in stats:
+        lines.append(f"| `{short(r['Name'])}` | {int(r['Calls']) / steps:.1f} | "
+                     f"{float(r['TotalDurationNs']) / steps / 1e6:.3f} | {float(r['AverageNs']) / 1e3:.1f} | "
+                     f"{float(r['Percentage']):.2f} |")
+    lines += ["", f"GPU kernel time per pipeline: {tot / steps / 1e6:.3f} ms", ""]
+    # ---- PMC passes
+    pmc = collections.defaultdict(lambda: collections.defaultdict(list))
+    for tagc, cnt in (("pmc_fetch", "FETCH_SIZE"), ("pmc_write", "WRITE_SIZE")):
+        path = os.path.join(OUT, tagc, "run_counter_collection.csv")
+        if not os.path.exists(path):
+            continue
+        for r in csv.DictReader(open(path)):
+            pmc[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    traffic = {}
+    if pmc:
+        lines += ["## HBM traffic (separate `--pmc FETCH_SIZE` / `--pmc WRITE_SIZE` passes)", "",
+                  "hbm bytes/launch = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 (gfx950 FETCH_SIZE counts half of a "
+                  "wide coalesced read: MI355X_MICROARCH.md, HBM)", "",
+                  "| kernel | launches | FETCH_SIZE KiB | WRITE_SIZE KiB | hbm MB/launch |", "|---|---|---|---|---|"]
+        for name, cs in sorted(pmc.items()):
+            f = cs.get("FETCH_SIZE", [0.0])
+            w = cs.get("WRITE_SIZE", [0.0])
+            fa, wa = sum(f) / len(f), sum(w) / len(w)
+            hb = (2 * fa + wa) * 1024
+            traffic[short(name)] = {"launches": len(f), "fetch_kib": fa, "write_kib": wa, "hbm_bytes": hb}
+            lines.append(f"| `{short(name)}` | {len(f)} | {fa:.0f} | {wa:.0f} | {hb / 1e6:.2f} |")
+    with open(os.path.join(ROOT, "profiles", f"{tag}_summary.md"), "w") as fh:
+        fh.write("\n".join(lines) + "\n")
+    if traffic:
+        cfg = bench["config"]
+        with open(os.path.join(ROOT, "profiles", f"{tag}_traffic.json"), "w") as fh:
+            json.dump({"tag": tag, "n0": cfg["n0"], "k": cfg["k"], "kernels": traffic,
+                       "classes": CLASSES}, fh, indent=1)
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main()
