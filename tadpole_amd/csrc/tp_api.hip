@@ -797,7 +797,8 @@ void tp_debug_eig(const double *H, const int *b, double *ms, double *ev_out, int
         hipEvent_t e0, e1;
         TP_HIP(hipEventCreate(&e0));
         TP_HIP(hipEventCreate(&e1));
-        for (int which = 0; which < 3; ++which) {
+        double *dWork = c.buf[S_PARTIAL].as<double>((size_t)B * B + 4 * B + 64);
+        for (int which = 0; which < 5; ++which) {
             float best = 1e30f;
             for (int rep = 0; rep < 3; ++rep) {
                 TP_HIP(hipMemcpyAsync(dA, H, (size_t)B * B * 8, hipMemcpyHostToDevice, s));
@@ -810,6 +811,8 @@ void tp_debug_eig(const double *H, const int *b, double *ms, double *ev_out, int
                                           dA, B, 1e-14, dRes, 20, nsw, dW, info);
                 else if (which == 2)
                     st = rocsolver_dsyevdj(h, rocblas_evect_original, rocblas_fill_upper, B, dA, B, dW, info);
+                else
+                    tp::eig_sym(h, dA, B, dW, dWork, info, s, which - 3);
                 TP_HIP(hipEventRecord(e1, s));
                 TP_HIP(hipEventSynchronize(e1));
                 if (st != rocblas_status_success) { best = -1; break; }
@@ -819,6 +822,9 @@ void tp_debug_eig(const double *H, const int *b, double *ms, double *ev_out, int
             }
             ms[which] = best;
             TP_HIP(hipMemcpy(ev_out + (size_t)which * B, dW, B * 8, hipMemcpyDeviceToHost));
+            if (which == 4) {   // eigenvectors of the custom path: ev_out[5B ..) = V (B x B)
+                TP_HIP(hipMemcpy(ev_out + (size_t)5 * B, dA, (size_t)B * B * 8, hipMemcpyDeviceToHost));
+            }
         }
         (void)hipEventDestroy(e0);
         (void)hipEventDestroy(e1);
@@ -826,4 +832,32 @@ void tp_debug_eig(const double *H, const int *b, double *ms, double *ev_out, int
     });
 }
 
+}  // extern "C"
+
+extern "C" {
+// Test hook for the PCA's Rayleigh-Ritz eigensolver (tp_eig.hip, not part of the
+// reference-facing ABI): H (b x b, column-major, symmetric) -> theta ascending,
+// V eigenvectors (columns).  method 0: sytrd + rocSOLVER dstedc, 1: sytrd +
+// bisection + inverse iteration (the product path).
+void tp_debug_eigsym(const double *H, const int *b, const int *method, double *theta, double *V, int *status) {
+    guarded(status, [&] {
+        Ctx &c = ctx_for(0);
+        hipStream_t s = c.cur;
+        const int B = *b;
+        if (!tp::eig_sym_supported(B)) fail(TP_ERR_UNSUPPORTED, "b > 512");
+        rocblas_handle h;
+        if (rocblas_create_handle(&h) != rocblas_status_success) fail(TP_ERR_HIP, "handle");
+        (void)rocblas_set_stream(h, s);
+        double *dA = c.buf[S_SMALL].as<double>((size_t)B * B + B + 64);
+        double *dW = dA + (size_t)B * B;
+        double *dWork = c.buf[S_PARTIAL].as<double>((size_t)B * B + 4 * B + 64);
+        int *info = c.buf[S_MISC].as<int>(64);
+        TP_HIP(hipMemcpyAsync(dA, H, (size_t)B * B * 8, hipMemcpyHostToDevice, s));
+        tp::eig_sym(h, dA, B, dW, dWork, info, s, *method);
+        TP_HIP(hipMemcpyAsync(theta, dW, (size_t)B * 8, hipMemcpyDeviceToHost, s));
+        TP_HIP(hipMemcpyAsync(V, dA, (size_t)B * B * 8, hipMemcpyDeviceToHost, s));
+        TP_HIP(hipStreamSynchronize(s));
+        (void)rocblas_destroy_handle(h);
+    });
+}
 }  // extern "C"

@@ -11,17 +11,19 @@ namespace tp {
 __device__ __forceinline__ double r_na() { return __longlong_as_double(0x7FF00000000007A2LL); }
 __device__ __forceinline__ double r_nan() { return __longlong_as_double(0x7FF8000000000000LL); }
 
-// DPP lane moves on a double (two 32-bit halves).  CTRL: 0xB1 = quad_perm
-// [1,0,3,2] (xor 1), 0x4E = quad_perm [2,3,0,1] (xor 2), 0x141 = row_half_mirror,
-// 0x140 = row_mirror.
+// DPP lane moves on a double (two 32-bit halves, no "old" operand, so no
+// zero-fill moves).  CTRL: 0xB1 = quad_perm [1,0,3,2] (xor 1), 0x4E =
+// quad_perm [2,3,0,1] (xor 2), 0x141 = row_half_mirror, 0x140 = row_mirror,
+// 0x142 = row_bcast:15 (lane 15 of row r-1 -> row r), 0x143 = row_bcast:31
+// (lane 31 -> rows 2 and 3).  Lanes without a source read 0 (bound_ctrl).
 template <int CTRL> __device__ __forceinline__ double dpp_d(double v) {
     int lo = __double2loint(v), hi = __double2hiint(v);
-    lo = __builtin_amdgcn_update_dpp(0, lo, CTRL, 0xF, 0xF, false);
-    hi = __builtin_amdgcn_update_dpp(0, hi, CTRL, 0xF, 0xF, false);
+    lo = __builtin_amdgcn_mov_dpp(lo, CTRL, 0xF, 0xF, true);
+    hi = __builtin_amdgcn_mov_dpp(hi, CTRL, 0xF, 0xF, true);
     return __hiloint2double(hi, lo);
 }
 template <int CTRL> __device__ __forceinline__ int dpp_i(int v) {
-    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+    return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, true);
 }
 __device__ __forceinline__ double readlane_d(double v, int lane) {
     int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
@@ -29,20 +31,41 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
     return __hiloint2double(hi, lo);
 }
 
+// IEEE minNum of two doubles in one instruction: a quiet-NaN operand is
+// ignored (fmin() would add two canonicalising v_max per call).  The s_nop
+// covers the VALU-write -> DPP-read hazard the compiler cannot see through asm.
+__device__ __forceinline__ double vmin(double a, double b) {
+    double r;
+    asm volatile("v_min_f64 %0, %1, %2\n\ts_nop 1" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 // Canonical wave sum = xor butterfly (masks 1,2,4,8,16,32) of the oracle's
 // butterfly64().  Steps 1-2 are the xor-1/xor-2 quad permutes; after them every
 // lane of a quad holds the same bits, so row_half_mirror pairs l with a lane of
 // quad l^4 (same value as lane l^4) and, one step later, row_mirror pairs l
-// with a lane of the 8-group l^8.  The 16- and 32-lane steps are done on the
-// four row values read with readlane: (R0 + R1) + (R2 + R3), exactly the
-// butterfly's last two levels.  All lanes return the same bits.
+// with a lane of the 8-group l^8: every lane of row r then holds R_r.  The 16-
+// and 32-lane levels are the two row broadcasts: lane 63 ends with
+// (R3 + R2) + (R1 + R0), the butterfly's (R0 + R1) + (R2 + R3) bit for bit
+// (IEEE addition is commutative).  Returned wave-uniform (lane 63).
 __device__ __forceinline__ double wave_sum(double v) {
     v = v + dpp_d<0xB1>(v);
     v = v + dpp_d<0x4E>(v);
     v = v + dpp_d<0x141>(v);
     v = v + dpp_d<0x140>(v);
-    double r0 = readlane_d(v, 0), r1 = readlane_d(v, 16), r2 = readlane_d(v, 32), r3 = readlane_d(v, 48);
-    return (r0 + r1) + (r2 + r3);
+    v = v + dpp_d<0x142>(v);
+    v = v + dpp_d<0x143>(v);
+    return readlane_d(v, 63);
+}
+// minimum over the wave ignoring NaN lanes (NaN only if every lane is NaN)
+__device__ __forceinline__ double wave_min(double v) {
+    v = vmin(v, dpp_d<0xB1>(v));
+    v = vmin(v, dpp_d<0x4E>(v));
+    v = vmin(v, dpp_d<0x141>(v));
+    v = vmin(v, dpp_d<0x140>(v));
+    v = vmin(v, dpp_d<0x142>(v));
+    v = vmin(v, dpp_d<0x143>(v));
+    return readlane_d(v, 63);
 }
 
 // double-double accumulation (oracle: dd_add_d / dd_div_d)

@@ -1,0 +1,518 @@
+// Symmetric eigendecomposition of the small b x b Rayleigh-Ritz matrix of the
+// PCA (H = Q'GQ, b = block size, <= 512), replacing rocSOLVER dsyevd whose
+// hundreds of tiny launches (latrd column by column) dominated the PCA.
+//
+//   k_sytrd_l   one 1024-thread workgroup reduces H to tridiagonal T = Q_H' H Q_H
+//               (Householder, LAPACK dsytd2 'L' conventions: reflector j has
+//               u[j+1] = 1, u[r] = A[r][j] for r >= j+2, stored in place).  The
+//               rank-2 update of step j is applied lazily inside step j+1's pass
+//               over the trailing lower triangle, fused with the product
+//               p = A22 v of step j+1: one read + one write of the trailing
+//               matrix per step (L2-resident), column dots by wave reductions,
+//               row dots in per-lane registers (lane owns rows r = 64q + lane).
+//   rocsolver_dstedc  eigenpairs of T (divide and conquer)
+//   k_ormtr_l   C <- Q_H C: one wave per column of C, reflectors applied in
+//               reverse order with the column held in registers.
+#include <rocblas/rocblas.h>
+#include <rocsolver/rocsolver.h>
+
+#include "tp_common.cuh"
+#include "tp_internal.h"
+
+namespace tp {
+
+constexpr int EIG_BMAX = 512;
+constexpr int SY_WAVES = 16;
+
+template <int QM>
+__global__ void __launch_bounds__(1024) k_sytrd_l(double *A, int b, double *d, double *e, double *tau) {
+    __shared__ double V[2][EIG_BMAX], W[2][EIG_BMAX], PC[EIG_BMAX];
+    __shared__ double PRW[SY_WAVES][EIG_BMAX];
+    __shared__ double RED[SY_WAVES + 8];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    double vold[QM], wold[QM], vnew[QM], prow[QM], nxt[QM];
+#pragma unroll
+    for (int q = 0; q < QM; ++q) vold[q] = wold[q] = nxt[q] = 0.0;
+    for (int r = t; r < EIG_BMAX; r += 1024) V[1][r] = W[1][r] = V[0][r] = W[0][r] = 0.0;
+    __syncthreads();
+
+    for (int j = 0; j + 2 < b; ++j) {
+        const int P = j & 1;
+        // ---- (a)+(b) wave 0: column j with the pending update of step j-1,
+        //      then the reflector of column j (dlarfg)
+        if (wv == 0) {
+            const double uj = V[P ^ 1][j], wj = W[P ^ 1][j];
+            double cur[QM];
+            double xs = 0.0, al = 0.0;
+#pragma unroll
+            for (int q = 0; q < QM; ++q) {
+                const int r = 64 * q + lane;
+                cur[q] = 0.0;
+                if (r >= j && r < b) {
+                    // column j as left by the previous pass (wave 0 kept it), or memory at j = 0
+                    double a = j == 0 ? A[(size_t)j * b + r] : nxt[q];
+                    a = fma(-vold[q], wj, fma(-wold[q], uj, a));
+                    cur[q] = a;
+                    if (r == j) d[j] = a;
+                    if (r == j + 1) al = a;
+                    if (r >= j + 2) xs = fma(a, a, xs);
+                }
+            }
+            const double xnorm2 = wave_sum(xs);
+            const double alpha = readlane_d(al, (j + 1) & 63);   // the lane owning row j+1
+            double beta, tj, scale;
+            if (xnorm2 == 0.0) {
+                beta = alpha;
+                tj = 0.0;
+                scale = 0.0;
+            } else {
+                beta = -copysign(sqrt(fma(alpha, alpha, xnorm2)), alpha);
+                tj = (beta - alpha) / beta;
+                scale = 1.0 / (alpha - beta);
+            }
+#pragma unroll
+            for (int q = 0; q < QM; ++q) {
+                const int r = 64 * q + lane;
+                if (r < b) {
+                    double v = 0.0;
+                    if (r == j + 1) v = 1.0;
+                    else if (r >= j + 2) {
+                        v = cur[q] * scale;
+                        A[(size_t)j * b + r] = v;
+                    }
+                    V[P][r] = v;
+                }
+            }
+            if (lane == 0) {
+                e[j] = beta;
+                tau[j] = tj;
+                RED[SY_WAVES] = tj;
+            }
+        }
+        __syncthreads();
+        const double tj = RED[SY_WAVES];
+        // ---- (c) pass over the trailing lower triangle, columns c >= j+1:
+        //      apply update j-1, accumulate p = A22 v_j
+#pragma unroll
+        for (int q = 0; q < QM; ++q) {
+            vnew[q] = V[P][64 * q + lane];
+            prow[q] = 0.0;
+        }
+        // columns c = j+1+wv+16k, four per batch: all loads of a batch are in
+        // flight together (the pass is L2-latency bound otherwise)
+        constexpr int U = QM <= 4 ? 4 : 2;
+        for (int cb = j + 1 + wv; cb < b; cb += SY_WAVES * U) {
+            double a[U][QM];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int c = cb + SY_WAVES * u;
+#pragma unroll
+                for (int q = 0; q < QM; ++q) {
+                    const int r = 64 * q + lane;
+                    a[u][q] = (c < b && r >= c && r < b) ? A[(size_t)c * b + r] : 0.0;
+                }
+            }
+            double pc[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int c = cb + SY_WAVES * u;
+                pc[u] = 0.0;
+                if (c < b) {
+                    const double uc = V[P ^ 1][c], wc = W[P ^ 1][c], vc = V[P][c];
+                    double *col = A + (size_t)c * b;
+#pragma unroll
+                    for (int q = 0; q < QM; ++q) {
+                        const int r = 64 * q + lane;
+                        if (r >= c && r < b) {
+                            double x = fma(-vold[q], wc, fma(-wold[q], uc, a[u][q]));
+                            a[u][q] = x;
+                            if (c != j + 1) col[r] = x;   // column j+1 stays in wave 0's registers
+                            prow[q] = fma(x, vc, prow[q]);
+                            if (r > c) pc[u] = fma(x, vnew[q], pc[u]);
+                        }
+                    }
+                }
+            }
+            if (wv == 0 && cb == j + 1) {
+#pragma unroll
+                for (int q = 0; q < QM; ++q) nxt[q] = a[0][q];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int c = cb + SY_WAVES * u;
+                const double ps = wave_sum(pc[u]);
+                if (lane == 0 && c < b) PC[c] = ps;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < QM; ++q) PRW[wv][64 * q + lane] = prow[q];
+        __syncthreads();
+        // ---- (d) p = tau A22 v, alpha2 = -tau/2 p'v, w = p + alpha2 v
+        double p = 0.0, pv = 0.0;
+        if (t < b && t >= j + 1) {
+            double s = PC[t];
+#pragma unroll
+            for (int w = 0; w < SY_WAVES; ++w) s = s + PRW[w][t];
+            p = tj * s;
+            pv = p * V[P][t];
+        }
+        pv = wave_sum(pv);
+        if (lane == 0) RED[wv] = pv;
+        __syncthreads();
+        double dot = 0.0;
+#pragma unroll
+        for (int w = 0; w < SY_WAVES; ++w) dot = dot + RED[w];
+        const double alpha2 = -0.5 * tj * dot;
+        if (t < EIG_BMAX) W[P][t] = (t < b && t >= j + 1) ? fma(alpha2, V[P][t], p) : 0.0;
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < QM; ++q) {
+            vold[q] = V[P][64 * q + lane];
+            wold[q] = W[P][64 * q + lane];
+        }
+    }
+    // ---- last 2 x 2 block with the pending update, T entries.  Column b-2 was
+    //      left in wave 0's registers by the last pass: write it back first.
+    if (wv == 0 && b >= 3) {
+#pragma unroll
+        for (int q = 0; q < QM; ++q) {
+            const int r = 64 * q + lane;
+            if (r >= b - 2 && r < b) A[(size_t)(b - 2) * b + r] = nxt[q];
+        }
+    }
+    __syncthreads();
+    if (t == 0) {
+        if (b >= 2) {
+            const int j = b - 2;
+            const int P = (b - 3) & 1;   // parity of the last reflector step (if any)
+            double a00 = A[(size_t)j * b + j], a10 = A[(size_t)j * b + j + 1], a11 = A[(size_t)(j + 1) * b + j + 1];
+            if (b >= 3) {
+                const double v0 = V[P][j], v1 = V[P][j + 1], w0 = W[P][j], w1 = W[P][j + 1];
+                a00 = a00 - (v0 * w0 + w0 * v0);
+                a10 = a10 - (v1 * w0 + w1 * v0);
+                a11 = a11 - (v1 * w1 + w1 * v1);
+            }
+            d[j] = a00;
+            d[j + 1] = a11;
+            e[j] = a10;
+            tau[j] = 0.0;
+        } else {
+            d[0] = A[0];
+        }
+    }
+}
+
+// C <- Q_H C, Q_H = H_0 H_1 ... H_{b-3}: one wave per column of C (b x b, ldc = b)
+template <int QM>
+__global__ void __launch_bounds__(256) k_ormtr_l(const double *A, const double *tau, int b, double *C) {
+    const int lane = threadIdx.x & 63;
+    const int col = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (col >= b) return;
+    double x[QM];
+#pragma unroll
+    for (int q = 0; q < QM; ++q) {
+        const int r = 64 * q + lane;
+        x[q] = r < b ? C[(size_t)col * b + r] : 0.0;
+    }
+    // reflector j's vector is loaded one iteration ahead (latency hidden)
+    auto load_u = [&](double (&u)[QM], int j) {
+#pragma unroll
+        for (int q = 0; q < QM; ++q) {
+            const int r = 64 * q + lane;
+            u[q] = (r == j + 1) ? 1.0 : ((r >= j + 2 && r < b) ? A[(size_t)j * b + r] : 0.0);
+        }
+    };
+    double un[QM];
+    double tn = 0.0;
+    if (b >= 3) {
+        load_u(un, b - 3);
+        tn = tau[b - 3];
+    }
+    for (int j = b - 3; j >= 0; --j) {
+        double u[QM];
+#pragma unroll
+        for (int q = 0; q < QM; ++q) u[q] = un[q];
+        const double tj = tn;
+        if (j > 0) {
+            load_u(un, j - 1);
+            tn = tau[j - 1];
+        }
+        if (tj == 0.0) continue;
+        double s = 0.0;
+#pragma unroll
+        for (int q = 0; q < QM; ++q) s = fma(u[q], x[q], s);
+        s = wave_sum(s) * tj;
+#pragma unroll
+        for (int q = 0; q < QM; ++q) x[q] = fma(-s, u[q], x[q]);
+    }
+#pragma unroll
+    for (int q = 0; q < QM; ++q) {
+        const int r = 64 * q + lane;
+        if (r < b) C[(size_t)col * b + r] = x[q];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Eigenpairs of the symmetric tridiagonal T (d, e) without rocSOLVER:
+//   k_bisect: one wave per eigenvalue index, 64-section per step (each lane one
+//     Sturm count, the first lane whose count exceeds the index brackets it):
+//     6 bits per step, ~10 steps to 2 ulp.  Gershgorin interval, LAPACK pivmin.
+//   k_invit: inverse iteration (LAPACK dstein scheme) one wave per vector:
+//     LU with partial pivoting of T - sigma I and the solves by lane 0 in LDS,
+//     2 iterations from a deterministic pseudo-random start (the shift is a
+//     2-ulp eigenvalue: one solve already converges); eigenvalues
+//     closer than ctol = 1e-7 ||T|| form a cluster whose first wave computes
+//     all members, modified Gram-Schmidt against earlier members every
+//     iteration.  theta = Rayleigh quotient of the final vector.
+struct TriNorm {
+    double lo, hi, tnorm, pivmin;
+};
+
+__device__ TriNorm tri_bounds(const double *d, const double *e, int b, double *sd, double *se, double *red) {
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6, nw = blockDim.x >> 6;
+    double lo = 1e308, hi = -1e308, em = 0.0;
+    for (int i = t; i < b; i += blockDim.x) {
+        const double di = d[i];
+        const double el = i > 0 ? fabs(e[i - 1]) : 0.0, er = i + 1 < b ? fabs(e[i]) : 0.0;
+        sd[i] = di;
+        se[i] = i + 1 < b ? e[i] : 0.0;
+        lo = fmin(lo, di - el - er);
+        hi = fmax(hi, di + el + er);
+        em = fmax(em, er * er);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        lo = fmin(lo, __shfl_xor(lo, o, 64));
+        hi = fmax(hi, __shfl_xor(hi, o, 64));
+        em = fmax(em, __shfl_xor(em, o, 64));
+    }
+    if (lane == 0) {
+        red[wv] = lo;
+        red[8 + wv] = hi;
+        red[16 + wv] = em;
+    }
+    __syncthreads();
+    for (int w = 0; w < nw; ++w) {
+        lo = fmin(lo, red[w]);
+        hi = fmax(hi, red[8 + w]);
+        em = fmax(em, red[16 + w]);
+    }
+    TriNorm r;
+    r.tnorm = fmax(fabs(lo), fabs(hi));
+    r.pivmin = 2.2250738585072014e-308 * fmax(1.0, em);
+    const double fudge = 2.0 * 2.220446049250313e-16 * r.tnorm * (double)b + 4.0 * r.pivmin;
+    r.lo = lo - fudge;
+    r.hi = hi + fudge;
+    return r;
+}
+
+// se2 = e^2.  1/q by the hardware reciprocal + two Newton steps (a Sturm count
+// tolerates a last-bit error in the quotient: it is the count of a matrix a
+// few ulps away, as LAPACK's own pivmin guard already assumes).
+__device__ __forceinline__ int sturm_count(const double *sd, const double *se2, int b, double x, double pivmin) {
+    int cnt = 0;
+    double q = sd[0] - x;
+    if (fabs(q) < pivmin) q = -pivmin;
+    cnt += q < 0.0;
+#pragma unroll 4
+    for (int i = 1; i < b; ++i) {
+        double r = __builtin_amdgcn_rcp(q);
+        r = r * fma(-q, r, 2.0);
+        r = r * fma(-q, r, 2.0);
+        q = (sd[i] - x) - se2[i - 1] * r;
+        if (fabs(q) < pivmin) q = -pivmin;
+        cnt += q < 0.0;
+    }
+    return cnt;
+}
+
+// lam[idx] = idx-th smallest eigenvalue (midpoint of a ~2-ulp bracket);
+// lam[b] = ||T|| bound (Gershgorin), written by block 0.
+__global__ void __launch_bounds__(256) k_bisect(const double *d, const double *e, int b, double *lam) {
+    __shared__ double sd[EIG_BMAX], se[EIG_BMAX], red[32];
+    const TriNorm tn = tri_bounds(d, e, b, sd, se, red);
+    for (int i = threadIdx.x; i + 1 < b; i += blockDim.x) se[i] = se[i] * se[i];   // e^2 for the counts
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int idx = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (blockIdx.x == 0 && threadIdx.x == 0) lam[b] = tn.tnorm;
+    if (idx >= b) return;
+    double lo = tn.lo, hi = tn.hi;
+    for (int it = 0; it < 40; ++it) {
+        const double width = hi - lo;
+        if (!(width > fmax(4.440892098500626e-16 * fmax(fabs(lo), fabs(hi)), 2.0 * tn.pivmin))) break;
+        const double x = lo + width * ((double)(lane + 1) * (1.0 / 65.0));
+        const int cnt = sturm_count(sd, se, b, x, tn.pivmin);
+        const unsigned long long m = __ballot(cnt > idx);
+        if (m == 0ULL) {
+            lo = readlane_d(x, 63);
+        } else {
+            const int f = (int)__builtin_ctzll(m);
+            const double xf = readlane_d(x, f);
+            if (f > 0) lo = readlane_d(x, f - 1);
+            hi = xf;
+        }
+    }
+    if (lane == 0) lam[idx] = 0.5 * (lo + hi);
+}
+
+__device__ __forceinline__ double hash_unit(unsigned int m, unsigned int i) {
+    uint64_t z = 0x9E3779B97F4A7C15ULL * ((uint64_t)m * 1000003ULL + i + 1);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    z ^= z >> 31;
+    return (double)(z >> 11) * (2.0 / 9007199254740992.0) - 1.0;
+}
+
+// Z (b x b, column m = eigenvector m), theta[m] = Rayleigh quotient.  dd holds
+// the reciprocal pivots of U.
+__global__ void __launch_bounds__(256) k_invit(const double *d, const double *e, int b, const double *lam,
+                                               double *Z, double *theta) {
+    __shared__ double sd[EIG_BMAX], se[EIG_BMAX];
+    __shared__ double dd[4][EIG_BMAX], du[4][EIG_BMAX], du2[4][EIG_BMAX], dl[4][EIG_BMAX], xv[4][EIG_BMAX];
+    __shared__ unsigned char swp[4][EIG_BMAX];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    for (int i = t; i < b; i += 256) {
+        sd[i] = d[i];
+        se[i] = i + 1 < b ? e[i] : 0.0;
+    }
+    __syncthreads();
+    const int idx = blockIdx.x * 4 + wv;
+    if (idx >= b) return;
+    const double tnorm = lam[b];
+    const double eps = 2.220446049250313e-16;
+    const double ctol = 1e-7 * tnorm;
+    if (idx > 0 && lam[idx] - lam[idx - 1] <= ctol) return;   // a member: its leader computes it
+    int last = idx;
+    while (last + 1 < b && lam[last + 1] - lam[last] <= ctol) ++last;
+    double *x = xv[wv];
+    double sig_prev = 0.0;
+    for (int m = idx; m <= last; ++m) {
+        double sig = lam[m];
+        if (m > idx && sig - sig_prev < 10.0 * eps * fabs(sig)) sig = sig_prev + 10.0 * eps * fmax(fabs(sig), tnorm * eps);
+        sig_prev = sig;
+        // ---- LU with partial pivoting of T - sig I (dgttrf), lane 0
+        if (lane == 0) {
+            const double tiny = eps * tnorm + 1e-300;
+            double cd = sd[0] - sig;                 // current diagonal
+            double cu = b > 1 ? se[0] : 0.0;         // current superdiagonal
+            for (int i = 0; i + 1 < b; ++i) {
+                const double sub = se[i];            // T(i+1, i)
+                const double nd = sd[i + 1] - sig;   // T(i+1, i+1)
+                const double nu = i + 2 < b ? se[i + 1] : 0.0;   // T(i+1, i+2)
+                if (fabs(cd) >= fabs(sub)) {
+                    const double piv = cd != 0.0 ? cd : tiny;
+                    const double f = sub / piv;
+                    dd[wv][i] = 1.0 / piv;
+                    du[wv][i] = cu;
+                    du2[wv][i] = 0.0;
+                    dl[wv][i] = f;
+                    swp[wv][i] = 0;
+                    cd = nd - f * cu;
+                    cu = nu;
+                } else {
+                    const double f = cd / sub;
+                    dd[wv][i] = 1.0 / sub;
+                    du[wv][i] = nd;
+                    du2[wv][i] = nu;
+                    dl[wv][i] = f;
+                    swp[wv][i] = 1;
+                    cd = cu - f * nd;
+                    cu = -f * nu;
+                }
+            }
+            dd[wv][b - 1] = 1.0 / (cd != 0.0 ? cd : tiny);
+        }
+        // ---- start vector
+        for (int i = lane; i < b; i += 64) x[i] = hash_unit((unsigned)m, (unsigned)i);
+        for (int it = 0; it < 2; ++it) {
+            // scale to max-norm 1, then solve L U x = y (lane 0)
+            double mx = 0.0;
+            for (int i = lane; i < b; i += 64) mx = fmax(mx, fabs(x[i]));
+            for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
+            const double inv = mx > 0.0 ? 1.0 / mx : 1.0;
+            for (int i = lane; i < b; i += 64) x[i] *= inv;
+            if (lane == 0) {
+                for (int i = 0; i + 1 < b; ++i) {
+                    double yi = x[i], yn = x[i + 1];
+                    if (swp[wv][i]) {
+                        const double tmp = yi;
+                        yi = yn;
+                        yn = tmp;
+                        x[i] = yi;
+                    }
+                    x[i + 1] = yn - dl[wv][i] * yi;
+                }
+                double x2 = 0.0, x1 = x[b - 1] * dd[wv][b - 1];
+                x[b - 1] = x1;
+                for (int i = b - 2; i >= 0; --i) {
+                    const double xi = (x[i] - du[wv][i] * x1 - du2[wv][i] * x2) * dd[wv][i];
+                    x[i] = xi;
+                    x2 = x1;
+                    x1 = xi;
+                }
+            }
+            // MGS against the earlier cluster members, then normalise
+            for (int p = idx; p < m; ++p) {
+                double s = 0.0;
+                for (int i = lane; i < b; i += 64) s = fma(Z[(size_t)p * b + i], x[i], s);
+                s = wave_sum(s);
+                for (int i = lane; i < b; i += 64) x[i] = fma(-s, Z[(size_t)p * b + i], x[i]);
+            }
+            double nn = 0.0;
+            for (int i = lane; i < b; i += 64) nn = fma(x[i], x[i], nn);
+            nn = wave_sum(nn);
+            const double rn = 1.0 / sqrt(nn);
+            for (int i = lane; i < b; i += 64) x[i] *= rn;
+        }
+        // ---- store, Rayleigh quotient
+        double rq = 0.0;
+        for (int i = lane; i < b; i += 64) {
+            const double xi = x[i];
+            double tx = sd[i] * xi;
+            if (i > 0) tx = fma(se[i - 1], x[i - 1], tx);
+            if (i + 1 < b) tx = fma(se[i], x[i + 1], tx);
+            rq = fma(xi, tx, rq);
+            Z[(size_t)m * b + i] = xi;
+        }
+        rq = wave_sum(rq);
+        if (lane == 0) theta[m] = rq;
+    }
+}
+
+static void rb_ok(rocblas_status st, const char *what) {
+    if (st != rocblas_status_success) fail(TP_ERR_HIP, std::string("rocSOLVER failure in ") + what);
+}
+
+bool eig_sym_supported(int b) { return b >= 1 && b <= EIG_BMAX; }
+
+// In place: A (b x b, lower triangle of a symmetric matrix) <- eigenvectors,
+// theta <- eigenvalues ascending.  work: >= b*b + 4*b + 8 doubles; info: device
+// int (dstedc path).  method 0: rocSOLVER dstedc for the tridiagonal stage,
+// 1: k_bisect + k_invit.
+void eig_sym(rocblas_handle h, double *A, int b, double *theta, double *work, int *info, hipStream_t s,
+             int method) {
+    if (!eig_sym_supported(b)) fail(TP_ERR_UNSUPPORTED, "eig_sym: b > 512");
+    double *C = work, *e = C + (size_t)b * b, *tau = e + b, *dg = tau + b, *lam = dg + b;   // lam: b + 1
+    if (b <= 256)
+        hipLaunchKernelGGL(k_sytrd_l<4>, dim3(1), dim3(1024), 0, s, A, b, dg, e, tau);
+    else
+        hipLaunchKernelGGL(k_sytrd_l<8>, dim3(1), dim3(1024), 0, s, A, b, dg, e, tau);
+    TP_HIP(hipGetLastError());
+    if (method == 0) {
+        TP_HIP(hipMemcpyAsync(theta, dg, (size_t)b * sizeof(double), hipMemcpyDeviceToDevice, s));
+        rb_ok(rocsolver_dstedc(h, rocblas_evect_tridiagonal, b, theta, e, C, b, info), "dstedc");
+    } else {
+        const unsigned g = (unsigned)((b + 3) / 4);
+        hipLaunchKernelGGL(k_bisect, dim3(g), dim3(256), 0, s, dg, e, b, lam);
+        hipLaunchKernelGGL(k_invit, dim3(g), dim3(256), 0, s, dg, e, b, lam, C, theta);
+        TP_HIP(hipGetLastError());
+    }
+    if (b <= 256)
+        hipLaunchKernelGGL(k_ormtr_l<4>, dim3((b + 3) / 4), dim3(256), 0, s, A, tau, b, C);
+    else
+        hipLaunchKernelGGL(k_ormtr_l<8>, dim3((b + 3) / 4), dim3(256), 0, s, A, tau, b, C);
+    TP_HIP(hipGetLastError());
+    TP_HIP(hipMemcpyAsync(A, C, (size_t)b * b * sizeof(double), hipMemcpyDeviceToDevice, s));
+}
+
+}  // namespace tp

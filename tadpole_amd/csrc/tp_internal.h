@@ -1,6 +1,7 @@
 // Internal declarations shared by the HIP translation units of libtadpole_hip.
 // Nothing here is part of the C ABI (include/tadpole_hip.h is).
 #pragma once
+#include <rocblas/rocblas.h>
 
 #include <hip/hip_runtime.h>
 #include <cstddef>
@@ -139,6 +140,13 @@ void launch_transpose(const double *d_A, int rows, int cols, int lda, double *d_
                       hipStream_t s);
 
 // PCA (tp_pca.cpp): P (n x k col-major, ld n) and Pt (n x k row-major) from C.
+// Symmetric eigendecomposition for b <= 512 (tp_eig.hip): A (b x b, lower
+// triangle) <- eigenvectors, theta <- ascending eigenvalues.  work >= b*b + 4b + 8.
+// method 0: tridiagonal stage by rocSOLVER dstedc, 1: bisection + inverse iteration.
+bool eig_sym_supported(int b);
+void eig_sym(rocblas_handle h, double *A, int b, double *theta, double *work, int *info, hipStream_t s,
+             int method = 1);
+
 struct PcaStats { int iters = 0; double resid = 0; double rate = 0; int block = 0; int blocks = 0; };
 PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d_Pt,
                  double *h_sdev);

@@ -150,8 +150,12 @@ PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d
         double *E = c.buf[S_Z].as<double>((size_t)n * n);
         TP_HIP(hipMemcpyAsync(E, G, (size_t)n * n * sizeof(double), hipMemcpyDeviceToDevice, s));
         double *offbuf = c.buf[S_Q].as<double>((size_t)n + 64);
-        rb_check(rocsolver_dsyevd(h, rocblas_evect_original, rocblas_fill_upper, n, E, n, theta, offbuf, d_info),
-                 "dsyevd");
+        if (eig_sym_supported(n))
+            eig_sym(h, E, n, theta, c.buf[S_PARTIAL].as<double>((size_t)n * n + 4 * n + 64), d_info, s);
+        else
+            rb_check(rocsolver_dsyevd(h, rocblas_evect_original, rocblas_fill_upper, n, E, n, theta, offbuf,
+                                      d_info),
+                     "dsyevd");
         size_t tot = (size_t)n * k;
         hipLaunchKernelGGL(k_select_rev, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, E, n, k, V);
         TP_HIP(hipGetLastError());
@@ -283,9 +287,12 @@ PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d
             hq.sym_upper = true;
             hq.splitk = std::max(1, std::min(32, n / 128));
             gemm_f64(hq, c.buf[S_PARTIAL], s);
-            rb_check(rocsolver_dsyevd(h, rocblas_evect_original, rocblas_fill_upper, b, Wsm, b, theta, offd,
-                                      d_info),
-                     "dsyevd(RR)");
+            if (eig_sym_supported(b))
+                eig_sym(h, Wsm, b, theta, c.buf[S_PARTIAL].as<double>((size_t)b * b + 4 * b + 64), d_info, s);
+            else
+                rb_check(rocsolver_dsyevd(h, rocblas_evect_original, rocblas_fill_upper, b, Wsm, b, theta, offd,
+                                          d_info),
+                         "dsyevd(RR)");
             size_t tot = (size_t)b * b;
             hipLaunchKernelGGL(k_select_rev, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, Wsm, b, b, Xinv);
             GemmArgs rq{n, b, b, Q, n, false, Xinv, b, Z, n};

@@ -24,32 +24,6 @@ namespace tp {
 
 constexpr int KMAXSLOT = 4;   // columns per lane: k <= 256
 
-__device__ __forceinline__ bool key_less(double v1, int i1, double v2, int i2) {
-    return v1 < v2 || (v1 == v2 && i1 < i2);
-}
-template <int CTRL> __device__ __forceinline__ void amin_step(double &v, int &idx) {
-    double v2 = dpp_d<CTRL>(v);
-    int i2 = dpp_i<CTRL>(idx);
-    if (key_less(v2, i2, v, idx)) { v = v2; idx = i2; }
-}
-// lexicographic (value, index) minimum over the wave; every lane gets it
-__device__ __forceinline__ void wave_argmin(double &v, int &idx) {
-    amin_step<0xB1>(v, idx);
-    amin_step<0x4E>(v, idx);
-    amin_step<0x141>(v, idx);
-    amin_step<0x140>(v, idx);
-    double bv = readlane_d(v, 0);
-    int bi = __builtin_amdgcn_readlane(idx, 0);
-#pragma unroll
-    for (int r = 16; r < 64; r += 16) {
-        double v2 = readlane_d(v, r);
-        int i2 = __builtin_amdgcn_readlane(idx, r);
-        if (key_less(v2, i2, bv, bi)) { bv = v2; bi = i2; }
-    }
-    v = bv;
-    idx = bi;
-}
-
 // pairwise tree over 64 leaves = the xor butterfly's summation tree
 template <int W> struct PTree {
     template <class F> __device__ static __forceinline__ double run(const F &f, int m0) {
@@ -60,9 +34,18 @@ template <> struct PTree<1> {
     template <class F> __device__ static __forceinline__ double run(const F &f, int m0) { return f(m0); }
 };
 
-// tree i (1-based) keeps an n x i slab; trees tree0+1..tree0+ntrees are packed
+// Tree i (1-based) keeps an n x ld(i) slab, ld(i) = 64 * ceil(i / 64): rows
+// are padded with zeros to whole 64-column slots, so a lane's loads, stores and
+// Ward terms never need a column guard (a zero pad contributes fma(0, 0, acc)
+// = acc exactly: the canonical sums are unchanged).  Trees tree0+1..tree0+ntrees
+// are packed.  pad_prefix(m) = sum_{t=1..m} ld(t).
+static __host__ __device__ inline size_t pad_prefix(long m) {
+    const long g = m / 64, r = m % 64;
+    return (size_t)64 * (size_t)(64 * g * (g + 1) / 2 + r * (g + 1));
+}
+static __host__ __device__ inline int slab_ld(int i) { return ((i + 63) / 64) * 64; }
 static __host__ __device__ inline size_t sums_off(int n, int tree0, int i) {
-    return (size_t)n * ((size_t)i * (i - 1) / 2 - (size_t)(tree0 + 1) * tree0 / 2);
+    return (size_t)n * (pad_prefix(i - 1) - pad_prefix(tree0));
 }
 size_t sweep_sums_doubles(int n, int tree0, int ntrees) { return sums_off(n, tree0, tree0 + ntrees + 1); }
 
@@ -83,15 +66,6 @@ __device__ __forceinline__ double nan2inf(double x) { return isnan(x) ? __longlo
 // Synchronisation: the workgroup is one wave.  Every lane writes the same value
 // to each shared LDS word it updates, so no barrier is needed in the loop.
 
-__device__ __forceinline__ double wave_min(double v) {   // ignores NaN lanes
-    v = fmin(v, dpp_d<0xB1>(v));
-    v = fmin(v, dpp_d<0x4E>(v));
-    v = fmin(v, dpp_d<0x141>(v));
-    v = fmin(v, dpp_d<0x140>(v));
-    double r0 = readlane_d(v, 0), r1 = readlane_d(v, 16), r2 = readlane_d(v, 32), r3 = readlane_d(v, 48);
-    return fmin(fmin(r0, r1), fmin(r2, r3));
-}
-
 // two canonical wave sums interleaved (independent chains, same bits as wave_sum)
 __device__ __forceinline__ void wave_sum2(double &u, double &v) {
     u = u + dpp_d<0xB1>(u);
@@ -102,32 +76,23 @@ __device__ __forceinline__ void wave_sum2(double &u, double &v) {
     v = v + dpp_d<0x141>(v);
     u = u + dpp_d<0x140>(u);
     v = v + dpp_d<0x140>(v);
-    double u0 = readlane_d(u, 0), u1 = readlane_d(u, 16), u2 = readlane_d(u, 32), u3 = readlane_d(u, 48);
-    double v0 = readlane_d(v, 0), v1 = readlane_d(v, 16), v2 = readlane_d(v, 32), v3 = readlane_d(v, 48);
-    u = (u0 + u1) + (u2 + u3);
-    v = (v0 + v1) + (v2 + v3);
+    u = u + dpp_d<0x142>(u);
+    v = v + dpp_d<0x142>(v);
+    u = u + dpp_d<0x143>(u);
+    v = v + dpp_d<0x143>(v);
+    u = readlane_d(u, 63);
+    v = readlane_d(v, 63);
 }
 
-__device__ __forceinline__ double ward_part(const double (&sa)[KMAXSLOT], double fa, const double (&sb)[KMAXSLOT],
-                                            double fb, int lane, int ncols) {
-    double acc = 0.0;
-#pragma unroll
-    for (int t = 0; t < KMAXSLOT; ++t)
-        if (lane + 64 * t < ncols) {
-            double t1 = sa[t] * fb;
-            double t2 = sb[t] * fa;
-            double e = t1 - t2;
-            acc = fma(e, e, acc);
-        }
-    return acc;
-}
 
 // ---- seeding: every tree's cluster-sum slab starts as the first i columns of
-// the scores, and the initial adjacent (singleton) costs are e_j = x_j - y_j,
-// cost = tot / 2 (canonical order).  One wave per (tree, 64 positions).
+// the scores (zero-padded to ld(i)), and the initial adjacent (singleton) costs
+// are e_j = x_j - y_j, cost = tot / 2 (canonical order).  One wave per
+// (tree, 64 positions).
 __global__ void __launch_bounds__(64) k_seed(SweepDev sd, double *cost0) {
     const int n = sd.n, ldp = sd.ldp;
     const int ti = blockIdx.x, i = sd.tree0 + ti + 1;
+    const int ld = slab_ld(i);
     const int lane = threadIdx.x;
     double *S = sd.sums + sums_off(n, sd.tree0, i);
     double *c0 = cost0 + (size_t)ti * ((n + 63) / 64) * 64;
@@ -150,7 +115,7 @@ __global__ void __launch_bounds__(64) k_seed(SweepDev sd, double *cost0) {
         for (int t = 0; t < KMAXSLOT; ++t) {
             x[t] = y[t];
             const int j = lane + 64 * t;
-            if (j < i) S[(size_t)p * i + j] = x[t];
+            if (j < ld) S[(size_t)p * ld + j] = x[t];
             y[t] = (p + 1 < n && j < i) ? sd.Pt[(size_t)(p + 1) * ldp + j] : 0.0;
         }
         if (p + 1 < n) {
@@ -168,10 +133,32 @@ __global__ void __launch_bounds__(64) k_seed(SweepDev sd, double *cost0) {
     c0[p0 + lane] = mycost;
 }
 
-constexpr int BSLOT = 4;   // block minima per lane (registers): n <= 64 * 64 * BSLOT
+template <int NS>
+__device__ __forceinline__ double ward_part(const double (&sa)[NS], double fa, const double (&sb)[NS], double fb) {
+    double acc = 0.0;
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {
+        const double t1 = sa[t] * fb;
+        const double t2 = sb[t] * fa;
+        const double e = t1 - t2;
+        acc = fma(e, e, acc);
+    }
+    return acc;
+}
 
-template <bool STAMPS>
-__global__ void __launch_bounds__(64) k_coniss_t(SweepDev sd, const double *cost0) {
+// One tree's CONISS with NS = ld(i) / 64 column slots per lane and BS block-
+// minimum slots per lane (n <= 4096 BS).
+//
+// Speculative prefetch.  After merge s (pair a|b -> m at a) the next merge is
+// one of exactly three: the smallest cost among positions merge s does not
+// touch (a2, found with ls/a/b masked out), ls|m (new cost cl) or m|r (new
+// cost cr).  The rows each of them needs are loaded during merge s:
+//   a2:   rows a2, b2, ls2, r2 (one that is m comes from registers)
+//   ls|m: sl, sm, row(ll), sr        m|r: sm, sr, sl, row(rr)
+// and the choice among them is applied at the next merge, after its own
+// structural work, so the loads have a whole merge to land.
+template <bool STAMPS, int NS, int BS>
+__device__ __forceinline__ void coniss_tree(const SweepDev &sd, const double *cost0, double *lds) {
     long long st_acc[6] = {0, 0, 0, 0, 0, 0};
     long long st_t0 = STAMPS ? (long long)__builtin_amdgcn_s_memtime() : 0;
 #define TP_STAMP(ph)                                                      \
@@ -180,26 +167,26 @@ __global__ void __launch_bounds__(64) k_coniss_t(SweepDev sd, const double *cost
         st_acc[ph] += _t - st_t0;                                         \
         st_t0 = _t;                                                       \
     }
-    extern __shared__ double lds[];
     const int n = sd.n;
     const int ti = blockIdx.x;                 // tree slot
     const int i = sd.tree0 + ti + 1;           // PC prefix length
+    constexpr int ld = NS * 64;
     const int lane = threadIdx.x;
     const int nbk = (n + 63) / 64;
     const double QNAN = __longlong_as_double(0x7FF8000000000000LL);
     double *cost = lds;                        // nbk*64: NaN = not a candidate
     int *link = (int *)(cost + nbk * 64);      // n: cluster start <-> end
     int *rn = link + n;                        // n: end of the right neighbour (at cluster starts)
-    double *S = sd.sums + sums_off(n, sd.tree0, i);
+    double *S = sd.sums + sums_off(n, sd.tree0, i) + lane;
     int *mrg_a = sd.mrg_a + (size_t)ti * (n - 1);
     int *mrg_b = sd.mrg_b + (size_t)ti * (n - 1);
     double *mcost = sd.cost + (size_t)ti * (n - 1);
     double *height = sd.height + (size_t)ti * (n - 1);
     const double *c0 = cost0 + (size_t)ti * nbk * 64;
 
-    double bmr[BSLOT];
+    double bmr[BS];
 #pragma unroll
-    for (int q = 0; q < BSLOT; ++q) bmr[q] = QNAN;
+    for (int q = 0; q < BS; ++q) bmr[q] = QNAN;
     for (int bk = 0; bk < nbk; ++bk) {
         const int p = bk * 64 + lane;
         const double cp = c0[p];
@@ -211,59 +198,57 @@ __global__ void __launch_bounds__(64) k_coniss_t(SweepDev sd, const double *cost
         const double m = wave_min(cp);
         if (lane == (bk & 63)) {
 #pragma unroll
-            for (int q = 0; q < BSLOT; ++q)
+            for (int q = 0; q < BS; ++q)
                 if (q == (bk >> 6)) bmr[q] = m;
         }
     }
     __syncthreads();
-    TP_STAMP(4);
 
-    // ---- the first merge: global argmin, then its four cluster rows
     auto argmin_pos = [&](double vmin) -> int {   // leftmost position holding vmin (-1: none)
         if (isnan(vmin)) return -1;
         int blk = 0;
 #pragma unroll
-        for (int q = BSLOT - 1; q >= 0; --q) {
+        for (int q = BS - 1; q >= 0; --q) {
             const unsigned long long m = __ballot(bmr[q] == vmin);
             if (m) blk = 64 * q + (int)__builtin_ctzll(m);
         }
         const unsigned long long mp = __ballot(cost[blk * 64 + lane] == vmin);
         return blk * 64 + (int)__builtin_ctzll(mp);
     };
-    auto load_row = [&](double (&dst)[KMAXSLOT], int start) {
-        const double *pr = S + (size_t)start * i;
+    auto load_row = [&](double (&dst)[NS], int start) {
+        const double *pr = S + (size_t)start * ld;
 #pragma unroll
-        for (int t = 0; t < KMAXSLOT; ++t) {
-            const int j = lane + 64 * t;
-            dst[t] = j < i ? pr[j] : 0.0;
-        }
+        for (int t = 0; t < NS; ++t) dst[t] = pr[64 * t];
     };
-    double gv0 = bmr[0];
+    auto gmin = [&]() {
+        double g = bmr[0];
 #pragma unroll
-    for (int q = 1; q < BSLOT; ++q) gv0 = fmin(gv0, bmr[q]);
-    double c = wave_min(gv0);
+        for (int q = 1; q < BS; ++q) g = vmin(g, bmr[q]);
+        return wave_min(g);
+    };
+    // ---- the first merge; its rows enter as a "which = 0" prefetch
+    double c = gmin();
     int a = argmin_pos(c);
-    double sa[KMAXSLOT], sb[KMAXSLOT], sl[KMAXSLOT], sr[KMAXSLOT];
+    double pa[NS], pb[NS], pl[NS], pr[NS], pll[NS], prr[NS], sl[NS], sr[NS], sm[NS];
+    int which = 0, ls2p, r2p, aprev = -1;
     {
         const int ea = link[a], eb = rn[a];
         const int ls = a > 0 ? link[a - 1] : -1;
         const int r = eb + 1 < n ? eb + 1 : -1;
-        load_row(sa, a);
-        load_row(sb, ea + 1);
-        load_row(sl, ls >= 0 ? ls : a);
-        load_row(sr, r >= 0 ? r : a);
+        load_row(pa, a);
+        load_row(pb, ea + 1);
+        load_row(pl, ls >= 0 ? ls : a);
+        load_row(pr, r >= 0 ? r : a);
+        ls2p = ls;
+        r2p = r;
+#pragma unroll
+        for (int t = 0; t < NS; ++t) pll[t] = prr[t] = sl[t] = sr[t] = sm[t] = 0.0;
     }
     TP_STAMP(4);
 
-    // Speculative prefetch.  After merge s (pair a|b -> m at a) the next merge is
-    // one of exactly three: the smallest cost among positions this merge does
-    // not touch (a2; found while merge s is in flight, with ls/a/b masked out),
-    // ls|m (new cost cl) or m|r (new cost cr).  The rows each of them needs are
-    // loaded during merge s, so no merge waits on HBM for its own operands:
-    //   a2:   rows a2, b2, ls2, r2 (any of them that is m comes from registers)
-    //   ls|m: sl, sm, row(ll), sr        m|r: sm, sr, sl, row(rr)
     double h = 0.0;
     for (int s = 0; s < n - 1; ++s) {
+        // ---- (1) links of the merge a|b
         const int ea = link[a];
         const int eb = rn[a];
         const int ls = a > 0 ? link[a - 1] : -1;
@@ -272,20 +257,7 @@ __global__ void __launch_bounds__(64) k_coniss_t(SweepDev sd, const double *cost
         const int er = r >= 0 ? rn[b] : -1;
         const int na = ea - a + 1, nbb = eb - b + 1, nm = na + nbb;
         const int nl = ls >= 0 ? a - ls : 0, nr = r >= 0 ? er - r + 1 : 0;
-        double sm[KMAXSLOT];
-#pragma unroll
-        for (int t = 0; t < KMAXSLOT; ++t) {
-            sm[t] = sa[t] + sb[t];
-            const int j = lane + 64 * t;
-            if (j < i) S[(size_t)a * i + j] = sm[t];
-        }
-        if (lane == 0) {
-            mrg_a[s] = a;
-            mrg_b[s] = b;
-            mcost[s] = c;
-        }
-        TP_STAMP(1);
-        // ---- structure update; ls, a, b masked out of the cost array
+        // ---- (2) structure update; ls, a, b masked out; speculative argmin
         link[a] = eb;
         link[eb] = a;
         rn[a] = er;
@@ -301,19 +273,41 @@ __global__ void __launch_bounds__(64) k_coniss_t(SweepDev sd, const double *cost
             const double mb = bb != ba ? wave_min(cost[bb * 64 + lane]) : ma;
             const double ml = (bl != ba && bl != bb) ? wave_min(cost[bl * 64 + lane]) : ma;
 #pragma unroll
-            for (int q = 0; q < BSLOT; ++q) {
+            for (int q = 0; q < BS; ++q) {
                 if (lane == (ba & 63) && q == (ba >> 6)) bmr[q] = ma;
                 if (bb != ba && lane == (bb & 63) && q == (bb >> 6)) bmr[q] = mb;
                 if (bl != ba && bl != bb && lane == (bl & 63) && q == (bl >> 6)) bmr[q] = ml;
             }
         }
-        double gv = bmr[0];
-#pragma unroll
-        for (int q = 1; q < BSLOT; ++q) gv = fmin(gv, bmr[q]);
-        const double v2 = wave_min(gv);
+        const double v2 = gmin();
         const int a2 = argmin_pos(v2);
         TP_STAMP(0);
-        // ---- prefetch the candidates' rows (post-merge links)
+        // ---- (3a) this merge's rows from the previous merge's prefetch
+        double sa[NS], sb[NS];
+        if (which == 0) {
+#pragma unroll
+            for (int t = 0; t < NS; ++t) {
+                sa[t] = pa[t];
+                sb[t] = pb[t];
+                sl[t] = ls2p == aprev ? sm[t] : pl[t];
+                sr[t] = r2p == aprev ? sm[t] : pr[t];
+            }
+        } else if (which == 1) {   // ls | m
+#pragma unroll
+            for (int t = 0; t < NS; ++t) {
+                sa[t] = sl[t];
+                sb[t] = sm[t];
+                sl[t] = pll[t];
+            }
+        } else {                   // m | r
+#pragma unroll
+            for (int t = 0; t < NS; ++t) {
+                sa[t] = sm[t];
+                sb[t] = sr[t];
+                sr[t] = prr[t];
+            }
+        }
+        // ---- (3b) prefetch the next merge's candidates (post-merge links)
         const int a2s = a2 >= 0 ? a2 : a;
         const int b2 = link[a2s] + 1;
         const int ls2 = a2s > 0 ? link[a2s - 1] : -1;
@@ -321,59 +315,51 @@ __global__ void __launch_bounds__(64) k_coniss_t(SweepDev sd, const double *cost
         const int r2 = (e2 >= 0 && e2 + 1 < n) ? e2 + 1 : -1;
         const int ll = ls > 0 ? link[ls - 1] : -1;
         const int rr = (r >= 0 && er + 1 < n) ? er + 1 : -1;
-        double pa[KMAXSLOT], pb[KMAXSLOT], pl[KMAXSLOT], pr[KMAXSLOT], pll[KMAXSLOT], prr[KMAXSLOT];
         load_row(pa, a2s);
         load_row(pb, b2 < n ? b2 : a);
         load_row(pl, ls2 >= 0 ? ls2 : a);
         load_row(pr, r2 >= 0 ? r2 : a);
         load_row(pll, ll >= 0 ? ll : a);
         load_row(prr, rr >= 0 ? rr : a);
-        // ---- the two new adjacent costs (division-free Ward form), paired
+        TP_STAMP(1);
+        // ---- (4) merged sums, merge record
+#pragma unroll
+        for (int t = 0; t < NS; ++t) {
+            sm[t] = sa[t] + sb[t];
+            S[(size_t)a * ld + 64 * t] = sm[t];
+        }
+        if (lane == 0) {
+            mrg_a[s] = a;
+            mrg_b[s] = b;
+            mcost[s] = c;
+        }
+        // ---- (5) the two new adjacent costs (division-free Ward form), paired
         const double fm = (double)nm, fl = (double)nl, fr = (double)nr;
-        double ul = ward_part(sl, fl, sm, fm, lane, i);
-        double ur = ward_part(sm, fm, sr, fr, lane, i);
+        double ul = ward_part<NS>(sl, fl, sm, fm);
+        double ur = ward_part<NS>(sm, fm, sr, fr);
         wave_sum2(ul, ur);
         const double cl = ls >= 0 ? nan2inf(ul / (fl * fm * (fl + fm))) : QNAN;
         const double cr = r >= 0 ? nan2inf(ur / (fm * fr * (fm + fr))) : QNAN;
         h = h + c;
         if (lane == 0) height[s] = h;
         TP_STAMP(2);
+        // ---- (6) new costs in, next merge: lexicographic (cost, position)
+        //      minimum of the three candidates
         cost[a] = cr;                     // QNAN when there is no right neighbour
         if (ls >= 0) cost[ls] = cl;
 #pragma unroll
-        for (int q = 0; q < BSLOT; ++q) {
-            if (lane == (ba & 63) && q == (ba >> 6)) bmr[q] = fmin(bmr[q], cr);
-            if (ls >= 0 && lane == (bl & 63) && q == (bl >> 6)) bmr[q] = fmin(bmr[q], cl);
+        for (int q = 0; q < BS; ++q) {
+            if (lane == (ba & 63) && q == (ba >> 6)) bmr[q] = vmin(bmr[q], cr);
+            if (ls >= 0 && lane == (bl & 63) && q == (bl >> 6)) bmr[q] = vmin(bmr[q], cl);
         }
-        // ---- next merge: lexicographic (cost, position) minimum of the three
         double nv = v2;
         int np = a2;
-        int which = 0;
+        which = 0;
         if (ls >= 0 && (np < 0 || cl < nv || (cl == nv && ls < np))) { nv = cl; np = ls; which = 1; }
         if (r >= 0 && (np < 0 || cr < nv || (cr == nv && a < np))) { nv = cr; np = a; which = 2; }
-        if (which == 0) {
-#pragma unroll
-            for (int t = 0; t < KMAXSLOT; ++t) {
-                sa[t] = pa[t];
-                sb[t] = pb[t];
-                sl[t] = ls2 == a ? sm[t] : pl[t];
-                sr[t] = r2 == a ? sm[t] : pr[t];
-            }
-        } else if (which == 1) {   // ls | m
-#pragma unroll
-            for (int t = 0; t < KMAXSLOT; ++t) {
-                sa[t] = sl[t];
-                sb[t] = sm[t];
-                sl[t] = pll[t];
-            }
-        } else {                   // m | r
-#pragma unroll
-            for (int t = 0; t < KMAXSLOT; ++t) {
-                sa[t] = sm[t];
-                sb[t] = sr[t];
-                sr[t] = prr[t];
-            }
-        }
+        ls2p = ls2;
+        r2p = r2;
+        aprev = a;
         a = np;
         c = nv;
         TP_STAMP(3);
@@ -408,9 +394,23 @@ __global__ void __launch_bounds__(64) k_coniss_t(SweepDev sd, const double *cost
         for (int q = 0; q < 6; ++q) sd.stamps[(size_t)ti * 8 + q] = st_acc[q];
 #undef TP_STAMP
 }
-template __global__ void k_coniss_t<false>(SweepDev, const double *);
-template __global__ void k_coniss_t<true>(SweepDev, const double *);
-#define k_coniss k_coniss_t<false>
+
+// STAMPS: diagnostic build (see coniss_tree).  BS: block-minimum slots (n <= 4096 BS).
+template <bool STAMPS, int BS>
+__global__ void __launch_bounds__(64) k_coniss_t(SweepDev sd, const double *cost0) {
+    extern __shared__ double lds[];
+    const int i = sd.tree0 + blockIdx.x + 1;
+    switch ((i + 63) / 64) {
+        case 1: coniss_tree<STAMPS, 1, BS>(sd, cost0, lds); break;
+        case 2: coniss_tree<STAMPS, 2, BS>(sd, cost0, lds); break;
+        case 3: coniss_tree<STAMPS, 3, BS>(sd, cost0, lds); break;
+        default: coniss_tree<STAMPS, 4, BS>(sd, cost0, lds); break;
+    }
+}
+template __global__ void k_coniss_t<false, 1>(SweepDev, const double *);
+template __global__ void k_coniss_t<false, 3>(SweepDev, const double *);
+template __global__ void k_coniss_t<true, 1>(SweepDev, const double *);
+template __global__ void k_coniss_t<true, 3>(SweepDev, const double *);
 
 // ------------------------------------------------------------ CH over cuts
 // canonical segment statistics of rows s..e, by one wave (see tpo_seg_ss)
@@ -623,20 +623,26 @@ static size_t coniss_lds_bytes(int n) {
 }
 
 // seed kernel + CONISS (cost0 = initial adjacent costs, ntrees x nbk*64)
+template <bool STAMPS, int BS>
+static void launch_coniss_bs(const SweepDev &sd, const double *cost0, size_t lds, hipStream_t s) {
+    TP_HIP(hipFuncSetAttribute((const void *)k_coniss_t<STAMPS, BS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)lds));
+    hipLaunchKernelGGL((k_coniss_t<STAMPS, BS>), dim3(sd.ntrees), dim3(64), lds, s, sd, cost0);
+}
 static void run_coniss(const SweepDev &sd, hipStream_t s, bool stamped, Ctx *prof) {
     const int nbk = (sd.n + 63) / 64;
     double *cost0 = sd.cost0;
     hipLaunchKernelGGL(k_seed, dim3(sd.ntrees, nbk), dim3(64), 0, s, sd, cost0);
     TP_HIP(hipGetLastError());
-    size_t lds = coniss_lds_bytes(sd.n);
+    const size_t lds = coniss_lds_bytes(sd.n);
+    const bool small = sd.n <= 4096;
     if (stamped) {
-        TP_HIP(hipFuncSetAttribute((const void *)k_coniss_t<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)lds));
-        hipLaunchKernelGGL(k_coniss_t<true>, dim3(sd.ntrees), dim3(64), lds, s, sd, (const double *)cost0);
+        if (small) launch_coniss_bs<true, 1>(sd, cost0, lds, s);
+        else launch_coniss_bs<true, 3>(sd, cost0, lds, s);
     } else {
-        TP_HIP(hipFuncSetAttribute((const void *)k_coniss, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         if (prof) kprof_begin(*prof, K_CONISS);
-        hipLaunchKernelGGL(k_coniss, dim3(sd.ntrees), dim3(64), lds, s, sd, (const double *)cost0);
+        if (small) launch_coniss_bs<false, 1>(sd, cost0, lds, s);
+        else launch_coniss_bs<false, 3>(sd, cost0, lds, s);
         if (prof) kprof_end(*prof, K_CONISS);
     }
     TP_HIP(hipGetLastError());
@@ -646,8 +652,8 @@ void launch_sweep(const SweepDev &sd, hipStream_t s, Ctx *prof) {
     if (sd.k > 64 * KMAXSLOT) fail(TP_ERR_UNSUPPORTED, "max_pcs > 256 is not supported by this build");
     if (sd.n < 3) fail(TP_ERR_NO_BSTICK, "fewer than 3 good bins: no broken-stick level");
     size_t lds = coniss_lds_bytes(sd.n);
-    if (lds > 160 * 1024 || sd.n > 64 * 64 * BSLOT)
-        fail(TP_ERR_UNSUPPORTED, "matrix too large for the LDS-resident CONISS (n > 13600)");
+    if (lds > 160 * 1024 || sd.n > 64 * 64 * 3)
+        fail(TP_ERR_UNSUPPORTED, "matrix too large for the LDS-resident CONISS (n > 10200)");
     if (sd.ntrees < 1 || sd.tree0 < 0 || sd.tree0 + sd.ntrees > sd.k) fail(TP_ERR_ARG, "bad tree range");
     size_t cnt = (size_t)sd.ntrees * sd.w_cap;
     double na;
@@ -671,8 +677,8 @@ void launch_coniss_stamped(const SweepDev &sd, hipStream_t s) { run_coniss(sd, s
 void launch_coniss_only(const SweepDev &sd, hipStream_t s) {
     if (sd.tree0 + sd.ntrees > 64 * KMAXSLOT) fail(TP_ERR_UNSUPPORTED, "more than 256 columns");
     size_t lds = coniss_lds_bytes(sd.n);
-    if (lds > 160 * 1024 || sd.n > 64 * 64 * BSLOT)
-        fail(TP_ERR_UNSUPPORTED, "matrix too large for the LDS-resident CONISS (n > 13600)");
+    if (lds > 160 * 1024 || sd.n > 64 * 64 * 3)
+        fail(TP_ERR_UNSUPPORTED, "matrix too large for the LDS-resident CONISS (n > 10200)");
     run_coniss(sd, s, false, nullptr);
 }
 

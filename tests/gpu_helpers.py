@@ -121,3 +121,16 @@ def sweep(p, min_clusters=2):
     ww = w.value
     return dict(n_cluster=nclu, scores=sc[:k * ww].reshape(ww, k).T.copy(), n_pcs=npcs.value,
                 n_clusters=ncl.value, merge=merge.reshape(2, n - 1).T.copy(), height=h)
+
+
+def eigsym(h, method=1):
+    """PCA Rayleigh-Ritz eigensolver test hook (tp_debug_eigsym)."""
+    L = _lib.load()
+    hf = np.asfortranarray(h, np.float64)
+    b = hf.shape[0]
+    theta = np.zeros(b)
+    v = np.zeros((b, b), order="F")
+    st = _st()
+    L.tp_debug_eigsym(dp(hf), B(cint(b)), B(cint(method)), dp(theta), dp(v), B(st))
+    _lib.check(st)
+    return theta, v

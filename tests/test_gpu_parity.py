@@ -119,6 +119,40 @@ def test_pca_scores(gpu, n0, k):
         assert np.abs(_proj(p, i) - _proj(op, i)).max() < 1e-7, i
 
 
+# ------------------------------------------------- Rayleigh-Ritz eigensolver
+
+def _spectrum(kind, b, rng):
+    if kind == "graded":          # like a filtered PCA block: lambda_1 / lambda_b ~ 400
+        return np.sort(np.exp(rng.uniform(np.log(2.5e-3), 0, b)))[::-1] * 1e5
+    if kind == "clustered":       # near-degenerate groups and exact repeats
+        base = np.repeat(rng.uniform(1, 100, (b + 3) // 4), 4)[:b]
+        return np.sort(base + rng.standard_normal(b) * 1e-9 * (rng.random(b) < 0.5))[::-1]
+    if kind == "rankdef":         # centred-Gram style: several exact zeros
+        ev = rng.gamma(1.0, 1.0, b) ** 2
+        ev[rng.choice(b, size=max(1, b // 8), replace=False)] = 0.0
+        return np.sort(ev)[::-1]
+    return rng.standard_normal(b)  # indefinite
+
+
+@pytest.mark.parametrize("b,kind", [(1, "graded"), (2, "indefinite"), (3, "graded"), (5, "clustered"),
+                                    (64, "graded"), (200, "rankdef"), (256, "graded"), (256, "clustered"),
+                                    (300, "graded"), (512, "graded")])
+def test_eigsym(gpu, b, kind):
+    rng = np.random.default_rng(b * 7 + len(kind))
+    ev = _spectrum(kind, b, rng)
+    q, _ = np.linalg.qr(rng.standard_normal((b, b)))
+    h = (q * ev) @ q.T
+    h = (h + h.T) / 2
+    theta, v = G.eigsym(h)
+    ref = np.linalg.eigvalsh(h)
+    scale = max(np.abs(ref).max(), 1e-300)
+    assert np.all(np.diff(theta) >= -1e-13 * scale)
+    np.testing.assert_allclose(theta, ref, atol=1e-12 * scale, rtol=0)
+    # residual and orthogonality (bars: LAPACK-level backward error)
+    assert np.abs(h @ v - v * theta).max() <= 1e-12 * scale
+    assert np.abs(v.T @ v - np.eye(b)).max() <= 1e-9
+
+
 # ---------------------------------------------------------- coniss / dist
 
 @pytest.mark.parametrize("n,c,seed", [(2, 1, 0), (3, 1, 1), (50, 1, 2), (97, 7, 3), (300, 64, 4), (300, 65, 5),

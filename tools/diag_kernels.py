@@ -49,7 +49,7 @@ def coniss(n0=2000, k=200):
                              stamps.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)), B(ms), B(st))
     _lib.check(st)
     s = stamps.reshape(k, 8)[:, :6].astype(float)
-    names = ["argmin", "links+loads", "costs", "update+refresh", "init", "bstick"]
+    names = ["links+mask+refresh+argmin", "select+prefetch", "sums+costs", "choice", "init", "bstick"]
     print(f"coniss n={n} k={k}: kernel {ms.value:.3f} ms", flush=True)
     for i in (0, 63, 127, k - 1):
         tot = s[i].sum()
@@ -64,18 +64,29 @@ def eig(b=256):
     ev = np.sort(rng.gamma(1.0, 1.0, b))[::-1] ** 4
     H = (q * ev) @ q.T
     H = np.asfortranarray((H + H.T) / 2)
-    ms = np.zeros(4); out = np.zeros(4 * b); st = ctypes.c_int(0)
+    ms = np.zeros(5); out = np.zeros(5 * b + b * b); st = ctypes.c_int(0)
     L.tp_debug_eig(H.ctypes.data_as(D), B(ctypes.c_int(b)), ms.ctypes.data_as(D), out.ctypes.data_as(D), B(st))
     _lib.check(st)
     ref = np.sort(ev)
-    for w, name in enumerate(["syevd", "syevj", "syevdj"]):
+    for w, name in enumerate(["syevd", "syevj", "syevdj", "sytrd+stedc", "custom"]):
         got = np.sort(out[w * b:(w + 1) * b])
         print(f"eig {name} b={b}: {ms[w]:.3f} ms  max|dev|/max={np.abs(got-ref).max()/ref.max():.2e}", flush=True)
+    V = out[5 * b:].reshape(b, b).T   # column-major
+    th = out[4 * b:5 * b]
+    res = np.abs(H @ V - V * th).max() / ref.max()
+    orth = np.abs(V.T @ V - np.eye(b)).max()
+    print(f"eig custom b={b}: resid/max {res:.2e}  |V'V-I| {orth:.2e}  ascending {bool(np.all(np.diff(th) >= 0))}",
+          flush=True)
 
 
 if __name__ == "__main__":
-    eig(256)
-    chol(256, 1e3)
-    chol(256, 1e10)
-    chol(480, 1e6)
-    coniss()
+    import sys
+    what = sys.argv[1:] or ["chol", "coniss"]
+    if "eig" in what:
+        eig(256)
+    if "chol" in what:
+        chol(256, 1e3)
+        chol(256, 1e10)
+        chol(480, 1e6)
+    if "coniss" in what:
+        coniss()
