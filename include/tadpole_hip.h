@@ -60,6 +60,18 @@ void tp_shutdown(void);                         /* free every device context    
 int  tp_last_error(char *buf, int len);         /* ctypes form                   */
 void tp_last_error_r(char **buf, int *len);     /* R .C form                     */
 
+/* --------------------------------------------------------------- load_mat */
+/* bigmemory::read.big.matrix(mat_file, type='double', sep='\t') (R/TADpole.R:17,
+ * :160) natively: a memory-mapped, multi-threaded parse of the headerless
+ * tab-separated matrix.  path: char** (the R .C string convention).
+ * tp_tsv_dims: rows (lines) and columns (fields of the first line).
+ * tp_read_tsv: fills out (nrow x ncol, column-major, or row-major with
+ * TP_FLAG_ROW_MAJOR); NA/NaN/empty/non-numeric -> NaN, short lines NaN-padded,
+ * long lines TP_ERR_ARG.  nthreads <= 0: all hardware threads.  Host only. */
+void tp_tsv_dims(const char **path, int *nrow, int *ncol, int *status);
+void tp_read_tsv(const char **path, const int *nrow, const int *ncol,
+                 const int *nthreads, const int *flags, double *out, int *status);
+
 /* ------------------------------------------------------------------- mask */
 /* R/TADpole.R:19-20 (NA->0, forceSymmetric(uplo='U')), :35-37 (rowMeans, diag==0,
  * quantile type 7 at bad_frac), :88-89 (subset).  M: n0 x n0.  Outputs:

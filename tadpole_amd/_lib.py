@@ -23,7 +23,7 @@ TP_FLAG_NO_MASK = 4
 EXPORTS = (
     "tp_version", "tp_device_count", "tp_shutdown", "tp_last_error", "tp_last_error_r",
     "tp_mask", "tp_cor", "tp_pca", "tp_sweep", "tp_coniss", "tp_dist", "tp_ch",
-    "tp_pipeline", "tp_pipeline_dev", "tp_sweep_dev",
+    "tp_pipeline", "tp_pipeline_dev", "tp_sweep_dev", "tp_tsv_dims", "tp_read_tsv",
 )
 
 
@@ -76,6 +76,9 @@ def load() -> ctypes.CDLL:
                               _I, _D, _I, _D, _I]
     L.tp_pipeline_dev.argtypes = [_V, _I, _I, _I, _D, _I, _I, _V, _I, _I, _I, _I, _I, _I, _I, _D, _I,
                                   _I, _I, _I, _D, _I, _D, _I]
+    _S = ctypes.POINTER(ctypes.c_char_p)
+    L.tp_tsv_dims.argtypes = [_S, _I, _I, _I]
+    L.tp_read_tsv.argtypes = [_S, _I, _I, _I, _I, _D, _I]
     L.tp_sweep_dev.argtypes = [_V, _I, _I, _I, _I, _V, _I, _I, _D, _I, _I, _I, _D, _D, _I]
     _lib = L
     return L

@@ -9,6 +9,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <rocblas/rocblas.h>
@@ -858,6 +859,27 @@ void tp_debug_eigsym(const double *H, const int *b, const int *method, double *t
         TP_HIP(hipMemcpyAsync(V, dA, (size_t)B * B * 8, hipMemcpyDeviceToHost, s));
         TP_HIP(hipStreamSynchronize(s));
         (void)rocblas_destroy_handle(h);
+    });
+}
+}  // extern "C"
+
+extern "C" {
+// ------------------------------------------------------------------ load_mat
+// bigmemory::read.big.matrix(mat_file, type = 'double', sep = '\t')
+// (R/TADpole.R:17,160) natively: path is a char** (R .C passes strings so).
+void tp_tsv_dims(const char **path, int *nrow, int *ncol, int *status) {
+    guarded(status, [&] {
+        if (!path || !*path) fail(TP_ERR_ARG, "null path");
+        tp::tsv_dims(*path, nrow, ncol);
+    });
+}
+
+void tp_read_tsv(const char **path, const int *nrow, const int *ncol, const int *nthreads, const int *flags,
+                 double *out, int *status) {
+    guarded(status, [&] {
+        if (!path || !*path || !nrow || !ncol || !out) fail(TP_ERR_ARG, "null argument");
+        const int th = (nthreads && *nthreads > 0) ? *nthreads : (int)std::max(1u, std::thread::hardware_concurrency());
+        tp::tsv_read(*path, *nrow, *ncol, th, flags && (*flags & TP_FLAG_ROW_MAJOR), out);
     });
 }
 }  // extern "C"

@@ -147,6 +147,10 @@ bool eig_sym_supported(int b);
 void eig_sym(rocblas_handle h, double *A, int b, double *theta, double *work, int *info, hipStream_t s,
              int method = 1);
 
+// tp_io.hip: native reader of read.big.matrix(sep = '\t') files (host code)
+void tsv_dims(const char *path, int *nrow, int *ncol);
+void tsv_read(const char *path, int nrow, int ncol, int nthreads, bool row_major, double *out);
+
 struct PcaStats { int iters = 0; double resid = 0; double rate = 0; int block = 0; int blocks = 0; };
 PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d_Pt,
                  double *h_sdev);
