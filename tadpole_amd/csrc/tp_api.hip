@@ -883,3 +883,31 @@ void tp_read_tsv(const char **path, const int *nrow, const int *ncol, const int 
     });
 }
 }  // extern "C"
+
+extern "C" {
+// diagnostic: k_sytrd_l time and per-phase cycles for H (b x b)
+void tp_debug_sytrd(const double *H, const int *b, double *ms, long long *stamps, int *status) {
+    guarded(status, [&] {
+        Ctx &c = ctx_for(0);
+        hipStream_t s = c.cur;
+        const int B = *b;
+        double *dA = c.buf[S_SMALL].as<double>((size_t)B * B + 64);
+        double *dWork = c.buf[S_PARTIAL].as<double>((size_t)4 * B + 64);
+        long long *dst = (long long *)c.buf[S_MISC].as<int>(64);
+        hipEvent_t e0, e1;
+        TP_HIP(hipEventCreate(&e0));
+        TP_HIP(hipEventCreate(&e1));
+        TP_HIP(hipMemcpyAsync(dA, H, (size_t)B * B * 8, hipMemcpyHostToDevice, s));
+        TP_HIP(hipEventRecord(e0, s));
+        tp::sytrd_stamped(dA, B, dWork, dst, s);
+        TP_HIP(hipEventRecord(e1, s));
+        TP_HIP(hipEventSynchronize(e1));
+        float t = 0;
+        TP_HIP(hipEventElapsedTime(&t, e0, e1));
+        *ms = t;
+        TP_HIP(hipMemcpy(stamps, dst, 3 * sizeof(long long), hipMemcpyDeviceToHost));
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+    });
+}
+}  // extern "C"

@@ -24,8 +24,17 @@ namespace tp {
 constexpr int EIG_BMAX = 512;
 constexpr int SY_WAVES = 16;
 
-template <int QM>
-__global__ void __launch_bounds__(1024) k_sytrd_l(double *A, int b, double *d, double *e, double *tau) {
+template <int QM, bool ST = false>
+__global__ void __launch_bounds__(1024) k_sytrd_l(double *A, int b, double *d, double *e, double *tau,
+                                                  long long *stamps = nullptr) {
+    long long sacc[4] = {0, 0, 0, 0};
+    long long st0 = ST ? (long long)__builtin_amdgcn_s_memtime() : 0;
+#define SY_STAMP(ph)                                                      \
+    if (ST) {                                                             \
+        long long _t = (long long)__builtin_amdgcn_s_memtime();           \
+        sacc[ph] += _t - st0;                                             \
+        st0 = _t;                                                         \
+    }
     __shared__ double V[2][EIG_BMAX], W[2][EIG_BMAX], PC[EIG_BMAX];
     __shared__ double PRW[SY_WAVES][EIG_BMAX];
     __shared__ double RED[SY_WAVES + 8];
@@ -90,6 +99,7 @@ __global__ void __launch_bounds__(1024) k_sytrd_l(double *A, int b, double *d, d
             }
         }
         __syncthreads();
+        SY_STAMP(0);
         const double tj = RED[SY_WAVES];
         // ---- (c) pass over the trailing lower triangle, columns c >= j+1:
         //      apply update j-1, accumulate p = A22 v_j
@@ -147,6 +157,7 @@ __global__ void __launch_bounds__(1024) k_sytrd_l(double *A, int b, double *d, d
 #pragma unroll
         for (int q = 0; q < QM; ++q) PRW[wv][64 * q + lane] = prow[q];
         __syncthreads();
+        SY_STAMP(1);
         // ---- (d) p = tau A22 v, alpha2 = -tau/2 p'v, w = p + alpha2 v
         double p = 0.0, pv = 0.0;
         if (t < b && t >= j + 1) {
@@ -170,7 +181,11 @@ __global__ void __launch_bounds__(1024) k_sytrd_l(double *A, int b, double *d, d
             vold[q] = V[P][64 * q + lane];
             wold[q] = W[P][64 * q + lane];
         }
+        SY_STAMP(2);
     }
+    if (ST && threadIdx.x == 0)
+        for (int q = 0; q < 3; ++q) stamps[q] = sacc[q];
+#undef SY_STAMP
     // ---- last 2 x 2 block with the pending update, T entries.  Column b-2 was
     //      left in wave 0's registers by the last pass: write it back first.
     if (wv == 0 && b >= 3) {
@@ -494,9 +509,9 @@ void eig_sym(rocblas_handle h, double *A, int b, double *theta, double *work, in
     if (!eig_sym_supported(b)) fail(TP_ERR_UNSUPPORTED, "eig_sym: b > 512");
     double *C = work, *e = C + (size_t)b * b, *tau = e + b, *dg = tau + b, *lam = dg + b;   // lam: b + 1
     if (b <= 256)
-        hipLaunchKernelGGL(k_sytrd_l<4>, dim3(1), dim3(1024), 0, s, A, b, dg, e, tau);
+        hipLaunchKernelGGL((k_sytrd_l<4, false>), dim3(1), dim3(1024), 0, s, A, b, dg, e, tau, (long long *)nullptr);
     else
-        hipLaunchKernelGGL(k_sytrd_l<8>, dim3(1), dim3(1024), 0, s, A, b, dg, e, tau);
+        hipLaunchKernelGGL((k_sytrd_l<8, false>), dim3(1), dim3(1024), 0, s, A, b, dg, e, tau, (long long *)nullptr);
     TP_HIP(hipGetLastError());
     if (method == 0) {
         TP_HIP(hipMemcpyAsync(theta, dg, (size_t)b * sizeof(double), hipMemcpyDeviceToDevice, s));
@@ -513,6 +528,17 @@ void eig_sym(rocblas_handle h, double *A, int b, double *theta, double *work, in
         hipLaunchKernelGGL(k_ormtr_l<8>, dim3((b + 3) / 4), dim3(256), 0, s, A, tau, b, C);
     TP_HIP(hipGetLastError());
     TP_HIP(hipMemcpyAsync(A, C, (size_t)b * b * sizeof(double), hipMemcpyDeviceToDevice, s));
+}
+
+// diagnostic: the tridiagonalisation alone with per-phase cycle stamps
+// (0 reflector, 1 trailing pass, 2 p/w combine), in a separate build of the kernel
+void sytrd_stamped(double *A, int b, double *work, long long *d_stamps, hipStream_t s) {
+    double *e = work, *tau = e + b, *dg = tau + b;
+    if (b <= 256)
+        hipLaunchKernelGGL((k_sytrd_l<4, true>), dim3(1), dim3(1024), 0, s, A, b, dg, e, tau, d_stamps);
+    else
+        hipLaunchKernelGGL((k_sytrd_l<8, true>), dim3(1), dim3(1024), 0, s, A, b, dg, e, tau, d_stamps);
+    TP_HIP(hipGetLastError());
 }
 
 }  // namespace tp

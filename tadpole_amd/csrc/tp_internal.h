@@ -144,6 +144,7 @@ void launch_transpose(const double *d_A, int rows, int cols, int lda, double *d_
 // triangle) <- eigenvectors, theta <- ascending eigenvalues.  work >= b*b + 4b + 8.
 // method 0: tridiagonal stage by rocSOLVER dstedc, 1: bisection + inverse iteration.
 bool eig_sym_supported(int b);
+void sytrd_stamped(double *A, int b, double *work, long long *d_stamps, hipStream_t s);
 void eig_sym(rocblas_handle h, double *A, int b, double *theta, double *work, int *info, hipStream_t s,
              int method = 1);
 

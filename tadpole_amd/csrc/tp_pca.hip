@@ -224,10 +224,15 @@ PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d
         };
         const double target = 1e-12;
         const int max_deg = 600;
-        // phase 1: a few plain iterations, then read the spectrum estimate off the
-        // Cholesky diagonal (|U_jj| -> lambda_j in orthogonal iteration)
+        // phase 1: four plain iterations as two squared ones (Z = G (G Q), one
+        // CholQR each), then read the spectrum estimate off the Cholesky
+        // diagonal (|U_jj| -> lambda_j^2 in orthogonal iteration on G^2)
         int done = 4;
-        iterate(done);
+        for (int it = 0; it < 2; ++it) {
+            gemm_gq(Q, T);
+            gemm_gq(T, Z);
+            orth_cholqr(c, Z, Q, T, n, b, Wsm, Xinv, d_info, 1, 1e-14);
+        }
         double cut = 0.0, gk = 2.0, g1cap = 10.0;
         int mdeg = 1;
         {
@@ -235,6 +240,7 @@ PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d
             hipLaunchKernelGGL(k_diag, dim3((b + 255) / 256), dim3(256), 0, s, Wsm, b, resid);
             TP_HIP(hipMemcpyAsync(dg.data(), resid, b * sizeof(double), hipMemcpyDeviceToHost, s));
             TP_HIP(hipStreamSynchronize(s));
+            for (double &x : dg) x = std::sqrt(x);
             const double l1 = dg[0], lk = dg[k - 1], lb = dg[b - 1];
             cut = lb;
             if (cut > 0 && lk > cut && l1 >= lk) {
