@@ -52,6 +52,17 @@ def _pmc_traffic(kernel_class, n0, k):
     return None, None
 
 
+def _config_name(n0, max_pcs):
+    """BASELINE.json config this run corresponds to."""
+    if max_pcs == 200 and n0 == 2000:
+        return "C2"
+    if max_pcs == 200 and n0 == 7808:
+        return "C3 shape (chr18 @10kb)"
+    if n0 == 200:
+        return "C1 shape"
+    return "custom"
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -181,7 +192,8 @@ def main():
                "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
                "data": "synthetic (SURVEY.md §8(d) Hi-C generator, seed 20261015+2+1000*rank)",
-               "config": {"workload": f"C2: synthetic {n0}x{n0} Hi-C matrix per GPU, max_pcs={args.max_pcs}",
+               "config": {"workload": f"{_config_name(n0, args.max_pcs)}: synthetic {n0}x{n0} Hi-C matrix per GPU, "
+                                      f"max_pcs={args.max_pcs}",
                           "n0": n0, "n_good": n, "k": k, "max_pcs": args.max_pcs,
                           "parallelism": f"one matrix per GPU x{world}"},
                "roofline": roof}
