@@ -39,16 +39,20 @@ def _pmc_traffic(kernel_class, n0, k):
     the same workload.  GEMM classes share one kernel symbol: no per-class
     figure, so null."""
     import glob
-    names = {"coniss": "tp::k_coniss_t<false>", "ch": "tp::k_ch"}
-    if kernel_class not in names:
+    prefixes = {"coniss": "tp::k_coniss_t<false", "ch": "tp::k_ch"}
+    if kernel_class not in prefixes:
         return None, None
     for path in sorted(glob.glob(os.path.join(HERE, "profiles", "*_traffic.json")), reverse=True):
         try:
             t = json.load(open(path))
         except (OSError, ValueError):
             continue
-        if t.get("n0") == n0 and t.get("k") == k and names[kernel_class] in t.get("kernels", {}):
-            return round(t["kernels"][names[kernel_class]]["hbm_bytes"]), os.path.relpath(path, HERE)
+        if t.get("n0") != n0 or t.get("k") != k:
+            continue
+        for name, rec in t.get("kernels", {}).items():
+            if name == prefixes[kernel_class] or name.startswith(prefixes[kernel_class] + ",") or \
+                    name.startswith(prefixes[kernel_class] + ">"):
+                return round(rec["hbm_bytes"]), os.path.relpath(path, HERE)
     return None, None
 
 
