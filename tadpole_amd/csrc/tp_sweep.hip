@@ -147,18 +147,28 @@ __device__ __forceinline__ double ward_part(const double (&sa)[NS], double fa, c
 }
 
 // One tree's CONISS with NS = ld(i) / 64 column slots per lane and BS block-
-// minimum slots per lane (n <= 4096 BS).
+// minimum slots per lane (n <= 4096 BS), on two waves of one workgroup (two
+// SIMDs) that run the two independent halves of every merge concurrently:
+//   wave A (structure): LDS costs/links, masking, block-minimum refresh, the
+//     speculative argmin a2 and the descriptions of the three possible next
+//     merges; after barrier X only the choice among them;
+//   wave B (sums): the rows in registers, merged sums, Ward costs cl/cr, merge
+//     records and heights; after X the prefetch of a2's rows.
+// Same merges and arithmetic as the oracle (bit-identical).
 //
 // Speculative prefetch.  After merge s (pair a|b -> m at a) the next merge is
 // one of exactly three: the smallest cost among positions merge s does not
-// touch (a2, found with ls/a/b masked out), ls|m (new cost cl) or m|r (new
-// cost cr).  The rows each of them needs are loaded during merge s:
-//   a2:   rows a2, b2, ls2, r2 (one that is m comes from registers)
-//   ls|m: sl, sm, row(ll), sr        m|r: sm, sr, sl, row(rr)
-// and the choice among them is applied at the next merge, after its own
-// structural work, so the loads have a whole merge to land.
+// touch (a2, found with ls/a/b masked out), ls|m (new cost cl) or m|r (new cost
+// cr).  Their rows are loaded during merge s -- rows a2, b2, ls2, r2 (one that is
+// m comes from registers) for a2; sl, sm, row(ll), sr for ls|m; sm, sr, sl,
+// row(rr) for m|r -- and the choice is applied at the next merge.
+//
+// Mailbox words in LDS: a2's row starts (A -> B before X), cl/cr (B -> A
+// before X), the chosen next merge and its cost (A -> B before barrier Y); the
+// three candidates are described in A's registers before X, so after X A only
+// chooses.  Every lane of the writing wave writes the same value.
 template <bool STAMPS, int NS, int BS>
-__device__ __forceinline__ void coniss_tree(const SweepDev &sd, const double *cost0, double *lds) {
+__device__ __forceinline__ void coniss_tree2(const SweepDev &sd, const double *cost0, double *lds) {
     long long st_acc[6] = {0, 0, 0, 0, 0, 0};
     long long st_t0 = STAMPS ? (long long)__builtin_amdgcn_s_memtime() : 0;
 #define TP_STAMP(ph)                                                      \
@@ -168,15 +178,21 @@ __device__ __forceinline__ void coniss_tree(const SweepDev &sd, const double *co
         st_t0 = _t;                                                       \
     }
     const int n = sd.n;
-    const int ti = blockIdx.x;                 // tree slot
-    const int i = sd.tree0 + ti + 1;           // PC prefix length
+    const int ti = blockIdx.x;
+    const int i = sd.tree0 + ti + 1;
     constexpr int ld = NS * 64;
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const bool waveA = __builtin_amdgcn_readfirstlane((int)threadIdx.x) < 64;   // wave-uniform: a scalar branch
     const int nbk = (n + 63) / 64;
     const double QNAN = __longlong_as_double(0x7FF8000000000000LL);
-    double *cost = lds;                        // nbk*64: NaN = not a candidate
-    int *link = (int *)(cost + nbk * 64);      // n: cluster start <-> end
-    int *rn = link + n;                        // n: end of the right neighbour (at cluster starts)
+    double *cost = lds;
+    int *link = (int *)(cost + nbk * 64);
+    int *rn = link + n;
+    // mailbox (16-byte aligned): mbd[0..1] = cl, cr (B -> A), mbd[2] = next cost;
+    // rec = next merge (A -> B after X), pre = a2's row starts (A -> B before X)
+    double *mbd = (double *)(((uintptr_t)(rn + n) + 15) & ~(uintptr_t)15);
+    int4 *rec4 = (int4 *)(mbd + 4);   // 3 x int4: a, b, ls, r | nm, nl, nr, lls | rrs, which, -, -
+    int4 *pre4 = rec4 + 3;            // 2 x int4: a2s, b2s, l2s, r2s | ls2, r2, -, -
     double *S = sd.sums + sums_off(n, sd.tree0, i) + lane;
     int *mrg_a = sd.mrg_a + (size_t)ti * (n - 1);
     int *mrg_b = sd.mrg_b + (size_t)ti * (n - 1);
@@ -185,26 +201,7 @@ __device__ __forceinline__ void coniss_tree(const SweepDev &sd, const double *co
     const double *c0 = cost0 + (size_t)ti * nbk * 64;
 
     double bmr[BS];
-#pragma unroll
-    for (int q = 0; q < BS; ++q) bmr[q] = QNAN;
-    for (int bk = 0; bk < nbk; ++bk) {
-        const int p = bk * 64 + lane;
-        const double cp = c0[p];
-        cost[p] = cp;
-        if (p < n) {
-            link[p] = p;
-            rn[p] = p + 1 < n ? p + 1 : -1;
-        }
-        const double m = wave_min(cp);
-        if (lane == (bk & 63)) {
-#pragma unroll
-            for (int q = 0; q < BS; ++q)
-                if (q == (bk >> 6)) bmr[q] = m;
-        }
-    }
-    __syncthreads();
-
-    auto argmin_pos = [&](double vmin) -> int {   // leftmost position holding vmin (-1: none)
+    auto argmin_pos = [&](double vmin) -> int {
         if (isnan(vmin)) return -1;
         int blk = 0;
 #pragma unroll
@@ -215,163 +212,231 @@ __device__ __forceinline__ void coniss_tree(const SweepDev &sd, const double *co
         const unsigned long long mp = __ballot(cost[blk * 64 + lane] == vmin);
         return blk * 64 + (int)__builtin_ctzll(mp);
     };
-    auto load_row = [&](double (&dst)[NS], int start) {
-        const double *pr = S + (size_t)start * ld;
-#pragma unroll
-        for (int t = 0; t < NS; ++t) dst[t] = pr[64 * t];
-    };
     auto gmin = [&]() {
         double g = bmr[0];
 #pragma unroll
         for (int q = 1; q < BS; ++q) g = vmin(g, bmr[q]);
         return wave_min(g);
     };
-    // ---- the first merge; its rows enter as a "which = 0" prefetch
-    double c = gmin();
-    int a = argmin_pos(c);
+    auto load_row = [&](double (&dst)[NS], int start) {
+        const double *pr = S + (size_t)start * ld;
+#pragma unroll
+        for (int t = 0; t < NS; ++t) dst[t] = pr[64 * t];
+    };
+    // A: a merge described by (a, ea, eb, ls, r, er); b = ea + 1; ll = start of
+    // the cluster left of ls (its ls|m successor's left row)
+    struct Mg {
+        int a, ea, eb, ls, r, er, ll;
+    };
+    auto merge_at = [&](int p) {   // current links -> the merge of the pair starting at p
+        Mg m;
+        m.a = p;
+        m.ea = link[p];
+        m.eb = rn[p];
+        m.ls = p > 0 ? link[p - 1] : -1;
+        m.r = m.eb >= 0 && m.eb + 1 < n ? m.eb + 1 : -1;
+        m.er = m.r >= 0 ? rn[m.ea + 1] : -1;
+        m.ll = m.ls > 0 ? link[m.ls - 1] : -1;
+        return m;
+    };
+    auto publish = [&](const Mg &m, int which) {   // A -> B: the next merge
+        const int rr = (m.r >= 0 && m.er + 1 < n) ? m.er + 1 : -1;
+        rec4[0] = make_int4(m.a, m.ea + 1 < n ? m.ea + 1 : m.a, m.ls, m.r);
+        rec4[1] = make_int4(m.eb - m.a + 1, m.ls >= 0 ? m.a - m.ls : 0, m.r >= 0 ? m.er - m.r + 1 : 0,
+                            m.ll >= 0 ? m.ll : m.a);
+        rec4[2] = make_int4(rr >= 0 ? rr : m.a, which, 0, 0);
+    };
+    Mg cur = {0, 0, 0, -1, -1, -1, -1};
+    double c = 0.0, pcl = QNAN, pcr = QNAN;
+    int pls = -1, pa_ = 0;   // A: the previous merge's new costs, applied at the next merge's start
+    if (waveA) {
+#pragma unroll
+        for (int q = 0; q < BS; ++q) bmr[q] = QNAN;
+        for (int bk = 0; bk < nbk; ++bk) {
+            const int p = bk * 64 + lane;
+            const double cp = c0[p];
+            cost[p] = cp;
+            if (p < n) {
+                link[p] = p;
+                rn[p] = p + 1 < n ? p + 1 : -1;
+            }
+            const double m = wave_min(cp);
+            if (lane == (bk & 63)) {
+#pragma unroll
+                for (int q = 0; q < BS; ++q)
+                    if (q == (bk >> 6)) bmr[q] = m;
+            }
+        }
+        c = gmin();
+        cur = merge_at(argmin_pos(c));
+        publish(cur, 0);
+        mbd[2] = c;
+    }
+    __syncthreads();
+    // B's registers
     double pa[NS], pb[NS], pl[NS], pr[NS], pll[NS], prr[NS], sl[NS], sr[NS], sm[NS];
-    int which = 0, ls2p, r2p, aprev = -1;
-    {
-        const int ea = link[a], eb = rn[a];
-        const int ls = a > 0 ? link[a - 1] : -1;
-        const int r = eb + 1 < n ? eb + 1 : -1;
-        load_row(pa, a);
-        load_row(pb, ea + 1);
-        load_row(pl, ls >= 0 ? ls : a);
-        load_row(pr, r >= 0 ? r : a);
-        ls2p = ls;
-        r2p = r;
+    int ls2p = -1, r2p = -1, aprev = -1;
+    double h = 0.0;
+    if (!waveA) {
+        const int4 r0 = rec4[0];
+        load_row(pa, r0.x);
+        load_row(pb, r0.y);
+        load_row(pl, r0.z >= 0 ? r0.z : r0.x);
+        load_row(pr, r0.w >= 0 ? r0.w : r0.x);
+        ls2p = r0.z;
+        r2p = r0.w;
 #pragma unroll
         for (int t = 0; t < NS; ++t) pll[t] = prr[t] = sl[t] = sr[t] = sm[t] = 0.0;
     }
     TP_STAMP(4);
 
-    double h = 0.0;
     for (int s = 0; s < n - 1; ++s) {
-        // ---- (1) links of the merge a|b
-        const int ea = link[a];
-        const int eb = rn[a];
-        const int ls = a > 0 ? link[a - 1] : -1;
-        const int b = ea + 1;
-        const int r = eb + 1 < n ? eb + 1 : -1;
-        const int er = r >= 0 ? rn[b] : -1;
-        const int na = ea - a + 1, nbb = eb - b + 1, nm = na + nbb;
-        const int nl = ls >= 0 ? a - ls : 0, nr = r >= 0 ? er - r + 1 : 0;
-        // ---- (2) structure update; ls, a, b masked out; speculative argmin
-        link[a] = eb;
-        link[eb] = a;
-        rn[a] = er;
-        cost[b] = QNAN;
-        cost[a] = QNAN;
-        if (ls >= 0) {
-            cost[ls] = QNAN;
-            rn[ls] = eb;
-        }
-        const int ba = a >> 6, bb = b >> 6, bl = ls >= 0 ? (ls >> 6) : ba;
-        {
-            const double ma = wave_min(cost[ba * 64 + lane]);
-            const double mb = bb != ba ? wave_min(cost[bb * 64 + lane]) : ma;
-            const double ml = (bl != ba && bl != bb) ? wave_min(cost[bl * 64 + lane]) : ma;
+        if (waveA) {
+            // ---- the previous merge's new costs, then this merge's structure
+            //      update with ls, a, b masked, refresh, speculative argmin
+            const int a = cur.a, eb = cur.eb, ls = cur.ls, b = cur.ea + 1, r = cur.r, er = cur.er;
+            if (s > 0) {
+                if (pls >= 0) cost[pls] = pcl;
+                cost[pa_] = pcr;
+            }
+            link[a] = eb;
+            link[eb] = a;
+            rn[a] = er;
+            cost[b] = QNAN;
+            cost[a] = QNAN;
+            if (ls >= 0) {
+                cost[ls] = QNAN;
+                rn[ls] = eb;
+            }
+            const int ba = a >> 6, bb = b >> 6, bl = ls >= 0 ? (ls >> 6) : ba;
+            {
+                const double ma = wave_min(cost[ba * 64 + lane]);
+                const double mb = bb != ba ? wave_min(cost[bb * 64 + lane]) : ma;
+                const double ml = (bl != ba && bl != bb) ? wave_min(cost[bl * 64 + lane]) : ma;
+#pragma unroll
+                for (int q = 0; q < BS; ++q) {
+                    if (lane == (ba & 63) && q == (ba >> 6)) bmr[q] = ma;
+                    if (bb != ba && lane == (bb & 63) && q == (bb >> 6)) bmr[q] = mb;
+                    if (bl != ba && bl != bb && lane == (bl & 63) && q == (bl >> 6)) bmr[q] = ml;
+                }
+            }
+            const double v2 = gmin();
+            const int a2 = argmin_pos(v2);
+            // ---- the three possible next merges (post-update links)
+            const Mg m0 = merge_at(a2 >= 0 ? a2 : a);
+            Mg m1;   // ls | m
+            m1.a = ls; m1.ea = a - 1; m1.eb = eb; m1.ls = cur.ll; m1.r = r; m1.er = er;
+            m1.ll = m1.ls > 0 ? link[m1.ls - 1] : -1;
+            Mg m2;   // m | r
+            m2.a = a; m2.ea = eb; m2.eb = er; m2.ls = ls;
+            m2.r = (r >= 0 && er + 1 < n) ? er + 1 : -1;
+            m2.er = m2.r >= 0 ? rn[r] : -1;
+            m2.ll = cur.ll;
+            pre4[0] = make_int4(m0.a, m0.ea + 1 < n ? m0.ea + 1 : a, m0.ls >= 0 ? m0.ls : a, m0.r >= 0 ? m0.r : a);
+            pre4[1] = make_int4(m0.ls, m0.r, 0, 0);
+            TP_STAMP(0);
+            __syncthreads();   // X
+            TP_STAMP(1);
+            // ---- the choice: lexicographic (cost, position) minimum
+            const double cl = mbd[0], cr = mbd[1];
+            double nv = v2;
+            int np = a2;
+            int which = 0;
+            if (ls >= 0 && (np < 0 || cl < nv || (cl == nv && ls < np))) { nv = cl; np = ls; which = 1; }
+            if (r >= 0 && (np < 0 || cr < nv || (cr == nv && a < np))) { nv = cr; np = a; which = 2; }
+            cur = which == 0 ? m0 : (which == 1 ? m1 : m2);
+            c = nv;
+            publish(cur, which);
+            mbd[2] = nv;
+            // block minima absorb the new costs now (the LDS words follow at the
+            // next merge's start, before its refresh reads them)
 #pragma unroll
             for (int q = 0; q < BS; ++q) {
-                if (lane == (ba & 63) && q == (ba >> 6)) bmr[q] = ma;
-                if (bb != ba && lane == (bb & 63) && q == (bb >> 6)) bmr[q] = mb;
-                if (bl != ba && bl != bb && lane == (bl & 63) && q == (bl >> 6)) bmr[q] = ml;
+                if (lane == (ba & 63) && q == (ba >> 6)) bmr[q] = vmin(bmr[q], cr);
+                if (ls >= 0 && lane == (bl & 63) && q == (bl >> 6)) bmr[q] = vmin(bmr[q], cl);
             }
-        }
-        const double v2 = gmin();
-        const int a2 = argmin_pos(v2);
-        TP_STAMP(0);
-        // ---- (3a) this merge's rows from the previous merge's prefetch
-        double sa[NS], sb[NS];
-        if (which == 0) {
+            pcl = cl;
+            pcr = cr;
+            pls = ls;
+            pa_ = a;
+            TP_STAMP(2);
+            __syncthreads();   // Y
+            TP_STAMP(3);
+        } else {
+            // ---- this merge's rows from the previous merge's prefetch
+            const int4 q0 = rec4[0], q1 = rec4[1], q2 = rec4[2];
+            const int a_ = q0.x, b_ = q0.y, ls_ = q0.z, r_ = q0.w;
+            const int nm = q1.x, nl = q1.y, nr = q1.z, lls = q1.w;
+            const int rrs = q2.x, which = q2.y;
+            const double cc = mbd[2];
+            double sa[NS], sb[NS];
+            if (which == 0) {
+#pragma unroll
+                for (int t = 0; t < NS; ++t) {
+                    sa[t] = pa[t];
+                    sb[t] = pb[t];
+                    sl[t] = ls2p == aprev ? sm[t] : pl[t];
+                    sr[t] = r2p == aprev ? sm[t] : pr[t];
+                }
+            } else if (which == 1) {   // ls | m
+#pragma unroll
+                for (int t = 0; t < NS; ++t) {
+                    sa[t] = sl[t];
+                    sb[t] = sm[t];
+                    sl[t] = pll[t];
+                }
+            } else {                   // m | r
+#pragma unroll
+                for (int t = 0; t < NS; ++t) {
+                    sa[t] = sm[t];
+                    sb[t] = sr[t];
+                    sr[t] = prr[t];
+                }
+            }
+            // rows the ls|m and m|r candidates of the next merge need
+            load_row(pll, lls);
+            load_row(prr, rrs);
 #pragma unroll
             for (int t = 0; t < NS; ++t) {
-                sa[t] = pa[t];
-                sb[t] = pb[t];
-                sl[t] = ls2p == aprev ? sm[t] : pl[t];
-                sr[t] = r2p == aprev ? sm[t] : pr[t];
+                sm[t] = sa[t] + sb[t];
+                S[(size_t)a_ * ld + 64 * t] = sm[t];
             }
-        } else if (which == 1) {   // ls | m
-#pragma unroll
-            for (int t = 0; t < NS; ++t) {
-                sa[t] = sl[t];
-                sb[t] = sm[t];
-                sl[t] = pll[t];
+            const double fm = (double)nm, fl = (double)nl, fr = (double)nr;
+            double ul = ward_part<NS>(sl, fl, sm, fm);
+            double ur = ward_part<NS>(sm, fm, sr, fr);
+            wave_sum2(ul, ur);
+            const double cl = ls_ >= 0 ? nan2inf(ul / (fl * fm * (fl + fm))) : QNAN;
+            const double cr = r_ >= 0 ? nan2inf(ur / (fm * fr * (fm + fr))) : QNAN;
+            h = h + cc;
+            mbd[0] = cl;
+            mbd[1] = cr;
+            if (lane == 0) {
+                mrg_a[s] = a_;
+                mrg_b[s] = b_;
+                mcost[s] = cc;
+                height[s] = h;
             }
-        } else {                   // m | r
-#pragma unroll
-            for (int t = 0; t < NS; ++t) {
-                sa[t] = sm[t];
-                sb[t] = sr[t];
-                sr[t] = prr[t];
-            }
+            __syncthreads();   // X
+            // ---- prefetch a2's rows for the next merge
+            const int4 p0 = pre4[0], p1 = pre4[1];
+            load_row(pa, p0.x);
+            load_row(pb, p0.y);
+            load_row(pl, p0.z);
+            load_row(pr, p0.w);
+            ls2p = p1.x;
+            r2p = p1.y;
+            aprev = a_;
+            __syncthreads();   // Y
         }
-        // ---- (3b) prefetch the next merge's candidates (post-merge links)
-        const int a2s = a2 >= 0 ? a2 : a;
-        const int b2 = link[a2s] + 1;
-        const int ls2 = a2s > 0 ? link[a2s - 1] : -1;
-        const int e2 = rn[a2s];
-        const int r2 = (e2 >= 0 && e2 + 1 < n) ? e2 + 1 : -1;
-        const int ll = ls > 0 ? link[ls - 1] : -1;
-        const int rr = (r >= 0 && er + 1 < n) ? er + 1 : -1;
-        load_row(pa, a2s);
-        load_row(pb, b2 < n ? b2 : a);
-        load_row(pl, ls2 >= 0 ? ls2 : a);
-        load_row(pr, r2 >= 0 ? r2 : a);
-        load_row(pll, ll >= 0 ? ll : a);
-        load_row(prr, rr >= 0 ? rr : a);
-        TP_STAMP(1);
-        // ---- (4) merged sums, merge record
-#pragma unroll
-        for (int t = 0; t < NS; ++t) {
-            sm[t] = sa[t] + sb[t];
-            S[(size_t)a * ld + 64 * t] = sm[t];
-        }
-        if (lane == 0) {
-            mrg_a[s] = a;
-            mrg_b[s] = b;
-            mcost[s] = c;
-        }
-        // ---- (5) the two new adjacent costs (division-free Ward form), paired
-        const double fm = (double)nm, fl = (double)nl, fr = (double)nr;
-        double ul = ward_part<NS>(sl, fl, sm, fm);
-        double ur = ward_part<NS>(sm, fm, sr, fr);
-        wave_sum2(ul, ur);
-        const double cl = ls >= 0 ? nan2inf(ul / (fl * fm * (fl + fm))) : QNAN;
-        const double cr = r >= 0 ? nan2inf(ur / (fm * fr * (fm + fr))) : QNAN;
-        h = h + c;
-        if (lane == 0) height[s] = h;
-        TP_STAMP(2);
-        // ---- (6) new costs in, next merge: lexicographic (cost, position)
-        //      minimum of the three candidates
-        cost[a] = cr;                     // QNAN when there is no right neighbour
-        if (ls >= 0) cost[ls] = cl;
-#pragma unroll
-        for (int q = 0; q < BS; ++q) {
-            if (lane == (ba & 63) && q == (ba >> 6)) bmr[q] = vmin(bmr[q], cr);
-            if (ls >= 0 && lane == (bl & 63) && q == (bl >> 6)) bmr[q] = vmin(bmr[q], cl);
-        }
-        double nv = v2;
-        int np = a2;
-        which = 0;
-        if (ls >= 0 && (np < 0 || cl < nv || (cl == nv && ls < np))) { nv = cl; np = ls; which = 1; }
-        if (r >= 0 && (np < 0 || cr < nv || (cr == nv && a < np))) { nv = cr; np = a; which = 2; }
-        ls2p = ls2;
-        r2p = r2;
-        aprev = a;
-        a = np;
-        c = nv;
-        TP_STAMP(3);
     }
-
+    __syncthreads();
     // ---- broken stick (rioja bstick.chclust, vegan bstick.default) on heights
-    if (lane == 0) {
+    if (threadIdx.x == 0) {
         const int nobj = n - 1;
         int ncl = -1;
         if (nobj >= 2) {
             const double tot = height[nobj - 1];
-            double *cs = cost;   // reuse: cs[t], t = 1..nobj  (n entries)
+            double *cs = cost;
             double hi = 0.0, lo = 0.0;
             for (int t = 1; t <= nobj; ++t) {
                 dd_add_d(hi, lo, tot / (double)(nobj - t + 1));
@@ -390,21 +455,21 @@ __device__ __forceinline__ void coniss_tree(const SweepDev &sd, const double *co
         sd.n_cluster[ti] = ncl;
     }
     TP_STAMP(5);
-    if (STAMPS && lane == 0)
+    if (STAMPS && threadIdx.x == 0)
         for (int q = 0; q < 6; ++q) sd.stamps[(size_t)ti * 8 + q] = st_acc[q];
 #undef TP_STAMP
 }
 
-// STAMPS: diagnostic build (see coniss_tree).  BS: block-minimum slots (n <= 4096 BS).
+// STAMPS: diagnostic build (see coniss_tree2).  BS: block-minimum slots (n <= 4096 BS).
 template <bool STAMPS, int BS>
-__global__ void __launch_bounds__(64) k_coniss_t(SweepDev sd, const double *cost0) {
+__global__ void __launch_bounds__(128) k_coniss_t(SweepDev sd, const double *cost0) {
     extern __shared__ double lds[];
     const int i = sd.tree0 + blockIdx.x + 1;
     switch ((i + 63) / 64) {
-        case 1: coniss_tree<STAMPS, 1, BS>(sd, cost0, lds); break;
-        case 2: coniss_tree<STAMPS, 2, BS>(sd, cost0, lds); break;
-        case 3: coniss_tree<STAMPS, 3, BS>(sd, cost0, lds); break;
-        default: coniss_tree<STAMPS, 4, BS>(sd, cost0, lds); break;
+        case 1: coniss_tree2<STAMPS, 1, BS>(sd, cost0, lds); break;
+        case 2: coniss_tree2<STAMPS, 2, BS>(sd, cost0, lds); break;
+        case 3: coniss_tree2<STAMPS, 3, BS>(sd, cost0, lds); break;
+        default: coniss_tree2<STAMPS, 4, BS>(sd, cost0, lds); break;
     }
 }
 template __global__ void k_coniss_t<false, 1>(SweepDev, const double *);
@@ -617,9 +682,9 @@ __global__ void k_fill(double *p, size_t cnt, double v) {
     if (t < cnt) p[t] = v;
 }
 
-static size_t coniss_lds_bytes(int n) {
+static size_t coniss_lds_bytes(int n) {   // costs, links, right ends, mailbox
     size_t nbk = (n + 63) / 64;
-    return nbk * 64 * 8 + (size_t)n * 8 + 16;
+    return nbk * 64 * 8 + (size_t)n * 8 + 16 + 32 + 5 * 16;
 }
 
 // seed kernel + CONISS (cost0 = initial adjacent costs, ntrees x nbk*64)
@@ -627,7 +692,7 @@ template <bool STAMPS, int BS>
 static void launch_coniss_bs(const SweepDev &sd, const double *cost0, size_t lds, hipStream_t s) {
     TP_HIP(hipFuncSetAttribute((const void *)k_coniss_t<STAMPS, BS>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)lds));
-    hipLaunchKernelGGL((k_coniss_t<STAMPS, BS>), dim3(sd.ntrees), dim3(64), lds, s, sd, cost0);
+    hipLaunchKernelGGL((k_coniss_t<STAMPS, BS>), dim3(sd.ntrees), dim3(128), lds, s, sd, cost0);
 }
 static void run_coniss(const SweepDev &sd, hipStream_t s, bool stamped, Ctx *prof) {
     const int nbk = (sd.n + 63) / 64;

@@ -49,7 +49,7 @@ def coniss(n0=2000, k=200):
                              stamps.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)), B(ms), B(st))
     _lib.check(st)
     s = stamps.reshape(k, 8)[:, :6].astype(float)
-    names = ["links+mask+refresh+argmin", "select+prefetch", "sums+costs", "choice", "init", "bstick"]
+    names = ["A:mask+refresh+argmin", "A:wait X", "A:choice+links", "A:wait Y", "init", "bstick"]
     print(f"coniss n={n} k={k}: kernel {ms.value:.3f} ms", flush=True)
     for i in (0, 63, 127, k - 1):
         tot = s[i].sum()
