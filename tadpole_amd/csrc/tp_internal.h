@@ -127,7 +127,9 @@ struct SweepDev {
     long long *stamps = nullptr;   // diagnostic builds only (k_coniss_t<true>)
     double *cost0 = nullptr;       // ntrees x roundup(n, 64) initial costs (scratch)
 };
-inline size_t sweep_cost0_doubles(int n, int ntrees) { return (size_t)ntrees * ((n + 63) / 64) * 64; }
+// initial costs (ntrees x roundup(n, 64)) + link scratch of the global-memory
+// CONISS variant (ntrees x 2n ints)
+inline size_t sweep_cost0_doubles(int n, int ntrees) { return (size_t)ntrees * (((n + 63) / 64) * 64 + n); }
 size_t sweep_sums_doubles(int n, int tree0, int ntrees);
 void blas_shutdown_all();
 void launch_sweep(const SweepDev &sd, hipStream_t s, Ctx *prof = nullptr);

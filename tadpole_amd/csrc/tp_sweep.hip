@@ -167,8 +167,8 @@ __device__ __forceinline__ double ward_part(const double (&sa)[NS], double fa, c
 // before X), the chosen next merge and its cost (A -> B before barrier Y); the
 // three candidates are described in A's registers before X, so after X A only
 // chooses.  Every lane of the writing wave writes the same value.
-template <bool STAMPS, int NS, int BS>
-__device__ __forceinline__ void coniss_tree2(const SweepDev &sd, const double *cost0, double *lds) {
+template <bool STAMPS, int NS, int BS, bool GLB>
+__device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, double *lds) {
     long long st_acc[6] = {0, 0, 0, 0, 0, 0};
     long long st_t0 = STAMPS ? (long long)__builtin_amdgcn_s_memtime() : 0;
 #define TP_STAMP(ph)                                                      \
@@ -185,12 +185,15 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, const double *c
     const bool waveA = __builtin_amdgcn_readfirstlane((int)threadIdx.x) < 64;   // wave-uniform: a scalar branch
     const int nbk = (n + 63) / 64;
     const double QNAN = __longlong_as_double(0x7FF8000000000000LL);
-    double *cost = lds;
-    int *link = (int *)(cost + nbk * 64);
+    // GLB (n above the LDS capacity): costs stay in this tree's slice of cost0
+    // and links in global scratch behind cost0 (L2 / MALL resident); only the
+    // mailbox is in LDS.  Same code path otherwise.
+    double *cost = GLB ? cost0 + (size_t)ti * nbk * 64 : lds;
+    int *link = GLB ? (int *)(cost0 + (size_t)sd.ntrees * nbk * 64) + (size_t)ti * 2 * n : (int *)(cost + nbk * 64);
     int *rn = link + n;
     // mailbox (16-byte aligned): mbd[0..1] = cl, cr (B -> A), mbd[2] = next cost;
     // rec = next merge (A -> B after X), pre = a2's row starts (A -> B before X)
-    double *mbd = (double *)(((uintptr_t)(rn + n) + 15) & ~(uintptr_t)15);
+    double *mbd = GLB ? lds : (double *)(((uintptr_t)(rn + n) + 15) & ~(uintptr_t)15);
     int4 *rec4 = (int4 *)(mbd + 4);   // 3 x int4: a, b, ls, r | nm, nl, nr, lls | rrs, which, -, -
     int4 *pre4 = rec4 + 3;            // 2 x int4: a2s, b2s, l2s, r2s | ls2, r2, -, -
     double *S = sd.sums + sums_off(n, sd.tree0, i) + lane;
@@ -255,7 +258,7 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, const double *c
         for (int bk = 0; bk < nbk; ++bk) {
             const int p = bk * 64 + lane;
             const double cp = c0[p];
-            cost[p] = cp;
+            if (!GLB) cost[p] = cp;
             if (p < n) {
                 link[p] = p;
                 rn[p] = p + 1 < n ? p + 1 : -1;
@@ -461,21 +464,23 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, const double *c
 }
 
 // STAMPS: diagnostic build (see coniss_tree2).  BS: block-minimum slots (n <= 4096 BS).
-template <bool STAMPS, int BS>
-__global__ void __launch_bounds__(128) k_coniss_t(SweepDev sd, const double *cost0) {
+template <bool STAMPS, int BS, bool GLB>
+__global__ void __launch_bounds__(128) k_coniss_t(SweepDev sd, double *cost0) {
     extern __shared__ double lds[];
     const int i = sd.tree0 + blockIdx.x + 1;
     switch ((i + 63) / 64) {
-        case 1: coniss_tree2<STAMPS, 1, BS>(sd, cost0, lds); break;
-        case 2: coniss_tree2<STAMPS, 2, BS>(sd, cost0, lds); break;
-        case 3: coniss_tree2<STAMPS, 3, BS>(sd, cost0, lds); break;
-        default: coniss_tree2<STAMPS, 4, BS>(sd, cost0, lds); break;
+        case 1: coniss_tree2<STAMPS, 1, BS, GLB>(sd, cost0, lds); break;
+        case 2: coniss_tree2<STAMPS, 2, BS, GLB>(sd, cost0, lds); break;
+        case 3: coniss_tree2<STAMPS, 3, BS, GLB>(sd, cost0, lds); break;
+        default: coniss_tree2<STAMPS, 4, BS, GLB>(sd, cost0, lds); break;
     }
 }
-template __global__ void k_coniss_t<false, 1>(SweepDev, const double *);
-template __global__ void k_coniss_t<false, 3>(SweepDev, const double *);
-template __global__ void k_coniss_t<true, 1>(SweepDev, const double *);
-template __global__ void k_coniss_t<true, 3>(SweepDev, const double *);
+template __global__ void k_coniss_t<false, 1, false>(SweepDev, double *);
+template __global__ void k_coniss_t<false, 3, false>(SweepDev, double *);
+template __global__ void k_coniss_t<false, 16, true>(SweepDev, double *);
+template __global__ void k_coniss_t<true, 1, false>(SweepDev, double *);
+template __global__ void k_coniss_t<true, 3, false>(SweepDev, double *);
+template __global__ void k_coniss_t<true, 16, true>(SweepDev, double *);
 
 // ------------------------------------------------------------ CH over cuts
 // canonical segment statistics of rows s..e, by one wave (see tpo_seg_ss)
@@ -686,39 +691,44 @@ static size_t coniss_lds_bytes(int n) {   // costs, links, right ends, mailbox
     size_t nbk = (n + 63) / 64;
     return nbk * 64 * 8 + (size_t)n * 8 + 16 + 32 + 5 * 16;
 }
+constexpr size_t kConissGlbLds = 16 + 32 + 5 * 16;   // mailbox only
+constexpr int kConissMaxN = 64 * 64 * 16;             // global variant: 16 block-minimum slots
+static bool coniss_in_lds(int n) { return coniss_lds_bytes(n) <= 160 * 1024 && n <= 64 * 64 * 3; }
 
-// seed kernel + CONISS (cost0 = initial adjacent costs, ntrees x nbk*64)
-template <bool STAMPS, int BS>
-static void launch_coniss_bs(const SweepDev &sd, const double *cost0, size_t lds, hipStream_t s) {
-    TP_HIP(hipFuncSetAttribute((const void *)k_coniss_t<STAMPS, BS>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)lds));
-    hipLaunchKernelGGL((k_coniss_t<STAMPS, BS>), dim3(sd.ntrees), dim3(128), lds, s, sd, cost0);
+// seed kernel + CONISS (cost0 = initial adjacent costs, ntrees x nbk*64, then
+// the global-variant link scratch: see sweep_cost0_doubles)
+template <bool STAMPS, int BS, bool GLB>
+static void launch_coniss_bs(const SweepDev &sd, double *cost0, size_t lds, hipStream_t s) {
+    TP_HIP(hipFuncSetAttribute((const void *)k_coniss_t<STAMPS, BS, GLB>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL((k_coniss_t<STAMPS, BS, GLB>), dim3(sd.ntrees), dim3(128), lds, s, sd, cost0);
 }
 static void run_coniss(const SweepDev &sd, hipStream_t s, bool stamped, Ctx *prof) {
     const int nbk = (sd.n + 63) / 64;
     double *cost0 = sd.cost0;
     hipLaunchKernelGGL(k_seed, dim3(sd.ntrees, nbk), dim3(64), 0, s, sd, cost0);
     TP_HIP(hipGetLastError());
-    const size_t lds = coniss_lds_bytes(sd.n);
+    const bool in_lds = coniss_in_lds(sd.n);
+    const size_t lds = in_lds ? coniss_lds_bytes(sd.n) : kConissGlbLds;
     const bool small = sd.n <= 4096;
+    if (!stamped && prof) kprof_begin(*prof, K_CONISS);
     if (stamped) {
-        if (small) launch_coniss_bs<true, 1>(sd, cost0, lds, s);
-        else launch_coniss_bs<true, 3>(sd, cost0, lds, s);
+        if (!in_lds) launch_coniss_bs<true, 16, true>(sd, cost0, lds, s);
+        else if (small) launch_coniss_bs<true, 1, false>(sd, cost0, lds, s);
+        else launch_coniss_bs<true, 3, false>(sd, cost0, lds, s);
     } else {
-        if (prof) kprof_begin(*prof, K_CONISS);
-        if (small) launch_coniss_bs<false, 1>(sd, cost0, lds, s);
-        else launch_coniss_bs<false, 3>(sd, cost0, lds, s);
-        if (prof) kprof_end(*prof, K_CONISS);
+        if (!in_lds) launch_coniss_bs<false, 16, true>(sd, cost0, lds, s);
+        else if (small) launch_coniss_bs<false, 1, false>(sd, cost0, lds, s);
+        else launch_coniss_bs<false, 3, false>(sd, cost0, lds, s);
     }
+    if (!stamped && prof) kprof_end(*prof, K_CONISS);
     TP_HIP(hipGetLastError());
 }
 
 void launch_sweep(const SweepDev &sd, hipStream_t s, Ctx *prof) {
     if (sd.k > 64 * KMAXSLOT) fail(TP_ERR_UNSUPPORTED, "max_pcs > 256 is not supported by this build");
     if (sd.n < 3) fail(TP_ERR_NO_BSTICK, "fewer than 3 good bins: no broken-stick level");
-    size_t lds = coniss_lds_bytes(sd.n);
-    if (lds > 160 * 1024 || sd.n > 64 * 64 * 3)
-        fail(TP_ERR_UNSUPPORTED, "matrix too large for the LDS-resident CONISS (n > 10200)");
+    if (sd.n > kConissMaxN) fail(TP_ERR_UNSUPPORTED, "more than 65536 bins per matrix");
     if (sd.ntrees < 1 || sd.tree0 < 0 || sd.tree0 + sd.ntrees > sd.k) fail(TP_ERR_ARG, "bad tree range");
     size_t cnt = (size_t)sd.ntrees * sd.w_cap;
     double na;
@@ -741,9 +751,7 @@ void launch_coniss_stamped(const SweepDev &sd, hipStream_t s) { run_coniss(sd, s
 
 void launch_coniss_only(const SweepDev &sd, hipStream_t s) {
     if (sd.tree0 + sd.ntrees > 64 * KMAXSLOT) fail(TP_ERR_UNSUPPORTED, "more than 256 columns");
-    size_t lds = coniss_lds_bytes(sd.n);
-    if (lds > 160 * 1024 || sd.n > 64 * 64 * 3)
-        fail(TP_ERR_UNSUPPORTED, "matrix too large for the LDS-resident CONISS (n > 10200)");
+    if (sd.n > kConissMaxN) fail(TP_ERR_UNSUPPORTED, "more than 65536 bins per matrix");
     run_coniss(sd, s, false, nullptr);
 }
 

@@ -223,6 +223,28 @@ def test_sweep_bit_exact(gpu, n0, k, seed):
     assert np.array_equal(a.view(np.uint64), b.view(np.uint64))   # incl. NA bit patterns
 
 
+def _structured_pcs(n, k, seed):
+    """Piecewise-constant PC scores + noise (TAD-like segments of 10-60 bins)."""
+    rng = np.random.default_rng(seed)
+    cuts = np.cumsum(rng.integers(10, 60, size=n))
+    seg = np.searchsorted(cuts, np.arange(n), side="right")
+    means = rng.standard_normal((seg.max() + 1, k)) * (1.0 / (1 + np.arange(k)))
+    return means[seg] + 0.05 * rng.standard_normal((n, k))
+
+
+@pytest.mark.parametrize("n,k,seed", [(10600, 6, 3), (20000, 3, 4)])
+def test_sweep_bit_exact_global_variant(gpu, n, k, seed):
+    # n beyond the LDS capacity (10 200): the CONISS keeps costs and links in
+    # global memory (same code path otherwise) -- the C5 arm sizes
+    p = _structured_pcs(n, k, seed)
+    got = G.sweep_dev(p)
+    ref = O.sweep(p)
+    assert np.array_equal(got["n_cluster"], ref.n_cluster)
+    assert np.array_equal(got["mrg_b"], ref.mrg_b)
+    assert np.array_equal(got["height"], ref.height)
+    assert np.array_equal(got["scores"].view(np.uint64), ref.scores.view(np.uint64))
+
+
 def test_sweep_selection_and_bstick_r_faithful(gpu):
     p = _pcs(300, 21)
     got = G.sweep(p)
