@@ -201,7 +201,7 @@ def main():
                           "n0": n0, "n_good": n, "k": k, "max_pcs": args.max_pcs,
                           "parallelism": f"one matrix per GPU x{world}"},
                "roofline": roof}
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:   # CPU baseline: rank 0 at N=1 only
             sys.path.insert(0, os.path.join(HERE, "oracle"))
             import tadpole_oracle as O
             threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
