@@ -734,6 +734,77 @@ void tp_debug_chol(const double *W, const int *b, const double *rel, const int *
     });
 }
 
+/* CholQR kernels for b <= 256 on Z = I: k_chol_inv + k_trsm_frag give
+ * Y = U^{-1} (W = U'U, S-scaled, + rel on the scaled diagonal); diag[b] =
+ * diag(U).  ms[0] chol kernel (16 waves), ms[1] info, ms[2] chol kernel (8
+ * waves), ms[3..4] stamps (prologue, factor cycles), ms[5] diag-factor cycles,
+ * ms[6] trsm kernel (n = b). */
+void tp_debug_chol_inv(const double *W, const int *b, const double *rel, const int *reps, double *diag, double *Y,
+                       double *ms, int *status) {
+    guarded(status, [&] {
+        Ctx &c = ctx_for(0);
+        hipStream_t s = c.cur;
+        const int B = *b;
+        double *dW = c.buf[S_SMALL].as<double>((size_t)4 * B * B + 2 * B);
+        double *dF = dW + (size_t)B * B;
+        double *dI = dF + (size_t)B * B;
+        double *dY = dI + (size_t)B * B;
+        double *rd = dY + (size_t)B * B;
+        double *sc = rd + B;
+        int *info = c.buf[S_MISC].as<int>(64);
+        std::vector<double> eye((size_t)B * B, 0.0);
+        for (int q = 0; q < B; ++q) eye[(size_t)q * B + q] = 1.0;
+        TP_HIP(hipMemcpyAsync(dI, eye.data(), (size_t)B * B * 8, hipMemcpyHostToDevice, s));
+        hipEvent_t e0, e1, e2;
+        TP_HIP(hipEventCreate(&e0));
+        TP_HIP(hipEventCreate(&e1));
+        TP_HIP(hipEventCreate(&e2));
+        const int R = std::max(1, *reps);
+        const int keep = g_chol_inv_waves;
+        for (int pass = 0; pass < 2; ++pass) {
+            g_chol_inv_waves = pass == 0 ? 16 : 8;
+            float tc = 0, tt = 0;
+            for (int r = 0; r < R; ++r) {
+                TP_HIP(hipMemcpyAsync(dW, W, (size_t)B * B * 8, hipMemcpyHostToDevice, s));
+                TP_HIP(hipEventRecord(e0, s));
+                launch_chol_inv(dW, dF, sc, rd, B, *rel, info, s);
+                TP_HIP(hipEventRecord(e1, s));
+                launch_trsm_frag(dI, B, B, dF, sc, dY, s);
+                TP_HIP(hipEventRecord(e2, s));
+                TP_HIP(hipEventSynchronize(e2));
+                float a = 0, bb = 0;
+                TP_HIP(hipEventElapsedTime(&a, e0, e1));
+                TP_HIP(hipEventElapsedTime(&bb, e1, e2));
+                tc += a;
+                tt += bb;
+            }
+            ms[pass == 0 ? 0 : 2] = tc / R;
+            if (pass == 0) ms[6] = tt / R;
+        }
+        g_chol_inv_waves = keep;
+        TP_HIP(hipMemcpyAsync(dW, W, (size_t)B * B * 8, hipMemcpyHostToDevice, s));
+        long long *dst = (long long *)c.buf[S_MISC].as<char>(1024) + 32;
+        launch_chol_inv(dW, dF, sc, rd, B, *rel, info, s, dst);
+        launch_trsm_frag(dI, B, B, dF, sc, dY, s);
+        long long hst[5];
+        TP_HIP(hipMemcpyAsync(hst, dst, sizeof(hst), hipMemcpyDeviceToHost, s));
+        int hinfo = 0;
+        std::vector<double> hw((size_t)B * B);
+        TP_HIP(hipMemcpyAsync(hw.data(), dW, (size_t)B * B * 8, hipMemcpyDeviceToHost, s));
+        TP_HIP(hipMemcpyAsync(Y, dY, (size_t)B * B * 8, hipMemcpyDeviceToHost, s));
+        TP_HIP(hipMemcpyAsync(&hinfo, info, sizeof(int), hipMemcpyDeviceToHost, s));
+        TP_HIP(hipStreamSynchronize(s));
+        for (int q = 0; q < B; ++q) diag[q] = hw[(size_t)q * B + q];
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        (void)hipEventDestroy(e2);
+        ms[1] = hinfo;
+        ms[3] = (double)hst[0];
+        ms[4] = (double)hst[1];
+        ms[5] = (double)hst[4];
+    });
+}
+
 /* stamped CONISS for trees 1..k on P (n x k col-major): stamps[k * 8]
  * (cycles per phase: argmin, loads, costs, update, init, bstick), kernel ms. */
 void tp_debug_coniss_stamps(const double *P, const int *n, const int *k, long long *stamps, double *ms,

@@ -105,6 +105,17 @@ void launch_chol_stamped(double *d_W, double *d_rdiag, int b, double rel, int *d
                          hipStream_t s);
 void launch_trsm_ru(const double *d_Z, int n, int b, const double *d_U, const double *d_rdiag, double *d_Q,
                     hipStream_t s);
+// CholQR for b <= 256 (b % 16 == 0), tp_chol.hip: k_chol_inv factors
+// S W S + rel I = U'^T U' (S = diag(W)^-1/2) in one register-resident
+// workgroup and leaves U' tiles and E_p = U'_pp^-T as MFMA operand fragments
+// in F (b x b doubles), S in sc (b), 1/diag(U) in rdiag (b), diag(U) on W's
+// diagonal; k_trsm_frag then forms Q = Z U^-1 (U = U' S^-1), n/16 waves.
+constexpr int kCholInvMax = 256;
+extern int g_chol_inv_waves;
+void launch_chol_inv(double *d_W, double *d_F, double *d_sc, double *d_rdiag, int b, double rel, int *d_info,
+                     hipStream_t s, long long *d_stamps = nullptr);
+void launch_trsm_frag(const double *d_Z, int n, int b, const double *d_F, const double *d_sc, double *d_Q,
+                      hipStream_t s);
 
 // sweep (tp_sweep.hip)
 struct SweepDev {

@@ -89,17 +89,25 @@ __global__ void __launch_bounds__(256) k_resid(const double *Y, const double *V,
 
 // Q = orth(Z): W = Z'Z (symmetric GEMM), U = chol(W + s I) (one workgroup),
 // Q = Z U^{-1} (row-block TRSM).  `passes` CholQR passes.  X holds 1/diag(U).
+// For b <= 256 the factor comes from one register-resident MFMA kernel and
+// Q = Z U^{-1} from an all-register MFMA solve; Y (b x b) holds the factor's
+// operand fragments, X (b x b) 1/diag(U) and the Jacobi scaling.
 static void orth_cholqr(Ctx &c, double *Z, double *Qout, double *Tmp, int n, int b, double *W, double *X,
-                        int *d_info, int passes, double shift) {
+                        double *Y, int *d_info, int passes, double shift) {
     double *src = Z;
     for (int p = 0; p < passes; ++p) {
         GemmArgs g{b, b, n, src, n, true, src, n, W, b};
         g.sym_upper = true;
         g.splitk = std::max(1, std::min(32, n / 128));
         gemm_f64(g, c.buf[S_PARTIAL], c.cur);
-        launch_chol(W, X, b, p == 0 ? shift : 0.0, d_info, c.cur);
         double *dst = ((passes - 1 - p) % 2 == 0) ? Qout : Tmp;   // last pass lands in Qout
-        launch_trsm_ru(src, n, b, W, X, dst, c.cur);
+        if (b <= kCholInvMax && b % 16 == 0) {
+            launch_chol_inv(W, Y, X + b, X, b, p == 0 ? shift : 0.0, d_info, c.cur);
+            launch_trsm_frag(src, n, b, Y, X + b, dst, c.cur);
+        } else {
+            launch_chol(W, X, b, p == 0 ? shift : 0.0, d_info, c.cur);
+            launch_trsm_ru(src, n, b, W, X, dst, c.cur);
+        }
         src = dst;
     }
 }
@@ -167,10 +175,11 @@ PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d
         double *Q = c.buf[S_Q].as<double>((size_t)n * b);
         double *Z = c.buf[S_Z].as<double>((size_t)n * b);
         double *T = c.buf[S_SWEEP].as<double>((size_t)n * b);
-        double *Wsm = c.buf[S_SMALL].as<double>((size_t)2 * b * b + 2 * b + 64);
+        double *Wsm = c.buf[S_SMALL].as<double>((size_t)3 * b * b + 2 * b + 64);
         double *Xinv = Wsm + (size_t)b * b;
         double *theta = Xinv + (size_t)b * b;
         double *offd = theta + b;
+        double *Yinv = offd + b;   // b x b, U^{-1} of the last CholQR
         double *resid = c.buf[S_MISC].as<double>(64 + k + b) + 64;
         int *d_info = c.buf[S_MISC].as<int>(64);
         const size_t nb = (size_t)n * b;
@@ -190,7 +199,7 @@ PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d
         auto iterate = [&](int count) {   // plain subspace iteration
             for (int it = 0; it < count; ++it) {
                 gemm_gq(Q, Z);
-                orth_cholqr(c, Z, Q, T, n, b, Wsm, Xinv, d_info, 1, 1e-14);
+                orth_cholqr(c, Z, Q, T, n, b, Wsm, Xinv, Yinv, d_info, 1, 1e-14);
             }
         };
         // Chebyshev filter of degree m on [0, cut]: Q <- orth(T_m((G - e)/h) Q),
@@ -220,7 +229,7 @@ PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d
                 cur = tmp;
                 tmp = (cur == T) ? Yb : T;
             }
-            orth_cholqr(c, cur, Q, tmp, n, b, Wsm, Xinv, d_info, 1, 1e-14);
+            orth_cholqr(c, cur, Q, tmp, n, b, Wsm, Xinv, Yinv, d_info, 1, 1e-14);
         };
         const double target = 1e-12;
         const int max_deg = 600;
@@ -231,7 +240,7 @@ PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d
         for (int it = 0; it < 2; ++it) {
             gemm_gq(Q, T);
             gemm_gq(T, Z);
-            orth_cholqr(c, Z, Q, T, n, b, Wsm, Xinv, d_info, 1, 1e-14);
+            orth_cholqr(c, Z, Q, T, n, b, Wsm, Xinv, Yinv, d_info, 1, 1e-14);
         }
         double cut = 0.0, gk = 2.0, g1cap = 10.0;
         int mdeg = 1;
@@ -284,7 +293,7 @@ PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d
             // Rayleigh-Ritz: orthonormalise tightly, H = Q'GQ, eigen-decompose, rotate
             // Q is orthonormal to ~kappa^2 eps after the last one-pass CholQR:
             // one more pass on Q itself restores eps-orthonormality
-            orth_cholqr(c, Q, Z, T, n, b, Wsm, Xinv, d_info, 1, 1e-14);
+            orth_cholqr(c, Q, Z, T, n, b, Wsm, Xinv, Yinv, d_info, 1, 1e-14);
             std::swap(Q, Z);
             GemmArgs g2{n, b, n, G, n, true, Q, n, Z, n};
             g2.splitk = 0;

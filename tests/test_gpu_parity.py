@@ -153,6 +153,41 @@ def test_eigsym(gpu, b, kind):
     assert np.abs(v.T @ v - np.eye(b)).max() <= 1e-9
 
 
+@pytest.mark.parametrize("b,cond,rel", [(16, 1e2, 0.0), (48, 1e4, 0.0), (128, 1e6, 0.0), (256, 1e6, 0.0),
+                                         (256, 1e12, 1e-14), (96, 1.0, 0.0)])
+def test_chol_inv_register_kernel(gpu, b, cond, rel):
+    """PCA CholQR kernels (k_chol_inv + k_trsm_frag) on Z = I: Y = U^{-1} for
+    U'U = W + rel diag(W) (Jacobi-scaled shift).  Checks Y upper triangular,
+    Y'(W + rel diag W)Y = I (bar ~ eps kappa(S W S)) and diag(U) = diag of
+    the Cholesky factor (bar ~ b eps kappa)."""
+    import ctypes
+    rng = np.random.default_rng(b + int(np.log10(cond)))
+    q, _ = np.linalg.qr(rng.standard_normal((b, b)))
+    ev = np.logspace(0, -np.log10(cond), b)
+    dsc = 10.0 ** rng.uniform(-3, 3, b)          # column norms spread (Jacobi scaling)
+    W = ((q * ev) @ q.T) * dsc[:, None] * dsc[None, :]
+    W = np.asfortranarray((W + W.T) / 2)
+    dg = np.zeros(b)
+    Y = np.zeros((b, b), order="F")
+    ms = np.zeros(8)
+    st = ctypes.c_int(0)
+    D = ctypes.POINTER(ctypes.c_double)
+    gpu.tp_debug_chol_inv(W.ctypes.data_as(D), ctypes.byref(ctypes.c_int(b)), ctypes.byref(ctypes.c_double(rel)),
+                          ctypes.byref(ctypes.c_int(3)), dg.ctypes.data_as(D), Y.ctypes.data_as(D),
+                          ms.ctypes.data_as(D), ctypes.byref(st))
+    assert st.value == 0
+    assert ms[1] == 0, "not positive definite"
+    assert np.all(np.tril(Y, -1) == 0.0)
+    s = np.sqrt(np.diag(W))
+    Wr = W + rel * np.diag(np.diag(W))
+    kap = np.linalg.cond(Wr / s[:, None] / s[None, :])
+    assert np.abs(Y.T @ Wr @ Y - np.eye(b)).max() <= 100 * b * 2.2e-16 * kap
+    Uref = np.linalg.cholesky(Wr).T
+    np.testing.assert_allclose(dg, np.diag(Uref), rtol=100 * b * 2.2e-16 * np.sqrt(kap))
+    print(f"chol_inv b={b}: chol {ms[0] * 1e3:.1f} us (16 waves), {ms[2] * 1e3:.1f} us (8 waves), "
+          f"trsm {ms[6] * 1e3:.1f} us; cycles prologue {ms[3]:.0f} factor {ms[4]:.0f} diag {ms[5]:.0f}")
+
+
 # ---------------------------------------------------------- coniss / dist
 
 @pytest.mark.parametrize("n,c,seed", [(2, 1, 0), (3, 1, 1), (50, 1, 2), (97, 7, 3), (300, 64, 4), (300, 65, 5),
