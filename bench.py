@@ -62,6 +62,8 @@ def _config_name(n0, max_pcs):
         return "C2"
     if max_pcs == 200 and n0 == 7808:
         return "C3 shape (chr18 @10kb)"
+    if max_pcs == 200 and n0 in (24300, 21300):
+        return "C5 arm shape (chr1 @5kb)"
     if n0 == 200:
         return "C1 shape"
     return "custom"
@@ -78,6 +80,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-reps", type=int, default=3)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--sharded", action="store_true",
+                    help="one matrix split over all ranks (SURVEY §8(e)2, C5 arms): strong scaling")
     return ap.parse_args()
 
 
@@ -101,8 +105,14 @@ def main():
 
     L = _lib.load()
     n0 = args.n0
-    seed = SEED_BASE + 2 + 1000 * rank
+    seed = SEED_BASE + 2 + (0 if args.sharded else 1000 * rank)   # sharded: every rank holds the same matrix
     host = synth_hic(n0, seed)
+    flags = _lib.TP_FLAG_ROW_MAJOR
+    if args.sharded:
+        from tadpole_amd import multi
+        if world > 1:
+            multi.init_comm(device=local)
+        flags |= _lib.TP_FLAG_SHARDED
     dev_m = torch.from_numpy(host).to(f"cuda:{local}")
     stream = torch.cuda.current_stream()
 
@@ -120,7 +130,7 @@ def main():
         n_good, k, w, n_pcs, n_clusters, st = outs
         L.tp_pipeline_dev(ctypes.c_void_p(dev_m.data_ptr()), ctypes.byref(I(n0)), ctypes.byref(I(args.max_pcs)),
                           ctypes.byref(I(args.min_clusters)), ctypes.byref(ctypes.c_double(0.01)),
-                          ctypes.byref(I(_lib.TP_FLAG_ROW_MAJOR)), ctypes.byref(I(local)),
+                          ctypes.byref(I(flags)), ctypes.byref(I(local)),
                           ctypes.c_void_p(stream.cuda_stream), ctypes.byref(I(k_cap)), ctypes.byref(I(w_cap)),
                           _lib.ip(b["bad"]), ctypes.byref(n_good), _lib.ip(b["good"]), ctypes.byref(k),
                           _lib.ip(b["nclu"]), _lib.dp(b["scores"]), ctypes.byref(w), ctypes.byref(n_pcs),
@@ -164,12 +174,13 @@ def main():
     k = int(tm[15])
 
     if rank == 0:
-        value = n0 * world * args.steps / elapsed
+        value = n0 * (1 if args.sharded else world) * args.steps / elapsed
         # ---- roofline of the dominant kernel
+        share = 1.0 / world if args.sharded else 1.0   # sharded: this rank's part of each product
         kern = {
-            "xtx_gemm": (tm[5], "mfma", 1, float(n) ** 3),                      # N^3 (symmetric half)
-            "xcxc_gemm": (tm[6], "mfma", 1, float(n) ** 3),
-            "gq_gemm": (tm[7], "mfma", max(1, int(tm[8])), 2.0 * n * n * int(tm[12]) if tm[12] else 0.0),
+            "xtx_gemm": (tm[5], "mfma", 1, share * float(n) ** 3),              # N^3 (symmetric half)
+            "xcxc_gemm": (tm[6], "mfma", 1, share * float(n) ** 3),
+            "gq_gemm": (tm[7], "mfma", max(1, int(tm[8])), share * 2.0 * n * n * int(tm[12]) if tm[12] else 0.0),
             "coniss": (tm[9], "hbm", 1, 40.0 * (n - 1) * k * (k + 1) / 2.0),    # bytes: 5 sum vectors/merge
             "ch": (tm[10], "hbm", 1, 16.0 * n * k * k),                         # bytes: 2 passes/tree
         }
@@ -194,14 +205,18 @@ def main():
         out = {"metric": "bins/sec (NxN matrix) at 1/2/4/8 GPUs; TAD boundary bit-match vs R ref",
                "value": round(value, 2), "unit": "bins/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-               "data": "synthetic (SURVEY.md §8(d) Hi-C generator, seed 20261015+2+1000*rank)",
-               "config": {"workload": f"{_config_name(n0, args.max_pcs)}: synthetic {n0}x{n0} Hi-C matrix per GPU, "
-                                      f"max_pcs={args.max_pcs}",
+               "higher_is_better": True, "scaling": "strong" if args.sharded else "weak", "vs_baseline": None,
+               "dtype": "f64",
+               "data": "synthetic (SURVEY.md §8(d) Hi-C generator, seed 20261015+2" +
+                       ("" if args.sharded else "+1000*rank") + ")",
+               "config": {"workload": (f"{_config_name(n0, args.max_pcs)}: synthetic {n0}x{n0} Hi-C matrix "
+                                       + ("sharded over all GPUs" if args.sharded else "per GPU")
+                                       + f", max_pcs={args.max_pcs}"),
                           "n0": n0, "n_good": n, "k": k, "max_pcs": args.max_pcs,
-                          "parallelism": f"one matrix per GPU x{world}"},
+                          "parallelism": (f"one matrix over {world} GPU(s): column/row-split products, "
+                                          "RCCL all-gather" if args.sharded else f"one matrix per GPU x{world}")},
                "roofline": roof}
-        if not args.no_cpu_baseline and world == 1:   # CPU baseline: rank 0 at N=1 only
+        if not args.no_cpu_baseline and world == 1 and not args.sharded:   # CPU baseline: rank 0 at N=1 only
             sys.path.insert(0, os.path.join(HERE, "oracle"))
             import tadpole_oracle as O
             threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
@@ -230,6 +245,9 @@ def main():
                 f.write(line + "\n")
     if world > 1:
         dist.barrier()
+        if args.sharded:
+            from tadpole_amd import multi
+            multi.destroy_comm(local)
         dist.destroy_process_group()
     L.tp_shutdown()
 

@@ -52,6 +52,10 @@ enum {
 #define TP_FLAG_CLEAN       2   /* input is already NA-free and symmetric          */
 #define TP_FLAG_NO_MASK     4   /* keep every bin: the per-arm matrices of
                                    R/TADpole.R:362 are correlated as given        */
+#define TP_FLAG_SHARDED     8   /* tp_pipeline_dev: split this matrix's products
+                                   over the ranks of the device's communicator
+                                   (tp_comm_init); every rank passes the same
+                                   matrix and gets the same results            */
 
 /* ---------------------------------------------------------------- runtime */
 int  tp_version(void);                          /* ABI version, 1                */
@@ -59,6 +63,28 @@ int  tp_device_count(void);                     /* HIP devices visible (>=0)    
 void tp_shutdown(void);                         /* free every device context     */
 int  tp_last_error(char *buf, int len);         /* ctypes form                   */
 void tp_last_error_r(char **buf, int *len);     /* R .C form                     */
+
+/* -------------------------------------------------------------- multi-GPU */
+/* One matrix over several GPUs (chr1 @5kb arms of ~24k bins;
+ * the reference has no multi-GPU path -- it forks over PC prefixes,
+ * R/TADpole.R:104).  One process (or host thread) per GPU.  Rank 0 calls
+ * tp_comm_unique_id, the host distributes the 128 bytes (torch.distributed,
+ * MPI, a file...), every rank calls tp_comm_init on its device, then
+ * tp_pipeline_dev(..., flags | TP_FLAG_SHARDED) with the same matrix: X'X and
+ * Xc'Xc are split by column tiles, G Q and Xc V by rows, the sweep by PC
+ * prefixes, all gathered over RCCL (xGMI).  Results are bit-identical for any
+ * rank count.  RCCL (librccl.so.1) is loaded at tp_comm_init.
+ * tp_set_virtual_shards: test hook running the sharded schedule as nvirt
+ * shards on one device (no communicator).  tp_shard_plan (host only): the
+ * split, kind 0 = tile columns of the symmetric products, 1 = rows (64-row
+ * blocks), 2 = trees; bounds[nranks + 1]. */
+void tp_comm_unique_id(char *id /* 128 bytes */, int *status);
+void tp_comm_init(const char *id, const int *nranks, const int *rank,
+                  const int *device, int *status);
+void tp_comm_destroy(const int *device);
+void tp_set_virtual_shards(const int *device, const int *nvirt, int *status);
+void tp_shard_plan(const int *n, const int *nranks, const int *kind,
+                   int *bounds, int *status);
 
 /* --------------------------------------------------------------- load_mat */
 /* bigmemory::read.big.matrix(mat_file, type='double', sep='\t') (R/TADpole.R:17,

@@ -18,12 +18,14 @@ TP_OK, TP_ERR_ARG, TP_ERR_HIP, TP_ERR_NO_BSTICK, TP_ERR_CAPACITY, TP_ERR_NUMERIC
 TP_FLAG_ROW_MAJOR = 1
 TP_FLAG_CLEAN = 2
 TP_FLAG_NO_MASK = 4
+TP_FLAG_SHARDED = 8
 
 #: every symbol include/tadpole_hip.h declares
 EXPORTS = (
     "tp_version", "tp_device_count", "tp_shutdown", "tp_last_error", "tp_last_error_r",
     "tp_mask", "tp_cor", "tp_pca", "tp_sweep", "tp_coniss", "tp_dist", "tp_ch",
     "tp_pipeline", "tp_pipeline_dev", "tp_sweep_dev", "tp_tsv_dims", "tp_read_tsv",
+    "tp_comm_unique_id", "tp_comm_init", "tp_comm_destroy", "tp_set_virtual_shards", "tp_shard_plan",
 )
 
 
@@ -80,6 +82,11 @@ def load() -> ctypes.CDLL:
     L.tp_tsv_dims.argtypes = [_S, _I, _I, _I]
     L.tp_read_tsv.argtypes = [_S, _I, _I, _I, _I, _D, _I]
     L.tp_sweep_dev.argtypes = [_V, _I, _I, _I, _I, _V, _I, _I, _D, _I, _I, _I, _D, _D, _I]
+    L.tp_comm_unique_id.argtypes = [ctypes.c_char_p, _I]
+    L.tp_comm_init.argtypes = [ctypes.c_char_p, _I, _I, _I, _I]
+    L.tp_comm_destroy.argtypes = [_I]
+    L.tp_set_virtual_shards.argtypes = [_I, _I, _I]
+    L.tp_shard_plan.argtypes = [_I, _I, _I, _I, _I]
     _lib = L
     return L
 

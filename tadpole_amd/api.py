@@ -360,12 +360,15 @@ def _assemble_rle(t, dendro, levels, good1, bad_idx1) -> Tadpole:
 
 def TADpole(mat_file, max_pcs: int = 200, min_clusters: int = 2, bad_frac: float = 0.01,
             chr=None, start=None, end=None, resol=None, centromere_search: bool = False,
-            device: int = 0) -> Tadpole:
+            device: int = 0, sharded: bool = False) -> Tadpole:
     """``TADpole()`` (R/TADpole.R:344-501).  ``mat_file`` may be a path to a
-    tab-separated matrix or an in-memory square array."""
+    tab-separated matrix or an in-memory square array.  ``sharded``: split this
+    matrix over the ranks of the communicator made by
+    ``tadpole_amd.multi.init_comm`` (every rank calls with the same matrix)."""
     raw = _as_matrix(mat_file)
+    shard_flag = _lib.TP_FLAG_SHARDED if sharded else 0
     if not centromere_search:
-        res = _pipeline(raw, max_pcs, min_clusters, bad_frac, 0, device)
+        res = _pipeline(raw, max_pcs, min_clusters, bad_frac, shard_flag, device)
         bad_idx1 = np.flatnonzero(res["bad"]) + 1
         return _assemble(res, bad_idx1)
     mat = load_mat(raw, bad_frac=bad_frac, centromere_search=True, device=device)
@@ -373,10 +376,10 @@ def TADpole(mat_file, max_pcs: int = 200, min_clusters: int = 2, bad_frac: float
         # R/TADpole.R:356: `mat$centromer` on a matrix is an error in R
         raise TypeError("$ operator is invalid for atomic vectors (no centromere split: the longest "
                         "bad run touches an end of the matrix; R/TADpole.R:66-70,356)")
-    return _tadpole_arms(mat, max_pcs, min_clusters, device)
+    return _tadpole_arms(mat, max_pcs, min_clusters, device, shard_flag)
 
 
-def _tadpole_arms(mat, max_pcs, min_clusters, device) -> Tadpole:
+def _tadpole_arms(mat, max_pcs, min_clusters, device, shard_flag: int = 0) -> Tadpole:
     """R/TADpole.R:351-442 (arm loop and arm merge), bug-compatible."""
     tad = Tadpole()
     centromer = mat["centromere"]
@@ -385,7 +388,7 @@ def _tadpole_arms(mat, max_pcs, min_clusters, device) -> Tadpole:
         am = mat[arm]
         bad_cols = am.bad_columns
         res = _pipeline(np.asarray(am), max_pcs, min_clusters, 0.0,
-                        _lib.TP_FLAG_CLEAN | _lib.TP_FLAG_NO_MASK, device)
+                        _lib.TP_FLAG_CLEAN | _lib.TP_FLAG_NO_MASK | shard_flag, device)
         names = am.names.astype(np.int32)   # rownames inherited from the full matrix
         res["good"] = names
         sub = _assemble_arm(res, bad_cols)

@@ -216,65 +216,112 @@ static SweepOut run_sweep(Ctx &c, const double *d_Pt, int n, int k, int min_clus
                           std::vector<int> *all_a = nullptr, std::vector<int> *all_b = nullptr,
                           std::vector<double> *all_cost = nullptr, std::vector<double> *all_h = nullptr) {
     hipStream_t s = c.cur;
+    // trees 1..k, split in contiguous ranges over the shards (one range when
+    // not sharded); per-shard outputs are packed blocks: n_cluster[t0..t1),
+    // scores (t1 - t0) x w_cap column-major at offset t0 * w_cap
+    const int R = shard_count(c);
+    std::vector<int> tb(R + 1);
+    shard_plan(k, R, 2, tb.data());
     SweepDev sd{};
     sd.Pt = d_Pt;
     sd.n = n;
     sd.ldp = k;
     sd.k = k;
-    sd.tree0 = 0;
-    sd.ntrees = k;
     sd.min_clusters = min_clusters;
-    sd.sums = c.buf[S_SWEEP].as<double>(sweep_sums_doubles(n, 0, k));
+    double *sums = c.buf[S_SWEEP].as<double>(sweep_sums_doubles(n, 0, k));
     const size_t rec = (size_t)k * (n - 1);
     char *recbuf = c.buf[S_SWEEP2].as<char>(rec * (4 + 4 + 8 + 8) + 256);
-    sd.mrg_a = (int *)recbuf;
-    sd.mrg_b = sd.mrg_a + rec;
-    sd.cost = (double *)(((uintptr_t)(sd.mrg_b + rec) + 15) & ~(uintptr_t)15);
-    sd.height = sd.cost + rec;
+    int *mrg_a = (int *)recbuf;
+    int *mrg_b = mrg_a + rec;
+    double *cost = (double *)(((uintptr_t)(mrg_b + rec) + 15) & ~(uintptr_t)15);
+    double *hgt = cost + rec;
     sd.w_cap = std::max(1, n - 1);
     sd.seg_cap = std::min(sd.w_cap, 1024);
-    char *sc = c.buf[S_SCORES].as<char>((size_t)k * sd.w_cap * 8 + (size_t)k * 4 + 64);
-    sd.scores = (double *)sc;
-    sd.n_cluster = (int *)(sd.scores + (size_t)k * sd.w_cap);
+    char *sc = c.buf[S_SCORES].as<char>((size_t)k * sd.w_cap * 8 + (size_t)k * 4 + (size_t)R * 4 + 64);
+    double *sc_all = (double *)sc;
+    int *nc_all = (int *)(sc_all + (size_t)k * sd.w_cap);
+    int *err_all = nc_all + k;   // one flag per shard
     sd.seg = c.buf[S_PARTIAL].as<double>((size_t)k * sd.seg_cap * (k + 1));
     sd.iseg = c.buf[S_MISC].as<int>((size_t)k * (2 * sd.seg_cap + 2) + 64) + 64;
-    sd.err = c.buf[S_MISC].as<int>(64);
     sd.trS = (double *)(c.buf[S_NGOOD].as<char>(64)) + 2;
     sd.cost0 = c.buf[S_SMALL].as<double>(sweep_cost0_doubles(n, k));
-    TP_HIP(hipMemsetAsync(sd.err, 0, sizeof(int), s));
-    launch_sweep(sd, s, &c);
-    std::vector<int> h_nc(k);
-    int h_err = 0;
-    TP_HIP(hipMemcpyAsync(h_nc.data(), sd.n_cluster, k * sizeof(int), hipMemcpyDeviceToHost, s));
-    TP_HIP(hipMemcpyAsync(&h_err, sd.err, sizeof(int), hipMemcpyDeviceToHost, s));
+    TP_HIP(hipMemsetAsync(err_all, 0, (size_t)R * sizeof(int), s));
+    for (int r = 0; r < R; ++r) {
+        const int t0 = tb[r], nt = tb[r + 1] - tb[r];
+        if (!shard_mine(c, r) || nt == 0) continue;
+        SweepDev d = sd;
+        d.tree0 = t0;
+        d.ntrees = nt;
+        d.sums = sums + sweep_sums_doubles(n, 0, t0);   // offset of tree t0 + 1
+        d.mrg_a = mrg_a + (size_t)t0 * (n - 1);
+        d.mrg_b = mrg_b + (size_t)t0 * (n - 1);
+        d.cost = cost + (size_t)t0 * (n - 1);
+        d.height = hgt + (size_t)t0 * (n - 1);
+        d.n_cluster = nc_all + t0;
+        d.scores = sc_all + (size_t)t0 * sd.w_cap;   // ld = nt
+        d.err = err_all + r;
+        launch_sweep(d, s, &c);
+    }
+    {
+        std::vector<size_t> off(R + 1);
+        for (int r = 0; r <= R; ++r) off[r] = (size_t)tb[r] * 4;
+        shard_gather_bytes(c, nc_all, off);
+        std::vector<size_t> off2(R + 1, 0);
+        for (int r = 0; r < R; ++r) off2[r + 1] = (size_t)(r + 1) * 4;
+        shard_gather_bytes(c, err_all, off2);
+    }
+    std::vector<int> h_nc(k), h_err(R);
+    TP_HIP(hipMemcpyAsync(h_nc.data(), nc_all, k * sizeof(int), hipMemcpyDeviceToHost, s));
+    TP_HIP(hipMemcpyAsync(h_err.data(), err_all, R * sizeof(int), hipMemcpyDeviceToHost, s));
     TP_HIP(hipStreamSynchronize(s));
     for (int i = 0; i < k; ++i)
         if (h_nc[i] < 1)
             fail(TP_ERR_NO_BSTICK, "no broken-stick level is significant for PC prefix " + std::to_string(i + 1) +
                                        " (R: invalid 'times' argument at R/TADpole.R:115)");
-    if (h_err) fail(TP_ERR_UNSUPPORTED, "a broken-stick cut exceeds the CH kernel's segment capacity");
+    for (int r = 0; r < R; ++r)
+        if (h_err[r]) fail(TP_ERR_UNSUPPORTED, "a broken-stick cut exceeds the CH kernel's segment capacity");
     SweepOut o;
     o.w = *std::max_element(h_nc.begin(), h_nc.end());
     if (o.w > w_cap_host) fail(TP_ERR_CAPACITY, "scores capacity (w_cap) too small: need " + std::to_string(o.w));
     if (n_cluster) memcpy(n_cluster, h_nc.data(), k * sizeof(int));
-    std::vector<double> h_sc((size_t)k * o.w);
-    TP_HIP(hipMemcpyAsync(h_sc.data(), sd.scores, h_sc.size() * sizeof(double), hipMemcpyDeviceToHost, s));
-    TP_HIP(hipStreamSynchronize(s));
+    {
+        std::vector<size_t> off(R + 1);
+        for (int r = 0; r <= R; ++r) off[r] = (size_t)tb[r] * sd.w_cap;
+        shard_gather(c, sc_all, off);   // whole blocks (each rank's w may differ)
+    }
+    std::vector<double> h_sc((size_t)k * o.w), blk;
+    for (int r = 0; r < R; ++r) {
+        const int t0 = tb[r], nt = tb[r + 1] - tb[r];
+        if (nt == 0) continue;
+        blk.resize((size_t)nt * o.w);
+        TP_HIP(hipMemcpyAsync(blk.data(), sc_all + (size_t)t0 * sd.w_cap, blk.size() * sizeof(double),
+                              hipMemcpyDeviceToHost, s));
+        TP_HIP(hipStreamSynchronize(s));
+        for (int j = 0; j < o.w; ++j)
+            for (int ti = 0; ti < nt; ++ti) h_sc[(size_t)(t0 + ti) + (size_t)j * k] = blk[(size_t)ti + (size_t)j * nt];
+    }
     if (scores) memcpy(scores, h_sc.data(), h_sc.size() * sizeof(double));
     select_params(h_sc.data(), k, o.w, &o.n_pcs, &o.n_clusters);
     const int t = o.n_pcs - 1;
+    {
+        int owner = 0;
+        while (owner + 1 < R && t >= tb[owner + 1]) ++owner;
+        shard_bcast_bytes(c, mrg_a + (size_t)t * (n - 1), (size_t)(n - 1) * 4, owner);
+        shard_bcast_bytes(c, mrg_b + (size_t)t * (n - 1), (size_t)(n - 1) * 4, owner);
+        shard_bcast_bytes(c, hgt + (size_t)t * (n - 1), (size_t)(n - 1) * 8, owner);
+    }
     std::vector<int> ma(n - 1), mb(n - 1);
     std::vector<double> he(n - 1);
-    TP_HIP(hipMemcpyAsync(ma.data(), sd.mrg_a + (size_t)t * (n - 1), (n - 1) * sizeof(int), hipMemcpyDeviceToHost, s));
-    TP_HIP(hipMemcpyAsync(mb.data(), sd.mrg_b + (size_t)t * (n - 1), (n - 1) * sizeof(int), hipMemcpyDeviceToHost, s));
-    TP_HIP(hipMemcpyAsync(he.data(), sd.height + (size_t)t * (n - 1), (n - 1) * sizeof(double),
-                          hipMemcpyDeviceToHost, s));
+    TP_HIP(hipMemcpyAsync(ma.data(), mrg_a + (size_t)t * (n - 1), (n - 1) * sizeof(int), hipMemcpyDeviceToHost, s));
+    TP_HIP(hipMemcpyAsync(mb.data(), mrg_b + (size_t)t * (n - 1), (n - 1) * sizeof(int), hipMemcpyDeviceToHost, s));
+    TP_HIP(hipMemcpyAsync(he.data(), hgt + (size_t)t * (n - 1), (n - 1) * sizeof(double), hipMemcpyDeviceToHost, s));
     if (all_a) {
+        if (R > 1 && c.shard.comm) fail(TP_ERR_ARG, "all-tree records are not gathered across ranks");
         all_a->resize(rec); all_b->resize(rec); all_cost->resize(rec); all_h->resize(rec);
-        TP_HIP(hipMemcpyAsync(all_a->data(), sd.mrg_a, rec * 4, hipMemcpyDeviceToHost, s));
-        TP_HIP(hipMemcpyAsync(all_b->data(), sd.mrg_b, rec * 4, hipMemcpyDeviceToHost, s));
-        TP_HIP(hipMemcpyAsync(all_cost->data(), sd.cost, rec * 8, hipMemcpyDeviceToHost, s));
-        TP_HIP(hipMemcpyAsync(all_h->data(), sd.height, rec * 8, hipMemcpyDeviceToHost, s));
+        TP_HIP(hipMemcpyAsync(all_a->data(), mrg_a, rec * 4, hipMemcpyDeviceToHost, s));
+        TP_HIP(hipMemcpyAsync(all_b->data(), mrg_b, rec * 4, hipMemcpyDeviceToHost, s));
+        TP_HIP(hipMemcpyAsync(all_cost->data(), cost, rec * 8, hipMemcpyDeviceToHost, s));
+        TP_HIP(hipMemcpyAsync(all_h->data(), hgt, rec * 8, hipMemcpyDeviceToHost, s));
     }
     TP_HIP(hipStreamSynchronize(s));
     if (merge) encode_merge(ma.data(), mb.data(), n, merge);
@@ -298,6 +345,13 @@ static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_cl
     if (max_pcs < 1) fail(TP_ERR_ARG, "max_pcs must be >= 1");
     if (!(bad_frac >= 0.0 && bad_frac <= 1.0)) fail(TP_ERR_ARG, "bad_frac must be in [0, 1]");
     Timer tm(timings != nullptr, s);
+    // TP_FLAG_SHARDED: this call splits its products over the ranks of the
+    // device's communicator (or its virtual shards); reset on every exit
+    struct ShardScope {
+        Ctx &c;
+        ShardScope(Ctx &cc, bool on) : c(cc) { c.shard.active = on; }
+        ~ShardScope() { c.shard.active = false; }
+    } shard_scope(c, (flags & TP_FLAG_SHARDED) != 0);
     c.prof = timings != nullptr;
     c.recs.clear();
     c.evnext = 0;
@@ -340,7 +394,7 @@ static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_cl
         GemmArgs g{n, n, n, X, n, true, X, n, S, n};
         g.sym_upper = true;
         kprof_begin(c, K_COR_GEMM);
-        gemm_f64(g, c.buf[S_PARTIAL], s);
+        sym_gemm_sharded(c, g);
         kprof_end(c, K_COR_GEMM);
     }
     launch_cor_epilogue(S, m, n, C, s);
@@ -414,6 +468,40 @@ int tp_device_count(void) {
 }
 
 void tp_shutdown(void) { ctx_shutdown_all(); }
+
+/* ------------------------------------------------------------ multi-GPU */
+void tp_comm_unique_id(char *id, int *status) {
+    guarded(status, [&] { comm_unique_id(id); });
+}
+
+void tp_comm_init(const char *id, const int *nranks, const int *rank, const int *device, int *status) {
+    guarded(status, [&] {
+        if (!id || !nranks || !rank) fail(TP_ERR_ARG, "tp_comm_init: NULL argument");
+        Ctx &c = ctx_for(dev_of(device));
+        comm_init(c, id, *nranks, *rank);
+    });
+}
+
+void tp_comm_destroy(const int *device) {
+    int st = 0;
+    guarded(&st, [&] { comm_destroy(ctx_for(dev_of(device))); });
+}
+
+void tp_set_virtual_shards(const int *device, const int *nvirt, int *status) {
+    guarded(status, [&] {
+        if (!nvirt || *nvirt < 1 || *nvirt > 64) fail(TP_ERR_ARG, "virtual shards must be in 1..64");
+        Ctx &c = ctx_for(dev_of(device));
+        if (c.shard.comm) fail(TP_ERR_ARG, "device has a communicator: virtual shards are a single-device hook");
+        c.shard.nvirt = *nvirt;
+    });
+}
+
+void tp_shard_plan(const int *n, const int *nranks, const int *kind, int *bounds, int *status) {
+    guarded(status, [&] {
+        if (!n || !nranks || !kind || !bounds || *n < 0 || *kind < 0 || *kind > 2) fail(TP_ERR_ARG, "tp_shard_plan");
+        shard_plan(*n, *nranks, *kind, bounds);
+    });
+}
 
 int tp_last_error(char *buf, int len) {
     if (!buf || len <= 0) return (int)g_err.size();

@@ -70,16 +70,16 @@ __device__ __forceinline__ void store_b(double (*Bs)[LDK], const double (&rb)[4]
 template <bool TA>
 __global__ void __launch_bounds__(256) k_gemm_f64(int M, int N, int K, const double *__restrict__ A, int lda,
                                                   const double *__restrict__ B, int ldb, double *__restrict__ C,
-                                                  int ldc, int store_t, int sym, int tiles_n, int kchunk,
+                                                  int ldc, int store_t, int sym, int tcol0, int kchunk,
                                                   size_t part_stride) {
     __shared__ double As[2][BM][LDK];
     __shared__ double Bs[2][BN][LDK];
     int bm, bn;
-    if (sym) {  // linear id -> (bm <= bn)
+    if (sym) {  // linear id -> upper tile (bm <= bn), column by column from tile column tcol0
         int id = blockIdx.x;
-        bm = 0;
-        while (id >= tiles_n - bm) { id -= tiles_n - bm; ++bm; }
-        bn = bm + id;
+        bn = tcol0;
+        while (id > bn) { id -= bn + 1; ++bn; }
+        bm = id;
     } else {
         bm = blockIdx.x % ((M + BM - 1) / BM);
         bn = blockIdx.x / ((M + BM - 1) / BM);
@@ -174,7 +174,11 @@ void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s) {
     if (g.M <= 0 || g.N <= 0) return;
     if (g.sym_upper && g.M != g.N) fail(TP_ERR_ARG, "sym_upper GEMM needs a square output");
     const int tm = (g.M + BM - 1) / BM, tn = (g.N + BN - 1) / BN;
-    long nblk = g.sym_upper ? (long)tn * (tn + 1) / 2 : (long)tm * tn;
+    // sym_upper: upper tiles of tile columns [tc0, tc1) (a column shard)
+    const int tc0 = g.sym_upper ? std::max(0, g.tcol0) : 0;
+    const int tc1 = g.sym_upper ? (g.tcol1 < 0 ? tn : std::min(tn, g.tcol1)) : 0;
+    if (g.sym_upper && tc1 <= tc0) return;
+    long nblk = g.sym_upper ? (long)tc1 * (tc1 + 1) / 2 - (long)tc0 * (tc0 + 1) / 2 : (long)tm * tn;
     int S = g.splitk;
     if (S < 1) {
         // auto: fill the 256 CUs when the output has few tiles and K is long
@@ -199,10 +203,10 @@ void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s) {
     }
     if (g.trans_a)
         hipLaunchKernelGGL(k_gemm_f64<true>, grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb, out, ldo,
-                           st, (int)g.sym_upper, tn, kchunk, pstride);
+                           st, (int)g.sym_upper, tc0, kchunk, pstride);
     else
         hipLaunchKernelGGL(k_gemm_f64<false>, grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb, out,
-                           ldo, st, (int)g.sym_upper, tn, kchunk, pstride);
+                           ldo, st, (int)g.sym_upper, tc0, kchunk, pstride);
     TP_HIP(hipGetLastError());
     if (S > 1) {
         size_t tot = (size_t)g.M * g.N;

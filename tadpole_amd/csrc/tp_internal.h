@@ -37,8 +37,17 @@ struct DevBuf {
 // Kernel classes timed with HIP events when a caller asks for timings.
 enum KClass { K_COR_GEMM = 0, K_G_GEMM, K_GQ_GEMM, K_CONISS, K_CH, K_NCLASS };
 
+// Multi-GPU sharding of one matrix (tp_shard.hip).
+struct Shard {
+    void *comm = nullptr;   // ncclComm_t of this device's rank (tp_comm_init)
+    int rank = 0, nranks = 1;
+    int nvirt = 1;          // test hook: virtual shards on one device (no comm)
+    bool active = false;    // this call runs sharded (TP_FLAG_SHARDED)
+};
+
 // Per-device state: one stream, named scratch buffers.
 struct Ctx {
+    Shard shard;
     bool prof = false;                  // record per-kernel events this call
     std::vector<hipEvent_t> evpool;
     size_t evnext = 0;
@@ -49,7 +58,7 @@ struct Ctx {
     int device = 0;
     hipStream_t stream = nullptr;   // library stream
     hipStream_t cur = nullptr;      // stream used by the current call
-    DevBuf buf[24];
+    DevBuf buf[32];
     DevBuf pinned_flag;
     void *host_pinned = nullptr;    // small pinned staging area
     size_t host_pinned_bytes = 0;
@@ -66,7 +75,7 @@ void ctx_shutdown_all();
 enum Slot {
     S_M = 0, S_ROWMEAN, S_DIAG, S_BAD, S_GOOD, S_NGOOD, S_X, S_COLMEAN,
     S_S, S_C, S_XC, S_XCT, S_G, S_Q, S_Z, S_W, S_SMALL, S_P, S_PT,
-    S_SWEEP, S_SWEEP2, S_SCORES, S_PARTIAL, S_MISC
+    S_SWEEP, S_SWEEP2, S_SCORES, S_PARTIAL, S_MISC, S_SHARD, S_SHARD2
 };
 
 // ---------------------------------------------------------------- kernels
@@ -98,6 +107,7 @@ struct GemmArgs {
     bool store_t = false;
     bool sym_upper = false;
     int splitk = 1;     // 0 = choose from the tile count
+    int tcol0 = 0, tcol1 = -1;   // sym_upper: only tile columns [tcol0, tcol1) (-1 = all)
 };
 void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s);
 void launch_chol(double *d_W, double *d_rdiag, int b, double rel, int *d_info, hipStream_t s);
@@ -164,6 +174,20 @@ void eig_sym(rocblas_handle h, double *A, int b, double *theta, double *work, in
 // tp_io.hip: native reader of read.big.matrix(sep = '\t') files (host code)
 void tsv_dims(const char *path, int *nrow, int *ncol);
 void tsv_read(const char *path, int nrow, int ncol, int nthreads, bool row_major, double *out);
+
+// sharding (tp_shard.hip)
+void comm_unique_id(char *id128);
+void comm_init(Ctx &c, const char *id128, int nranks, int rank);
+void comm_destroy(Ctx &c);
+int shard_count(const Ctx &c);
+bool shard_mine(const Ctx &c, int r);
+void shard_plan(int n, int R, int kind, int *bounds);
+void shard_gather(Ctx &c, double *buf, const std::vector<size_t> &off);
+void shard_gather_bytes(Ctx &c, void *buf, const std::vector<size_t> &off);
+void shard_bcast_bytes(Ctx &c, void *buf, size_t bytes, int root);
+void sym_gemm_sharded(Ctx &c, GemmArgs g);
+void rows_gemm_sharded(Ctx &c, const double *A, int lda, int M, const double *B, int ldb, int N, int K,
+                       double *Out, int splitk_plain);
 
 struct PcaStats { int iters = 0; double resid = 0; double rate = 0; int block = 0; int blocks = 0; };
 PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d_Pt,

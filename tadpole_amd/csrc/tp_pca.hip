@@ -141,7 +141,7 @@ PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d
         GemmArgs g{n, n, n, Xc, n, true, Xc, n, G, n};
         g.sym_upper = true;
         kprof_begin(c, K_G_GEMM);
-        gemm_f64(g, c.buf[S_PARTIAL], s);
+        sym_gemm_sharded(c, g);
         kprof_end(c, K_G_GEMM);
     }
     const int over = std::max(32, k / 4);
@@ -189,11 +189,9 @@ PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d
                            0x5EEDULL + (uint64_t)n);
         TP_HIP(hipGetLastError());
         double *Yb = c.buf[S_SWEEP2].as<double>((size_t)n * b);   // 4th block buffer (sweep scratch later)
-        auto gemm_gq = [&](const double *Yin, double *Out) {
-            GemmArgs g{n, b, n, G, n, true, Yin, n, Out, n};
-            g.splitk = 0;
+        auto gemm_gq = [&](const double *Yin, double *Out) {   // Out = G Yin (row-sharded)
             kprof_begin(c, K_GQ_GEMM);
-            gemm_f64(g, c.buf[S_PARTIAL], s);
+            rows_gemm_sharded(c, G, n, n, Yin, n, b, n, Out, 0);
             kprof_end(c, K_GQ_GEMM);
         };
         auto iterate = [&](int count) {   // plain subspace iteration
@@ -295,9 +293,7 @@ PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d
             // one more pass on Q itself restores eps-orthonormality
             orth_cholqr(c, Q, Z, T, n, b, Wsm, Xinv, Yinv, d_info, 1, 1e-14);
             std::swap(Q, Z);
-            GemmArgs g2{n, b, n, G, n, true, Q, n, Z, n};
-            g2.splitk = 0;
-            gemm_f64(g2, c.buf[S_PARTIAL], s);
+            rows_gemm_sharded(c, G, n, n, Q, n, b, n, Z, 0);
             GemmArgs hq{b, b, n, Q, n, true, Z, n, Wsm, b};
             hq.sym_upper = true;
             hq.splitk = std::max(1, std::min(32, n / 128));
@@ -315,9 +311,7 @@ PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d
             gemm_f64(rq, c.buf[S_PARTIAL], s);
             std::swap(Q, Z);
             // residuals of the top k Ritz pairs: ||G v - theta v||
-            GemmArgs gy{n, k, n, G, n, true, Q, n, Z, n};
-            gy.splitk = 0;
-            gemm_f64(gy, c.buf[S_PARTIAL], s);
+            rows_gemm_sharded(c, G, n, n, Q, n, k, n, Z, 0);
             hipLaunchKernelGGL(k_resid, dim3((k + 3) / 4), dim3(256), 0, s, Z, Q, theta, n, b, k, resid);
             TP_HIP(hipGetLastError());
             TP_HIP(hipMemcpyAsync(h_res.data(), resid, k * sizeof(double), hipMemcpyDeviceToHost, s));
@@ -347,11 +341,7 @@ PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d
         TP_HIP(hipMemcpyAsync(V, Q, (size_t)n * k * sizeof(double), hipMemcpyDeviceToDevice, s));
     }
     // scores P = Xc V  (= XcT' V): n x k column-major; Pt row-major
-    {
-        GemmArgs g{n, k, n, XcT, n, true, V, n, d_P, n};
-        g.splitk = 0;
-        gemm_f64(g, c.buf[S_PARTIAL], s);
-    }
+    rows_gemm_sharded(c, XcT, n, n, V, n, k, n, d_P, 0);
     if (d_Pt) launch_transpose(d_P, n, k, n, d_Pt, k, s);
     if (h_sdev) {
         // prcomp sdev = d / sqrt(max(1, n-1)), d = singular values of Xc = sqrt(eig(G))

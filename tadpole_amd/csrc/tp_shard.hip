@@ -1,0 +1,237 @@
+// One matrix sharded over several GPUs (C5, chr1 @5kb, an
+// arm of ~24k bins).  One process (or host thread) per GPU; the ranks share an
+// RCCL communicator (xGMI) created from a unique id the host distributes
+// (tp_comm_unique_id / tp_comm_init).  Every rank holds the full matrix and
+// runs the same pipeline; only the O(N^3) / O(N^2 b) products are split:
+//
+//   S = X'X, G = Xc'Xc   upper tiles of a contiguous range of 64-column tile
+//                        columns per rank (balanced by tile count), gathered
+//                        by one in-place ncclBroadcast per owner inside a
+//                        group, then the lower triangle mirrored locally
+//   Y = G Q, P = Xc V    rows split in 64-row blocks; each rank writes its rows
+//                        transposed (b-contiguous), gathered the same way,
+//                        transposed back
+//   the sweep            PC prefixes (trees) split in contiguous ranges;
+//                        n_cluster / CH rows gathered, the chosen tree's merge
+//                        record broadcast by its owner
+//
+// Every output element is computed by the same tile code with the same K order
+// whatever the rank count (split-K is off in the sharded products), and all
+// replicated stages see identical inputs, so results are bit-identical for 1,
+// 2, 4 or 8 ranks.  A test hook (tp_set_virtual_shards) runs the same sharded
+// schedule as V shards on one device with the gathers as no-ops.
+//
+// RCCL is bound at tp_comm_init with dlopen("librccl.so.1"): in a torch
+// process that is torch's own RCCL (same SONAME), so there is one RCCL and one
+// HIP runtime per process; the library itself has no link-time dependency.
+#include <dlfcn.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include <rccl/rccl.h>
+
+#include "tp_common.cuh"
+#include "tp_internal.h"
+
+namespace tp {
+
+// ------------------------------------------------------------------ RCCL
+struct Rccl {
+    void *h = nullptr;
+    decltype(&ncclGetUniqueId) get_uid = nullptr;
+    decltype(&ncclCommInitRank) init_rank = nullptr;
+    decltype(&ncclCommDestroy) destroy = nullptr;
+    decltype(&ncclBroadcast) bcast = nullptr;
+    decltype(&ncclGroupStart) gstart = nullptr;
+    decltype(&ncclGroupEnd) gend = nullptr;
+    decltype(&ncclGetErrorString) errstr = nullptr;
+};
+static Rccl g_rccl;
+
+static Rccl &rccl() {
+    if (g_rccl.h) return g_rccl;
+    void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) fail(TP_ERR_HIP, std::string("cannot load RCCL (librccl.so.1): ") + dlerror());
+    Rccl r;
+    r.h = h;
+#define TP_SYM(f, name)                                                             \
+    r.f = (decltype(r.f))dlsym(h, name);                                            \
+    if (!r.f) fail(TP_ERR_HIP, std::string("RCCL symbol missing: ") + name);
+    TP_SYM(get_uid, "ncclGetUniqueId")
+    TP_SYM(init_rank, "ncclCommInitRank")
+    TP_SYM(destroy, "ncclCommDestroy")
+    TP_SYM(bcast, "ncclBroadcast")
+    TP_SYM(gstart, "ncclGroupStart")
+    TP_SYM(gend, "ncclGroupEnd")
+    TP_SYM(errstr, "ncclGetErrorString")
+#undef TP_SYM
+    g_rccl = r;
+    return g_rccl;
+}
+
+static void nccl_ok(ncclResult_t r, const char *what) {
+    if (r != ncclSuccess)
+        fail(TP_ERR_HIP, std::string("RCCL failure in ") + what + ": " + (g_rccl.errstr ? g_rccl.errstr(r) : "?"));
+}
+
+void comm_unique_id(char *id128) {
+    ncclUniqueId u;
+    nccl_ok(rccl().get_uid(&u), "ncclGetUniqueId");
+    static_assert(sizeof(u) == 128, "ncclUniqueId is 128 bytes");
+    memcpy(id128, &u, 128);
+}
+
+void comm_init(Ctx &c, const char *id128, int nranks, int rank) {
+    if (nranks < 1 || rank < 0 || rank >= nranks) fail(TP_ERR_ARG, "comm_init: bad rank / nranks");
+    comm_destroy(c);
+    ncclUniqueId u;
+    memcpy(&u, id128, 128);
+    ncclComm_t comm = nullptr;
+    nccl_ok(rccl().init_rank(&comm, nranks, u, rank), "ncclCommInitRank");
+    c.shard.comm = comm;
+    c.shard.rank = rank;
+    c.shard.nranks = nranks;
+}
+
+void comm_destroy(Ctx &c) {
+    if (c.shard.comm) {
+        (void)hipStreamSynchronize(c.stream);
+        rccl().destroy((ncclComm_t)c.shard.comm);
+    }
+    c.shard.comm = nullptr;
+    c.shard.rank = 0;
+    c.shard.nranks = 1;
+}
+
+// -------------------------------------------------------------- planning
+int shard_count(const Ctx &c) {
+    if (!c.shard.active) return 1;
+    return c.shard.comm ? c.shard.nranks : std::max(1, c.shard.nvirt);
+}
+bool shard_mine(const Ctx &c, int r) { return !c.shard.comm || r == c.shard.rank; }
+
+// kind 0: tile-column bounds (in 64-column tiles) of the symmetric products,
+//   balanced by upper-tile count (tile column j holds j + 1 tiles);
+// kind 1: row bounds of the row-split products, whole 64-row blocks;
+// kind 2: tree (PC prefix) bounds of the sweep.
+// bounds[0..R]: shard r covers [bounds[r], bounds[r+1]).
+void shard_plan(int n, int R, int kind, int *bounds) {
+    if (R < 1) fail(TP_ERR_ARG, "shard_plan: nranks < 1");
+    bounds[0] = 0;
+    if (kind == 0) {
+        const int tn = (n + 63) / 64;
+        const double tot = (double)tn * (tn + 1) / 2.0;
+        int j = 0;
+        double cum = 0.0;
+        for (int r = 1; r < R; ++r) {
+            const double target = tot * r / R;
+            while (j < tn && cum + (j + 1) * 0.5 <= target) {   // take column j while its midpoint fits
+                cum += j + 1;
+                ++j;
+            }
+            bounds[r] = j;
+        }
+        bounds[R] = tn;
+    } else if (kind == 1) {
+        const int nb = (n + 63) / 64;
+        for (int r = 1; r < R; ++r) bounds[r] = std::min(n, (int)(((long)nb * r / R) * 64));
+        bounds[R] = n;
+    } else {
+        for (int r = 1; r < R; ++r) bounds[r] = (int)((long)n * r / R);
+        bounds[R] = n;
+    }
+    for (int r = 1; r <= R; ++r) bounds[r] = std::max(bounds[r], bounds[r - 1]);
+}
+
+// ------------------------------------------------------------- gathers
+// The owner of each contiguous chunk [off[r], off[r+1]) (doubles) of buf sends
+// it to every rank, in place.  No-op for virtual shards / one rank.
+void shard_gather(Ctx &c, double *buf, const std::vector<size_t> &off) {
+    if (!c.shard.active || !c.shard.comm || c.shard.nranks == 1) return;
+    Rccl &R = rccl();
+    nccl_ok(R.gstart(), "ncclGroupStart");
+    for (int r = 0; r + 1 < (int)off.size(); ++r) {
+        const size_t cnt = off[r + 1] - off[r];
+        if (cnt == 0) continue;
+        nccl_ok(R.bcast(buf + off[r], buf + off[r], cnt, ncclFloat64, r, (ncclComm_t)c.shard.comm, c.cur),
+                "ncclBroadcast");
+    }
+    nccl_ok(R.gend(), "ncclGroupEnd");
+}
+void shard_gather_bytes(Ctx &c, void *buf, const std::vector<size_t> &off) {
+    if (!c.shard.active || !c.shard.comm || c.shard.nranks == 1) return;
+    Rccl &R = rccl();
+    char *b = (char *)buf;
+    nccl_ok(R.gstart(), "ncclGroupStart");
+    for (int r = 0; r + 1 < (int)off.size(); ++r) {
+        const size_t cnt = off[r + 1] - off[r];
+        if (cnt == 0) continue;
+        nccl_ok(R.bcast(b + off[r], b + off[r], cnt, ncclUint8, r, (ncclComm_t)c.shard.comm, c.cur), "ncclBroadcast");
+    }
+    nccl_ok(R.gend(), "ncclGroupEnd");
+}
+void shard_bcast_bytes(Ctx &c, void *buf, size_t bytes, int root) {
+    if (!c.shard.active || !c.shard.comm || c.shard.nranks == 1) return;
+    nccl_ok(rccl().bcast(buf, buf, bytes, ncclUint8, root, (ncclComm_t)c.shard.comm, c.cur), "ncclBroadcast");
+}
+
+// ------------------------------------------------------ sharded products
+// C = A'A-style symmetric product (g.sym_upper): each shard computes the upper
+// tiles of its tile columns; columns gathered; lower triangle mirrored.
+void sym_gemm_sharded(Ctx &c, GemmArgs g) {
+    const int R = shard_count(c);
+    if (R == 1 && !c.shard.active) {
+        gemm_f64(g, c.buf[S_PARTIAL], c.cur);
+        return;
+    }
+    if (!g.sym_upper || g.M != g.N || g.ldc != g.M) fail(TP_ERR_ARG, "sym_gemm_sharded: square packed output only");
+    const int n = g.M;
+    std::vector<int> tb(R + 1);
+    shard_plan(n, R, 0, tb.data());
+    g.splitk = 1;   // the same K order for every rank count
+    for (int r = 0; r < R; ++r) {
+        if (!shard_mine(c, r) || tb[r + 1] <= tb[r]) continue;
+        GemmArgs h = g;
+        h.tcol0 = tb[r];
+        h.tcol1 = tb[r + 1];
+        gemm_f64(h, c.buf[S_PARTIAL], c.cur);
+    }
+    std::vector<size_t> off(R + 1);
+    for (int r = 0; r <= R; ++r) off[r] = (size_t)std::min(n, tb[r] * 64) * n;
+    shard_gather(c, g.C, off);
+    launch_clean_symmetrize(g.C, n, true, c.cur);   // lower <- upper (finite: NaN->0 is a no-op)
+}
+
+// Out (M x N col-major, ld M) = A' B with A stored K x M (col-major, lda) and
+// B K x N: rows of Out split in 64-row blocks, each written transposed into
+// the packed T (N x M col-major = Out row-major), gathered, transposed back.
+void rows_gemm_sharded(Ctx &c, const double *A, int lda, int M, const double *B, int ldb, int N, int K,
+                       double *Out, int splitk_plain) {
+    if (!c.shard.active) {
+        GemmArgs g{M, N, K, A, lda, true, B, ldb, Out, M};
+        g.splitk = splitk_plain;
+        gemm_f64(g, c.buf[S_PARTIAL], c.cur);
+        return;
+    }
+    const int R = shard_count(c);
+    std::vector<int> rb(R + 1);
+    shard_plan(M, R, 1, rb.data());
+    double *T = c.buf[S_SHARD].as<double>((size_t)M * N);
+    for (int r = 0; r < R; ++r) {
+        if (!shard_mine(c, r) || rb[r + 1] <= rb[r]) continue;
+        GemmArgs g{rb[r + 1] - rb[r], N, K, A + (size_t)rb[r] * lda, lda, true, B, ldb, T + (size_t)rb[r] * N, N};
+        g.store_t = true;
+        g.splitk = 1;
+        gemm_f64(g, c.buf[S_PARTIAL], c.cur);
+    }
+    std::vector<size_t> off(R + 1);
+    for (int r = 0; r <= R; ++r) off[r] = (size_t)rb[r] * N;
+    shard_gather(c, T, off);
+    launch_transpose(T, N, M, N, Out, M, c.cur);
+}
+
+}  // namespace tp

@@ -1,0 +1,87 @@
+"""One matrix over the GPUs of one node (BASELINE.json
+configs[4]: chr1 @5kb, arms of ~24k bins).
+
+One process per GPU (``torch.distributed.run``).  Rank 0 asks the library for
+an RCCL unique id (``tp_comm_unique_id``), the 128 bytes travel over the
+default process group (gloo or nccl), and every rank binds the library's own
+RCCL communicator to its device (``tp_comm_init``).  ``TADpole(...,
+sharded=True)`` then passes ``TP_FLAG_SHARDED``: every rank holds the same
+matrix, the O(N^3) / O(N^2 b) products are split by column tiles / rows and
+all-gathered over xGMI inside the library, the sweep is split by PC prefix,
+and every rank returns the same ``tadpole`` object, bit-identical for any rank
+count.  The reference has no multi-GPU path (it forks over PC prefixes on one
+host, R/TADpole.R:104).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Callable, Optional, Tuple
+
+import numpy as np
+
+from . import _lib
+
+
+def comm_unique_id() -> bytes:
+    """RCCL unique id (128 bytes) from the library (needs RCCL, not a GPU)."""
+    L = _lib.load()
+    buf = ctypes.create_string_buffer(128)
+    st = ctypes.c_int(0)
+    L.tp_comm_unique_id(buf, ctypes.byref(st))
+    _lib.check(st)
+    return buf.raw
+
+
+def _lib_init(uid: bytes, nranks: int, rank: int, device: int) -> None:
+    L = _lib.load()
+    st = ctypes.c_int(0)
+    L.tp_comm_init(uid, ctypes.byref(ctypes.c_int(nranks)), ctypes.byref(ctypes.c_int(rank)),
+                   ctypes.byref(ctypes.c_int(device)), ctypes.byref(st))
+    _lib.check(st)
+
+
+def init_comm(device: int, group=None, uid_fn: Optional[Callable[[], bytes]] = None,
+              init_fn: Optional[Callable[[bytes, int, int, int], None]] = None) -> Tuple[int, int]:
+    """Create the library's communicator for this rank over the ranks of
+    ``group`` (default: the default process group).  ``uid_fn`` / ``init_fn``
+    replace the library calls (tests on hosts without RCCL devices)."""
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    obj = [(uid_fn or comm_unique_id)() if rank == 0 else None]
+    src = 0 if group is None else dist.get_global_rank(group, 0)
+    dist.broadcast_object_list(obj, src=src, group=group)
+    uid = obj[0]
+    if not isinstance(uid, (bytes, bytearray)) or len(uid) != 128:
+        raise RuntimeError("bad RCCL unique id from rank 0")
+    (init_fn or _lib_init)(bytes(uid), world, rank, device)
+    return rank, world
+
+
+def destroy_comm(device: int = 0) -> None:
+    _lib.load().tp_comm_destroy(ctypes.byref(ctypes.c_int(device)))
+
+
+def set_virtual_shards(nvirt: int, device: int = 0) -> None:
+    """Test hook: run sharded calls as ``nvirt`` shards on one device."""
+    L = _lib.load()
+    st = ctypes.c_int(0)
+    L.tp_set_virtual_shards(ctypes.byref(ctypes.c_int(device)), ctypes.byref(ctypes.c_int(nvirt)),
+                            ctypes.byref(st))
+    _lib.check(st)
+
+
+PLAN_TILE_COLUMNS, PLAN_ROWS, PLAN_TREES = 0, 1, 2
+
+
+def shard_plan(n: int, nranks: int, kind: int) -> np.ndarray:
+    """The library's split (host only): bounds[r]..bounds[r+1] for rank r.
+    kind 0: 64-column tiles of X'X / Xc'Xc; 1: rows of G Q / Xc V; 2: trees."""
+    L = _lib.load()
+    b = np.zeros(nranks + 1, np.int32)
+    st = ctypes.c_int(0)
+    L.tp_shard_plan(ctypes.byref(ctypes.c_int(n)), ctypes.byref(ctypes.c_int(nranks)),
+                    ctypes.byref(ctypes.c_int(kind)), _lib.ip(b), ctypes.byref(st))
+    _lib.check(st)
+    return b

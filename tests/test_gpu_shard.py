@@ -1,0 +1,78 @@
+"""One matrix sharded over several GPUs on the one-GPU box:
+
+* virtual shards (tp_set_virtual_shards): the sharded schedule -- column-tile
+  split of X'X / Xc'Xc, row split of G Q / Xc V, tree split of the sweep -- as
+  V shards on one device.  Bar: bit-identical tadpole objects for V = 1, 2, 3,
+  and, at a size where the unsharded products run without split-K (N >= 3072),
+  bit-identical to the unsharded pipeline too;
+* a real RCCL communicator of one rank (tp_comm_unique_id / tp_comm_init):
+  the same schedule through ncclBroadcast; bit-identical to V = 1.
+True multi-rank runs need several GPUs (bench.py --sharded under
+torch.distributed.run); the exchange of the unique id is covered on CPU
+(tests/test_multi.py)."""
+import numpy as np
+import pytest
+
+import tadpole_amd as tp
+from tadpole_amd import multi
+from tadpole_amd.synth import synth_hic
+
+pytestmark = pytest.mark.gpu
+
+
+def _same(a, b):
+    assert a.n_pcs == b.n_pcs and a.optimal_n_clusters == b.optimal_n_clusters
+    assert set(a.clusters) == set(b.clusters)
+    for k in a.clusters:
+        assert np.array_equal(a.clusters[k], b.clusters[k]), k
+    sa, sb = np.asarray(a.scores), np.asarray(b.scores)
+    assert sa.shape == sb.shape
+    assert np.array_equal(sa.view(np.uint64), sb.view(np.uint64))   # bit for bit, NA patterns included
+
+
+@pytest.mark.parametrize("n0,seed", [(600, 31), (3300, 32)])
+def test_virtual_shards_bit_identical(gpu, n0, seed):
+    m = synth_hic(n0, seed)
+    try:
+        multi.set_virtual_shards(1)
+        ref = tp.TADpole(m, max_pcs=200, sharded=True)
+        for v in (2, 3):
+            multi.set_virtual_shards(v)
+            _same(tp.TADpole(m, max_pcs=200, sharded=True), ref)
+    finally:
+        multi.set_virtual_shards(1)
+    if n0 >= 3100:
+        _same(tp.TADpole(m, max_pcs=200), ref)
+
+
+def test_virtual_shards_centromere_arms(gpu):
+    m = synth_hic(700, 33, centromere=True)
+    try:
+        multi.set_virtual_shards(1)
+        ref = tp.TADpole(m, max_pcs=60, centromere_search=True, sharded=True)
+        multi.set_virtual_shards(4)
+        got = tp.TADpole(m, max_pcs=60, centromere_search=True, sharded=True)
+    finally:
+        multi.set_virtual_shards(1)
+    assert np.array_equal(got.merging_arms, ref.merging_arms)
+    _same(got.p, ref.p)
+    _same(got.q, ref.q)
+
+
+def test_rccl_one_rank_communicator(gpu):
+    m = synth_hic(500, 34)
+    multi.set_virtual_shards(1)
+    ref = tp.TADpole(m, max_pcs=100, sharded=True)
+    uid = multi.comm_unique_id()
+    assert len(uid) == 128
+    import ctypes
+    from tadpole_amd import _lib
+    L = _lib.load()
+    st = ctypes.c_int(0)
+    L.tp_comm_init(uid, ctypes.byref(ctypes.c_int(1)), ctypes.byref(ctypes.c_int(0)),
+                   ctypes.byref(ctypes.c_int(0)), ctypes.byref(st))
+    _lib.check(st)
+    try:
+        _same(tp.TADpole(m, max_pcs=100, sharded=True), ref)
+    finally:
+        multi.destroy_comm(0)

@@ -78,3 +78,68 @@ def test_genome_two_ranks_gloo():
     from tadpole_amd.synth import synth_hic
     r = O.tadpole(synth_hic(120, 100), max_pcs=30, nthreads=1)
     assert got["chrA"][1:] == (r.n_pcs, r.optimal_n_clusters)
+
+
+# ------------------------------------------- one matrix over several GPUs
+# (SURVEY.md §8(e)2).  The split is host logic of the library (tp_shard_plan,
+# no device needed); the unique-id exchange runs over gloo with the library
+# calls replaced (no RCCL device here); the sharded arithmetic itself is
+# covered on the GPU by tests/test_gpu_shard.py.
+
+@pytest.mark.parametrize("n", [64, 65, 1000, 7808, 24300, 49851])
+@pytest.mark.parametrize("R", [1, 2, 3, 4, 8])
+def test_shard_plan_tile_columns_balanced(n, R):
+    from tadpole_amd import multi
+    b = multi.shard_plan(n, R, multi.PLAN_TILE_COLUMNS)
+    tn = (n + 63) // 64
+    assert b[0] == 0 and b[-1] == tn and np.all(np.diff(b) >= 0)
+    w = np.array([sum(j + 1 for j in range(b[r], b[r + 1])) for r in range(R)])
+    assert w.sum() == tn * (tn + 1) // 2
+    # every rank within one tile column of the ideal share
+    assert np.all(np.abs(w - w.sum() / R) <= tn + 1)
+
+
+@pytest.mark.parametrize("n,R", [(24300, 8), (3300, 3), (100, 4), (7808, 2)])
+def test_shard_plan_rows_and_trees(n, R):
+    from tadpole_amd import multi
+    r = multi.shard_plan(n, R, multi.PLAN_ROWS)
+    assert r[0] == 0 and r[-1] == n and np.all(np.diff(r) >= 0)
+    assert all(x % 64 == 0 for x in r[:-1])
+    t = multi.shard_plan(200, R, multi.PLAN_TREES)
+    assert t[0] == 0 and t[-1] == 200 and np.all(np.diff(t) >= 0) and np.diff(t).max() - np.diff(t).min() <= 1
+
+
+def _comm_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from tadpole_amd import multi
+    seen = []
+    uid = bytes(range(128))
+
+    def uid_fn():
+        assert dist.get_rank() == 0, "only rank 0 makes the id"
+        return uid
+
+    def init_fn(u, nranks, r, device):
+        seen.append((u == uid, nranks, r, device))
+
+    rr, ww = multi.init_comm(device=rank, uid_fn=uid_fn, init_fn=init_fn)
+    out.put((rank, rr, ww, seen))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_comm_unique_id_exchange_two_ranks_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_comm_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = sorted(q.get(timeout=120) for _ in range(2))
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    for rank, rr, ww, seen in got:
+        assert (rr, ww) == (rank, 2)
+        assert seen == [(True, 2, rank, rank)]
