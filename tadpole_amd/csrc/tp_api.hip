@@ -1069,4 +1069,38 @@ void tp_debug_sytrd(const double *H, const int *b, double *ms, long long *stamps
         (void)hipEventDestroy(e1);
     });
 }
+/* one tridiagonalisation of H (b x b, lower triangle used) by k_sytrd_l
+ * (which 0) or k_sytrd_reg (which 1): d[b], e[b-1], tau[b-1], Aout = A with
+ * the reflectors below the subdiagonal; ms[0] = kernel time (mean of 3). */
+void tp_debug_sytrd2(const double *H, const int *b, const int *which, double *ms, double *d, double *e, double *tau,
+                     double *Aout, int *status) {
+    guarded(status, [&] {
+        Ctx &c = ctx_for(0);
+        hipStream_t s = c.cur;
+        const int B = *b;
+        double *dA = c.buf[S_SMALL].as<double>((size_t)B * B + 64);
+        double *dWork = c.buf[S_PARTIAL].as<double>((size_t)4 * B + 64);
+        hipEvent_t e0, e1;
+        TP_HIP(hipEventCreate(&e0));
+        TP_HIP(hipEventCreate(&e1));
+        float tot = 0;
+        for (int r = 0; r < 3; ++r) {
+            TP_HIP(hipMemcpyAsync(dA, H, (size_t)B * B * 8, hipMemcpyHostToDevice, s));
+            TP_HIP(hipEventRecord(e0, s));
+            sytrd_which(dA, B, dWork, *which, s);
+            TP_HIP(hipEventRecord(e1, s));
+            TP_HIP(hipEventSynchronize(e1));
+            float t = 0;
+            TP_HIP(hipEventElapsedTime(&t, e0, e1));
+            tot += t;
+        }
+        ms[0] = tot / 3;
+        TP_HIP(hipMemcpy(Aout, dA, (size_t)B * B * 8, hipMemcpyDeviceToHost));
+        TP_HIP(hipMemcpy(e, dWork, (size_t)(B > 1 ? B - 1 : 1) * 8, hipMemcpyDeviceToHost));
+        TP_HIP(hipMemcpy(tau, dWork + B, (size_t)(B > 1 ? B - 1 : 1) * 8, hipMemcpyDeviceToHost));
+        TP_HIP(hipMemcpy(d, dWork + 2 * B, (size_t)B * 8, hipMemcpyDeviceToHost));
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+    });
+}
 }  // extern "C"

@@ -606,7 +606,7 @@ __global__ void __launch_bounds__(256) k_trsm_frag(const double *__restrict__ Z,
                 }
             }
         }
-        __syncthreads();
+        lds_barrier();
 #pragma unroll
         for (int s = 0; s < S; ++s) {
             const int J = 4 * s + w;

@@ -108,6 +108,15 @@ __device__ __forceinline__ void wave_dd_sum(double &hi, double &lo) {
     }
 }
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS
+// operations, not for its outstanding global stores (__syncthreads' release
+// fence waits for those too -- a full HBM write latency per barrier in loops
+// that stream results out).  Only for data exchanged through LDS; global data
+// written before it is NOT visible to other waves after it.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // total order on doubles as unsigned keys (radix select)
 __device__ __forceinline__ uint64_t dkey(double x) {
     uint64_t u = (uint64_t)__double_as_longlong(x);

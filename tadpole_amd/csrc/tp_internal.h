@@ -167,7 +167,10 @@ void launch_transpose(const double *d_A, int rows, int cols, int lda, double *d_
 // triangle) <- eigenvectors, theta <- ascending eigenvalues.  work >= b*b + 4b + 8.
 // method 0: tridiagonal stage by rocSOLVER dstedc, 1: bisection + inverse iteration.
 bool eig_sym_supported(int b);
+extern int g_sytrd_reg;
 void sytrd_stamped(double *A, int b, double *work, long long *d_stamps, hipStream_t s);
+void sytrd_which(double *A, int b, double *work, int which, hipStream_t s,
+                 long long *d_stamps = nullptr);   // work: 3b (e, tau, d)
 void eig_sym(rocblas_handle h, double *A, int b, double *theta, double *work, int *info, hipStream_t s,
              int method = 1);
 

@@ -136,6 +136,7 @@ def _spectrum(kind, b, rng):
 
 @pytest.mark.parametrize("b,kind", [(1, "graded"), (2, "indefinite"), (3, "graded"), (5, "clustered"),
                                     (64, "graded"), (200, "rankdef"), (256, "graded"), (256, "clustered"),
+                                    (16, "graded"), (240, "clustered"), (208, "rankdef"),
                                     (300, "graded"), (512, "graded")])
 def test_eigsym(gpu, b, kind):
     rng = np.random.default_rng(b * 7 + len(kind))
@@ -186,6 +187,53 @@ def test_chol_inv_register_kernel(gpu, b, cond, rel):
     np.testing.assert_allclose(dg, np.diag(Uref), rtol=100 * b * 2.2e-16 * np.sqrt(kap))
     print(f"chol_inv b={b}: chol {ms[0] * 1e3:.1f} us (16 waves), {ms[2] * 1e3:.1f} us (8 waves), "
           f"trsm {ms[6] * 1e3:.1f} us; cycles prologue {ms[3]:.0f} factor {ms[4]:.0f} diag {ms[5]:.0f}")
+
+
+def _q_from_reflectors(A, tau, b):
+    """Q = H_0 H_1 ... H_{b-3} (LAPACK dsytrd 'L' storage: u[j+1] = 1,
+    u[r] = A[r, j] for r >= j+2)."""
+    Q = np.eye(b)
+    for j in range(b - 3, -1, -1):
+        u = np.zeros(b)
+        u[j + 1] = 1.0
+        u[j + 2:] = A[j + 2:, j]
+        Q = Q - tau[j] * np.outer(u, u @ Q)
+    return Q
+
+
+@pytest.mark.parametrize("b,which", [(16, 1), (48, 1), (208, 1), (240, 1), (256, 1), (256, 0), (96, 1)])
+def test_sytrd_kernels(gpu, b, which):
+    """Tridiagonalisation kernels of the Rayleigh-Ritz eigensolver: Q'HQ = T
+    with Q from the stored reflectors (bar ~ b eps |H|) and Q orthogonal;
+    which = 1: the register-resident kernel, 0: the L2-resident one."""
+    import ctypes
+    rng = np.random.default_rng(b)
+    h = rng.standard_normal((b, b))
+    h = np.asfortranarray(h + h.T)
+    hl = np.asfortranarray(np.tril(h))   # only the lower triangle is read
+    d = np.zeros(b); e = np.zeros(b); tau = np.zeros(b)
+    A = np.zeros((b, b), order="F")
+    ms = np.zeros(8)
+    st = ctypes.c_int(0)
+    D = ctypes.POINTER(ctypes.c_double)
+    gpu.tp_debug_sytrd2(hl.ctypes.data_as(D), ctypes.byref(ctypes.c_int(b)), ctypes.byref(ctypes.c_int(which)),
+                        ms.ctypes.data_as(D), d.ctypes.data_as(D), e.ctypes.data_as(D), tau.ctypes.data_as(D),
+                        A.ctypes.data_as(D), ctypes.byref(st))
+    assert st.value == 0
+    Q = _q_from_reflectors(A, tau, b)
+    Tm = np.diag(d) + np.diag(e[:b - 1], 1) + np.diag(e[:b - 1], -1)
+    scale = np.abs(h).max()
+    print(f"sytrd b={b} kernel={'reg' if which else 'l2'}: {ms[0] * 1e3:.1f} us")
+    # run-to-run determinism (three more calls, identical bits)
+    for _ in range(3):
+        d2 = np.zeros(b); e2 = np.zeros(b); t2 = np.zeros(b); A2 = np.zeros((b, b), order="F")
+        gpu.tp_debug_sytrd2(hl.ctypes.data_as(D), ctypes.byref(ctypes.c_int(b)), ctypes.byref(ctypes.c_int(which)),
+                            ms.ctypes.data_as(D), d2.ctypes.data_as(D), e2.ctypes.data_as(D),
+                            t2.ctypes.data_as(D), A2.ctypes.data_as(D), ctypes.byref(st))
+        assert st.value == 0
+        assert np.array_equal(d2, d) and np.array_equal(e2, e) and np.array_equal(t2, tau) and np.array_equal(A2, A)
+    assert np.abs(Q.T @ h @ Q - Tm).max() <= 200 * b * 2.2e-16 * scale
+    assert np.abs(Q.T @ Q - np.eye(b)).max() <= 100 * b * 2.2e-16
 
 
 # ---------------------------------------------------------- coniss / dist
