@@ -391,10 +391,8 @@ static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_cl
     double *S = c.buf[S_S].as<double>((size_t)n * n);
     double *C = c.buf[S_C].as<double>((size_t)n * n);
     {
-        GemmArgs g{n, n, n, X, n, true, X, n, S, n};
-        g.sym_upper = true;
         kprof_begin(c, K_COR_GEMM);
-        sym_gemm_sharded(c, g);
+        xtx_product(c, X, n, S);
         kprof_end(c, K_COR_GEMM);
     }
     launch_cor_epilogue(S, m, n, C, s);
@@ -556,9 +554,7 @@ void tp_cor(const double *X, const int *n, const int *device, double *cor, int *
         launch_colmean(dX, N, N, m, s);
         double *S = c.buf[S_S].as<double>((size_t)N * N);
         double *C = c.buf[S_C].as<double>((size_t)N * N);
-        GemmArgs g{N, N, N, dX, N, true, dX, N, S, N};
-        g.sym_upper = true;
-        gemm_f64(g, c.buf[S_PARTIAL], s);
+        xtx_product(c, dX, N, S);
         launch_cor_epilogue(S, m, N, C, s);
         TP_HIP(hipMemcpyAsync(cor, C, (size_t)N * N * 8, hipMemcpyDeviceToHost, s));
         TP_HIP(hipStreamSynchronize(s));
@@ -1101,6 +1097,53 @@ void tp_debug_sytrd2(const double *H, const int *b, const int *which, double *ms
         TP_HIP(hipMemcpy(d, dWork + 2 * B, (size_t)B * 8, hipMemcpyDeviceToHost));
         (void)hipEventDestroy(e0);
         (void)hipEventDestroy(e1);
+    });
+}
+}  // extern "C"
+
+extern "C" {
+/* S = X'X (n x n, column-major in and out) by mode 0 = fp64 MFMA GEMM, 1 = the
+ * int8-exact path (fails with TP_ERR_ARG when X is not non-negative integer
+ * counts below 2^21); *slices = slices used (0 for fp64); ms = mean of 3. */
+void tp_debug_xtx(const double *X, const int *n, const int *mode, double *S, int *slices, double *ms,
+                  int *status) {
+    guarded(status, [&] {
+        Ctx &c = ctx_for(0);
+        hipStream_t s = c.cur;
+        const int N = *n;
+        double *dX = c.buf[S_X].as<double>((size_t)N * N);
+        double *dS = c.buf[S_S].as<double>((size_t)N * N);
+        TP_HIP(hipMemcpyAsync(dX, X, (size_t)N * N * 8, hipMemcpyHostToDevice, s));
+        int ns = 0;
+        if (*mode == 1) {
+            ns = xtx_int_slices(c, dX, N);
+            if (ns == 0) fail(TP_ERR_ARG, "X is not non-negative integer counts < 2^21");
+        }
+        hipEvent_t e0, e1;
+        TP_HIP(hipEventCreate(&e0));
+        TP_HIP(hipEventCreate(&e1));
+        float tot = 0;
+        for (int r = 0; r < 3; ++r) {
+            TP_HIP(hipEventRecord(e0, s));
+            if (ns) {
+                const int8_t *sl = xtx_slices(c, dX, N, ns);
+                xtx_int8_tiles(c, sl, N, ns, dS, 0, -1);
+            } else {
+                GemmArgs g{N, N, N, dX, N, true, dX, N, dS, N};
+                g.sym_upper = true;
+                gemm_f64(g, c.buf[S_PARTIAL], s);
+            }
+            TP_HIP(hipEventRecord(e1, s));
+            TP_HIP(hipEventSynchronize(e1));
+            float t = 0;
+            TP_HIP(hipEventElapsedTime(&t, e0, e1));
+            tot += t;
+        }
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        *ms = tot / 3;
+        *slices = ns;
+        TP_HIP(hipMemcpy(S, dS, (size_t)N * N * 8, hipMemcpyDeviceToHost));
     });
 }
 }  // extern "C"

@@ -192,6 +192,15 @@ void sym_gemm_sharded(Ctx &c, GemmArgs g);
 void rows_gemm_sharded(Ctx &c, const double *A, int lda, int M, const double *B, int ldb, int N, int K,
                        double *Out, int splitk_plain);
 
+// exact X'X on int8 matrix cores for integer counts (tp_xtx.hip)
+extern int g_xtx_int8;
+int xtx_int_slices(Ctx &c, const double *d_X, int n);   // 0 = not integer counts (fp64 path)
+const int8_t *xtx_slices(Ctx &c, const double *d_X, int n, int ns);
+void xtx_int8_tiles(Ctx &c, const int8_t *sl, int n, int ns, double *d_S, int tc0, int tc1);   // 64-col tiles
+void xtx_int8_tiles128(Ctx &c, const int8_t *sl, int n, int ns, double *d_S, int tc0, int tc1);
+// S = X'X by the exact int8 path when possible, sharded like sym_gemm_sharded
+void xtx_product(Ctx &c, const double *d_X, int n, double *d_S);
+
 struct PcaStats { int iters = 0; double resid = 0; double rate = 0; int block = 0; int blocks = 0; };
 PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d_Pt,
                  double *h_sdev);

@@ -206,6 +206,40 @@ void sym_gemm_sharded(Ctx &c, GemmArgs g) {
     launch_clean_symmetrize(g.C, n, true, c.cur);   // lower <- upper (finite: NaN->0 is a no-op)
 }
 
+// S = X'X: int8-exact for integer counts, else the fp64 MFMA product; split by
+// tile columns over the shards exactly as sym_gemm_sharded.
+void xtx_product(Ctx &c, const double *X, int n, double *S) {
+    const int ns = xtx_int_slices(c, X, n);
+    if (ns == 0) {
+        GemmArgs g{n, n, n, X, n, true, X, n, S, n};
+        g.sym_upper = true;
+        sym_gemm_sharded(c, g);
+        return;
+    }
+    const int8_t *sl = xtx_slices(c, X, n, ns);
+    // 128-column tiles (the LDS-staged kernel) for n >= 1024 and <= 2 slices,
+    // else 64-column tiles; the products are exact, so any split gives the same bits
+    const bool big = n >= 1024 && ns <= 2;
+    const int tw = big ? 128 : 64;
+    auto tiles = [&](int t0, int t1) {
+        if (big) xtx_int8_tiles128(c, sl, n, ns, S, t0, t1);
+        else xtx_int8_tiles(c, sl, n, ns, S, t0, t1);
+    };
+    if (!c.shard.active) {
+        tiles(0, -1);
+        return;
+    }
+    const int R = shard_count(c);
+    std::vector<int> tb(R + 1);
+    shard_plan((n + tw / 64 - 1) / (tw / 64), R, 0, tb.data());   // kind 0 counts 64-wide tiles
+    for (int r = 0; r < R; ++r)
+        if (shard_mine(c, r)) tiles(tb[r], tb[r + 1]);
+    std::vector<size_t> off(R + 1);
+    for (int r = 0; r <= R; ++r) off[r] = (size_t)std::min(n, tb[r] * tw) * n;
+    shard_gather(c, S, off);
+    launch_clean_symmetrize(S, n, true, c.cur);
+}
+
 // Out (M x N col-major, ld M) = A' B with A stored K x M (col-major, lda) and
 // B K x N: rows of Out split in 64-row blocks, each written transposed into
 // the packed T (N x M col-major = Out row-major), gathered, transposed back.

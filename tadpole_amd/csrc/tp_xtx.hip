@@ -1,0 +1,323 @@
+// S = X'X (crossprod in sparse_cor, R/TADpole.R:96) EXACTLY on the int8 matrix
+// cores when X holds non-negative integer counts (raw Hi-C contact matrices).
+//
+// Each count x < 2^(7 ns) is split into ns 7-bit slices x = sum_s 2^(7s) x_s,
+// x_s in [0, 127] (a valid signed int8), so
+//     X'X = sum_{s,t} 2^(7(s+t)) X_s' X_t
+// and every X_s' X_t is an int8 GEMM with int32 accumulation, exact while
+// K * 127^2 < 2^31 (K < 133 000 bins).  The ns^2 partial products of a tile are
+// combined in int64 and converted to double once: S is the correctly rounded
+// exact product -- as close to R's dsyrk as the fp64 MFMA product is (both
+// differ from it only by rounding), and bit-identical for any tiling or rank
+// count.  ns = 2 (counts < 16384) costs 4 int8 products at ~32x the fp64
+// MFMA rate each.  Inputs that are not integer counts (balanced / normalised
+// matrices) take the fp64 MFMA path (tp_gemm.hip).
+//
+// Layout: slices are column-major int8 with K padded to a multiple of 64 and
+// columns to a multiple of 64 (zero padding), so a fragment load is one
+// aligned 16-byte load.  The MFMA operand k order is irrelevant here: A and B
+// fragments are loaded with the same k pattern and the product sums over k.
+// C/D: col = lane & 15, row = 4 (lane >> 4) + reg (cdna_hip_programming.md §3).
+#include "tp_common.cuh"
+#include "tp_internal.h"
+
+#include <algorithm>
+#include <cstring>
+
+namespace tp {
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+// max over X and a flag for entries that are not non-negative integers: one
+// workgroup per CU-sized chunk, reduced in LDS, ONE atomic per workgroup (a
+// per-wave atomic on one address from thousands of waves serialised at L2).
+__global__ void __launch_bounds__(256) k_int_scan(const double *X, size_t cnt, unsigned long long *maxbits,
+                                                  int *notint) {
+    __shared__ double wm[4];
+    __shared__ int wb[4];
+    double m = 0.0;
+    int bad = 0;
+    const size_t n2 = cnt / 2;
+    const double2 *X2 = (const double2 *)X;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n2; i += (size_t)gridDim.x * blockDim.x) {
+        const double2 v = X2[i];
+        bad |= !(v.x >= 0.0) || v.x != floor(v.x) || !(v.y >= 0.0) || v.y != floor(v.y);
+        m = fmax(m, fmax(v.x, v.y));
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0 && (cnt & 1)) {
+        const double x = X[cnt - 1];
+        bad |= !(x >= 0.0) || x != floor(x);
+        m = fmax(m, x);
+    }
+    for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
+    const int anyb = __ballot(bad) != 0ULL;
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        wm[w] = m;
+        wb[w] = anyb;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const double mm = fmax(fmax(wm[0], wm[1]), fmax(wm[2], wm[3]));
+        // non-negative doubles order like their bit patterns
+        atomicMax(maxbits, (unsigned long long)__double_as_longlong(mm));
+        if (wb[0] | wb[1] | wb[2] | wb[3]) atomicOr(notint, 1);
+    }
+}
+
+// slice s of column c, rows k..k+3: one thread, four contiguous doubles in,
+// one 4-byte word per slice out
+__global__ void __launch_bounds__(256) k_slice_i8(const double *X, int n, int Kp, int Np, int ns, int8_t *S) {
+    const int c = blockIdx.y;
+    const int k = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    if (k >= Kp) return;
+    unsigned v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = (c < n && k + u < n) ? (unsigned)X[(size_t)c * n + k + u] : 0u;
+    for (int s = 0; s < ns; ++s) {
+        unsigned w = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) w |= ((v[u] >> (7 * s)) & 127u) << (8 * u);
+        *(unsigned *)(S + (size_t)s * Np * Kp + (size_t)c * Kp + k) = w;
+    }
+}
+
+// Upper 64 x 64 tiles (tile column tcol0 onward, column by column, as the fp64
+// symmetric kernel), 4 waves of 32 x 32 (2 x 2 MFMA tiles), NS^2 products per
+// tile; fragments straight from global memory (L2 / MALL resident slices).
+template <int NS>
+__global__ void __launch_bounds__(256) k_xtx_i8(const int8_t *__restrict__ S, int n, int Kp, int Np,
+                                                double *__restrict__ C, int tcol0) {
+    int id = blockIdx.x, bn = tcol0;
+    while (id > bn) {
+        id -= bn + 1;
+        ++bn;
+    }
+    const int bm = id;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int i0 = bm * 64 + (w & 1) * 32, j0 = bn * 64 + (w >> 1) * 32;
+    const int fr = lane & 15, fk = (lane >> 4) * 16;
+    i32x4 acc[NS][NS][2][2];
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int t = 0; t < NS; ++t)
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b) acc[s][t][a][b] = i32x4{0, 0, 0, 0};
+    const size_t slice = (size_t)Np * Kp;
+    const int8_t *pa = S + (size_t)(i0 + fr) * Kp + fk;
+    const int8_t *pb = S + (size_t)(j0 + fr) * Kp + fk;
+    for (int kb = 0; kb < Kp; kb += 64) {
+        i32x4 fa[NS][2], fb[NS][2];
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+            for (int a = 0; a < 2; ++a) {
+                fa[s][a] = *(const i32x4 *)(pa + s * slice + (size_t)a * 16 * Kp + kb);
+                fb[s][a] = *(const i32x4 *)(pb + s * slice + (size_t)a * 16 * Kp + kb);
+            }
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+            for (int t = 0; t < NS; ++t)
+#pragma unroll
+                for (int a = 0; a < 2; ++a)
+#pragma unroll
+                    for (int b = 0; b < 2; ++b)
+                        acc[s][t][a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[s][a], fb[t][b], acc[s][t][a][b],
+                                                                                0, 0, 0);
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = i0 + 16 * a + (lane >> 4) * 4 + r;
+                const int j = j0 + 16 * b + fr;
+                if (i >= n || j >= n || i > j) continue;
+                long long v = 0;
+#pragma unroll
+                for (int s = 0; s < NS; ++s)
+#pragma unroll
+                    for (int t = 0; t < NS; ++t) v += (long long)acc[s][t][a][b][r] << (7 * (s + t));
+                const double d = (double)v;
+                C[(size_t)i + (size_t)j * n] = d;
+                C[(size_t)j + (size_t)i * n] = d;
+            }
+}
+
+// Large problems: 128 x 128 upper tiles per 8-wave workgroup (waves 2 x 4 of
+// 64 x 32, 4 x 2 MFMA tiles each), k-blocks of 64 staged through LDS
+// (double-buffered, one barrier per block) so each slice fragment is read
+// from L2 once per workgroup instead of once per wave.  LDS rows are 80 B
+// (64 B of k + pad) per column.  Same exact arithmetic as k_xtx_i8.
+constexpr int XB = 128, XK = 64, XLD = 80;
+template <int NS>
+__global__ void __launch_bounds__(512) k_xtx_i8_big(const int8_t *__restrict__ S, int n, int Kp, int Np,
+                                                    double *__restrict__ C, int tcol0) {
+    __shared__ __attribute__((aligned(16))) int8_t Ls[2][2][NS][XB * XLD];   // [buf][A/B][slice]
+    int id = blockIdx.x, bn = tcol0;
+    while (id > bn) {
+        id -= bn + 1;
+        ++bn;
+    }
+    const int bm = id;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int wm = (w & 1) * 64, wn = (w >> 1) * 32;
+    const size_t slice = (size_t)Np * Kp;
+    const int ia = bm * XB, jb = bn * XB;
+    // global -> LDS: per (operand, slice) 128 columns x 64 bytes = 512 x 16 B,
+    // one 16-byte load per thread
+    const int lc = t >> 2, lk = (t & 3) * 16;
+    auto gload = [&](i32x4 (&r)[2][NS], int kb) {
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const int ca = min(ia + lc, Np - 1), cb = min(jb + lc, Np - 1);
+            r[0][s] = *(const i32x4 *)(S + s * slice + (size_t)ca * Kp + kb + lk);
+            r[1][s] = *(const i32x4 *)(S + s * slice + (size_t)cb * Kp + kb + lk);
+        }
+    };
+    auto lstore = [&](int buf, const i32x4 (&r)[2][NS]) {
+#pragma unroll
+        for (int o = 0; o < 2; ++o)
+#pragma unroll
+            for (int s = 0; s < NS; ++s) *(i32x4 *)(&Ls[buf][o][s][lc * XLD + lk]) = r[o][s];
+    };
+    i32x4 acc[NS][NS][4][2];
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int u = 0; u < NS; ++u)
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b) acc[s][u][a][b] = i32x4{0, 0, 0, 0};
+    i32x4 rg[2][NS];
+    gload(rg, 0);
+    lstore(0, rg);
+    __syncthreads();
+    const int fr = lane & 15, fk = (lane >> 4) * 16;
+    int buf = 0;
+    for (int kb = 0; kb < Kp; kb += XK) {
+        const bool more = kb + XK < Kp;
+        if (more) gload(rg, kb + XK);
+        i32x4 fa[NS][4], fb[NS][2];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+#pragma unroll
+            for (int a = 0; a < 4; ++a) fa[s][a] = *(const i32x4 *)(&Ls[buf][0][s][(wm + 16 * a + fr) * XLD + fk]);
+#pragma unroll
+            for (int b = 0; b < 2; ++b) fb[s][b] = *(const i32x4 *)(&Ls[buf][1][s][(wn + 16 * b + fr) * XLD + fk]);
+        }
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+            for (int u = 0; u < NS; ++u)
+#pragma unroll
+                for (int a = 0; a < 4; ++a)
+#pragma unroll
+                    for (int b = 0; b < 2; ++b)
+                        acc[s][u][a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[s][a], fb[u][b], acc[s][u][a][b],
+                                                                                0, 0, 0);
+        if (more) lstore(buf ^ 1, rg);
+        __syncthreads();
+        buf ^= 1;
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = ia + wm + 16 * a + (lane >> 4) * 4 + r;
+                const int j = jb + wn + 16 * b + fr;
+                if (i >= n || j >= n || i > j) continue;
+                long long v = 0;
+#pragma unroll
+                for (int s = 0; s < NS; ++s)
+#pragma unroll
+                    for (int u = 0; u < NS; ++u) v += (long long)acc[s][u][a][b][r] << (7 * (s + u));
+                const double d = (double)v;
+                C[(size_t)i + (size_t)j * n] = d;
+                C[(size_t)j + (size_t)i * n] = d;
+            }
+}
+
+// Decide the path for X (n x n, col-major, device): 0 = fp64, else the slice count.
+int xtx_int_slices(Ctx &c, const double *d_X, int n) {
+    if (g_xtx_int8 == 0 || n > 130000) return 0;
+    unsigned long long *mb = (unsigned long long *)c.buf[S_SHARD2].as<char>(64);
+    int *flag = (int *)(mb + 1);
+    TP_HIP(hipMemsetAsync(mb, 0, 16, c.cur));
+    const size_t cnt = (size_t)n * n;
+    const unsigned g = (unsigned)std::max<size_t>(1, std::min<size_t>(512, (cnt / 2 + 255) / 256));
+    hipLaunchKernelGGL(k_int_scan, dim3(g), dim3(256), 0, c.cur, d_X, cnt, mb, flag);
+    TP_HIP(hipGetLastError());
+    unsigned long long h[2] = {0, 0};
+    TP_HIP(hipMemcpyAsync(h, mb, 16, hipMemcpyDeviceToHost, c.cur));
+    TP_HIP(hipStreamSynchronize(c.cur));
+    if ((int)h[1]) return 0;
+    double mx;
+    memcpy(&mx, &h[0], 8);
+    if (mx < 128.0) return 1;
+    if (mx < 16384.0) return 2;
+    if (mx < 2097152.0) return 3;
+    return 0;
+}
+
+// Slice column stride: whole 64-byte k-blocks, an ODD number of them, so
+// consecutive columns do not all start on the same HBM channel / L2 set (a
+// power-of-two stride such as 2048 B at n = 2000 ran 3x slower).
+static int xtx_kp(int n) {
+    const int blocks = (n + 63) / 64;
+    return 64 * (blocks | 1);
+}
+
+// int8 slices of X (device scratch, valid until the next call)
+const int8_t *xtx_slices(Ctx &c, const double *d_X, int n, int ns) {
+    const int Kp = xtx_kp(n), Np = (n + 127) / 128 * 128;
+    int8_t *sl = c.buf[S_SHARD2].as<int8_t>((size_t)ns * Np * Kp + 64) + 64;
+    dim3 g((unsigned)((Kp / 4 + 255) / 256), (unsigned)Np);
+    hipLaunchKernelGGL(k_slice_i8, g, dim3(256), 0, c.cur, d_X, n, Kp, Np, ns, sl);
+    TP_HIP(hipGetLastError());
+    return sl;
+}
+
+// S (n x n) = X'X exactly on the upper tiles of tile columns [tc0, tc1) and
+// their mirrors, from ns slices.
+// 128-column tiles [tc0, tc1) (tile units of 128) by the LDS-staged kernel
+void xtx_int8_tiles128(Ctx &c, const int8_t *sl, int n, int ns, double *d_S, int tc0, int tc1) {
+    const int Kp = xtx_kp(n), Np = (n + 127) / 128 * 128;
+    const int tn = Np / 128;
+    tc0 = std::max(0, tc0);
+    tc1 = tc1 < 0 ? tn : std::min(tn, tc1);
+    if (tc1 <= tc0) return;
+    const unsigned nb = (unsigned)((long)tc1 * (tc1 + 1) / 2 - (long)tc0 * (tc0 + 1) / 2);
+    if (ns == 1) hipLaunchKernelGGL(k_xtx_i8_big<1>, dim3(nb), dim3(512), 0, c.cur, sl, n, Kp, Np, d_S, tc0);
+    else if (ns == 2) hipLaunchKernelGGL(k_xtx_i8_big<2>, dim3(nb), dim3(512), 0, c.cur, sl, n, Kp, Np, d_S, tc0);
+    else fail(TP_ERR_ARG, "xtx_int8_tiles128: 1..2 slices");
+    TP_HIP(hipGetLastError());
+}
+
+void xtx_int8_tiles(Ctx &c, const int8_t *sl, int n, int ns, double *d_S, int tc0, int tc1) {
+    const int Kp = xtx_kp(n), Np = (n + 127) / 128 * 128;
+    const int tn = Kp / 64;
+    tc0 = std::max(0, tc0);
+    tc1 = tc1 < 0 ? tn : std::min(tn, tc1);
+    if (tc1 <= tc0) return;
+    const long nblk = (long)tc1 * (tc1 + 1) / 2 - (long)tc0 * (tc0 + 1) / 2;
+    switch (ns) {
+        case 1: hipLaunchKernelGGL(k_xtx_i8<1>, dim3((unsigned)nblk), dim3(256), 0, c.cur, sl, n, Kp, Np, d_S, tc0); break;
+        case 2: hipLaunchKernelGGL(k_xtx_i8<2>, dim3((unsigned)nblk), dim3(256), 0, c.cur, sl, n, Kp, Np, d_S, tc0); break;
+        case 3: hipLaunchKernelGGL(k_xtx_i8<3>, dim3((unsigned)nblk), dim3(256), 0, c.cur, sl, n, Kp, Np, d_S, tc0); break;
+        default: fail(TP_ERR_ARG, "xtx_int8: 1..3 slices");
+    }
+    TP_HIP(hipGetLastError());
+}
+
+int g_xtx_int8 = 1;   // 0: always the fp64 MFMA product (diagnostics / tests)
+
+}  // namespace tp

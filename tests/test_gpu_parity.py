@@ -383,3 +383,47 @@ def test_pipeline_errors(gpu):
     import tadpole_amd as tp
     with pytest.raises(tp.TadpoleError):
         tp.TADpole(np.zeros((10, 10)))         # everything bad
+
+
+# ------------------------------------------------------ X'X int8-exact path
+
+def _xtx(gpu, x, mode):
+    import ctypes
+    n = x.shape[0]
+    xf = np.asfortranarray(x, np.float64)
+    S = np.zeros((n, n), order="F")
+    ns = ctypes.c_int(-1); ms = ctypes.c_double(0); st = ctypes.c_int(0)
+    D = ctypes.POINTER(ctypes.c_double)
+    gpu.tp_debug_xtx(xf.ctypes.data_as(D), ctypes.byref(ctypes.c_int(n)), ctypes.byref(ctypes.c_int(mode)),
+                     S.ctypes.data_as(D), ctypes.byref(ns), ctypes.byref(ms), ctypes.byref(st))
+    return S, ns.value, ms.value, st.value
+
+
+@pytest.mark.parametrize("n,maxv,slices", [(64, 100, 1), (200, 5000, 2), (515, 16383, 2), (1000, 3000, 2),
+                                           (333, 2_000_000, 3), (2000, 4000, 2), (1100, 120, 1),
+                                           (1500, 16000, 2), (4100, 9000, 2)])
+def test_xtx_int8_exact(gpu, n, maxv, slices):
+    """sparse_cor's crossprod (R/TADpole.R:96) on the int8 matrix cores: for
+    integer counts the product is EXACT -- equal to numpy's int64 X'X rounded
+    once to double -- and symmetric; ragged n (not a multiple of 64)."""
+    rng = np.random.default_rng(n + maxv)
+    x = rng.integers(0, maxv, size=(n, n)).astype(np.float64)
+    x[0, 0] = maxv - 1
+    S, ns, ms, st = _xtx(gpu, x, 1)
+    assert st == 0 and ns == slices
+    xi = x.astype(np.int64)
+    ref = (xi.T @ xi).astype(np.float64)
+    assert np.array_equal(S, ref)
+    S64, _, ms64, st64 = _xtx(gpu, x, 0)
+    assert st64 == 0
+    assert np.max(np.abs(S64 - ref) / np.maximum(ref, 1)) < 1e-13
+    print(f"xtx n={n} slices={ns}: int8 {ms * 1e3:.1f} us, fp64 {ms64 * 1e3:.1f} us")
+
+
+def test_xtx_int8_rejects_non_counts(gpu):
+    x = np.random.default_rng(0).random((100, 100))
+    _, _, _, st = _xtx(gpu, x, 1)
+    assert st == 1
+    x = -np.ones((80, 80))
+    _, _, _, st = _xtx(gpu, x, 1)
+    assert st == 1
