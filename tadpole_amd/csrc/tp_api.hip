@@ -1147,3 +1147,40 @@ void tp_debug_xtx(const double *X, const int *n, const int *mode, double *S, int
     });
 }
 }  // extern "C"
+
+extern "C" {
+/* C = A'B (trans_a) or AB, fp64 MFMA, kernel 0 = 64 x 64 tiles, 1 = 128 x 128
+ * tiles (both without split-K); sym = upper tiles mirrored (M == N). */
+void tp_debug_gemm(const double *A, const double *B, const int *M, const int *N, const int *K, const int *trans_a,
+                   const int *sym, const int *kernel, double *C, double *ms, int *status) {
+    guarded(status, [&] {
+        Ctx &c = ctx_for(0);
+        hipStream_t s = c.cur;
+        const int m = *M, n = *N, k = *K;
+        const bool ta = *trans_a != 0;
+        const size_t na = (size_t)m * k, nb = (size_t)k * n, nc = (size_t)m * n;
+        double *dA = c.buf[S_X].as<double>(na), *dB = c.buf[S_S].as<double>(nb), *dC = c.buf[S_C].as<double>(nc);
+        TP_HIP(hipMemcpyAsync(dA, A, na * 8, hipMemcpyHostToDevice, s));
+        TP_HIP(hipMemcpyAsync(dB, B, nb * 8, hipMemcpyHostToDevice, s));
+        TP_HIP(hipMemsetAsync(dC, 0, nc * 8, s));
+        GemmArgs g{m, n, k, dA, ta ? k : m, ta, dB, k, dC, m};
+        g.sym_upper = *sym != 0;
+        g.splitk = 1;
+        g.big_cols = *kernel == 1;
+        if (*kernel == 1 && !g.sym_upper) g.splitk = 1;   // non-sym: big when the tile count allows
+        hipEvent_t e0, e1;
+        TP_HIP(hipEventCreate(&e0));
+        TP_HIP(hipEventCreate(&e1));
+        TP_HIP(hipEventRecord(e0, s));
+        gemm_f64(g, c.buf[S_PARTIAL], s);
+        TP_HIP(hipEventRecord(e1, s));
+        TP_HIP(hipEventSynchronize(e1));
+        float t = 0;
+        TP_HIP(hipEventElapsedTime(&t, e0, e1));
+        *ms = t;
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        TP_HIP(hipMemcpy(C, dC, nc * 8, hipMemcpyDeviceToHost));
+    });
+}
+}  // extern "C"

@@ -158,6 +158,115 @@ __global__ void __launch_bounds__(256) k_gemm_f64(int M, int N, int K, const dou
             }
 }
 
+// ---------------------------------------------------------------------------
+// Large products: 128 x 128 output tile per 256-thread workgroup, each wave a
+// 64 x 64 quadrant (4 x 4 MFMA tiles, 64 accumulators of f64), BK = 16 staged
+// k-contiguous in LDS (+2 pad) and double-buffered, next block prefetched into
+// registers during the MFMAs.  Half the L2 -> LDS traffic per flop of the
+// 64 x 64 kernel and 4x the MFMAs per LDS fragment read.  Every output element
+// sees the same k order (blocks of 16, steps of 4) as k_gemm_f64, so the two
+// kernels give identical bits and can be mixed freely (also across shards).
+constexpr int GB = 128, GBK = 16, GLD = GBK + 2;
+template <bool TA>
+__global__ void __launch_bounds__(256, 2) k_gemm_f64_big(int M, int N, int K, const double *__restrict__ A, int lda,
+                                                         const double *__restrict__ B, int ldb,
+                                                         double *__restrict__ C, int ldc, int store_t, int sym,
+                                                         int tcol0) {
+    __shared__ double As[2][GB][GLD];
+    __shared__ double Bs[2][GB][GLD];
+    int bm, bn;
+    if (sym) {
+        int id = blockIdx.x;
+        bn = tcol0;
+        while (id > bn) { id -= bn + 1; ++bn; }
+        bm = id;
+    } else {
+        const int tm = (M + GB - 1) / GB;
+        bm = blockIdx.x % tm;
+        bn = blockIdx.x / tm;
+    }
+    const int i0 = bm * GB, j0 = bn * GB;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int wm = (w & 1) * 64, wn = (w >> 1) * 64;
+    const int fr = lane & 15, fk = lane >> 4;
+    d4 acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = (d4){0.0, 0.0, 0.0, 0.0};
+    double ra[8], rb[8];
+    auto load = [&](int k0) {
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+            const int idx = t + 256 * p;
+            int row, kk;
+            if (TA) { row = idx >> 4; kk = idx & 15; }
+            else    { kk = idx >> 7; row = idx & 127; }
+            const int i = i0 + row, k = k0 + kk;
+            ra[p] = (i < M && k < K) ? (TA ? A[(size_t)k + (size_t)i * lda] : A[(size_t)i + (size_t)k * lda]) : 0.0;
+            const int col = idx >> 4, kb = idx & 15;
+            const int j = j0 + col, k2 = k0 + kb;
+            rb[p] = (j < N && k2 < K) ? B[(size_t)k2 + (size_t)j * ldb] : 0.0;
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+            const int idx = t + 256 * p;
+            int row, kk;
+            if (TA) { row = idx >> 4; kk = idx & 15; }
+            else    { kk = idx >> 7; row = idx & 127; }
+            As[buf][row][kk] = ra[p];
+            Bs[buf][idx >> 4][idx & 15] = rb[p];
+        }
+    };
+    load(0);
+    store(0);
+    __syncthreads();
+    int buf = 0;
+    for (int k0 = 0; k0 < K; k0 += GBK) {
+        const bool more = k0 + GBK < K;
+        if (more) load(k0 + GBK);
+#pragma unroll
+        for (int kk = 0; kk < GBK; kk += 4) {
+            double af[4], bf[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                af[u] = As[buf][wm + u * 16 + fr][kk + fk];
+                bf[u] = Bs[buf][wn + u * 16 + fr][kk + fk];
+            }
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[a], bf[b], acc[a][b], 0, 0, 0);
+        }
+        if (more) store(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = i0 + wm + a * 16 + fk + 4 * r;
+                const int j = j0 + wn + b * 16 + fr;
+                if (i >= M || j >= N) continue;
+                const double v = acc[a][b][r];
+                if (sym) {
+                    if (i > j) continue;
+                    C[(size_t)i + (size_t)j * ldc] = v;
+                    C[(size_t)j + (size_t)i * ldc] = v;
+                } else if (store_t) {
+                    C[(size_t)j + (size_t)i * ldc] = v;
+                } else {
+                    C[(size_t)i + (size_t)j * ldc] = v;
+                }
+            }
+}
+
 // Fixed-order split-K reduction: C = sum_{z=0..S-1} part[z] (column-major M x N).
 __global__ void __launch_bounds__(256) k_splitk_reduce(const double *part, size_t stride, int S, int M, int N,
                                                        double *C, int ldc, int store_t) {
@@ -179,6 +288,28 @@ void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s) {
     const int tc1 = g.sym_upper ? (g.tcol1 < 0 ? tn : std::min(tn, g.tcol1)) : 0;
     if (g.sym_upper && tc1 <= tc0) return;
     long nblk = g.sym_upper ? (long)tc1 * (tc1 + 1) / 2 - (long)tc0 * (tc0 + 1) / 2 : (long)tm * tn;
+    // 128 x 128 kernel: no split-K, enough tiles to fill the chip, and (sym) a
+    // tile-column range in 128-column units (g.big_cols)
+    {
+        const int tm2 = (g.M + 127) / 128, tn2 = (g.N + 127) / 128;
+        const int c0 = g.sym_upper ? std::max(0, g.tcol0) : 0;
+        const int c1 = g.sym_upper ? (g.tcol1 < 0 ? tn2 : std::min(tn2, g.tcol1)) : 0;
+        const long nb2 = g.sym_upper ? (long)c1 * (c1 + 1) / 2 - (long)c0 * (c0 + 1) / 2 : (long)tm2 * tn2;
+        // non-symmetric: >= 240 tiles of 128 means >= 960 of 64, where the auto
+        // split-K policy below picks no split either (same bits)
+        const bool want = g.sym_upper ? g.big_cols : (g.splitk <= 1 && nb2 >= 240 && g.K >= 512);
+        if (want) {
+            if (g.sym_upper && c1 <= c0) return;
+            if (g.trans_a)
+                hipLaunchKernelGGL(k_gemm_f64_big<true>, dim3((unsigned)nb2), dim3(256), 0, s, g.M, g.N, g.K, g.A,
+                                   g.lda, g.B, g.ldb, g.C, g.ldc, (int)g.store_t, (int)g.sym_upper, c0);
+            else
+                hipLaunchKernelGGL(k_gemm_f64_big<false>, dim3((unsigned)nb2), dim3(256), 0, s, g.M, g.N, g.K, g.A,
+                                   g.lda, g.B, g.ldb, g.C, g.ldc, (int)g.store_t, (int)g.sym_upper, c0);
+            TP_HIP(hipGetLastError());
+            return;
+        }
+    }
     int S = g.splitk;
     if (S < 1) {
         // auto: fill the 256 CUs when the output has few tiles and K is long

@@ -108,6 +108,7 @@ struct GemmArgs {
     bool sym_upper = false;
     int splitk = 1;     // 0 = choose from the tile count
     int tcol0 = 0, tcol1 = -1;   // sym_upper: only tile columns [tcol0, tcol1) (-1 = all)
+    bool big_cols = false;       // use the 128 x 128 kernel; tcol0/tcol1 then count 128-column tiles
 };
 void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s);
 void launch_chol(double *d_W, double *d_rdiag, int b, double rel, int *d_info, hipStream_t s);

@@ -427,3 +427,34 @@ def test_xtx_int8_rejects_non_counts(gpu):
     x = -np.ones((80, 80))
     _, _, _, st = _xtx(gpu, x, 1)
     assert st == 1
+
+
+# ------------------------------------------------ fp64 GEMM kernels agree
+
+def _gemm(gpu, A, B, M, N, K, ta, sym, kernel):
+    import ctypes
+    C = np.zeros((M, N), order="F")
+    ms = ctypes.c_double(0); st = ctypes.c_int(0)
+    D = ctypes.POINTER(ctypes.c_double)
+    I = lambda v: ctypes.byref(ctypes.c_int(v))  # noqa: E731
+    gpu.tp_debug_gemm(A.ctypes.data_as(D), B.ctypes.data_as(D), I(M), I(N), I(K), I(ta), I(sym), I(kernel),
+                      C.ctypes.data_as(D), ctypes.byref(ms), ctypes.byref(st))
+    assert st.value == 0
+    return C, ms.value
+
+
+@pytest.mark.parametrize("M,N,K,ta,sym", [(1500, 1500, 700, 1, 1), (16500, 256, 600, 1, 0), (16500, 200, 300, 0, 0),
+                                          (3000, 3000, 1000, 1, 1)])
+def test_gemm_big_tiles_same_bits(gpu, M, N, K, ta, sym):
+    """The 128 x 128 fp64 MFMA kernel keeps the k order of the 64 x 64 one: the
+    products agree bit for bit (so shard layouts / tile choices never change
+    results), and both match numpy to ~K eps."""
+    rng = np.random.default_rng(M + N + K)
+    A = np.asfortranarray(rng.standard_normal((K, M) if ta else (M, K)))
+    B = np.asfortranarray(A if sym else rng.standard_normal((K, N)))
+    c0, t0 = _gemm(gpu, A, B, M, N, K, ta, sym, 0)
+    c1, t1 = _gemm(gpu, A, B, M, N, K, ta, sym, 1)
+    assert np.array_equal(c0.view(np.uint64), c1.view(np.uint64))
+    ref = (A.T if ta else A) @ B
+    assert np.abs(c1 - ref).max() <= 1e-13 * np.abs(ref).max() * np.sqrt(K)
+    print(f"gemm {M}x{N}x{K} sym={sym}: 64-tile {t0 * 1e3:.0f} us, 128-tile {t1 * 1e3:.0f} us")
