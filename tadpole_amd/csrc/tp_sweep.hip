@@ -556,25 +556,27 @@ __global__ void __launch_bounds__(256) k_trS(const double *Pt, int n, int ldp, i
     const bool ok = j < k;
     const int jj = ok ? j : 0;
     const double fn = (double)n;
+    // one thread per column, rows in order (the canonical sequential sums):
+    // 32 loads in flight per batch -- the pass is L2-latency bound otherwise
     double sj = 0.0;
     int a = 0;
-    for (; a + 7 < n; a += 8) {
-        double x[8];
+    for (; a + 31 < n; a += 32) {
+        double x[32];
 #pragma unroll
-        for (int r = 0; r < 8; ++r) x[r] = Pt[(size_t)(a + r) * ldp + jj];
+        for (int r = 0; r < 32; ++r) x[r] = Pt[(size_t)(a + r) * ldp + jj];
 #pragma unroll
-        for (int r = 0; r < 8; ++r) sj = sj + x[r];
+        for (int r = 0; r < 32; ++r) sj = sj + x[r];
     }
     for (; a < n; ++a) sj = sj + Pt[(size_t)a * ldp + jj];
     const double mj = sj / fn;
     double ss = 0.0;
     a = 0;
-    for (; a + 7 < n; a += 8) {
-        double x[8];
+    for (; a + 31 < n; a += 32) {
+        double x[32];
 #pragma unroll
-        for (int r = 0; r < 8; ++r) x[r] = Pt[(size_t)(a + r) * ldp + jj];
+        for (int r = 0; r < 32; ++r) x[r] = Pt[(size_t)(a + r) * ldp + jj];
 #pragma unroll
-        for (int r = 0; r < 8; ++r) {
+        for (int r = 0; r < 32; ++r) {
             double d = x[r] - mj;
             ss = fma(d, d, ss);
         }
@@ -595,13 +597,19 @@ __global__ void __launch_bounds__(256) k_trS(const double *Pt, int n, int ldp, i
     }
 }
 
-__global__ void __launch_bounds__(256) k_ch(SweepDev sd) {
+// 16 waves per tree: the finest cut's segment statistics spread over them;
+// cut boundaries, alive flags and segment SS live in LDS (the coarser levels'
+// neighbour scans were chains of dependent global loads).
+constexpr int CH_THREADS = 1024, CH_SEGMAX = 1024;
+__global__ void __launch_bounds__(CH_THREADS) k_ch(SweepDev sd) {
+    __shared__ int segs[CH_SEGMAX + 1], alive[CH_SEGMAX], mbl[CH_SEGMAX];
+    __shared__ double ssg[CH_SEGMAX];
     const int n = sd.n, k = sd.k, ldp = sd.ldp;
     const int ti = blockIdx.x;
     const int nc = sd.n_cluster[ti];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
     if (nc < 1) return;
-    if (nc > sd.w_cap || nc > sd.seg_cap) {
+    if (nc > sd.w_cap || nc > sd.seg_cap || nc > CH_SEGMAX) {
         if (threadIdx.x == 0) atomicOr(sd.err, 1);
         return;
     }
@@ -613,21 +621,20 @@ __global__ void __launch_bounds__(256) k_ch(SweepDev sd) {
     }
     const int m = sd.min_clusters < nc ? sd.min_clusters : nc;
     const int *mb = sd.mrg_b + (size_t)ti * (n - 1);
-    // per-tree scratch (global; this workgroup only)
+    // per-tree scratch (global; this workgroup only): segment column sums
     double *seg = sd.seg + (size_t)ti * sd.seg_cap * (k + 1);   // seg_cap x k sums
-    double *ssg = seg + (size_t)sd.seg_cap * k;                        // seg_cap
-    int *segs = sd.iseg + (size_t)ti * (2 * sd.seg_cap + 2);     // nc + 1
-    int *alive = segs + sd.seg_cap + 1;                                // nc
     // finest cut: the boundaries removed by the last nc-1 merges, ascending
+    for (int t = threadIdx.x; t < nc - 1; t += blockDim.x) mbl[t] = mb[n - 2 - t];
+    __syncthreads();
     for (int t = threadIdx.x; t < nc - 1; t += blockDim.x) {
-        int bt = mb[n - 2 - t];
+        const int bt = mbl[t];
         int rank = 0;
-        for (int u = 0; u < nc - 1; ++u) rank += mb[n - 2 - u] < bt;
+        for (int u = 0; u < nc - 1; ++u) rank += mbl[u] < bt;
         segs[rank + 1] = bt;
     }
     if (threadIdx.x == 0) { segs[0] = 0; segs[nc] = n; }
     __syncthreads();
-    for (int g = w; g < nc; g += 4) {
+    for (int g = w; g < nc; g += nw) {
         double ss = seg_ss_wave(sd.Pt, ldp, k, segs[g], segs[g + 1] - 1, seg + (size_t)g * k, lane);
         if (lane == 0) { ssg[g] = ss; alive[g] = 1; }
     }
@@ -742,7 +749,7 @@ void launch_sweep(const SweepDev &sd, hipStream_t s, Ctx *prof) {
     TP_HIP(hipGetLastError());
     run_coniss(sd, s, false, prof);
     if (prof) kprof_begin(*prof, K_CH);
-    hipLaunchKernelGGL(k_ch, dim3(sd.ntrees), dim3(256), 0, s, sd);
+    hipLaunchKernelGGL(k_ch, dim3(sd.ntrees), dim3(CH_THREADS), 0, s, sd);
     TP_HIP(hipGetLastError());
     if (prof) kprof_end(*prof, K_CH);
 }
