@@ -6,8 +6,15 @@ correlation, PCA to max_pcs, CONISS sweep over every PC prefix, broken stick,
 Calinski-Harabasz, parameter choice, TAD coordinates of every significant level.
 Workload = BASELINE.json configs[1] (C2: synthetic 2000 x 2000, max_pcs=200).
 
+Throughput: up to --streams (default 3) matrices in flight per GPU, each on its
+own HIP stream / library context / host thread -- the latency-bound stages of
+one pipeline (CONISS merges, the one-workgroup Cholesky and tridiagonalisation)
+leave most of the 256 CUs idle, and a stream of matrices (a genome is 23 of
+them) fills them.  value = bins of all matrices / wall time; the one-matrix
+latency is reported next to it (config.single_stream_ms_per_matrix).
+
 Multi-GPU: one process per GPU (torch.distributed.run); each rank processes its
-own matrix (independent chromosomes): weak scaling, no
+own matrices (independent chromosomes): weak scaling, no
 data-path collective.  value = bins of all ranks / max-over-ranks time.
 
 Extra fields: "roofline" for the dominant kernel (HIP events inside the
@@ -80,6 +87,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-reps", type=int, default=3)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--streams", type=int, default=3,
+                    help="matrices in flight per GPU (one stream + host thread each; the single-CU stages of one "
+                         "pipeline leave most of the chip idle); 1 = one matrix at a time")
     ap.add_argument("--sharded", action="store_true",
                     help="one matrix split over all ranks (SURVEY §8(e)2, C5 arms): strong scaling")
     return ap.parse_args()
@@ -113,19 +123,31 @@ def main():
         if world > 1:
             multi.init_comm(device=local)
         flags |= _lib.TP_FLAG_SHARDED
-    dev_m = torch.from_numpy(host).to(f"cuda:{local}")
-    stream = torch.cuda.current_stream()
-
     k_cap = max(1, min(args.max_pcs, n0))
     w_cap = n0
-    bufs = dict(bad=np.zeros(n0, np.int32), good=np.zeros(n0, np.int32),
-                nclu=np.zeros(k_cap, np.int32), scores=np.zeros(k_cap * w_cap),
-                merge=np.zeros(2 * (n0 - 1), np.int32), height=np.zeros(n0 - 1),
-                boundary=np.zeros(n0 - 1, np.int32), timings=np.zeros(16))
     I = ctypes.c_int
+    # one pipeline at a time when sharded: the ranks' collectives must be issued
+    # in the same order, one communicator per device
+    S = 1 if args.sharded else max(1, args.streams)
 
-    def step(want_timings: bool):
-        b = bufs
+    class Lane:
+        """One pipeline in flight: its own stream (hence its own library context
+        and scratch), its own resident copy of the matrix, its own host outputs."""
+
+        def __init__(self, idx):
+            self.stream = torch.cuda.current_stream() if idx == 0 else torch.cuda.Stream(device=f"cuda:{local}")
+            self.dev_m = torch.from_numpy(host).to(f"cuda:{local}")
+            self.bufs = dict(bad=np.zeros(n0, np.int32), good=np.zeros(n0, np.int32),
+                             nclu=np.zeros(k_cap, np.int32), scores=np.zeros(k_cap * w_cap),
+                             merge=np.zeros(2 * (n0 - 1), np.int32), height=np.zeros(n0 - 1),
+                             boundary=np.zeros(n0 - 1, np.int32), timings=np.zeros(16))
+
+    lanes = [Lane(i) for i in range(S)]
+    torch.cuda.synchronize()
+
+    def step(want_timings: bool, lane=None):
+        lane = lane or lanes[0]
+        b, dev_m, stream = lane.bufs, lane.dev_m, lane.stream
         outs = [I(0) for _ in range(6)]
         n_good, k, w, n_pcs, n_clusters, st = outs
         L.tp_pipeline_dev(ctypes.c_void_p(dev_m.data_ptr()), ctypes.byref(I(n0)), ctypes.byref(I(args.max_pcs)),
@@ -148,7 +170,8 @@ def main():
         return _assemble(res, np.flatnonzero(res["bad"]) + 1)
 
     for _ in range(args.warmup):
-        step(False)
+        for ln in lanes:
+            step(False, ln)
 
     def barrier():
         if world > 1:
@@ -158,14 +181,43 @@ def main():
     barrier()
     t0 = time.perf_counter()
     last = None
-    for _ in range(args.steps):
-        last = step(False)
+    if S == 1:
+        for _ in range(args.steps):
+            last = step(False)
+    else:
+        # S host threads, one stream each, the K steps dealt round-robin (ctypes
+        # releases the GIL inside the library call)
+        import threading
+        outs = [None] * S
+
+        def run(i):
+            for _ in range(i, args.steps, S):
+                outs[i] = step(False, lanes[i])
+
+        th = [threading.Thread(target=run, args=(i,)) for i in range(S)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        last = outs[0]
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+
+    # latency of one matrix on its own (one stream), for reference next to the
+    # S-stream throughput in `value`
+    single_ms = None
+    if S > 1:
+        barrier()
+        t1 = time.perf_counter()
+        reps = max(3, min(10, args.steps // S))
+        for _ in range(reps):
+            step(False)
+        barrier()
+        single_ms = (time.perf_counter() - t1) / reps * 1e3
 
     # one more instrumented step for the per-kernel breakdown (not in `value`)
     prof = step(True)
@@ -214,7 +266,9 @@ def main():
                                        + f", max_pcs={args.max_pcs}"),
                           "n0": n0, "n_good": n, "k": k, "max_pcs": args.max_pcs,
                           "parallelism": (f"one matrix over {world} GPU(s): column/row-split products, "
-                                          "RCCL all-gather" if args.sharded else f"one matrix per GPU x{world}")},
+                                          "RCCL all-gather" if args.sharded else f"one matrix per GPU x{world}"),
+                          "streams_per_gpu": S,
+                          "single_stream_ms_per_matrix": round(single_ms, 3) if single_ms else None},
                "roofline": roof}
         if not args.no_cpu_baseline and world == 1 and not args.sharded:   # CPU baseline: rank 0 at N=1 only
             sys.path.insert(0, os.path.join(HERE, "oracle"))

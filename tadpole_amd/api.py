@@ -227,7 +227,10 @@ def _r_negative_keep(n: int, neg: np.ndarray) -> np.ndarray:
 # ---------------------------------------------------------------- pipeline
 
 def _pipeline(m: np.ndarray, max_pcs: int, min_clusters: int, bad_frac: float, flags: int,
-              device: int):
+              device: int, stream=None):
+    """One tp_pipeline call.  ``stream`` (a torch.cuda.Stream): the matrix is
+    staged on the device and the pipeline queued on that stream with its own
+    library context, so several pipelines can run concurrently on one GPU."""
     L = _lib.load()
     m, lay = _layout(m)
     flags |= lay
@@ -244,12 +247,27 @@ def _pipeline(m: np.ndarray, max_pcs: int, min_clusters: int, bad_frac: float, f
     timings = np.zeros(16)
     out = [cint(0) for _ in range(6)]
     n_good, k, w, n_pcs, n_clusters, st = out
-    L.tp_pipeline(dp(m), ctypes.byref(cint(n0)), ctypes.byref(cint(max_pcs)), ctypes.byref(cint(min_clusters)),
-                  ctypes.byref(cdbl(bad_frac)), ctypes.byref(cint(flags)), ctypes.byref(cint(device)),
-                  ctypes.byref(cint(k_cap)), ctypes.byref(cint(w_cap)), ip(bad), ctypes.byref(n_good),
-                  ip(good), ctypes.byref(k), ip(nclu), dp(scores), ctypes.byref(w), ctypes.byref(n_pcs),
-                  ctypes.byref(n_clusters), ip(merge), dp(height), ip(boundary), dp(timings),
-                  ctypes.byref(st))
+    if stream is None:
+        L.tp_pipeline(dp(m), ctypes.byref(cint(n0)), ctypes.byref(cint(max_pcs)), ctypes.byref(cint(min_clusters)),
+                      ctypes.byref(cdbl(bad_frac)), ctypes.byref(cint(flags)), ctypes.byref(cint(device)),
+                      ctypes.byref(cint(k_cap)), ctypes.byref(cint(w_cap)), ip(bad), ctypes.byref(n_good),
+                      ip(good), ctypes.byref(k), ip(nclu), dp(scores), ctypes.byref(w), ctypes.byref(n_pcs),
+                      ctypes.byref(n_clusters), ip(merge), dp(height), ip(boundary), dp(timings),
+                      ctypes.byref(st))
+    else:
+        import torch
+        host = m if m.flags["C_CONTIGUOUS"] else np.ascontiguousarray(m.T)   # same buffer order as `lay`
+        with torch.cuda.stream(stream):
+            dm = torch.from_numpy(host).to(f"cuda:{device}", non_blocking=False)
+        stream.synchronize()
+        L.tp_pipeline_dev(ctypes.c_void_p(dm.data_ptr()), ctypes.byref(cint(n0)), ctypes.byref(cint(max_pcs)),
+                          ctypes.byref(cint(min_clusters)), ctypes.byref(cdbl(bad_frac)), ctypes.byref(cint(flags)),
+                          ctypes.byref(cint(device)), ctypes.c_void_p(stream.cuda_stream),
+                          ctypes.byref(cint(k_cap)), ctypes.byref(cint(w_cap)), ip(bad), ctypes.byref(n_good),
+                          ip(good), ctypes.byref(k), ip(nclu), dp(scores), ctypes.byref(w), ctypes.byref(n_pcs),
+                          ctypes.byref(n_clusters), ip(merge), dp(height), ip(boundary), dp(timings),
+                          ctypes.byref(st))
+        del dm
     _lib.check(st)
     n = n_good.value
     kk, ww = k.value, w.value
@@ -360,15 +378,16 @@ def _assemble_rle(t, dendro, levels, good1, bad_idx1) -> Tadpole:
 
 def TADpole(mat_file, max_pcs: int = 200, min_clusters: int = 2, bad_frac: float = 0.01,
             chr=None, start=None, end=None, resol=None, centromere_search: bool = False,
-            device: int = 0, sharded: bool = False) -> Tadpole:
+            device: int = 0, sharded: bool = False, stream=None) -> Tadpole:
     """``TADpole()`` (R/TADpole.R:344-501).  ``mat_file`` may be a path to a
     tab-separated matrix or an in-memory square array.  ``sharded``: split this
     matrix over the ranks of the communicator made by
-    ``tadpole_amd.multi.init_comm`` (every rank calls with the same matrix)."""
+    ``tadpole_amd.multi.init_comm`` (every rank calls with the same matrix).
+    ``stream``: a torch.cuda.Stream to run on (concurrent pipelines per GPU)."""
     raw = _as_matrix(mat_file)
     shard_flag = _lib.TP_FLAG_SHARDED if sharded else 0
     if not centromere_search:
-        res = _pipeline(raw, max_pcs, min_clusters, bad_frac, shard_flag, device)
+        res = _pipeline(raw, max_pcs, min_clusters, bad_frac, shard_flag, device, stream)
         bad_idx1 = np.flatnonzero(res["bad"]) + 1
         return _assemble(res, bad_idx1)
     mat = load_mat(raw, bad_frac=bad_frac, centromere_search=True, device=device)
@@ -376,10 +395,10 @@ def TADpole(mat_file, max_pcs: int = 200, min_clusters: int = 2, bad_frac: float
         # R/TADpole.R:356: `mat$centromer` on a matrix is an error in R
         raise TypeError("$ operator is invalid for atomic vectors (no centromere split: the longest "
                         "bad run touches an end of the matrix; R/TADpole.R:66-70,356)")
-    return _tadpole_arms(mat, max_pcs, min_clusters, device, shard_flag)
+    return _tadpole_arms(mat, max_pcs, min_clusters, device, shard_flag, stream)
 
 
-def _tadpole_arms(mat, max_pcs, min_clusters, device, shard_flag: int = 0) -> Tadpole:
+def _tadpole_arms(mat, max_pcs, min_clusters, device, shard_flag: int = 0, stream=None) -> Tadpole:
     """R/TADpole.R:351-442 (arm loop and arm merge), bug-compatible."""
     tad = Tadpole()
     centromer = mat["centromere"]
@@ -388,7 +407,7 @@ def _tadpole_arms(mat, max_pcs, min_clusters, device, shard_flag: int = 0) -> Ta
         am = mat[arm]
         bad_cols = am.bad_columns
         res = _pipeline(np.asarray(am), max_pcs, min_clusters, 0.0,
-                        _lib.TP_FLAG_CLEAN | _lib.TP_FLAG_NO_MASK | shard_flag, device)
+                        _lib.TP_FLAG_CLEAN | _lib.TP_FLAG_NO_MASK | shard_flag, device, stream)
         names = am.names.astype(np.int32)   # rownames inherited from the full matrix
         res["good"] = names
         sub = _assemble_arm(res, bad_cols)

@@ -95,8 +95,17 @@ void kprof_collect(Ctx &c, double *ms, int *cnt) {
 
 static std::mutex g_mu;
 static Ctx *g_ctx[64] = {nullptr};
+// contexts of caller-supplied streams: one set of scratch buffers per stream,
+// so pipelines on different streams of one device can run concurrently
+static std::vector<std::pair<hipStream_t, Ctx *>> g_sctx[64];
 
-Ctx &ctx_for(int device) {
+static Ctx *new_ctx(int device) {
+    Ctx *c = new Ctx();
+    c->device = device;
+    return c;
+}
+
+Ctx &ctx_for(int device, hipStream_t stream) {
     int ndev = 0;
     hipError_t e = hipGetDeviceCount(&ndev);
     if (e != hipSuccess || ndev <= 0) fail(TP_ERR_HIP, "no HIP device available (libtadpole_hip has no CPU path)");
@@ -104,28 +113,52 @@ Ctx &ctx_for(int device) {
     std::lock_guard<std::mutex> lk(g_mu);
     TP_HIP(hipSetDevice(device));
     if (!g_ctx[device]) {
-        Ctx *c = new Ctx();
-        c->device = device;
+        Ctx *c = new_ctx(device);
         TP_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        c->owns_stream = true;
         g_ctx[device] = c;
     }
-    g_ctx[device]->cur = g_ctx[device]->stream;
-    return *g_ctx[device];
+    Ctx *def = g_ctx[device];
+    if (!stream || stream == def->stream) {
+        def->cur = def->stream;
+        return *def;
+    }
+    Ctx *c = nullptr;
+    for (auto &pr : g_sctx[device])
+        if (pr.first == stream) c = pr.second;
+    if (!c) {
+        c = new_ctx(device);
+        c->stream = stream;
+        c->owns_stream = false;
+        g_sctx[device].push_back({stream, c});
+    }
+    c->cur = stream;
+    // the communicator belongs to the device: every stream's context uses it
+    c->shard.comm = def->shard.comm;
+    c->shard.rank = def->shard.rank;
+    c->shard.nranks = def->shard.nranks;
+    c->shard.nvirt = def->shard.nvirt;
+    return *c;
+}
+
+static void free_ctx(Ctx *c) {
+    (void)hipStreamSynchronize(c->stream);
+    for (auto &b : c->buf) b.release();
+    c->pinned_flag.release();
+    if (c->host_pinned) (void)hipHostFree(c->host_pinned);
+    if (c->blas) rocblas_destroy_handle((rocblas_handle)c->blas);
+    if (c->owns_stream) (void)hipStreamDestroy(c->stream);
+    delete c;
 }
 
 void ctx_shutdown_all() {
     std::lock_guard<std::mutex> lk(g_mu);
-    blas_shutdown_all();
     for (int d = 0; d < 64; ++d) {
-        Ctx *c = g_ctx[d];
-        if (!c) continue;
+        if (!g_ctx[d] && g_sctx[d].empty()) continue;
         (void)hipSetDevice(d);
-        (void)hipStreamSynchronize(c->stream);
-        for (auto &b : c->buf) b.release();
-        c->pinned_flag.release();
-        if (c->host_pinned) (void)hipHostFree(c->host_pinned);
-        (void)hipStreamDestroy(c->stream);
-        delete c;
+        for (auto &pr : g_sctx[d]) free_ctx(pr.second);
+        g_sctx[d].clear();
+        if (g_ctx[d]) free_ctx(g_ctx[d]);
         g_ctx[d] = nullptr;
     }
 }
@@ -601,8 +634,7 @@ void tp_sweep_dev(const double *d_P, const int *n, const int *k, const int *min_
                   int *mrg_b_all, double *cost_all, double *height_all, int *status) {
     guarded(status, [&] {
         if (!d_P || !n || !k || *n < 3 || *k < 1 || !w_cap) fail(TP_ERR_ARG, "bad arguments");
-        Ctx &c = ctx_for(dev_of(device));
-        if (stream) c.cur = (hipStream_t)stream;
+        Ctx &c = ctx_for(dev_of(device), (hipStream_t)stream);
         hipStream_t s = c.cur;
         const int N = *n, K = *k;
         double *dPt = c.buf[S_PT].as<double>((size_t)N * K);
@@ -753,8 +785,7 @@ void tp_pipeline_dev(const double *d_M, const int *n0, const int *max_pcs, const
                      double *timings_ms, int *status) {
     guarded(status, [&] {
         if (!d_M || !n0 || *n0 < 1) fail(TP_ERR_ARG, "bad matrix");
-        Ctx &c = ctx_for(dev_of(device));
-        if (stream) c.cur = (hipStream_t)stream;
+        Ctx &c = ctx_for(dev_of(device), (hipStream_t)stream);
         pipeline_common(const_cast<double *>(d_M), n0, max_pcs, min_clusters, bad_frac, flags, c, k_cap, w_cap,
                         bad, n_good, good_idx, k, n_cluster, scores, w, n_pcs, n_clusters, merge, height, boundary,
                         timings_ms);

@@ -56,7 +56,9 @@ struct Ctx {
     int open_cls = -1;
     hipEvent_t open_ev = nullptr;
     int device = 0;
-    hipStream_t stream = nullptr;   // library stream
+    hipStream_t stream = nullptr;   // library stream (or the caller's, owns_stream = false)
+    bool owns_stream = false;
+    void *blas = nullptr;           // rocblas_handle of this context (lazily created)
     hipStream_t cur = nullptr;      // stream used by the current call
     DevBuf buf[32];
     DevBuf pinned_flag;
@@ -65,7 +67,9 @@ struct Ctx {
     void *pinned(size_t b);
 };
 
-Ctx &ctx_for(int device);
+// device context; a non-null stream other than the library's selects that
+// stream's own context (scratch buffers), so streams can run concurrently
+Ctx &ctx_for(int device, hipStream_t stream = nullptr);
 void kprof_begin(Ctx &c, int cls);
 void kprof_end(Ctx &c, int cls);
 void kprof_collect(Ctx &c, double *ms_per_class, int *count_per_class);

@@ -27,30 +27,18 @@ static void rb_check(rocblas_status st, const char *what) {
     if (st != rocblas_status_success) fail(TP_ERR_HIP, std::string("rocBLAS/rocSOLVER failure in ") + what);
 }
 
-struct Blas {
-    rocblas_handle h = nullptr;
-    int dev = -1;
-};
-static Blas g_blas[64];
-
 static rocblas_handle blas_for(Ctx &c) {
-    Blas &b = g_blas[c.device];
-    if (!b.h) {
-        rb_check(rocblas_create_handle(&b.h), "rocblas_create_handle");
-        b.dev = c.device;
+    if (!c.blas) {
+        rocblas_handle h;
+        rb_check(rocblas_create_handle(&h), "rocblas_create_handle");
+        c.blas = h;
     }
-    rb_check(rocblas_set_stream(b.h, c.cur), "rocblas_set_stream");
-    return b.h;
+    rocblas_handle h = (rocblas_handle)c.blas;
+    rb_check(rocblas_set_stream(h, c.cur), "rocblas_set_stream");
+    return h;
 }
 
-void blas_shutdown_all() {
-    for (auto &b : g_blas)
-        if (b.h) {
-            (void)hipSetDevice(b.dev);
-            rocblas_destroy_handle(b.h);
-            b.h = nullptr;
-        }
-}
+void blas_shutdown_all() {}   // handles are per context (freed with it)
 
 // deterministic pseudo-random start block, uniform in (-1, 1)
 __global__ void k_rand_block(double *Q, int n, int b, uint64_t seed) {

@@ -36,7 +36,7 @@ def matrix_cost(n_bins: int) -> float:
 
 
 def run_genome(matrices: Mapping[str, object], sizes: Optional[Mapping[str, int]] = None,
-               runner: Optional[Callable[[str, object, int], object]] = None,
+               runner: Optional[Callable[[str, object, int], object]] = None, streams: int = 3,
                **tadpole_kwargs) -> Tuple[Dict[str, object], Dict[str, float]]:
     """Process every chromosome once across the ranks of the default process
     group (or locally when torch.distributed is not initialised).
@@ -62,21 +62,46 @@ def run_genome(matrices: Mapping[str, object], sizes: Optional[Mapping[str, int]
                 raise ValueError(f"sizes[{name!r}] is needed when the matrix is not an array")
             sizes[name] = int(shape[0])
     plan = lpt_assign({c: matrix_cost(sizes[c]) for c in matrices}, world)
-    if runner is None:
-        from .api import TADpole
-
-        def runner(name, m, device):
-            return TADpole(m, device=device, **tadpole_kwargs)
-
     mine: Dict[str, object] = {}
     secs: Dict[str, float] = {}
-    for name in plan[rank]:
+
+    def one(name, run):
         m = matrices[name]
         if callable(m):
             m = m()
         t0 = time.perf_counter()
-        mine[name] = runner(name, m, local)
+        mine[name] = run(name, m, local)
         secs[name] = time.perf_counter() - t0
+
+    if runner is None and streams > 1 and len(plan[rank]) > 1:
+        # this rank's chromosomes, up to `streams` in flight on one GPU (one
+        # HIP stream and library context each): the latency-bound stages of a
+        # pipeline leave most CUs idle
+        import threading
+        from concurrent.futures import ThreadPoolExecutor
+
+        import torch
+
+        from .api import TADpole
+        tls = threading.local()
+
+        def run_stream(name, m, device):
+            if getattr(tls, "stream", None) is None:
+                tls.stream = torch.cuda.Stream(device=f"cuda:{device}")
+            return TADpole(m, device=device, stream=tls.stream, **tadpole_kwargs)
+
+        with ThreadPoolExecutor(max_workers=streams) as ex:
+            for f in [ex.submit(one, name, run_stream) for name in plan[rank]]:
+                f.result()
+    else:
+        if runner is None:
+            from .api import TADpole
+
+            def runner(name, m, device):
+                return TADpole(m, device=device, **tadpole_kwargs)
+
+        for name in plan[rank]:
+            one(name, runner)
     if not dist_on:
         return mine, secs
     gathered = [None] * world if rank == 0 else None

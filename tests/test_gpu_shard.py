@@ -76,3 +76,35 @@ def test_rccl_one_rank_communicator(gpu):
         _same(tp.TADpole(m, max_pcs=100, sharded=True), ref)
     finally:
         multi.destroy_comm(0)
+
+
+def test_concurrent_streams_same_results(gpu):
+    """Pipelines on several HIP streams at once (one library context per
+    stream): each result equals the one-at-a-time result, bit for bit."""
+    import threading
+
+    import torch
+    mats = [synth_hic(n, 40 + i) for i, n in enumerate((700, 640, 580, 700))]
+    ref = [tp.TADpole(m, max_pcs=120) for m in mats]
+    out = [None] * len(mats)
+    streams = [torch.cuda.Stream() for _ in range(3)]
+
+    def run(i):
+        for j in range(i, len(mats), 3):
+            out[j] = tp.TADpole(mats[j], max_pcs=120, stream=streams[i])
+
+    th = [threading.Thread(target=run, args=(i,)) for i in range(3)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    for a, b in zip(out, ref):
+        _same(a, b)
+
+
+def test_genome_driver_streams(gpu):
+    from tadpole_amd.genome import run_genome
+    mats = {f"chr{i}": synth_hic(n, 50 + i) for i, n in enumerate((500, 420, 460))}
+    res, secs = run_genome(mats, streams=3, max_pcs=80)
+    for name, m in mats.items():
+        _same(res[name], tp.TADpole(m, max_pcs=80))
