@@ -6,11 +6,13 @@ correlation, PCA to max_pcs, CONISS sweep over every PC prefix, broken stick,
 Calinski-Harabasz, parameter choice, TAD coordinates of every significant level.
 Workload = BASELINE.json configs[1] (C2: synthetic 2000 x 2000, max_pcs=200).
 
-Throughput: up to --streams (default 3) matrices in flight per GPU, each on its
-own HIP stream / library context / host thread -- the latency-bound stages of
-one pipeline (CONISS merges, the one-workgroup Cholesky and tridiagonalisation)
-leave most of the 256 CUs idle, and a stream of matrices (a genome is 23 of
-them) fills them.  value = bins of all matrices / wall time; the one-matrix
+Throughput: up to --streams (default 12) matrices in flight per GPU, each on
+its own HIP stream / library context / host thread -- the latency-bound stages
+of one pipeline (CONISS merges, the one-workgroup Cholesky and
+tridiagonalisation) leave most of the 256 CUs idle, and a stream of matrices (a
+genome is 23 of them) fills them.  HIP maps streams onto GPU_MAX_HW_QUEUES
+hardware queues (4 by default); streams sharing a queue serialise, so the bench
+asks for 16 unless the environment already sets it.  value = bins of all matrices / wall time; the one-matrix
 latency is reported next to it (config.single_stream_ms_per_matrix).
 
 Multi-GPU: one process per GPU (torch.distributed.run); each rank processes its
@@ -31,6 +33,10 @@ import sys
 import time
 
 import numpy as np
+
+# before HIP initialises (torch import / first device call): one hardware queue
+# per concurrent pipeline (see the docstring)
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
@@ -79,7 +85,7 @@ def _config_name(n0, max_pcs):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=96)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--n0", type=int, default=2000)
     ap.add_argument("--max-pcs", type=int, default=200)
@@ -87,7 +93,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-reps", type=int, default=3)
     ap.add_argument("--json-out", default=None)
-    ap.add_argument("--streams", type=int, default=3,
+    ap.add_argument("--streams", type=int, default=12,
                     help="matrices in flight per GPU (one stream + host thread each; the single-CU stages of one "
                          "pipeline leave most of the chip idle); 1 = one matrix at a time")
     ap.add_argument("--sharded", action="store_true",

@@ -4,6 +4,13 @@ R API mirror (reference NAMESPACE:3-8): ``TADpole``, ``load_mat``, ``diffT``,
 ``random_bed``.  Compute runs in ``libtadpole_hip.so`` (HIP, gfx950) through the
 C ABI of ``include/tadpole_hip.h``; there is no CPU fallback.
 """
+import os as _os
+
+# Concurrent pipelines (TADpole(stream=...), run_genome) need one hardware
+# queue per stream; HIP's default is 4 and streams that share a queue
+# serialise.  Takes effect only if HIP has not been initialised yet.
+_os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+
 from .api import (Chclust, Mat, Tadpole, TADpole, bin_index, diffT, is_na, is_r_na, load_mat,
                   mask, random_bed, read_matrix)
 from ._lib import TadpoleError

@@ -36,7 +36,7 @@ def matrix_cost(n_bins: int) -> float:
 
 
 def run_genome(matrices: Mapping[str, object], sizes: Optional[Mapping[str, int]] = None,
-               runner: Optional[Callable[[str, object, int], object]] = None, streams: int = 3,
+               runner: Optional[Callable[[str, object, int], object]] = None, streams: int = 8,
                **tadpole_kwargs) -> Tuple[Dict[str, object], Dict[str, float]]:
     """Process every chromosome once across the ranks of the default process
     group (or locally when torch.distributed is not initialised).
