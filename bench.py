@@ -12,7 +12,7 @@ of one pipeline (CONISS merges, the one-workgroup Cholesky and
 tridiagonalisation) leave most of the 256 CUs idle, and a stream of matrices (a
 genome is 23 of them) fills them.  HIP maps streams onto GPU_MAX_HW_QUEUES
 hardware queues (4 by default); streams sharing a queue serialise, so the bench
-asks for 16 unless the environment already sets it.  value = bins of all matrices / wall time; the one-matrix
+raises it to 16.  value = bins of all matrices / wall time; the one-matrix
 latency is reported next to it (config.single_stream_ms_per_matrix).
 
 Multi-GPU: one process per GPU (torch.distributed.run); each rank processes its
@@ -35,13 +35,19 @@ import time
 import numpy as np
 
 # before HIP initialises (torch import / first device call): one hardware queue
-# per concurrent pipeline (see the docstring)
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+# per concurrent pipeline (see the docstring); raises a lower setting (HIP's
+# default, 4, is often exported explicitly)
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
 FP64_MFMA_PEAK_TFLOPS = 78.6     # MI355X FP64 matrix, dense (AMD spec)
+# what v_mfma_f64_16x16x4_f64 sustains on this chip: back-to-back, independent
+# accumulators, 4 waves/SIMD on every CU (tools/mfma_rate.hip; 33 TF/s at 1
+# wave/SIMD, 43 at 2)
+FP64_MFMA_MEASURED_TFLOPS = 45.0
 HBM_PEAK_GBS = 8000.0            # MI355X HBM3E (MI355X_MICROARCH.md)
 
 
@@ -242,24 +248,50 @@ def main():
             "coniss": (tm[9], "hbm", 1, 40.0 * (n - 1) * k * (k + 1) / 2.0),    # bytes: 5 sum vectors/merge
             "ch": (tm[10], "hbm", 1, 16.0 * n * k * k),                         # bytes: 2 passes/tree
         }
-        dom = max(kern, key=lambda q: kern[q][0])
+        # Dominant kernel.  With S > 1 matrices in flight `value` is bound by
+        # how much of the chip each kernel class occupies, not by one
+        # pipeline's critical path: weight each class's time by the share of
+        # the 1024 SIMDs its grid fills (GEMMs: all; CONISS: 2 waves per tree;
+        # CH: 16 waves per tree).  With one stream: the longest class.
+        simd_share = {"xtx_gemm": 1.0, "xcxc_gemm": 1.0, "gq_gemm": 1.0,
+                      "coniss": min(1.0, 2.0 * k / 1024), "ch": min(1.0, 16.0 * k / 1024)}
+        chip_ms = {q: kern[q][0] * simd_share[q] for q in kern}
+        longest = max(kern, key=lambda q: kern[q][0])
+        dom = max(chip_ms, key=chip_ms.get) if S > 1 else longest
+
+        def rate(q):
+            ms_tot, bound, launches, per_launch = kern[q]
+            avg_ms = ms_tot / launches
+            if bound == "mfma":
+                return per_launch / (avg_ms * 1e-3) / 1e12, FP64_MFMA_PEAK_TFLOPS, "TFLOP/s", avg_ms
+            return per_launch / (avg_ms * 1e-3) / 1e9, HBM_PEAK_GBS, "GB/s", avg_ms
+
         ms_tot, bound, launches, per_launch = kern[dom]
-        avg_ms = ms_tot / launches
-        if bound == "mfma":
-            achieved = per_launch / (avg_ms * 1e-3) / 1e12
-            peak, unit = FP64_MFMA_PEAK_TFLOPS, "TFLOP/s"
-        else:
-            achieved = per_launch / (avg_ms * 1e-3) / 1e9
-            peak, unit = HBM_PEAK_GBS, "GB/s"
+        achieved, peak, unit, avg_ms = rate(dom)
         traffic, tsrc = _pmc_traffic(dom, n0, k)
         roof = {"kernel": dom, "bound": bound, "achieved": round(achieved, 3), "peak": peak, "unit": unit,
                 "frac": round(achieved / peak, 5), "traffic": traffic, "traffic_source": tsrc,
                 "algorithmic_per_launch": per_launch, "avg_launch_ms": round(avg_ms, 4),
                 "launches_per_step": launches,
+                "dominance": ("largest SIMD-time share per matrix with %d matrices in flight" % S if S > 1
+                              else "longest kernel class of one pipeline"),
+                "chip_ms_per_matrix": {q: round(v, 4) for q, v in chip_ms.items()},
                 "breakdown_ms": {q: round(kern[q][0], 4) for q in kern},
                 "stages_ms": {"mask": round(tm[0], 3), "cor": round(tm[1], 3), "pca": round(tm[2], 3),
                               "sweep": round(tm[3], 3), "total": round(tm[4], 3)},
                 "pca": {"iters": int(tm[11]), "block": int(tm[12]), "resid": float(tm[13])}}
+        if bound == "mfma":
+            roof["measured_mfma_ceiling"] = FP64_MFMA_MEASURED_TFLOPS
+            roof["frac_of_measured_ceiling"] = round(achieved / FP64_MFMA_MEASURED_TFLOPS, 4)
+        if longest != dom:   # the one-pipeline critical path (latency), beside it
+            a2, p2, u2, m2 = rate(longest)
+            t2, ts2 = _pmc_traffic(longest, n0, k)
+            roof["latency_critical"] = {"kernel": longest, "bound": kern[longest][1], "achieved": round(a2, 3),
+                                        "peak": p2, "unit": u2, "frac": round(a2 / p2, 5), "avg_launch_ms": round(m2, 4),
+                                        "traffic": t2, "traffic_source": ts2}
+            if longest == "coniss":
+                roof["latency_critical"]["note"] = "one dependent merge chain per tree: latency-bound"
+                roof["latency_critical"]["merges_per_s"] = round(k * (n - 1) / (m2 * 1e-3), 1)
         out = {"metric": "bins/sec (NxN matrix) at 1/2/4/8 GPUs; TAD boundary bit-match vs R ref",
                "value": round(value, 2), "unit": "bins/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),

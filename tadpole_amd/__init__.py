@@ -8,8 +8,10 @@ import os as _os
 
 # Concurrent pipelines (TADpole(stream=...), run_genome) need one hardware
 # queue per stream; HIP's default is 4 and streams that share a queue
-# serialise.  Takes effect only if HIP has not been initialised yet.
-_os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+# serialise.  Raised to 16 (TADPOLE_KEEP_HW_QUEUES=1 leaves it alone); takes
+# effect only if HIP has not been initialised yet.
+if not _os.environ.get("TADPOLE_KEEP_HW_QUEUES") and int(_os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:
+    _os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 from .api import (Chclust, Mat, Tadpole, TADpole, bin_index, diffT, is_na, is_r_na, load_mat,
                   mask, random_bed, read_matrix)

@@ -1196,14 +1196,25 @@ void tp_debug_gemm(const double *A, const double *B, const int *M, const int *N,
         TP_HIP(hipMemsetAsync(dC, 0, nc * 8, s));
         GemmArgs g{m, n, k, dA, ta ? k : m, ta, dB, k, dC, m};
         g.sym_upper = *sym != 0;
-        g.splitk = 1;
+        // kernel: 0 = 64 x 64 tiles, 1 = 128 x 128 (when the tile count allows),
+        // 2 = the library's policy (panel kernel for tall-skinny products),
+        // 3 = the split-K policy without the panel kernel
+        // kernel 10..99: 64 x 64 tiles with split-K (kernel - 10); 110..199: the
+        // same with 16-deep LDS stages
+        const int kern = *kernel >= 110 ? *kernel - 100 : *kernel;
+        g.splitk = kern >= 10 ? kern - 10 : (kern >= 2 ? 0 : 1);
+        const int keep_kb = g_gemm_kb;
+        if (*kernel >= 110) g_gemm_kb = 16;
         g.big_cols = *kernel == 1;
-        if (*kernel == 1 && !g.sym_upper) g.splitk = 1;   // non-sym: big when the tile count allows
+        const int keep_panel = g_gemm_panel;
+        g_gemm_panel = *kernel == 2 ? 1 : 0;
         hipEvent_t e0, e1;
         TP_HIP(hipEventCreate(&e0));
         TP_HIP(hipEventCreate(&e1));
         TP_HIP(hipEventRecord(e0, s));
         gemm_f64(g, c.buf[S_PARTIAL], s);
+        g_gemm_panel = keep_panel;
+        g_gemm_kb = keep_kb;
         TP_HIP(hipEventRecord(e1, s));
         TP_HIP(hipEventSynchronize(e1));
         float t = 0;

@@ -21,59 +21,63 @@ namespace tp {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-constexpr int BM = 64, BN = 64, BK = 16, LDK = BK + 2;
+constexpr int BM = 64, BN = 64, BK = 16;
 
-template <bool TA>
-__device__ __forceinline__ void load_a(double (&ra)[4], const double *A, int lda, int M, int K, int i0, int k0) {
+// KB = k depth of one LDS stage (16 or 32): per thread KB/4 elements of each
+// operand; rows stored k-contiguous with a +2 pad (conflict-free fragment reads)
+template <bool TA, int KB>
+__device__ __forceinline__ void load_a(double (&ra)[KB / 4], const double *A, int lda, int M, int K, int i0, int k0) {
     const int t = threadIdx.x;
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
+    for (int p = 0; p < KB / 4; ++p) {
         int idx = t + 256 * p;
         int row, kk;
-        if (TA) { row = idx >> 4; kk = idx & 15; }   // k contiguous in memory
+        if (TA) { row = idx / KB; kk = idx % KB; }   // k contiguous in memory
         else    { kk = idx >> 6; row = idx & 63; }   // i contiguous in memory
         int i = i0 + row, k = k0 + kk;
         ra[p] = (i < M && k < K) ? (TA ? A[(size_t)k + (size_t)i * lda] : A[(size_t)i + (size_t)k * lda]) : 0.0;
     }
 }
-template <bool TA>
-__device__ __forceinline__ void store_a(double (*As)[LDK], const double (&ra)[4]) {
+template <bool TA, int KB>
+__device__ __forceinline__ void store_a(double (*As)[KB + 2], const double (&ra)[KB / 4]) {
     const int t = threadIdx.x;
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
+    for (int p = 0; p < KB / 4; ++p) {
         int idx = t + 256 * p;
         int row, kk;
-        if (TA) { row = idx >> 4; kk = idx & 15; }
+        if (TA) { row = idx / KB; kk = idx % KB; }
         else    { kk = idx >> 6; row = idx & 63; }
         As[row][kk] = ra[p];
     }
 }
-__device__ __forceinline__ void load_b(double (&rb)[4], const double *B, int ldb, int N, int K, int j0, int k0) {
+template <int KB>
+__device__ __forceinline__ void load_b(double (&rb)[KB / 4], const double *B, int ldb, int N, int K, int j0, int k0) {
     const int t = threadIdx.x;
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
+    for (int p = 0; p < KB / 4; ++p) {
         int idx = t + 256 * p;
-        int col = idx >> 4, kk = idx & 15;
+        int col = idx / KB, kk = idx % KB;
         int j = j0 + col, k = k0 + kk;
         rb[p] = (j < N && k < K) ? B[(size_t)k + (size_t)j * ldb] : 0.0;
     }
 }
-__device__ __forceinline__ void store_b(double (*Bs)[LDK], const double (&rb)[4]) {
+template <int KB>
+__device__ __forceinline__ void store_b(double (*Bs)[KB + 2], const double (&rb)[KB / 4]) {
     const int t = threadIdx.x;
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
+    for (int p = 0; p < KB / 4; ++p) {
         int idx = t + 256 * p;
-        Bs[idx >> 4][idx & 15] = rb[p];
+        Bs[idx / KB][idx % KB] = rb[p];
     }
 }
 
-template <bool TA>
+template <bool TA, int KB>
 __global__ void __launch_bounds__(256) k_gemm_f64(int M, int N, int K, const double *__restrict__ A, int lda,
                                                   const double *__restrict__ B, int ldb, double *__restrict__ C,
                                                   int ldc, int store_t, int sym, int tcol0, int kchunk,
                                                   size_t part_stride) {
-    __shared__ double As[2][BM][LDK];
-    __shared__ double Bs[2][BN][LDK];
+    __shared__ double As[2][BM][KB + 2];
+    __shared__ double Bs[2][BN][KB + 2];
     int bm, bn;
     if (sym) {  // linear id -> upper tile (bm <= bn), column by column from tile column tcol0
         int id = blockIdx.x;
@@ -99,23 +103,23 @@ __global__ void __launch_bounds__(256) k_gemm_f64(int M, int N, int K, const dou
 #pragma unroll
         for (int b = 0; b < 2; ++b) acc[a][b] = (d4){0.0, 0.0, 0.0, 0.0};
 
-    double ra[4], rb[4];
+    double ra[KB / 4], rb[KB / 4];
     int buf = 0;
     if (kbeg < kend) {
-        load_a<TA>(ra, A, lda, M, kend, i0, kbeg);
-        load_b(rb, B, ldb, N, kend, j0, kbeg);
-        store_a<TA>(As[0], ra);
-        store_b(Bs[0], rb);
+        load_a<TA, KB>(ra, A, lda, M, kend, i0, kbeg);
+        load_b<KB>(rb, B, ldb, N, kend, j0, kbeg);
+        store_a<TA, KB>(As[0], ra);
+        store_b<KB>(Bs[0], rb);
     }
     __syncthreads();
-    for (int k0 = kbeg; k0 < kend; k0 += BK) {
-        const bool more = k0 + BK < kend;
+    for (int k0 = kbeg; k0 < kend; k0 += KB) {
+        const bool more = k0 + KB < kend;
         if (more) {
-            load_a<TA>(ra, A, lda, M, kend, i0, k0 + BK);
-            load_b(rb, B, ldb, N, kend, j0, k0 + BK);
+            load_a<TA, KB>(ra, A, lda, M, kend, i0, k0 + KB);
+            load_b<KB>(rb, B, ldb, N, kend, j0, k0 + KB);
         }
 #pragma unroll
-        for (int kk = 0; kk < BK; kk += 4) {
+        for (int kk = 0; kk < KB; kk += 4) {
             double af[2], bf[2];
 #pragma unroll
             for (int t = 0; t < 2; ++t) {
@@ -129,8 +133,8 @@ __global__ void __launch_bounds__(256) k_gemm_f64(int M, int N, int K, const dou
                     acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[a], bf[b], acc[a][b], 0, 0, 0);
         }
         if (more) {
-            store_a<TA>(As[buf ^ 1], ra);
-            store_b(Bs[buf ^ 1], rb);
+            store_a<TA, KB>(As[buf ^ 1], ra);
+            store_b<KB>(Bs[buf ^ 1], rb);
         }
         __syncthreads();
         buf ^= 1;
@@ -157,6 +161,7 @@ __global__ void __launch_bounds__(256) k_gemm_f64(int M, int N, int K, const dou
                 }
             }
 }
+int g_gemm_kb = 16;   // k depth of the 64 x 64 kernel's LDS stages (16 / 32; same bits; 32 measured no faster)
 
 // ---------------------------------------------------------------------------
 // Large products: 128 x 128 output tile per 256-thread workgroup, each wave a
@@ -267,6 +272,109 @@ __global__ void __launch_bounds__(256, 2) k_gemm_f64_big(int M, int N, int K, co
             }
 }
 
+// ---------------------------------------------------------------------------
+// Tall-skinny products (Z = G Q, P = Xc V, Q X: M ~ n, N = b <= 256): a
+// 32 x 64 output tile per 256-thread workgroup, the 4 waves in a 2 x 2 grid,
+// each 16 x 32 (two MFMA tiles), full K in every workgroup.  At n = 2000,
+// b = 256 that is 62 x 4 = 248 workgroups -- one per CU -- where the 64 x 64
+// kernel has 124 tiles.  Used for short K (the Ritz rotation Q X, K = b),
+// where the 64 x 64 policy takes no split either.  BK = 32 per LDS stage (one barrier per 16 MFMAs a wave).  The
+// k order of every output element is that of k_gemm_f64 (steps of 4 within
+// blocks of 16; a 32-block is two 16-blocks back to back), so all three
+// kernels give identical bits.
+constexpr int PM = 32, PN = 64, PK = 32, PLD = PK + 2, PSETS = 3;
+// Global loads run PSETS - 1 stages ahead of the MFMAs (register sets rotate):
+// a stage is only ~1k MFMA cycles a wave, less than an HBM/MALL round trip.
+template <bool TA>
+__global__ void __launch_bounds__(256) k_gemm_f64_panel(int M, int N, int K, const double *__restrict__ A, int lda,
+                                                        const double *__restrict__ B, int ldb,
+                                                        double *__restrict__ C, int ldc, int store_t) {
+    __shared__ double As[2][PM][PLD];
+    __shared__ double Bs[2][PN][PLD];
+    const int tm = (M + PM - 1) / PM;
+    const int bm = blockIdx.x % tm, bn = blockIdx.x / tm;
+    const int i0 = bm * PM, j0 = bn * PN;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int wm = (w & 1) * 16, wn = (w >> 1) * 32;
+    const int fr = lane & 15, fk = lane >> 4;
+    d4 acc[2];
+    acc[0] = (d4){0.0, 0.0, 0.0, 0.0};
+    acc[1] = (d4){0.0, 0.0, 0.0, 0.0};
+    // per stage: A tile PM x PK (4 per thread) + B tile PN x PK (8 per thread)
+    double r[PSETS][12];
+    auto load = [&](double (&x)[12], int k0) {
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int idx = t + 256 * p;
+            int row, kk;
+            if (TA) { row = idx >> 5; kk = idx & 31; }
+            else    { kk = idx >> 5; row = idx & 31; }
+            const int i = i0 + row, k = k0 + kk;
+            x[p] = (i < M && k < K) ? (TA ? A[(size_t)k + (size_t)i * lda] : A[(size_t)i + (size_t)k * lda]) : 0.0;
+        }
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+            const int idx = t + 256 * p;
+            const int col = idx >> 5, kb = idx & 31;
+            const int j = j0 + col, k = k0 + kb;
+            x[4 + p] = (j < N && k < K) ? B[(size_t)k + (size_t)j * ldb] : 0.0;
+        }
+    };
+    auto store = [&](const double (&x)[12], int buf) {
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int idx = t + 256 * p;
+            int row, kk;
+            if (TA) { row = idx >> 5; kk = idx & 31; }
+            else    { kk = idx >> 5; row = idx & 31; }
+            As[buf][row][kk] = x[p];
+        }
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+            const int idx = t + 256 * p;
+            Bs[buf][idx >> 5][idx & 31] = x[4 + p];
+        }
+    };
+    const int S = (K + PK - 1) / PK;
+#pragma unroll
+    for (int u = 0; u < PSETS - 1; ++u)
+        if (u < S) load(r[u], u * PK);
+    if (S > 0) store(r[0], 0);
+    __syncthreads();
+    for (int s0 = 0; s0 < S; s0 += PSETS) {
+#pragma unroll
+        for (int u = 0; u < PSETS; ++u) {
+            const int st = s0 + u;
+            if (st >= S) break;
+            // stage st is in LDS buffer st & 1; r[(u+1)%PSETS] holds stage st+1;
+            // r[(u+PSETS-1)%PSETS] (stage st-1, already in LDS) takes stage st+PSETS-1
+            if (st + PSETS - 1 < S) load(r[(u + PSETS - 1) % PSETS], (st + PSETS - 1) * PK);
+            const int buf = st & 1;
+#pragma unroll
+            for (int kk = 0; kk < PK; kk += 4) {
+                const double af = As[buf][wm + fr][kk + fk];
+                const double b0 = Bs[buf][wn + fr][kk + fk];
+                const double b1 = Bs[buf][wn + 16 + fr][kk + fk];
+                acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(af, b0, acc[0], 0, 0, 0);
+                acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(af, b1, acc[1], 0, 0, 0);
+            }
+            if (st + 1 < S) store(r[(u + 1) % PSETS], buf ^ 1);
+            __syncthreads();
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int i = i0 + wm + fk + 4 * q;
+            const int j = j0 + wn + b * 16 + fr;
+            if (i >= M || j >= N) continue;
+            if (store_t) C[(size_t)j + (size_t)i * ldc] = acc[b][q];
+            else C[(size_t)i + (size_t)j * ldc] = acc[b][q];
+        }
+}
+int g_gemm_panel = 1;   // 0: tall-skinny products take the split-K 64 x 64 path (A/B tests)
+
 // Fixed-order split-K reduction: C = sum_{z=0..S-1} part[z] (column-major M x N).
 __global__ void __launch_bounds__(256) k_splitk_reduce(const double *part, size_t stride, int S, int M, int N,
                                                        double *C, int ldc, int store_t) {
@@ -310,6 +418,24 @@ void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s) {
             return;
         }
     }
+    // tall-skinny, not symmetric: 32 x 64 tiles, full K, when the 64 x 64 grid
+    // is too small to fill the chip without a split (or a split is allowed)
+    // (K < 512 only: with full K a wave per SIMD issues an f64 MFMA every ~150
+    // cycles at best -- tools/mfma_rate.hip -- and the split-K 64 x 64 grid
+    // with two workgroups a CU is faster)
+    if (g_gemm_panel && !g.sym_upper && g.splitk <= 1 && nblk < 192 && g.N <= 512 && g.K < 512) {
+        const long np = (long)((g.M + PM - 1) / PM) * ((g.N + PN - 1) / PN);
+        if (np >= 128) {
+            if (g.trans_a)
+                hipLaunchKernelGGL(k_gemm_f64_panel<true>, dim3((unsigned)np), dim3(256), 0, s, g.M, g.N, g.K, g.A,
+                                   g.lda, g.B, g.ldb, g.C, g.ldc, (int)g.store_t);
+            else
+                hipLaunchKernelGGL(k_gemm_f64_panel<false>, dim3((unsigned)np), dim3(256), 0, s, g.M, g.N, g.K, g.A,
+                                   g.lda, g.B, g.ldb, g.C, g.ldc, (int)g.store_t);
+            TP_HIP(hipGetLastError());
+            return;
+        }
+    }
     int S = g.splitk;
     if (S < 1) {
         // auto: fill the 256 CUs when the output has few tiles and K is long
@@ -317,7 +443,7 @@ void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s) {
         if (nblk < 192 && g.K >= 512) S = (int)std::min<long>(8, std::max<long>(1, (384 + nblk - 1) / nblk));
         S = std::min(S, std::max(1, g.K / 128));
     }
-    int kchunk = ((g.K + S - 1) / S + BK - 1) / BK * BK;
+    int kchunk = ((g.K + S - 1) / S + BK - 1) / BK * BK;   // multiple of 16 for either stage depth
     if (kchunk < BK) kchunk = BK;
     S = (g.K + kchunk - 1) / kchunk;
     if (S < 1) S = 1;
@@ -332,12 +458,21 @@ void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s) {
         ldo = g.M;
         st = 0;
     }
-    if (g.trans_a)
-        hipLaunchKernelGGL(k_gemm_f64<true>, grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb, out, ldo,
-                           st, (int)g.sym_upper, tc0, kchunk, pstride);
-    else
-        hipLaunchKernelGGL(k_gemm_f64<false>, grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb, out,
-                           ldo, st, (int)g.sym_upper, tc0, kchunk, pstride);
+    if (g_gemm_kb == 32) {
+        if (g.trans_a)
+            hipLaunchKernelGGL((k_gemm_f64<true, 32>), grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb,
+                               out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride);
+        else
+            hipLaunchKernelGGL((k_gemm_f64<false, 32>), grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb,
+                               out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride);
+    } else {
+        if (g.trans_a)
+            hipLaunchKernelGGL((k_gemm_f64<true, 16>), grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb,
+                               out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride);
+        else
+            hipLaunchKernelGGL((k_gemm_f64<false, 16>), grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb,
+                               out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride);
+    }
     TP_HIP(hipGetLastError());
     if (S > 1) {
         size_t tot = (size_t)g.M * g.N;

@@ -458,3 +458,47 @@ def test_gemm_big_tiles_same_bits(gpu, M, N, K, ta, sym):
     ref = (A.T if ta else A) @ B
     assert np.abs(c1 - ref).max() <= 1e-13 * np.abs(ref).max() * np.sqrt(K)
     print(f"gemm {M}x{N}x{K} sym={sym}: 64-tile {t0 * 1e3:.0f} us, 128-tile {t1 * 1e3:.0f} us")
+
+
+@pytest.mark.parametrize("M,N,K,ta", [(1980, 256, 1980, 1), (1980, 200, 1980, 1), (1980, 256, 256, 0),
+                                      (4100, 130, 1001, 1), (8000, 64, 333, 0)])
+def test_gemm_panel_same_bits(gpu, M, N, K, ta):
+    """The 32 x 64 tall-skinny kernel (Z = G Q, scores, Ritz rotation) keeps the
+    k order of the 64 x 64 kernel without split-K: identical bits; timings of
+    the panel kernel vs the split-K policy it replaces are printed."""
+    rng = np.random.default_rng(M * 3 + N + K)
+    A = np.asfortranarray(rng.standard_normal((K, M) if ta else (M, K)))
+    B = np.asfortranarray(rng.standard_normal((K, N)))
+    c0, t0 = _gemm(gpu, A, B, M, N, K, ta, 0, 0)
+    c2, t2 = _gemm(gpu, A, B, M, N, K, ta, 0, 2)
+    c3, t3 = _gemm(gpu, A, B, M, N, K, ta, 0, 3)
+    t2 = min(t2, _gemm(gpu, A, B, M, N, K, ta, 0, 2)[1])
+    t3 = min(t3, _gemm(gpu, A, B, M, N, K, ta, 0, 3)[1])
+    if K < 512:   # the panel kernel's range (longer K keeps the split-K policy)
+        assert np.array_equal(c0.view(np.uint64), c2.view(np.uint64))
+    ref = (A.T if ta else A) @ B
+    assert np.abs(c2 - ref).max() <= 1e-13 * np.abs(ref).max() * np.sqrt(K)
+    assert np.abs(c3 - ref).max() <= 1e-13 * np.abs(ref).max() * np.sqrt(K)
+    tf = 2.0 * M * N * K / 1e9
+    print(f"gemm {M}x{N}x{K}: 64-tile {t0 * 1e3:.1f} us, panel {t2 * 1e3:.1f} us ({tf / t2:.1f} TF/s), "
+          f"split-K policy {t3 * 1e3:.1f} us ({tf / t3:.1f} TF/s)")
+
+
+def test_gemm_splitk_sweep(gpu):
+    """Z = G Q at the C2 shape with every split-K factor: all agree with numpy
+    to ~K eps (timings printed; the policy in gemm_f64 picks from them)."""
+    M, N, K = 1980, 256, 1980
+    rng = np.random.default_rng(7)
+    A = np.asfortranarray(rng.standard_normal((K, M)))
+    B = np.asfortranarray(rng.standard_normal((K, N)))
+    ref = A.T @ B
+    for S in (1, 2, 3, 4, 6, 8, 12, 16):
+        for kb, base in ((32, 10), (16, 110)):
+            c, t = _gemm(gpu, A, B, M, N, K, 1, 0, base + S)
+            t = min(t, _gemm(gpu, A, B, M, N, K, 1, 0, base + S)[1], _gemm(gpu, A, B, M, N, K, 1, 0, base + S)[1])
+            assert np.abs(c - ref).max() <= 1e-13 * np.abs(ref).max() * np.sqrt(K)
+            if kb == 32:
+                c32 = c
+            else:   # the stage depth never changes the k order
+                assert np.array_equal(c.view(np.uint64), c32.view(np.uint64))
+            print(f"splitk {S} stage {kb}: {t * 1e3:.1f} us, {2.0 * M * N * K / t / 1e9:.1f} TF/s")
