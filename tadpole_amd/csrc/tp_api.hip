@@ -278,6 +278,11 @@ static SweepOut run_sweep(Ctx &c, const double *d_Pt, int n, int k, int min_clus
     sd.iseg = c.buf[S_MISC].as<int>((size_t)k * (2 * sd.seg_cap + 2) + 64) + 64;
     sd.trS = (double *)(c.buf[S_NGOOD].as<char>(64)) + 2;
     sd.cost0 = c.buf[S_SMALL].as<double>(sweep_cost0_doubles(n, k));
+    if (g_ch_dedup) {   // CH segment statistics shared across trees
+        int hcap = 0, ucap = 0;
+        const size_t bytes = sweep_dedup_bytes(n, k, k, sd.seg_cap, &hcap, &ucap);
+        sweep_dedup_bind(sd, c.buf[S_DEDUP].as<char>(bytes), hcap, ucap);
+    }
     TP_HIP(hipMemsetAsync(err_all, 0, (size_t)R * sizeof(int), s));
     for (int r = 0; r < R; ++r) {
         const int t0 = tb[r], nt = tb[r + 1] - tb[r];
@@ -1180,6 +1185,28 @@ void tp_debug_xtx(const double *X, const int *n, const int *mode, double *S, int
 }  // extern "C"
 
 extern "C" {
+/* Test hook: set a tuning switch, *old = its previous value.  which: 0 CH
+ * segment statistics shared across trees, 1 cap on their store (0 = automatic),
+ * 2 short-K panel GEMM, 3 GEMM LDS stage depth (16 / 32), 4 register-resident
+ * tridiagonalisation, 5 int8 X'X. */
+void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
+    guarded(status, [&] {
+        int *p = nullptr;
+        switch (*which) {
+        case 0: p = &g_ch_dedup; break;
+        case 1: p = &g_ch_dedup_ucap; break;
+        case 2: p = &g_gemm_panel; break;
+        case 3: p = &g_gemm_kb; break;
+        case 4: p = &g_sytrd_reg; break;
+        case 5: p = &g_xtx_int8; break;
+        default: fail(TP_ERR_ARG, "unknown knob");
+        }
+        if (*which == 3 && *value != 16 && *value != 32) fail(TP_ERR_ARG, "stage depth must be 16 or 32");
+        *old = *p;
+        *p = *value;
+    });
+}
+
 /* C = A'B (trans_a) or AB, fp64 MFMA, kernel 0 = 64 x 64 tiles, 1 = 128 x 128
  * tiles (both without split-K); sym = upper tiles mirrored (M == N). */
 void tp_debug_gemm(const double *A, const double *B, const int *M, const int *N, const int *K, const int *trans_a,
@@ -1205,6 +1232,7 @@ void tp_debug_gemm(const double *A, const double *B, const int *M, const int *N,
         g.splitk = kern >= 10 ? kern - 10 : (kern >= 2 ? 0 : 1);
         const int keep_kb = g_gemm_kb;
         if (*kernel >= 110) g_gemm_kb = 16;
+        else if (*kernel >= 10) g_gemm_kb = 32;
         g.big_cols = *kernel == 1;
         const int keep_panel = g_gemm_panel;
         g_gemm_panel = *kernel == 2 ? 1 : 0;

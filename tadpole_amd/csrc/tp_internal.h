@@ -79,7 +79,7 @@ void ctx_shutdown_all();
 enum Slot {
     S_M = 0, S_ROWMEAN, S_DIAG, S_BAD, S_GOOD, S_NGOOD, S_X, S_COLMEAN,
     S_S, S_C, S_XC, S_XCT, S_G, S_Q, S_Z, S_W, S_SMALL, S_P, S_PT,
-    S_SWEEP, S_SWEEP2, S_SCORES, S_PARTIAL, S_MISC, S_SHARD, S_SHARD2
+    S_SWEEP, S_SWEEP2, S_SCORES, S_PARTIAL, S_MISC, S_SHARD, S_SHARD2, S_DEDUP
 };
 
 // ---------------------------------------------------------------- kernels
@@ -154,7 +154,23 @@ struct SweepDev {
     int *err;           // device flag: 1 = a cut exceeded seg_cap / w_cap
     long long *stamps = nullptr;   // diagnostic builds only (k_coniss_t<true>)
     double *cost0 = nullptr;       // ntrees x roundup(n, 64) initial costs (scratch)
+    // CH segment statistics shared across trees (null: every tree computes its
+    // own): the finest cuts' segments [s, e) go into an open-addressing set
+    // (hkeys, empty = ~0), each distinct one gets a slot of ustore (k column
+    // sums + SS) computed once; see sweep_dedup_bytes
+    unsigned long long *hkeys = nullptr;
+    int *hidx = nullptr;                  // hcap: ustore index per set slot (-1: store full)
+    int hcap = 0;                         // power of two >= 2 x the segments inserted
+    unsigned long long *ukey = nullptr;   // ucap: key of each stored segment
+    double *ustore = nullptr;             // ucap x (k + 1)
+    int ucap = 0;
+    int *ucount = nullptr;                // distinct segments inserted (may exceed ucap)
 };
+// scratch of the shared CH segment statistics for ntrees trees
+extern int g_ch_dedup;        // 0: every tree computes its own segment statistics
+extern int g_ch_dedup_ucap;   // > 0: cap on the shared store (tests of the overflow path)
+size_t sweep_dedup_bytes(int n, int k, int ntrees, int seg_cap, int *hcap, int *ucap);
+void sweep_dedup_bind(SweepDev &sd, void *base, int hcap, int ucap);
 // initial costs (ntrees x roundup(n, 64)) + link scratch of the global-memory
 // CONISS variant (ntrees x 2n ints)
 inline size_t sweep_cost0_doubles(int n, int ntrees) { return (size_t)ntrees * (((n + 63) / 64) * 64 + n); }

@@ -134,3 +134,12 @@ def eigsym(h, method=1):
     L.tp_debug_eigsym(dp(hf), B(cint(b)), B(cint(method)), dp(theta), dp(v), B(st))
     _lib.check(st)
     return theta, v
+
+
+def knob(which, value):
+    """tp_debug_knob: set a tuning switch, return its previous value."""
+    L = _lib.load()
+    old, st = cint(0), _st()
+    L.tp_debug_knob(B(cint(which)), B(cint(value)), B(old), B(st))
+    _lib.check(st)
+    return old.value

@@ -337,6 +337,29 @@ def test_sweep_selection_and_bstick_r_faithful(gpu):
     assert (got["n_pcs"], got["n_clusters"]) == O.select_params(ref.scores)
 
 
+@pytest.mark.parametrize("ucap", [0, 7])
+def test_sweep_shared_segment_stats(gpu, ucap):
+    """CH segment statistics shared across trees (k_ch_cut / k_ch_segstat) give
+    the bits of every tree computing its own -- also when the shared store
+    overflows (ucap 7: most segments take the per-tree fallback) -- and of the
+    oracle."""
+    p = _pcs(700, 13, 200)
+    old = G.knob(1, ucap)
+    try:
+        got = G.sweep_dev(p)
+    finally:
+        G.knob(1, old)
+    was = G.knob(0, 0)
+    try:
+        own = G.sweep_dev(p)
+    finally:
+        G.knob(0, was)
+    ref = O.sweep(p)
+    for r in (own, ref if isinstance(ref, dict) else {"scores": ref.scores, "n_cluster": ref.n_cluster}):
+        assert np.array_equal(got["n_cluster"], r["n_cluster"])
+        assert np.array_equal(got["scores"].view(np.uint64), r["scores"].view(np.uint64))
+
+
 @pytest.mark.parametrize("mc", [1, 2, 5, 50])
 def test_sweep_min_clusters(gpu, mc):
     p = _pcs(250, 22, 40)
