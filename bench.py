@@ -252,9 +252,9 @@ def main():
         # how much of the chip each kernel class occupies, not by one
         # pipeline's critical path: weight each class's time by the share of
         # the 1024 SIMDs its grid fills (GEMMs: all; CONISS: 2 waves per tree;
-        # CH: 16 waves per tree).  With one stream: the longest class.
+        # CH: 4 waves per tree).  With one stream: the longest class.
         simd_share = {"xtx_gemm": 1.0, "xcxc_gemm": 1.0, "gq_gemm": 1.0,
-                      "coniss": min(1.0, 2.0 * k / 1024), "ch": min(1.0, 16.0 * k / 1024)}
+                      "coniss": min(1.0, 2.0 * k / 1024), "ch": min(1.0, 4.0 * k / 1024)}
         chip_ms = {q: kern[q][0] * simd_share[q] for q in kern}
         longest = max(kern, key=lambda q: kern[q][0])
         dom = max(chip_ms, key=chip_ms.get) if S > 1 else longest

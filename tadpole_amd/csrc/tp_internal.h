@@ -115,8 +115,8 @@ struct GemmArgs {
     bool big_cols = false;       // use the 128 x 128 kernel; tcol0/tcol1 then count 128-column tiles
 };
 void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s);
-extern int g_gemm_panel;
-extern int g_gemm_kb;      // LDS stage depth of the 64 x 64 kernel (16 / 32)   // tall-skinny 32 x 64 kernel enabled (default 1)
+extern int g_gemm_panel;   // short-K tall-skinny 32 x 64 kernel enabled (default 1)
+extern int g_gemm_kb;      // LDS stage depth of the 64 x 64 kernel (16 / 32)
 void launch_chol(double *d_W, double *d_rdiag, int b, double rel, int *d_info, hipStream_t s);
 void launch_chol_stamped(double *d_W, double *d_rdiag, int b, double rel, int *d_info, long long *d_st,
                          hipStream_t s);
@@ -224,6 +224,7 @@ void xtx_int8_tiles128(Ctx &c, const int8_t *sl, int n, int ns, double *d_S, int
 // S = X'X by the exact int8 path when possible, sharded like sym_gemm_sharded
 void xtx_product(Ctx &c, const double *d_X, int n, double *d_S);
 
+extern int g_pca_margin;   // extra Chebyshev degrees over the planned count (default 0)
 struct PcaStats { int iters = 0; double resid = 0; double rate = 0; int block = 0; int blocks = 0; };
 PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d_Pt,
                  double *h_sdev);

@@ -116,6 +116,8 @@ __global__ void k_diag(const double *W, int b, double *d) {
     if (j < b) d[j] = fabs(W[(size_t)j * b + j]);
 }
 
+int g_pca_margin = 0;   // extra Chebyshev degrees over the planned count (the residual check adds more when needed; tools/pca_margin.py)
+
 PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d_Pt, double *h_sdev) {
     PcaStats st;
     hipStream_t s = c.cur;
@@ -250,7 +252,7 @@ PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d
                 cut = 0.0;
             }
             st.rate = gk > 1 ? 1.0 / gk : 0.9;
-            int need = (int)std::ceil(std::log(1.0 / target) / std::log(std::max(gk, 1.0005))) + 2;
+            int need = (int)std::ceil(std::log(1.0 / target) / std::log(std::max(gk, 1.0005))) + g_pca_margin;
             need = std::min(need, max_deg);
             if (cut > 0) {
                 // Block degrees double: after total degree D the j-th column's
