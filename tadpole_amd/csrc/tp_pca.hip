@@ -296,13 +296,17 @@ PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d
                          "dsyevd(RR)");
             size_t tot = (size_t)b * b;
             hipLaunchKernelGGL(k_select_rev, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, Wsm, b, b, Xinv);
-            GemmArgs rq{n, b, b, Q, n, false, Xinv, b, Z, n};
+            // rotate: V = Q X (into T); G V = (G Q) X = Z X for the residuals of
+            // the top k Ritz pairs, ||G v - theta v||, without another product
+            // with G (into Yb)
+            GemmArgs rq{n, b, b, Q, n, false, Xinv, b, T, n};
             rq.splitk = 0;
             gemm_f64(rq, c.buf[S_PARTIAL], s);
-            std::swap(Q, Z);
-            // residuals of the top k Ritz pairs: ||G v - theta v||
-            rows_gemm_sharded(c, G, n, n, Q, n, k, n, Z, 0);
-            hipLaunchKernelGGL(k_resid, dim3((k + 3) / 4), dim3(256), 0, s, Z, Q, theta, n, b, k, resid);
+            GemmArgs gv{n, k, b, Z, n, false, Xinv, b, Yb, n};
+            gv.splitk = 0;
+            gemm_f64(gv, c.buf[S_PARTIAL], s);
+            std::swap(Q, T);
+            hipLaunchKernelGGL(k_resid, dim3((k + 3) / 4), dim3(256), 0, s, Yb, Q, theta, n, b, k, resid);
             TP_HIP(hipGetLastError());
             TP_HIP(hipMemcpyAsync(h_res.data(), resid, k * sizeof(double), hipMemcpyDeviceToHost, s));
             TP_HIP(hipMemcpyAsync(h_theta.data(), theta, b * sizeof(double), hipMemcpyDeviceToHost, s));
