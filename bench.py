@@ -52,15 +52,11 @@ HBM_PEAK_GBS = 8000.0            # MI355X HBM3E (MI355X_MICROARCH.md)
 
 
 def _pmc_traffic(kernel_class, n0, k):
-    """HBM bytes per launch of the dominant kernel from the newest committed
-    PMC summary (profiles/*_traffic.json, written by tools/prof_summary.py from
-    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench) for
-    the same workload.  GEMM classes share one kernel symbol: no per-class
-    figure, so null."""
+    """HBM bytes per launch of a kernel class (the kernels one launch runs,
+    summed) from the newest committed PMC summary (profiles/*_traffic.json,
+    written by tools/prof_summary.py from separate rocprofv3 --pmc FETCH_SIZE /
+    WRITE_SIZE passes of this bench) for the same workload; null when absent."""
     import glob
-    prefixes = {"coniss": "tp::k_coniss_t<false", "ch": "tp::k_ch"}
-    if kernel_class not in prefixes:
-        return None, None
     for path in sorted(glob.glob(os.path.join(HERE, "profiles", "*_traffic.json")), reverse=True):
         try:
             t = json.load(open(path))
@@ -68,10 +64,9 @@ def _pmc_traffic(kernel_class, n0, k):
             continue
         if t.get("n0") != n0 or t.get("k") != k:
             continue
-        for name, rec in t.get("kernels", {}).items():
-            if name == prefixes[kernel_class] or name.startswith(prefixes[kernel_class] + ",") or \
-                    name.startswith(prefixes[kernel_class] + ">"):
-                return round(rec["hbm_bytes"]), os.path.relpath(path, HERE)
+        rec = t.get("classes", {}).get(kernel_class)
+        if isinstance(rec, dict) and rec.get("hbm_bytes") is not None:
+            return round(rec["hbm_bytes"]), os.path.relpath(path, HERE)
     return None, None
 
 

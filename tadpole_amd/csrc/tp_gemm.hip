@@ -71,27 +71,40 @@ __device__ __forceinline__ void store_b(double (*Bs)[KB + 2], const double (&rb)
     }
 }
 
-template <bool TA, int KB>
+// TAG only names the symbol (1 = the PCA's G Y products), so profiles can
+// attribute launches; the code is the same.
+template <bool TA, int KB, int TAG = 0>
 __global__ void __launch_bounds__(256) k_gemm_f64(int M, int N, int K, const double *__restrict__ A, int lda,
                                                   const double *__restrict__ B, int ldb, double *__restrict__ C,
                                                   int ldc, int store_t, int sym, int tcol0, int kchunk,
                                                   size_t part_stride) {
     __shared__ double As[2][BM][KB + 2];
     __shared__ double Bs[2][BN][KB + 2];
-    int bm, bn;
+    // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs (each
+    // with its own L2), so the logical tile index Lg makes consecutive
+    // workgroups of one XCD neighbours -- the tiles of one A row panel (all
+    // column tiles, same k chunk) run together and share it in that L2.
+    const int total = (int)gridDim.x;   // tiles x k chunks
+    const int xcd = (int)blockIdx.x & 7, slot = (int)blockIdx.x >> 3;
+    const int Lg = xcd * (total >> 3) + min(xcd, total & 7) + slot;
+    int bm, bn, z;
     if (sym) {  // linear id -> upper tile (bm <= bn), column by column from tile column tcol0
-        int id = blockIdx.x;
+        const int nt = total / ((K + kchunk - 1) / kchunk);   // tiles (total / k chunks)
+        int id = Lg % nt;
+        z = Lg / nt;
         bn = tcol0;
         while (id > bn) { id -= bn + 1; ++bn; }
         bm = id;
     } else {
-        bm = blockIdx.x % ((M + BM - 1) / BM);
-        bn = blockIdx.x / ((M + BM - 1) / BM);
+        const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
+        bn = Lg % tn;
+        bm = (Lg / tn) % tm;
+        z = Lg / (tn * tm);
     }
     const int i0 = bm * BM, j0 = bn * BN;
-    const int kbeg = blockIdx.z * kchunk;
+    const int kbeg = z * kchunk;
     const int kend = min(K, kbeg + kchunk);
-    C += part_stride * blockIdx.z;
+    C += part_stride * z;
 
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int wm = (w & 1) * 32, wn = (w >> 1) * 32;
@@ -376,6 +389,7 @@ __global__ void __launch_bounds__(256) k_gemm_f64_panel(int M, int N, int K, con
 int g_gemm_panel = 1;   // 0: tall-skinny products take the split-K 64 x 64 path (A/B tests)
 
 // Fixed-order split-K reduction: C = sum_{z=0..S-1} part[z] (column-major M x N).
+template <int TAG = 0>
 __global__ void __launch_bounds__(256) k_splitk_reduce(const double *part, size_t stride, int S, int M, int N,
                                                        double *C, int ldc, int store_t) {
     size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -447,7 +461,8 @@ void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s) {
     if (kchunk < BK) kchunk = BK;
     S = (g.K + kchunk - 1) / kchunk;
     if (S < 1) S = 1;
-    dim3 grid((unsigned)nblk, 1, (unsigned)S);
+    // 1-D grid of tiles x k chunks (the kernel maps it XCD-aware)
+    dim3 grid((unsigned)(nblk * S), 1, 1);
     double *out = g.C;
     int ldo = g.ldc;
     int st = g.store_t;
@@ -465,19 +480,26 @@ void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s) {
         else
             hipLaunchKernelGGL((k_gemm_f64<false, 32>), grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb,
                                out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride);
+    } else if (g.trans_a && g.tag == 1) {
+        hipLaunchKernelGGL((k_gemm_f64<true, 16, 1>), grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb,
+                           out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride);
+    } else if (g.trans_a) {
+        hipLaunchKernelGGL((k_gemm_f64<true, 16>), grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb,
+                           out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride);
     } else {
-        if (g.trans_a)
-            hipLaunchKernelGGL((k_gemm_f64<true, 16>), grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb,
-                               out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride);
-        else
-            hipLaunchKernelGGL((k_gemm_f64<false, 16>), grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb,
-                               out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride);
+        hipLaunchKernelGGL((k_gemm_f64<false, 16>), grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb,
+                           out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride);
     }
     TP_HIP(hipGetLastError());
     if (S > 1) {
         size_t tot = (size_t)g.M * g.N;
-        hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, out, pstride, S,
-                           g.M, g.N, g.C, g.ldc, (int)g.store_t);
+        const dim3 rg((unsigned)((tot + 255) / 256));
+        if (g.tag == 1)
+            hipLaunchKernelGGL(k_splitk_reduce<1>, rg, dim3(256), 0, s, out, pstride, S, g.M, g.N, g.C, g.ldc,
+                               (int)g.store_t);
+        else
+            hipLaunchKernelGGL(k_splitk_reduce<0>, rg, dim3(256), 0, s, out, pstride, S, g.M, g.N, g.C, g.ldc,
+                               (int)g.store_t);
         TP_HIP(hipGetLastError());
     }
 }

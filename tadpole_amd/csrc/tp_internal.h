@@ -113,6 +113,7 @@ struct GemmArgs {
     int splitk = 1;     // 0 = choose from the tile count
     int tcol0 = 0, tcol1 = -1;   // sym_upper: only tile columns [tcol0, tcol1) (-1 = all)
     bool big_cols = false;       // use the 128 x 128 kernel; tcol0/tcol1 then count 128-column tiles
+    int tag = 0;                 // 1: the PCA's G Y products (own kernel symbols for profiles)
 };
 void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s);
 extern int g_gemm_panel;   // short-K tall-skinny 32 x 64 kernel enabled (default 1)
@@ -213,7 +214,7 @@ void shard_gather_bytes(Ctx &c, void *buf, const std::vector<size_t> &off);
 void shard_bcast_bytes(Ctx &c, void *buf, size_t bytes, int root);
 void sym_gemm_sharded(Ctx &c, GemmArgs g);
 void rows_gemm_sharded(Ctx &c, const double *A, int lda, int M, const double *B, int ldb, int N, int K,
-                       double *Out, int splitk_plain);
+                       double *Out, int splitk_plain, int tag = 0);
 
 // exact X'X on int8 matrix cores for integer counts (tp_xtx.hip)
 extern int g_xtx_int8;

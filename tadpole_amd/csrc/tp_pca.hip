@@ -181,7 +181,7 @@ PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d
         double *Yb = c.buf[S_SWEEP2].as<double>((size_t)n * b);   // 4th block buffer (sweep scratch later)
         auto gemm_gq = [&](const double *Yin, double *Out) {   // Out = G Yin (row-sharded)
             kprof_begin(c, K_GQ_GEMM);
-            rows_gemm_sharded(c, G, n, n, Yin, n, b, n, Out, 0);
+            rows_gemm_sharded(c, G, n, n, Yin, n, b, n, Out, 0, 1);
             kprof_end(c, K_GQ_GEMM);
         };
         auto iterate = [&](int count) {   // plain subspace iteration

@@ -250,10 +250,11 @@ void xtx_product(Ctx &c, const double *X, int n, double *S) {
 // B K x N: rows of Out split in 64-row blocks, each written transposed into
 // the packed T (N x M col-major = Out row-major), gathered, transposed back.
 void rows_gemm_sharded(Ctx &c, const double *A, int lda, int M, const double *B, int ldb, int N, int K,
-                       double *Out, int splitk_plain) {
+                       double *Out, int splitk_plain, int tag) {
     if (!c.shard.active) {
         GemmArgs g{M, N, K, A, lda, true, B, ldb, Out, M};
         g.splitk = splitk_plain;
+        g.tag = tag;
         gemm_f64(g, c.buf[S_PARTIAL], c.cur);
         return;
     }
@@ -266,6 +267,7 @@ void rows_gemm_sharded(Ctx &c, const double *A, int lda, int M, const double *B,
         GemmArgs g{rb[r + 1] - rb[r], N, K, A + (size_t)rb[r] * lda, lda, true, B, ldb, T + (size_t)rb[r] * N, N};
         g.store_t = true;
         g.splitk = 1;
+        g.tag = tag;
         gemm_f64(g, c.buf[S_PARTIAL], c.cur);
     }
     std::vector<size_t> off(R + 1);

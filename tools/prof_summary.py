@@ -18,9 +18,11 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "gpurun_out")
 
-# bench.py kernel class -> rocprof kernel-name prefix
-CLASSES = {"coniss": "void tp::k_coniss_t<false>", "ch": "tp::k_ch(", "gq_gemm": "void tp::k_gemm_f64<true>",
-           "xtx_gemm": "void tp::k_gemm_f64<true>", "xcxc_gemm": "void tp::k_gemm_f64<true>"}
+# bench.py kernel class -> the kernels one launch of that class runs (short names)
+CLASSES = {"coniss": ["tp::k_coniss_t<false, 1, false>"],
+           "ch": ["tp::k_ch_cut", "tp::k_ch_segstat", "tp::k_ch"],
+           "gq_gemm": ["tp::k_gemm_f64<true, 16, 1>", "tp::k_splitk_reduce<1>"],
+           "xtx_gemm": ["tp::k_xtx_i8_big<2>"]}
 
 
 def short(name):
@@ -36,7 +38,8 @@ def main():
                 os.path.join(ROOT, "profiles", f"{tag}_kernel_stats.csv"))
     tot = sum(float(r["TotalDurationNs"]) for r in stats)
     lines = [f"# {tag}: rocprofv3 --kernel-trace --stats, `python bench.py --steps {bench['steps']} "
-             f"--warmup {bench['warmup']} --no-cpu-baseline` ({steps} pipelines, C2 2000x2000, max_pcs=200)",
+             f"--warmup {bench['warmup']} --streams {bench['config'].get('streams_per_gpu', 1)} --no-cpu-baseline` "
+             f"({steps} pipelines, C2 2000x2000, max_pcs=200)",
              "", f"bench line of the profiled run: value {bench['value']} bins/s, "
                  f"{bench['ms_per_step']} ms/step (profiler attached)", "",
              "| kernel | calls/pipeline | ms/pipeline | avg us | % |", "|---|---|---|---|---|"]
@@ -66,13 +69,28 @@ def main():
             hb = (2 * fa + wa) * 1024
             traffic[short(name)] = {"launches": len(f), "fetch_kib": fa, "write_kib": wa, "hbm_bytes": hb}
             lines.append(f"| `{short(name)}` | {len(f)} | {fa:.0f} | {wa:.0f} | {hb / 1e6:.2f} |")
+    # per-class figures: kernels of one class launch, summed (avg duration from
+    # the trace stats, HBM bytes from the PMC passes)
+    avg_us = {short(r["Name"]): float(r["AverageNs"]) / 1e3 for r in stats}
+    classes = {}
+    for cls, names in CLASSES.items():
+        if all(nm in avg_us for nm in names):
+            classes[cls] = {"kernels": names, "avg_us": sum(avg_us[nm] for nm in names),
+                            "hbm_bytes": (sum(traffic[nm]["hbm_bytes"] for nm in names)
+                                          if all(nm in traffic for nm in names) else None)}
+    if classes:
+        lines += ["", "## Bench kernel classes (one launch = these kernels)", "",
+                  "| class | kernels | avg us | hbm MB |", "|---|---|---|---|"]
+        for cls, rec in classes.items():
+            hb = f"{rec['hbm_bytes'] / 1e6:.2f}" if rec["hbm_bytes"] is not None else "-"
+            lines.append(f"| {cls} | {' + '.join('`%s`' % k for k in rec['kernels'])} | {rec['avg_us']:.1f} | {hb} |")
     with open(os.path.join(ROOT, "profiles", f"{tag}_summary.md"), "w") as fh:
         fh.write("\n".join(lines) + "\n")
     if traffic:
         cfg = bench["config"]
         with open(os.path.join(ROOT, "profiles", f"{tag}_traffic.json"), "w") as fh:
             json.dump({"tag": tag, "n0": cfg["n0"], "k": cfg["k"], "kernels": traffic,
-                       "classes": CLASSES}, fh, indent=1)
+                       "classes": classes}, fh, indent=1)
     print("\n".join(lines))
 
 

@@ -44,3 +44,16 @@ if what == "xtx":
                    S.ctypes.data_as(D), ctypes.byref(ns), ctypes.byref(ms), ctypes.byref(st))
     _lib.check(st)
     print(f"xtx b={b} mode={mode} slices={ns.value}: {ms.value*1e3:.1f} us")
+if what == "gemm":   # Z = G Q at the C2 shape by the library's policy: gemm M N K [reps]
+    M, N, K = b, int(sys.argv[3]), int(sys.argv[4])
+    reps = int(sys.argv[5]) if len(sys.argv) > 5 else 3
+    A = np.asfortranarray(rng.standard_normal((K, M)))
+    Bm = np.asfortranarray(rng.standard_normal((K, N)))
+    C = np.zeros((M, N), order="F")
+    ms = ctypes.c_double(0)
+    I = lambda v: ctypes.byref(ctypes.c_int(v))  # noqa: E731
+    for _ in range(reps):
+        L.tp_debug_gemm(A.ctypes.data_as(D), Bm.ctypes.data_as(D), I(M), I(N), I(K), I(1), I(0), I(2),
+                        C.ctypes.data_as(D), ctypes.byref(ms), ctypes.byref(st))
+        _lib.check(st)
+    print(f"gemm {M}x{N}x{K}: {ms.value*1e3:.1f} us")
