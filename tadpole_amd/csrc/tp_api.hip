@@ -24,6 +24,17 @@ static thread_local std::string g_err;
 
 void fail(int status, const std::string &msg) { throw Error{status, msg}; }
 
+// TP_TRACE_SYNC=1 (debugging hangs): synchronise and report at stage marks
+void trace_mark(hipStream_t s, const char *what) {
+    static const bool on = getenv("TP_TRACE_SYNC") && getenv("TP_TRACE_SYNC")[0] == '1';
+    if (!on) return;
+    fprintf(stderr, "[tp] %s ...", what);
+    fflush(stderr);
+    const hipError_t e = hipStreamSynchronize(s);
+    fprintf(stderr, " %s\n", e == hipSuccess ? "done" : hipGetErrorString(e));
+    fflush(stderr);
+}
+
 void hip_check(hipError_t e, const char *what, const char *file, int line) {
     if (e != hipSuccess) {
         char b[512];
@@ -424,16 +435,19 @@ static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_cl
     double *X = c.buf[S_X].as<double>((size_t)n * n);
     double *m = c.buf[S_COLMEAN].as<double>(n);
     launch_gather_colmean(d_M, n0, d_good, n, X, m, s);
+    trace_mark(s, "mask");
     tm.mark();
     // ---- sparse_cor (R/TADpole.R:94-100,448-449)
     double *S = c.buf[S_S].as<double>((size_t)n * n);
     double *C = c.buf[S_C].as<double>((size_t)n * n);
     {
         kprof_begin(c, K_COR_GEMM);
+        trace_mark(s, "cor: start");
         xtx_product(c, X, n, S);
         kprof_end(c, K_COR_GEMM);
     }
     launch_cor_epilogue(S, m, n, C, s);
+    trace_mark(s, "cor");
     tm.mark();
     // ---- prcomp (R/TADpole.R:452-453)
     const int k = std::min(max_pcs, n);
@@ -442,6 +456,7 @@ static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_cl
     double *P = c.buf[S_P].as<double>((size_t)n * k);
     double *Pt = c.buf[S_PT].as<double>((size_t)n * k);
     PcaStats ps = pca_dev(c, C, n, k, P, Pt, nullptr);
+    trace_mark(s, "pca");
     tm.mark();
     // ---- find_params + final tree (R/TADpole.R:456-460)
     o.sw = run_sweep(c, Pt, n, k, min_clusters, w_cap, n_cluster, scores, merge, height, boundary);

@@ -22,6 +22,7 @@ struct Error {
 };
 
 [[noreturn]] void fail(int status, const std::string &msg);
+void trace_mark(hipStream_t s, const char *what);   // TP_TRACE_SYNC=1: sync + stderr mark
 void hip_check(hipError_t e, const char *what, const char *file, int line);
 #define TP_HIP(x) ::tp::hip_check((x), #x, __FILE__, __LINE__)
 

@@ -134,6 +134,7 @@ PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d
         sym_gemm_sharded(c, g);
         kprof_end(c, K_G_GEMM);
     }
+    trace_mark(s, "pca: G");
     const int over = std::max(32, k / 4);
     int b = std::min(n, ((k + over + 31) / 32) * 32);
     st.block = b;
@@ -160,6 +161,7 @@ PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d
         h_theta.resize(n);
         TP_HIP(hipMemcpyAsync(h_theta.data(), theta, n * sizeof(double), hipMemcpyDeviceToHost, s));
         TP_HIP(hipStreamSynchronize(s));
+        trace_mark(s, "pca: exact eig");
         st.iters = 0;
     } else {
         double *Q = c.buf[S_Q].as<double>((size_t)n * b);

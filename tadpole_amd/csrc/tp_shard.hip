@@ -223,6 +223,7 @@ void xtx_product(Ctx &c, const double *X, int n, double *S) {
         return;
     }
     const int8_t *sl = xtx_slices(c, X, n, ns);
+    trace_mark(c.cur, "xtx: slices");
     // 128-column tiles (the LDS-staged kernel) for n >= 1024 and <= 2 slices,
     // else 64-column tiles; the products are exact, so any split gives the same bits
     const bool big = n >= 1024 && ns <= 2;
@@ -233,6 +234,7 @@ void xtx_product(Ctx &c, const double *X, int n, double *S) {
     };
     if (!c.shard.active) {
         tiles(0, -1);
+        trace_mark(c.cur, "xtx: tiles");
         return;
     }
     const int R = shard_count(c);

@@ -485,6 +485,9 @@ template __global__ void k_coniss_t<true, 16, true>(SweepDev, double *);
 
 // ------------------------------------------------------------ CH over cuts
 // canonical segment statistics of rows s..e, by one wave (see tpo_seg_ss)
+// RB rows per batch (RB x KMAXSLOT loads in flight); the order of the sums is
+// the same for any RB
+template <int RB = 4>
 __device__ double seg_ss_wave(const double *Pt, int ldp, int k, int s, int e, double *sumout, int lane) {
     const double fn = (double)(e - s + 1);
     bool ok[KMAXSLOT];
@@ -495,18 +498,18 @@ __device__ double seg_ss_wave(const double *Pt, int ldp, int k, int s, int e, do
         ok[t] = jj[t] < k;
         if (!ok[t]) jj[t] = 0;   // safe address, value unused
     }
-    // pass 1: column sums, sequential over rows per column; 4 rows per step
-    // so 16 independent loads are in flight
+    // pass 1: column sums, sequential over rows per column; RB rows per step
+    // so RB x KMAXSLOT independent loads are in flight
     double sj[KMAXSLOT] = {0.0, 0.0, 0.0, 0.0};
     int a = s;
-    for (; a + 3 <= e; a += 4) {
-        double x[4][KMAXSLOT];
+    for (; a + RB - 1 <= e; a += RB) {
+        double x[RB][KMAXSLOT];
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
+        for (int r = 0; r < RB; ++r)
 #pragma unroll
             for (int t = 0; t < KMAXSLOT; ++t) x[r][t] = Pt[(size_t)(a + r) * ldp + jj[t]];
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
+        for (int r = 0; r < RB; ++r)
 #pragma unroll
             for (int t = 0; t < KMAXSLOT; ++t) sj[t] = sj[t] + x[r][t];
     }
@@ -520,14 +523,14 @@ __device__ double seg_ss_wave(const double *Pt, int ldp, int k, int s, int e, do
         if (sumout && ok[t]) sumout[jj[t]] = sj[t];
     }
     a = s;
-    for (; a + 3 <= e; a += 4) {
-        double x[4][KMAXSLOT];
+    for (; a + RB - 1 <= e; a += RB) {
+        double x[RB][KMAXSLOT];
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
+        for (int r = 0; r < RB; ++r)
 #pragma unroll
             for (int t = 0; t < KMAXSLOT; ++t) x[r][t] = Pt[(size_t)(a + r) * ldp + jj[t]];
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
+        for (int r = 0; r < RB; ++r)
 #pragma unroll
             for (int t = 0; t < KMAXSLOT; ++t) {
                 double d = x[r][t] - mj[t];
@@ -547,44 +550,52 @@ __device__ double seg_ss_wave(const double *Pt, int ldp, int k, int s, int e, do
     return wave_sum(part);
 }
 
-// tr(S) over all rows: wave w owns column slot t = w (columns 64w + lane);
-// per column the canonical sequential sums, combined in slot order through LDS
-// exactly as seg_ss_wave's `part` (same bits).
+// tr(S) over all rows: thread j owns column j (the canonical sequential sums
+// of seg_ss_wave, combined in slot order through LDS exactly as its `part`:
+// same bits).  Rows stream in batches of 32 with the next batch's loads
+// issued before the current batch is summed (the pass is latency-bound).
 __global__ void __launch_bounds__(256) k_trS(const double *Pt, int n, int ldp, int k, double *out) {
     __shared__ double ssl[KMAXSLOT][64];
+    constexpr int RB = 32;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int j = lane + 64 * w;
-    const bool ok = j < k;
-    const int jj = ok ? j : 0;
+    const int jj = j < k ? j : 0;
     const double fn = (double)n;
-    // one thread per column, rows in order (the canonical sequential sums):
-    // 32 loads in flight per batch -- the pass is L2-latency bound otherwise
+    double x[2][RB];
+    auto fetch = [&](double (&d)[RB], int a) {
+#pragma unroll
+        for (int r = 0; r < RB; ++r) d[r] = a + r < n ? Pt[(size_t)(a + r) * ldp + jj] : 0.0;
+    };
     double sj = 0.0;
-    int a = 0;
-    for (; a + 31 < n; a += 32) {
-        double x[32];
+    fetch(x[0], 0);
+    for (int a = 0; a < n; a += 2 * RB) {
+        fetch(x[1], a + RB);
 #pragma unroll
-        for (int r = 0; r < 32; ++r) x[r] = Pt[(size_t)(a + r) * ldp + jj];
+        for (int r = 0; r < RB; ++r)
+            if (a + r < n) sj = sj + x[0][r];
+        fetch(x[0], a + 2 * RB);
 #pragma unroll
-        for (int r = 0; r < 32; ++r) sj = sj + x[r];
+        for (int r = 0; r < RB; ++r)
+            if (a + RB + r < n) sj = sj + x[1][r];
     }
-    for (; a < n; ++a) sj = sj + Pt[(size_t)a * ldp + jj];
     const double mj = sj / fn;
     double ss = 0.0;
-    a = 0;
-    for (; a + 31 < n; a += 32) {
-        double x[32];
+    fetch(x[0], 0);
+    for (int a = 0; a < n; a += 2 * RB) {
+        fetch(x[1], a + RB);
 #pragma unroll
-        for (int r = 0; r < 32; ++r) x[r] = Pt[(size_t)(a + r) * ldp + jj];
+        for (int r = 0; r < RB; ++r)
+            if (a + r < n) {
+                const double d = x[0][r] - mj;
+                ss = fma(d, d, ss);
+            }
+        fetch(x[0], a + 2 * RB);
 #pragma unroll
-        for (int r = 0; r < 32; ++r) {
-            double d = x[r] - mj;
-            ss = fma(d, d, ss);
-        }
-    }
-    for (; a < n; ++a) {
-        double d = Pt[(size_t)a * ldp + jj] - mj;
-        ss = fma(d, d, ss);
+        for (int r = 0; r < RB; ++r)
+            if (a + RB + r < n) {
+                const double d = x[1][r] - mj;
+                ss = fma(d, d, ss);
+            }
     }
     ssl[w][lane] = ss;
     __syncthreads();
@@ -593,7 +604,7 @@ __global__ void __launch_bounds__(256) k_trS(const double *Pt, int n, int ldp, i
 #pragma unroll
         for (int t = 0; t < KMAXSLOT; ++t)
             if (lane + 64 * t < k) part = part + ssl[t][lane];
-        double v = wave_sum(part);
+        const double v = wave_sum(part);
         if (lane == 0) *out = v;
     }
 }
@@ -714,8 +725,9 @@ void sweep_dedup_bind(SweepDev &sd, void *base, int hcap, int ucap) {
     sd.ucap = ucap;
 }
 __global__ void __launch_bounds__(CH_THREADS) k_ch(SweepDev sd) {
-    __shared__ int segs[CH_SEGMAX + 1], alive[CH_SEGMAX], mbl[CH_SEGMAX];
+    __shared__ int segs[CH_SEGMAX + 1], mbl[CH_SEGMAX];
     __shared__ int src[CH_SEGMAX];   // segment's statistics: ustore index, or -1 = this tree's scratch
+    __shared__ int gbl[CH_SEGMAX], lnk_l[CH_SEGMAX], lnk_r[CH_SEGMAX];   // level -> segment, alive list
     __shared__ double ssg[CH_SEGMAX];
     const int n = sd.n, k = sd.k, ldp = sd.ldp;
     const int ti = blockIdx.x;
@@ -749,7 +761,6 @@ __global__ void __launch_bounds__(CH_THREADS) k_ch(SweepDev sd) {
             while (sd.hkeys[slot] != key) slot = (slot + 1) & mask;   // k_ch_cut inserted it
             const int idx = sd.hidx[slot];
             src[g] = idx;
-            alive[g] = 1;
             if (idx >= 0) ssg[g] = sd.ustore[(size_t)idx * (k + 1) + k];
         }
         __syncthreads();
@@ -762,61 +773,113 @@ __global__ void __launch_bounds__(CH_THREADS) k_ch(SweepDev sd) {
         finest_cut(sd, ti, nc, mbl, segs);
         for (int g = w; g < nc; g += nw) {
             double ss = seg_ss_wave(sd.Pt, ldp, k, segs[g], segs[g + 1] - 1, seg + (size_t)g * k, lane);
-            if (lane == 0) { ssg[g] = ss; alive[g] = 1; src[g] = -1; }
+            if (lane == 0) { ssg[g] = ss; src[g] = -1; }
         }
+    }
+    // level structure, in parallel: the segment whose start each level's
+    // boundary is (binary search of the sorted cut) and the alive list links
+    for (int t = threadIdx.x; t < nc - 1; t += blockDim.x) {
+        const int bt = mb[n - 2 - t];   // level lev = t + 1 removes boundary bt
+        int lo = 1, hi = nc - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (segs[mid] < bt) lo = mid + 1;
+            else hi = mid;
+        }
+        gbl[t] = lo;
+    }
+    for (int g = threadIdx.x; g < nc; g += blockDim.x) {
+        lnk_l[g] = g - 1;
+        lnk_r[g] = g + 1;
     }
     __syncthreads();
     if (w != 0) return;
-    // wave 0 only from here: every lane keeps its own copy of the state it
-    // reads back (alive flags written by all lanes, sums by their own lane)
+    // wave 0 only from here.  Level lev merges segment gb (starting at the
+    // removed boundary) into its alive left neighbour ga.  The merged sums stay
+    // in registers for the next level, whose other operands are loaded while
+    // this level's increment is computed.  LDS state is written by every lane
+    // with the same value.
     const double trS = *sd.trS;
     double trW = 0.0;
     for (int g = 0; g < nc; ++g) trW = trW + ssg[g];
     if (lane == 0)
         score_row[(size_t)(nc - 1) * ldsc] = ((double)(n - nc) * (trS - trW)) / ((double)(nc - 1) * trW);
-    for (int lev = nc - 1; lev >= m && lev >= 1; --lev) {
-        const int b = mb[n - lev - 1];
-        int gb = -1;
-        for (int g = lane; g < nc; g += 64)
-            if (alive[g] && segs[g] == b) gb = g;
-        for (int o = 1; o < 64; o <<= 1) gb = max(gb, __shfl_xor(gb, o, 64));   // once per level
-        int ga = gb - 1;
-        while (ga >= 0 && !alive[ga]) --ga;
-        int nx = gb + 1;
-        while (nx < nc && !alive[nx]) ++nx;
+    auto sums_of = [&](int g) -> const double * {
+        const int ix = src[g];
+        return ix >= 0 ? sd.ustore + (size_t)ix * (k + 1) : seg + (size_t)g * k;
+    };
+    auto load4 = [&](double (&d)[KMAXSLOT], const double *p) {
+#pragma unroll
+        for (int t = 0; t < KMAXSLOT; ++t) {
+            const int j = lane + 64 * t;
+            d[t] = j < k ? p[j] : 0.0;
+        }
+    };
+    int lev = nc - 1;
+    double A[KMAXSLOT], B[KMAXSLOT], M[KMAXSLOT], A2[KMAXSLOT], B2[KMAXSLOT];
+    int ga = 0, gb = 0, nx = 0;
+    if (lev >= m && lev >= 1) {
+        gb = gbl[lev - 1];
+        ga = lnk_l[gb];
+        nx = lnk_r[gb];
+        load4(A, sums_of(ga));
+        load4(B, sums_of(gb));
+    }
+    for (; lev >= m && lev >= 1; --lev) {
+        const int b = segs[gb];
         const int na = b - segs[ga];
         const int nbb = (nx < nc ? segs[nx] : n) - b;
-        const double fa = (double)na, fb = (double)nbb;
-        const int ia = src[ga], ib = src[gb];
-        const double *SA = ia >= 0 ? sd.ustore + (size_t)ia * (k + 1) : seg + (size_t)ga * k;
-        const double *SB = ib >= 0 ? sd.ustore + (size_t)ib * (k + 1) : seg + (size_t)gb * k;
-        double *DA = seg + (size_t)ga * k;   // the merged segment's sums
-        double acc = 0.0;
-#pragma unroll
-        for (int t = 0; t < KMAXSLOT; ++t) {
-            int j = lane + 64 * t;
-            if (j < k) {
-                double t1 = SA[j] * fb;
-                double t2 = SB[j] * fa;
-                double e = t1 - t2;
-                acc = fma(e, e, acc);
-            }
-        }
-        double tot = wave_sum(acc);
-        trW = trW + tot / (fa * fb * (fa + fb));
-#pragma unroll
-        for (int t = 0; t < KMAXSLOT; ++t) {
-            int j = lane + 64 * t;
-            if (j < k) DA[j] = SA[j] + SB[j];
-        }
-        alive[gb] = 0;
+        // unlink gb; ga's sums move to this tree's scratch (stored below)
+        lnk_r[ga] = nx;
+        if (nx < nc) lnk_l[nx] = ga;
         src[ga] = -1;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // the next level's operands other than the merged segment: loads in flight now
+        const bool more = lev - 1 >= m && lev - 1 >= 1;
+        int ga2 = ga, gb2 = gb, nx2 = nx;
+        if (more) {
+            gb2 = gbl[lev - 2];
+            ga2 = lnk_l[gb2];
+            nx2 = lnk_r[gb2];
+            if (ga2 != ga) load4(A2, sums_of(ga2));
+            if (gb2 != ga) load4(B2, sums_of(gb2));
+        }
+        const double fa = (double)na, fb = (double)nbb;
+        double acc = 0.0;
+#pragma unroll
+        for (int t = 0; t < KMAXSLOT; ++t) {
+            const int j = lane + 64 * t;
+            if (j < k) {
+                const double t1 = A[t] * fb;
+                const double t2 = B[t] * fa;
+                const double e = t1 - t2;
+                acc = fma(e, e, acc);
+            }
+        }
+        const double tot = wave_sum(acc);
+        trW = trW + tot / (fa * fb * (fa + fb));
+        double *DA = seg + (size_t)ga * k;   // the merged segment's sums
+#pragma unroll
+        for (int t = 0; t < KMAXSLOT; ++t) {
+            const int j = lane + 64 * t;
+            M[t] = A[t] + B[t];
+            if (j < k) DA[j] = M[t];
+        }
         if (lane == 0)
             score_row[(size_t)(lev - 1) * ldsc] =
                 lev == 1 ? r_nan() : ((double)(n - lev) * (trS - trW)) / ((double)(lev - 1) * trW);
+        if (more) {
+#pragma unroll
+            for (int t = 0; t < KMAXSLOT; ++t) {
+                A[t] = ga2 == ga ? M[t] : A2[t];
+                B[t] = gb2 == ga ? M[t] : B2[t];
+            }
+            ga = ga2;
+            gb = gb2;
+            nx = nx2;
+        }
     }
 }
 
@@ -878,21 +941,26 @@ void launch_sweep(const SweepDev &sd, hipStream_t s, Ctx *prof) {
     TP_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_trS, dim3(1), dim3(256), 0, s, sd.Pt, sd.n, sd.ldp, sd.k, sd.trS);
     TP_HIP(hipGetLastError());
+    trace_mark(s, "trS");
     run_coniss(sd, s, false, prof);
+    trace_mark(s, "coniss");
     if (prof) kprof_begin(*prof, K_CH);
     if (sd.hkeys) {
         TP_HIP(hipMemsetAsync(sd.hkeys, 0xFF, (size_t)sd.hcap * sizeof(unsigned long long), s));
         TP_HIP(hipMemsetAsync(sd.ucount, 0, sizeof(int), s));
         hipLaunchKernelGGL(k_ch_cut, dim3(sd.ntrees), dim3(256), 0, s, sd);
         TP_HIP(hipGetLastError());
+        trace_mark(s, "ch_cut");
         const int g = std::max(1, std::min(256, (sd.ucap + 3) / 4));
         hipLaunchKernelGGL(k_ch_segstat, dim3(g), dim3(256), 0, s, sd);
         TP_HIP(hipGetLastError());
+        trace_mark(s, "ch_segstat");
         hipLaunchKernelGGL(k_ch, dim3(sd.ntrees), dim3(256), 0, s, sd);
     } else {
         hipLaunchKernelGGL(k_ch, dim3(sd.ntrees), dim3(CH_THREADS), 0, s, sd);
     }
     TP_HIP(hipGetLastError());
+    trace_mark(s, "ch");
     if (prof) kprof_end(*prof, K_CH);
 }
 

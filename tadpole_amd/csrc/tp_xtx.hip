@@ -304,7 +304,7 @@ void xtx_int8_tiles128(Ctx &c, const int8_t *sl, int n, int ns, double *d_S, int
 
 void xtx_int8_tiles(Ctx &c, const int8_t *sl, int n, int ns, double *d_S, int tc0, int tc1) {
     const int Kp = xtx_kp(n), Np = (n + 127) / 128 * 128;
-    const int tn = Kp / 64;
+    const int tn = (n + 63) / 64;   // output column tiles (rows of the slices: < Np)
     tc0 = std::max(0, tc0);
     tc1 = tc1 < 0 ? tn : std::min(tn, tc1);
     if (tc1 <= tc0) return;
