@@ -1203,7 +1203,7 @@ extern "C" {
 /* Test hook: set a tuning switch, *old = its previous value.  which: 0 CH
  * segment statistics shared across trees, 1 cap on their store (0 = automatic),
  * 2 short-K panel GEMM, 3 GEMM LDS stage depth (16 / 32), 4 register-resident
- * tridiagonalisation, 5 int8 X'X, 6 PCA degree margin. */
+ * tridiagonalisation, 5 int8 X'X, 6 PCA degree margin, 7 XCD-aware GEMM order. */
 void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
     guarded(status, [&] {
         int *p = nullptr;
@@ -1215,6 +1215,7 @@ void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
         case 4: p = &g_sytrd_reg; break;
         case 5: p = &g_xtx_int8; break;
         case 6: p = &g_pca_margin; break;
+        case 7: p = &g_gemm_xcd; break;
         default: fail(TP_ERR_ARG, "unknown knob");
         }
         if (*which == 3 && *value != 16 && *value != 32) fail(TP_ERR_ARG, "stage depth must be 16 or 32");

@@ -77,7 +77,7 @@ template <bool TA, int KB, int TAG = 0>
 __global__ void __launch_bounds__(256) k_gemm_f64(int M, int N, int K, const double *__restrict__ A, int lda,
                                                   const double *__restrict__ B, int ldb, double *__restrict__ C,
                                                   int ldc, int store_t, int sym, int tcol0, int kchunk,
-                                                  size_t part_stride) {
+                                                  size_t part_stride, int g_xcd_order) {
     __shared__ double As[2][BM][KB + 2];
     __shared__ double Bs[2][BN][KB + 2];
     // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs (each
@@ -86,7 +86,7 @@ __global__ void __launch_bounds__(256) k_gemm_f64(int M, int N, int K, const dou
     // column tiles, same k chunk) run together and share it in that L2.
     const int total = (int)gridDim.x;   // tiles x k chunks
     const int xcd = (int)blockIdx.x & 7, slot = (int)blockIdx.x >> 3;
-    const int Lg = xcd * (total >> 3) + min(xcd, total & 7) + slot;
+    const int Lg = g_xcd_order ? xcd * (total >> 3) + min(xcd, total & 7) + slot : (int)blockIdx.x;
     int bm, bn, z;
     if (sym) {  // linear id -> upper tile (bm <= bn), column by column from tile column tcol0
         const int nt = total / ((K + kchunk - 1) / kchunk);   // tiles (total / k chunks)
@@ -174,6 +174,7 @@ __global__ void __launch_bounds__(256) k_gemm_f64(int M, int N, int K, const dou
                 }
             }
 }
+int g_gemm_xcd = 1;   // XCD-aware workgroup order (0: linear; A/B tests)
 int g_gemm_kb = 16;   // k depth of the 64 x 64 kernel's LDS stages (16 / 32; same bits; 32 measured no faster)
 
 // ---------------------------------------------------------------------------
@@ -476,19 +477,19 @@ void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s) {
     if (g_gemm_kb == 32) {
         if (g.trans_a)
             hipLaunchKernelGGL((k_gemm_f64<true, 32>), grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb,
-                               out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride);
+                               out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride, g_gemm_xcd);
         else
             hipLaunchKernelGGL((k_gemm_f64<false, 32>), grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb,
-                               out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride);
+                               out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride, g_gemm_xcd);
     } else if (g.trans_a && g.tag == 1) {
         hipLaunchKernelGGL((k_gemm_f64<true, 16, 1>), grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb,
-                           out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride);
+                           out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride, g_gemm_xcd);
     } else if (g.trans_a) {
         hipLaunchKernelGGL((k_gemm_f64<true, 16>), grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb,
-                           out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride);
+                           out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride, g_gemm_xcd);
     } else {
         hipLaunchKernelGGL((k_gemm_f64<false, 16>), grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb,
-                           out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride);
+                           out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride, g_gemm_xcd);
     }
     TP_HIP(hipGetLastError());
     if (S > 1) {

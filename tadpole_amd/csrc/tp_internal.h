@@ -119,6 +119,7 @@ struct GemmArgs {
 void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s);
 extern int g_gemm_panel;   // short-K tall-skinny 32 x 64 kernel enabled (default 1)
 extern int g_gemm_kb;      // LDS stage depth of the 64 x 64 kernel (16 / 32)
+extern int g_gemm_xcd;     // XCD-aware workgroup order of the 64 x 64 kernel (default 1)
 void launch_chol(double *d_W, double *d_rdiag, int b, double rel, int *d_info, hipStream_t s);
 void launch_chol_stamped(double *d_W, double *d_rdiag, int b, double rel, int *d_info, long long *d_st,
                          hipStream_t s);

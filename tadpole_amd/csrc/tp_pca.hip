@@ -18,6 +18,9 @@
 #include <cmath>
 #include <vector>
 
+#include <cstdio>
+#include <cstdlib>
+
 #include "tp_common.cuh"
 #include "tp_internal.h"
 
@@ -320,14 +323,27 @@ PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d
             const double thk = h_theta[b - k], thb = h_theta[0];
             const double rho = (thk > 0 && thb > 0) ? std::min(0.98, std::max(1e-3, thb / thk)) : 0.9;
             st.rate = rho;
+            if (getenv("TP_TRACE_PCA"))
+                fprintf(stderr, "[pca] n=%d round %d degree %d worst %.2e thk/thb %.3f cut %.3e gk %.3f mdeg %d\n", n,
+                        round, done, worst, thb > 0 ? thk / thb : 0.0, cut, gk, mdeg);
             if (!(worst > target * 10) || done >= max_deg) break;
-            int need = (int)std::ceil(std::log(target / worst) / std::log(rho)) + 2;
-            int more = std::max(2, std::min(max_deg - done, need));
+            int more;
             if (cut > 0) {
-                // Ritz values bound the spectrum better now: cut at theta_b
+                // Ritz values bound the spectrum better now: cut at theta_b and
+                // take the Chebyshev growth at theta_k per degree for the
+                // factor worst / target still to remove
                 cut = std::max(cut, thb);
-                for (int deg = 0; deg < more; deg += mdeg) cheb_block(mdeg, cut);
+                double g = 1.0005;
+                if (thk > cut) {
+                    const double x = 2.0 * thk / cut - 1.0;
+                    g = std::max(g, x + std::sqrt(x * x - 1.0));
+                }
+                const int need = (int)std::ceil(std::log(worst / target) / std::log(g)) + 1;
+                more = std::max(1, std::min(max_deg - done, need));
+                for (int deg = 0; deg < more; deg += mdeg) cheb_block(std::min(mdeg, more - deg), cut);
             } else {
+                const int need = (int)std::ceil(std::log(target / worst) / std::log(rho)) + 2;
+                more = std::max(2, std::min(max_deg - done, need));
                 iterate(more);
             }
             done += more;
