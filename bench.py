@@ -3,25 +3,28 @@
 A step = one TADpole()-equivalent pipeline over one synthetic N0 x N0 Hi-C
 matrix already resident in HBM: NA->0 + symmetrise, bad-column mask, Pearson
 correlation, PCA to max_pcs, CONISS sweep over every PC prefix, broken stick,
-Calinski-Harabasz, parameter choice, TAD coordinates of every significant level.
-Workload = BASELINE.json configs[1] (C2: synthetic 2000 x 2000, max_pcs=200).
+Calinski-Harabasz, parameter choice, TAD coordinates of every significant level
+(host assembly of the `tadpole` object included).
 
-Throughput: up to --streams (default 12) matrices in flight per GPU, each on
-its own HIP stream / library context / host thread -- the latency-bound stages
-of one pipeline (CONISS merges, the one-workgroup Cholesky and
-tridiagonalisation) leave most of the 256 CUs idle, and a stream of matrices (a
-genome is 23 of them) fills them.  HIP maps streams onto GPU_MAX_HW_QUEUES
-hardware queues (4 by default); streams sharing a queue serialise, so the bench
-raises it to 16.  value = bins of all matrices / wall time; the one-matrix
-latency is reported next to it (config.single_stream_ms_per_matrix).
+Workload: BASELINE.json configs[2], C3 (chr18 @10kb shape: 7808 x 7808,
+max_pcs = 200), the largest configuration that is one matrix on one GPU (C4 is
+23 matrices, C5 two arms over 8 GPUs).  value = N0 x K / wall time of K
+pipelines run one after another on one stream (N0 over one
+pipeline's wall time).  The throughput of S matrices in flight on S streams is
+reported beside it (`throughput`), never as `value`.
 
 Multi-GPU: one process per GPU (torch.distributed.run); each rank processes its
-own matrices (independent chromosomes): weak scaling, no
+own matrix (independent chromosomes): weak scaling, no
 data-path collective.  value = bins of all ranks / max-over-ranks time.
+--sharded: one matrix split over all ranks (RCCL all-gathers, strong scaling).
+--e2e-tsv N: the north_star end-to-end line instead: TADpole() on an N-bin
+tab-separated file (native parse + upload + pipeline + assembly).
 
-Extra fields: "roofline" for the dominant kernel (HIP events inside the
-library, same stream), "cpu_baseline" (the CPU oracle on this host, rank 0),
-"parity" (rank 0's TAD boundaries vs the oracle on the same matrix).
+Extra fields: "roofline" for the kernel class with the largest time per
+pipeline (HIP events recorded inside the library on the stream the kernels run
+on, averaged over the timed steps), "cpu_baseline" (the CPU oracle on this
+host, rank 0, N=1), "parity" (rank 0's result vs the committed oracle fixture
+and vs the CPU oracle run on the same matrix).
 """
 from __future__ import annotations
 
@@ -34,21 +37,12 @@ import time
 
 import numpy as np
 
-# before HIP initialises (torch import / first device call): one hardware queue
-# per concurrent pipeline (see the docstring); raises a lower setting (HIP's
-# default, 4, is often exported explicitly)
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:
-    os.environ["GPU_MAX_HW_QUEUES"] = "16"
-
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
-FP64_MFMA_PEAK_TFLOPS = 78.6     # MI355X FP64 matrix, dense (AMD spec)
-# what v_mfma_f64_16x16x4_f64 sustains on this chip: back-to-back, independent
-# accumulators, 4 waves/SIMD on every CU (tools/mfma_rate.hip; 33 TF/s at 1
-# wave/SIMD, 43 at 2)
-FP64_MFMA_MEASURED_TFLOPS = 45.0
+FP64_MFMA_PEAK_TFLOPS = 78.6     # MI355X FP64 matrix, dense (AMD spec; MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0            # MI355X HBM3E (MI355X_MICROARCH.md)
+METRIC = "bins/sec (NxN matrix) at 1/2/4/8 GPUs; TAD boundary bit-match vs R ref"
 
 
 def _pmc_traffic(kernel_class, n0, k):
@@ -72,12 +66,12 @@ def _pmc_traffic(kernel_class, n0, k):
 
 def _config_name(n0, max_pcs):
     """BASELINE.json config this run corresponds to."""
+    if max_pcs == 200 and n0 == 7808:
+        return "C3"
     if max_pcs == 200 and n0 == 2000:
         return "C2"
-    if max_pcs == 200 and n0 == 7808:
-        return "C3 shape (chr18 @10kb)"
     if max_pcs == 200 and n0 in (24300, 21300):
-        return "C5 arm shape (chr1 @5kb)"
+        return "C5 arm shape"
     if n0 == 200:
         return "C1 shape"
     return "custom"
@@ -86,24 +80,79 @@ def _config_name(n0, max_pcs):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=96)
+    ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--n0", type=int, default=2000)
+    ap.add_argument("--n0", type=int, default=7808)
     ap.add_argument("--max-pcs", type=int, default=200)
     ap.add_argument("--min-clusters", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-reps", type=int, default=3)
     ap.add_argument("--json-out", default=None)
-    ap.add_argument("--streams", type=int, default=12,
-                    help="matrices in flight per GPU (one stream + host thread each; the single-CU stages of one "
-                         "pipeline leave most of the chip idle); 1 = one matrix at a time")
+    ap.add_argument("--throughput-streams", type=int, default=8,
+                    help="after the timed region: S matrices in flight on S streams (0/1 = skip)")
+    ap.add_argument("--throughput-steps", type=int, default=16)
     ap.add_argument("--sharded", action="store_true",
                     help="one matrix split over all ranks (SURVEY §8(e)2, C5 arms): strong scaling")
+    ap.add_argument("--e2e-tsv", type=int, default=0,
+                    help="end-to-end TADpole() on an N-bin TSV file (parse included) instead of the HBM bench")
     return ap.parse_args()
+
+
+def write_tsv(m, path):
+    """Headerless tab-separated integer matrix (read.big.matrix's input)."""
+    vmax = int(m.max())
+    table = np.array([str(v) for v in range(vmax + 1)], dtype=object)
+    mi = m.astype(np.int64)
+    with open(path, "w") as f:
+        for r in range(mi.shape[0]):
+            f.write("\t".join(table[mi[r]]))
+            f.write("\n")
+
+
+def e2e_tsv(args):
+    """north_star: end-to-end TADpole() on a 10 000-bin matrix file."""
+    import tadpole_amd as tp
+    from tadpole_amd.synth import SEED_BASE, synth_hic
+    n0 = args.e2e_tsv
+    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"tadpole_e2e_{n0}.tsv")
+    m = synth_hic(n0, SEED_BASE + 3)
+    write_tsv(m, path)
+    size = os.path.getsize(path)
+    tp.TADpole(path, max_pcs=args.max_pcs)            # warm-up (device context, code objects)
+    t_parse, t_all = [], []
+    res = None
+    for _ in range(max(1, args.steps)):
+        t0 = time.perf_counter()
+        raw = tp.read_matrix(path)
+        t_parse.append(time.perf_counter() - t0)
+        del raw
+        t0 = time.perf_counter()
+        res = tp.TADpole(path, max_pcs=args.max_pcs)
+        t_all.append(time.perf_counter() - t0)
+    med = float(np.median(t_all))
+    stages = ["mask", "cor", "pca", "sweep", "total"]
+    out = {"metric": "end-to-end TADpole() seconds on an N-bin TSV file (north_star: < 1 s at 10k bins)",
+           "value": round(med, 4), "unit": "s", "higher_is_better": False, "n0": n0, "steps": len(t_all),
+           "tsv_bytes": size, "parse_s_median": round(float(np.median(t_parse)), 4),
+           "bins_per_s": round(n0 / med, 1), "n_pcs": res.n_pcs, "optimal_n_clusters": res.optimal_n_clusters,
+           "device_stages_ms": {q: round(float(res.timings_ms[i]), 3) for i, q in enumerate(stages)},
+           "data": "synthetic (tadpole_amd/synth.py, seed 20261015+3) written as an integer TSV"}
+    os.remove(path)
+    line = json.dumps(out)
+    print(line, flush=True)
+    if args.json_out:
+        with open(args.json_out, "w") as f:
+            f.write(line + "\n")
 
 
 def main():
     args = parse()
+    if args.throughput_streams > 1 and not args.sharded:
+        # concurrent pipelines need one hardware queue per stream (HIP's default
+        # is 4 and streams sharing a queue serialise); only before HIP starts
+        if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:
+            os.environ["GPU_MAX_HW_QUEUES"] = "16"
+    if args.e2e_tsv:
+        return e2e_tsv(args)
     import torch
     import torch.distributed as dist
 
@@ -115,14 +164,14 @@ def main():
         dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
     torch.cuda.set_device(local)
 
-    import tadpole_amd as tp
     from tadpole_amd import _lib
     from tadpole_amd.api import _assemble
     from tadpole_amd.synth import SEED_BASE, synth_hic
 
     L = _lib.load()
     n0 = args.n0
-    seed = SEED_BASE + 2 + (0 if args.sharded else 1000 * rank)   # sharded: every rank holds the same matrix
+    cfg = {7808: 3, 2000: 2}.get(n0, 3)
+    seed = SEED_BASE + cfg + (0 if args.sharded else 1000 * rank)   # sharded: every rank holds the same matrix
     host = synth_hic(n0, seed)
     flags = _lib.TP_FLAG_ROW_MAJOR
     if args.sharded:
@@ -133,9 +182,6 @@ def main():
     k_cap = max(1, min(args.max_pcs, n0))
     w_cap = n0
     I = ctypes.c_int
-    # one pipeline at a time when sharded: the ranks' collectives must be issued
-    # in the same order, one communicator per device
-    S = 1 if args.sharded else max(1, args.streams)
 
     class Lane:
         """One pipeline in flight: its own stream (hence its own library context
@@ -147,13 +193,12 @@ def main():
             self.bufs = dict(bad=np.zeros(n0, np.int32), good=np.zeros(n0, np.int32),
                              nclu=np.zeros(k_cap, np.int32), scores=np.zeros(k_cap * w_cap),
                              merge=np.zeros(2 * (n0 - 1), np.int32), height=np.zeros(n0 - 1),
-                             boundary=np.zeros(n0 - 1, np.int32), timings=np.zeros(16))
+                             boundary=np.zeros(n0 - 1, np.int32), timings=np.zeros(32))
 
-    lanes = [Lane(i) for i in range(S)]
+    lane0 = Lane(0)
     torch.cuda.synchronize()
 
-    def step(want_timings: bool, lane=None):
-        lane = lane or lanes[0]
+    def step(lane, want_timings=True):
         b, dev_m, stream = lane.bufs, lane.dev_m, lane.stream
         outs = [I(0) for _ in range(6)]
         n_good, k, w, n_pcs, n_clusters, st = outs
@@ -177,154 +222,175 @@ def main():
         return _assemble(res, np.flatnonzero(res["bad"]) + 1)
 
     for _ in range(args.warmup):
-        for ln in lanes:
-            step(False, ln)
+        step(lane0)
 
     def barrier():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
 
+    # ---- timed region: K pipelines, one after another, on one stream; the
+    # library records HIP events per kernel class on that stream
+    tms = []
     barrier()
     t0 = time.perf_counter()
     last = None
-    if S == 1:
-        for _ in range(args.steps):
-            last = step(False)
-    else:
-        # S host threads, one stream each, the K steps dealt round-robin (ctypes
-        # releases the GIL inside the library call)
-        import threading
-        outs = [None] * S
-
-        def run(i):
-            for _ in range(i, args.steps, S):
-                outs[i] = step(False, lanes[i])
-
-        th = [threading.Thread(target=run, args=(i,)) for i in range(S)]
-        for x in th:
-            x.start()
-        for x in th:
-            x.join()
-        last = outs[0]
+    for _ in range(args.steps):
+        last = step(lane0)
+        tms.append(last.timings_ms)
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    tm = np.mean(np.stack(tms), axis=0)
+    n, k = int(tm[14]), int(tm[15])
 
-    # latency of one matrix on its own (one stream), for reference next to the
-    # S-stream throughput in `value`
-    single_ms = None
+    # ---- throughput with S matrices in flight (not `value`)
+    thr = None
+    S = 1 if args.sharded else args.throughput_streams
     if S > 1:
+        import threading
+        lanes = [lane0] + [Lane(i) for i in range(1, S)]
+        for ln in lanes[1:]:
+            step(ln, False)
+        done = [0] * S
+        errs = []
+        outs = [None] * S
+
+        def run(i):
+            try:
+                for _ in range(i, args.throughput_steps, S):
+                    outs[i] = step(lanes[i], False)
+                    done[i] += 1
+            except Exception as e:   # noqa: BLE001 -- collected; the run fails below
+                errs.append(repr(e))
+
         barrier()
         t1 = time.perf_counter()
-        reps = max(3, min(10, args.steps // S))
-        for _ in range(reps):
-            step(False)
+        th = [threading.Thread(target=run, args=(i,)) for i in range(S)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
         barrier()
-        single_ms = (time.perf_counter() - t1) / reps * 1e3
-
-    # one more instrumented step for the per-kernel breakdown (not in `value`)
-    prof = step(True)
-    tm = prof.timings_ms
-    n = int(tm[14])
-    k = int(tm[15])
+        el2 = time.perf_counter() - t1
+        if errs:
+            raise RuntimeError(f"throughput lanes failed: {errs[:3]}")
+        same = all(o is not None and o.n_pcs == last.n_pcs and o.optimal_n_clusters == last.optimal_n_clusters
+                   and np.array_equal(o.scores.view(np.uint64), last.scores.view(np.uint64))
+                   and all(np.array_equal(o.clusters[q], last.clusters[q]) for q in last.clusters)
+                   for o in outs)
+        thr = {"streams": S, "matrices": int(sum(done)), "bins_per_s": round(n0 * sum(done) / el2, 1),
+               "ms_per_matrix": round(el2 / sum(done) * 1e3, 3), "lanes_identical": bool(same),
+               "note": "S matrices in flight on S streams (own library context each); not `value`"}
+        del lanes
 
     if rank == 0:
         value = n0 * (1 if args.sharded else world) * args.steps / elapsed
-        # ---- roofline of the dominant kernel
         share = 1.0 / world if args.sharded else 1.0   # sharded: this rank's part of each product
-        kern = {
-            "xtx_gemm": (tm[5], "mfma", 1, share * float(n) ** 3),              # N^3 (symmetric half)
-            "xcxc_gemm": (tm[6], "mfma", 1, share * float(n) ** 3),
-            "gq_gemm": (tm[7], "mfma", max(1, int(tm[8])), share * 2.0 * n * n * int(tm[12]) if tm[12] else 0.0),
-            "coniss": (tm[9], "hbm", 1, 40.0 * (n - 1) * k * (k + 1) / 2.0),    # bytes: 5 sum vectors/merge
-            "ch": (tm[10], "hbm", 1, 16.0 * n * k * k),                         # bytes: 2 passes/tree
+        krylov_steps, krylov_d, block = int(tm[16]), int(tm[17]), int(tm[12])
+        gq_launches = max(1, int(round(tm[8])))
+        if krylov_steps:   # one record = Xc K_t and Xc'(Xc K_t): 2 x 2 N^2 p flops
+            p = krylov_d // max(1, krylov_steps)
+            gq_flops = share * 4.0 * n * n * p
+        else:              # one record = G Q: 2 N^2 b flops
+            gq_flops = share * 2.0 * n * n * block
+        kern = {   # class: (ms per pipeline, bound, launches per pipeline, algorithmic work per launch, peak)
+            "xtx_gemm": (tm[5], "mfma", 1, share * float(n) ** 3, FP64_MFMA_PEAK_TFLOPS),
+            "xcxc_gemm": (tm[6], "mfma", 1, share * float(n) ** 3, FP64_MFMA_PEAK_TFLOPS),
+            "gq_gemm": (tm[7], "mfma", gq_launches, gq_flops, FP64_MFMA_PEAK_TFLOPS),
+            "coniss": (tm[9], "hbm", 1, 40.0 * (n - 1) * k * (k + 1) / 2.0, HBM_PEAK_GBS),   # 5 sum rows/merge
+            "ch": (tm[10], "hbm", 1, 16.0 * n * k * k, HBM_PEAK_GBS),                        # 2 passes/tree
         }
-        # Dominant kernel.  With S > 1 matrices in flight `value` is bound by
-        # how much of the chip each kernel class occupies, not by one
-        # pipeline's critical path: weight each class's time by the share of
-        # the 1024 SIMDs its grid fills (GEMMs: all; CONISS: 2 waves per tree;
-        # CH: 4 waves per tree).  With one stream: the longest class.
-        simd_share = {"xtx_gemm": 1.0, "xcxc_gemm": 1.0, "gq_gemm": 1.0,
-                      "coniss": min(1.0, 2.0 * k / 1024), "ch": min(1.0, 4.0 * k / 1024)}
-        chip_ms = {q: kern[q][0] * simd_share[q] for q in kern}
-        longest = max(kern, key=lambda q: kern[q][0])
-        dom = max(chip_ms, key=chip_ms.get) if S > 1 else longest
+        dom = max(kern, key=lambda q: kern[q][0])
 
         def rate(q):
-            ms_tot, bound, launches, per_launch = kern[q]
+            ms_tot, bound, launches, per_launch, peak = kern[q]
             avg_ms = ms_tot / launches
             if bound == "mfma":
-                return per_launch / (avg_ms * 1e-3) / 1e12, FP64_MFMA_PEAK_TFLOPS, "TFLOP/s", avg_ms
-            return per_launch / (avg_ms * 1e-3) / 1e9, HBM_PEAK_GBS, "GB/s", avg_ms
+                return per_launch / (avg_ms * 1e-3) / 1e12, peak, "TFLOP/s", avg_ms
+            return per_launch / (avg_ms * 1e-3) / 1e9, peak, "GB/s", avg_ms
 
-        ms_tot, bound, launches, per_launch = kern[dom]
+        ms_tot, bound, launches, per_launch, _ = kern[dom]
         achieved, peak, unit, avg_ms = rate(dom)
         traffic, tsrc = _pmc_traffic(dom, n0, k)
         roof = {"kernel": dom, "bound": bound, "achieved": round(achieved, 3), "peak": peak, "unit": unit,
                 "frac": round(achieved / peak, 5), "traffic": traffic, "traffic_source": tsrc,
                 "algorithmic_per_launch": per_launch, "avg_launch_ms": round(avg_ms, 4),
                 "launches_per_step": launches,
-                "dominance": ("largest SIMD-time share per matrix with %d matrices in flight" % S if S > 1
-                              else "longest kernel class of one pipeline"),
-                "chip_ms_per_matrix": {q: round(v, 4) for q, v in chip_ms.items()},
-                "breakdown_ms": {q: round(kern[q][0], 4) for q in kern},
+                "dominance": "largest kernel-class time of one pipeline (events over the timed steps)",
+                "classes": {q: {"ms_per_step": round(kern[q][0], 4),
+                                "frac_of_peak": round(rate(q)[0] / rate(q)[1], 5) if kern[q][0] > 0 else None}
+                            for q in kern},
                 "stages_ms": {"mask": round(tm[0], 3), "cor": round(tm[1], 3), "pca": round(tm[2], 3),
                               "sweep": round(tm[3], 3), "total": round(tm[4], 3)},
-                "pca": {"iters": int(tm[11]), "block": int(tm[12]), "resid": float(tm[13])}}
-        if bound == "mfma":
-            roof["measured_mfma_ceiling"] = FP64_MFMA_MEASURED_TFLOPS
-            roof["frac_of_measured_ceiling"] = round(achieved / FP64_MFMA_MEASURED_TFLOPS, 4)
-        if longest != dom:   # the one-pipeline critical path (latency), beside it
-            a2, p2, u2, m2 = rate(longest)
-            t2, ts2 = _pmc_traffic(longest, n0, k)
-            roof["latency_critical"] = {"kernel": longest, "bound": kern[longest][1], "achieved": round(a2, 3),
-                                        "peak": p2, "unit": u2, "frac": round(a2 / p2, 5), "avg_launch_ms": round(m2, 4),
-                                        "traffic": t2, "traffic_source": ts2}
-            if longest == "coniss":
-                roof["latency_critical"]["note"] = "one dependent merge chain per tree: latency-bound"
-                roof["latency_critical"]["merges_per_s"] = round(k * (n - 1) / (m2 * 1e-3), 1)
-        out = {"metric": "bins/sec (NxN matrix) at 1/2/4/8 GPUs; TAD boundary bit-match vs R ref",
+                "pca": {"path": "block Krylov (G never formed)" if krylov_steps else "G = Xc'Xc + subspace iteration",
+                        "krylov_steps": krylov_steps, "krylov_dim": krylov_d, "chebyshev_degrees": int(tm[11]),
+                        "block": block, "resid": float(tm[13])}}
+        if dom == "coniss":
+            roof["note"] = "one dependent merge chain per tree: latency-bound (merges/s below)"
+            roof["merges_per_s"] = round(k * (n - 1) / (avg_ms * 1e-3), 1)
+        out = {"metric": METRIC,
                "value": round(value, 2), "unit": "bins/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
                "higher_is_better": True, "scaling": "strong" if args.sharded else "weak", "vs_baseline": None,
                "dtype": "f64",
-               "data": "synthetic (SURVEY.md §8(d) Hi-C generator, seed 20261015+2" +
+               "data": "synthetic (SURVEY.md §8(d) Hi-C generator, seed 20261015+%d" % cfg +
                        ("" if args.sharded else "+1000*rank") + ")",
                "config": {"workload": (f"{_config_name(n0, args.max_pcs)}: synthetic {n0}x{n0} Hi-C matrix "
                                        + ("sharded over all GPUs" if args.sharded else "per GPU")
-                                       + f", max_pcs={args.max_pcs}"),
+                                       + f", max_pcs={args.max_pcs}, one pipeline at a time on one stream"),
                           "n0": n0, "n_good": n, "k": k, "max_pcs": args.max_pcs,
                           "parallelism": (f"one matrix over {world} GPU(s): column/row-split products, "
-                                          "RCCL all-gather" if args.sharded else f"one matrix per GPU x{world}"),
-                          "streams_per_gpu": S,
-                          "single_stream_ms_per_matrix": round(single_ms, 3) if single_ms else None},
+                                          "RCCL all-gather" if args.sharded else f"one matrix per GPU x{world}")},
                "roofline": roof}
+        if thr:
+            out["throughput"] = thr
+        # parity vs the committed oracle fixture of this workload (R-faithful SVD PCA)
+        par = {}
+        gold = os.path.join(HERE, "tests", "golden", f"c{cfg}.npz")
+        if not args.sharded and os.path.exists(gold) and n0 == {3: 7808, 2: 2000}[cfg] and args.max_pcs == 200:
+            z = np.load(gold)
+            lev = z["levels"]
+            co = z["coords"]
+            ok = (last.n_pcs == int(z["n_pcs"]) and last.optimal_n_clusters == int(z["optimal_n_clusters"])
+                  and set(last.clusters) == {str(int(q)) for q in lev}
+                  and all(np.array_equal(last.clusters[str(int(q))], co[co[:, 0] == q][:, 1:]) for q in lev)
+                  and np.array_equal(last.dendro.merge, z["merge"]))
+            a, b = last.scores, z["scores"]
+            fin = ~np.isnan(b)
+            par["golden_fixture"] = os.path.relpath(gold, HERE)
+            par["boundaries_match_golden"] = bool(ok)
+            par["ch_max_rel_err_golden"] = (float(np.max(np.abs(a[fin] - b[fin]) / np.abs(b[fin])))
+                                            if a.shape == b.shape else None)
         if not args.no_cpu_baseline and world == 1 and not args.sharded:   # CPU baseline: rank 0 at N=1 only
             sys.path.insert(0, os.path.join(HERE, "oracle"))
             import tadpole_oracle as O
             threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
             t1 = time.perf_counter()
-            ref = None
-            for _ in range(args.cpu_reps):
-                ref = O.tadpole(host, max_pcs=args.max_pcs, min_clusters=args.min_clusters, nthreads=threads)
-            cpu_s = (time.perf_counter() - t1) / args.cpu_reps
+            ref = O.tadpole(host, max_pcs=args.max_pcs, min_clusters=args.min_clusters, nthreads=threads,
+                            pca="eigh")
+            cpu_s = time.perf_counter() - t1
             out["cpu_baseline"] = {"value": round(n0 / cpu_s, 2), "unit": "bins/s", "cores": threads,
                                    "kind": "port",
-                                   "sample": f"{args.cpu_reps} full C2 pipelines (numpy LAPACK SVD + C sweep, "
-                                             f"OpenMP over PC prefixes), {cpu_s:.3f} s each"}
+                                   "sample": (f"one full {_config_name(n0, args.max_pcs)} pipeline of the CPU oracle "
+                                              f"({cpu_s:.2f} s): numpy mask + X'X correlation, LAPACK dsyevr top-"
+                                              f"{k} eigenpairs of Xc'Xc (cheaper than R's full gesdd SVD), OpenMP C "
+                                              "CONISS/CH sweep over all PC prefixes")}
             same = (last.n_pcs == ref.n_pcs and last.optimal_n_clusters == ref.optimal_n_clusters
                     and set(last.clusters) == {str(q) for q in ref.clusters}
                     and all(np.array_equal(last.clusters[str(q)], v) for q, v in ref.clusters.items()))
             a, b = last.scores, ref.scores
             fin = ~np.isnan(b)
-            rel = float(np.max(np.abs(a[fin] - b[fin]) / np.abs(b[fin]))) if a.shape == b.shape else None
-            out["parity"] = {"boundaries_match_oracle": bool(same), "n_pcs": [last.n_pcs, ref.n_pcs],
-                             "n_clusters": [last.optimal_n_clusters, ref.optimal_n_clusters],
-                             "ch_max_rel_err": rel}
+            par["boundaries_match_cpu_oracle"] = bool(same)
+            par["n_pcs"] = [last.n_pcs, ref.n_pcs]
+            par["n_clusters"] = [last.optimal_n_clusters, ref.optimal_n_clusters]
+            par["ch_max_rel_err_cpu_oracle"] = (float(np.max(np.abs(a[fin] - b[fin]) / np.abs(b[fin])))
+                                                if a.shape == b.shape else None)
+        if par:
+            out["parity"] = par
         line = json.dumps(out)
         print(line, flush=True)
         if args.json_out:

@@ -106,6 +106,11 @@ void tp_read_tsv(const char **path, const int *nrow, const int *ncol,
 void tp_mask(const double *M, const int *n0, const double *bad_frac,
              const int *flags, const int *device, int *bad, double *rowmean,
              int *n_good, int *good_idx, int *status);
+/* Same on a device-resident d_M (n0 x n0), work queued on `stream`; unless
+ * TP_FLAG_CLEAN, d_M is cleaned and symmetrised IN PLACE (R/TADpole.R:19-20). */
+void tp_mask_dev(double *d_M, const int *n0, const double *bad_frac,
+                 const int *flags, const int *device, void *stream, int *bad,
+                 double *rowmean, int *n_good, int *good_idx, int *status);
 
 /* -------------------------------------------------------------------- cor */
 /* sparse_cor(x)$cor with NaN -> 0 (R/TADpole.R:94-100,449).  X: n x n
@@ -165,11 +170,13 @@ void tp_ch(const double *P, const int *n, const int *k, const int *labels,
  *   (k x w column-major, leading dimension *k), *w
  *   *n_pcs, *n_clusters (1-based), merge[2*(n0-1)] and height[n0-1] of the
  *   final tree (first n_good-1 rows valid), boundary[n0-1] (1-based, may be
- *   NULL), timings_ms[16] (may be NULL; when given, HIP events time:
+ *   NULL), timings_ms[32] (may be NULL; when given, HIP events time:
  *   [0] mask+subset [1] cor [2] pca [3] sweep [4] total (ms), kernels
- *   [5] X'X GEMM [6] Xc'Xc GEMM [7] sum of G*Q GEMMs [8] their count
- *   [9] CONISS [10] CH, and [11] PCA iterations [12] block [13] residual
- *   [14] n_good [15] k). */
+ *   [5] X'X GEMM [6] Xc'Xc GEMM (0 on the block Krylov path) [7] sum of
+ *   the products with G (G*Q, or the Krylov steps' Xc'(Xc K_t)) [8] their
+ *   count [9] CONISS [10] CH, and [11] PCA Chebyshev degrees [12] block
+ *   [13] residual [14] n_good [15] k [16] Krylov steps (0: G formed)
+ *   [17] Krylov dimension D; [18..31] reserved, written 0). */
 void tp_pipeline(const double *M, const int *n0, const int *max_pcs,
                  const int *min_clusters, const double *bad_frac,
                  const int *flags, const int *device, const int *k_cap,

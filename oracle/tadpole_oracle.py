@@ -135,12 +135,20 @@ def sparse_cor(x: np.ndarray) -> np.ndarray:
     return cor
 
 
-def prcomp_x(c: np.ndarray, k: int) -> np.ndarray:
+def prcomp_x(c: np.ndarray, k: int, method: str = "svd") -> np.ndarray:
     """``prcomp(cor, rank.=k)$x`` (``R/TADpole.R:453``): centre columns,
-    LAPACK gesdd SVD, scores = Xc V[:, :k]."""
+    LAPACK gesdd SVD (as R's La.svd), scores = Xc V[:, :k].  ``method="eigh"``:
+    the top-k eigenvectors of Xc'Xc by LAPACK dsyevr instead (same subspaces,
+    several times cheaper than the full SVD; used only for the bench's CPU
+    baseline timing)."""
     mu = np.array([float(np.sum(c[:, j], dtype=np.longdouble) / c.shape[0])
                    for j in range(c.shape[1])])
     xc = c - mu[None, :]
+    if method == "eigh" and k < xc.shape[1]:
+        import scipy.linalg as sl
+        n = xc.shape[1]
+        _, v = sl.eigh(xc.T @ xc, subset_by_index=[n - k, n - 1], driver="evr")
+        return xc @ v[:, ::-1]
     _, _, vt = np.linalg.svd(xc, full_matrices=False)
     return xc @ vt[:k].T
 
@@ -224,6 +232,56 @@ def select_params(scores: np.ndarray):
 
 # ----------------------------------------------------------------- cutree ---
 
+def hclust_merge(mrg_a: np.ndarray, mrg_b: np.ndarray, n: int) -> np.ndarray:
+    """``chclust(...)$merge`` (rioja, ``R/TADpole.R:108,460,465``) in
+    ``stats::hclust`` encoding [ext: hclust's hcass2 conventions; rioja's own
+    row order is unverified here]: row s joins the adjacent clusters whose
+    first bins are mrg_a[s] (left) and mrg_b[s] (right), 0-based; an
+    observation is -(bin+1) and a cluster the 1-based step that formed it (a
+    merged cluster keeps the id of its left part, as hclust keeps the smaller
+    index); a singleton comes before a cluster, and of two clusters the
+    earlier step comes first; two singletons in observation order."""
+    ident = -(np.arange(n, dtype=np.int64) + 1)
+    out = np.empty((n - 1, 2), np.int64)
+    for s in range(n - 1):
+        x, y = int(ident[mrg_a[s]]), int(ident[mrg_b[s]])
+        if (x > 0 > y) or (x > 0 and y > 0 and x > y):
+            x, y = y, x
+        out[s] = (x, y)
+        ident[mrg_a[s]] = s + 1
+    return out
+
+
+def hclust_cutree(merge: np.ndarray, n: int, kk: int) -> np.ndarray:
+    """``stats::cutree(tree, k)`` on an hclust merge matrix, from its
+    definition: apply the first n-k merges (union-find), then number the
+    groups 1..k in order of their first observation.  Independent of the
+    constrained-tree shortcut in ``cutree_labels``."""
+    parent = np.arange(n)
+
+    def find(x):
+        while parent[x] != x:
+            parent[x] = parent[parent[x]]
+            x = parent[x]
+        return x
+    rep = {}
+    for s in range(n - kk):
+        ends = []
+        for v in merge[s]:
+            ends.append(-v - 1 if v < 0 else rep[v])
+        ra, rb = find(ends[0]), find(ends[1])
+        parent[max(ra, rb)] = min(ra, rb)
+        rep[s + 1] = min(ra, rb)
+    roots = np.array([find(x) for x in range(n)])
+    lab = np.zeros(n, np.int64)
+    seen = {}
+    for x in range(n):
+        if roots[x] not in seen:
+            seen[roots[x]] = len(seen) + 1
+        lab[x] = seen[roots[x]]
+    return lab
+
+
 def cutree_labels(mrg_b: np.ndarray, n: int, kk: int) -> np.ndarray:
     """``stats::cutree(clust, k)`` for a constrained tree: the boundaries of the
     last kk-1 merges, labels 1..kk left to right."""
@@ -284,36 +342,140 @@ class OracleResult:
     sweep: Sweep = None
     merge_b: np.ndarray = None
     height: np.ndarray = None
+    merge: np.ndarray = None
+    fixed_opt: np.ndarray = None      # fixed cluster vector at optimal_n_clusters (arm merge input)
 
 
-def tadpole(mat: np.ndarray, max_pcs: int = 200, min_clusters: int = 2,
-            bad_frac: float = 0.01, pcs: np.ndarray | None = None,
-            bstick: str = "dd", nthreads: int = 0) -> OracleResult:
-    """``TADpole(..., centromere_search=FALSE)`` body, ``R/TADpole.R:344-349,
-    444-497``, from an in-memory matrix (``load_mat`` minus the plots)."""
-    m = clean_symmetrize(mat)
-    bad, _, _ = bad_mask(m, bad_frac)
-    good = np.flatnonzero(~bad)
-    x = m[np.ix_(good, good)]
+def _core(x: np.ndarray, good_names1: np.ndarray, bad_idx1: np.ndarray, max_pcs: int,
+          min_clusters: int, bstick: str, nthreads: int, pcs=None, pca: str = "svd") -> OracleResult:
+    """``R/TADpole.R:444-497`` (and the per-arm body ``:359-432``) on a masked
+    matrix x whose rows carry the 1-based names ``good_names1``."""
     c = None
     if pcs is None:
         c = sparse_cor(x)
         k = min(max_pcs, x.shape[0])
-        pcs = prcomp_x(c, k)
+        pcs = prcomp_x(c, k, pca)
     sw = sweep(pcs, min_clusters, bstick=bstick, nthreads=nthreads)
     if sw.status == 1:
         raise ValueError("invalid 'times' argument (no broken-stick level)")
     n_pcs, n_clusters = select_params(sw.scores)
     n = x.shape[0]
     mb = sw.mrg_b[n_pcs - 1]
-    res = OracleResult(n_pcs, n_clusters, sw.scores, bad=bad, good_idx1=good + 1,
-                       pcs=pcs, cor=c, sweep=sw, merge_b=mb, height=sw.height[n_pcs - 1])
-    bad_idx1 = np.flatnonzero(bad) + 1
+    res = OracleResult(n_pcs, n_clusters, sw.scores, good_idx1=good_names1,
+                       pcs=pcs, cor=c, sweep=sw, merge_b=mb, height=sw.height[n_pcs - 1],
+                       merge=hclust_merge(sw.mrg_a[n_pcs - 1], mb, n))
     row = sw.scores[n_pcs - 1]
     for kk in np.flatnonzero(~np.isnan(row)) + 1:
         lab = cutree_labels(mb, n, int(kk))
-        res.clusters[int(kk)] = coords_for(lab, good + 1, bad_idx1)
+        res.clusters[int(kk)] = coords_for(lab, good_names1, bad_idx1)
+    lab = cutree_labels(mb, n, n_clusters)
+    res.fixed_opt = fixed_vector(lab, good_names1, bad_idx1)
     return res
+
+
+def tadpole(mat: np.ndarray, max_pcs: int = 200, min_clusters: int = 2,
+            bad_frac: float = 0.01, pcs: np.ndarray | None = None,
+            bstick: str = "dd", nthreads: int = 0, pca: str = "svd") -> OracleResult:
+    """``TADpole(..., centromere_search=FALSE)`` body, ``R/TADpole.R:344-349,
+    444-497``, from an in-memory matrix (``load_mat`` minus the plots).
+    ``pca``: "svd" (R's full SVD) or "eigh" (see ``prcomp_x``)."""
+    m = clean_symmetrize(mat)
+    bad, _, _ = bad_mask(m, bad_frac)
+    good = np.flatnonzero(~bad)
+    x = m[np.ix_(good, good)]
+    res = _core(x, good + 1, np.flatnonzero(bad) + 1, max_pcs, min_clusters, bstick, nthreads, pcs, pca)
+    res.bad = bad
+    return res
+
+
+def fixed_vector(labels_good, names1, bad_idx1) -> np.ndarray:
+    """``R/TADpole.R:413-432``: c(good, bad = 0) ordered by numeric name,
+    fix_values, inverse.rle (duplicate names kept, stable order)."""
+    names = np.concatenate([np.asarray(names1), np.asarray(bad_idx1)]).astype(np.float64)
+    vals = np.concatenate([np.asarray(labels_good, np.float64), np.zeros(len(bad_idx1))])
+    order = np.argsort(names, kind="stable")
+    lens, v = fix_values(*rle(vals[order]))
+    return np.repeat(v, lens)
+
+
+def _r_drop(n: int, neg) -> np.ndarray:
+    """Positions 0..n-1 kept by R's ``x[-neg, ]`` for numeric ``neg`` (R
+    negativeSubscript [ext]: in-range values drop that position, out-of-range
+    ones are ignored)."""
+    neg = np.asarray(neg, np.int64)
+    drop = neg[(neg >= 1) & (neg <= n)] - 1
+    return np.setdiff1d(np.arange(n), drop)
+
+
+def load_mat_arms(mat: np.ndarray, bad_frac: float = 0.01, fixed: bool = False):
+    """``load_mat(..., centromere_search=TRUE)`` (``R/TADpole.R:15-92``)
+    without plots.  Returns ``("matrix", x, names1, bad_idx1)`` when there is no
+    bad bin or the longest bad run touches an end (``:66-70``), else
+    ``("arms", {"p": (x, names1, bad_idx1), "q": ...}, centromere1)``.
+
+    Bug-compatible by default: the q-arm bad bins are removed with their
+    ORIGINAL indices as positions in the arm-local matrix (``:78-80``), so an
+    index inside the arm's length drops the wrong bin and one beyond it is
+    ignored.  ``fixed=True`` removes them at their arm-local positions."""
+    m = clean_symmetrize(mat)
+    n0 = m.shape[0]
+    bad, _, _ = bad_mask(m, bad_frac)
+    idx = np.flatnonzero(bad) + 1
+    if idx.size == 0:
+        return ("matrix", m, np.arange(1, n0 + 1), idx)
+    cut = np.flatnonzero(np.diff(idx) > 1) + 1
+    runs = np.split(idx, cut)
+    longest = runs[int(np.argmax([len(r) for r in runs]))]   # which.max: first max
+    cs, ce = int(longest[0]), int(longest[-1])
+    if cs == 1 or ce == n0:
+        good = np.flatnonzero(~bad)
+        return ("matrix", m[np.ix_(good, good)], good + 1, idx)
+    arms = {}
+    for arm, lo, hi, bad_arm in (("p", 1, cs - 1, idx[idx < cs]), ("q", ce + 1, n0, idx[idx > ce])):
+        names = np.arange(lo, hi + 1)
+        sub = np.ascontiguousarray(m[lo - 1:hi, lo - 1:hi])
+        if bad_arm.size:
+            keep = _r_drop(len(names), (bad_arm - lo + 1) if fixed else bad_arm)
+            sub = sub[np.ix_(keep, keep)]
+            names = names[keep]
+        arms[arm] = (sub, names, bad_arm)
+    return ("arms", arms, np.arange(cs, ce + 1))
+
+
+@dataclass
+class ArmsResult:
+    p: OracleResult
+    q: OracleResult
+    merging_arms: np.ndarray
+    centromere: np.ndarray
+
+
+def tadpole_arms(mat: np.ndarray, max_pcs: int = 200, min_clusters: int = 2,
+                 bad_frac: float = 0.01, fixed: bool = False, nthreads: int = 0):
+    """``TADpole(..., centromere_search=TRUE)`` (``R/TADpole.R:351-442``).
+    Returns an ``ArmsResult``; when ``load_mat`` returned a plain matrix R
+    fails at ``mat$centromer`` (``:356``): bug-compatible mode raises, fixed
+    mode runs the single-matrix path instead."""
+    kind, *rest = load_mat_arms(mat, bad_frac, fixed)
+    if kind == "matrix":
+        if not fixed:
+            raise TypeError("$ operator is invalid for atomic vectors")
+        return tadpole(mat, max_pcs, min_clusters, bad_frac, nthreads=nthreads)
+    arms, cen = rest
+    out = {}
+    parts = []
+    for arm in ("p", "q"):
+        x, names, bad_arm = arms[arm]
+        r = _core(x, names, bad_arm, max_pcs, min_clusters, "dd", nthreads)
+        out[arm] = r
+        parts += [r.fixed_opt, np.zeros(len(cen))]
+    allv = np.concatenate(parts)[:-len(cen)]
+    lens, v = rle(allv)
+    eb = np.cumsum(lens)
+    start = np.concatenate([[1], eb[:-1] + 1])
+    keep = v != 0
+    coords = np.stack([start[keep], eb[keep]], axis=1).astype(np.int64)
+    return ArmsResult(out["p"], out["q"], coords, cen)
 
 
 # ------------------------------------------------------------------ diffT ---

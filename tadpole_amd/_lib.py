@@ -23,7 +23,7 @@ TP_FLAG_SHARDED = 8
 #: every symbol include/tadpole_hip.h declares
 EXPORTS = (
     "tp_version", "tp_device_count", "tp_shutdown", "tp_last_error", "tp_last_error_r",
-    "tp_mask", "tp_cor", "tp_pca", "tp_sweep", "tp_coniss", "tp_dist", "tp_ch",
+    "tp_mask", "tp_mask_dev", "tp_cor", "tp_pca", "tp_sweep", "tp_coniss", "tp_dist", "tp_ch",
     "tp_pipeline", "tp_pipeline_dev", "tp_sweep_dev", "tp_tsv_dims", "tp_read_tsv",
     "tp_comm_unique_id", "tp_comm_init", "tp_comm_destroy", "tp_set_virtual_shards", "tp_shard_plan",
 )

@@ -12,8 +12,10 @@ out of scope: they draw, they do not compute.
 from __future__ import annotations
 
 import ctypes
+import logging
 import os
 import struct
+import sys
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence
 
@@ -21,6 +23,8 @@ import numpy as np
 
 from . import _lib
 from ._lib import TadpoleError, cdbl, cint, dp, ip
+
+_log = logging.getLogger("tadpole_amd")
 
 NA_BITS = 0x7FF00000000007A2
 NA_REAL = struct.unpack("<d", struct.pack("<Q", NA_BITS))[0]
@@ -130,12 +134,19 @@ def _layout(m: np.ndarray):
 
 
 def clean_symmetrize(m: np.ndarray) -> np.ndarray:
-    """R/TADpole.R:19-20 on the host (used for the arm split and for load_mat's
-    return value; the pipeline does the same on the device)."""
+    """R/TADpole.R:19-20 on the host (load_mat's return value): NaN -> 0, then
+    forceSymmetric(uplo='U').  Row blocks, so no N^2 index arrays (the
+    pipeline does the same on the device)."""
     out = np.array(m, dtype=np.float64, copy=True)
-    out[np.isnan(out)] = 0.0
-    iu = np.triu_indices(out.shape[0], 1)
-    out.T[iu] = out[iu]
+    np.nan_to_num(out, copy=False, nan=0.0, posinf=np.inf, neginf=-np.inf)
+    n = out.shape[0]
+    blk = max(1, min(n, (1 << 22) // max(n, 1)))
+    for r0 in range(0, n, blk):
+        r1 = min(n, r0 + blk)
+        out[r0:r1, :r0] = out[:r0, r0:r1].T
+        sub = out[r0:r1, r0:r1]
+        il = np.tril_indices(r1 - r0, -1)
+        sub[il] = sub.T[il]
     return out
 
 
@@ -181,37 +192,65 @@ def _runs(idx: np.ndarray) -> List[np.ndarray]:
     return np.split(idx, cut)
 
 
+def _message(text: str, verbose: bool) -> None:
+    """R ``message()`` (R/TADpole.R:55-56,65,67,136-137,358): logged on the
+    ``tadpole_amd`` logger, and written to stderr when ``verbose``."""
+    _log.info(text)
+    if verbose:
+        print(text, file=sys.stderr, flush=True)
+
+
+def _arm_plan(bad: np.ndarray, fixed: bool = False, verbose: bool = False):
+    """The centromere split of load_mat (R/TADpole.R:58-85) as index sets.
+
+    Returns None when R returns a plain matrix (no bad bin, R/TADpole.R:87-90,
+    or the longest bad run touches an end, :66-70), else
+    ``{"p": (names1, bad1), "q": (names1, bad1), "centromere": idx1}`` where
+    names1 are the 1-based original bins each arm keeps.  Bug-compatible by
+    default: the q-arm bad bins are removed with their ORIGINAL indices used
+    as arm-local positions (R/TADpole.R:78-80; R ignores out-of-range negative
+    subscripts and drops in-range ones, so the wrong bins go or none do);
+    ``fixed=True`` removes them at their arm-local positions."""
+    idx = np.flatnonzero(bad) + 1
+    n0 = len(bad)
+    if idx.size == 0:
+        return None
+    runs = _runs(idx)
+    longest = runs[int(np.argmax([len(r) for r in runs]))]    # which.max: first max
+    cs, ce = int(longest[0]), int(longest[-1])
+    _message(f"centromere position: {cs} {ce}", verbose)
+    if cs == 1 or ce == n0:
+        _message("longest stretch of bad rows/columns at the ends, not splitting the matrix.", verbose)
+        return None
+    names_p, names_q = np.arange(1, cs), np.arange(ce + 1, n0 + 1)
+    bad_p, bad_q = idx[idx < cs], idx[idx > ce]
+    keep_p = _r_negative_keep(len(names_p), bad_p)
+    keep_q = _r_negative_keep(len(names_q), bad_q - ce if fixed else bad_q)
+    return {"p": (names_p[keep_p], bad_p), "q": (names_q[keep_q], bad_q), "centromere": np.arange(cs, ce + 1)}
+
+
 def load_mat(mat_file, chr=None, start=None, end=None, resol=None, bad_frac: float = 0.01,
-             centromere_search: bool = False, device: int = 0):
+             centromere_search: bool = False, device: int = 0, fixed_centromere: bool = False,
+             verbose: bool = False):
     """``load_mat`` (R/TADpole.R:15-92) without its plots.
 
     Returns the masked matrix (``Mat`` with ``bad_columns``) or, with
     ``centromere_search``, ``{"p": Mat, "q": Mat, "centromere": ndarray}``,
-    bug-compatible with the reference (q-arm bad columns removed with original
-    indices, R/TADpole.R:78-80; a plain matrix when the longest bad run touches
-    an end, R/TADpole.R:66-70)."""
+    bug-compatible with the reference unless ``fixed_centromere`` (see
+    ``_arm_plan``); a plain matrix when the longest bad run touches an end
+    (R/TADpole.R:66-70)."""
     raw = _as_matrix(mat_file)
     bad, _, good = mask(raw, bad_frac, device)
-    m = clean_symmetrize(raw)
-    n0 = m.shape[0]
     bad_idx = np.flatnonzero(bad) + 1
-    if bad.any() and centromere_search:
-        runs = _runs(bad_idx)
-        longest = runs[int(np.argmax([len(r) for r in runs]))]
-        cs, ce = int(longest[0]), int(longest[-1])
-        if cs == 1 or ce == n0:
-            return Mat(m[np.ix_(good - 1, good - 1)], bad_idx, good)
-        idx_p = np.arange(1, cs)
-        idx_q = np.arange(ce + 1, n0 + 1)
-        bad_p = bad_idx[bad_idx < cs]
-        bad_q = bad_idx[bad_idx > ce]
-        keep_p = _r_negative_keep(len(idx_p), bad_p)
-        keep_q = _r_negative_keep(len(idx_q), bad_q)
-        sel_p, sel_q = idx_p[keep_p] - 1, idx_q[keep_q] - 1
-        return {"p": Mat(m[np.ix_(sel_p, sel_p)], bad_p, sel_p + 1),
-                "q": Mat(m[np.ix_(sel_q, sel_q)], bad_q, sel_q + 1),
-                "centromere": np.arange(cs, ce + 1)}
-    return Mat(m[np.ix_(good - 1, good - 1)], bad_idx, good)
+    _message(f"{len(bad_idx)} bad columns found at position(s):", verbose)
+    _message(" ".join(str(int(b)) for b in bad_idx), verbose)
+    plan = _arm_plan(bad, fixed_centromere, verbose) if (bad.any() and centromere_search) else None
+    if plan is None:
+        return Mat(clean_symmetrize(raw[np.ix_(good - 1, good - 1)]), bad_idx, good)
+    out = {arm: Mat(clean_symmetrize(raw[np.ix_(plan[arm][0] - 1, plan[arm][0] - 1)]), plan[arm][1], plan[arm][0])
+           for arm in ("p", "q")}
+    out["centromere"] = plan["centromere"]
+    return out
 
 
 def _r_negative_keep(n: int, neg: np.ndarray) -> np.ndarray:
@@ -226,14 +265,31 @@ def _r_negative_keep(n: int, neg: np.ndarray) -> np.ndarray:
 
 # ---------------------------------------------------------------- pipeline
 
-def _pipeline(m: np.ndarray, max_pcs: int, min_clusters: int, bad_frac: float, flags: int,
+def _is_device(m) -> bool:
+    """A torch tensor resident on a GPU (the matrix is already in HBM)."""
+    return type(m).__module__.startswith("torch") and getattr(m, "is_cuda", False)
+
+
+def _pipeline(m, max_pcs: int, min_clusters: int, bad_frac: float, flags: int,
               device: int, stream=None):
-    """One tp_pipeline call.  ``stream`` (a torch.cuda.Stream): the matrix is
-    staged on the device and the pipeline queued on that stream with its own
-    library context, so several pipelines can run concurrently on one GPU."""
+    """One tp_pipeline call.  ``m``: a host array, or a square float64 torch
+    tensor on the GPU (tp_pipeline_dev on it: no host staging; unless
+    TP_FLAG_CLEAN it is cleaned in place).  ``stream`` (a torch.cuda.Stream):
+    the pipeline is queued on that stream with its own library context, so
+    several pipelines can run concurrently on one GPU."""
     L = _lib.load()
-    m, lay = _layout(m)
-    flags |= lay
+    dev_in = _is_device(m)
+    if dev_in:
+        if m.dim() != 2 or m.shape[0] != m.shape[1]:
+            raise ValueError("the interaction matrix must be square")
+        import torch
+        if m.dtype != torch.float64 or not m.is_contiguous():
+            m = m.to(torch.float64).contiguous()
+        flags |= _lib.TP_FLAG_ROW_MAJOR
+        device = m.device.index if m.device.index is not None else device
+    else:
+        m, lay = _layout(m)
+        flags |= lay
     n0 = m.shape[0]
     k_cap = max(1, min(max_pcs, n0))
     w_cap = max(1, n0)
@@ -244,10 +300,10 @@ def _pipeline(m: np.ndarray, max_pcs: int, min_clusters: int, bad_frac: float, f
     merge = np.zeros(2 * max(1, n0 - 1), np.int32)
     height = np.zeros(max(1, n0 - 1))
     boundary = np.zeros(max(1, n0 - 1), np.int32)
-    timings = np.zeros(16)
+    timings = np.zeros(32)
     out = [cint(0) for _ in range(6)]
     n_good, k, w, n_pcs, n_clusters, st = out
-    if stream is None:
+    if stream is None and not dev_in:
         L.tp_pipeline(dp(m), ctypes.byref(cint(n0)), ctypes.byref(cint(max_pcs)), ctypes.byref(cint(min_clusters)),
                       ctypes.byref(cdbl(bad_frac)), ctypes.byref(cint(flags)), ctypes.byref(cint(device)),
                       ctypes.byref(cint(k_cap)), ctypes.byref(cint(w_cap)), ip(bad), ctypes.byref(n_good),
@@ -256,10 +312,21 @@ def _pipeline(m: np.ndarray, max_pcs: int, min_clusters: int, bad_frac: float, f
                       ctypes.byref(st))
     else:
         import torch
-        host = m if m.flags["C_CONTIGUOUS"] else np.ascontiguousarray(m.T)   # same buffer order as `lay`
-        with torch.cuda.stream(stream):
-            dm = torch.from_numpy(host).to(f"cuda:{device}", non_blocking=False)
-        stream.synchronize()
+        if stream is None:
+            stream = torch.cuda.current_stream(device)
+        if dev_in:
+            dm = m
+            # the library's own stream (handle 0 selects it) does not order
+            # with torch's default stream: finish the producer of m first
+            if stream.cuda_stream == 0:
+                torch.cuda.current_stream(device).synchronize()
+            else:
+                stream.wait_stream(torch.cuda.current_stream(device))
+        else:
+            host = m if m.flags["C_CONTIGUOUS"] else np.ascontiguousarray(m.T)   # same buffer order as `lay`
+            with torch.cuda.stream(stream):
+                dm = torch.from_numpy(host).to(f"cuda:{device}", non_blocking=False)
+            stream.synchronize()
         L.tp_pipeline_dev(ctypes.c_void_p(dm.data_ptr()), ctypes.byref(cint(n0)), ctypes.byref(cint(max_pcs)),
                           ctypes.byref(cint(min_clusters)), ctypes.byref(cdbl(bad_frac)), ctypes.byref(cint(flags)),
                           ctypes.byref(cint(device)), ctypes.c_void_p(stream.cuda_stream),
@@ -276,6 +343,33 @@ def _pipeline(m: np.ndarray, max_pcs: int, min_clusters: int, bad_frac: float, f
                 scores=sc, n_pcs=n_pcs.value, n_clusters=n_clusters.value,
                 merge=merge[:2 * (n - 1)].reshape(2, n - 1).T.copy(), height=height[:n - 1].copy(),
                 boundary=boundary[:n - 1].copy(), timings=timings)
+
+
+def mask_dev(dm, bad_frac: float = 0.01, stream=None):
+    """tp_mask_dev on a GPU-resident square float64 tensor (cleaned and
+    symmetrised in place, R/TADpole.R:19-20).  Returns (bad bool[N0],
+    rowMeans, good 1-based indices)."""
+    import torch
+    L = _lib.load()
+    device = dm.device.index if dm.device.index is not None else 0
+    if dm.dtype != torch.float64 or not dm.is_contiguous():
+        raise ValueError("mask_dev needs a contiguous float64 tensor")
+    stream = stream or torch.cuda.current_stream(device)
+    if stream.cuda_stream == 0:       # see _pipeline: order with torch's default stream
+        torch.cuda.current_stream(device).synchronize()
+    else:
+        stream.wait_stream(torch.cuda.current_stream(device))
+    n0 = dm.shape[0]
+    bad = np.zeros(n0, np.int32)
+    rm = np.zeros(n0)
+    good = np.zeros(n0, np.int32)
+    ng, st = cint(0), cint(0)
+    L.tp_mask_dev(ctypes.c_void_p(dm.data_ptr()), ctypes.byref(cint(n0)), ctypes.byref(cdbl(bad_frac)),
+                  ctypes.byref(cint(_lib.TP_FLAG_ROW_MAJOR)), ctypes.byref(cint(device)),
+                  ctypes.c_void_p(stream.cuda_stream), ip(bad), dp(rm), ctypes.byref(ng), ip(good),
+                  ctypes.byref(st))
+    _lib.check(st)
+    return bad.astype(bool), rm, good[:ng.value].copy()
 
 
 def rle(x):
@@ -336,7 +430,7 @@ def _level_coords(boundary, n, kk, pos):
     return out
 
 
-def _assemble(res, bad_idx1, arm_mode: bool = False) -> Tadpole:
+def _assemble(res, bad_idx1) -> Tadpole:
     n = len(res["good"])
     good1 = np.asarray(res["good"])
     dendro = Chclust(merge=res["merge"], height=res["height"], order=np.arange(1, n + 1),
@@ -378,58 +472,83 @@ def _assemble_rle(t, dendro, levels, good1, bad_idx1) -> Tadpole:
 
 def TADpole(mat_file, max_pcs: int = 200, min_clusters: int = 2, bad_frac: float = 0.01,
             chr=None, start=None, end=None, resol=None, centromere_search: bool = False,
-            device: int = 0, sharded: bool = False, stream=None) -> Tadpole:
+            device: int = 0, sharded: bool = False, stream=None, fixed_centromere: bool = False,
+            verbose: bool = False) -> Tadpole:
     """``TADpole()`` (R/TADpole.R:344-501).  ``mat_file`` may be a path to a
     tab-separated matrix or an in-memory square array.  ``sharded``: split this
     matrix over the ranks of the communicator made by
     ``tadpole_amd.multi.init_comm`` (every rank calls with the same matrix).
-    ``stream``: a torch.cuda.Stream to run on (concurrent pipelines per GPU)."""
-    raw = _as_matrix(mat_file)
+    ``stream``: a torch.cuda.Stream to run on (concurrent pipelines per GPU).
+    ``fixed_centromere``: the centromere split without the reference's q-arm
+    index bug (R/TADpole.R:78-80), and the single-matrix path where R would
+    fail on a plain matrix (:66-70,356).  ``verbose``: R's message() lines on
+    stderr (always logged on the ``tadpole_amd`` logger)."""
+    raw = mat_file if _is_device(mat_file) else _as_matrix(mat_file)
     shard_flag = _lib.TP_FLAG_SHARDED if sharded else 0
     if not centromere_search:
         res = _pipeline(raw, max_pcs, min_clusters, bad_frac, shard_flag, device, stream)
         bad_idx1 = np.flatnonzero(res["bad"]) + 1
-        return _assemble(res, bad_idx1)
-    mat = load_mat(raw, bad_frac=bad_frac, centromere_search=True, device=device)
-    if not isinstance(mat, dict):
-        # R/TADpole.R:356: `mat$centromer` on a matrix is an error in R
-        raise TypeError("$ operator is invalid for atomic vectors (no centromere split: the longest "
-                        "bad run touches an end of the matrix; R/TADpole.R:66-70,356)")
-    return _tadpole_arms(mat, max_pcs, min_clusters, device, shard_flag, stream)
+        _message(f"{len(bad_idx1)} bad columns found at position(s):", verbose)
+        _message(" ".join(str(int(b)) for b in bad_idx1), verbose)
+        t = _assemble(res, bad_idx1)
+        _message(f"Optimal number of PCs: {t.n_pcs}", verbose)
+        _message(f"Optimal number of clusters: {t.optimal_n_clusters}", verbose)
+        return t
+    if _is_device(raw):
+        import torch
+        raw = raw.to(torch.float64).contiguous()
+        bad, _, _ = mask_dev(raw, bad_frac, stream)   # raw is clean and symmetric from here on
+    else:
+        bad, _, _ = mask(raw, bad_frac, device)
+    bad_idx1 = np.flatnonzero(bad) + 1
+    _message(f"{len(bad_idx1)} bad columns found at position(s):", verbose)
+    _message(" ".join(str(int(b)) for b in bad_idx1), verbose)
+    plan = _arm_plan(bad, fixed_centromere, verbose) if bad.any() else None
+    if plan is None:
+        if not fixed_centromere:
+            # R/TADpole.R:356: `mat$centromer` on a matrix is an error in R
+            raise TypeError("$ operator is invalid for atomic vectors (no centromere split: no bad bin, or the "
+                            "longest bad run touches an end of the matrix; R/TADpole.R:66-70,87-90,356)")
+        return TADpole(raw, max_pcs, min_clusters, bad_frac, device=device, sharded=sharded, stream=stream,
+                       verbose=verbose)
+    return _tadpole_arms(raw, plan, max_pcs, min_clusters, device, shard_flag, stream, verbose)
 
 
-def _tadpole_arms(mat, max_pcs, min_clusters, device, shard_flag: int = 0, stream=None) -> Tadpole:
-    """R/TADpole.R:351-442 (arm loop and arm merge), bug-compatible."""
+def _tadpole_arms(raw, plan, max_pcs, min_clusters, device, shard_flag: int = 0, stream=None,
+                  verbose: bool = False) -> Tadpole:
+    """R/TADpole.R:351-442 (arm loop and arm merge).  Each arm is the raw
+    principal submatrix of its kept bins; NA->0 and forceSymmetric(uplo='U')
+    commute with taking it, so the device cleans it (TP_FLAG_NO_MASK: the arm
+    matrices are correlated as given, R/TADpole.R:362)."""
     tad = Tadpole()
-    centromer = mat["centromere"]
+    centromer = plan["centromere"]
     fixed_arms: List[np.ndarray] = []
     for arm in ("p", "q"):
-        am = mat[arm]
-        bad_cols = am.bad_columns
-        res = _pipeline(np.asarray(am), max_pcs, min_clusters, 0.0,
-                        _lib.TP_FLAG_CLEAN | _lib.TP_FLAG_NO_MASK | shard_flag, device, stream)
-        names = am.names.astype(np.int32)   # rownames inherited from the full matrix
-        res["good"] = names
-        sub = _assemble_arm(res, bad_cols)
-        setattr(tad, arm, sub)
-        lab = sub.dendro.cutree(sub.optimal_n_clusters)
-        if bad_cols is not None and len(bad_cols):
-            fixed, _ = _fixed_clusters(lab, names, np.asarray(bad_cols))
+        _message(f"Processing arm {arm}", verbose)
+        names, bad_cols = plan[arm]
+        if _is_device(raw):   # already cleaned by tp_mask_dev
+            import torch
+            sel = torch.as_tensor(names - 1, device=raw.device)
+            sub = raw.index_select(0, sel).index_select(1, sel)
+            clean = _lib.TP_FLAG_CLEAN
         else:
-            order = np.argsort(names.astype(np.float64), kind="stable")
-            lens, v = fix_values(*rle(np.asarray(lab, np.float64)[order]))
-            fixed = np.repeat(v, lens)
+            sub = raw[np.ix_(names - 1, names - 1)]
+            clean = 0
+        res = _pipeline(sub, max_pcs, min_clusters, 0.0, _lib.TP_FLAG_NO_MASK | clean | shard_flag, device, stream)
+        del sub
+        res["good"] = names.astype(np.int32)   # rownames inherited from the full matrix
+        sub_t = _assemble(res, np.asarray(bad_cols))
+        _message(f"Optimal number of PCs: {sub_t.n_pcs}", verbose)
+        _message(f"Optimal number of clusters: {sub_t.optimal_n_clusters}", verbose)
+        setattr(tad, arm, sub_t)
+        lab = sub_t.dendro.cutree(sub_t.optimal_n_clusters)
+        fixed, _ = _fixed_clusters(lab, names, np.asarray(bad_cols))
         fixed_arms.append(fixed)
         fixed_arms.append(np.zeros(len(centromer)))
     allv = np.concatenate(fixed_arms)
     allv = allv[: len(allv) - len(centromer)]
     tad.merging_arms = _coords(allv)
     return tad
-
-
-def _assemble_arm(res, bad_cols) -> Tadpole:
-    t = _assemble(res, np.asarray(bad_cols) if bad_cols is not None and len(bad_cols) else None)
-    return t
 
 
 # ------------------------------------------------------------------ diffT

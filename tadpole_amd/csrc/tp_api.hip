@@ -206,15 +206,21 @@ static void select_params(const double *scores, int k, int w, int *n_pcs, int *n
     *n_clusters = bj + 1;
 }
 
-// hclust merge encoding of a constrained tree: row s = (left id, right id),
-// singleton = -(bin), cluster formed at step t = t.  Column-major (n-1) x 2.
+// rioja chclust `merge` (R/TADpole.R:465, consumed by cutree / ggdendro at
+// :231-232) in stats::hclust encoding: row s joins the clusters starting at
+// mrg_a[s] (left) and mrg_b[s] (right); an observation is -(bin + 1), a cluster
+// the 1-based step that made it (a merged cluster keeps its left part's id, as
+// hclust keeps the smaller index).  hcass2's row order: a singleton before a
+// cluster, the earlier step first of two clusters, two singletons left to right.
 static void encode_merge(const int *mrg_a, const int *mrg_b, int n, int *merge) {
     std::vector<int> id(n);
     for (int p = 0; p < n; ++p) id[p] = -(p + 1);
     for (int s = 0; s < n - 1; ++s) {
-        int a = mrg_a[s], b = mrg_b[s];
-        merge[s] = id[a];
-        merge[s + (n - 1)] = id[b];
+        const int a = mrg_a[s], b = mrg_b[s];
+        int x = id[a], y = id[b];
+        if ((x > 0 && y < 0) || (x > 0 && y > 0 && x > y)) std::swap(x, y);
+        merge[s] = x;
+        merge[s + (n - 1)] = y;
         id[a] = s + 1;
     }
 }
@@ -481,6 +487,9 @@ static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_cl
         timings[13] = ps.resid;
         timings[14] = n;
         timings[15] = k;
+        timings[16] = ps.krylov_steps;
+        timings[17] = ps.krylov_dim;
+        for (int q = 18; q < 32; ++q) timings[q] = 0.0;
     }
     c.prof = false;
     return o;
@@ -564,34 +573,46 @@ void tp_last_error_r(char **buf, int *len) {
     if (buf && buf[0] && len && *len > 0) snprintf(buf[0], (size_t)*len, "%s", g_err.c_str());
 }
 
+static void mask_core(Ctx &c, double *dM, int N0, double bf, int fl, int *bad, double *rowmean, int *n_good,
+                      int *good_idx) {
+    hipStream_t s = c.cur;
+    if (!(fl & TP_FLAG_CLEAN)) launch_clean_symmetrize(dM, N0, !(fl & TP_FLAG_ROW_MAJOR), s);
+    double *rm = c.buf[S_ROWMEAN].as<double>(N0);
+    double *dg = c.buf[S_DIAG].as<double>(N0);
+    int *d_bad = c.buf[S_BAD].as<int>(N0);
+    int *d_good = c.buf[S_GOOD].as<int>(N0);
+    int *d_ng = (int *)c.buf[S_NGOOD].as<char>(64);
+    launch_rowmean_diag(dM, N0, rm, dg, s);
+    launch_mask_select(rm, dg, N0, bf, 1.0 + (double)(N0 - 1) * bf, d_bad, d_good, d_ng, s);
+    int ng = 0;
+    TP_HIP(hipMemcpyAsync(&ng, d_ng, 4, hipMemcpyDeviceToHost, s));
+    if (bad) TP_HIP(hipMemcpyAsync(bad, d_bad, N0 * 4, hipMemcpyDeviceToHost, s));
+    if (rowmean) TP_HIP(hipMemcpyAsync(rowmean, rm, N0 * 8, hipMemcpyDeviceToHost, s));
+    if (good_idx) TP_HIP(hipMemcpyAsync(good_idx, d_good, N0 * 4, hipMemcpyDeviceToHost, s));
+    TP_HIP(hipStreamSynchronize(s));
+    if (n_good) *n_good = ng;
+    if (good_idx)
+        for (int q = 0; q < ng; ++q) good_idx[q] += 1;
+}
+
 void tp_mask(const double *M, const int *n0, const double *bad_frac, const int *flags, const int *device, int *bad,
              double *rowmean, int *n_good, int *good_idx, int *status) {
     guarded(status, [&] {
         if (!M || !n0 || *n0 < 1) fail(TP_ERR_ARG, "bad matrix");
         Ctx &c = ctx_for(dev_of(device));
-        hipStream_t s = c.cur;
         const int N0 = *n0;
-        const int fl = flags ? *flags : 0;
         double *dM = c.buf[S_M].as<double>((size_t)N0 * N0);
-        TP_HIP(hipMemcpyAsync(dM, M, (size_t)N0 * N0 * 8, hipMemcpyHostToDevice, s));
-        if (!(fl & TP_FLAG_CLEAN)) launch_clean_symmetrize(dM, N0, !(fl & TP_FLAG_ROW_MAJOR), s);
-        double *rm = c.buf[S_ROWMEAN].as<double>(N0);
-        double *dg = c.buf[S_DIAG].as<double>(N0);
-        int *d_bad = c.buf[S_BAD].as<int>(N0);
-        int *d_good = c.buf[S_GOOD].as<int>(N0);
-        int *d_ng = (int *)c.buf[S_NGOOD].as<char>(64);
-        launch_rowmean_diag(dM, N0, rm, dg, s);
-        const double bf = bad_frac ? *bad_frac : 0.01;
-        launch_mask_select(rm, dg, N0, bf, 1.0 + (double)(N0 - 1) * bf, d_bad, d_good, d_ng, s);
-        int ng = 0;
-        TP_HIP(hipMemcpyAsync(&ng, d_ng, 4, hipMemcpyDeviceToHost, s));
-        if (bad) TP_HIP(hipMemcpyAsync(bad, d_bad, N0 * 4, hipMemcpyDeviceToHost, s));
-        if (rowmean) TP_HIP(hipMemcpyAsync(rowmean, rm, N0 * 8, hipMemcpyDeviceToHost, s));
-        if (good_idx) TP_HIP(hipMemcpyAsync(good_idx, d_good, N0 * 4, hipMemcpyDeviceToHost, s));
-        TP_HIP(hipStreamSynchronize(s));
-        if (n_good) *n_good = ng;
-        if (good_idx)
-            for (int q = 0; q < ng; ++q) good_idx[q] += 1;
+        TP_HIP(hipMemcpyAsync(dM, M, (size_t)N0 * N0 * 8, hipMemcpyHostToDevice, c.cur));
+        mask_core(c, dM, N0, bad_frac ? *bad_frac : 0.01, flags ? *flags : 0, bad, rowmean, n_good, good_idx);
+    });
+}
+
+void tp_mask_dev(double *d_M, const int *n0, const double *bad_frac, const int *flags, const int *device,
+                 void *stream, int *bad, double *rowmean, int *n_good, int *good_idx, int *status) {
+    guarded(status, [&] {
+        if (!d_M || !n0 || *n0 < 1) fail(TP_ERR_ARG, "bad matrix");
+        Ctx &c = ctx_for(dev_of(device), (hipStream_t)stream);
+        mask_core(c, d_M, *n0, bad_frac ? *bad_frac : 0.01, flags ? *flags : 0, bad, rowmean, n_good, good_idx);
     });
 }
 
@@ -1216,9 +1237,14 @@ void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
         case 5: p = &g_xtx_int8; break;
         case 6: p = &g_pca_margin; break;
         case 7: p = &g_gemm_xcd; break;
+        case 8: p = &g_pca_krylov_min; break;
+        case 9: p = &g_pca_krylov_block; break;
+        case 10: p = &g_pca_krylov_steps; break;
         default: fail(TP_ERR_ARG, "unknown knob");
         }
         if (*which == 3 && *value != 16 && *value != 32) fail(TP_ERR_ARG, "stage depth must be 16 or 32");
+        if (*which == 9 && *value != 0 && (*value % 16 != 0 || *value > 256))
+            fail(TP_ERR_ARG, "Krylov block must be 0 or a multiple of 16 up to 256");
         *old = *p;
         *p = *value;
     });

@@ -3,6 +3,15 @@
 // arithmetic wants are written as fma() explicitly (oracle/tp_oracle.c does the
 // same), so GPU and oracle round identically.
 #pragma once
+#include <cassert>
+
+// Device-side bounds checks for debug builds (make DEVICE_ASSERTS=1): compiled
+// out of the product library.
+#ifdef TP_DEVICE_ASSERTS
+#define TP_DASSERT(cond) assert(cond)
+#else
+#define TP_DASSERT(cond) ((void)0)
+#endif
 #include <hip/hip_runtime.h>
 #include <cstdint>
 

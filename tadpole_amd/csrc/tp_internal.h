@@ -80,7 +80,8 @@ void ctx_shutdown_all();
 enum Slot {
     S_M = 0, S_ROWMEAN, S_DIAG, S_BAD, S_GOOD, S_NGOOD, S_X, S_COLMEAN,
     S_S, S_C, S_XC, S_XCT, S_G, S_Q, S_Z, S_W, S_SMALL, S_P, S_PT,
-    S_SWEEP, S_SWEEP2, S_SCORES, S_PARTIAL, S_MISC, S_SHARD, S_SHARD2, S_DEDUP
+    S_SWEEP, S_SWEEP2, S_SCORES, S_PARTIAL, S_MISC, S_SHARD, S_SHARD2, S_DEDUP,
+    S_KRY, S_KRYG, S_KRYT, S_KRYV
 };
 
 // ---------------------------------------------------------------- kernels
@@ -228,7 +229,11 @@ void xtx_int8_tiles128(Ctx &c, const int8_t *sl, int n, int ns, double *d_S, int
 void xtx_product(Ctx &c, const double *d_X, int n, double *d_S);
 
 extern int g_pca_margin;   // extra Chebyshev degrees over the planned count (default 0)
-struct PcaStats { int iters = 0; double resid = 0; double rate = 0; int block = 0; int blocks = 0; };
+struct PcaStats {
+    int iters = 0; double resid = 0; double rate = 0; int block = 0; int blocks = 0;
+    int krylov_steps = 0, krylov_dim = 0;   // block Krylov path (0: G formed)
+};
+extern int g_pca_krylov_min, g_pca_krylov_block, g_pca_krylov_steps;
 PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d_Pt,
                  double *h_sdev);
 

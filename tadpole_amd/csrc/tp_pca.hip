@@ -1,21 +1,33 @@
 // prcomp(cor, rank. = k)$x  (R/TADpole.R:452-453) on the GPU.
 //
 // R computes a FULL thin SVD of the column-centred N x N matrix (LAPACK gesdd)
-// and keeps k = min(max_pcs, N) right singular vectors.  Here:
-//   Xc = C - 1 colMeans(C)'                       (centring, tp_prep.hip)
-//   G  = Xc' Xc                                   (fp64 MFMA GEMM, symmetric)
-//   block subspace iteration on G, block b = k + oversampling, CholQR2
-//   orthonormalisation, Rayleigh-Ritz at the end (b x b eigensolve)
-//   P  = Xc V_k                                   (fp64 MFMA GEMM)
-// Only span(V_1..V_i) matters downstream (distances and CH are invariant to
-// sign and to rotations inside the top-i space), and the iteration stops when
-// every Ritz pair j <= k has ||G v - theta v|| <= tol * theta_1.
-// When N <= b the Ritz problem is G itself (exact full eigendecomposition).
+// and keeps k = min(max_pcs, N) right singular vectors, i.e. the top-k
+// eigenvectors of G = Xc' Xc, Xc = C - 1 colMeans(C)' (centring, tp_prep.hip).
+// Two ways to the same eigenvectors (only span(V_1..V_i) matters downstream:
+// distances and CH are invariant to sign and to rotations inside a prefix):
+//
+//  * small N (N < g_pca_krylov_min): G = Xc'Xc on the fp64 MFMA (N^3), then
+//    Chebyshev-filtered block subspace iteration on G (block b = k +
+//    oversampling, CholQR orthonormalisation, Rayleigh-Ritz at the end);
+//  * large N: G is never formed.  A block Krylov space of G (block p, s steps,
+//    D = s p columns) is built with two skinny products per step, W = Xc'(Xc Q)
+//    (2 x 2 N^2 p flops instead of N^3 + 2 N^2 b per subspace-iteration degree),
+//    every block re-orthogonalised twice against all earlier ones (CGS2) and
+//    orthonormalised by CholQR2.  The projected T = K'GK (D x D) is then solved
+//    for its top k eigenpairs by the same subspace iteration (products with T
+//    are D x D, not N x N), and V = K Y.  Block Krylov needs ~10x fewer products
+//    with G than subspace iteration (C3: D = 1024 columns vs 27 x 256).
+//
+// Either way the iteration stops when every Ritz pair j <= k has
+// ||G v - theta v|| <= tol * theta_1 (checked in the N-dimensional space), and
+// the scores are P = Xc V_k (fp64 MFMA GEMM).  When N <= b the Ritz problem is
+// G itself (exact full eigendecomposition).
 #include <rocblas/rocblas.h>
 #include <rocsolver/rocsolver.h>
 
 #include <algorithm>
 #include <cmath>
+#include <functional>
 #include <vector>
 
 #include <cstdio>
@@ -119,38 +131,38 @@ __global__ void k_diag(const double *W, int b, double *d) {
     if (j < b) d[j] = fabs(W[(size_t)j * b + j]);
 }
 
-int g_pca_margin = 0;   // extra Chebyshev degrees over the planned count (the residual check adds more when needed; tools/pca_margin.py)
+int g_pca_margin = 0;     // extra Chebyshev degrees over the planned count (the residual check adds more when needed; tools/pca_margin.py)
+int g_pca_krylov_min = 4096;   // N at which the block Krylov path replaces forming G (0: always, huge: never)
+int g_pca_krylov_block = 0;    // Krylov block p (0: 64 for k >= 128, else 32)
+int g_pca_krylov_steps = 0;    // Krylov steps s before the first check (0: ceil(5 k / p))
 
-PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d_Pt, double *h_sdev) {
-    PcaStats st;
+using Prod = std::function<void(const double *, double *)>;
+
+// W -= U: elementwise (n x p)
+__global__ void k_sub(double *W, const double *U, size_t cnt) {
+    size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < cnt) W[t] = W[t] - U[t];
+}
+
+// Top-k eigenpairs of a symmetric n x n operator by Chebyshev-filtered block
+// subspace iteration.  prod(Y, Out): Out = A Y (n x b, ld n).  A (n x n, ld n)
+// is read only when b >= n (exact eigendecomposition).  V (n x k): the Ritz
+// vectors, descending; h_theta: ascending Ritz values of the last Rayleigh-Ritz
+// problem.  Scratch: S_Q S_Z S_SWEEP S_SWEEP2 S_SMALL S_MISC (+ S_PARTIAL).
+static void subspace_topk(Ctx &c, const double *A, int n, int k, const Prod &prod, double *V,
+                          std::vector<double> &h_theta, PcaStats &st, uint64_t seed) {
     hipStream_t s = c.cur;
-    double *mean = c.buf[S_COLMEAN].as<double>(n);
-    double *Xc = c.buf[S_XC].as<double>((size_t)n * n);
-    double *XcT = c.buf[S_XCT].as<double>((size_t)n * n);
-    double *G = c.buf[S_G].as<double>((size_t)n * n);
-    launch_colmean(d_C, n, n, mean, s);
-    launch_center(d_C, mean, n, Xc, XcT, s);
-    {
-        GemmArgs g{n, n, n, Xc, n, true, Xc, n, G, n};
-        g.sym_upper = true;
-        kprof_begin(c, K_G_GEMM);
-        sym_gemm_sharded(c, g);
-        kprof_end(c, K_G_GEMM);
-    }
-    trace_mark(s, "pca: G");
     const int over = std::max(32, k / 4);
     int b = std::min(n, ((k + over + 31) / 32) * 32);
     st.block = b;
-    double *V = c.buf[S_W].as<double>((size_t)n * k);       // n x k, descending
-    std::vector<double> h_theta;
     if (b >= n) {
-        // exact: eigendecomposition of G itself (small n)
+        // exact: eigendecomposition of A itself (small n)
         rocblas_handle h = blas_for(c);
         b = n;
         int *d_info = c.buf[S_MISC].as<int>(64);
         double *theta = c.buf[S_SMALL].as<double>((size_t)n + 64);
         double *E = c.buf[S_Z].as<double>((size_t)n * n);
-        TP_HIP(hipMemcpyAsync(E, G, (size_t)n * n * sizeof(double), hipMemcpyDeviceToDevice, s));
+        TP_HIP(hipMemcpyAsync(E, A, (size_t)n * n * sizeof(double), hipMemcpyDeviceToDevice, s));
         double *offbuf = c.buf[S_Q].as<double>((size_t)n + 64);
         if (eig_sym_supported(n))
             eig_sym(h, E, n, theta, c.buf[S_PARTIAL].as<double>((size_t)n * n + 4 * n + 64), d_info, s);
@@ -166,191 +178,339 @@ PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d
         TP_HIP(hipStreamSynchronize(s));
         trace_mark(s, "pca: exact eig");
         st.iters = 0;
-    } else {
-        double *Q = c.buf[S_Q].as<double>((size_t)n * b);
-        double *Z = c.buf[S_Z].as<double>((size_t)n * b);
-        double *T = c.buf[S_SWEEP].as<double>((size_t)n * b);
-        double *Wsm = c.buf[S_SMALL].as<double>((size_t)3 * b * b + 2 * b + 64);
-        double *Xinv = Wsm + (size_t)b * b;
-        double *theta = Xinv + (size_t)b * b;
-        double *offd = theta + b;
-        double *Yinv = offd + b;   // b x b, U^{-1} of the last CholQR
-        double *resid = c.buf[S_MISC].as<double>(64 + k + b) + 64;
-        int *d_info = c.buf[S_MISC].as<int>(64);
-        const size_t nb = (size_t)n * b;
-        // random start block (well conditioned: the first iteration's CholQR
-        // orthonormalises G Q0 directly)
-        hipLaunchKernelGGL(k_rand_block, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, s, Q, n, b,
-                           0x5EEDULL + (uint64_t)n);
-        TP_HIP(hipGetLastError());
-        double *Yb = c.buf[S_SWEEP2].as<double>((size_t)n * b);   // 4th block buffer (sweep scratch later)
-        auto gemm_gq = [&](const double *Yin, double *Out) {   // Out = G Yin (row-sharded)
-            kprof_begin(c, K_GQ_GEMM);
-            rows_gemm_sharded(c, G, n, n, Yin, n, b, n, Out, 0, 1);
-            kprof_end(c, K_GQ_GEMM);
-        };
-        auto iterate = [&](int count) {   // plain subspace iteration
-            for (int it = 0; it < count; ++it) {
-                gemm_gq(Q, Z);
-                orth_cholqr(c, Z, Q, T, n, b, Wsm, Xinv, Yinv, d_info, 1, 1e-14);
-            }
-        };
-        // Chebyshev filter of degree m on [0, cut]: Q <- orth(T_m((G - e)/h) Q),
-        // e = h = cut / 2 (scaled three-term recurrence), then CholQR
-        auto cheb_block = [&](int m, double cut) {
-            const double e = 0.5 * cut, hh = 0.5 * cut;
-            const size_t cnt = (size_t)n * b;
-            const unsigned grid = (unsigned)((cnt + 255) / 256);
-            double *prev = Q, *cur = T, *gy = Z, *nxt = Yb;
-            gemm_gq(Q, gy);
-            hipLaunchKernelGGL(k_cheb, dim3(grid), dim3(256), 0, s, cur, gy, Q, (const double *)nullptr, cnt,
-                               1.0 / hh, -e / hh, 0.0);
-            for (int j = 1; j < m; ++j) {
-                gemm_gq(cur, gy);
-                hipLaunchKernelGGL(k_cheb, dim3(grid), dim3(256), 0, s, nxt, gy, cur, prev, cnt, 2.0 / hh,
-                                   -2.0 * e / hh, -1.0);
-                double *old = prev;
-                prev = cur;
-                cur = nxt;
-                nxt = old;
-            }
-            TP_HIP(hipGetLastError());
-            // cur holds Y_m; orthonormalise into Q (the CholQR temp must differ)
-            double *tmp = (cur == T) ? Yb : T;
-            if (cur == Q) {   // never: Q is Y_0 and m >= 1, but keep the buffers distinct
-                TP_HIP(hipMemcpyAsync(tmp, cur, cnt * sizeof(double), hipMemcpyDeviceToDevice, s));
-                cur = tmp;
-                tmp = (cur == T) ? Yb : T;
-            }
-            orth_cholqr(c, cur, Q, tmp, n, b, Wsm, Xinv, Yinv, d_info, 1, 1e-14);
-        };
-        const double target = 1e-12;
-        const int max_deg = 600;
-        // phase 1: four plain iterations as two squared ones (Z = G (G Q), one
-        // CholQR each), then read the spectrum estimate off the Cholesky
-        // diagonal (|U_jj| -> lambda_j^2 in orthogonal iteration on G^2)
-        int done = 4;
-        for (int it = 0; it < 2; ++it) {
-            gemm_gq(Q, T);
-            gemm_gq(T, Z);
+        st.resid = 0.0;
+        return;
+    }
+    double *Q = c.buf[S_Q].as<double>((size_t)n * b);
+    double *Z = c.buf[S_Z].as<double>((size_t)n * b);
+    double *T = c.buf[S_SWEEP].as<double>((size_t)n * b);
+    double *Wsm = c.buf[S_SMALL].as<double>((size_t)3 * b * b + 2 * b + 64);
+    double *Xinv = Wsm + (size_t)b * b;
+    double *theta = Xinv + (size_t)b * b;
+    double *offd = theta + b;
+    double *Yinv = offd + b;   // b x b, U^{-1} of the last CholQR
+    double *resid = c.buf[S_MISC].as<double>(64 + k + b) + 64;
+    int *d_info = c.buf[S_MISC].as<int>(64);
+    const size_t nb = (size_t)n * b;
+    // random start block (well conditioned: the first iteration's CholQR
+    // orthonormalises A Q0 directly)
+    hipLaunchKernelGGL(k_rand_block, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, s, Q, n, b, seed);
+    TP_HIP(hipGetLastError());
+    double *Yb = c.buf[S_SWEEP2].as<double>((size_t)n * b);   // 4th block buffer (sweep scratch later)
+    auto iterate = [&](int count) {   // plain subspace iteration
+        for (int it = 0; it < count; ++it) {
+            prod(Q, Z);
             orth_cholqr(c, Z, Q, T, n, b, Wsm, Xinv, Yinv, d_info, 1, 1e-14);
         }
-        double cut = 0.0, gk = 2.0, g1cap = 10.0;
-        int mdeg = 1;
+    };
+    // Chebyshev filter of degree m on [0, cut]: Q <- orth(T_m((A - e)/h) Q),
+    // e = h = cut / 2 (scaled three-term recurrence), then CholQR
+    auto cheb_block = [&](int m, double cut) {
+        const double e = 0.5 * cut, hh = 0.5 * cut;
+        const size_t cnt = (size_t)n * b;
+        const unsigned grid = (unsigned)((cnt + 255) / 256);
+        double *prev = Q, *cur = T, *gy = Z, *nxt = Yb;
+        prod(Q, gy);
+        hipLaunchKernelGGL(k_cheb, dim3(grid), dim3(256), 0, s, cur, gy, Q, (const double *)nullptr, cnt,
+                           1.0 / hh, -e / hh, 0.0);
+        for (int j = 1; j < m; ++j) {
+            prod(cur, gy);
+            hipLaunchKernelGGL(k_cheb, dim3(grid), dim3(256), 0, s, nxt, gy, cur, prev, cnt, 2.0 / hh,
+                               -2.0 * e / hh, -1.0);
+            double *old = prev;
+            prev = cur;
+            cur = nxt;
+            nxt = old;
+        }
+        TP_HIP(hipGetLastError());
+        // cur holds Y_m; orthonormalise into Q (the CholQR temp must differ)
+        double *tmp = (cur == T) ? Yb : T;
+        if (cur == Q) {   // never: Q is Y_0 and m >= 1, but keep the buffers distinct
+            TP_HIP(hipMemcpyAsync(tmp, cur, cnt * sizeof(double), hipMemcpyDeviceToDevice, s));
+            cur = tmp;
+            tmp = (cur == T) ? Yb : T;
+        }
+        orth_cholqr(c, cur, Q, tmp, n, b, Wsm, Xinv, Yinv, d_info, 1, 1e-14);
+    };
+    const double target = 1e-12;
+    const int max_deg = 600;
+    // phase 1: four plain iterations as two squared ones (Z = A (A Q), one
+    // CholQR each), then read the spectrum estimate off the Cholesky
+    // diagonal (|U_jj| -> lambda_j^2 in orthogonal iteration on A^2)
+    int done = 4;
+    for (int it = 0; it < 2; ++it) {
+        prod(Q, T);
+        prod(T, Z);
+        orth_cholqr(c, Z, Q, T, n, b, Wsm, Xinv, Yinv, d_info, 1, 1e-14);
+    }
+    double cut = 0.0, gk = 2.0, g1cap = 10.0;
+    int mdeg = 1;
+    {
+        std::vector<double> dg(b);
+        hipLaunchKernelGGL(k_diag, dim3((b + 255) / 256), dim3(256), 0, s, Wsm, b, resid);
+        TP_HIP(hipMemcpyAsync(dg.data(), resid, b * sizeof(double), hipMemcpyDeviceToHost, s));
+        TP_HIP(hipStreamSynchronize(s));
+        for (double &x : dg) x = std::sqrt(x);
+        const double l1 = dg[0], lk = dg[k - 1], lb = dg[b - 1];
+        cut = lb;
+        if (cut > 0 && lk > cut && l1 >= lk) {
+            const double x1 = 2.0 * l1 / cut - 1.0, xk = 2.0 * lk / cut - 1.0;
+            const double g1 = x1 + std::sqrt(x1 * x1 - 1.0);
+            gk = xk + std::sqrt(xk * xk - 1.0);
+            g1cap = g1;
+            // keep the filtered block CholQR-conditionable: (g1/gk)^m <= 1e6
+            mdeg = (int)std::floor(std::log(1e6) / std::log(std::max(g1 / gk, 1.0001)));
+            mdeg = std::max(1, std::min(8, mdeg));
+        } else {
+            cut = 0.0;
+        }
+        st.rate = gk > 1 ? 1.0 / gk : 0.9;
+        int need = (int)std::ceil(std::log(1.0 / target) / std::log(std::max(gk, 1.0005))) + g_pca_margin;
+        need = std::min(need, max_deg);
+        if (cut > 0) {
+            // Block degrees double: after total degree D the j-th column's
+            // components along the larger eigenvectors l < j have shrunk
+            // by (g_j/g_l)^D, so a block of degree D + mdeg amplifies them
+            // no more than the first block of degree mdeg did.  Capped so
+            // T_m(lambda_1) stays far from overflow in the Gram matrix.
+            const int mcap = std::max(1, std::min(24, (int)std::floor(100.0 / std::log10(std::max(g1cap, 10.0)))));
+            int deg = 0;
+            while (deg < need) {
+                const int m = std::min({need - deg, std::max(mdeg, deg + mdeg), mcap});
+                cheb_block(m, cut);
+                deg += m;
+                ++st.blocks;
+            }
+            done += need;
+        } else {
+            iterate(need);
+            done += need;
+        }
+    }
+    std::vector<double> h_res(k);
+    h_theta.resize(b);
+    rocblas_handle h = blas_for(c);
+    for (int round = 0; round < 6; ++round) {
+        // Rayleigh-Ritz: orthonormalise tightly, H = Q'AQ, eigen-decompose, rotate
+        // Q is orthonormal to ~kappa^2 eps after the last one-pass CholQR:
+        // one more pass on Q itself restores eps-orthonormality
+        orth_cholqr(c, Q, Z, T, n, b, Wsm, Xinv, Yinv, d_info, 1, 1e-14);
+        std::swap(Q, Z);
+        prod(Q, Z);
+        GemmArgs hq{b, b, n, Q, n, true, Z, n, Wsm, b};
+        hq.sym_upper = true;
+        hq.splitk = std::max(1, std::min(32, n / 128));
+        gemm_f64(hq, c.buf[S_PARTIAL], s);
+        if (eig_sym_supported(b))
+            eig_sym(h, Wsm, b, theta, c.buf[S_PARTIAL].as<double>((size_t)b * b + 4 * b + 64), d_info, s);
+        else
+            rb_check(rocsolver_dsyevd(h, rocblas_evect_original, rocblas_fill_upper, b, Wsm, b, theta, offd,
+                                      d_info),
+                     "dsyevd(RR)");
+        size_t tot = (size_t)b * b;
+        hipLaunchKernelGGL(k_select_rev, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, Wsm, b, b, Xinv);
+        // rotate: V = Q X (into T); A V = (A Q) X = Z X for the residuals of
+        // the top k Ritz pairs, ||A v - theta v||, without another product
+        // with A (into Yb)
+        GemmArgs rq{n, b, b, Q, n, false, Xinv, b, T, n};
+        rq.splitk = 0;
+        gemm_f64(rq, c.buf[S_PARTIAL], s);
+        GemmArgs gv{n, k, b, Z, n, false, Xinv, b, Yb, n};
+        gv.splitk = 0;
+        gemm_f64(gv, c.buf[S_PARTIAL], s);
+        std::swap(Q, T);
+        hipLaunchKernelGGL(k_resid, dim3((k + 3) / 4), dim3(256), 0, s, Yb, Q, theta, n, b, k, resid);
+        TP_HIP(hipGetLastError());
+        TP_HIP(hipMemcpyAsync(h_res.data(), resid, k * sizeof(double), hipMemcpyDeviceToHost, s));
+        TP_HIP(hipMemcpyAsync(h_theta.data(), theta, b * sizeof(double), hipMemcpyDeviceToHost, s));
+        TP_HIP(hipStreamSynchronize(s));
+        const double th1 = std::fabs(h_theta[b - 1]);
+        double worst = 0.0;
+        for (int j = 0; j < k; ++j) worst = std::max(worst, h_res[j] / (th1 > 0 ? th1 : 1.0));
+        st.resid = worst;
+        const double thk = h_theta[b - k], thb = h_theta[0];
+        const double rho = (thk > 0 && thb > 0) ? std::min(0.98, std::max(1e-3, thb / thk)) : 0.9;
+        st.rate = rho;
+        if (getenv("TP_TRACE_PCA"))
+            fprintf(stderr, "[pca] n=%d round %d degree %d worst %.2e thk/thb %.3f cut %.3e gk %.3f mdeg %d\n", n,
+                    round, done, worst, thb > 0 ? thk / thb : 0.0, cut, gk, mdeg);
+        if (!(worst > target * 10) || done >= max_deg) break;
+        int more;
+        if (cut > 0) {
+            // Ritz values bound the spectrum better now: cut at theta_b and
+            // take the Chebyshev growth at theta_k per degree for the
+            // factor worst / target still to remove
+            cut = std::max(cut, thb);
+            double g = 1.0005;
+            if (thk > cut) {
+                const double x = 2.0 * thk / cut - 1.0;
+                g = std::max(g, x + std::sqrt(x * x - 1.0));
+            }
+            const int need = (int)std::ceil(std::log(worst / target) / std::log(g)) + 1;
+            more = std::max(1, std::min(max_deg - done, need));
+            for (int deg = 0; deg < more; deg += mdeg) cheb_block(std::min(mdeg, more - deg), cut);
+        } else {
+            const int need = (int)std::ceil(std::log(target / worst) / std::log(rho)) + 2;
+            more = std::max(2, std::min(max_deg - done, need));
+            iterate(more);
+        }
+        done += more;
+    }
+    st.iters = done;
+    if (!(st.resid <= 1e-8)) fail(TP_ERR_NUMERIC, "PCA subspace iteration did not converge");
+    TP_HIP(hipMemcpyAsync(V, Q, (size_t)n * k * sizeof(double), hipMemcpyDeviceToDevice, s));
+}
+
+// Block Krylov path (see the file comment): V (n x k) = top-k eigenvectors of
+// G = Xc'Xc without forming G.  Blocks K_t (n x p) in S_KRY, G K_t in S_KRYG,
+// T = K'GK in S_KRYT, the small problem's vectors in S_KRYV.
+static void krylov_topk(Ctx &c, const double *Xc, const double *XcT, int n, int k, double *V,
+                        std::vector<double> &h_theta, PcaStats &st) {
+    hipStream_t s = c.cur;
+    const int p = g_pca_krylov_block > 0 ? g_pca_krylov_block : (k >= 128 ? 64 : 32);
+    // D ~ 5k columns; denser spectra of larger matrices need more (C5 arms:
+    // +4 steps at 24k bins)
+    int steps = (5 * k + p - 1) / p;
+    if (n > 12000) steps += 2 * (int)std::ceil(std::log2((double)n / 12000.0));
+    if (g_pca_krylov_steps > 0) steps = g_pca_krylov_steps;
+    const int smax = std::max(steps, std::min(steps + 24, (n / 2) / p));
+    steps = std::min(steps, smax);
+    double *K = c.buf[S_KRY].as<double>((size_t)n * p * smax);
+    double *GK = c.buf[S_KRYG].as<double>((size_t)n * p * smax);
+    const size_t np = (size_t)n * p;
+    const unsigned g1 = (unsigned)((np + 255) / 256);
+    // per-step scratch; re-fetched by every extend() because the small
+    // problem (subspace_topk) grows and reallocates the same slots
+    double *W, *Zt, *U, *Xp, *Wsm, *Xinv, *Yinv;
+    int *d_info;
+    auto scratch = [&]() {
+        W = c.buf[S_Q].as<double>(np);
+        Zt = c.buf[S_Z].as<double>(np);
+        U = c.buf[S_SWEEP2].as<double>(np);
+        Xp = c.buf[S_SWEEP].as<double>((size_t)p * p * smax);
+        Wsm = c.buf[S_SMALL].as<double>((size_t)3 * p * p + 2 * p + 64);
+        Xinv = Wsm + (size_t)p * p;
+        Yinv = Xinv + (size_t)p * p;
+        d_info = c.buf[S_MISC].as<int>(64);
+    };
+    scratch();
+    hipLaunchKernelGGL(k_rand_block, dim3(g1), dim3(256), 0, s, W, n, p, 0x5EEDULL + (uint64_t)n);
+    TP_HIP(hipGetLastError());
+    orth_cholqr(c, W, K, Zt, n, p, Wsm, Xinv, Yinv, d_info, 2, 1e-14);
+    const double target = 1e-12;
+    int built = 0;   // blocks with G K_t computed
+    int kdone = 1;   // blocks K_t available
+    auto extend = [&](int upto) {
+        scratch();
+        for (int t = built; t < upto; ++t) {
+            if (t >= kdone) {
+                // K_t: G K_{t-1} re-orthogonalised twice against K_0..K_{t-1} (CGS2), CholQR2
+                TP_HIP(hipMemcpyAsync(W, GK + (size_t)(t - 1) * np, np * sizeof(double), hipMemcpyDeviceToDevice, s));
+                const int D = t * p;
+                for (int pass = 0; pass < 2; ++pass) {
+                    GemmArgs pr{D, p, n, K, n, true, W, n, Xp, D};   // K'W
+                    pr.splitk = 0;
+                    gemm_f64(pr, c.buf[S_PARTIAL], s);
+                    GemmArgs up{n, p, D, K, n, false, Xp, D, U, n};   // K (K'W)
+                    up.splitk = 0;
+                    gemm_f64(up, c.buf[S_PARTIAL], s);
+                    hipLaunchKernelGGL(k_sub, dim3(g1), dim3(256), 0, s, W, U, np);
+                    TP_HIP(hipGetLastError());
+                }
+                orth_cholqr(c, W, K + (size_t)t * np, Zt, n, p, Wsm, Xinv, Yinv, d_info, 2, 1e-14);
+                kdone = t + 1;
+            }
+            double *Kt = K + (size_t)t * np;
+            double *GKt = GK + (size_t)t * np;
+            kprof_begin(c, K_GQ_GEMM);
+            rows_gemm_sharded(c, XcT, n, n, Kt, n, p, n, Zt, 0, 1);     // Xc K_t
+            rows_gemm_sharded(c, Xc, n, n, Zt, n, p, n, GKt, 0, 1);     // Xc'(Xc K_t)
+            kprof_end(c, K_GQ_GEMM);
+        }
+        built = std::max(built, upto);
+    };
+    std::vector<double> h_res(k);
+    for (;;) {
+        extend(steps);
+        const int D = steps * p;
+        trace_mark(s, "pca: krylov");
+        // T = K'GK (upper tiles, mirrored), then its top k eigenpairs
+        double *Tm = c.buf[S_KRYT].as<double>((size_t)D * D);
+        GemmArgs tg{D, D, n, K, n, true, GK, n, Tm, D};
+        tg.sym_upper = true;
+        tg.splitk = 0;
+        gemm_f64(tg, c.buf[S_PARTIAL], s);
+        double *Vs = c.buf[S_KRYV].as<double>((size_t)D * k);
+        PcaStats sst;
+        Prod tprod = [&](const double *Y, double *Out) {
+            GemmArgs g{D, sst.block, D, Tm, D, true, Y, D, Out, D};
+            g.splitk = 0;
+            gemm_f64(g, c.buf[S_PARTIAL], s);
+        };
+        subspace_topk(c, Tm, D, k, tprod, Vs, h_theta, sst, 0x5EEDULL + (uint64_t)D);
+        // V = K Y, G V = (G K) Y; residuals in the n-dimensional space
+        GemmArgs vg{n, k, D, K, n, false, Vs, D, V, n};
+        vg.splitk = 0;
+        gemm_f64(vg, c.buf[S_PARTIAL], s);
+        double *GV = c.buf[S_Q].as<double>((size_t)n * k);
+        GemmArgs gg{n, k, D, GK, n, false, Vs, D, GV, n};
+        gg.splitk = 0;
+        gemm_f64(gg, c.buf[S_PARTIAL], s);
+        const int bs = (int)h_theta.size();
+        double *dth = c.buf[S_MISC].as<double>(64 + 2 * bs + k) + 64;
+        double *resid = dth + bs;
+        TP_HIP(hipMemcpyAsync(dth, h_theta.data(), bs * sizeof(double), hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(k_resid, dim3((k + 3) / 4), dim3(256), 0, s, GV, V, dth, n, bs, k, resid);
+        TP_HIP(hipGetLastError());
+        TP_HIP(hipMemcpyAsync(h_res.data(), resid, k * sizeof(double), hipMemcpyDeviceToHost, s));
+        TP_HIP(hipStreamSynchronize(s));
+        const double th1 = std::fabs(h_theta[bs - 1]);
+        double worst = 0.0;
+        for (int j = 0; j < k; ++j) worst = std::max(worst, h_res[j] / (th1 > 0 ? th1 : 1.0));
+        st.resid = worst;
+        st.iters = sst.iters;
+        st.block = sst.block;
+        st.blocks = sst.blocks;
+        st.krylov_steps = steps;
+        st.krylov_dim = D;
+        if (getenv("TP_TRACE_PCA"))
+            fprintf(stderr, "[pca] krylov n=%d p=%d steps=%d D=%d small: degree %d resid %.2e | n-space worst %.2e\n",
+                    n, p, steps, D, sst.iters, sst.resid, worst);
+        if (!(worst > target * 10) || steps >= smax) break;
+        steps = std::min(smax, steps + 4);
+    }
+    if (!(st.resid <= 1e-8)) fail(TP_ERR_NUMERIC, "PCA block Krylov iteration did not converge");
+}
+
+PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d_Pt, double *h_sdev) {
+    PcaStats st;
+    hipStream_t s = c.cur;
+    double *mean = c.buf[S_COLMEAN].as<double>(n);
+    double *Xc = c.buf[S_XC].as<double>((size_t)n * n);
+    double *XcT = c.buf[S_XCT].as<double>((size_t)n * n);
+    launch_colmean(d_C, n, n, mean, s);
+    launch_center(d_C, mean, n, Xc, XcT, s);
+    double *V = c.buf[S_W].as<double>((size_t)n * k);       // n x k, descending
+    std::vector<double> h_theta;
+    const int b_est = std::min(n, ((k + std::max(32, k / 4) + 31) / 32) * 32);
+    if (n >= g_pca_krylov_min && b_est < n) {
+        krylov_topk(c, Xc, XcT, n, k, V, h_theta, st);
+    } else {
+        double *G = c.buf[S_G].as<double>((size_t)n * n);
         {
-            std::vector<double> dg(b);
-            hipLaunchKernelGGL(k_diag, dim3((b + 255) / 256), dim3(256), 0, s, Wsm, b, resid);
-            TP_HIP(hipMemcpyAsync(dg.data(), resid, b * sizeof(double), hipMemcpyDeviceToHost, s));
-            TP_HIP(hipStreamSynchronize(s));
-            for (double &x : dg) x = std::sqrt(x);
-            const double l1 = dg[0], lk = dg[k - 1], lb = dg[b - 1];
-            cut = lb;
-            if (cut > 0 && lk > cut && l1 >= lk) {
-                const double x1 = 2.0 * l1 / cut - 1.0, xk = 2.0 * lk / cut - 1.0;
-                const double g1 = x1 + std::sqrt(x1 * x1 - 1.0);
-                gk = xk + std::sqrt(xk * xk - 1.0);
-                g1cap = g1;
-                // keep the filtered block CholQR-conditionable: (g1/gk)^m <= 1e6
-                mdeg = (int)std::floor(std::log(1e6) / std::log(std::max(g1 / gk, 1.0001)));
-                mdeg = std::max(1, std::min(8, mdeg));
-            } else {
-                cut = 0.0;
-            }
-            st.rate = gk > 1 ? 1.0 / gk : 0.9;
-            int need = (int)std::ceil(std::log(1.0 / target) / std::log(std::max(gk, 1.0005))) + g_pca_margin;
-            need = std::min(need, max_deg);
-            if (cut > 0) {
-                // Block degrees double: after total degree D the j-th column's
-                // components along the larger eigenvectors l < j have shrunk
-                // by (g_j/g_l)^D, so a block of degree D + mdeg amplifies them
-                // no more than the first block of degree mdeg did.  Capped so
-                // T_m(lambda_1) stays far from overflow in the Gram matrix.
-                const int mcap = std::max(1, std::min(24, (int)std::floor(100.0 / std::log10(std::max(g1cap, 10.0)))));
-                int deg = 0;
-                while (deg < need) {
-                    const int m = std::min({need - deg, std::max(mdeg, deg + mdeg), mcap});
-                    cheb_block(m, cut);
-                    deg += m;
-                    ++st.blocks;
-                }
-                done += need;
-            } else {
-                iterate(need);
-                done += need;
-            }
+            GemmArgs g{n, n, n, Xc, n, true, Xc, n, G, n};
+            g.sym_upper = true;
+            kprof_begin(c, K_G_GEMM);
+            sym_gemm_sharded(c, g);
+            kprof_end(c, K_G_GEMM);
         }
-        std::vector<double> h_res(k);
-        h_theta.resize(b);
-        rocblas_handle h = blas_for(c);
-        for (int round = 0; round < 6; ++round) {
-            // Rayleigh-Ritz: orthonormalise tightly, H = Q'GQ, eigen-decompose, rotate
-            // Q is orthonormal to ~kappa^2 eps after the last one-pass CholQR:
-            // one more pass on Q itself restores eps-orthonormality
-            orth_cholqr(c, Q, Z, T, n, b, Wsm, Xinv, Yinv, d_info, 1, 1e-14);
-            std::swap(Q, Z);
-            rows_gemm_sharded(c, G, n, n, Q, n, b, n, Z, 0);
-            GemmArgs hq{b, b, n, Q, n, true, Z, n, Wsm, b};
-            hq.sym_upper = true;
-            hq.splitk = std::max(1, std::min(32, n / 128));
-            gemm_f64(hq, c.buf[S_PARTIAL], s);
-            if (eig_sym_supported(b))
-                eig_sym(h, Wsm, b, theta, c.buf[S_PARTIAL].as<double>((size_t)b * b + 4 * b + 64), d_info, s);
-            else
-                rb_check(rocsolver_dsyevd(h, rocblas_evect_original, rocblas_fill_upper, b, Wsm, b, theta, offd,
-                                          d_info),
-                         "dsyevd(RR)");
-            size_t tot = (size_t)b * b;
-            hipLaunchKernelGGL(k_select_rev, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, Wsm, b, b, Xinv);
-            // rotate: V = Q X (into T); G V = (G Q) X = Z X for the residuals of
-            // the top k Ritz pairs, ||G v - theta v||, without another product
-            // with G (into Yb)
-            GemmArgs rq{n, b, b, Q, n, false, Xinv, b, T, n};
-            rq.splitk = 0;
-            gemm_f64(rq, c.buf[S_PARTIAL], s);
-            GemmArgs gv{n, k, b, Z, n, false, Xinv, b, Yb, n};
-            gv.splitk = 0;
-            gemm_f64(gv, c.buf[S_PARTIAL], s);
-            std::swap(Q, T);
-            hipLaunchKernelGGL(k_resid, dim3((k + 3) / 4), dim3(256), 0, s, Yb, Q, theta, n, b, k, resid);
-            TP_HIP(hipGetLastError());
-            TP_HIP(hipMemcpyAsync(h_res.data(), resid, k * sizeof(double), hipMemcpyDeviceToHost, s));
-            TP_HIP(hipMemcpyAsync(h_theta.data(), theta, b * sizeof(double), hipMemcpyDeviceToHost, s));
-            TP_HIP(hipStreamSynchronize(s));
-            const double th1 = std::fabs(h_theta[b - 1]);
-            double worst = 0.0;
-            for (int j = 0; j < k; ++j) worst = std::max(worst, h_res[j] / (th1 > 0 ? th1 : 1.0));
-            st.resid = worst;
-            const double thk = h_theta[b - k], thb = h_theta[0];
-            const double rho = (thk > 0 && thb > 0) ? std::min(0.98, std::max(1e-3, thb / thk)) : 0.9;
-            st.rate = rho;
-            if (getenv("TP_TRACE_PCA"))
-                fprintf(stderr, "[pca] n=%d round %d degree %d worst %.2e thk/thb %.3f cut %.3e gk %.3f mdeg %d\n", n,
-                        round, done, worst, thb > 0 ? thk / thb : 0.0, cut, gk, mdeg);
-            if (!(worst > target * 10) || done >= max_deg) break;
-            int more;
-            if (cut > 0) {
-                // Ritz values bound the spectrum better now: cut at theta_b and
-                // take the Chebyshev growth at theta_k per degree for the
-                // factor worst / target still to remove
-                cut = std::max(cut, thb);
-                double g = 1.0005;
-                if (thk > cut) {
-                    const double x = 2.0 * thk / cut - 1.0;
-                    g = std::max(g, x + std::sqrt(x * x - 1.0));
-                }
-                const int need = (int)std::ceil(std::log(worst / target) / std::log(g)) + 1;
-                more = std::max(1, std::min(max_deg - done, need));
-                for (int deg = 0; deg < more; deg += mdeg) cheb_block(std::min(mdeg, more - deg), cut);
-            } else {
-                const int need = (int)std::ceil(std::log(target / worst) / std::log(rho)) + 2;
-                more = std::max(2, std::min(max_deg - done, need));
-                iterate(more);
-            }
-            done += more;
-        }
-        st.iters = done;
-        if (!(st.resid <= 1e-8)) fail(TP_ERR_NUMERIC, "PCA subspace iteration did not converge");
-        TP_HIP(hipMemcpyAsync(V, Q, (size_t)n * k * sizeof(double), hipMemcpyDeviceToDevice, s));
+        trace_mark(s, "pca: G");
+        Prod gq = [&](const double *Yin, double *Out) {   // Out = G Yin (row-sharded)
+            kprof_begin(c, K_GQ_GEMM);
+            rows_gemm_sharded(c, G, n, n, Yin, n, st.block, n, Out, 0, 1);
+            kprof_end(c, K_GQ_GEMM);
+        };
+        subspace_topk(c, G, n, k, gq, V, h_theta, st, 0x5EEDULL + (uint64_t)n);
     }
     // scores P = Xc V  (= XcT' V): n x k column-major; Pt row-major
     rows_gemm_sharded(c, XcT, n, n, V, n, k, n, d_P, 0);

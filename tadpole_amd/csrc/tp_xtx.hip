@@ -109,6 +109,8 @@ __global__ void __launch_bounds__(256) k_xtx_i8(const int8_t *__restrict__ S, in
     const size_t slice = (size_t)Np * Kp;
     const int8_t *pa = S + (size_t)(i0 + fr) * Kp + fk;
     const int8_t *pb = S + (size_t)(j0 + fr) * Kp + fk;
+    // slice rows read: i0 + 31, j0 + 31 (< Np); k bytes kb + fk .. + 15 (< Kp)
+    TP_DASSERT(i0 + 31 < Np && j0 + 31 < Np && Kp % 64 == 0);
     for (int kb = 0; kb < Kp; kb += 64) {
         i32x4 fa[NS][2], fb[NS][2];
 #pragma unroll
@@ -176,6 +178,7 @@ __global__ void __launch_bounds__(512) k_xtx_i8_big(const int8_t *__restrict__ S
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
             const int ca = min(ia + lc, Np - 1), cb = min(jb + lc, Np - 1);
+            TP_DASSERT(kb + lk + 16 <= Kp && ca >= 0 && cb >= 0);
             r[0][s] = *(const i32x4 *)(S + s * slice + (size_t)ca * Kp + kb + lk);
             r[1][s] = *(const i32x4 *)(S + s * slice + (size_t)cb * Kp + kb + lk);
         }

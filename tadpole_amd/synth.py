@@ -68,8 +68,12 @@ def synth_hic(n0: int, seed: int, zero_frac: float = 0.005,
                  + 1.0 * (meta[r0:r1, None] == meta[None, :]))
         e[idx[None, :] < i] = 0.0          # draw the upper triangle only
         out[r0:r1] = rng.poisson(e)
-    iu = np.tril_indices(n0, -1)
-    out[iu] = out.T[iu]                    # mirror: upper wins
+    for r0 in range(0, n0, blk):           # mirror: upper wins (row blocks, no N^2 index arrays)
+        r1 = min(n0, r0 + blk)
+        out[r0:r1, :r0] = out[:r0, r0:r1].T
+        sub = out[r0:r1, r0:r1]
+        il = np.tril_indices(r1 - r0, -1)
+        sub[il] = sub.T[il]
     nz = max(1, int(round(zero_frac * n0))) if zero_frac > 0 else 0
     if nz:
         z = rng.choice(n0, nz, replace=False)
@@ -90,3 +94,25 @@ def config_matrix(config: int, **kw) -> np.ndarray:
 def genome_bins(resol: int = 25000):
     """Bins per chromosome for C4 (whole genome @resol)."""
     return {c: -(-bp // resol) for c, bp in HG19_BP.items()}
+
+
+def genome_seed(name: str) -> int:
+    """Seed of chromosome ``name``'s C4 matrix: SEED_BASE + 4 + 100 * (its index
+    in HG19_BP)."""
+    return SEED_BASE + 4 + 100 * list(HG19_BP).index(name)
+
+
+def genome_matrix(name: str, resol: int = 25000) -> np.ndarray:
+    """C4: the synthetic matrix of one chromosome at ``resol``."""
+    return synth_hic(genome_bins(resol)[name], genome_seed(name))
+
+
+def early_centromere_matrix(n0: int, seed: int, lo: int, hi: int) -> np.ndarray:
+    """A synthetic matrix whose centromere (zero run) is bins [lo, hi) of the
+    first half, so the reference's q-arm removal by original index
+    (R/TADpole.R:78-80) drops bins inside the arm (the C5 layout, centromere
+    past the middle, drops none)."""
+    m = synth_hic(n0, seed)
+    m[lo:hi, :] = 0
+    m[:, lo:hi] = 0
+    return m

@@ -1,0 +1,254 @@
+"""GPU parity at the BASELINE configs (BASELINE.json configs[1..4]) and on the
+paths around them, against committed oracle fixtures (tests/golden/, made by
+make_golden.py from oracle/tadpole_oracle.py) or, at full C5 size, through
+size-independent properties.
+
+Bars (north_star): TAD start/end indices, n_pcs, optimal_n_clusters, bad
+columns, n_cluster per tree, the final tree's boundary order and hclust merge
+matrix bit-exact; CH scores within 1e-6 relative (NA pattern exact); heights
+within 1e-8 relative (different PCA algorithm from LAPACK: the PC scores agree
+to ~1e-12, not bit for bit).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import gpu_helpers as G
+import tadpole_oracle as O
+from tadpole_amd.synth import (SEED_BASE, early_centromere_matrix, genome_bins, genome_matrix, synth_hic)
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _coords_dict(z, prefix=""):
+    lev = z[prefix + "levels"]
+    co = z[prefix + "coords"]
+    return {int(q): co[co[:, 0] == q][:, 1:] for q in lev}
+
+
+def _check(got, z, prefix="", bad=True):
+    assert got.n_pcs == int(z[prefix + "n_pcs"])
+    assert got.optimal_n_clusters == int(z[prefix + "optimal_n_clusters"])
+    ref = _coords_dict(z, prefix)
+    assert set(got.clusters) == {str(q) for q in ref}
+    for q, v in ref.items():
+        assert np.array_equal(got.clusters[str(q)], v), q
+    if bad and (prefix + "bad_idx1") in z:
+        assert np.array_equal(got.bad_columns, z[prefix + "bad_idx1"])
+    a, b = got.scores, z[prefix + "scores"]
+    assert a.shape == b.shape
+    fin = ~np.isnan(b)
+    assert np.array_equal(np.isnan(a), ~fin)
+    assert np.max(np.abs(a[fin] - b[fin]) / np.abs(b[fin])) < 1e-6
+    assert np.array_equal(got.dendro.boundary - 1, z[prefix + "merge_b"])
+    assert np.array_equal(got.dendro.merge, z[prefix + "merge"])
+    np.testing.assert_allclose(got.dendro.height, z[prefix + "height"], rtol=1e-8)
+
+
+@pytest.mark.parametrize("name", ["c2", "c3"])
+def test_config_golden(gpu, name):
+    """C2 (synthetic 2000 x 2000) and C3 (chr18 @10kb shape, 7808 bins), full
+    size, max_pcs = 200, end to end through TADpole() vs the oracle's outputs."""
+    import tadpole_amd as tp
+    z = np.load(os.path.join(GOLD, f"{name}.npz"))
+    m = synth_hic(int(z["n0"]), int(z["seed"]))
+    got = tp.TADpole(m, max_pcs=int(z["max_pcs"]))
+    _check(got, z)
+    # the PCA residual the pipeline accepted (||G v - theta v|| / theta_1)
+    assert got.timings_ms[13] <= 1e-11
+
+
+def test_config_c3_from_hbm(gpu):
+    """C3 with the matrix already resident in HBM (a torch tensor: the bench's
+    input form) gives the same result as from host memory."""
+    import torch
+    import tadpole_amd as tp
+    z = np.load(os.path.join(GOLD, "c3.npz"))
+    m = synth_hic(int(z["n0"]), int(z["seed"]))
+    got = tp.TADpole(torch.from_numpy(m).cuda(), max_pcs=200)
+    _check(got, z)
+
+
+@pytest.mark.parametrize("forced", [True, False])
+def test_pca_krylov_path_vs_lapack(gpu, forced):
+    """The block Krylov PCA (G never formed) against LAPACK's SVD on a matrix
+    below its default size threshold (forced) and the G path on the same
+    matrix: every prefix subspace the sweep uses agrees."""
+    n0 = 2600
+    m = synth_hic(n0, SEED_BASE + 77)
+    cm = O.clean_symmetrize(m)
+    obad, _, _ = O.bad_mask(cm, 0.01)
+    g = np.flatnonzero(~obad)
+    c = O.sparse_cor(cm[np.ix_(g, g)])
+    old = G.knob(8, 0 if forced else 1 << 30)
+    try:
+        p, _ = G.pca(c, 200)
+    finally:
+        G.knob(8, old)
+    op = O.prcomp_x(c, 200)
+    s = np.sign(np.sum(p * op, axis=0))
+    s[s == 0] = 1
+    scale = np.abs(op).max()
+    np.testing.assert_allclose(p[:, :20] * s[:20], op[:, :20], atol=1e-9 * scale)
+    sv = np.linalg.svd(op, compute_uv=False)
+
+    def proj(x, i):
+        q, _ = np.linalg.qr(x[:, :i])
+        return q @ q.T
+    for i in (1, 5, 20, 100, 199, 200):
+        if i < 200 and sv[i - 1] / max(sv[i], 1e-300) < 1.0 + 1e-6:
+            continue
+        assert np.abs(proj(p, i) - proj(op, i)).max() < 1e-7, i
+
+
+def test_pipeline_krylov_forced_end_to_end(gpu):
+    """A whole TADpole() through the Krylov PCA at a size the oracle runs live."""
+    import tadpole_amd as tp
+    m = synth_hic(2400, SEED_BASE + 78)
+    old = G.knob(8, 0)
+    try:
+        got = tp.TADpole(m, max_pcs=200)
+    finally:
+        G.knob(8, old)
+    assert got.timings_ms[16] > 0          # the Krylov path ran
+    ref = O.tadpole(m, max_pcs=200)
+    assert (got.n_pcs, got.optimal_n_clusters) == (ref.n_pcs, ref.optimal_n_clusters)
+    for q, v in ref.clusters.items():
+        assert np.array_equal(got.clusters[str(q)], v), q
+    a, b = got.scores, ref.scores
+    fin = ~np.isnan(b)
+    assert np.array_equal(np.isnan(a), ~fin)
+    assert np.max(np.abs(a[fin] - b[fin]) / np.abs(b[fin])) < 1e-6
+
+
+# ------------------------------------------------------------ arm path (C5)
+
+@pytest.mark.parametrize("name", ["arm_c5layout", "arm_early"])
+@pytest.mark.parametrize("mode", ["bug", "fixed"])
+def test_arms_golden(gpu, name, mode):
+    """centromere_search=TRUE (R/TADpole.R:58-85,351-442) against the oracle:
+    merging_arms, and per arm n_pcs, optimal_n_clusters, scores, dendro and
+    every `cluster` level; bug-compatible (q-arm bad bins removed by original
+    index) and fixed modes."""
+    import tadpole_amd as tp
+    z = np.load(os.path.join(GOLD, f"{name}.npz"))
+    n0, seed = int(z["n0"]), int(z["seed"])
+    early = tuple(int(x) for x in z["early"])
+    m = early_centromere_matrix(n0, seed, *early) if early[0] >= 0 else synth_hic(n0, seed, centromere=True)
+    got = tp.TADpole(m, max_pcs=200, centromere_search=True, fixed_centromere=(mode == "fixed"))
+    assert np.array_equal(got.merging_arms, z[f"{mode}_merging_arms"])
+    for arm in ("p", "q"):
+        sub = getattr(got, arm)
+        assert np.array_equal(sub.dendro.labels, z[f"{mode}_{arm}_names"].astype(str).tolist())
+        _check(sub, z, f"{mode}_{arm}_", bad=False)
+        assert sub.cluster is sub.clusters        # R's `$cluster` slot on the arm branch
+
+
+def test_arms_bug_mode_errors_like_r(gpu):
+    import tadpole_amd as tp
+    m = synth_hic(300, 5)
+    m[:20, :] = 0
+    m[:, :20] = 0                                 # longest bad run touches the start
+    with pytest.raises(TypeError):
+        tp.TADpole(m, centromere_search=True)
+    got = tp.TADpole(m, centromere_search=True, fixed_centromere=True)
+    ref = tp.TADpole(m)
+    assert got.n_pcs == ref.n_pcs and got.clusters.keys() == ref.clusters.keys()
+
+
+# ----------------------------------------------------------- genome (C4)
+
+def test_genome_c4_one_gpu(gpu):
+    """C4: the 23 hg19 chromosomes @25 kb through run_genome on one GPU
+    (concurrent streams): every result equals its own single-stream run, and
+    the three smallest equal the oracle fixtures."""
+    import tadpole_amd as tp
+    from tadpole_amd.genome import run_genome
+    sizes = genome_bins()
+    mats = {c: genome_matrix(c) for c in sizes}
+    res, secs = run_genome(mats, sizes=sizes, streams=4, max_pcs=200)
+    assert set(res) == set(sizes)
+    for c in sizes:
+        one = tp.TADpole(mats[c], max_pcs=200)
+        r = res[c]
+        assert (r.n_pcs, r.optimal_n_clusters) == (one.n_pcs, one.optimal_n_clusters), c
+        assert r.clusters.keys() == one.clusters.keys(), c
+        for q in one.clusters:
+            assert np.array_equal(r.clusters[q], one.clusters[q]), (c, q)
+        assert np.array_equal(r.scores.view(np.uint64), one.scores.view(np.uint64)), c
+    for c in ("chr21", "chr22", "chr19"):
+        _check(res[c], np.load(os.path.join(GOLD, f"genome_{c}.npz")))
+    print("C4 seconds per chromosome:", {c: round(s, 3) for c, s in sorted(secs.items())})
+
+
+# ------------------------------------------------- C5 at full size (properties)
+
+def _nested(clusters):
+    """Boundaries of level k are a subset of those of level k+1 (cuts of one
+    tree) and every level tiles its bins in order."""
+    levels = sorted(int(q) for q in clusters)
+    prev = None
+    for q in levels:
+        c = clusters[str(q)]
+        assert np.all(c[:, 0] <= c[:, 1]) and np.all(c[1:, 0] > c[:-1, 1])
+        starts = set(c[:, 0].tolist())
+        if prev is not None:
+            assert prev <= starts
+        prev = starts
+
+
+def test_c5_full_size_sharded_bit_identical(gpu):
+    """C5 (chr1 @5kb shape, 49 851 bins, centromere_search=TRUE): the arms
+    (~24.3k and ~21.3k bins) split over 8 virtual shards give the bits of the
+    unsplit schedule; the PCA residual bound holds at full size; the levels
+    nest.  The matrix is generated in HBM (torch, seeded) and stays there."""
+    import torch
+    import tadpole_amd as tp
+    n0 = 49851
+    gen = torch.Generator(device="cuda").manual_seed(SEED_BASE + 5)
+    idx = torch.arange(n0, device="cuda", dtype=torch.float64)
+    m = torch.empty((n0, n0), dtype=torch.float64, device="cuda")
+    blk = 2048
+    for r0 in range(0, n0, blk):
+        r1 = min(n0, r0 + blk)
+        e = 1000.0 / (1.0 + (idx[r0:r1, None] - idx[None, :]).abs())
+        m[r0:r1] = torch.poisson(e, generator=gen)
+        del e
+    for r0 in range(0, n0, blk):          # mirror the upper triangle (upper wins)
+        r1 = min(n0, r0 + blk)
+        m[r0:r1, :r0] = m[:r0, r0:r1].T
+        m[r0:r1, r0:r1] = torch.triu(m[r0:r1, r0:r1]) + torch.triu(m[r0:r1, r0:r1], 1).T
+    a, b = int(0.4875 * n0), int(0.572 * n0)
+    m[a:b, :] = 0
+    m[:, a:b] = 0
+    z = torch.randint(0, n0, (250,), generator=gen, device="cuda")
+    m[z, :] = 0
+    m[:, z] = 0
+    from tadpole_amd import multi
+    outs = []
+    for v in (1, 8):
+        multi.set_virtual_shards(v)
+        try:
+            outs.append(tp.TADpole(m.clone(), max_pcs=200, centromere_search=True, sharded=True))
+        finally:
+            multi.set_virtual_shards(1)
+    del m
+    torch.cuda.empty_cache()
+    g1, g8 = outs
+    assert np.array_equal(g1.merging_arms, g8.merging_arms)
+    for arm in ("p", "q"):
+        x, y = getattr(g1, arm), getattr(g8, arm)
+        assert (x.n_pcs, x.optimal_n_clusters) == (y.n_pcs, y.optimal_n_clusters)
+        assert np.array_equal(x.scores.view(np.uint64), y.scores.view(np.uint64))
+        assert np.array_equal(x.dendro.boundary, y.dendro.boundary)
+        assert np.array_equal(x.dendro.height.view(np.uint64), y.dendro.height.view(np.uint64))
+        assert x.timings_ms[13] <= 1e-11 and y.timings_ms[13] <= 1e-11
+        _nested(x.clusters)
+        print(f"C5 arm {arm}: n={int(x.timings_ms[14])} n_pcs={x.n_pcs} k*={x.optimal_n_clusters} "
+              f"pca resid {x.timings_ms[13]:.1e}")
+    c = g1.merging_arms
+    # bug-compatible: the q arm keeps its bad bins AND re-inserts them as zeros
+    # (duplicate names, R/TADpole.R:78-80,413-423), so coordinates may run past N0
+    assert np.all(c[:, 0] <= c[:, 1]) and np.all(c[1:, 0] > c[:-1, 1])

@@ -247,8 +247,11 @@ def test_coniss_bit_exact(gpu, n, c, seed):
     ma, mb, co, he = O.coniss(p)
     assert np.array_equal(bnd, mb)
     assert np.array_equal(h, he)               # canonical order: bit-identical
-    # hclust encoding is consistent with the boundary order
-    assert merge.shape == (n - 1, 2)
+    # hclust merge matrix (R/TADpole.R:465; cutree / ggdendro consume it)
+    assert np.array_equal(merge, O.hclust_merge(ma, mb, n))
+    # cutree from merge + height alone reproduces every cut's segments
+    for kk in sorted({1, 2, min(n, 3), min(n, 7), n // 2 or 1, n}):
+        assert np.array_equal(O.hclust_cutree(merge, n, kk), O.cutree_labels(mb, n, kk)), kk
 
 
 def test_coniss_ties_leftmost(gpu):
@@ -441,6 +444,22 @@ def test_xtx_int8_exact(gpu, n, maxv, slices):
     assert st64 == 0
     assert np.max(np.abs(S64 - ref) / np.maximum(ref, 1)) < 1e-13
     print(f"xtx n={n} slices={ns}: int8 {ms * 1e3:.1f} us, fp64 {ms64 * 1e3:.1f} us")
+
+
+@pytest.mark.parametrize("n,maxv", [(515, 16000), (1100, 9000), (1100, 120)])
+def test_xtx_int8_exact_fresh_context(gpu, n, maxv):
+    """Regression for the out-of-bounds slice reads fixed in 5295f4f (64-tile
+    int8 X'X kernel: slice tiles counted from the padded k stride; it faulted
+    only when the scratch was exactly sized).  tp_shutdown() frees every
+    context, so this call runs with freshly allocated, exactly sized scratch
+    at ragged n (not a multiple of 64)."""
+    gpu.tp_shutdown()
+    rng = np.random.default_rng(n * 7 + maxv)
+    x = rng.integers(0, maxv, size=(n, n)).astype(np.float64)
+    S, ns, _, st = _xtx(gpu, x, 1)
+    assert st == 0 and ns >= 1
+    xi = x.astype(np.int64)
+    assert np.array_equal(S, (xi.T @ xi).astype(np.float64))
 
 
 def test_xtx_int8_rejects_non_counts(gpu):

@@ -38,7 +38,7 @@ def test_assembly_matches_oracle_on_golden(name):
     n = len(good1)
     res = dict(good=good1, merge=np.zeros((n - 1, 2), np.int32), height=g["height"], boundary=g["merge_b"] + 1,
                n_pcs=int(g["n_pcs"]), n_clusters=int(g["optimal_n_clusters"]), scores=g["scores"],
-               timings=np.zeros(16))
+               timings=np.zeros(32))
     t = api._assemble(res, np.flatnonzero(bad) + 1)
     coords = np.concatenate([np.c_[np.full(len(t.clusters[q]), int(q)), t.clusters[q]]
                              for q in sorted(t.clusters, key=int)])
@@ -66,7 +66,7 @@ def test_vectorised_assembly_equals_literal_rle(seed):
     scores = np.full((3, n - 1), np.nan)
     scores[1, rng.choice(n - 1, size=min(n - 1, 7), replace=False)] = 1.0
     res = dict(good=good1, merge=np.zeros((n - 1, 2), np.int32), height=np.arange(n - 1, dtype=float),
-               boundary=mb + 1, n_pcs=2, n_clusters=2, scores=scores, timings=np.zeros(16))
+               boundary=mb + 1, n_pcs=2, n_clusters=2, scores=scores, timings=np.zeros(32))
     for b in (bad1, None):
         fast = api._assemble(res, b)
         slow = api._assemble_rle(api.Tadpole(), fast.dendro, np.flatnonzero(~np.isnan(scores[1])) + 1, good1, b)

@@ -8,7 +8,7 @@ fatal() { [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; }
 timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 400 python bench.py --steps 10 --warmup 2 --cpu-reps 1 > gpurun_out/bench.log 2>&1
+timeout -k 10 400 python bench.py --steps 10 --warmup 2  > gpurun_out/bench.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -1 gpurun_out/bench.log | cut -c1-1800
 [ $rc -eq 0 ] || exit $rc
 if [ -n "$DIAG" ]; then
@@ -17,6 +17,6 @@ if [ -n "$DIAG" ]; then
   fatal $rc && exit $rc
 fi
 if [ -n "$PROF" ]; then
-  ./gpu_prof.sh; exit $?
+  ./tools/gpu_prof.sh; exit $?
 fi
 exit 0

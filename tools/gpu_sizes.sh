@@ -9,7 +9,7 @@ if [ -z "$NOTEST" ]; then
   rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_gpu.log
   [ $rc -eq 0 ] || exit $rc
 fi
-for cfg in "7808 3 1 --streams 1" "10000 3 1 --streams 1" "24300 2 1 --sharded" "7808 8 1 --streams 4"; do
+for cfg in "7808 3 1 --throughput-streams 0" "10000 3 1 --throughput-streams 0" "24300 2 1 --sharded" "7808 8 1 --throughput-streams 4"; do
   set -- $cfg
   timeout -k 10 400 python bench.py --n0 $1 --steps $2 --warmup $3 $4 $5 --no-cpu-baseline > gpurun_out/bench_$1_$2.log 2>&1
   rc=$?; echo "bench $cfg rc=$rc"; tail -1 gpurun_out/bench_$1_$2.log | grep -o '"value": [0-9.]*\|"ms_per_step": [0-9.]*\|"single_stream_ms_per_matrix": [0-9.a-z]*'; tail -1 gpurun_out/bench_$1_$2.log | grep -o '"stages_ms[^}]*}'
