@@ -70,6 +70,21 @@ void *Ctx::pinned(size_t b) {
     return host_pinned;
 }
 
+hipStream_t side_fork(Ctx &c) {
+    if (!c.side) {
+        TP_HIP(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
+        TP_HIP(hipEventCreateWithFlags(&c.fork_ev, hipEventDisableTiming));
+        TP_HIP(hipEventCreateWithFlags(&c.join_ev, hipEventDisableTiming));
+    }
+    TP_HIP(hipEventRecord(c.fork_ev, c.cur));
+    TP_HIP(hipStreamWaitEvent(c.side, c.fork_ev, 0));
+    return c.side;
+}
+void side_join(Ctx &c) {
+    TP_HIP(hipEventRecord(c.join_ev, c.side));
+    TP_HIP(hipStreamWaitEvent(c.cur, c.join_ev, 0));
+}
+
 static hipEvent_t next_event(Ctx &c) {
     if (c.evnext == c.evpool.size()) {
         hipEvent_t e;
@@ -158,6 +173,12 @@ static void free_ctx(Ctx *c) {
     c->pinned_flag.release();
     if (c->host_pinned) (void)hipHostFree(c->host_pinned);
     if (c->blas) rocblas_destroy_handle((rocblas_handle)c->blas);
+    if (c->side) {
+        (void)hipStreamSynchronize(c->side);
+        (void)hipStreamDestroy(c->side);
+        (void)hipEventDestroy(c->fork_ev);
+        (void)hipEventDestroy(c->join_ev);
+    }
     if (c->owns_stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1240,6 +1261,7 @@ void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
         case 8: p = &g_pca_krylov_min; break;
         case 9: p = &g_pca_krylov_block; break;
         case 10: p = &g_pca_krylov_steps; break;
+        
         default: fail(TP_ERR_ARG, "unknown knob");
         }
         if (*which == 3 && *value != 16 && *value != 32) fail(TP_ERR_ARG, "stage depth must be 16 or 32");

@@ -61,6 +61,8 @@ struct Ctx {
     bool owns_stream = false;
     void *blas = nullptr;           // rocblas_handle of this context (lazily created)
     hipStream_t cur = nullptr;      // stream used by the current call
+    hipStream_t side = nullptr;     // fork-join helper stream (side_stream())
+    hipEvent_t fork_ev = nullptr, join_ev = nullptr;
     DevBuf buf[32];
     DevBuf pinned_flag;
     void *host_pinned = nullptr;    // small pinned staging area
@@ -71,6 +73,10 @@ struct Ctx {
 // device context; a non-null stream other than the library's selects that
 // stream's own context (scratch buffers), so streams can run concurrently
 Ctx &ctx_for(int device, hipStream_t stream = nullptr);
+// a second stream of this context for work that overlaps the current stream's
+// (fork: side waits for cur's work so far; join: cur waits for side's)
+hipStream_t side_fork(Ctx &c);
+void side_join(Ctx &c);
 void kprof_begin(Ctx &c, int cls);
 void kprof_end(Ctx &c, int cls);
 void kprof_collect(Ctx &c, double *ms_per_class, int *count_per_class);

@@ -150,7 +150,7 @@ __global__ void k_sub(double *W, const double *U, size_t cnt) {
 // vectors, descending; h_theta: ascending Ritz values of the last Rayleigh-Ritz
 // problem.  Scratch: S_Q S_Z S_SWEEP S_SWEEP2 S_SMALL S_MISC (+ S_PARTIAL).
 static void subspace_topk(Ctx &c, const double *A, int n, int k, const Prod &prod, double *V,
-                          std::vector<double> &h_theta, PcaStats &st, uint64_t seed) {
+                          std::vector<double> &h_theta, PcaStats &st, uint64_t seed, int margin = 0) {
     hipStream_t s = c.cur;
     const int over = std::max(32, k / 4);
     int b = std::min(n, ((k + over + 31) / 32) * 32);
@@ -265,7 +265,7 @@ static void subspace_topk(Ctx &c, const double *A, int n, int k, const Prod &pro
             cut = 0.0;
         }
         st.rate = gk > 1 ? 1.0 / gk : 0.9;
-        int need = (int)std::ceil(std::log(1.0 / target) / std::log(std::max(gk, 1.0005))) + g_pca_margin;
+        int need = (int)std::ceil(std::log(1.0 / target) / std::log(std::max(gk, 1.0005))) + g_pca_margin + margin;
         need = std::min(need, max_deg);
         if (cut > 0) {
             // Block degrees double: after total degree D the j-th column's
@@ -447,7 +447,11 @@ static void krylov_topk(Ctx &c, const double *Xc, const double *XcT, int n, int 
             g.splitk = 0;
             gemm_f64(g, c.buf[S_PARTIAL], s);
         };
-        subspace_topk(c, Tm, D, k, tprod, Vs, h_theta, sst, 0x5EEDULL + (uint64_t)D);
+        // +8 planned degrees: a product with T costs ~1.5 % of a Rayleigh-Ritz
+        // round (one-workgroup tridiagonalisation) that a miss of the residual
+        // check would add, and the spectrum estimate from four power steps on
+        // T plans short (C3: 31 planned, 39 needed)
+        subspace_topk(c, Tm, D, k, tprod, Vs, h_theta, sst, 0x5EEDULL + (uint64_t)D, 8);
         // V = K Y, G V = (G K) Y; residuals in the n-dimensional space
         GemmArgs vg{n, k, D, K, n, false, Vs, D, V, n};
         vg.splitk = 0;

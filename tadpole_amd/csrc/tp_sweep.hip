@@ -169,7 +169,8 @@ __device__ __forceinline__ double ward_part(const double (&sa)[NS], double fa, c
 // three candidates are described in A's registers before X, so after X A only
 // chooses.  Every lane of the writing wave writes the same value.
 template <bool STAMPS, int NS, int BS, bool GLB>
-__device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, double *lds) {
+__device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, double *lds, double *mb_d,
+                                             int4 *mb_i) {
     long long st_acc[6] = {0, 0, 0, 0, 0, 0};
     long long st_t0 = STAMPS ? (long long)__builtin_amdgcn_s_memtime() : 0;
 #define TP_STAMP(ph)                                                      \
@@ -192,11 +193,14 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
     double *cost = GLB ? cost0 + (size_t)ti * nbk * 64 : lds;
     int *link = GLB ? (int *)(cost0 + (size_t)sd.ntrees * nbk * 64) + (size_t)ti * 2 * n : (int *)(cost + nbk * 64);
     int *rn = link + n;
-    // mailbox (16-byte aligned): mbd[0..1] = cl, cr (B -> A), mbd[2] = next cost;
-    // rec = next merge (A -> B after X), pre = a2's row starts (A -> B before X)
-    double *mbd = GLB ? lds : (double *)(((uintptr_t)(rn + n) + 15) & ~(uintptr_t)15);
-    int4 *rec4 = (int4 *)(mbd + 4);   // 3 x int4: a, b, ls, r | nm, nl, nr, lls | rrs, which, -, -
-    int4 *pre4 = rec4 + 3;            // 2 x int4: a2s, b2s, l2s, r2s | ls2, r2, -, -
+    // mailbox (static LDS, so every access is a ds_ op that waits on lgkmcnt
+    // only: a generic pointer here made each access a flat_ op whose wait also
+    // drained the prefetched row loads): mbd[0..1] = cl, cr (B -> A), mbd[2] =
+    // next cost; rec = next merge (A -> B after X), pre = a2's row starts
+    // (A -> B before X)
+    double *mbd = mb_d;
+    int4 *rec4 = mb_i;      // 3 x int4: a, b, ls, r | nm, nl, nr, lls | rrs, which, -, -
+    int4 *pre4 = mb_i + 3;  // 2 x int4: a2s, b2s, l2s, r2s | ls2, r2, -, -
     double *S = sd.sums + sums_off(n, sd.tree0, i) + lane;
     int *mrg_a = sd.mrg_a + (size_t)ti * (n - 1);
     int *mrg_b = sd.mrg_b + (size_t)ti * (n - 1);
@@ -468,12 +472,14 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
 template <bool STAMPS, int BS, bool GLB>
 __global__ void __launch_bounds__(128) k_coniss_t(SweepDev sd, double *cost0) {
     extern __shared__ double lds[];
+    __shared__ double mb_d[4];
+    __shared__ int4 mb_i[5];
     const int i = sd.tree0 + blockIdx.x + 1;
     switch ((i + 63) / 64) {
-        case 1: coniss_tree2<STAMPS, 1, BS, GLB>(sd, cost0, lds); break;
-        case 2: coniss_tree2<STAMPS, 2, BS, GLB>(sd, cost0, lds); break;
-        case 3: coniss_tree2<STAMPS, 3, BS, GLB>(sd, cost0, lds); break;
-        default: coniss_tree2<STAMPS, 4, BS, GLB>(sd, cost0, lds); break;
+        case 1: coniss_tree2<STAMPS, 1, BS, GLB>(sd, cost0, lds, mb_d, mb_i); break;
+        case 2: coniss_tree2<STAMPS, 2, BS, GLB>(sd, cost0, lds, mb_d, mb_i); break;
+        case 3: coniss_tree2<STAMPS, 3, BS, GLB>(sd, cost0, lds, mb_d, mb_i); break;
+        default: coniss_tree2<STAMPS, 4, BS, GLB>(sd, cost0, lds, mb_d, mb_i); break;
     }
 }
 template __global__ void k_coniss_t<false, 1, false>(SweepDev, double *);
@@ -888,13 +894,13 @@ __global__ void k_fill(double *p, size_t cnt, double v) {
     if (t < cnt) p[t] = v;
 }
 
-static size_t coniss_lds_bytes(int n) {   // costs, links, right ends, mailbox
+static size_t coniss_lds_bytes(int n) {   // costs, links, right ends (the mailbox is static LDS)
     size_t nbk = (n + 63) / 64;
-    return nbk * 64 * 8 + (size_t)n * 8 + 16 + 32 + 5 * 16;
+    return nbk * 64 * 8 + (size_t)n * 8;
 }
-constexpr size_t kConissGlbLds = 16 + 32 + 5 * 16;   // mailbox only
+constexpr size_t kConissGlbLds = 16;   // nothing: the mailbox is static LDS
 constexpr int kConissMaxN = 64 * 64 * 16;             // global variant: 16 block-minimum slots
-static bool coniss_in_lds(int n) { return coniss_lds_bytes(n) <= 160 * 1024 && n <= 64 * 64 * 3; }
+static bool coniss_in_lds(int n) { return coniss_lds_bytes(n) <= 160 * 1024 - 256 && n <= 64 * 64 * 3; }   // 256: static mailbox
 
 // seed kernel + CONISS (cost0 = initial adjacent costs, ntrees x nbk*64, then
 // the global-variant link scratch: see sweep_cost0_doubles)
@@ -939,11 +945,12 @@ void launch_sweep(const SweepDev &sd, hipStream_t s, Ctx *prof) {
     }
     hipLaunchKernelGGL(k_fill, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, sd.scores, cnt, na);
     TP_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_trS, dim3(1), dim3(256), 0, s, sd.Pt, sd.n, sd.ldp, sd.k, sd.trS);
+    hipStream_t ts = prof ? side_fork(*prof) : s;
+    hipLaunchKernelGGL(k_trS, dim3(1), dim3(256), 0, ts, sd.Pt, sd.n, sd.ldp, sd.k, sd.trS);
     TP_HIP(hipGetLastError());
-    trace_mark(s, "trS");
     run_coniss(sd, s, false, prof);
-    trace_mark(s, "coniss");
+    if (prof) side_join(*prof);
+    trace_mark(s, "coniss + trS");
     if (prof) kprof_begin(*prof, K_CH);
     if (sd.hkeys) {
         TP_HIP(hipMemsetAsync(sd.hkeys, 0xFF, (size_t)sd.hcap * sizeof(unsigned long long), s));
