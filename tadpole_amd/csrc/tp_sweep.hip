@@ -67,6 +67,21 @@ __device__ __forceinline__ double nan2inf(double x) { return isnan(x) ? __longlo
 // Synchronisation: the workgroup is one wave.  Every lane writes the same value
 // to each shared LDS word it updates, so no barrier is needed in the loop.
 
+// four wave minima interleaved (independent DPP chains), broadcast (lane 63)
+__device__ __forceinline__ void wave_min4(double &a, double &b, double &c, double &d) {
+#define TP_MIN4(ctl)                    \
+    a = vmin(a, dpp_d<ctl>(a));         \
+    b = vmin(b, dpp_d<ctl>(b));         \
+    c = vmin(c, dpp_d<ctl>(c));         \
+    d = vmin(d, dpp_d<ctl>(d));
+    TP_MIN4(0xB1) TP_MIN4(0x4E) TP_MIN4(0x141) TP_MIN4(0x140) TP_MIN4(0x142) TP_MIN4(0x143)
+#undef TP_MIN4
+    a = readlane_d(a, 63);
+    b = readlane_d(b, 63);
+    c = readlane_d(c, 63);
+    d = readlane_d(d, 63);
+}
+
 // two canonical wave sums interleaved (independent chains, same bits as wave_sum)
 __device__ __forceinline__ void wave_sum2(double &u, double &v) {
     u = u + dpp_d<0xB1>(u);
@@ -171,7 +186,7 @@ __device__ __forceinline__ double ward_part(const double (&sa)[NS], double fa, c
 template <bool STAMPS, int NS, int BS, bool GLB>
 __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, double *lds, double *mb_d,
                                              int4 *mb_i) {
-    long long st_acc[6] = {0, 0, 0, 0, 0, 0};
+    long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     long long st_t0 = STAMPS ? (long long)__builtin_amdgcn_s_memtime() : 0;
 #define TP_STAMP(ph)                                                      \
     if (STAMPS) {                                                         \
@@ -247,12 +262,23 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
         m.ll = m.ls > 0 ? link[m.ls - 1] : -1;
         return m;
     };
-    auto publish = [&](const Mg &m, int which) {   // A -> B: the next merge
+    struct Rec {
+        int4 x, y, z;
+    };
+    auto make_rec = [&](const Mg &m, int which) {   // A -> B: the record of a next merge
         const int rr = (m.r >= 0 && m.er + 1 < n) ? m.er + 1 : -1;
-        rec4[0] = make_int4(m.a, m.ea + 1 < n ? m.ea + 1 : m.a, m.ls, m.r);
-        rec4[1] = make_int4(m.eb - m.a + 1, m.ls >= 0 ? m.a - m.ls : 0, m.r >= 0 ? m.er - m.r + 1 : 0,
-                            m.ll >= 0 ? m.ll : m.a);
-        rec4[2] = make_int4(rr >= 0 ? rr : m.a, which, 0, 0);
+        Rec rc;
+        rc.x = make_int4(m.a, m.ea + 1 < n ? m.ea + 1 : m.a, m.ls, m.r);
+        rc.y = make_int4(m.eb - m.a + 1, m.ls >= 0 ? m.a - m.ls : 0, m.r >= 0 ? m.er - m.r + 1 : 0,
+                         m.ll >= 0 ? m.ll : m.a);
+        rc.z = make_int4(rr >= 0 ? rr : m.a, which, 0, 0);
+        return rc;
+    };
+    auto publish = [&](const Mg &m, int which) {
+        const Rec rc = make_rec(m, which);
+        rec4[0] = rc.x;
+        rec4[1] = rc.y;
+        rec4[2] = rc.z;
     };
     Mg cur = {0, 0, 0, -1, -1, -1, -1};
     double c = 0.0, pcl = QNAN, pcr = QNAN;
@@ -316,29 +342,60 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
                 cost[ls] = QNAN;
                 rn[ls] = eb;
             }
+            // links the two candidate merges next to m need (independent of a2:
+            // issued before the argmin's reductions so their latency overlaps)
+            const int m1ll = cur.ll > 0 ? link[cur.ll - 1] : -1;
+            const int m2er = (r >= 0 && er + 1 < n) ? rn[r] : -1;
+            // refresh the three touched blocks and, concurrently, the minimum of
+            // the untouched ones: four interleaved wave reductions, no second
+            // (dependent) reduction for the global minimum
             const int ba = a >> 6, bb = b >> 6, bl = ls >= 0 ? (ls >> 6) : ba;
-            {
-                const double ma = wave_min(cost[ba * 64 + lane]);
-                const double mb = bb != ba ? wave_min(cost[bb * 64 + lane]) : ma;
-                const double ml = (bl != ba && bl != bb) ? wave_min(cost[bl * 64 + lane]) : ma;
+            const double va = cost[ba * 64 + lane];
+            const double vb = cost[bb * 64 + lane];
+            const double vl = cost[bl * 64 + lane];
+            double rest = QNAN;
 #pragma unroll
-                for (int q = 0; q < BS; ++q) {
-                    if (lane == (ba & 63) && q == (ba >> 6)) bmr[q] = ma;
-                    if (bb != ba && lane == (bb & 63) && q == (bb >> 6)) bmr[q] = mb;
-                    if (bl != ba && bl != bb && lane == (bl & 63) && q == (bl >> 6)) bmr[q] = ml;
-                }
+            for (int q = 0; q < BS; ++q) {
+                const int blk = 64 * q + lane;
+                rest = vmin(rest, (blk == ba || blk == bb || blk == bl) ? QNAN : bmr[q]);
             }
-            const double v2 = gmin();
-            const int a2 = argmin_pos(v2);
+            TP_STAMP(6);
+            double ma = va, mb = vb, ml = vl, mr = rest;
+            wave_min4(ma, mb, ml, mr);
+#pragma unroll
+            for (int q = 0; q < BS; ++q) {
+                if (lane == (ba & 63) && q == (ba >> 6)) bmr[q] = ma;
+                if (lane == (bb & 63) && q == (bb >> 6)) bmr[q] = mb;
+                if (lane == (bl & 63) && q == (bl >> 6)) bmr[q] = ml;
+            }
+            const double v2 = vmin(vmin(mr, ma), vmin(mb, ml));
+            // leftmost position holding v2: its block from the block minima; a
+            // touched block's words are already in registers
+            int a2 = -1;
+            if (!isnan(v2)) {
+                int blk = 0;
+#pragma unroll
+                for (int q = BS - 1; q >= 0; --q) {
+                    const unsigned long long m = __ballot(bmr[q] == v2);
+                    if (m) blk = 64 * q + (int)__builtin_ctzll(m);
+                }
+                double vv;
+                if (blk == ba) vv = va;
+                else if (blk == bb) vv = vb;
+                else if (blk == bl) vv = vl;
+                else vv = cost[blk * 64 + lane];
+                a2 = blk * 64 + (int)__builtin_ctzll(__ballot(vv == v2));
+            }
+            TP_STAMP(7);
             // ---- the three possible next merges (post-update links)
             const Mg m0 = merge_at(a2 >= 0 ? a2 : a);
             Mg m1;   // ls | m
             m1.a = ls; m1.ea = a - 1; m1.eb = eb; m1.ls = cur.ll; m1.r = r; m1.er = er;
-            m1.ll = m1.ls > 0 ? link[m1.ls - 1] : -1;
+            m1.ll = m1ll;
             Mg m2;   // m | r
             m2.a = a; m2.ea = eb; m2.eb = er; m2.ls = ls;
             m2.r = (r >= 0 && er + 1 < n) ? er + 1 : -1;
-            m2.er = m2.r >= 0 ? rn[r] : -1;
+            m2.er = m2er;
             m2.ll = cur.ll;
             pre4[0] = make_int4(m0.a, m0.ea + 1 < n ? m0.ea + 1 : a, m0.ls >= 0 ? m0.ls : a, m0.r >= 0 ? m0.r : a);
             pre4[1] = make_int4(m0.ls, m0.r, 0, 0);
@@ -352,7 +409,15 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
             int which = 0;
             if (ls >= 0 && (np < 0 || cl < nv || (cl == nv && ls < np))) { nv = cl; np = ls; which = 1; }
             if (r >= 0 && (np < 0 || cr < nv || (cr == nv && a < np))) { nv = cr; np = a; which = 2; }
-            cur = which == 0 ? m0 : (which == 1 ? m1 : m2);
+            // field by field (a select of whole structs goes through scratch)
+            auto sel = [&](int x0, int x1, int x2) { return which == 0 ? x0 : (which == 1 ? x1 : x2); };
+            cur.a = sel(m0.a, m1.a, m2.a);
+            cur.ea = sel(m0.ea, m1.ea, m2.ea);
+            cur.eb = sel(m0.eb, m1.eb, m2.eb);
+            cur.ls = sel(m0.ls, m1.ls, m2.ls);
+            cur.r = sel(m0.r, m1.r, m2.r);
+            cur.er = sel(m0.er, m1.er, m2.er);
+            cur.ll = sel(m0.ll, m1.ll, m2.ll);
             c = nv;
             publish(cur, which);
             mbd[2] = nv;
@@ -464,7 +529,7 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
     }
     TP_STAMP(5);
     if (STAMPS && threadIdx.x == 0)
-        for (int q = 0; q < 6; ++q) sd.stamps[(size_t)ti * 8 + q] = st_acc[q];
+        for (int q = 0; q < 8; ++q) sd.stamps[(size_t)ti * 8 + q] = st_acc[q];
 #undef TP_STAMP
 }
 

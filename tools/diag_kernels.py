@@ -48,13 +48,14 @@ def coniss(n0=2000, k=200):
     L.tp_debug_coniss_stamps(p.ctypes.data_as(D), B(ctypes.c_int(n)), B(ctypes.c_int(k)),
                              stamps.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)), B(ms), B(st))
     _lib.check(st)
-    s = stamps.reshape(k, 8)[:, :6].astype(float)
-    names = ["A:mask+refresh+argmin", "A:wait X", "A:choice+links", "A:wait Y", "init", "bstick"]
+    s = stamps.reshape(k, 8).astype(float)
+    names = ["A:merge_at+records", "A:wait X", "A:choice+links", "A:wait Y", "init", "bstick",
+             "A:writes+block loads", "A:reductions+argmin"]
     print(f"coniss n={n} k={k}: kernel {ms.value:.3f} ms", flush=True)
     for i in (0, 63, 127, k - 1):
         tot = s[i].sum()
         print(f"  tree {i+1:3d}: total {tot/1e6:.2f} Mcyc; per merge " +
-              ", ".join(f"{nm} {s[i, j]/(n-1):.0f}" for j, nm in enumerate(names[:4])) +
+              ", ".join(f"{names[j]} {s[i, j]/(n-1):.0f}" for j in (6, 7, 0, 1, 2, 3)) +
               f"; init {s[i,4]/1e3:.0f} kcyc, bstick {s[i,5]/1e3:.0f} kcyc", flush=True)
 
 
