@@ -274,9 +274,17 @@ static void subspace_topk(Ctx &c, const double *A, int n, int k, const Prod &pro
             // no more than the first block of degree mdeg did.  Capped so
             // T_m(lambda_1) stays far from overflow in the Gram matrix.
             const int mcap = std::max(1, std::min(24, (int)std::floor(100.0 / std::log10(std::max(g1cap, 10.0)))));
+            // The span of a filtered block is accurate only to ~kappa eps, kappa
+            // ~ the block's amplification ratio (g1/gk)^m: a schedule ending on a
+            // long block stalls near 1e-10 (C3's small problem: planned 31
+            // degrees, 8.9e-11 after 37).  The last `tail` degrees (a factor
+            // 1e3 at the rate gk) therefore go in blocks of at most 2.
+            const int tail = std::min(need, (int)std::ceil(std::log(1e3) / std::log(std::max(gk, 1.0005))));
             int deg = 0;
             while (deg < need) {
-                const int m = std::min({need - deg, std::max(mdeg, deg + mdeg), mcap});
+                int m = std::min({need - deg, std::max(mdeg, deg + mdeg), mcap});
+                if (need - deg <= tail) m = std::min(m, std::min(2, mdeg));
+                else m = std::min(m, need - tail - deg);
                 cheb_block(m, cut);
                 deg += m;
                 ++st.blocks;
@@ -447,11 +455,10 @@ static void krylov_topk(Ctx &c, const double *Xc, const double *XcT, int n, int 
             g.splitk = 0;
             gemm_f64(g, c.buf[S_PARTIAL], s);
         };
-        // +8 planned degrees: a product with T costs ~1.5 % of a Rayleigh-Ritz
-        // round (one-workgroup tridiagonalisation) that a miss of the residual
-        // check would add, and the spectrum estimate from four power steps on
-        // T plans short (C3: 31 planned, 39 needed)
-        subspace_topk(c, Tm, D, k, tprod, Vs, h_theta, sst, 0x5EEDULL + (uint64_t)D, 8);
+        // +2 planned degrees: a product with T costs ~1.5 % of a Rayleigh-Ritz
+        // round (one-workgroup tridiagonalisation) that a near miss of the
+        // residual check would add
+        subspace_topk(c, Tm, D, k, tprod, Vs, h_theta, sst, 0x5EEDULL + (uint64_t)D, 2);
         // V = K Y, G V = (G K) Y; residuals in the n-dimensional space
         GemmArgs vg{n, k, D, K, n, false, Vs, D, V, n};
         vg.splitk = 0;
