@@ -355,7 +355,10 @@ static SweepOut run_sweep(Ctx &c, const double *d_Pt, int n, int k, int min_clus
             fail(TP_ERR_NO_BSTICK, "no broken-stick level is significant for PC prefix " + std::to_string(i + 1) +
                                        " (R: invalid 'times' argument at R/TADpole.R:115)");
     for (int r = 0; r < R; ++r)
-        if (h_err[r]) fail(TP_ERR_UNSUPPORTED, "a broken-stick cut exceeds the CH kernel's segment capacity");
+        if (h_err[r])
+            fail(TP_ERR_UNSUPPORTED,
+                 "a PC prefix has more than 1024 significant broken-stick levels: this build's CH kernel "
+                 "holds at most 1024 segments per cut (R's loop at R/TADpole.R:117-120 has no limit)");
     SweepOut o;
     o.w = *std::max_element(h_nc.begin(), h_nc.end());
     if (o.w > w_cap_host) fail(TP_ERR_CAPACITY, "scores capacity (w_cap) too small: need " + std::to_string(o.w));

@@ -998,7 +998,9 @@ static void run_coniss(const SweepDev &sd, hipStream_t s, bool stamped, Ctx *pro
 }
 
 void launch_sweep(const SweepDev &sd, hipStream_t s, Ctx *prof) {
-    if (sd.k > 64 * KMAXSLOT) fail(TP_ERR_UNSUPPORTED, "max_pcs > 256 is not supported by this build");
+    if (sd.k > 64 * KMAXSLOT)
+        fail(TP_ERR_UNSUPPORTED, "min(max_pcs, n_good) > 256: this build's sweep kernels hold at most 256 PC columns "
+                                 "per lane group (R accepts any max_pcs, R/TADpole.R:344,452)");
     if (sd.n < 3) fail(TP_ERR_NO_BSTICK, "fewer than 3 good bins: no broken-stick level");
     if (sd.n > kConissMaxN) fail(TP_ERR_UNSUPPORTED, "more than 65536 bins per matrix");
     if (sd.ntrees < 1 || sd.tree0 < 0 || sd.tree0 + sd.ntrees > sd.k) fail(TP_ERR_ARG, "bad tree range");

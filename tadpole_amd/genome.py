@@ -37,7 +37,7 @@ def matrix_cost(n_bins: int) -> float:
 
 def run_genome(matrices: Mapping[str, object], sizes: Optional[Mapping[str, int]] = None,
                runner: Optional[Callable[[str, object, int], object]] = None, streams: int = 8,
-               **tadpole_kwargs) -> Tuple[Dict[str, object], Dict[str, float]]:
+               retries: int = 1, **tadpole_kwargs) -> Tuple[Dict[str, object], Dict[str, float]]:
     """Process every chromosome once across the ranks of the default process
     group (or locally when torch.distributed is not initialised).
 
@@ -45,8 +45,13 @@ def run_genome(matrices: Mapping[str, object], sizes: Optional[Mapping[str, int]
     owner of a chromosome materialises it).  sizes: name -> bins (for the
     plan; read from the arrays when absent).  runner(name, matrix, device)
     defaults to ``TADpole(matrix, device=device, **tadpole_kwargs)``.
-    Returns (results, seconds per chromosome) on rank 0 (empty dicts elsewhere
-    unless every rank asked for them).
+
+    Failure handling: a chromosome whose run raises is
+    re-queued up to ``retries`` times; the failures of all ranks are gathered
+    and re-planned (LPT) onto the OTHER ranks when there are any, one matrix at
+    a time.  What still fails afterwards raises a RuntimeError on every rank,
+    naming the chromosomes and their last errors.
+    Returns (results, seconds per chromosome) on rank 0 (empty dicts elsewhere).
     """
     import torch.distributed as dist
 
@@ -64,44 +69,80 @@ def run_genome(matrices: Mapping[str, object], sizes: Optional[Mapping[str, int]
     plan = lpt_assign({c: matrix_cost(sizes[c]) for c in matrices}, world)
     mine: Dict[str, object] = {}
     secs: Dict[str, float] = {}
+    failed: Dict[str, str] = {}
 
     def one(name, run):
         m = matrices[name]
-        if callable(m):
-            m = m()
-        t0 = time.perf_counter()
-        mine[name] = run(name, m, local)
-        secs[name] = time.perf_counter() - t0
+        try:
+            if callable(m):
+                m = m()
+            t0 = time.perf_counter()
+            mine[name] = run(name, m, local)
+            secs[name] = time.perf_counter() - t0
+            failed.pop(name, None)
+        except Exception as e:   # noqa: BLE001 -- recorded, re-queued below
+            failed[name] = f"{type(e).__name__}: {e}"
 
-    if runner is None and streams > 1 and len(plan[rank]) > 1:
-        # this rank's chromosomes, up to `streams` in flight on one GPU (one
-        # HIP stream and library context each): the latency-bound stages of a
-        # pipeline leave most CUs idle
-        import threading
-        from concurrent.futures import ThreadPoolExecutor
-
-        import torch
-
+    if runner is None:
         from .api import TADpole
-        tls = threading.local()
 
-        def run_stream(name, m, device):
-            if getattr(tls, "stream", None) is None:
-                tls.stream = torch.cuda.Stream(device=f"cuda:{device}")
-            return TADpole(m, device=device, stream=tls.stream, **tadpole_kwargs)
+        def runner(name, m, device):
+            return TADpole(m, device=device, **tadpole_kwargs)
 
-        with ThreadPoolExecutor(max_workers=streams) as ex:
-            for f in [ex.submit(one, name, run_stream) for name in plan[rank]]:
-                f.result()
+        if streams > 1 and len(plan[rank]) > 1:
+            # this rank's chromosomes, up to `streams` in flight on one GPU (one
+            # HIP stream and library context each): the latency-bound stages of
+            # a pipeline leave most CUs idle.  (Hardware queues: see
+            # tadpole_amd.use_hw_queues.)
+            import threading
+            from concurrent.futures import ThreadPoolExecutor
+
+            import torch
+            tls = threading.local()
+
+            def run_stream(name, m, device):
+                if getattr(tls, "stream", None) is None:
+                    tls.stream = torch.cuda.Stream(device=f"cuda:{device}")
+                return TADpole(m, device=device, stream=tls.stream, **tadpole_kwargs)
+
+            with ThreadPoolExecutor(max_workers=streams) as ex:
+                for f in [ex.submit(one, name, run_stream) for name in plan[rank]]:
+                    f.result()
+        else:
+            for name in plan[rank]:
+                one(name, runner)
     else:
-        if runner is None:
-            from .api import TADpole
-
-            def runner(name, m, device):
-                return TADpole(m, device=device, **tadpole_kwargs)
-
         for name in plan[rank]:
             one(name, runner)
+
+    def gather_failed():
+        if not dist_on:
+            return {c: (rank, e) for c, e in failed.items()}
+        parts = [None] * world
+        dist.all_gather_object(parts, {c: (rank, e) for c, e in failed.items()})
+        out = {}
+        for p in parts:
+            out.update(p)
+        return out
+
+    for _ in range(max(0, retries)):
+        all_failed = gather_failed()
+        if not all_failed:
+            break
+        # re-plan onto the other ranks (a rank that failed a matrix may have a
+        # bad device); alone, retry locally
+        replan = lpt_assign({c: matrix_cost(sizes[c]) for c in all_failed}, world)
+        failed.clear()   # every failure is re-owned below (and re-recorded if it fails again)
+        for w, names in enumerate(replan):
+            for name in names:
+                owner = (w + 1 + all_failed[name][0]) % world if world > 1 else 0
+                if owner == rank:
+                    one(name, runner)
+    still = gather_failed()
+    if still:
+        raise RuntimeError("chromosomes failed after %d retr%s: %s" % (
+            retries, "y" if retries == 1 else "ies",
+            "; ".join(f"{c} (rank {r}): {e}" for c, (r, e) in sorted(still.items()))))
     if not dist_on:
         return mine, secs
     gathered = [None] * world if rank == 0 else None

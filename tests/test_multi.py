@@ -80,6 +80,52 @@ def test_genome_two_ranks_gloo():
     assert got["chrA"][1:] == (r.n_pcs, r.optimal_n_clusters)
 
 
+def _flaky_worker(rank, world, port, out, always):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sizes = {"chrA": 120, "chrB": 90, "chrC": 70, "chrD": 60}
+    mats = {c: np.full((n, n), 1.0) for c, n in sizes.items()}
+
+    def runner(name, m, device):
+        # chrB fails on whichever rank first gets it (rank 1 under LPT);
+        # `always`: on every rank, every time
+        if name == "chrB" and (always or rank == 1):
+            raise RuntimeError(f"device lost on rank {rank}")
+        return (rank, m.shape[0])
+
+    try:
+        res, _ = run_genome(mats, sizes=sizes, runner=runner, retries=1)
+        msg = None
+    except RuntimeError as e:
+        res, msg = {}, str(e)
+    if rank == 0:
+        out.put((sorted(res.items()), msg))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("always", [False, True])
+def test_genome_failed_chromosome_requeued_on_other_rank(always):
+    """a chromosome that fails on one rank is re-planned onto
+    another rank; one that fails everywhere is reported by name."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_flaky_worker, args=(r, 2, port, q, always)) for r in range(2)]
+    for p in ps:
+        p.start()
+    items, msg = q.get(timeout=300)
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    if always:
+        assert msg is not None and "chrB" in msg and "device lost" in msg
+    else:
+        got = dict(items)
+        assert msg is None and sorted(got) == ["chrA", "chrB", "chrC", "chrD"]
+        assert got["chrB"] == (0, 90)          # re-run by rank 0 after rank 1 failed it
+
+
 # ------------------------------------------- one matrix over several GPUs
 # (SURVEY.md §8(e)2).  The split is host logic of the library (tp_shard_plan,
 # no device needed); the unique-id exchange runs over gloo with the library

@@ -185,3 +185,17 @@ def test_cutree_and_fix_values():
     assert list(vals) == [0, 1, 1, 1, 2, 0, 3, 0]   # interior 0 between equal labels absorbed
     c = O.coords_for(np.array([1, 1, 2, 2]), np.array([1, 2, 4, 6]), np.array([3, 5]))
     assert c.tolist() == [[1, 2], [4, 6]]        # bin 5 absorbed, bin 3 is a gap
+
+
+def test_oracle_under_asan():
+    """The C half of the oracle built with AddressSanitizer + UBSan (make -C
+    oracle asan) runs every entry point at ragged sizes without a memory or
+    UB error, and its Ward-form CONISS equals the distance-matrix definition."""
+    import os
+    import subprocess
+    here = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle")
+    subprocess.run(["make", "-s", "-C", here, "asan"], check=True)
+    r = subprocess.run([os.path.join(here, "_asan", "tp_oracle_asan")], capture_output=True, text=True,
+                       env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1"), timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "MISMATCH" not in r.stdout
