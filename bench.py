@@ -40,7 +40,8 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
-FP64_MFMA_PEAK_TFLOPS = 78.6     # MI355X FP64 matrix, dense (AMD spec; MI355X_MICROARCH.md)
+FP64_MFMA_PEAK_TFLOPS = 78.6     # MI355X FP64 matrix, dense (AMD spec)
+INT8_MFMA_PEAK_TOPS = 5000.0     # MI355X I8 MFMA, dense: 2x the BF16 rate per clock (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0            # MI355X HBM3E (MI355X_MICROARCH.md)
 METRIC = "bins/sec (NxN matrix) at 1/2/4/8 GPUs; TAD boundary bit-match vs R ref"
 
@@ -297,12 +298,15 @@ def main():
             gq_flops = share * 4.0 * n * n * p
         else:              # one record = G Q: 2 N^2 b flops
             gq_flops = share * 2.0 * n * n * block
+        ns = int(tm[18])   # int8 slices of the exact X'X (0: fp64 product)
         kern = {   # class: (ms per pipeline, bound, launches per pipeline, algorithmic work per launch, peak)
-            "xtx_gemm": (tm[5], "mfma", 1, share * float(n) ** 3, FP64_MFMA_PEAK_TFLOPS),
+            # X'X: ns^2 slice products of N^3 int8 ops each (upper tiles: N^2/2 outputs x N MACs x 2)
+            "xtx_gemm": ((tm[5], "mfma", 1, share * ns * ns * float(n) ** 3, INT8_MFMA_PEAK_TOPS) if ns else
+                         (tm[5], "mfma", 1, share * float(n) ** 3, FP64_MFMA_PEAK_TFLOPS)),
             "xcxc_gemm": (tm[6], "mfma", 1, share * float(n) ** 3, FP64_MFMA_PEAK_TFLOPS),
             "gq_gemm": (tm[7], "mfma", gq_launches, gq_flops, FP64_MFMA_PEAK_TFLOPS),
             "coniss": (tm[9], "hbm", 1, 40.0 * (n - 1) * k * (k + 1) / 2.0, HBM_PEAK_GBS),   # 5 sum rows/merge
-            "ch": (tm[10], "hbm", 1, 16.0 * n * k * k, HBM_PEAK_GBS),                        # 2 passes/tree
+            "ch": (tm[10], "hbm", 1, 16.0 * n * k, HBM_PEAK_GBS),   # the scores twice (segment statistics shared by the trees)
         }
         dom = max(kern, key=lambda q: kern[q][0])
 
@@ -310,7 +314,8 @@ def main():
             ms_tot, bound, launches, per_launch, peak = kern[q]
             avg_ms = ms_tot / launches
             if bound == "mfma":
-                return per_launch / (avg_ms * 1e-3) / 1e12, peak, "TFLOP/s", avg_ms
+                unit = "TOP/s (int8)" if (q == "xtx_gemm" and ns) else "TFLOP/s"
+                return per_launch / (avg_ms * 1e-3) / 1e12, peak, unit, avg_ms
             return per_launch / (avg_ms * 1e-3) / 1e9, peak, "GB/s", avg_ms
 
         ms_tot, bound, launches, per_launch, _ = kern[dom]
@@ -322,8 +327,12 @@ def main():
                 "launches_per_step": launches,
                 "dominance": "largest kernel-class time of one pipeline (events over the timed steps)",
                 "classes": {q: {"ms_per_step": round(kern[q][0], 4),
+                                "achieved": round(rate(q)[0], 3) if kern[q][0] > 0 else None, "unit": rate(q)[2],
                                 "frac_of_peak": round(rate(q)[0] / rate(q)[1], 5) if kern[q][0] > 0 else None}
                             for q in kern},
+                "xtx": {"int8_slices": ns,
+                        "fp64_equivalent_tflops": (round(share * float(n) ** 3 / (tm[5] * 1e-3) / 1e12, 2)
+                                                   if tm[5] > 0 else None)},
                 "stages_ms": {"mask": round(tm[0], 3), "cor": round(tm[1], 3), "pca": round(tm[2], 3),
                               "sweep": round(tm[3], 3), "total": round(tm[4], 3)},
                 "pca": {"path": "block Krylov (G never formed)" if krylov_steps else "G = Xc'Xc + subspace iteration",

@@ -513,7 +513,8 @@ static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_cl
         timings[15] = k;
         timings[16] = ps.krylov_steps;
         timings[17] = ps.krylov_dim;
-        for (int q = 18; q < 32; ++q) timings[q] = 0.0;
+        timings[18] = c.last_xtx_ns;
+        for (int q = 19; q < 32; ++q) timings[q] = 0.0;
     }
     c.prof = false;
     return o;
@@ -916,8 +917,8 @@ void tp_debug_chol(const double *W, const int *b, const double *rel, const int *
 
 /* CholQR kernels for b <= 256 on Z = I: k_chol_inv + k_trsm_frag give
  * Y = U^{-1} (W = U'U, S-scaled, + rel on the scaled diagonal); diag[b] =
- * diag(U).  ms[0] chol kernel (16 waves), ms[1] info, ms[2] chol kernel (8
- * waves), ms[3..4] stamps (prologue, factor cycles), ms[5] diag-factor cycles,
+ * diag(U).  ms[0] chol kernel (the product's choice of waves), ms[1] info,
+ * ms[2] chol kernel (16 waves), ms[3..4] stamps (prologue, factor cycles), ms[5] diag-factor cycles,
  * ms[6] trsm kernel (n = b). */
 void tp_debug_chol_inv(const double *W, const int *b, const double *rel, const int *reps, double *diag, double *Y,
                        double *ms, int *status) {
@@ -942,7 +943,7 @@ void tp_debug_chol_inv(const double *W, const int *b, const double *rel, const i
         const int R = std::max(1, *reps);
         const int keep = g_chol_inv_waves;
         for (int pass = 0; pass < 2; ++pass) {
-            g_chol_inv_waves = pass == 0 ? 16 : 8;
+            g_chol_inv_waves = pass == 0 ? 0 : 16;
             float tc = 0, tt = 0;
             for (int r = 0; r < R; ++r) {
                 TP_HIP(hipMemcpyAsync(dW, W, (size_t)B * B * 8, hipMemcpyHostToDevice, s));
@@ -985,8 +986,8 @@ void tp_debug_chol_inv(const double *W, const int *b, const double *rel, const i
     });
 }
 
-/* stamped CONISS for trees 1..k on P (n x k col-major): stamps[k * 8]
- * (cycles per phase: argmin, loads, costs, update, init, bstick), kernel ms. */
+/* stamped CONISS for trees 1..k on P (n x k col-major): stamps[k * 16]
+ * (cycles per phase, wave A 0..7 and wave B 8..15, tp_sweep.hip), kernel ms. */
 void tp_debug_coniss_stamps(const double *P, const int *n, const int *k, long long *stamps, double *ms,
                             int *status) {
     guarded(status, [&] {
@@ -1012,7 +1013,7 @@ void tp_debug_coniss_stamps(const double *P, const int *n, const int *k, long lo
         sd.cost = (double *)(((uintptr_t)(sd.mrg_b + rec) + 15) & ~(uintptr_t)15);
         sd.height = sd.cost + rec;
         sd.n_cluster = c.buf[S_MISC].as<int>(K + 64);
-        long long *dst = (long long *)c.buf[S_SCORES].as<char>((size_t)K * 8 * 8);
+        long long *dst = (long long *)c.buf[S_SCORES].as<char>((size_t)K * 16 * 8);
         sd.stamps = dst;
         sd.cost0 = c.buf[S_SMALL].as<double>(sweep_cost0_doubles(N, K));
         hipEvent_t e0, e1;
@@ -1025,7 +1026,7 @@ void tp_debug_coniss_stamps(const double *P, const int *n, const int *k, long lo
         float t = 0;
         TP_HIP(hipEventElapsedTime(&t, e0, e1));
         *ms = t;
-        TP_HIP(hipMemcpy(stamps, dst, (size_t)K * 8 * 8, hipMemcpyDeviceToHost));
+        TP_HIP(hipMemcpy(stamps, dst, (size_t)K * 16 * 8, hipMemcpyDeviceToHost));
         (void)hipEventDestroy(e0);
         (void)hipEventDestroy(e1);
     });
@@ -1264,6 +1265,7 @@ void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
         case 8: p = &g_pca_krylov_min; break;
         case 9: p = &g_pca_krylov_block; break;
         case 10: p = &g_pca_krylov_steps; break;
+        case 11: p = &g_chol_inv_waves; break;
         
         default: fail(TP_ERR_ARG, "unknown knob");
         }

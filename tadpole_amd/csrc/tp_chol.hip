@@ -370,10 +370,11 @@ __device__ __forceinline__ void ci_diag(tp_d4 &v, int l, double *Eb, bool &bad) 
     }
 }
 
-template <int CI_W>
+// CI_W waves; TMAX: the largest tile count b / 16 the instance handles
+template <int CI_W, int TMAX>
 __global__ void __launch_bounds__(64 * CI_W) k_chol_inv(double *W, double *F, double *sc, double *rdiag, int b,
                                                         double rel, int *info, long long *stamps) {
-    constexpr int CI_SLOTS = (136 + CI_W - 1) / CI_W;   // tiles per wave
+    constexpr int CI_SLOTS = (TMAX * (TMAX + 1) / 2 + CI_W - 1) / CI_W;   // tiles per wave
     // stamps (diagnostics, may be NULL): [0] prologue [1] factorisation +
     // output cycles, [4] cycles inside diagonal factors
     __shared__ unsigned long long dcyc;
@@ -394,9 +395,9 @@ __global__ void __launch_bounds__(64 * CI_W) k_chol_inv(double *W, double *F, do
         if (stamps && l == 0)                                                \
             atomicAdd(&dcyc, (unsigned long long)((long long)__builtin_amdgcn_s_memtime() - _a)); \
     }
-    __shared__ double Eb[16][4 * 64];   // E_p fragments (A-operand layout)
-    __shared__ double Pb[16][4 * 64];   // row panel of U
-    __shared__ double scl[CI_BMAX];
+    __shared__ double Eb[TMAX][4 * 64];   // E_p fragments (A-operand layout)
+    __shared__ double Pb[TMAX][4 * 64];   // row panel of U
+    __shared__ double scl[16 * TMAX];
     const int t = threadIdx.x, l = t & 63;
     const int w = __builtin_amdgcn_readfirstlane(t >> 6);
     const int T = b >> 4;
@@ -542,10 +543,11 @@ __global__ void __launch_bounds__(64 * CI_W) k_chol_inv(double *W, double *F, do
 #undef CI_DIAG
 }
 
-template __global__ void k_chol_inv<8>(double *, double *, double *, double *, int, double, int *, long long *);
-template __global__ void k_chol_inv<16>(double *, double *, double *, double *, int, double, int *, long long *);
+template __global__ void k_chol_inv<8, 16>(double *, double *, double *, double *, int, double, int *, long long *);
+template __global__ void k_chol_inv<16, 16>(double *, double *, double *, double *, int, double, int *, long long *);
+template __global__ void k_chol_inv<4, 4>(double *, double *, double *, double *, int, double, int *, long long *);
 
-int g_chol_inv_waves = 16;   // 8 or 16 (diagnostics switch)
+int g_chol_inv_waves = 0;   // 0: 4 waves for b <= 64, else 16; 4 / 8 / 16 force (diagnostics switch)
 
 // ---------------------------------------------------------------------------
 // k_trsm_frag: Q = Z U^-1 = (Z S) U'^-1 from k_chol_inv's fragments, one
@@ -625,11 +627,15 @@ __global__ void __launch_bounds__(256) k_trsm_frag(const double *__restrict__ Z,
 void launch_chol_inv(double *d_W, double *d_F, double *d_sc, double *d_rdiag, int b, double rel, int *d_info,
                      hipStream_t s, long long *d_stamps) {
     if (b % 16 != 0 || b > CI_BMAX || b < 16) fail(TP_ERR_ARG, "chol_inv: block size must be a multiple of 16, <= 256");
-    if (g_chol_inv_waves == 8)
-        hipLaunchKernelGGL(k_chol_inv<8>, dim3(1), dim3(512), 0, s, d_W, d_F, d_sc, d_rdiag, b, rel, d_info,
+    const int w = g_chol_inv_waves ? g_chol_inv_waves : (b <= 64 ? 4 : 16);
+    if (w == 4 && b <= 64)
+        hipLaunchKernelGGL((k_chol_inv<4, 4>), dim3(1), dim3(256), 0, s, d_W, d_F, d_sc, d_rdiag, b, rel, d_info,
+                           d_stamps);
+    else if (w == 8)
+        hipLaunchKernelGGL((k_chol_inv<8, 16>), dim3(1), dim3(512), 0, s, d_W, d_F, d_sc, d_rdiag, b, rel, d_info,
                            d_stamps);
     else
-        hipLaunchKernelGGL(k_chol_inv<16>, dim3(1), dim3(1024), 0, s, d_W, d_F, d_sc, d_rdiag, b, rel, d_info,
+        hipLaunchKernelGGL((k_chol_inv<16, 16>), dim3(1), dim3(1024), 0, s, d_W, d_F, d_sc, d_rdiag, b, rel, d_info,
                            d_stamps);
     TP_HIP(hipGetLastError());
 }

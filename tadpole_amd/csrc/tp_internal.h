@@ -57,6 +57,7 @@ struct Ctx {
     int open_cls = -1;
     hipEvent_t open_ev = nullptr;
     int device = 0;
+    int last_xtx_ns = 0;            // int8 slices of the last X'X product (0: fp64 MFMA product)
     hipStream_t stream = nullptr;   // library stream (or the caller's, owns_stream = false)
     bool owns_stream = false;
     void *blas = nullptr;           // rocblas_handle of this context (lazily created)
@@ -181,9 +182,16 @@ extern int g_ch_dedup;        // 0: every tree computes its own segment statisti
 extern int g_ch_dedup_ucap;   // > 0: cap on the shared store (tests of the overflow path)
 size_t sweep_dedup_bytes(int n, int k, int ntrees, int seg_cap, int *hcap, int *ucap);
 void sweep_dedup_bind(SweepDev &sd, void *base, int hcap, int ucap);
-// initial costs (ntrees x roundup(n, 64)) + link scratch of the global-memory
-// CONISS variant (ntrees x 2n ints)
-inline size_t sweep_cost0_doubles(int n, int ntrees) { return (size_t)ntrees * (((n + 63) / 64) * 64 + n); }
+// CONISS per-tree rows: roundup(n, 64) costs + 64 (a dummy slot, index
+// roundup(n, 64), that takes the branch-free writes of absent positions); link
+// and right-end arrays of n + 64 ints (dummy slot n)
+__host__ __device__ inline size_t coniss_cost_stride(int n) { return (size_t)((n + 63) / 64) * 64 + 64; }
+__host__ __device__ inline size_t coniss_link_stride(int n) { return (size_t)n + 64; }
+// initial costs (ntrees x cost stride) + link scratch of the global-memory
+// CONISS variant (ntrees x 2 link strides of ints)
+inline size_t sweep_cost0_doubles(int n, int ntrees) {
+    return (size_t)ntrees * (coniss_cost_stride(n) + coniss_link_stride(n));
+}
 size_t sweep_sums_doubles(int n, int tree0, int ntrees);
 void blas_shutdown_all();
 void launch_sweep(const SweepDev &sd, hipStream_t s, Ctx *prof = nullptr);

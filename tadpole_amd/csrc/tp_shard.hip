@@ -216,6 +216,7 @@ void sym_gemm_sharded(Ctx &c, GemmArgs g) {
 // tile columns over the shards exactly as sym_gemm_sharded.
 void xtx_product(Ctx &c, const double *X, int n, double *S) {
     const int ns = xtx_int_slices(c, X, n);
+    c.last_xtx_ns = ns;
     if (ns == 0) {
         GemmArgs g{n, n, n, X, n, true, X, n, S, n};
         g.sym_upper = true;

@@ -50,12 +50,18 @@ static __host__ __device__ inline size_t sums_off(int n, int tree0, int i) {
 }
 size_t sweep_sums_doubles(int n, int tree0, int ntrees) { return sums_off(n, tree0, tree0 + ntrees + 1); }
 
+// keeps a load unconditional (the compiler would otherwise sink a load whose
+// value is only selected under a condition into an exec-masked branch)
+__device__ __forceinline__ int pin(int x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+
 __device__ __forceinline__ double nan2inf(double x) { return isnan(x) ? __longlong_as_double(0x7FF0000000000000LL) : x; }
 
 // STAMPS: diagnostic build accumulating s_memtime cycles per merge phase into
-// sd.stamps[tree * 8 + phase] (0 mask + refresh + speculative argmin,
-// 1 links + merged sums, 2 prefetch + costs, 3 choice of the next merge,
-// 4 init, 5 bstick).  The product launches STAMPS=false.
+// sd.stamps[tree * 16 + phase]: wave A 0..7, wave B 8..15 (phase names in
+// tools/diag_kernels.py).  The product launches STAMPS=false.
 //
 // Argmin without index keys: candidate costs are never NaN (NaN -> +inf) and a
 // non-candidate position holds NaN, which v_min ignores.  The smallest value is
@@ -80,6 +86,17 @@ __device__ __forceinline__ void wave_min4(double &a, double &b, double &c, doubl
     b = readlane_d(b, 63);
     c = readlane_d(c, 63);
     d = readlane_d(d, 63);
+}
+
+// two wave minima interleaved, broadcast (lane 63)
+__device__ __forceinline__ void wave_min2(double &a, double &b) {
+#define TP_MIN2(ctl)                    \
+    a = vmin(a, dpp_d<ctl>(a));         \
+    b = vmin(b, dpp_d<ctl>(b));
+    TP_MIN2(0xB1) TP_MIN2(0x4E) TP_MIN2(0x141) TP_MIN2(0x140) TP_MIN2(0x142) TP_MIN2(0x143)
+#undef TP_MIN2
+    a = readlane_d(a, 63);
+    b = readlane_d(b, 63);
 }
 
 // two canonical wave sums interleaved (independent chains, same bits as wave_sum)
@@ -111,7 +128,7 @@ __global__ void __launch_bounds__(64) k_seed(SweepDev sd, double *cost0) {
     const int ld = slab_ld(i);
     const int lane = threadIdx.x;
     double *S = sd.sums + sums_off(n, sd.tree0, i);
-    double *c0 = cost0 + (size_t)ti * ((n + 63) / 64) * 64;
+    double *c0 = cost0 + (size_t)ti * coniss_cost_stride(n);
     const int p0 = blockIdx.y * 64;
     const double QNAN = __longlong_as_double(0x7FF8000000000000LL);
     double x[KMAXSLOT], y[KMAXSLOT];
@@ -179,10 +196,12 @@ __device__ __forceinline__ double ward_part(const double (&sa)[NS], double fa, c
 // m comes from registers) for a2; sl, sm, row(ll), sr for ls|m; sm, sr, sl,
 // row(rr) for m|r -- and the choice is applied at the next merge.
 //
-// Mailbox words in LDS: a2's row starts (A -> B before X), cl/cr (B -> A
-// before X), the chosen next merge and its cost (A -> B before barrier Y); the
-// three candidates are described in A's registers before X, so after X A only
-// chooses.  Every lane of the writing wave writes the same value.
+// Two barriers per merge.  Before X, A publishes a2's row starts and B cl and
+// cr; after X, B prefetches a2's rows while A chooses the next merge among the
+// three candidates it holds and publishes its record and cost before Y.  (One
+// barrier with both waves choosing was slower: B's prefetch of a2's rows then
+// has only B's own choice to hide behind, and HBM latency shows.)  Mailbox
+// words are written before one barrier and read after it.
 template <bool STAMPS, int NS, int BS, bool GLB>
 __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, double *lds, double *mb_d,
                                              int4 *mb_i) {
@@ -205,23 +224,25 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
     // GLB (n above the LDS capacity): costs stay in this tree's slice of cost0
     // and links in global scratch behind cost0 (L2 / MALL resident); only the
     // mailbox is in LDS.  Same code path otherwise.
-    double *cost = GLB ? cost0 + (size_t)ti * nbk * 64 : lds;
-    int *link = GLB ? (int *)(cost0 + (size_t)sd.ntrees * nbk * 64) + (size_t)ti * 2 * n : (int *)(cost + nbk * 64);
-    int *rn = link + n;
+    const size_t cst = coniss_cost_stride(n), lst = coniss_link_stride(n);
+    double *cost = GLB ? cost0 + (size_t)ti * cst : lds;
+    int *link = GLB ? (int *)(cost0 + (size_t)sd.ntrees * cst) + (size_t)ti * 2 * lst : (int *)(cost + cst);
+    int *rn = link + lst;
+    // dummy slots: branch-free code writes absent positions there (an exec-
+    // masked `if` costs ~55 cycles on the merge chain, a select ~14)
+    const int DC = nbk * 64, DL = n;
     // mailbox (static LDS, so every access is a ds_ op that waits on lgkmcnt
     // only: a generic pointer here made each access a flat_ op whose wait also
-    // drained the prefetched row loads): mbd[0..1] = cl, cr (B -> A), mbd[2] =
-    // next cost; rec = next merge (A -> B after X), pre = a2's row starts
-    // (A -> B before X)
-    double *mbd = mb_d;
-    int4 *rec4 = mb_i;      // 3 x int4: a, b, ls, r | nm, nl, nr, lls | rrs, which, -, -
-    int4 *pre4 = mb_i + 3;  // 2 x int4: a2s, b2s, l2s, r2s | ls2, r2, -, -
+    // drained the prefetched row loads): mb_d[0..1] = cl, cr (B -> A before
+    // X), mb_d[2] = the next merge's cost (A -> B before Y); mb_i[0..2] = the
+    // next merge's record (A -> B before Y), mb_i[3] = a2's row starts
+    // (a2s, b2s, ls2, r2) (A -> B before X).
     double *S = sd.sums + sums_off(n, sd.tree0, i) + lane;
     int *mrg_a = sd.mrg_a + (size_t)ti * (n - 1);
     int *mrg_b = sd.mrg_b + (size_t)ti * (n - 1);
     double *mcost = sd.cost + (size_t)ti * (n - 1);
     double *height = sd.height + (size_t)ti * (n - 1);
-    const double *c0 = cost0 + (size_t)ti * nbk * 64;
+    const double *c0 = cost0 + (size_t)ti * cst;
 
     double bmr[BS];
     auto argmin_pos = [&](double vmin) -> int {
@@ -251,15 +272,25 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
     struct Mg {
         int a, ea, eb, ls, r, er, ll;
     };
-    auto merge_at = [&](int p) {   // current links -> the merge of the pair starting at p
+    auto merge_at1 = [&](int p) {   // current links -> the pair starting at p, first level (no branches)
         Mg m;
         m.a = p;
         m.ea = link[p];
         m.eb = rn[p];
-        m.ls = p > 0 ? link[p - 1] : -1;
+        const int lsv = pin(link[p > 0 ? p - 1 : DL]);
+        m.ls = p > 0 ? lsv : -1;
         m.r = m.eb >= 0 && m.eb + 1 < n ? m.eb + 1 : -1;
-        m.er = m.r >= 0 ? rn[m.ea + 1] : -1;
-        m.ll = m.ls > 0 ? link[m.ls - 1] : -1;
+        return m;
+    };
+    auto merge_at2 = [&](Mg &m) {   // second level: the right end of r, the cluster left of ls
+        const int erv = pin(rn[m.ea + 1 < n ? m.ea + 1 : DL]);
+        const int llv = pin(link[m.ls > 0 ? m.ls - 1 : DL]);
+        m.er = m.r >= 0 ? erv : -1;
+        m.ll = m.ls > 0 ? llv : -1;
+    };
+    auto merge_at = [&](int p) {
+        Mg m = merge_at1(p);
+        merge_at2(m);
         return m;
     };
     struct Rec {
@@ -274,15 +305,19 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
         rc.z = make_int4(rr >= 0 ? rr : m.a, which, 0, 0);
         return rc;
     };
-    auto publish = [&](const Mg &m, int which) {
-        const Rec rc = make_rec(m, which);
-        rec4[0] = rc.x;
-        rec4[1] = rc.y;
-        rec4[2] = rc.z;
+    // the choice after merge (a, ls, r): the lexicographic (cost, position)
+    // minimum of (v2, a2), (cl, ls), (cr, a) -- both waves evaluate it
+    auto choose = [](int a, int ls, int r, double v2, int a2, double cl, double cr, bool &c1, bool &c2,
+                     double &nv) {
+        c1 = (ls >= 0) & ((a2 < 0) | (cl < v2) | ((cl == v2) & (ls < a2)));
+        nv = c1 ? cl : v2;
+        const int np = c1 ? ls : a2;
+        c2 = (r >= 0) & ((np < 0) | (cr < nv) | ((cr == nv) & (a < np)));
+        nv = c2 ? cr : nv;
     };
     Mg cur = {0, 0, 0, -1, -1, -1, -1};
     double c = 0.0, pcl = QNAN, pcr = QNAN;
-    int pls = -1, pa_ = 0;   // A: the previous merge's new costs, applied at the next merge's start
+    int pls = DC, pa_ = DC;   // A: where the previous merge's new costs go (applied at the next merge's start)
     if (waveA) {
 #pragma unroll
         for (int q = 0; q < BS; ++q) bmr[q] = QNAN;
@@ -294,6 +329,7 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
                 link[p] = p;
                 rn[p] = p + 1 < n ? p + 1 : -1;
             }
+            if (bk == 0) link[DL + lane] = rn[DL + lane] = -1;
             const double m = wave_min(cp);
             if (lane == (bk & 63)) {
 #pragma unroll
@@ -303,8 +339,11 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
         }
         c = gmin();
         cur = merge_at(argmin_pos(c));
-        publish(cur, 0);
-        mbd[2] = c;
+        const Rec rc = make_rec(cur, 0);
+        mb_i[0] = rc.x;
+        mb_i[1] = rc.y;
+        mb_i[2] = rc.z;
+        mb_d[2] = c;
     }
     __syncthreads();
     // B's registers
@@ -312,13 +351,13 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
     int ls2p = -1, r2p = -1, aprev = -1;
     double h = 0.0;
     if (!waveA) {
-        const int4 r0 = rec4[0];
-        load_row(pa, r0.x);
-        load_row(pb, r0.y);
-        load_row(pl, r0.z >= 0 ? r0.z : r0.x);
-        load_row(pr, r0.w >= 0 ? r0.w : r0.x);
-        ls2p = r0.z;
-        r2p = r0.w;
+        const int4 q0 = mb_i[0];
+        load_row(pa, q0.x);
+        load_row(pb, q0.y);
+        load_row(pl, q0.z >= 0 ? q0.z : q0.x);
+        load_row(pr, q0.w >= 0 ? q0.w : q0.x);
+        ls2p = q0.z;
+        r2p = q0.w;
 #pragma unroll
         for (int t = 0; t < NS; ++t) pll[t] = prr[t] = sl[t] = sr[t] = sm[t] = 0.0;
     }
@@ -329,26 +368,24 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
             // ---- the previous merge's new costs, then this merge's structure
             //      update with ls, a, b masked, refresh, speculative argmin
             const int a = cur.a, eb = cur.eb, ls = cur.ls, b = cur.ea + 1, r = cur.r, er = cur.er;
-            if (s > 0) {
-                if (pls >= 0) cost[pls] = pcl;
-                cost[pa_] = pcr;
-            }
+            // branch-free: absent positions write the dummy slots
+            cost[pls] = pcl;
+            cost[pa_] = pcr;
             link[a] = eb;
             link[eb] = a;
             rn[a] = er;
             cost[b] = QNAN;
             cost[a] = QNAN;
-            if (ls >= 0) {
-                cost[ls] = QNAN;
-                rn[ls] = eb;
-            }
+            cost[ls >= 0 ? ls : DC] = QNAN;
+            rn[ls >= 0 ? ls : DL] = eb;
             // links the two candidate merges next to m need (independent of a2:
             // issued before the argmin's reductions so their latency overlaps)
-            const int m1ll = cur.ll > 0 ? link[cur.ll - 1] : -1;
-            const int m2er = (r >= 0 && er + 1 < n) ? rn[r] : -1;
+            const int m1llv = pin(link[cur.ll > 0 ? cur.ll - 1 : DL]);
+            const int m2erv = pin(rn[r >= 0 ? r : DL]);
+            const int m1ll = cur.ll > 0 ? m1llv : -1;
+            const int m2er = (r >= 0 && er + 1 < n) ? m2erv : -1;
             // refresh the three touched blocks and, concurrently, the minimum of
-            // the untouched ones: four interleaved wave reductions, no second
-            // (dependent) reduction for the global minimum
+            // the untouched ones: four interleaved wave reductions
             const int ba = a >> 6, bb = b >> 6, bl = ls >= 0 ? (ls >> 6) : ba;
             const double va = cost[ba * 64 + lane];
             const double vb = cost[bb * 64 + lane];
@@ -364,31 +401,27 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
             wave_min4(ma, mb, ml, mr);
 #pragma unroll
             for (int q = 0; q < BS; ++q) {
-                if (lane == (ba & 63) && q == (ba >> 6)) bmr[q] = ma;
-                if (lane == (bb & 63) && q == (bb >> 6)) bmr[q] = mb;
-                if (lane == (bl & 63) && q == (bl >> 6)) bmr[q] = ml;
+                bmr[q] = (lane == (ba & 63) && q == (ba >> 6)) ? ma : bmr[q];
+                bmr[q] = (lane == (bb & 63) && q == (bb >> 6)) ? mb : bmr[q];
+                bmr[q] = (lane == (bl & 63) && q == (bl >> 6)) ? ml : bmr[q];
             }
             const double v2 = vmin(vmin(mr, ma), vmin(mb, ml));
-            // leftmost position holding v2: its block from the block minima; a
-            // touched block's words are already in registers
-            int a2 = -1;
-            if (!isnan(v2)) {
-                int blk = 0;
+            // leftmost position holding v2: its block from the block minima, then
+            // the block's words (v2 NaN: no ballot matches, a2 = -1)
+            int blk = 0;
 #pragma unroll
-                for (int q = BS - 1; q >= 0; --q) {
-                    const unsigned long long m = __ballot(bmr[q] == v2);
-                    if (m) blk = 64 * q + (int)__builtin_ctzll(m);
-                }
-                double vv;
-                if (blk == ba) vv = va;
-                else if (blk == bb) vv = vb;
-                else if (blk == bl) vv = vl;
-                else vv = cost[blk * 64 + lane];
-                a2 = blk * 64 + (int)__builtin_ctzll(__ballot(vv == v2));
+            for (int q = BS - 1; q >= 0; --q) {
+                const unsigned long long m = __ballot(bmr[q] == v2);
+                blk = m ? 64 * q + (int)__builtin_ctzll(m) : blk;
             }
+            const unsigned long long mv = __ballot(cost[blk * 64 + lane] == v2);
+            const int a2 = mv ? blk * 64 + (int)__builtin_ctzll(mv) : -1;
             TP_STAMP(7);
-            // ---- the three possible next merges (post-update links)
-            const Mg m0 = merge_at(a2 >= 0 ? a2 : a);
+            // ---- the three possible next merges (post-update links); a2's
+            //      clusters go to B at once (its row prefetch starts before X)
+            Mg m0 = merge_at1(a2 >= 0 ? a2 : a);
+            mb_i[3] = make_int4(m0.a, m0.ea + 1 < n ? m0.ea + 1 : m0.a, m0.ls, m0.r);
+            merge_at2(m0);
             Mg m1;   // ls | m
             m1.a = ls; m1.ea = a - 1; m1.eb = eb; m1.ls = cur.ll; m1.r = r; m1.er = er;
             m1.ll = m1ll;
@@ -397,20 +430,16 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
             m2.r = (r >= 0 && er + 1 < n) ? er + 1 : -1;
             m2.er = m2er;
             m2.ll = cur.ll;
-            pre4[0] = make_int4(m0.a, m0.ea + 1 < n ? m0.ea + 1 : a, m0.ls >= 0 ? m0.ls : a, m0.r >= 0 ? m0.r : a);
-            pre4[1] = make_int4(m0.ls, m0.r, 0, 0);
             TP_STAMP(0);
             __syncthreads();   // X
             TP_STAMP(1);
-            // ---- the choice: lexicographic (cost, position) minimum
-            const double cl = mbd[0], cr = mbd[1];
-            double nv = v2;
-            int np = a2;
-            int which = 0;
-            if (ls >= 0 && (np < 0 || cl < nv || (cl == nv && ls < np))) { nv = cl; np = ls; which = 1; }
-            if (r >= 0 && (np < 0 || cr < nv || (cr == nv && a < np))) { nv = cr; np = a; which = 2; }
+            // ---- the choice
+            const double cl = mb_d[0], cr = mb_d[1];
+            bool c1, c2;
+            double nv;
+            choose(a, ls, r, v2, a2, cl, cr, c1, c2, nv);
             // field by field (a select of whole structs goes through scratch)
-            auto sel = [&](int x0, int x1, int x2) { return which == 0 ? x0 : (which == 1 ? x1 : x2); };
+            auto sel = [&](int x0, int x1, int x2) { return c2 ? x2 : (c1 ? x1 : x0); };
             cur.a = sel(m0.a, m1.a, m2.a);
             cur.ea = sel(m0.ea, m1.ea, m2.ea);
             cur.eb = sel(m0.eb, m1.eb, m2.eb);
@@ -419,29 +448,37 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
             cur.er = sel(m0.er, m1.er, m2.er);
             cur.ll = sel(m0.ll, m1.ll, m2.ll);
             c = nv;
-            publish(cur, which);
-            mbd[2] = nv;
+            {
+                const Rec rc = make_rec(cur, c2 ? 2 : (c1 ? 1 : 0));
+                mb_i[0] = rc.x;
+                mb_i[1] = rc.y;
+                mb_i[2] = rc.z;
+                mb_d[2] = nv;
+            }
             // block minima absorb the new costs now (the LDS words follow at the
             // next merge's start, before its refresh reads them)
 #pragma unroll
             for (int q = 0; q < BS; ++q) {
-                if (lane == (ba & 63) && q == (ba >> 6)) bmr[q] = vmin(bmr[q], cr);
-                if (ls >= 0 && lane == (bl & 63) && q == (bl >> 6)) bmr[q] = vmin(bmr[q], cl);
+                const double tr = vmin(bmr[q], cr);
+                bmr[q] = (lane == (ba & 63) && q == (ba >> 6)) ? tr : bmr[q];
+                const double tl = vmin(bmr[q], cl);
+                bmr[q] = (ls >= 0 && lane == (bl & 63) && q == (bl >> 6)) ? tl : bmr[q];
             }
             pcl = cl;
             pcr = cr;
-            pls = ls;
+            pls = ls >= 0 ? ls : DC;
             pa_ = a;
             TP_STAMP(2);
             __syncthreads();   // Y
             TP_STAMP(3);
         } else {
             // ---- this merge's rows from the previous merge's prefetch
-            const int4 q0 = rec4[0], q1 = rec4[1], q2 = rec4[2];
+            const int4 q0 = mb_i[0], q1 = mb_i[1], q2 = mb_i[2];
+            const double cc = mb_d[2];
             const int a_ = q0.x, b_ = q0.y, ls_ = q0.z, r_ = q0.w;
             const int nm = q1.x, nl = q1.y, nr = q1.z, lls = q1.w;
             const int rrs = q2.x, which = q2.y;
-            const double cc = mbd[2];
+            TP_STAMP(0);
             double sa[NS], sb[NS];
             if (which == 0) {
 #pragma unroll
@@ -474,6 +511,13 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
                 sm[t] = sa[t] + sb[t];
                 S[(size_t)a_ * ld + 64 * t] = sm[t];
             }
+            if (STAMPS) {   // waits for the rows (the stamp below then counts the HBM wait)
+                double z = 0.0;
+#pragma unroll
+                for (int t = 0; t < NS; ++t) z += sm[t];
+                asm volatile("" ::"v"(z));
+            }
+            TP_STAMP(1);
             const double fm = (double)nm, fl = (double)nl, fr = (double)nr;
             double ul = ward_part<NS>(sl, fl, sm, fm);
             double ur = ward_part<NS>(sm, fm, sr, fr);
@@ -481,25 +525,29 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
             const double cl = ls_ >= 0 ? nan2inf(ul / (fl * fm * (fl + fm))) : QNAN;
             const double cr = r_ >= 0 ? nan2inf(ur / (fm * fr * (fm + fr))) : QNAN;
             h = h + cc;
-            mbd[0] = cl;
-            mbd[1] = cr;
+            mb_d[0] = cl;
+            mb_d[1] = cr;
             if (lane == 0) {
                 mrg_a[s] = a_;
                 mrg_b[s] = b_;
                 mcost[s] = cc;
                 height[s] = h;
             }
+            TP_STAMP(2);
             __syncthreads();   // X
+            TP_STAMP(3);
             // ---- prefetch a2's rows for the next merge
-            const int4 p0 = pre4[0], p1 = pre4[1];
+            const int4 p0 = mb_i[3];
             load_row(pa, p0.x);
             load_row(pb, p0.y);
-            load_row(pl, p0.z);
-            load_row(pr, p0.w);
-            ls2p = p1.x;
-            r2p = p1.y;
+            load_row(pl, p0.z >= 0 ? p0.z : p0.x);
+            load_row(pr, p0.w >= 0 ? p0.w : p0.x);
+            ls2p = p0.z;
+            r2p = p0.w;
             aprev = a_;
+            TP_STAMP(6);
             __syncthreads();   // Y
+            TP_STAMP(7);
         }
     }
     __syncthreads();
@@ -528,8 +576,8 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
         sd.n_cluster[ti] = ncl;
     }
     TP_STAMP(5);
-    if (STAMPS && threadIdx.x == 0)
-        for (int q = 0; q < 8; ++q) sd.stamps[(size_t)ti * 8 + q] = st_acc[q];
+    if (STAMPS && lane == 0)   // wave A: slots 0..7, wave B: 8..15
+        for (int q = 0; q < 8; ++q) sd.stamps[(size_t)ti * 16 + (waveA ? 0 : 8) + q] = st_acc[q];
 #undef TP_STAMP
 }
 
@@ -538,7 +586,7 @@ template <bool STAMPS, int BS, bool GLB>
 __global__ void __launch_bounds__(128) k_coniss_t(SweepDev sd, double *cost0) {
     extern __shared__ double lds[];
     __shared__ double mb_d[4];
-    __shared__ int4 mb_i[5];
+    __shared__ int4 mb_i[4];
     const int i = sd.tree0 + blockIdx.x + 1;
     switch ((i + 63) / 64) {
         case 1: coniss_tree2<STAMPS, 1, BS, GLB>(sd, cost0, lds, mb_d, mb_i); break;
@@ -548,9 +596,11 @@ __global__ void __launch_bounds__(128) k_coniss_t(SweepDev sd, double *cost0) {
     }
 }
 template __global__ void k_coniss_t<false, 1, false>(SweepDev, double *);
+template __global__ void k_coniss_t<false, 2, false>(SweepDev, double *);
 template __global__ void k_coniss_t<false, 3, false>(SweepDev, double *);
 template __global__ void k_coniss_t<false, 16, true>(SweepDev, double *);
 template __global__ void k_coniss_t<true, 1, false>(SweepDev, double *);
+template __global__ void k_coniss_t<true, 2, false>(SweepDev, double *);
 template __global__ void k_coniss_t<true, 3, false>(SweepDev, double *);
 template __global__ void k_coniss_t<true, 16, true>(SweepDev, double *);
 
@@ -960,8 +1010,7 @@ __global__ void k_fill(double *p, size_t cnt, double v) {
 }
 
 static size_t coniss_lds_bytes(int n) {   // costs, links, right ends (the mailbox is static LDS)
-    size_t nbk = (n + 63) / 64;
-    return nbk * 64 * 8 + (size_t)n * 8;
+    return coniss_cost_stride(n) * 8 + coniss_link_stride(n) * 8;
 }
 constexpr size_t kConissGlbLds = 16;   // nothing: the mailbox is static LDS
 constexpr int kConissMaxN = 64 * 64 * 16;             // global variant: 16 block-minimum slots
@@ -982,15 +1031,17 @@ static void run_coniss(const SweepDev &sd, hipStream_t s, bool stamped, Ctx *pro
     TP_HIP(hipGetLastError());
     const bool in_lds = coniss_in_lds(sd.n);
     const size_t lds = in_lds ? coniss_lds_bytes(sd.n) : kConissGlbLds;
-    const bool small = sd.n <= 4096;
+    const int bs = (nbk + 63) / 64;   // block-minimum slots per lane
     if (!stamped && prof) kprof_begin(*prof, K_CONISS);
     if (stamped) {
         if (!in_lds) launch_coniss_bs<true, 16, true>(sd, cost0, lds, s);
-        else if (small) launch_coniss_bs<true, 1, false>(sd, cost0, lds, s);
+        else if (bs == 1) launch_coniss_bs<true, 1, false>(sd, cost0, lds, s);
+        else if (bs == 2) launch_coniss_bs<true, 2, false>(sd, cost0, lds, s);
         else launch_coniss_bs<true, 3, false>(sd, cost0, lds, s);
     } else {
         if (!in_lds) launch_coniss_bs<false, 16, true>(sd, cost0, lds, s);
-        else if (small) launch_coniss_bs<false, 1, false>(sd, cost0, lds, s);
+        else if (bs == 1) launch_coniss_bs<false, 1, false>(sd, cost0, lds, s);
+        else if (bs == 2) launch_coniss_bs<false, 2, false>(sd, cost0, lds, s);
         else launch_coniss_bs<false, 3, false>(sd, cost0, lds, s);
     }
     if (!stamped && prof) kprof_end(*prof, K_CONISS);

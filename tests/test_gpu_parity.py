@@ -155,7 +155,7 @@ def test_eigsym(gpu, b, kind):
 
 
 @pytest.mark.parametrize("b,cond,rel", [(16, 1e2, 0.0), (48, 1e4, 0.0), (128, 1e6, 0.0), (256, 1e6, 0.0),
-                                         (256, 1e12, 1e-14), (96, 1.0, 0.0)])
+                                         (256, 1e12, 1e-14), (96, 1.0, 0.0), (64, 1e8, 1e-14), (32, 1e3, 0.0)])
 def test_chol_inv_register_kernel(gpu, b, cond, rel):
     """PCA CholQR kernels (k_chol_inv + k_trsm_frag) on Z = I: Y = U^{-1} for
     U'U = W + rel diag(W) (Jacobi-scaled shift).  Checks Y upper triangular,
@@ -185,7 +185,7 @@ def test_chol_inv_register_kernel(gpu, b, cond, rel):
     assert np.abs(Y.T @ Wr @ Y - np.eye(b)).max() <= 100 * b * 2.2e-16 * kap
     Uref = np.linalg.cholesky(Wr).T
     np.testing.assert_allclose(dg, np.diag(Uref), rtol=100 * b * 2.2e-16 * np.sqrt(kap))
-    print(f"chol_inv b={b}: chol {ms[0] * 1e3:.1f} us (16 waves), {ms[2] * 1e3:.1f} us (8 waves), "
+    print(f"chol_inv b={b}: chol {ms[0] * 1e3:.1f} us (product, 4 waves for b <= 64), {ms[2] * 1e3:.1f} us (16 waves), "
           f"trsm {ms[6] * 1e3:.1f} us; cycles prologue {ms[3]:.0f} factor {ms[4]:.0f} diag {ms[5]:.0f}")
 
 
@@ -425,6 +425,17 @@ def _xtx(gpu, x, mode):
     return S, ns.value, ms.value, st.value
 
 
+def _exact_xtx(x):
+    """X'X of a non-negative integer matrix, exactly: in float64 (BLAS) every
+    partial sum is an integer below 2^53 when n * max^2 < 2^53, so any summation
+    order is exact; numpy's int64 product (no BLAS) otherwise."""
+    n, mx = x.shape[0], float(x.max())
+    if n * mx * mx < 2.0 ** 53:
+        return x.T @ x
+    xi = x.astype(np.int64)
+    return (xi.T @ xi).astype(np.float64)
+
+
 @pytest.mark.parametrize("n,maxv,slices", [(64, 100, 1), (200, 5000, 2), (515, 16383, 2), (1000, 3000, 2),
                                            (333, 2_000_000, 3), (2000, 4000, 2), (1100, 120, 1),
                                            (1500, 16000, 2), (4100, 9000, 2)])
@@ -437,8 +448,7 @@ def test_xtx_int8_exact(gpu, n, maxv, slices):
     x[0, 0] = maxv - 1
     S, ns, ms, st = _xtx(gpu, x, 1)
     assert st == 0 and ns == slices
-    xi = x.astype(np.int64)
-    ref = (xi.T @ xi).astype(np.float64)
+    ref = _exact_xtx(x)
     assert np.array_equal(S, ref)
     S64, _, ms64, st64 = _xtx(gpu, x, 0)
     assert st64 == 0
@@ -458,8 +468,7 @@ def test_xtx_int8_exact_fresh_context(gpu, n, maxv):
     x = rng.integers(0, maxv, size=(n, n)).astype(np.float64)
     S, ns, _, st = _xtx(gpu, x, 1)
     assert st == 0 and ns >= 1
-    xi = x.astype(np.int64)
-    assert np.array_equal(S, (xi.T @ xi).astype(np.float64))
+    assert np.array_equal(S, _exact_xtx(x))
 
 
 def test_xtx_int8_rejects_non_counts(gpu):

@@ -35,28 +35,41 @@ def chol(b=256, cond=1e6):
 
 
 def coniss(n0=2000, k=200):
+    """Per-merge cycle budget of both CONISS waves on the scores of a synthetic
+    matrix (mask on the host, correlation and PCA through the library)."""
     import tadpole_oracle as O
     from tadpole_amd.synth import synth_hic
     m = synth_hic(n0, 20261017)
     cm = O.clean_symmetrize(m)
     bad, _, _ = O.bad_mask(cm, 0.01)
     g = np.flatnonzero(~bad)
-    p = np.asfortranarray(O.prcomp_x(O.sparse_cor(cm[np.ix_(g, g)]), k))
-    n = p.shape[0]
-    stamps = np.zeros(k * 8, np.int64)
-    ms = ctypes.c_double(0); st = ctypes.c_int(0)
-    L.tp_debug_coniss_stamps(p.ctypes.data_as(D), B(ctypes.c_int(n)), B(ctypes.c_int(k)),
-                             stamps.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)), B(ms), B(st))
+    x = np.asfortranarray(cm[np.ix_(g, g)])
+    n = x.shape[0]
+    cor = np.zeros((n, n), order="F")
+    p = np.zeros((n, k), order="F")
+    st = ctypes.c_int(0)
+    L.tp_cor(x.ctypes.data_as(D), B(ctypes.c_int(n)), B(ctypes.c_int(0)), cor.ctypes.data_as(D), B(st))
     _lib.check(st)
-    s = stamps.reshape(k, 8).astype(float)
-    names = ["A:merge_at+records", "A:wait X", "A:choice+links", "A:wait Y", "init", "bstick",
-             "A:writes+block loads", "A:reductions+argmin"]
-    print(f"coniss n={n} k={k}: kernel {ms.value:.3f} ms", flush=True)
+    L.tp_pca(cor.ctypes.data_as(D), B(ctypes.c_int(n)), B(ctypes.c_int(k)), B(ctypes.c_int(0)), p.ctypes.data_as(D),
+             None, B(st))
+    _lib.check(st)
+    stamps = np.zeros(k * 16, np.int64)
+    ms = ctypes.c_double(0)
+    for _ in range(2):   # second run: warm code objects
+        L.tp_debug_coniss_stamps(p.ctypes.data_as(D), B(ctypes.c_int(n)), B(ctypes.c_int(k)),
+                                 stamps.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)), B(ms), B(st))
+        _lib.check(st)
+    s = stamps.reshape(k, 16).astype(float) / (n - 1)
+    na = {6: "writes+block loads", 7: "reductions+argmin", 0: "merge_at+records", 1: "wait X", 2: "choice",
+          3: "wait Y"}
+    nb = {8: "rec read", 9: "row wait+sums", 10: "ward+records", 11: "wait X", 14: "prefetch", 15: "wait Y"}
+    print(f"coniss n={n} k={k}: stamped kernel {ms.value:.3f} ms ({ms.value * 1e3 / (n - 1):.2f} us/merge)",
+          flush=True)
     for i in (0, 63, 127, k - 1):
-        tot = s[i].sum()
-        print(f"  tree {i+1:3d}: total {tot/1e6:.2f} Mcyc; per merge " +
-              ", ".join(f"{names[j]} {s[i, j]/(n-1):.0f}" for j in (6, 7, 0, 1, 2, 3)) +
-              f"; init {s[i,4]/1e3:.0f} kcyc, bstick {s[i,5]/1e3:.0f} kcyc", flush=True)
+        print(f"  tree {i + 1:3d}: A " + ", ".join(f"{v} {s[i, q]:.0f}" for q, v in na.items()) +
+              f" (sum {sum(s[i, q] for q in na):.0f})", flush=True)
+        print(f"            B " + ", ".join(f"{v} {s[i, q]:.0f}" for q, v in nb.items()) +
+              f" (sum {sum(s[i, q] for q in nb):.0f})", flush=True)
 
 
 def eig(b=256):
@@ -106,3 +119,5 @@ if __name__ == "__main__":
         chol(480, 1e6)
     if "coniss" in what:
         coniss()
+    if "coniss3" in what:
+        coniss(7808, 200)

@@ -18,11 +18,17 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "gpurun_out")
 
-# bench.py kernel class -> the kernels one launch of that class runs (short names)
-CLASSES = {"coniss": ["tp::k_coniss_t<false, 1, false>"],
-           "ch": ["tp::k_ch_cut", "tp::k_ch_segstat", "tp::k_ch"],
-           "gq_gemm": ["tp::k_gemm_f64<true, 16, 1>", "tp::k_splitk_reduce<1>"],
-           "xtx_gemm": ["tp::k_xtx_i8_big<2>"]}
+# bench.py kernel class -> name prefixes of the kernels one launch of that class
+# runs; per prefix the variant with the largest total time in the trace is taken
+# (the CONISS block size and the GEMM tile are chosen per problem size)
+CLASSES = {"coniss": ["tp::k_coniss_t<false,"],
+           "ch": ["tp::k_ch_cut", "tp::k_ch_segstat", "tp::k_ch("],
+           "xtx_gemm": ["tp::k_xtx_i8_big<"]}
+
+
+def pick(stats, prefix):
+    cand = [r for r in stats if r["Name"].replace("void ", "").startswith(prefix)]
+    return short(max(cand, key=lambda r: float(r["TotalDurationNs"]))["Name"]) if cand else None
 
 
 def short(name):
@@ -32,14 +38,14 @@ def short(name):
 def main():
     tag = sys.argv[1]
     bench = json.load(open(os.path.join(OUT, "prof_bench.json")))
-    steps = bench["steps"] + bench["warmup"] + 1          # timed + warmup + instrumented step
+    steps = bench["steps"] + bench["warmup"]              # timed + warmup pipelines
     stats = list(csv.DictReader(open(os.path.join(OUT, "prof", "run_kernel_stats.csv"))))
     shutil.copy(os.path.join(OUT, "prof", "run_kernel_stats.csv"),
                 os.path.join(ROOT, "profiles", f"{tag}_kernel_stats.csv"))
     tot = sum(float(r["TotalDurationNs"]) for r in stats)
     lines = [f"# {tag}: rocprofv3 --kernel-trace --stats, `python bench.py --steps {bench['steps']} "
-             f"--warmup {bench['warmup']} --streams {bench['config'].get('streams_per_gpu', 1)} --no-cpu-baseline` "
-             f"({steps} pipelines, C2 2000x2000, max_pcs=200)",
+             f"--warmup {bench['warmup']} --throughput-streams 0 --no-cpu-baseline` "
+             f"({steps} pipelines, {bench['config']['workload']})",
              "", f"bench line of the profiled run: value {bench['value']} bins/s, "
                  f"{bench['ms_per_step']} ms/step (profiler attached)", "",
              "| kernel | calls/pipeline | ms/pipeline | avg us | % |", "|---|---|---|---|---|"]
@@ -73,8 +79,9 @@ def main():
     # the trace stats, HBM bytes from the PMC passes)
     avg_us = {short(r["Name"]): float(r["AverageNs"]) / 1e3 for r in stats}
     classes = {}
-    for cls, names in CLASSES.items():
-        if all(nm in avg_us for nm in names):
+    for cls, prefixes in CLASSES.items():
+        names = [pick(stats, pf) for pf in prefixes]
+        if all(nm is not None and nm in avg_us for nm in names):
             classes[cls] = {"kernels": names, "avg_us": sum(avg_us[nm] for nm in names),
                             "hbm_bytes": (sum(traffic[nm]["hbm_bytes"] for nm in names)
                                           if all(nm in traffic for nm in names) else None)}
