@@ -56,6 +56,10 @@ __device__ __forceinline__ int pin(int x) {
     asm volatile("" : "+v"(x));
     return x;
 }
+__device__ __forceinline__ double pin_d(double x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
 
 __device__ __forceinline__ double nan2inf(double x) { return isnan(x) ? __longlong_as_double(0x7FF0000000000000LL) : x; }
 
@@ -522,17 +526,19 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
             double ul = ward_part<NS>(sl, fl, sm, fm);
             double ur = ward_part<NS>(sm, fm, sr, fr);
             wave_sum2(ul, ur);
-            const double cl = ls_ >= 0 ? nan2inf(ul / (fl * fm * (fl + fm))) : QNAN;
-            const double cr = r_ >= 0 ? nan2inf(ur / (fm * fr * (fm + fr))) : QNAN;
+            // both divisions unconditionally (interleaved, no branch), then select
+            const double ql = pin_d(ul / (fl * fm * (fl + fm)));
+            const double qr = pin_d(ur / (fm * fr * (fm + fr)));
+            const double cl = ls_ >= 0 ? nan2inf(ql) : QNAN;
+            const double cr = r_ >= 0 ? nan2inf(qr) : QNAN;
             h = h + cc;
             mb_d[0] = cl;
             mb_d[1] = cr;
-            if (lane == 0) {
-                mrg_a[s] = a_;
-                mrg_b[s] = b_;
-                mcost[s] = cc;
-                height[s] = h;
-            }
+            // every lane stores the same words (one request each; no exec mask)
+            mrg_a[s] = a_;
+            mrg_b[s] = b_;
+            mcost[s] = cc;
+            height[s] = h;
             TP_STAMP(2);
             __syncthreads();   // X
             TP_STAMP(3);
