@@ -484,7 +484,7 @@ static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_cl
     o.k = k;
     if (k > k_cap) fail(TP_ERR_CAPACITY, "k_cap smaller than min(max_pcs, n_good)");
     double *P = c.buf[S_P].as<double>((size_t)n * k);
-    double *Pt = c.buf[S_PT].as<double>((size_t)n * k);
+    double *Pt = c.buf[S_PT].as<double>(pt_doubles(n, k));
     PcaStats ps = pca_dev(c, C, n, k, P, Pt, nullptr);
     trace_mark(s, "pca");
     tm.mark();
@@ -684,7 +684,7 @@ void tp_sweep(const double *P, const int *n, const int *k, const int *min_cluste
         hipStream_t s = c.cur;
         const int N = *n, K = *k;
         double *dP = c.buf[S_P].as<double>((size_t)N * K);
-        double *dPt = c.buf[S_PT].as<double>((size_t)N * K);
+        double *dPt = c.buf[S_PT].as<double>(pt_doubles(N, K));
         TP_HIP(hipMemcpyAsync(dP, P, (size_t)N * K * 8, hipMemcpyHostToDevice, s));
         launch_transpose(dP, N, K, N, dPt, K, s);
         SweepOut o = run_sweep(c, dPt, N, K, min_clusters ? *min_clusters : 2, *w_cap, n_cluster, scores, merge,
@@ -703,7 +703,7 @@ void tp_sweep_dev(const double *d_P, const int *n, const int *k, const int *min_
         Ctx &c = ctx_for(dev_of(device), (hipStream_t)stream);
         hipStream_t s = c.cur;
         const int N = *n, K = *k;
-        double *dPt = c.buf[S_PT].as<double>((size_t)N * K);
+        double *dPt = c.buf[S_PT].as<double>(pt_doubles(N, K));
         launch_transpose(d_P, N, K, N, dPt, K, s);
         std::vector<int> A, B;
         std::vector<double> Co, H;
@@ -729,7 +729,7 @@ void tp_coniss(const double *P, const int *n, const int *ncols, const int *devic
         hipStream_t s = c.cur;
         const int N = *n, K = *ncols;
         double *dP = c.buf[S_P].as<double>((size_t)N * K);
-        double *dPt = c.buf[S_PT].as<double>((size_t)N * K);
+        double *dPt = c.buf[S_PT].as<double>(pt_doubles(N, K));
         TP_HIP(hipMemcpyAsync(dP, P, (size_t)N * K * 8, hipMemcpyHostToDevice, s));
         launch_transpose(dP, N, K, N, dPt, K, s);
         SweepDev sd{};
@@ -800,7 +800,7 @@ void tp_ch(const double *P, const int *n, const int *k, const int *labels, const
         Ctx &c = ctx_for(dev_of(device));
         hipStream_t s = c.cur;
         double *dP = c.buf[S_P].as<double>((size_t)N * K);
-        double *dPt = c.buf[S_PT].as<double>((size_t)N * K);
+        double *dPt = c.buf[S_PT].as<double>(pt_doubles(N, K));
         int *dB = c.buf[S_GOOD].as<int>(CN + 1);
         double *seg = c.buf[S_PARTIAL].as<double>(CN + 8);
         double *out = c.buf[S_SMALL].as<double>(8);
@@ -995,7 +995,7 @@ void tp_debug_coniss_stamps(const double *P, const int *n, const int *k, long lo
         hipStream_t s = c.cur;
         const int N = *n, K = *k;
         double *dP = c.buf[S_P].as<double>((size_t)N * K);
-        double *dPt = c.buf[S_PT].as<double>((size_t)N * K);
+        double *dPt = c.buf[S_PT].as<double>(pt_doubles(N, K));
         TP_HIP(hipMemcpyAsync(dP, P, (size_t)N * K * 8, hipMemcpyHostToDevice, s));
         launch_transpose(dP, N, K, N, dPt, K, s);
         SweepDev sd{};

@@ -189,6 +189,9 @@ __host__ __device__ inline size_t coniss_cost_stride(int n) { return (size_t)((n
 __host__ __device__ inline size_t coniss_link_stride(int n) { return (size_t)n + 64; }
 // initial costs (ntrees x cost stride) + link scratch of the global-memory
 // CONISS variant (ntrees x 2 link strides of ints)
+// row-major scores Pt (n x k) + slack: CONISS reads whole 64-column slots of a
+// row (up to 256 columns) and masks the columns past its prefix
+inline size_t pt_doubles(int n, int k) { return (size_t)n * k + 256; }
 inline size_t sweep_cost0_doubles(int n, int ntrees) {
     return (size_t)ntrees * (coniss_cost_stride(n) + coniss_link_stride(n));
 }

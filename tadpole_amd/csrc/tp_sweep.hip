@@ -24,6 +24,7 @@
 namespace tp {
 
 constexpr int KMAXSLOT = 4;   // columns per lane: k <= 256
+constexpr int ROW_PT = 1 << 30;   // CONISS row code flag: the row is in Pt (a singleton)
 
 // pairwise tree over 64 leaves = the xor butterfly's summation tree
 template <int W> struct PTree {
@@ -44,7 +45,6 @@ static __host__ __device__ inline size_t pad_prefix(long m) {
     const long g = m / 64, r = m % 64;
     return (size_t)64 * (size_t)(64 * g * (g + 1) / 2 + r * (g + 1));
 }
-static __host__ __device__ inline int slab_ld(int i) { return ((i + 63) / 64) * 64; }
 static __host__ __device__ inline size_t sums_off(int n, int tree0, int i) {
     return (size_t)n * (pad_prefix(i - 1) - pad_prefix(tree0));
 }
@@ -122,62 +122,59 @@ __device__ __forceinline__ void wave_sum2(double &u, double &v) {
 }
 
 
-// ---- seeding: every tree's cluster-sum slab starts as the first i columns of
-// the scores (zero-padded to ld(i)), and the initial adjacent (singleton) costs
-// are e_j = x_j - y_j, cost = tot / 2 (canonical order).  One wave per
-// (tree, 64 positions).
+// ---- initial adjacent (singleton) costs of every tree: e_j = x_j - y_j over
+// the first i score columns, cost = tot / 2 (canonical order).  One wave per
+// (tree, 64 positions).  The trees' cluster-sum slabs are not seeded: a
+// singleton's sums are its row of the shared scores Pt (read there by
+// k_coniss); a slab row is written only when a merge forms that cluster.
 __global__ void __launch_bounds__(64) k_seed(SweepDev sd, double *cost0) {
     const int n = sd.n, ldp = sd.ldp;
     const int ti = blockIdx.x, i = sd.tree0 + ti + 1;
-    const int ld = slab_ld(i);
     const int lane = threadIdx.x;
-    double *S = sd.sums + sums_off(n, sd.tree0, i);
     double *c0 = cost0 + (size_t)ti * coniss_cost_stride(n);
     const int p0 = blockIdx.y * 64;
     const double QNAN = __longlong_as_double(0x7FF8000000000000LL);
     double x[KMAXSLOT], y[KMAXSLOT];
-    {
-        const int p = p0;
 #pragma unroll
-        for (int t = 0; t < KMAXSLOT; ++t) {
-            const int j = lane + 64 * t;
-            y[t] = (p < n && j < i) ? sd.Pt[(size_t)p * ldp + j] : 0.0;
-        }
+    for (int t = 0; t < KMAXSLOT; ++t) {
+        const int j = lane + 64 * t;
+        y[t] = (p0 < n && j < i) ? sd.Pt[(size_t)p0 * ldp + j] : 0.0;
     }
     double mycost = QNAN;
     for (int q = 0; q < 64; ++q) {
         const int p = p0 + q;
-        if (p >= n) break;
+        if (p + 1 >= n) break;
 #pragma unroll
         for (int t = 0; t < KMAXSLOT; ++t) {
             x[t] = y[t];
             const int j = lane + 64 * t;
-            if (j < ld) S[(size_t)p * ld + j] = x[t];
-            y[t] = (p + 1 < n && j < i) ? sd.Pt[(size_t)(p + 1) * ldp + j] : 0.0;
+            y[t] = j < i ? sd.Pt[(size_t)(p + 1) * ldp + j] : 0.0;
         }
-        if (p + 1 < n) {
-            double acc = 0.0;
+        double acc = 0.0;
 #pragma unroll
-            for (int t = 0; t < KMAXSLOT; ++t)
-                if (lane + 64 * t < i) {
-                    double e = x[t] - y[t];
-                    acc = fma(e, e, acc);
-                }
-            double tot = wave_sum(acc);
-            if (lane == q) mycost = nan2inf(tot / 2.0);
-        }
+        for (int t = 0; t < KMAXSLOT; ++t)
+            if (lane + 64 * t < i) {
+                double e = x[t] - y[t];
+                acc = fma(e, e, acc);
+            }
+        double tot = wave_sum(acc);
+        if (lane == q) mycost = nan2inf(tot / 2.0);
     }
     c0[p0 + lane] = mycost;
 }
 
+// Columns i..ld-1 of a row hold whatever the row was read from (later PCs of
+// Pt, or their sums): the last slot's term is selected to 0 there, which adds
+// fma(0, 0, acc) = acc -- the canonical sum over the first i columns.
 template <int NS>
-__device__ __forceinline__ double ward_part(const double (&sa)[NS], double fa, const double (&sb)[NS], double fb) {
+__device__ __forceinline__ double ward_part(const double (&sa)[NS], double fa, const double (&sb)[NS], double fb,
+                                            bool last_in) {
     double acc = 0.0;
 #pragma unroll
     for (int t = 0; t < NS; ++t) {
         const double t1 = sa[t] * fb;
         const double t2 = sb[t] * fa;
-        const double e = t1 - t2;
+        const double e = (t < NS - 1 || last_in) ? t1 - t2 : 0.0;
         acc = fma(e, e, acc);
     }
     return acc;
@@ -241,7 +238,14 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
     // X), mb_d[2] = the next merge's cost (A -> B before Y); mb_i[0..2] = the
     // next merge's record (A -> B before Y), mb_i[3] = a2's row starts
     // (a2s, b2s, ls2, r2) (A -> B before X).
+    // Row codes: a cluster's start position, | ROW_PT when the cluster is a
+    // singleton (its sums are its row of the shared scores Pt, which no tree
+    // writes: slabs hold only merged clusters).  A knows the ends of every
+    // cluster it names, so it flags singletons in what it sends B.
     double *S = sd.sums + sums_off(n, sd.tree0, i) + lane;
+    const double *P0 = sd.Pt + lane;
+    const int ldp = sd.ldp;
+    const bool last_in = lane + 64 * (NS - 1) < i;
     int *mrg_a = sd.mrg_a + (size_t)ti * (n - 1);
     int *mrg_b = sd.mrg_b + (size_t)ti * (n - 1);
     double *mcost = sd.cost + (size_t)ti * (n - 1);
@@ -266,15 +270,19 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
         for (int q = 1; q < BS; ++q) g = vmin(g, bmr[q]);
         return wave_min(g);
     };
-    auto load_row = [&](double (&dst)[NS], int start) {
-        const double *pr = S + (size_t)start * ld;
+    auto load_row = [&](double (&dst)[NS], int code) {
+        code = __builtin_amdgcn_readfirstlane(code);
+        const int p = code & (ROW_PT - 1);
+        const double *pr = (code & ROW_PT) ? P0 + (size_t)p * ldp : S + (size_t)p * ld;
 #pragma unroll
         for (int t = 0; t < NS; ++t) dst[t] = pr[64 * t];
     };
+    auto rowc = [](int start, bool single) { return start | (single ? ROW_PT : 0); };
     // A: a merge described by (a, ea, eb, ls, r, er); b = ea + 1; ll = start of
-    // the cluster left of ls (its ls|m successor's left row)
+    // the cluster left of ls (its ls|m successor's left row); rre = end of the
+    // cluster right of r (rr, its m|r successor's right row)
     struct Mg {
-        int a, ea, eb, ls, r, er, ll;
+        int a, ea, eb, ls, r, er, ll, rre;
     };
     auto merge_at1 = [&](int p) {   // current links -> the pair starting at p, first level (no branches)
         Mg m;
@@ -286,11 +294,13 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
         m.r = m.eb >= 0 && m.eb + 1 < n ? m.eb + 1 : -1;
         return m;
     };
-    auto merge_at2 = [&](Mg &m) {   // second level: the right end of r, the cluster left of ls
+    auto merge_at2 = [&](Mg &m) {   // second level: the right ends of r and rr, the cluster left of ls
         const int erv = pin(rn[m.ea + 1 < n ? m.ea + 1 : DL]);
         const int llv = pin(link[m.ls > 0 ? m.ls - 1 : DL]);
+        const int rrev = pin(rn[m.r >= 0 ? m.r : DL]);
         m.er = m.r >= 0 ? erv : -1;
         m.ll = m.ls > 0 ? llv : -1;
+        m.rre = rrev;
     };
     auto merge_at = [&](int p) {
         Mg m = merge_at1(p);
@@ -302,11 +312,12 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
     };
     auto make_rec = [&](const Mg &m, int which) {   // A -> B: the record of a next merge
         const int rr = (m.r >= 0 && m.er + 1 < n) ? m.er + 1 : -1;
+        const int ac = rowc(m.a, m.ea == m.a);
         Rec rc;
         rc.x = make_int4(m.a, m.ea + 1 < n ? m.ea + 1 : m.a, m.ls, m.r);
         rc.y = make_int4(m.eb - m.a + 1, m.ls >= 0 ? m.a - m.ls : 0, m.r >= 0 ? m.er - m.r + 1 : 0,
-                         m.ll >= 0 ? m.ll : m.a);
-        rc.z = make_int4(rr >= 0 ? rr : m.a, which, 0, 0);
+                         m.ll >= 0 ? rowc(m.ll, m.ll == m.ls - 1) : ac);
+        rc.z = make_int4(rr >= 0 ? rowc(rr, m.rre == rr) : ac, which, 0, 0);
         return rc;
     };
     // the choice after merge (a, ls, r): the lexicographic (cost, position)
@@ -319,7 +330,7 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
         c2 = (r >= 0) & ((np < 0) | (cr < nv) | ((cr == nv) & (a < np)));
         nv = c2 ? cr : nv;
     };
-    Mg cur = {0, 0, 0, -1, -1, -1, -1};
+    Mg cur = {0, 0, 0, -1, -1, -1, -1, -1};
     double c = 0.0, pcl = QNAN, pcr = QNAN;
     int pls = DC, pa_ = DC;   // A: where the previous merge's new costs go (applied at the next merge's start)
     if (waveA) {
@@ -356,10 +367,11 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
     double h = 0.0;
     if (!waveA) {
         const int4 q0 = mb_i[0];
-        load_row(pa, q0.x);
-        load_row(pb, q0.y);
-        load_row(pl, q0.z >= 0 ? q0.z : q0.x);
-        load_row(pr, q0.w >= 0 ? q0.w : q0.x);
+        // the first merge's clusters are all singletons
+        load_row(pa, rowc(q0.x, true));
+        load_row(pb, rowc(q0.y, true));
+        load_row(pl, rowc(q0.z >= 0 ? q0.z : q0.x, true));
+        load_row(pr, rowc(q0.w >= 0 ? q0.w : q0.x, true));
         ls2p = q0.z;
         r2p = q0.w;
 #pragma unroll
@@ -386,6 +398,7 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
             // issued before the argmin's reductions so their latency overlaps)
             const int m1llv = pin(link[cur.ll > 0 ? cur.ll - 1 : DL]);
             const int m2erv = pin(rn[r >= 0 ? r : DL]);
+            const int m2rrev = pin(rn[(r >= 0 && er + 1 < n) ? er + 1 : DL]);
             const int m1ll = cur.ll > 0 ? m1llv : -1;
             const int m2er = (r >= 0 && er + 1 < n) ? m2erv : -1;
             // refresh the three touched blocks and, concurrently, the minimum of
@@ -424,16 +437,23 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
             // ---- the three possible next merges (post-update links); a2's
             //      clusters go to B at once (its row prefetch starts before X)
             Mg m0 = merge_at1(a2 >= 0 ? a2 : a);
-            mb_i[3] = make_int4(m0.a, m0.ea + 1 < n ? m0.ea + 1 : m0.a, m0.ls, m0.r);
             merge_at2(m0);
+            {   // a2's four rows (absent ls / r: -1), singletons flagged
+                const int bs2 = m0.ea + 1 < n ? m0.ea + 1 : m0.a;
+                mb_i[3] = make_int4(rowc(m0.a, m0.ea == m0.a), rowc(bs2, m0.eb == bs2),
+                                    m0.ls >= 0 ? rowc(m0.ls, m0.ls == m0.a - 1) : -1,
+                                    m0.r >= 0 ? rowc(m0.r, m0.er == m0.r) : -1);
+            }
             Mg m1;   // ls | m
             m1.a = ls; m1.ea = a - 1; m1.eb = eb; m1.ls = cur.ll; m1.r = r; m1.er = er;
             m1.ll = m1ll;
+            m1.rre = m2erv;
             Mg m2;   // m | r
             m2.a = a; m2.ea = eb; m2.eb = er; m2.ls = ls;
             m2.r = (r >= 0 && er + 1 < n) ? er + 1 : -1;
             m2.er = m2er;
             m2.ll = cur.ll;
+            m2.rre = m2rrev;
             TP_STAMP(0);
             __syncthreads();   // X
             TP_STAMP(1);
@@ -451,6 +471,7 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
             cur.r = sel(m0.r, m1.r, m2.r);
             cur.er = sel(m0.er, m1.er, m2.er);
             cur.ll = sel(m0.ll, m1.ll, m2.ll);
+            cur.rre = sel(m0.rre, m1.rre, m2.rre);
             c = nv;
             {
                 const Rec rc = make_rec(cur, c2 ? 2 : (c1 ? 1 : 0));
@@ -523,8 +544,8 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
             }
             TP_STAMP(1);
             const double fm = (double)nm, fl = (double)nl, fr = (double)nr;
-            double ul = ward_part<NS>(sl, fl, sm, fm);
-            double ur = ward_part<NS>(sm, fm, sr, fr);
+            double ul = ward_part<NS>(sl, fl, sm, fm, last_in);
+            double ur = ward_part<NS>(sm, fm, sr, fr, last_in);
             wave_sum2(ul, ur);
             // both divisions unconditionally (interleaved, no branch), then select
             const double ql = pin_d(ul / (fl * fm * (fl + fm)));
