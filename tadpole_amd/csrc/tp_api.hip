@@ -1266,7 +1266,7 @@ void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
         case 9: p = &g_pca_krylov_block; break;
         case 10: p = &g_pca_krylov_steps; break;
         case 11: p = &g_chol_inv_waves; break;
-        
+        case 12: p = &g_gemm_splitk; break;
         default: fail(TP_ERR_ARG, "unknown knob");
         }
         if (*which == 3 && *value != 16 && *value != 32) fail(TP_ERR_ARG, "stage depth must be 16 or 32");

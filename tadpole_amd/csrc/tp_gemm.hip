@@ -389,7 +389,9 @@ __global__ void __launch_bounds__(256) k_gemm_f64_panel(int M, int N, int K, con
 }
 int g_gemm_panel = 1;   // 0: tall-skinny products take the split-K 64 x 64 path (A/B tests)
 
-// Fixed-order split-K reduction: C = sum_{z=0..S-1} part[z] (column-major M x N).
+// Fixed-order split-K reduction: C = sum_{z=0..S-1} part[z] (column-major M x N),
+// z ascending; loads issued 8 at a time (S is a runtime count: one dependent
+// load per partial otherwise).
 template <int TAG = 0>
 __global__ void __launch_bounds__(256) k_splitk_reduce(const double *part, size_t stride, int S, int M, int N,
                                                        double *C, int ldc, int store_t) {
@@ -397,10 +399,50 @@ __global__ void __launch_bounds__(256) k_splitk_reduce(const double *part, size_
     if (idx >= (size_t)M * N) return;
     int i = (int)(idx % M), j = (int)(idx / M);
     double v = part[idx];
-    for (int z = 1; z < S; ++z) v = v + part[idx + z * stride];
+    int z = 1;
+    for (; z + 8 <= S; z += 8) {
+        double t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t[u] = part[idx + (size_t)(z + u) * stride];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v = v + t[u];
+    }
+    for (; z < S; ++z) v = v + part[idx + (size_t)z * stride];
     if (store_t) C[(size_t)j + (size_t)i * ldc] = v;
     else C[(size_t)i + (size_t)j * ldc] = v;
 }
+
+// Many partials of a small output (Gram matrices of CholQR, K'W of the Krylov
+// re-orthogonalisation): 64 outputs per workgroup, the partials of each split
+// over the 4 waves (wave w: z = w, w + 4, ...: ascending), the four group sums
+// combined in wave order.  Fixed order for a given S.
+__global__ void __launch_bounds__(256) k_splitk_reduce4(const double *part, size_t stride, int S, int M, int N,
+                                                        double *C, int ldc, int store_t) {
+    __shared__ double red[4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const size_t idx = (size_t)blockIdx.x * 64 + lane;
+    const bool live = idx < (size_t)M * N;
+    const size_t src = live ? idx : 0;
+    double v = 0.0;
+    int z = w;
+    for (; z + 28 < S; z += 32) {
+        double t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t[u] = part[src + (size_t)(z + 4 * u) * stride];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v = v + t[u];
+    }
+    for (; z < S; z += 4) v = v + part[src + (size_t)z * stride];
+    red[w][lane] = v;
+    __syncthreads();
+    if (w == 0 && live) {
+        const double r = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+        const int i = (int)(idx % M), j = (int)(idx / M);
+        if (store_t) C[(size_t)j + (size_t)i * ldc] = r;
+        else C[(size_t)i + (size_t)j * ldc] = r;
+    }
+}
+int g_gemm_splitk = 1;   // auto split-K policy: 1 = deep splits for few-tile long-K products, 0 = round-1 policy
 
 void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s) {
     if (g.M <= 0 || g.N <= 0) return;
@@ -457,6 +499,20 @@ void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s) {
         S = 1;
         if (nblk < 192 && g.K >= 512) S = (int)std::min<long>(8, std::max<long>(1, (384 + nblk - 1) / nblk));
         S = std::min(S, std::max(1, g.K / 128));
+        if (g_gemm_splitk && nblk <= 64 && g.K >= 512) {
+            // few output tiles, long K (Gram matrices Z'Z, the Krylov K'W, T Y):
+            // one k-chunk is otherwise a long chain of dependent stages on a
+            // quarter of the chip.  ~1024 workgroups, chunks of >= 8 stages
+            // (>= 4 for a single tile), partials bounded by ~1/64 of the
+            // operand bytes the product streams.
+            const int kmin = nblk <= 4 ? 64 : 128;
+            long s2 = std::min<long>(g.K / kmin, (1024 + nblk - 1) / nblk);
+            const double outb = 8.0 * g.M * g.N;
+            const double budget = std::max(16.0e6, 8.0 * g.M * (double)g.N * g.K / 64.0);
+            s2 = std::min<long>(s2, (long)(budget / outb));
+            s2 = std::min<long>(s2, 128);
+            if (s2 > S) S = (int)s2;
+        }
     }
     int kchunk = ((g.K + S - 1) / S + BK - 1) / BK * BK;   // multiple of 16 for either stage depth
     if (kchunk < BK) kchunk = BK;
@@ -495,7 +551,10 @@ void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s) {
     if (S > 1) {
         size_t tot = (size_t)g.M * g.N;
         const dim3 rg((unsigned)((tot + 255) / 256));
-        if (g.tag == 1)
+        if (S >= 16 && tot <= ((size_t)1 << 18))
+            hipLaunchKernelGGL(k_splitk_reduce4, dim3((unsigned)((tot + 63) / 64)), dim3(256), 0, s, out, pstride, S,
+                               g.M, g.N, g.C, g.ldc, (int)g.store_t);
+        else if (g.tag == 1)
             hipLaunchKernelGGL(k_splitk_reduce<1>, rg, dim3(256), 0, s, out, pstride, S, g.M, g.N, g.C, g.ldc,
                                (int)g.store_t);
         else

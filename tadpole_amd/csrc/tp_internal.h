@@ -140,6 +140,7 @@ void launch_trsm_ru(const double *d_Z, int n, int b, const double *d_U, const do
 // diagonal; k_trsm_frag then forms Q = Z U^-1 (U = U' S^-1), n/16 waves.
 constexpr int kCholInvMax = 256;
 extern int g_chol_inv_waves;
+extern int g_gemm_splitk;
 void launch_chol_inv(double *d_W, double *d_F, double *d_sc, double *d_rdiag, int b, double rel, int *d_info,
                      hipStream_t s, long long *d_stamps = nullptr);
 void launch_trsm_frag(const double *d_Z, int n, int b, const double *d_F, const double *d_sc, double *d_Q,
