@@ -46,6 +46,8 @@ void hip_check(hipError_t e, const char *what, const char *file, int line) {
 void *DevBuf::get(size_t b) {
     if (b == 0) b = 8;
     if (b > bytes) {
+        // work queued on any stream may still read the old block
+        if (p) TP_HIP(hipDeviceSynchronize());
         if (p) TP_HIP(hipFree(p));
         p = nullptr;
         size_t nb = std::max(b, bytes + bytes / 4);
@@ -1267,6 +1269,7 @@ void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
         case 10: p = &g_pca_krylov_steps; break;
         case 11: p = &g_chol_inv_waves; break;
         case 12: p = &g_gemm_splitk; break;
+        case 13: p = &g_gemm_ts; break;
         default: fail(TP_ERR_ARG, "unknown knob");
         }
         if (*which == 3 && *value != 16 && *value != 32) fail(TP_ERR_ARG, "stage depth must be 16 or 32");
@@ -1274,6 +1277,18 @@ void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
             fail(TP_ERR_ARG, "Krylov block must be 0 or a multiple of 16 up to 256");
         *old = *p;
         *p = *value;
+    });
+}
+
+/* The scores P (n x k, column-major) of the last pipeline on device 0's default
+ * context (test hook: compares the PCA of two schedules). */
+void tp_debug_last_scores(const int *n, const int *k, double *P, int *status) {
+    guarded(status, [&] {
+        Ctx &c = ctx_for(0);
+        const size_t cnt = (size_t)(*n) * (*k);
+        if (c.buf[S_P].bytes < cnt * 8) fail(TP_ERR_ARG, "no scores of that size");
+        TP_HIP(hipStreamSynchronize(c.cur));
+        TP_HIP(hipMemcpy(P, c.buf[S_P].p, cnt * 8, hipMemcpyDeviceToHost));
     });
 }
 
@@ -1295,7 +1310,7 @@ void tp_debug_gemm(const double *A, const double *B, const int *M, const int *N,
         g.sym_upper = *sym != 0;
         // kernel: 0 = 64 x 64 tiles, 1 = 128 x 128 (when the tile count allows),
         // 2 = the library's policy (panel kernel for tall-skinny products),
-        // 3 = the split-K policy without the panel kernel
+        // 3 = the split-K policy without the panel kernel, 4 = row-shardable
         // kernel 10..99: 64 x 64 tiles with split-K (kernel - 10); 110..199: the
         // same with 16-deep LDS stages
         const int kern = *kernel >= 110 ? *kernel - 100 : *kernel;
@@ -1304,12 +1319,22 @@ void tp_debug_gemm(const double *A, const double *B, const int *M, const int *N,
         if (*kernel >= 110) g_gemm_kb = 16;
         else if (*kernel >= 10) g_gemm_kb = 32;
         g.big_cols = *kernel == 1;
+        g.rows = *kernel == 4 || *kernel == 5;   // 4: a row-shardable product (128 x 64 kernel, k chunks by K)
+        if (*kernel == 5) {   // 5: the same, stored transposed (C row-major m x n, as a row shard writes it)
+            g.store_t = true;
+            g.ldc = n;
+        }
         const int keep_panel = g_gemm_panel;
         g_gemm_panel = *kernel == 2 ? 1 : 0;
         hipEvent_t e0, e1;
         TP_HIP(hipEventCreate(&e0));
         TP_HIP(hipEventCreate(&e1));
         TP_HIP(hipEventRecord(e0, s));
+        if (*kernel == 6) {   // 6: the row-sharded schedule (virtual shards of tp_set_virtual_shards), A'B
+            c.shard.active = true;
+            rows_gemm_sharded(c, dA, k, m, dB, k, n, k, dC, 0, 0);
+            c.shard.active = false;
+        } else
         gemm_f64(g, c.buf[S_PARTIAL], s);
         g_gemm_panel = keep_panel;
         g_gemm_kb = keep_kb;

@@ -389,6 +389,106 @@ __global__ void __launch_bounds__(256) k_gemm_f64_panel(int M, int N, int K, con
 }
 int g_gemm_panel = 1;   // 0: tall-skinny products take the split-K 64 x 64 path (A/B tests)
 
+// ---------------------------------------------------------------------------
+// Long-K tall-skinny products C = A'B with A k-contiguous (the PCA's Xc K_t,
+// Xc'(Xc K_t) and the scores Xc V: M = n, N = 64..256, K = n): a 128 x 64
+// output tile per 256-thread workgroup, wave w owning rows 32w..32w+31 of it
+// across all 64 columns -- 2 x 4 MFMA tiles, 8 accumulators, 6 LDS fragment
+// reads per 8 MFMAs (the 64 x 64 kernel: 4 per 4).  BK = 16 double-buffered
+// in LDS (+2 pad, 55 KB: two workgroups a CU), next stage prefetched into
+// registers during the MFMAs, split-K chunks for a grid of ~2 workgroups a
+// CU.  Same k order as k_gemm_f64 (steps of 4 within blocks of 16): for the
+// same chunking the bits are those of the 64 x 64 kernel.
+constexpr int TSM = 128, TSN = 64, TSK = 16, TSLD = TSK + 2;
+template <int TAG>
+__global__ void __launch_bounds__(256, 2) k_gemm_ts(int M, int N, int K, const double *__restrict__ A, int lda,
+                                                    const double *__restrict__ B, int ldb, double *__restrict__ C,
+                                                    int ldc, int store_t, int kchunk, size_t part_stride) {
+    __shared__ double As[2][TSM][TSLD];
+    __shared__ double Bs[2][TSN][TSLD];
+    const int tm = (M + TSM - 1) / TSM, tn = (N + TSN - 1) / TSN;
+    // XCD-aware order (see k_gemm_f64): the column tiles of one row panel and
+    // its neighbours run on one XCD and share the A panel in its L2
+    const int total = (int)gridDim.x;
+    const int xcd = (int)blockIdx.x & 7, slot = (int)blockIdx.x >> 3;
+    const int Lg = xcd * (total >> 3) + min(xcd, total & 7) + slot;
+    const int bn = Lg % tn, bm = (Lg / tn) % tm, z = Lg / (tn * tm);
+    const int i0 = bm * TSM, j0 = bn * TSN;
+    const int kbeg = z * kchunk, kend = min(K, kbeg + kchunk);
+    C += part_stride * z;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int wm = 32 * w;
+    const int fr = lane & 15, fk = lane >> 4;
+    d4 acc[2][4];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = (d4){0.0, 0.0, 0.0, 0.0};
+    double ra[8], rb[4];
+    // thread t loads k = t & 15 of rows (t >> 4) + 16 p: 16 lanes read 128
+    // contiguous bytes of one row
+    const int lk = t & 15, lr = t >> 4;
+    auto load = [&](int k0) {
+        const int k = k0 + lk;
+        const bool kin = k < kend;
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+            const int i = i0 + lr + 16 * p;
+            ra[p] = (kin && i < M) ? A[(size_t)k + (size_t)i * lda] : 0.0;
+        }
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int j = j0 + lr + 16 * p;
+            rb[p] = (kin && j < N) ? B[(size_t)k + (size_t)j * ldb] : 0.0;
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int p = 0; p < 8; ++p) As[buf][lr + 16 * p][lk] = ra[p];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) Bs[buf][lr + 16 * p][lk] = rb[p];
+    };
+    if (kbeg < kend) {
+        load(kbeg);
+        store(0);
+    }
+    __syncthreads();
+    int buf = 0;
+    for (int k0 = kbeg; k0 < kend; k0 += TSK) {
+        const bool more = k0 + TSK < kend;
+        if (more) load(k0 + TSK);
+#pragma unroll
+        for (int kk = 0; kk < TSK; kk += 4) {
+            double af[2], bf[4];
+#pragma unroll
+            for (int a = 0; a < 2; ++a) af[a] = As[buf][wm + 16 * a + fr][kk + fk];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) bf[b] = Bs[buf][16 * b + fr][kk + fk];
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[a], bf[b], acc[a][b], 0, 0, 0);
+        }
+        if (more) store(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = i0 + wm + 16 * a + fk + 4 * r;
+                const int j = j0 + 16 * b + fr;
+                if (i >= M || j >= N) continue;
+                if (store_t) C[(size_t)j + (size_t)i * ldc] = acc[a][b][r];
+                else C[(size_t)i + (size_t)j * ldc] = acc[a][b][r];
+            }
+}
+int g_gemm_ts = 8;   // k_gemm_ts: most k chunks (0: off -> the 64 x 64 split-K kernel)
+
 // Fixed-order split-K reduction: C = sum_{z=0..S-1} part[z] (column-major M x N),
 // z ascending; loads issued 8 at a time (S is a runtime count: one dependent
 // load per partial otherwise).
@@ -453,6 +553,46 @@ void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s) {
     const int tc1 = g.sym_upper ? (g.tcol1 < 0 ? tn : std::min(tn, g.tcol1)) : 0;
     if (g.sym_upper && tc1 <= tc0) return;
     long nblk = g.sym_upper ? (long)tc1 * (tc1 + 1) / 2 - (long)tc0 * (tc0 + 1) / 2 : (long)tm * tn;
+    // long-K tall-skinny A'B (Xc products of the PCA): 128 x 64 tiles, before
+    // any other choice -- a row shard must take the same kernel and k chunks
+    if (g.rows && rows_ts(g.K, g.N) && g.trans_a && !g.sym_upper && (g.splitk <= 0 || g.splitk == 1)) {
+        const long tiles = (long)((g.M + TSM - 1) / TSM) * ((g.N + TSN - 1) / TSN);
+        // the k chunks depend on K alone (not on M): a row shard of the
+        // product (tp_shard.hip) then sums every element in the same order
+        int S = 1;
+        if (g.splitk <= 0) S = std::max(1, std::min(g_gemm_ts, g.K / 256));
+        int kchunk = ((g.K + S - 1) / S + TSK - 1) / TSK * TSK;
+        S = (g.K + kchunk - 1) / kchunk;
+        double *out = g.C;
+        int ldo = g.ldc, st = g.store_t;
+        size_t pstride = 0;
+        if (S > 1) {
+            pstride = (size_t)g.M * g.N;
+            out = work.as<double>(pstride * S);
+            ldo = g.M;
+            st = 0;
+        }
+        const dim3 grid((unsigned)(tiles * S));
+        if (g.tag == 1)
+            hipLaunchKernelGGL(k_gemm_ts<1>, grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb, out, ldo, st,
+                               kchunk, pstride);
+        else
+            hipLaunchKernelGGL(k_gemm_ts<0>, grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb, out, ldo, st,
+                               kchunk, pstride);
+        TP_HIP(hipGetLastError());
+        if (S > 1) {
+            const size_t tot = (size_t)g.M * g.N;
+            const dim3 rg((unsigned)((tot + 255) / 256));
+            if (g.tag == 1)
+                hipLaunchKernelGGL(k_splitk_reduce<1>, rg, dim3(256), 0, s, out, pstride, S, g.M, g.N, g.C, g.ldc,
+                                   (int)g.store_t);
+            else
+                hipLaunchKernelGGL(k_splitk_reduce<0>, rg, dim3(256), 0, s, out, pstride, S, g.M, g.N, g.C, g.ldc,
+                                   (int)g.store_t);
+            TP_HIP(hipGetLastError());
+        }
+        return;
+    }
     // 128 x 128 kernel: no split-K, enough tiles to fill the chip, and (sym) a
     // tile-column range in 128-column units (g.big_cols)
     {

@@ -123,6 +123,7 @@ struct GemmArgs {
     int tcol0 = 0, tcol1 = -1;   // sym_upper: only tile columns [tcol0, tcol1) (-1 = all)
     bool big_cols = false;       // use the 128 x 128 kernel; tcol0/tcol1 then count 128-column tiles
     int tag = 0;                 // 1: the PCA's G Y products (own kernel symbols for profiles)
+    bool rows = false;           // row-shardable long-K product (rows_gemm_sharded): 128 x 64 kernel, k chunks by K
 };
 void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s);
 extern int g_gemm_panel;   // short-K tall-skinny 32 x 64 kernel enabled (default 1)
@@ -141,6 +142,10 @@ void launch_trsm_ru(const double *d_Z, int n, int b, const double *d_U, const do
 constexpr int kCholInvMax = 256;
 extern int g_chol_inv_waves;
 extern int g_gemm_splitk;
+extern int g_gemm_ts;
+// row-shardable products that take the 128 x 64 kernel with k chunks fixed by K
+// (tp_gemm.hip); shards and the unsharded call must agree on it
+inline bool rows_ts(int K, int N) { return g_gemm_ts > 0 && K >= 4096 && N <= 256; }
 void launch_chol_inv(double *d_W, double *d_F, double *d_sc, double *d_rdiag, int b, double rel, int *d_info,
                      hipStream_t s, long long *d_stamps = nullptr);
 void launch_trsm_frag(const double *d_Z, int n, int b, const double *d_F, const double *d_sc, double *d_Q,

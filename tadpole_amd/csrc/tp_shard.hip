@@ -258,6 +258,7 @@ void rows_gemm_sharded(Ctx &c, const double *A, int lda, int M, const double *B,
         GemmArgs g{M, N, K, A, lda, true, B, ldb, Out, M};
         g.splitk = splitk_plain;
         g.tag = tag;
+        g.rows = true;
         gemm_f64(g, c.buf[S_PARTIAL], c.cur);
         return;
     }
@@ -269,8 +270,11 @@ void rows_gemm_sharded(Ctx &c, const double *A, int lda, int M, const double *B,
         if (!shard_mine(c, r) || rb[r + 1] <= rb[r]) continue;
         GemmArgs g{rb[r + 1] - rb[r], N, K, A + (size_t)rb[r] * lda, lda, true, B, ldb, T + (size_t)rb[r] * N, N};
         g.store_t = true;
-        g.splitk = 1;
+        // long-K products (128 x 64 kernel): k chunks fixed by K, the same bits
+        // as unsharded; otherwise no split (chunks would follow the shard's tiles)
+        g.splitk = rows_ts(K, N) ? splitk_plain : 1;
         g.tag = tag;
+        g.rows = true;
         gemm_f64(g, c.buf[S_PARTIAL], c.cur);
     }
     std::vector<size_t> off(R + 1);

@@ -553,3 +553,22 @@ def test_gemm_splitk_sweep(gpu):
             else:   # the stage depth never changes the k order
                 assert np.array_equal(c.view(np.uint64), c32.view(np.uint64))
             print(f"splitk {S} stage {kb}: {t * 1e3:.1f} us, {2.0 * M * N * K / t / 1e9:.1f} TF/s")
+
+
+@pytest.mark.parametrize("M,N,K", [(3000, 64, 4100), (1300, 200, 5000), (7729, 64, 7729), (24300, 200, 4096)])
+def test_gemm_rows_kernel_row_independent(gpu, M, N, K):
+    """The 128 x 64 long-K kernel of the PCA's Xc products (k chunks fixed by K):
+    any row slice of the product -- a row shard on another GPU -- has the bits of
+    the same rows of the full product; repeat runs are identical; numpy to ~K eps."""
+    rng = np.random.default_rng(M + 7 * N + K)
+    A = np.asfortranarray(rng.standard_normal((K, M)))
+    B = np.asfortranarray(rng.standard_normal((K, N)))
+    c, t = _gemm(gpu, A, B, M, N, K, 1, 0, 4)
+    c2, _ = _gemm(gpu, A, B, M, N, K, 1, 0, 4)
+    assert np.array_equal(c.view(np.uint64), c2.view(np.uint64))
+    for r0, r1 in ((0, 64), (640, 1280), (M - 193, M)):
+        cs, _ = _gemm(gpu, np.asfortranarray(A[:, r0:r1]), B, r1 - r0, N, K, 1, 0, 4)
+        assert np.array_equal(cs.view(np.uint64), c[r0:r1].view(np.uint64)), (r0, r1)
+    ref = A.T @ B
+    assert np.abs(c - ref).max() <= 1e-13 * np.abs(ref).max() * np.sqrt(K)
+    print(f"rows gemm {M}x{N}x{K}: {t * 1e3:.1f} us, {2.0 * M * N * K / t / 1e9:.1f} TF/s")
