@@ -478,7 +478,7 @@ static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_cl
         xtx_product(c, X, n, S);
         kprof_end(c, K_COR_GEMM);
     }
-    launch_cor_epilogue(S, m, n, C, s);
+    launch_cor_epilogue(S, m, n, C, c.buf[S_DIAG].as<double>(n), s);
     trace_mark(s, "cor");
     tm.mark();
     // ---- prcomp (R/TADpole.R:452-453)
@@ -656,7 +656,7 @@ void tp_cor(const double *X, const int *n, const int *device, double *cor, int *
         double *S = c.buf[S_S].as<double>((size_t)N * N);
         double *C = c.buf[S_C].as<double>((size_t)N * N);
         xtx_product(c, dX, N, S);
-        launch_cor_epilogue(S, m, N, C, s);
+        launch_cor_epilogue(S, m, N, C, c.buf[S_DIAG].as<double>(N), s);
         TP_HIP(hipMemcpyAsync(cor, C, (size_t)N * N * 8, hipMemcpyDeviceToHost, s));
         TP_HIP(hipStreamSynchronize(s));
     });

@@ -102,7 +102,7 @@ void launch_mask_select(const double *d_rowmean, const double *d_diag, int n0,
 void launch_gather_colmean(const double *d_M, int n0, const int *d_good, int n,
                            double *d_X, double *d_colmean, hipStream_t s);
 void launch_colmean(const double *d_A, int n, int ld, double *d_mean, hipStream_t s);
-void launch_cor_epilogue(const double *d_S, const double *d_m, int n, double *d_C,
+void launch_cor_epilogue(const double *d_S, const double *d_m, int n, double *d_C, double *d_sd,
                          hipStream_t s);
 void launch_center(const double *d_C, const double *d_mean, int n, double *d_Xc,
                    double *d_XcT, hipStream_t s);

@@ -58,6 +58,21 @@ void launch_clean_symmetrize(double *d_M, int n0, bool src_upper, hipStream_t s)
     TP_HIP(hipGetLastError());
 }
 
+// Lane-strided double-double sum of a column (rows lane, lane + 64, ...), U
+// loads in flight per lane; the accumulation order is the sequential one.
+template <int U>
+__device__ __forceinline__ void dd_col_acc(const double *src, int n, int lane, double &hi, double &lo) {
+    int r = lane;
+    for (; r + 64 * (U - 1) < n; r += 64 * U) {
+        double v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = src[r + 64 * u];
+#pragma unroll
+        for (int u = 0; u < U; ++u) dd_add_d(hi, lo, v[u]);
+    }
+    for (; r < n; r += 64) dd_add_d(hi, lo, src[r]);
+}
+
 // ------------------------------------------ rowMeans (long double in R) + diag
 // The matrix is symmetric here, so row a is column a (contiguous).  One wave
 // per column; double-double accumulation stands in for R's LDOUBLE.
@@ -67,7 +82,7 @@ __global__ void __launch_bounds__(256) k_rowmean_diag(const double *M, int n0, d
     if (a >= n0) return;
     const double *col = M + (size_t)a * n0;
     double hi = 0.0, lo = 0.0;
-    for (int r = lane; r < n0; r += 64) dd_add_d(hi, lo, col[r]);
+    dd_col_acc<8>(col, n0, lane, hi, lo);
     wave_dd_sum(hi, lo);
     if (lane == 0) {
         rm[a] = dd_div_d(hi, lo, (double)n0);
@@ -193,7 +208,22 @@ __global__ void __launch_bounds__(256) k_gather_colmean(const double *M, int n0,
     const double *src = M + (size_t)good[j] * n0;
     double *dst = X + (size_t)j * n;
     double hi = 0.0, lo = 0.0;
-    for (int a = lane; a < n; a += 64) {
+    constexpr int U = 8;   // gathers in flight per lane (same accumulation order)
+    int a = lane;
+    for (; a + 64 * (U - 1) < n; a += 64 * U) {
+        int gi[U];
+        double v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) gi[u] = good[a + 64 * u];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = src[gi[u]];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            dst[a + 64 * u] = v[u];
+            dd_add_d(hi, lo, v[u]);
+        }
+    }
+    for (; a < n; a += 64) {
         double v = src[good[a]];
         dst[a] = v;
         dd_add_d(hi, lo, v);
@@ -214,7 +244,7 @@ __global__ void __launch_bounds__(256) k_colmean(const double *A, int n, int ld,
     if (j >= n) return;
     const double *src = A + (size_t)j * ld;
     double hi = 0.0, lo = 0.0;
-    for (int a = lane; a < n; a += 64) dd_add_d(hi, lo, src[a]);
+    dd_col_acc<8>(src, n, lane, hi, lo);
     wave_dd_sum(hi, lo);
     if (lane == 0) cm[j] = dd_div_d(hi, lo, (double)n);
 }
@@ -227,23 +257,45 @@ void launch_colmean(const double *d_A, int n, int ld, double *d_mean, hipStream_
 // ------------------------------------------------- sparse_cor epilogue (R order)
 // cov = (S - n * (m m')) / (n - 1); cor = cov / (sd sd'), sd = sqrt(diag(cov));
 // NaN -> 0 (R/TADpole.R:96-98,449).  Rounding order as R evaluates it.
-__global__ void __launch_bounds__(256) k_cor_epilogue(const double *S, const double *m, int n, double *C) {
-    size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    size_t tot = (size_t)n * n;
-    if (idx >= tot) return;
-    int i = (int)(idx % n), j = (int)(idx / n);
+// sd[j] = sqrt(cov_jj) (the expression of the per-element form, once per column)
+__global__ void __launch_bounds__(256) k_cor_sd(const double *S, const double *m, int n, double *sd) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
     const double fn = (double)n, fn1 = (double)(n - 1);
-    double cij = (S[idx] - fn * (m[i] * m[j])) / fn1;
-    double cii = (S[(size_t)i * n + i] - fn * (m[i] * m[i])) / fn1;
-    double cjj = (S[(size_t)j * n + j] - fn * (m[j] * m[j])) / fn1;
-    double v = cij / (sqrt(cii) * sqrt(cjj));
-    if (isnan(v)) v = 0.0;
-    C[idx] = v;
+    sd[j] = sqrt((S[(size_t)j * n + j] - fn * (m[j] * m[j])) / fn1);
 }
 
-void launch_cor_epilogue(const double *d_S, const double *d_m, int n, double *d_C, hipStream_t s) {
+// two elements of one column per thread (n even: a 16-byte pair; else scalar)
+__global__ void __launch_bounds__(256) k_cor_epilogue(const double *S, const double *m, const double *sd, int n,
+                                                      double *C) {
+    const size_t tot = (size_t)n * n;
+    const size_t idx = 2 * ((size_t)blockIdx.x * blockDim.x + threadIdx.x);
+    if (idx >= tot) return;
+    const double fn = (double)n, fn1 = (double)(n - 1);
+    auto one = [&](size_t id, double sij) {
+        const int i = (int)(id % n), j = (int)(id / n);
+        const double cij = (sij - fn * (m[i] * m[j])) / fn1;
+        double v = cij / (sd[i] * sd[j]);
+        if (isnan(v)) v = 0.0;
+        return v;
+    };
+    if ((n & 1) == 0) {
+        const double2 x = *(const double2 *)(S + idx);
+        double2 y;
+        y.x = one(idx, x.x);
+        y.y = one(idx + 1, x.y);
+        *(double2 *)(C + idx) = y;
+    } else {
+        C[idx] = one(idx, S[idx]);
+        if (idx + 1 < tot) C[idx + 1] = one(idx + 1, S[idx + 1]);
+    }
+}
+
+void launch_cor_epilogue(const double *d_S, const double *d_m, int n, double *d_C, double *d_sd, hipStream_t s) {
     size_t tot = (size_t)n * n;
-    hipLaunchKernelGGL(k_cor_epilogue, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, d_S, d_m, n, d_C);
+    hipLaunchKernelGGL(k_cor_sd, dim3((n + 255) / 256), dim3(256), 0, s, d_S, d_m, n, d_sd);
+    const size_t th = (tot + 1) / 2;
+    hipLaunchKernelGGL(k_cor_epilogue, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, s, d_S, d_m, d_sd, n, d_C);
     TP_HIP(hipGetLastError());
 }
 

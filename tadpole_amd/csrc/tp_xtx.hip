@@ -39,7 +39,19 @@ __global__ void __launch_bounds__(256) k_int_scan(const double *X, size_t cnt, u
     int bad = 0;
     const size_t n2 = cnt / 2;
     const double2 *X2 = (const double2 *)X;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n2; i += (size_t)gridDim.x * blockDim.x) {
+    const size_t G = (size_t)gridDim.x * blockDim.x;
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + 3 * G < n2; i += 4 * G) {   // four 16-byte loads in flight per thread
+        double2 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = X2[i + u * G];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            bad |= !(v[u].x >= 0.0) || v[u].x != floor(v[u].x) || !(v[u].y >= 0.0) || v[u].y != floor(v[u].y);
+            m = fmax(m, fmax(v[u].x, v[u].y));
+        }
+    }
+    for (; i < n2; i += G) {
         const double2 v = X2[i];
         bad |= !(v.x >= 0.0) || v.x != floor(v.x) || !(v.y >= 0.0) || v.y != floor(v.y);
         m = fmax(m, fmax(v.x, v.y));
@@ -256,7 +268,7 @@ int xtx_int_slices(Ctx &c, const double *d_X, int n) {
     int *flag = (int *)(mb + 1);
     TP_HIP(hipMemsetAsync(mb, 0, 16, c.cur));
     const size_t cnt = (size_t)n * n;
-    const unsigned g = (unsigned)std::max<size_t>(1, std::min<size_t>(512, (cnt / 2 + 255) / 256));
+    const unsigned g = (unsigned)std::max<size_t>(1, std::min<size_t>(2048, (cnt / 2 + 255) / 256));
     hipLaunchKernelGGL(k_int_scan, dim3(g), dim3(256), 0, c.cur, d_X, cnt, mb, flag);
     TP_HIP(hipGetLastError());
     unsigned long long h[2] = {0, 0};
