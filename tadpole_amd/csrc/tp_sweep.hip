@@ -56,6 +56,9 @@ __device__ __forceinline__ int pin(int x) {
     asm volatile("" : "+v"(x));
     return x;
 }
+// three loads pinned together: one wait for all of them (pinning each load
+// separately waits for it before the next is issued -- serial LDS round trips)
+__device__ __forceinline__ void pin3(int &a, int &b, int &c) { asm volatile("" : "+v"(a), "+v"(b), "+v"(c)); }
 __device__ __forceinline__ double pin_d(double x) {
     asm volatile("" : "+v"(x));
     return x;
@@ -295,9 +298,10 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
         return m;
     };
     auto merge_at2 = [&](Mg &m) {   // second level: the right ends of r and rr, the cluster left of ls
-        const int erv = pin(rn[m.ea + 1 < n ? m.ea + 1 : DL]);
-        const int llv = pin(link[m.ls > 0 ? m.ls - 1 : DL]);
-        const int rrev = pin(rn[m.r >= 0 ? m.r : DL]);
+        int erv = rn[m.ea + 1 < n ? m.ea + 1 : DL];
+        int llv = link[m.ls > 0 ? m.ls - 1 : DL];
+        int rrev = rn[m.r >= 0 ? m.r : DL];
+        pin3(erv, llv, rrev);
         m.er = m.r >= 0 ? erv : -1;
         m.ll = m.ls > 0 ? llv : -1;
         m.rre = rrev;
@@ -396,11 +400,9 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
             rn[ls >= 0 ? ls : DL] = eb;
             // links the two candidate merges next to m need (independent of a2:
             // issued before the argmin's reductions so their latency overlaps)
-            const int m1llv = pin(link[cur.ll > 0 ? cur.ll - 1 : DL]);
-            const int m2erv = pin(rn[r >= 0 ? r : DL]);
-            const int m2rrev = pin(rn[(r >= 0 && er + 1 < n) ? er + 1 : DL]);
-            const int m1ll = cur.ll > 0 ? m1llv : -1;
-            const int m2er = (r >= 0 && er + 1 < n) ? m2erv : -1;
+            int m1llv = link[cur.ll > 0 ? cur.ll - 1 : DL];
+            int m2erv = rn[r >= 0 ? r : DL];
+            int m2rrev = rn[(r >= 0 && er + 1 < n) ? er + 1 : DL];
             // refresh the three touched blocks and, concurrently, the minimum of
             // the untouched ones: four interleaved wave reductions
             const int ba = a >> 6, bb = b >> 6, bl = ls >= 0 ? (ls >> 6) : ba;
@@ -438,6 +440,9 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
             //      clusters go to B at once (its row prefetch starts before X)
             Mg m0 = merge_at1(a2 >= 0 ? a2 : a);
             merge_at2(m0);
+            pin3(m1llv, m2erv, m2rrev);   // issued before the reductions; waited for only here
+            const int m1ll = cur.ll > 0 ? m1llv : -1;
+            const int m2er = (r >= 0 && er + 1 < n) ? m2erv : -1;
             {   // a2's four rows (absent ls / r: -1), singletons flagged
                 const int bs2 = m0.ea + 1 < n ? m0.ea + 1 : m0.a;
                 mb_i[3] = make_int4(rowc(m0.a, m0.ea == m0.a), rowc(bs2, m0.eb == bs2),
