@@ -49,11 +49,19 @@ class Chclust:
     merge: np.ndarray            # (n-1) x 2 int, hclust encoding
     height: np.ndarray           # n-1 cumulative total dispersion
     order: np.ndarray            # 1..n
-    labels: List[str]            # original bin indices
+    label_ids: np.ndarray        # original bin indices (R's labels, as integers)
     boundary: np.ndarray         # 1-based first bin (in 1..n) of the right cluster per merge
     method: str = "coniss"
     dist_method: str = "euclidean"
     call: str = "rioja::chclust(d = dist(pcs))"
+
+    @property
+    def labels(self) -> List[str]:
+        """R's ``labels`` (character): built on first use, not per pipeline."""
+        lab = self.__dict__.get("_labels")
+        if lab is None:
+            lab = self.__dict__["_labels"] = np.asarray(self.label_ids, np.int64).astype(str).tolist()
+        return lab
 
     @property
     def n(self) -> int:
@@ -434,7 +442,7 @@ def _assemble(res, bad_idx1) -> Tadpole:
     n = len(res["good"])
     good1 = np.asarray(res["good"])
     dendro = Chclust(merge=res["merge"], height=res["height"], order=np.arange(1, n + 1),
-                     labels=good1.astype(np.int64).astype(str).tolist(), boundary=res["boundary"])
+                     label_ids=good1, boundary=res["boundary"])
     t = Tadpole(n_pcs=res["n_pcs"], optimal_n_clusters=res["n_clusters"], dendro=dendro,
                 scores=res["scores"], bad_columns=bad_idx1, timings_ms=res["timings"])
     row = res["scores"][res["n_pcs"] - 1]
@@ -450,9 +458,37 @@ def _assemble(res, bad_idx1) -> Tadpole:
         rank[order] = np.arange(1, len(names) + 1)
         pos = rank[:n]
     bnd = np.asarray(res["boundary"], np.int64)
-    for kk in levels:
-        t.clusters[str(int(kk))] = _level_coords(bnd, n, int(kk), pos)
+    for kk, co in zip(levels, _all_level_coords(bnd, n, levels, pos)):
+        t.clusters[str(int(kk))] = co
     return t
+
+
+def _all_level_coords(boundary, n, levels, pos):
+    """``_level_coords`` of every level at once (the cuts are nested: the cut
+    into kk clusters is the cut into kk - 1 plus boundary[n - kk]): one sort of
+    the deepest level's boundaries, each level's subset taken in that order."""
+    levels = np.asarray(levels, np.int64)
+    if len(levels) == 0:
+        return []
+    L = int(levels.max())
+    B = boundary[n - L:] if L > 1 else boundary[:0]          # boundary[n - L + j] joins at kk >= L - j
+    order = np.argsort(B, kind="stable")
+    vals = B[order] - 1
+    joins = (L - np.arange(len(B)))[order]
+    M = joins[None, :] <= levels[:, None]                   # level x sorted boundary
+    lev_i, col = np.nonzero(M)                              # row-major: each level's boundaries ascending
+    b = vals[col]
+    cnt = levels - 1
+    off = np.concatenate([[0], np.cumsum(levels)])          # level l occupies rows off[l] .. off[l+1]-1
+    out = np.empty((int(off[-1]), 2), np.int64)
+    out[off[:-1], 0] = pos[0]
+    out[off[1:] - 1, 1] = pos[n - 1]
+    first = np.concatenate([[0], np.cumsum(cnt)])[:-1]
+    rank = np.arange(len(b)) - np.repeat(first, cnt)        # position of each boundary within its level
+    rows = off[lev_i] + rank
+    out[rows + 1, 0] = pos[b]
+    out[rows, 1] = pos[b - 1]
+    return [out[off[l]:off[l + 1]] for l in range(len(levels))]
 
 
 def _assemble_rle(t, dendro, levels, good1, bad_idx1) -> Tadpole:

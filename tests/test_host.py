@@ -16,7 +16,7 @@ GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 def _chclust(mb, n):
     return api.Chclust(merge=np.zeros((n - 1, 2), np.int32), height=np.arange(n - 1, dtype=float),
-                       order=np.arange(1, n + 1), labels=[str(i) for i in range(1, n + 1)],
+                       order=np.arange(1, n + 1), label_ids=np.arange(1, n + 1),
                        boundary=np.asarray(mb) + 1)
 
 
