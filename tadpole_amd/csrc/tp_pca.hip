@@ -101,7 +101,7 @@ static void orth_cholqr(Ctx &c, double *Z, double *Qout, double *Tmp, int n, int
     for (int p = 0; p < passes; ++p) {
         GemmArgs g{b, b, n, src, n, true, src, n, W, b};
         g.sym_upper = true;
-        g.splitk = std::max(1, std::min(32, n / 128));
+        g.splitk = 0;   // auto: deep split for few-tile Gram matrices (tp_gemm.hip)
         gemm_f64(g, c.buf[S_PARTIAL], c.cur);
         double *dst = ((passes - 1 - p) % 2 == 0) ? Qout : Tmp;   // last pass lands in Qout
         if (b <= kCholInvMax && b % 16 == 0) {
