@@ -636,541 +636,6 @@ template __global__ void k_coniss_t<true, 2, false>(SweepDev, double *);
 template __global__ void k_coniss_t<true, 3, false>(SweepDev, double *);
 template __global__ void k_coniss_t<true, 16, true>(SweepDev, double *);
 
-// ===================================================== batched CONISS
-// One wave per tree; several merges per step (design: tools/coniss_llist_model.py
-// and tools/coniss_batch_model.py, both checked merge for merge against the
-// oracle's CONISS).
-//
-// Candidate list.  Lane j holds entry j of a list L of (cost, position) pairs
-// sorted lexicographically (live entries in lane order; dead lanes are holes),
-// complete below a bound T: every current adjacent cost (c, p) <lex T is a live
-// entry.  A merge kills the entries of its three touched positions and inserts
-// its two new costs when they are <lex T (a full list drops its last entry and
-// T becomes that entry).  The next merge is the first live entry; an exhausted
-// list is rebuilt from 16-position block minima kept in LDS as float keys
-// rounded down (a lower bound per block is all the rebuild needs).
-//
-// Batch.  The first KB live entries are taken in order while no later one
-// shares a merged cluster with an earlier one's window (ls, a, b, r): such
-// merges change disjoint rows and costs, so their new costs are computed from
-// the pre-batch rows, all rows loaded at once (one memory latency per batch).
-// Candidate j is the true next merge iff (c_j, p_j) <lex every new cost made by
-// candidates before it (everything else is either a later list entry or
-// >=lex T); the leading run of such candidates is applied.  Same merges,
-// records and arithmetic (ward_part, the canonical wave sums, the divisions)
-// as coniss_tree2: bit-identical.
-constexpr int CB_BR = 10;      // block keys per lane: 16-position blocks <= 640 (n <= 10240)
-constexpr int CB_KBLK = 12;    // blocks gathered per rebuild (3 rounds of 4 x 16 lanes)
-constexpr int CB_ROUNDS = 3;
-constexpr int CB_KBMAX = 8;
-constexpr unsigned CB_TOP = 0x7F800001u;   // block key bound past +inf: every non-NaN cost
-
-struct CbCand {
-    int a, ea, eb, ls;
-    int r, er, pad0, pad1;
-    double c, pad2;
-};
-
-__device__ __forceinline__ bool lexlt(double c1, int p1, double c2, int p2) {
-    return (c1 < c2) | ((c1 == c2) & (p1 < p2));
-}
-// block key: the float at or below c, as ordered bits (costs are >= 0); NaN -> ~0
-__device__ __forceinline__ unsigned fkey(double c) {
-    if (isnan(c)) return 0xFFFFFFFFu;
-    const unsigned u = __float_as_uint(__double2float_rd(c));
-    return (u >> 31) ? 0u : u;
-}
-__device__ __forceinline__ unsigned umin_(unsigned a, unsigned b) { return a < b ? a : b; }
-__device__ __forceinline__ unsigned wave_min_u(unsigned v) {
-    v = umin_(v, (unsigned)dpp_i<0xB1>((int)v));
-    v = umin_(v, (unsigned)dpp_i<0x4E>((int)v));
-    v = umin_(v, (unsigned)dpp_i<0x141>((int)v));
-    v = umin_(v, (unsigned)dpp_i<0x140>((int)v));
-    v = umin_(v, (unsigned)dpp_i<0x142>((int)v));
-    v = umin_(v, (unsigned)dpp_i<0x143>((int)v));
-    return (unsigned)__builtin_amdgcn_readlane((int)v, 63);
-}
-__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
-#pragma unroll
-    for (int m = 1; m < 64; m <<= 1) {
-        const unsigned long long o = __shfl_xor(v, m, 64);
-        v = o < v ? o : v;
-    }
-    return v;
-}
-// minimum over each 16-lane row (NaN ignored), in every lane of the row
-__device__ __forceinline__ double row_min16(double v) {
-    v = vmin(v, dpp_d<0xB1>(v));
-    v = vmin(v, dpp_d<0x4E>(v));
-    v = vmin(v, dpp_d<0x141>(v));
-    v = vmin(v, dpp_d<0x140>(v));
-    return v;
-}
-__device__ __forceinline__ int lanes_below(unsigned long long m) {
-    return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-}
-// wave shift right by one lane (lane 0 reads 0)
-__device__ __forceinline__ int shr1_i(int v) { return __builtin_amdgcn_mov_dpp(v, 0x138, 0xF, 0xF, true); }
-__device__ __forceinline__ double shr1_d(double v) {
-    return __hiloint2double(shr1_i(__double2hiint(v)), shr1_i(__double2loint(v)));
-}
-
-struct CbShared {
-    CbCand cand[CB_KBMAX];
-    int4 win[CB_KBMAX];
-    double stc[64];
-    int stp[64];
-    int blist[16];
-    int tbl[3 * CB_KBMAX + 4];
-};
-
-// STAMPS: diagnostic build, s_memtime cycles per phase into sd.stamps[tree * 16 +
-// phase] (0 rebuild, 1 candidates, 2 row loads + new costs, 3 validity + apply,
-// 4 block keys) and counters (8 batches, 9 rebuilds, 10 slow rebuilds).
-template <bool STAMPS, int NS, int KB>
-__device__ __forceinline__ void coniss_batch(const SweepDev &sd, const double *cost0, double *lds, CbShared &sh) {
-    long long st_acc[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    long long st_t0 = STAMPS ? (long long)__builtin_amdgcn_s_memtime() : 0;
-#define TP_STAMP(ph)                                                      \
-    if (STAMPS) {                                                         \
-        long long _t = (long long)__builtin_amdgcn_s_memtime();           \
-        st_acc[ph] += _t - st_t0;                                         \
-        st_t0 = _t;                                                       \
-    }
-    const int n = sd.n;
-    const int ti = blockIdx.x;
-    const int i = sd.tree0 + ti + 1;
-    constexpr int ld = NS * 64;
-    const int lane = threadIdx.x;
-    const int nbk = (n + 63) / 64, nb16 = nbk * 4;
-    const double QNAN = __longlong_as_double(0x7FF8000000000000LL);
-    const double PINF = __longlong_as_double(0x7FF0000000000000LL);
-    const size_t cst = coniss_cost_stride(n), lst = coniss_link_stride(n);
-    double *cost = lds;
-    int *link = (int *)(cost + cst);
-    int *rn = link + lst;
-    unsigned *bkey = (unsigned *)(rn + lst);
-    const int DL = n;
-    double *S = sd.sums + sums_off(n, sd.tree0, i) + lane;
-    const double *P0 = sd.Pt + lane;
-    const int ldp = sd.ldp;
-    const bool last_in = lane + 64 * (NS - 1) < i;
-    int *mrg_a = sd.mrg_a + (size_t)ti * (n - 1);
-    int *mrg_b = sd.mrg_b + (size_t)ti * (n - 1);
-    double *mcost = sd.cost + (size_t)ti * (n - 1);
-    double *height = sd.height + (size_t)ti * (n - 1);
-    const double *c0 = cost0 + (size_t)ti * cst;
-
-    for (int bk = 0; bk < nbk; ++bk) {
-        const int p = bk * 64 + lane;
-        cost[p] = c0[p];
-        if (p < n) {
-            link[p] = p;
-            rn[p] = p + 1 < n ? p + 1 : -1;
-        }
-    }
-    link[DL + lane] = rn[DL + lane] = -1;
-    // 16-position block keys, four blocks per read
-    auto refresh4 = [&](int beta) {   // this lane's block (its 16-lane row's), -1: none
-        const double v = beta >= 0 ? cost[beta * 16 + (lane & 15)] : QNAN;
-        const double m = row_min16(v);
-        if (beta >= 0 && (lane & 15) == 0) bkey[beta] = fkey(m);
-    };
-    for (int r = 0; r < nbk; ++r) refresh4(4 * r + (lane >> 4));
-
-    auto load_row = [&](double (&dst)[NS], int code) {
-        code = __builtin_amdgcn_readfirstlane(code);
-        const int p = code & (ROW_PT - 1);
-        const double *pr = (code & ROW_PT) ? P0 + (size_t)p * ldp : S + (size_t)p * ld;
-#pragma unroll
-        for (int t = 0; t < NS; ++t) dst[t] = pr[64 * t];
-    };
-    auto rowc = [](int start, bool single) { return start | (single ? ROW_PT : 0); };
-
-    // ---- the list
-    double Lc = PINF, Tc = PINF;
-    int Lp = 0x7FFFFFFF, lv = 0, Tp = 0x7FFFFFFF;
-
-    auto rebuild = [&]() {
-        unsigned bk[CB_BR];
-        unsigned mn = 0xFFFFFFFFu;
-#pragma unroll
-        for (int q = 0; q < CB_BR; ++q) {
-            const int beta = q * 64 + lane;
-            bk[q] = beta < nb16 ? bkey[beta] : 0xFFFFFFFFu;
-            mn = umin_(mn, bk[q]);
-        }
-        mn = wave_min_u(mn);
-        auto bcount = [&](unsigned tk) {
-            int c = 0;
-#pragma unroll
-            for (int q = 0; q < CB_BR; ++q) c += __popcll(__ballot(bk[q] < tk));
-            return c;
-        };
-        bool slow = mn == 0xFFFFFFFFu;
-        unsigned tk = CB_TOP;
-        if (!slow && bcount(CB_TOP) > CB_KBLK) {
-            unsigned lo = mn + 1, hi = CB_TOP;   // bcount(lo) >= 1, bcount(hi) > KBLK
-            if (bcount(lo) > CB_KBLK) {
-                slow = true;
-            } else {
-                while (hi - lo > 1) {
-                    const unsigned mid = lo + (hi - lo) / 2;
-                    const int c = bcount(mid);
-                    if (c <= CB_KBLK) {
-                        lo = mid;
-                        if (2 * c >= CB_KBLK) break;
-                    } else {
-                        hi = mid;
-                    }
-                }
-                tk = lo;
-            }
-        }
-        double ec[CB_ROUNDS];
-        int ep[CB_ROUNDS];
-        bool ev[CB_ROUNDS];
-        int C = 0;
-        if (!slow) {
-            if (tk == CB_TOP) {
-                Tc = PINF;
-                Tp = 0x7FFFFFFF;
-            } else {
-                Tc = (double)__uint_as_float(tk);
-                Tp = -1;
-            }
-            int nb = 0;
-#pragma unroll
-            for (int q = 0; q < CB_BR; ++q) {
-                const bool in = bk[q] < tk;
-                const unsigned long long m = __ballot(in);
-                if (in) sh.blist[nb + lanes_below(m)] = q * 64 + lane;
-                nb += __popcll(m);
-            }
-#pragma unroll
-            for (int r = 0; r < CB_ROUNDS; ++r) {
-                const int idx = 4 * r + (lane >> 4);
-                const int beta = idx < nb ? sh.blist[idx] : -1;
-                const int pos = beta * 16 + (lane & 15);
-                const double c = beta >= 0 ? cost[beta >= 0 ? pos : 0] : QNAN;
-                ec[r] = c;
-                ep[r] = pos;
-                ev[r] = beta >= 0 && lexlt(c, pos, Tc, Tp);
-                C += __popcll(__ballot(ev[r]));
-            }
-            if (C > 64) {   // lower T to the largest c* with #(c < c*) <= 64
-                auto key = [](double c) { return (unsigned long long)__double_as_longlong(c); };
-                unsigned long long km = ~0ull;
-#pragma unroll
-                for (int r = 0; r < CB_ROUNDS; ++r) km = ev[r] && key(ec[r]) < km ? key(ec[r]) : km;
-                km = wave_min_u64(km);
-                auto ecount = [&](unsigned long long t) {
-                    int c = 0;
-#pragma unroll
-                    for (int r = 0; r < CB_ROUNDS; ++r) c += __popcll(__ballot(ev[r] && key(ec[r]) < t));
-                    return c;
-                };
-                unsigned long long lo = km + 1, hi = Tp == 0x7FFFFFFF ? key(PINF) + 1 : key(Tc);
-                if (ecount(lo) > 64) {
-                    slow = true;
-                } else {
-                    while (hi - lo > 1) {
-                        const unsigned long long mid = lo + (hi - lo) / 2;
-                        const int c = ecount(mid);
-                        if (c <= 64) {
-                            lo = mid;
-                            if (2 * c >= 64) break;
-                        } else {
-                            hi = mid;
-                        }
-                    }
-                    Tc = __longlong_as_double((long long)lo);
-                    Tp = -1;
-                    C = 0;
-#pragma unroll
-                    for (int r = 0; r < CB_ROUNDS; ++r) {
-                        ev[r] = ev[r] && ec[r] < Tc;
-                        C += __popcll(__ballot(ev[r]));
-                    }
-                }
-            }
-        }
-        if (!slow) {
-            int base = 0;
-#pragma unroll
-            for (int r = 0; r < CB_ROUNDS; ++r) {
-                const unsigned long long m = __ballot(ev[r]);
-                if (ev[r]) {
-                    sh.stc[base + lanes_below(m)] = ec[r];
-                    sh.stp[base + lanes_below(m)] = ep[r];
-                }
-                base += __popcll(m);
-            }
-            const double mc = lane < C ? sh.stc[lane] : PINF;
-            const int mp = lane < C ? sh.stp[lane] : 0x7FFFFFFF;
-            int rank = 0;
-            for (int x = 0; x < C; ++x) rank += lexlt(sh.stc[x], sh.stp[x], mc, mp) ? 1 : 0;
-            if (lane < C) {
-                sh.stc[rank] = mc;
-                sh.stp[rank] = mp;
-            }
-            Lc = lane < C ? sh.stc[lane] : PINF;
-            Lp = lane < C ? sh.stp[lane] : 0x7FFFFFFF;
-            lv = lane < C;
-        } else {
-            // degenerate ties: the lexicographic minimum alone, T just past it
-            if (STAMPS) ++st_acc[10];
-            double bc = QNAN;
-            int bp = 0x7FFFFFFF;
-            for (int b = 0; b < nbk; ++b) {
-                const int p = b * 64 + lane;
-                const double c = cost[p];
-                const bool u = !isnan(c) && (bp == 0x7FFFFFFF || c < bc);
-                bc = u ? c : bc;
-                bp = u ? p : bp;
-            }
-            const double m = wave_min(bc);
-            unsigned long long pm = (bc == m) ? (unsigned long long)bp : ~0ull;
-            pm = wave_min_u64(pm);
-            Lc = m;
-            Lp = (int)pm;
-            lv = lane == 0;
-            Tc = m;
-            Tp = (int)pm + 1;
-        }
-    };
-    auto insert = [&](double c, int p) {   // (c, p) <lex T
-        const unsigned long long lm = __ballot(lv);
-        const unsigned long long gm = __ballot(lv && lexlt(c, p, Lc, Lp));
-        const int q = gm ? (int)__builtin_ctzll(gm) : (lm ? 64 - (int)__builtin_clzll(lm) : 0);
-        if (q > 0 && !((lm >> (q - 1)) & 1ull)) {   // a hole right below: no shift
-            if (lane == q - 1) {
-                Lc = c;
-                Lp = p;
-                lv = 1;
-            }
-            return;
-        }
-        if (q == 64) {   // past a full list: the new entry becomes the bound
-            Tc = c;
-            Tp = p;
-            return;
-        }
-        const unsigned long long holes = ~lm & (~0ull << q);
-        const int z = holes ? (int)__builtin_ctzll(holes) : 63;   // lanes q..z shift up (z = 63: lane 63 drops)
-        if (!holes) {
-            Tc = readlane_d(Lc, 63);
-            Tp = __builtin_amdgcn_readlane(Lp, 63);
-        }
-        const double sc = shr1_d(Lc);
-        const int sp = shr1_i(Lp), sv = shr1_i(lv);
-        if (lane == q) {
-            Lc = c;
-            Lp = p;
-            lv = 1;
-        } else if (lane > q && lane <= z) {
-            Lc = sc;
-            Lp = sp;
-            lv = sv;
-        }
-    };
-
-    rebuild();
-    int done = 0;
-    double h = 0.0;
-    while (done < n - 1) {
-        unsigned long long lm = __ballot(lv);
-        TP_STAMP(5);
-        if (!lm) {
-            rebuild();
-            lm = __ballot(lv);
-            if (STAMPS) ++st_acc[9];
-        }
-        if (STAMPS) ++st_acc[8];
-        TP_STAMP(0);
-        // ---- candidates: the first KB live entries and their windows
-        const int rk = lanes_below(lm);
-        const bool cnd = lv && rk < KB;
-        const int nc = __popcll(lm) < KB ? __popcll(lm) : KB;
-        const int p = cnd ? Lp : 0;
-        int ea = link[p], eb = rn[p], lsv = link[p > 0 ? p - 1 : DL];
-        pin3(ea, eb, lsv);
-        const int bb = ea + 1 < n ? ea + 1 : DL;
-        const int erv = rn[bb];
-        const int ls = p > 0 ? lsv : -1;
-        const int r = (eb >= 0 && eb + 1 < n) ? eb + 1 : -1;
-        const int er = r >= 0 ? erv : -1;
-        const int wl = ls >= 0 ? ls : p, wr = r >= 0 ? er : eb;
-        if (cnd) {
-            sh.win[rk] = make_int4(p, eb, wl, wr);
-            CbCand cd;
-            cd.a = p;
-            cd.ea = ea;
-            cd.eb = eb;
-            cd.ls = ls;
-            cd.r = r;
-            cd.er = er;
-            cd.pad0 = cd.pad1 = 0;
-            cd.c = Lc;
-            cd.pad2 = 0.0;
-            sh.cand[rk] = cd;
-        }
-        // a candidate conflicts with an earlier one when either's merged pair
-        // meets the other's window (bins: clusters partition them)
-        bool conf = false;
-#pragma unroll
-        for (int q = 0; q < KB - 1; ++q) {
-            if (q < nc - 1) {
-                const int4 w = sh.win[q];
-                const bool ov = (w.x <= wr && wl <= w.y) || (p <= w.w && w.z <= eb);
-                conf = conf || (q < rk && ov);
-            }
-        }
-        const unsigned long long cm = __ballot(cnd && conf);
-        const int A = cm ? __builtin_amdgcn_readlane(rk, (int)__builtin_ctzll(cm)) : nc;
-        TP_STAMP(1);
-        // ---- rows of the accepted candidates, all loads in flight together
-        CbCand cd[KB];
-        double ra[KB][NS], rb[KB][NS], rl[KB][NS], rr[KB][NS];
-#pragma unroll
-        for (int q = 0; q < KB; ++q) {
-            if (q < A) {
-                cd[q] = sh.cand[q];
-                const int a = cd[q].a, b = cd[q].ea + 1;
-                const int ac = rowc(a, cd[q].ea == a);
-                load_row(ra[q], ac);
-                load_row(rb[q], rowc(b, cd[q].eb == b));
-                load_row(rl[q], cd[q].ls >= 0 ? rowc(cd[q].ls, cd[q].ls == a - 1) : ac);
-                load_row(rr[q], cd[q].r >= 0 ? rowc(cd[q].r, cd[q].er == cd[q].r) : ac);
-            }
-        }
-        // ---- merged sums and the two new costs of each candidate
-        double ncl[KB], ncr[KB];
-#pragma unroll
-        for (int q = 0; q < KB; ++q) {
-            if (q < A) {
-                const int a = cd[q].a;
-                const double fm = (double)(cd[q].eb - a + 1);
-                const double fl = (double)(cd[q].ls >= 0 ? a - cd[q].ls : 0);
-                const double fr = (double)(cd[q].r >= 0 ? cd[q].er - cd[q].r + 1 : 0);
-#pragma unroll
-                for (int t = 0; t < NS; ++t) ra[q][t] = ra[q][t] + rb[q][t];
-                double ul = ward_part<NS>(rl[q], fl, ra[q], fm, last_in);
-                double ur = ward_part<NS>(ra[q], fm, rr[q], fr, last_in);
-                wave_sum2(ul, ur);
-                const double ql = pin_d(ul / (fl * fm * (fl + fm)));
-                const double qr = pin_d(ur / (fm * fr * (fm + fr)));
-                ncl[q] = cd[q].ls >= 0 ? nan2inf(ql) : QNAN;
-                ncr[q] = cd[q].r >= 0 ? nan2inf(qr) : QNAN;
-            }
-        }
-        TP_STAMP(2);
-        // ---- the leading run of candidates that are the true next merges
-        int V = A;
-        {
-            double pc = PINF;
-            int pp = 0x7FFFFFFF;
-#pragma unroll
-            for (int q = 0; q < KB; ++q) {
-                if (q < V) {
-                    if (q > 0 && !lexlt(cd[q].c, cd[q].a, pc, pp)) {
-                        V = q;
-                    } else {
-                        if (cd[q].ls >= 0 && lexlt(ncl[q], cd[q].ls, pc, pp)) {
-                            pc = ncl[q];
-                            pp = cd[q].ls;
-                        }
-                        if (cd[q].r >= 0 && lexlt(ncr[q], cd[q].a, pc, pp)) {
-                            pc = ncr[q];
-                            pp = cd[q].a;
-                        }
-                    }
-                }
-            }
-        }
-        // ---- apply them in order
-#pragma unroll
-        for (int q = 0; q < KB; ++q) {
-            if (q < V) {
-                const int a = cd[q].a, b = cd[q].ea + 1, eb_ = cd[q].eb, ls_ = cd[q].ls, r_ = cd[q].r;
-                const double cc = cd[q].c;
-                h = h + cc;
-                mrg_a[done] = a;
-                mrg_b[done] = b;
-                mcost[done] = cc;
-                height[done] = h;
-                ++done;
-#pragma unroll
-                for (int t = 0; t < NS; ++t) S[(size_t)a * ld + 64 * t] = ra[q][t];
-                link[a] = eb_;
-                link[eb_] = a;
-                rn[a] = cd[q].er;
-                rn[ls_ >= 0 ? ls_ : DL] = eb_;
-                cost[b] = QNAN;
-                cost[a] = ncr[q];
-                if (ls_ >= 0) cost[ls_] = ncl[q];
-                lv = lv && Lp != a && Lp != b && Lp != ls_;
-                if (ls_ >= 0 && lexlt(ncl[q], ls_, Tc, Tp)) insert(ncl[q], ls_);
-                if (r_ >= 0 && lexlt(ncr[q], a, Tc, Tp)) insert(ncr[q], a);
-                sh.tbl[3 * q] = (ls_ >= 0 ? ls_ : a) >> 4;
-                sh.tbl[3 * q + 1] = a >> 4;
-                sh.tbl[3 * q + 2] = b >> 4;
-            }
-        }
-        TP_STAMP(3);
-        // ---- block keys of the touched blocks (after every write of the batch)
-        for (int r4 = 0; r4 < 3 * V; r4 += 4) {
-            const int idx = r4 + (lane >> 4);
-            refresh4(idx < 3 * V ? sh.tbl[idx] : -1);
-        }
-        if (STAMPS) {   // waits for the refresh's LDS traffic
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        }
-        TP_STAMP(4);
-    }
-    __syncthreads();
-    // ---- broken stick (rioja bstick.chclust, vegan bstick.default) on heights
-    if (threadIdx.x == 0) {
-        const int nobj = n - 1;
-        int ncl = -1;
-        if (nobj >= 2) {
-            const double tot = height[nobj - 1];
-            double *cs = cost;
-            double hi = 0.0, lo = 0.0;
-            for (int t = 1; t <= nobj; ++t) {
-                dd_add_d(hi, lo, tot / (double)(nobj - t + 1));
-                cs[t - 1] = hi + lo;
-            }
-            int run = 0;
-            bool started = false;
-            for (int j = 1; j <= nobj - 1; ++j) {
-                double disp = fabs(height[nobj - 1 - j] - height[nobj - j]);
-                double bs = cs[nobj - j] / (double)nobj;
-                if (disp > bs) { started = true; ++run; }
-                else if (started) break;
-            }
-            ncl = started ? run : -1;
-        }
-        sd.n_cluster[ti] = ncl;
-    }
-    if (STAMPS && lane == 0)
-        for (int q = 0; q < 11; ++q) sd.stamps[(size_t)ti * 16 + q] = st_acc[q];
-#undef TP_STAMP
-}
-
-template <bool STAMPS>
-__global__ void __launch_bounds__(64) k_coniss_b(SweepDev sd, double *cost0) {
-    extern __shared__ double lds[];
-    __shared__ CbShared sh;
-    const int i = sd.tree0 + blockIdx.x + 1;
-    switch ((i + 63) / 64) {
-        case 1: coniss_batch<STAMPS, 1, 8>(sd, cost0, lds, sh); break;
-        case 2: coniss_batch<STAMPS, 2, 8>(sd, cost0, lds, sh); break;
-        case 3: coniss_batch<STAMPS, 3, 8>(sd, cost0, lds, sh); break;
-        default: coniss_batch<STAMPS, 4, 6>(sd, cost0, lds, sh); break;
-    }
-}
-
 // ------------------------------------------------------------ CH over cuts
 // canonical segment statistics of rows s..e, by one wave (see tpo_seg_ss)
 // RB rows per batch (RB x KMAXSLOT loads in flight); the order of the sums is
@@ -1591,31 +1056,11 @@ static void launch_coniss_bs(const SweepDev &sd, double *cost0, size_t lds, hipS
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL((k_coniss_t<STAMPS, BS, GLB>), dim3(sd.ntrees), dim3(128), lds, s, sd, cost0);
 }
-// batched kernel: costs, links, right ends and the 16-position block keys in LDS
-static size_t coniss_b_lds_bytes(int n) { return coniss_cost_stride(n) * 8 + coniss_link_stride(n) * 8 + (size_t)((n + 63) / 64) * 16; }
-static bool coniss_b_fits(int n) {
-    return g_coniss_batch && coniss_b_lds_bytes(n) + sizeof(CbShared) <= 160 * 1024 && (n + 63) / 64 * 4 <= 64 * CB_BR;
-}
-int g_coniss_batch = 0;   // off until it beats the two-wave kernel (tools/diag_kernels.py coniss)
-
 static void run_coniss(const SweepDev &sd, hipStream_t s, bool stamped, Ctx *prof) {
     const int nbk = (sd.n + 63) / 64;
     double *cost0 = sd.cost0;
     hipLaunchKernelGGL(k_seed, dim3(sd.ntrees, nbk), dim3(64), 0, s, sd, cost0);
     TP_HIP(hipGetLastError());
-    if (coniss_b_fits(sd.n)) {
-        const size_t lds = coniss_b_lds_bytes(sd.n);
-        const void *fn = stamped ? (const void *)k_coniss_b<true> : (const void *)k_coniss_b<false>;
-        TP_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        if (prof) kprof_begin(*prof, K_CONISS);
-        if (stamped)
-            hipLaunchKernelGGL(k_coniss_b<true>, dim3(sd.ntrees), dim3(64), lds, s, sd, cost0);
-        else
-            hipLaunchKernelGGL(k_coniss_b<false>, dim3(sd.ntrees), dim3(64), lds, s, sd, cost0);
-        if (prof) kprof_end(*prof, K_CONISS);
-        TP_HIP(hipGetLastError());
-        return;
-    }
     const bool in_lds = coniss_in_lds(sd.n);
     const size_t lds = in_lds ? coniss_lds_bytes(sd.n) : kConissGlbLds;
     const int bs = (nbk + 63) / 64;   // block-minimum slots per lane

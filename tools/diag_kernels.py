@@ -34,7 +34,7 @@ def chol(b=256, cond=1e6):
           f"trailing {ms[4]:.0f} prologue {ms[5]:.0f}", flush=True)
 
 
-def coniss(n0=2000, k=200, batch=True):
+def coniss(n0=2000, k=200):
     """Per-merge cycle budget of both CONISS waves on the scores of a synthetic
     matrix (mask on the host, correlation and PCA through the library)."""
     import tadpole_oracle as O
@@ -55,23 +55,11 @@ def coniss(n0=2000, k=200, batch=True):
     _lib.check(st)
     stamps = np.zeros(k * 16, np.int64)
     ms = ctypes.c_double(0)
-    old = ctypes.c_int(0)
-    L.tp_debug_knob(B(ctypes.c_int(14)), B(ctypes.c_int(1 if batch else 0)), B(old), B(st))
     for _ in range(2):   # second run: warm code objects
         L.tp_debug_coniss_stamps(p.ctypes.data_as(D), B(ctypes.c_int(n)), B(ctypes.c_int(k)),
                                  stamps.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)), B(ms), B(st))
         _lib.check(st)
     s = stamps.reshape(k, 16).astype(float) / (n - 1)
-    if batch:   # batched kernel: phases per merge, counters per tree
-        c = stamps.reshape(k, 16)
-        nb = {0: "rebuild", 1: "candidates", 2: "loads+costs", 3: "apply", 4: "block keys", 5: "loop"}
-        print(f"coniss (batched) n={n} k={k}: stamped kernel {ms.value:.3f} ms ({ms.value * 1e3 / (n - 1):.2f} us/merge)",
-              flush=True)
-        for i in (0, 63, 127, k - 1):
-            print(f"  tree {i + 1:3d}: " + ", ".join(f"{v} {s[i, q]:.0f}" for q, v in nb.items()) +
-                  f" (sum {sum(s[i, q] for q in nb):.0f}); merges/batch {(n - 1) / max(1, c[i, 8]):.2f}, "
-                  f"rebuilds {c[i, 9]} (slow {c[i, 10]})", flush=True)
-        return
     na = {6: "writes+block loads", 7: "reductions+argmin", 0: "merge_at+records", 1: "wait X", 2: "choice",
           3: "wait Y"}
     nb = {8: "rec read", 9: "row wait+sums", 10: "ward+records", 11: "wait X", 14: "prefetch", 15: "wait Y"}
@@ -133,6 +121,4 @@ if __name__ == "__main__":
         coniss()
     if "coniss3" in what:
         coniss(7808, 200)
-    if "coniss_old" in what:
-        coniss(2000, 200, batch=False)
-        coniss(7808, 200, batch=False)
+
