@@ -1251,7 +1251,8 @@ extern "C" {
 /* Test hook: set a tuning switch, *old = its previous value.  which: 0 CH
  * segment statistics shared across trees, 1 cap on their store (0 = automatic),
  * 2 short-K panel GEMM, 3 GEMM LDS stage depth (16 / 32), 4 register-resident
- * tridiagonalisation, 5 int8 X'X, 6 PCA degree margin, 7 XCD-aware GEMM order. */
+ * tridiagonalisation, 5 int8 X'X, 6 PCA degree margin, 7 XCD-aware GEMM order, ..., 14 supertile
+ * order of the int8 X'X tiles. */
 void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
     guarded(status, [&] {
         int *p = nullptr;
@@ -1270,6 +1271,7 @@ void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
         case 11: p = &g_chol_inv_waves; break;
         case 12: p = &g_gemm_splitk; break;
         case 13: p = &g_gemm_ts; break;
+        case 14: p = &g_xtx_supertile; break;
         default: fail(TP_ERR_ARG, "unknown knob");
         }
         if (*which == 3 && *value != 16 && *value != 32) fail(TP_ERR_ARG, "stage depth must be 16 or 32");

@@ -143,6 +143,7 @@ constexpr int kCholInvMax = 256;
 extern int g_chol_inv_waves;
 extern int g_gemm_splitk;
 extern int g_gemm_ts;
+extern int g_xtx_supertile;   // int8 X'X: XCD-contiguous supertile order of the 128 x 128 tiles (0: columns)
 // row-shardable products that take the 128 x 64 kernel with k chunks fixed by K
 // (tp_gemm.hip); shards and the unsharded call must agree on it
 inline bool rows_ts(int K, int N) { return g_gemm_ts > 0 && K >= 4096 && N <= 256; }

@@ -168,17 +168,59 @@ __global__ void __launch_bounds__(256) k_xtx_i8(const int8_t *__restrict__ S, in
 // (double-buffered, one barrier per block) so each slice fragment is read
 // from L2 once per workgroup instead of once per wave.  LDS rows are 80 B
 // (64 B of k + pad) per column.  Same exact arithmetic as k_xtx_i8.
-constexpr int XB = 128, XK = 64, XLD = 80;
+//
+// Tile order (whole triangle, tcol0 = 0 and tn tile columns): workgroups are
+// dealt round-robin over the 8 XCDs (blockIdx % 8); each XCD takes a contiguous
+// run of an order that walks 8 x 8 supertiles of the triangle (column by
+// column inside each), so the ~32-64 tiles one XCD holds at a time share 16
+// slice panels instead of one B panel and ~40 A panels (same tiles, same bits).
+// Sharded calls (tcol0 > 0) keep the column order.
+constexpr int XB = 128, XK = 64, XLD = 80, XST = 8;
+__device__ __forceinline__ void xtx_supertile(int L, int tn, int &bm, int &bn) {
+    const int U = (tn + XST - 1) / XST;
+    for (int Q = 0; Q < U; ++Q) {
+        const int w = min(XST, tn - XST * Q);
+        for (int P = 0; P <= Q; ++P) {
+            const int h = min(XST, tn - XST * P);
+            const int cnt = P < Q ? h * w : w * (w + 1) / 2;
+            if (L < cnt) {
+                if (P < Q) {
+                    bn = XST * Q + L / h;
+                    bm = XST * P + L % h;
+                } else {
+                    int c = 0;
+                    while (L > c) {
+                        L -= c + 1;
+                        ++c;
+                    }
+                    bn = XST * Q + c;
+                    bm = XST * P + L;
+                }
+                return;
+            }
+            L -= cnt;
+        }
+    }
+    bm = bn = 0;   // not reached for L < tn (tn + 1) / 2
+}
 template <int NS>
 __global__ void __launch_bounds__(512) k_xtx_i8_big(const int8_t *__restrict__ S, int n, int Kp, int Np,
-                                                    double *__restrict__ C, int tcol0) {
+                                                    double *__restrict__ C, int tcol0, int tn_all) {
     __shared__ __attribute__((aligned(16))) int8_t Ls[2][2][NS][XB * XLD];   // [buf][A/B][slice]
-    int id = blockIdx.x, bn = tcol0;
-    while (id > bn) {
-        id -= bn + 1;
-        ++bn;
+    int bm, bn;
+    if (tn_all > 0) {
+        const int total = tn_all * (tn_all + 1) / 2;
+        const int xcd = (int)blockIdx.x & 7, slot = (int)blockIdx.x >> 3;
+        xtx_supertile(xcd * (total >> 3) + min(xcd, total & 7) + slot, tn_all, bm, bn);
+    } else {
+        int id = blockIdx.x;
+        bn = tcol0;
+        while (id > bn) {
+            id -= bn + 1;
+            ++bn;
+        }
+        bm = id;
     }
-    const int bm = id;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int wm = (w & 1) * 64, wn = (w >> 1) * 32;
     const size_t slice = (size_t)Np * Kp;
@@ -301,6 +343,8 @@ const int8_t *xtx_slices(Ctx &c, const double *d_X, int n, int ns) {
     return sl;
 }
 
+int g_xtx_supertile = 1;
+
 // S (n x n) = X'X exactly on the upper tiles of tile columns [tc0, tc1) and
 // their mirrors, from ns slices.
 // 128-column tiles [tc0, tc1) (tile units of 128) by the LDS-staged kernel
@@ -311,8 +355,11 @@ void xtx_int8_tiles128(Ctx &c, const int8_t *sl, int n, int ns, double *d_S, int
     tc1 = tc1 < 0 ? tn : std::min(tn, tc1);
     if (tc1 <= tc0) return;
     const unsigned nb = (unsigned)((long)tc1 * (tc1 + 1) / 2 - (long)tc0 * (tc0 + 1) / 2);
-    if (ns == 1) hipLaunchKernelGGL(k_xtx_i8_big<1>, dim3(nb), dim3(512), 0, c.cur, sl, n, Kp, Np, d_S, tc0);
-    else if (ns == 2) hipLaunchKernelGGL(k_xtx_i8_big<2>, dim3(nb), dim3(512), 0, c.cur, sl, n, Kp, Np, d_S, tc0);
+    const int tn_all = (tc0 == 0 && tc1 == tn && g_xtx_supertile) ? tn : 0;
+    if (ns == 1)
+        hipLaunchKernelGGL(k_xtx_i8_big<1>, dim3(nb), dim3(512), 0, c.cur, sl, n, Kp, Np, d_S, tc0, tn_all);
+    else if (ns == 2)
+        hipLaunchKernelGGL(k_xtx_i8_big<2>, dim3(nb), dim3(512), 0, c.cur, sl, n, Kp, Np, d_S, tc0, tn_all);
     else fail(TP_ERR_ARG, "xtx_int8_tiles128: 1..2 slices");
     TP_HIP(hipGetLastError());
 }

@@ -25,5 +25,5 @@ for cfg in sys.argv[2:]:
     for w, v in olds:
         G.knob(w, v)
     tm = np.median(np.array(runs), axis=0)
-    print(f"{cfg or 'default'}: total {tm[4]:.2f} ms  pca {tm[2]:.2f} sweep {tm[3]:.2f}  G {tm[6]:.2f} "
+    print(f"{cfg or 'default'}: total {tm[4]:.2f} ms  cor {tm[1]:.3f}  pca {tm[2]:.2f} sweep {tm[3]:.2f}  G {tm[6]:.2f} "
           f"GQ {tm[7]:.2f} ({int(tm[8])})  iters {int(tm[11])} resid {tm[13]:.1e} krylov {int(tm[16])}x{int(tm[17])}", flush=True)
