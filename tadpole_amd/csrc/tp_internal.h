@@ -88,7 +88,7 @@ enum Slot {
     S_M = 0, S_ROWMEAN, S_DIAG, S_BAD, S_GOOD, S_NGOOD, S_X, S_COLMEAN,
     S_S, S_C, S_XC, S_XCT, S_G, S_Q, S_Z, S_W, S_SMALL, S_P, S_PT,
     S_SWEEP, S_SWEEP2, S_SCORES, S_PARTIAL, S_MISC, S_SHARD, S_SHARD2, S_DEDUP,
-    S_KRY, S_KRYG, S_KRYT, S_KRYV
+    S_KRY, S_KRYG, S_KRYT, S_KRYV, S_KRYX
 };
 
 // ---------------------------------------------------------------- kernels

@@ -372,7 +372,7 @@ static void subspace_topk(Ctx &c, const double *A, int n, int k, const Prod &pro
 // Block Krylov path (see the file comment): V (n x k) = top-k eigenvectors of
 // G = Xc'Xc without forming G.  Blocks K_t (n x p) in S_KRY, G K_t in S_KRYG,
 // T = K'GK in S_KRYT, the small problem's vectors in S_KRYV.
-static void krylov_topk(Ctx &c, const double *Xc, const double *XcT, int n, int k, double *V,
+static void krylov_topk(Ctx &c, const double *Xc, const double *XcT, int n, int k, double *V, double *P,
                         std::vector<double> &h_theta, PcaStats &st) {
     hipStream_t s = c.cur;
     const int p = g_pca_krylov_block > 0 ? g_pca_krylov_block : (k >= 128 ? 64 : 32);
@@ -385,6 +385,7 @@ static void krylov_topk(Ctx &c, const double *Xc, const double *XcT, int n, int 
     steps = std::min(steps, smax);
     double *K = c.buf[S_KRY].as<double>((size_t)n * p * smax);
     double *GK = c.buf[S_KRYG].as<double>((size_t)n * p * smax);
+    double *XK = c.buf[S_KRYX].as<double>((size_t)n * p * smax);   // Xc K_t: the scores come from it
     const size_t np = (size_t)n * p;
     const unsigned g1 = (unsigned)((np + 255) / 256);
     // per-step scratch; re-fetched by every extend() because the small
@@ -430,9 +431,10 @@ static void krylov_topk(Ctx &c, const double *Xc, const double *XcT, int n, int 
             }
             double *Kt = K + (size_t)t * np;
             double *GKt = GK + (size_t)t * np;
+            double *XKt = XK + (size_t)t * np;
             kprof_begin(c, K_GQ_GEMM);
-            rows_gemm_sharded(c, XcT, n, n, Kt, n, p, n, Zt, 0, 1);     // Xc K_t
-            rows_gemm_sharded(c, Xc, n, n, Zt, n, p, n, GKt, 0, 1);     // Xc'(Xc K_t)
+            rows_gemm_sharded(c, XcT, n, n, Kt, n, p, n, XKt, 0, 1);    // Xc K_t
+            rows_gemm_sharded(c, Xc, n, n, XKt, n, p, n, GKt, 0, 1);    // Xc'(Xc K_t)
             kprof_end(c, K_GQ_GEMM);
         }
         built = std::max(built, upto);
@@ -491,6 +493,12 @@ static void krylov_topk(Ctx &c, const double *Xc, const double *XcT, int n, int 
         steps = std::min(smax, steps + 4);
     }
     if (!(st.resid <= 1e-8)) fail(TP_ERR_NUMERIC, "PCA block Krylov iteration did not converge");
+    // scores P = Xc V = (Xc K) Y: an n x D by D x k product instead of another
+    // pass over Xc (2 n D k flops, not 2 n^2 k)
+    GemmArgs pg{n, k, st.krylov_dim, XK, n, false, c.buf[S_KRYV].as<double>((size_t)st.krylov_dim * k),
+                st.krylov_dim, P, n};
+    pg.splitk = 0;
+    gemm_f64(pg, c.buf[S_PARTIAL], s);
 }
 
 PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d_Pt, double *h_sdev) {
@@ -504,8 +512,9 @@ PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d
     double *V = c.buf[S_W].as<double>((size_t)n * k);       // n x k, descending
     std::vector<double> h_theta;
     const int b_est = std::min(n, ((k + std::max(32, k / 4) + 31) / 32) * 32);
-    if (n >= g_pca_krylov_min && b_est < n) {
-        krylov_topk(c, Xc, XcT, n, k, V, h_theta, st);
+    const bool krylov = n >= g_pca_krylov_min && b_est < n;
+    if (krylov) {
+        krylov_topk(c, Xc, XcT, n, k, V, d_P, h_theta, st);
     } else {
         double *G = c.buf[S_G].as<double>((size_t)n * n);
         {
@@ -523,8 +532,9 @@ PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d
         };
         subspace_topk(c, G, n, k, gq, V, h_theta, st, 0x5EEDULL + (uint64_t)n);
     }
-    // scores P = Xc V  (= XcT' V): n x k column-major; Pt row-major
-    rows_gemm_sharded(c, XcT, n, n, V, n, k, n, d_P, 0);
+    // scores P = Xc V  (= XcT' V): n x k column-major; Pt row-major (the
+    // Krylov path formed them from its stored Xc K_t)
+    if (!krylov) rows_gemm_sharded(c, XcT, n, n, V, n, k, n, d_P, 0);
     if (d_Pt) launch_transpose(d_P, n, k, n, d_Pt, k, s);
     if (h_sdev) {
         // prcomp sdev = d / sqrt(max(1, n-1)), d = singular values of Xc = sqrt(eig(G))
