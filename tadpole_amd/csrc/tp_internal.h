@@ -257,7 +257,7 @@ struct PcaStats {
     int iters = 0; double resid = 0; double rate = 0; int block = 0; int blocks = 0;
     int krylov_steps = 0, krylov_dim = 0;   // block Krylov path (0: G formed)
 };
-extern int g_pca_krylov_min, g_pca_krylov_block, g_pca_krylov_steps;
+extern int g_pca_krylov_min, g_pca_krylov_block, g_pca_krylov_steps, g_pca_over;
 PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d_Pt,
                  double *h_sdev);
 

@@ -134,6 +134,7 @@ __global__ void k_diag(const double *W, int b, double *d) {
 int g_pca_margin = 0;     // extra Chebyshev degrees over the planned count (the residual check adds more when needed; tools/pca_margin.py)
 int g_pca_krylov_min = 4096;   // N at which the block Krylov path replaces forming G (0: always, huge: never)
 int g_pca_krylov_block = 0;    // Krylov block p (0: 64 for k >= 128, else 32)
+int g_pca_over = 0;            // subspace oversampling b - k (0: max(32, k / 4), b rounded to 32; else rounded to 16)
 int g_pca_krylov_steps = 0;    // Krylov steps s before the first check (0: ceil(5 k / p))
 
 using Prod = std::function<void(const double *, double *)>;
@@ -152,8 +153,9 @@ __global__ void k_sub(double *W, const double *U, size_t cnt) {
 static void subspace_topk(Ctx &c, const double *A, int n, int k, const Prod &prod, double *V,
                           std::vector<double> &h_theta, PcaStats &st, uint64_t seed, int margin = 0) {
     hipStream_t s = c.cur;
-    const int over = std::max(32, k / 4);
-    int b = std::min(n, ((k + over + 31) / 32) * 32);
+    const int over = g_pca_over > 0 ? g_pca_over : std::max(32, k / 4);
+    const int rnd = g_pca_over > 0 ? 16 : 32;
+    int b = std::min(n, ((k + over + rnd - 1) / rnd) * rnd);
     st.block = b;
     if (b >= n) {
         // exact: eigendecomposition of A itself (small n)
