@@ -161,8 +161,13 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
+        # control only (barriers, the max of the elapsed times, the sharded
+        # path's RCCL id): no data-path collective, so gloo over TCP
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+        dist.init_process_group("gloo")
+    # one GPU per rank; more ranks than GPUs (a rehearsal on a smaller box)
+    # share devices round-robin
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
 
     from tadpole_amd import _lib
@@ -242,7 +247,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     tm = np.mean(np.stack(tms), axis=0)
@@ -313,6 +318,8 @@ def main():
         def rate(q):
             ms_tot, bound, launches, per_launch, peak = kern[q]
             avg_ms = ms_tot / launches
+            if not avg_ms > 0:   # a class this path does not run (e.g. G = Xc'Xc on the Krylov path)
+                return float("nan"), peak, "TFLOP/s" if bound == "mfma" else "GB/s", avg_ms
             if bound == "mfma":
                 unit = "TOP/s (int8)" if (q == "xtx_gemm" and ns) else "TFLOP/s"
                 return per_launch / (avg_ms * 1e-3) / 1e12, peak, unit, avg_ms
