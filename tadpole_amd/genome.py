@@ -130,12 +130,13 @@ def run_genome(matrices: Mapping[str, object], sizes: Optional[Mapping[str, int]
         if not all_failed:
             break
         # re-plan onto the other ranks (a rank that failed a matrix may have a
-        # bad device); alone, retry locally
-        replan = lpt_assign({c: matrix_cost(sizes[c]) for c in all_failed}, world)
+        # bad device): LPT over world - 1 bins, bin w of a matrix that failed on
+        # rank r going to rank (r + 1 + w) % world, never r; alone, retry locally
+        replan = lpt_assign({c: matrix_cost(sizes[c]) for c in all_failed}, max(1, world - 1))
         failed.clear()   # every failure is re-owned below (and re-recorded if it fails again)
         for w, names in enumerate(replan):
             for name in names:
-                owner = (w + 1 + all_failed[name][0]) % world if world > 1 else 0
+                owner = (all_failed[name][0] + 1 + w) % world if world > 1 else 0
                 if owner == rank:
                     one(name, runner)
     still = gather_failed()

@@ -87,9 +87,10 @@ def _flaky_worker(rank, world, port, out, always):
     mats = {c: np.full((n, n), 1.0) for c, n in sizes.items()}
 
     def runner(name, m, device):
-        # chrB fails on whichever rank first gets it (rank 1 under LPT);
-        # `always`: on every rank, every time
-        if name == "chrB" and (always or rank == 1):
+        # "one": chrB fails on whichever rank first gets it (rank 1 under LPT);
+        # "rank1": everything fails on rank 1 (a lost device: all of its
+        # chromosomes must move to rank 0); "always": chrB on every rank
+        if (always == "rank1" and rank == 1) or (name == "chrB" and (always == "always" or rank == 1)):
             raise RuntimeError(f"device lost on rank {rank}")
         return (rank, m.shape[0])
 
@@ -104,7 +105,7 @@ def _flaky_worker(rank, world, port, out, always):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("always", [False, True])
+@pytest.mark.parametrize("always", ["one", "rank1", "always"])
 def test_genome_failed_chromosome_requeued_on_other_rank(always):
     """a chromosome that fails on one rank is re-planned onto
     another rank; one that fails everywhere is reported by name."""
@@ -118,12 +119,14 @@ def test_genome_failed_chromosome_requeued_on_other_rank(always):
     for p in ps:
         p.join(60)
         assert p.exitcode == 0
-    if always:
+    if always == "always":
         assert msg is not None and "chrB" in msg and "device lost" in msg
     else:
         got = dict(items)
         assert msg is None and sorted(got) == ["chrA", "chrB", "chrC", "chrD"]
         assert got["chrB"] == (0, 90)          # re-run by rank 0 after rank 1 failed it
+        if always == "rank1":                  # every chromosome ends on the healthy rank
+            assert all(r == 0 for r, _ in got.values())
 
 
 # ------------------------------------------- one matrix over several GPUs
