@@ -348,10 +348,16 @@ static SweepOut run_sweep(Ctx &c, const double *d_Pt, int n, int k, int min_clus
         for (int r = 0; r < R; ++r) off2[r + 1] = (size_t)(r + 1) * 4;
         shard_gather_bytes(c, err_all, off2);
     }
+    // host read-backs go through the context's pinned staging (one sync per
+    // phase; pageable copies each stage and synchronise on their own)
     std::vector<int> h_nc(k), h_err(R);
-    TP_HIP(hipMemcpyAsync(h_nc.data(), nc_all, k * sizeof(int), hipMemcpyDeviceToHost, s));
-    TP_HIP(hipMemcpyAsync(h_err.data(), err_all, R * sizeof(int), hipMemcpyDeviceToHost, s));
-    TP_HIP(hipStreamSynchronize(s));
+    {
+        int *pi = (int *)c.pinned((size_t)(k + R) * sizeof(int));   // nc_all and err_all are contiguous
+        TP_HIP(hipMemcpyAsync(pi, nc_all, (size_t)(k + R) * sizeof(int), hipMemcpyDeviceToHost, s));
+        TP_HIP(hipStreamSynchronize(s));
+        memcpy(h_nc.data(), pi, k * sizeof(int));
+        memcpy(h_err.data(), pi + k, R * sizeof(int));
+    }
     for (int i = 0; i < k; ++i)
         if (h_nc[i] < 1)
             fail(TP_ERR_NO_BSTICK, "no broken-stick level is significant for PC prefix " + std::to_string(i + 1) +
@@ -370,16 +376,24 @@ static SweepOut run_sweep(Ctx &c, const double *d_Pt, int n, int k, int min_clus
         for (int r = 0; r <= R; ++r) off[r] = (size_t)tb[r] * sd.w_cap;
         shard_gather(c, sc_all, off);   // whole blocks (each rank's w may differ)
     }
-    std::vector<double> h_sc((size_t)k * o.w), blk;
-    for (int r = 0; r < R; ++r) {
-        const int t0 = tb[r], nt = tb[r + 1] - tb[r];
-        if (nt == 0) continue;
-        blk.resize((size_t)nt * o.w);
-        TP_HIP(hipMemcpyAsync(blk.data(), sc_all + (size_t)t0 * sd.w_cap, blk.size() * sizeof(double),
-                              hipMemcpyDeviceToHost, s));
+    std::vector<double> h_sc((size_t)k * o.w);
+    {
+        // every shard's block (nt x w at offset t0 * w_cap, ld nt) in one
+        // pinned buffer, one sync, then reordered to k x w
+        double *ps = (double *)c.pinned((size_t)k * o.w * sizeof(double));
+        for (int r = 0; r < R; ++r) {
+            const int t0 = tb[r], nt = tb[r + 1] - tb[r];
+            if (nt == 0) continue;
+            TP_HIP(hipMemcpyAsync(ps + (size_t)t0 * o.w, sc_all + (size_t)t0 * sd.w_cap,
+                                  (size_t)nt * o.w * sizeof(double), hipMemcpyDeviceToHost, s));
+        }
         TP_HIP(hipStreamSynchronize(s));
-        for (int j = 0; j < o.w; ++j)
-            for (int ti = 0; ti < nt; ++ti) h_sc[(size_t)(t0 + ti) + (size_t)j * k] = blk[(size_t)ti + (size_t)j * nt];
+        for (int r = 0; r < R; ++r) {
+            const int t0 = tb[r], nt = tb[r + 1] - tb[r];
+            const double *blk = ps + (size_t)t0 * o.w;
+            for (int j = 0; j < o.w; ++j)
+                for (int ti = 0; ti < nt; ++ti) h_sc[(size_t)(t0 + ti) + (size_t)j * k] = blk[(size_t)ti + (size_t)j * nt];
+        }
     }
     if (scores) memcpy(scores, h_sc.data(), h_sc.size() * sizeof(double));
     select_params(h_sc.data(), k, o.w, &o.n_pcs, &o.n_clusters);
@@ -393,9 +407,12 @@ static SweepOut run_sweep(Ctx &c, const double *d_Pt, int n, int k, int min_clus
     }
     std::vector<int> ma(n - 1), mb(n - 1);
     std::vector<double> he(n - 1);
-    TP_HIP(hipMemcpyAsync(ma.data(), mrg_a + (size_t)t * (n - 1), (n - 1) * sizeof(int), hipMemcpyDeviceToHost, s));
-    TP_HIP(hipMemcpyAsync(mb.data(), mrg_b + (size_t)t * (n - 1), (n - 1) * sizeof(int), hipMemcpyDeviceToHost, s));
-    TP_HIP(hipMemcpyAsync(he.data(), hgt + (size_t)t * (n - 1), (n - 1) * sizeof(double), hipMemcpyDeviceToHost, s));
+    char *pm = (char *)c.pinned((size_t)(n - 1) * 16);   // a, b (ints), then heights (8-byte aligned)
+    int *pa = (int *)pm, *pb = pa + (n - 1);
+    double *ph = (double *)(pm + (size_t)(n - 1) * 8);
+    TP_HIP(hipMemcpyAsync(pa, mrg_a + (size_t)t * (n - 1), (n - 1) * sizeof(int), hipMemcpyDeviceToHost, s));
+    TP_HIP(hipMemcpyAsync(pb, mrg_b + (size_t)t * (n - 1), (n - 1) * sizeof(int), hipMemcpyDeviceToHost, s));
+    TP_HIP(hipMemcpyAsync(ph, hgt + (size_t)t * (n - 1), (n - 1) * sizeof(double), hipMemcpyDeviceToHost, s));
     if (all_a) {
         if (R > 1 && c.shard.comm) fail(TP_ERR_ARG, "all-tree records are not gathered across ranks");
         all_a->resize(rec); all_b->resize(rec); all_cost->resize(rec); all_h->resize(rec);
@@ -405,6 +422,9 @@ static SweepOut run_sweep(Ctx &c, const double *d_Pt, int n, int k, int min_clus
         TP_HIP(hipMemcpyAsync(all_h->data(), hgt, rec * 8, hipMemcpyDeviceToHost, s));
     }
     TP_HIP(hipStreamSynchronize(s));
+    memcpy(ma.data(), pa, (n - 1) * sizeof(int));
+    memcpy(mb.data(), pb, (n - 1) * sizeof(int));
+    memcpy(he.data(), ph, (n - 1) * sizeof(double));
     if (merge) encode_merge(ma.data(), mb.data(), n, merge);
     if (height) memcpy(height, he.data(), (n - 1) * sizeof(double));
     if (boundary)
@@ -456,11 +476,19 @@ static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_cl
         launch_rowmean_diag(d_M, n0, rm, dg, s);
         const double qindex = 1.0 + (double)(n0 - 1) * bad_frac;
         launch_mask_select(rm, dg, n0, bad_frac, qindex, d_bad, d_good, d_ng, s);
-        TP_HIP(hipMemcpyAsync(&n, d_ng, sizeof(int), hipMemcpyDeviceToHost, s));
-        TP_HIP(hipStreamSynchronize(s));
     }
-    if (bad) TP_HIP(hipMemcpyAsync(bad, d_bad, n0 * sizeof(int), hipMemcpyDeviceToHost, s));
-    if (good_idx) TP_HIP(hipMemcpyAsync(good_idx, d_good, n * sizeof(int), hipMemcpyDeviceToHost, s));
+    {
+        // n_good, the mask and the good indices through the pinned staging:
+        // one sync, then the gather is launched at once
+        int *pi = (int *)c.pinned((size_t)(2 * n0 + 1) * sizeof(int));
+        TP_HIP(hipMemcpyAsync(pi + 2 * n0, d_ng, sizeof(int), hipMemcpyDeviceToHost, s));
+        if (bad) TP_HIP(hipMemcpyAsync(pi, d_bad, n0 * sizeof(int), hipMemcpyDeviceToHost, s));
+        if (good_idx) TP_HIP(hipMemcpyAsync(pi + n0, d_good, n0 * sizeof(int), hipMemcpyDeviceToHost, s));
+        TP_HIP(hipStreamSynchronize(s));
+        if (!(flags & TP_FLAG_NO_MASK)) n = pi[2 * n0];
+        if (bad) memcpy(bad, pi, n0 * sizeof(int));
+        if (good_idx) memcpy(good_idx, pi + n0, (size_t)n * sizeof(int));
+    }
     PipeOut o;
     o.n_good = n;
     if (n < 3) fail(TP_ERR_NO_BSTICK, "fewer than 3 good bins after masking");

@@ -314,8 +314,10 @@ int xtx_int_slices(Ctx &c, const double *d_X, int n) {
     hipLaunchKernelGGL(k_int_scan, dim3(g), dim3(256), 0, c.cur, d_X, cnt, mb, flag);
     TP_HIP(hipGetLastError());
     unsigned long long h[2] = {0, 0};
-    TP_HIP(hipMemcpyAsync(h, mb, 16, hipMemcpyDeviceToHost, c.cur));
+    unsigned long long *ph = (unsigned long long *)c.pinned(16);   // pinned: no staged copy
+    TP_HIP(hipMemcpyAsync(ph, mb, 16, hipMemcpyDeviceToHost, c.cur));
     TP_HIP(hipStreamSynchronize(c.cur));
+    memcpy(h, ph, 16);
     if ((int)h[1]) return 0;
     double mx;
     memcpy(&mx, &h[0], 8);
