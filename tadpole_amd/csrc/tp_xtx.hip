@@ -167,7 +167,7 @@ __global__ void __launch_bounds__(256) k_xtx_i8(const int8_t *__restrict__ S, in
 // 64 x 32, 4 x 2 MFMA tiles each), k-blocks of 64 staged through LDS
 // (double-buffered, one barrier per block) so each slice fragment is read
 // from L2 once per workgroup instead of once per wave.  LDS rows are 80 B
-// (64 B of k + pad) per column.  Same exact arithmetic as k_xtx_i8.
+// (64 B of k + 32 B pad: the b128 fragment reads of a 16-lane group hit distinct banks) per column.  Same exact arithmetic as k_xtx_i8.
 //
 // Tile order (whole triangle, tcol0 = 0 and tn tile columns): workgroups are
 // dealt round-robin over the 8 XCDs (blockIdx % 8); each XCD takes a contiguous
@@ -175,7 +175,7 @@ __global__ void __launch_bounds__(256) k_xtx_i8(const int8_t *__restrict__ S, in
 // column inside each), so the ~32-64 tiles one XCD holds at a time share 16
 // slice panels instead of one B panel and ~40 A panels (same tiles, same bits).
 // Sharded calls (tcol0 > 0) keep the column order.
-constexpr int XB = 128, XK = 64, XLD = 80, XST = 8;
+constexpr int XB = 128, XK = 64, XLD = 96, XST = 8;   // XLD 80 B gave 2-way conflicts in every lane group
 __device__ __forceinline__ void xtx_supertile(int L, int tn, int &bm, int &bn) {
     const int U = (tn + XST - 1) / XST;
     for (int Q = 0; Q < U; ++Q) {
