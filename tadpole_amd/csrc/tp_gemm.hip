@@ -77,7 +77,8 @@ template <bool TA, int KB, int TAG = 0>
 __global__ void __launch_bounds__(256) k_gemm_f64(int M, int N, int K, const double *__restrict__ A, int lda,
                                                   const double *__restrict__ B, int ldb, double *__restrict__ C,
                                                   int ldc, int store_t, int sym, int tcol0, int kchunk,
-                                                  size_t part_stride, int g_xcd_order) {
+                                                  size_t part_stride, int g_xcd_order,
+                                                  const double *__restrict__ C0 = nullptr) {
     __shared__ double As[2][BM][KB + 2];
     __shared__ double Bs[2][BN][KB + 2];
     // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs (each
@@ -170,7 +171,8 @@ __global__ void __launch_bounds__(256) k_gemm_f64(int M, int N, int K, const dou
                 } else if (store_t) {
                     C[(size_t)j + (size_t)i * ldc] = v;
                 } else {
-                    C[(size_t)i + (size_t)j * ldc] = v;
+                    const size_t ci = (size_t)i + (size_t)j * ldc;
+                    C[ci] = C0 ? C0[ci] - v : v;   // C0: C = C0 - A'B (one rounding, as a separate subtraction)
                 }
             }
 }
@@ -302,7 +304,8 @@ constexpr int PM = 32, PN = 64, PK = 32, PLD = PK + 2, PSETS = 3;
 template <bool TA>
 __global__ void __launch_bounds__(256) k_gemm_f64_panel(int M, int N, int K, const double *__restrict__ A, int lda,
                                                         const double *__restrict__ B, int ldb,
-                                                        double *__restrict__ C, int ldc, int store_t) {
+                                                        double *__restrict__ C, int ldc, int store_t,
+                                                        const double *__restrict__ C0) {
     __shared__ double As[2][PM][PLD];
     __shared__ double Bs[2][PN][PLD];
     const int tm = (M + PM - 1) / PM;
@@ -383,8 +386,12 @@ __global__ void __launch_bounds__(256) k_gemm_f64_panel(int M, int N, int K, con
             const int i = i0 + wm + fk + 4 * q;
             const int j = j0 + wn + b * 16 + fr;
             if (i >= M || j >= N) continue;
-            if (store_t) C[(size_t)j + (size_t)i * ldc] = acc[b][q];
-            else C[(size_t)i + (size_t)j * ldc] = acc[b][q];
+            if (store_t) {
+                C[(size_t)j + (size_t)i * ldc] = acc[b][q];
+            } else {
+                const size_t ci = (size_t)i + (size_t)j * ldc;
+                C[ci] = C0 ? C0[ci] - acc[b][q] : acc[b][q];
+            }
         }
 }
 int g_gemm_panel = 1;   // 0: tall-skinny products take the split-K 64 x 64 path (A/B tests)
@@ -494,7 +501,7 @@ int g_gemm_ts = 8;   // k_gemm_ts: most k chunks (0: off -> the 64 x 64 split-K 
 // load per partial otherwise).
 template <int TAG = 0>
 __global__ void __launch_bounds__(256) k_splitk_reduce(const double *part, size_t stride, int S, int M, int N,
-                                                       double *C, int ldc, int store_t) {
+                                                       double *C, int ldc, int store_t, const double *C0) {
     size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= (size_t)M * N) return;
     int i = (int)(idx % M), j = (int)(idx / M);
@@ -508,8 +515,12 @@ __global__ void __launch_bounds__(256) k_splitk_reduce(const double *part, size_
         for (int u = 0; u < 8; ++u) v = v + t[u];
     }
     for (; z < S; ++z) v = v + part[idx + (size_t)z * stride];
-    if (store_t) C[(size_t)j + (size_t)i * ldc] = v;
-    else C[(size_t)i + (size_t)j * ldc] = v;
+    if (store_t) {
+        C[(size_t)j + (size_t)i * ldc] = v;
+    } else {
+        const size_t ci = (size_t)i + (size_t)j * ldc;
+        C[ci] = C0 ? C0[ci] - v : v;
+    }
 }
 
 // Many partials of a small output (Gram matrices of CholQR, K'W of the Krylov
@@ -517,7 +528,7 @@ __global__ void __launch_bounds__(256) k_splitk_reduce(const double *part, size_
 // over the 4 waves (wave w: z = w, w + 4, ...: ascending), the four group sums
 // combined in wave order.  Fixed order for a given S.
 __global__ void __launch_bounds__(256) k_splitk_reduce4(const double *part, size_t stride, int S, int M, int N,
-                                                        double *C, int ldc, int store_t) {
+                                                        double *C, int ldc, int store_t, const double *C0) {
     __shared__ double red[4][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const size_t idx = (size_t)blockIdx.x * 64 + lane;
@@ -538,14 +549,20 @@ __global__ void __launch_bounds__(256) k_splitk_reduce4(const double *part, size
     if (w == 0 && live) {
         const double r = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
         const int i = (int)(idx % M), j = (int)(idx / M);
-        if (store_t) C[(size_t)j + (size_t)i * ldc] = r;
-        else C[(size_t)i + (size_t)j * ldc] = r;
+        if (store_t) {
+            C[(size_t)j + (size_t)i * ldc] = r;
+        } else {
+            const size_t ci = (size_t)i + (size_t)j * ldc;
+            C[ci] = C0 ? C0[ci] - r : r;
+        }
     }
 }
 int g_gemm_splitk = 1;   // auto split-K policy: 1 = deep splits for few-tile long-K products, 0 = round-1 policy
 
 void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s) {
     if (g.M <= 0 || g.N <= 0) return;
+    if (g.sub_from && (g.sym_upper || g.store_t || g.rows))
+        fail(TP_ERR_ARG, "gemm_f64: C = C0 - A'B only for plain column-major outputs");
     if (g.sym_upper && g.M != g.N) fail(TP_ERR_ARG, "sym_upper GEMM needs a square output");
     const int tm = (g.M + BM - 1) / BM, tn = (g.N + BN - 1) / BN;
     // sym_upper: upper tiles of tile columns [tc0, tc1) (a column shard)
@@ -585,10 +602,10 @@ void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s) {
             const dim3 rg((unsigned)((tot + 255) / 256));
             if (g.tag == 1)
                 hipLaunchKernelGGL(k_splitk_reduce<1>, rg, dim3(256), 0, s, out, pstride, S, g.M, g.N, g.C, g.ldc,
-                                   (int)g.store_t);
+                                   (int)g.store_t, (const double *)nullptr);
             else
                 hipLaunchKernelGGL(k_splitk_reduce<0>, rg, dim3(256), 0, s, out, pstride, S, g.M, g.N, g.C, g.ldc,
-                                   (int)g.store_t);
+                                   (int)g.store_t, (const double *)nullptr);
             TP_HIP(hipGetLastError());
         }
         return;
@@ -603,7 +620,7 @@ void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s) {
         // non-symmetric: >= 240 tiles of 128 means >= 960 of 64, where the auto
         // split-K policy below picks no split either (same bits)
         const bool want = g.sym_upper ? g.big_cols : (g.splitk <= 1 && nb2 >= 240 && g.K >= 512);
-        if (want) {
+        if (want && !g.sub_from) {
             if (g.sym_upper && c1 <= c0) return;
             if (g.trans_a)
                 hipLaunchKernelGGL(k_gemm_f64_big<true>, dim3((unsigned)nb2), dim3(256), 0, s, g.M, g.N, g.K, g.A,
@@ -625,10 +642,10 @@ void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s) {
         if (np >= 128) {
             if (g.trans_a)
                 hipLaunchKernelGGL(k_gemm_f64_panel<true>, dim3((unsigned)np), dim3(256), 0, s, g.M, g.N, g.K, g.A,
-                                   g.lda, g.B, g.ldb, g.C, g.ldc, (int)g.store_t);
+                                   g.lda, g.B, g.ldb, g.C, g.ldc, (int)g.store_t, g.sub_from);
             else
                 hipLaunchKernelGGL(k_gemm_f64_panel<false>, dim3((unsigned)np), dim3(256), 0, s, g.M, g.N, g.K, g.A,
-                                   g.lda, g.B, g.ldb, g.C, g.ldc, (int)g.store_t);
+                                   g.lda, g.B, g.ldb, g.C, g.ldc, (int)g.store_t, g.sub_from);
             TP_HIP(hipGetLastError());
             return;
         }
@@ -673,19 +690,19 @@ void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s) {
     if (g_gemm_kb == 32) {
         if (g.trans_a)
             hipLaunchKernelGGL((k_gemm_f64<true, 32>), grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb,
-                               out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride, g_gemm_xcd);
+                               out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride, g_gemm_xcd, S == 1 ? g.sub_from : nullptr);
         else
             hipLaunchKernelGGL((k_gemm_f64<false, 32>), grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb,
-                               out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride, g_gemm_xcd);
+                               out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride, g_gemm_xcd, S == 1 ? g.sub_from : nullptr);
     } else if (g.trans_a && g.tag == 1) {
         hipLaunchKernelGGL((k_gemm_f64<true, 16, 1>), grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb,
-                           out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride, g_gemm_xcd);
+                           out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride, g_gemm_xcd, S == 1 ? g.sub_from : nullptr);
     } else if (g.trans_a) {
         hipLaunchKernelGGL((k_gemm_f64<true, 16>), grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb,
-                           out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride, g_gemm_xcd);
+                           out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride, g_gemm_xcd, S == 1 ? g.sub_from : nullptr);
     } else {
         hipLaunchKernelGGL((k_gemm_f64<false, 16>), grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb,
-                           out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride, g_gemm_xcd);
+                           out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride, g_gemm_xcd, S == 1 ? g.sub_from : nullptr);
     }
     TP_HIP(hipGetLastError());
     if (S > 1) {
@@ -693,13 +710,13 @@ void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s) {
         const dim3 rg((unsigned)((tot + 255) / 256));
         if (S >= 16 && tot <= ((size_t)1 << 18))
             hipLaunchKernelGGL(k_splitk_reduce4, dim3((unsigned)((tot + 63) / 64)), dim3(256), 0, s, out, pstride, S,
-                               g.M, g.N, g.C, g.ldc, (int)g.store_t);
+                               g.M, g.N, g.C, g.ldc, (int)g.store_t, g.sub_from);
         else if (g.tag == 1)
             hipLaunchKernelGGL(k_splitk_reduce<1>, rg, dim3(256), 0, s, out, pstride, S, g.M, g.N, g.C, g.ldc,
-                               (int)g.store_t);
+                               (int)g.store_t, g.sub_from);
         else
             hipLaunchKernelGGL(k_splitk_reduce<0>, rg, dim3(256), 0, s, out, pstride, S, g.M, g.N, g.C, g.ldc,
-                               (int)g.store_t);
+                               (int)g.store_t, g.sub_from);
         TP_HIP(hipGetLastError());
     }
 }

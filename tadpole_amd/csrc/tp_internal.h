@@ -124,6 +124,8 @@ struct GemmArgs {
     bool big_cols = false;       // use the 128 x 128 kernel; tcol0/tcol1 then count 128-column tiles
     int tag = 0;                 // 1: the PCA's G Y products (own kernel symbols for profiles)
     bool rows = false;           // row-shardable long-K product (rows_gemm_sharded): 128 x 64 kernel, k chunks by K
+    const double *sub_from = nullptr;   // C = sub_from - A'B (plain column-major C; may alias C): same bits as
+                                        // the product into a temporary and a separate subtraction
 };
 void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s);
 extern int g_gemm_panel;   // short-K tall-skinny 32 x 64 kernel enabled (default 1)

@@ -139,12 +139,6 @@ int g_pca_krylov_steps = 0;    // Krylov steps s before the first check (0: ceil
 
 using Prod = std::function<void(const double *, double *)>;
 
-// W -= U: elementwise (n x p)
-__global__ void k_sub(double *W, const double *U, size_t cnt) {
-    size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t < cnt) W[t] = W[t] - U[t];
-}
-
 // Top-k eigenpairs of a symmetric n x n operator by Chebyshev-filtered block
 // subspace iteration.  prod(Y, Out): Out = A Y (n x b, ld n).  A (n x n, ld n)
 // is read only when b >= n (exact eigendecomposition).  V (n x k): the Ritz
@@ -392,12 +386,11 @@ static void krylov_topk(Ctx &c, const double *Xc, const double *XcT, int n, int 
     const unsigned g1 = (unsigned)((np + 255) / 256);
     // per-step scratch; re-fetched by every extend() because the small
     // problem (subspace_topk) grows and reallocates the same slots
-    double *W, *Zt, *U, *Xp, *Wsm, *Xinv, *Yinv;
+    double *W, *Zt, *Xp, *Wsm, *Xinv, *Yinv;
     int *d_info;
     auto scratch = [&]() {
         W = c.buf[S_Q].as<double>(np);
         Zt = c.buf[S_Z].as<double>(np);
-        U = c.buf[S_SWEEP2].as<double>(np);
         Xp = c.buf[S_SWEEP].as<double>((size_t)p * p * smax);
         Wsm = c.buf[S_SMALL].as<double>((size_t)3 * p * p + 2 * p + 64);
         Xinv = Wsm + (size_t)p * p;
@@ -415,18 +408,18 @@ static void krylov_topk(Ctx &c, const double *Xc, const double *XcT, int n, int 
         scratch();
         for (int t = built; t < upto; ++t) {
             if (t >= kdone) {
-                // K_t: G K_{t-1} re-orthogonalised twice against K_0..K_{t-1} (CGS2), CholQR2
-                TP_HIP(hipMemcpyAsync(W, GK + (size_t)(t - 1) * np, np * sizeof(double), hipMemcpyDeviceToDevice, s));
+                // K_t: G K_{t-1} re-orthogonalised twice against K_0..K_{t-1} (CGS2), CholQR2.
+                // W = src - K (K'src) in the product's epilogue (src = G K_{t-1}, then W)
                 const int D = t * p;
                 for (int pass = 0; pass < 2; ++pass) {
-                    GemmArgs pr{D, p, n, K, n, true, W, n, Xp, D};   // K'W
+                    const double *src = pass == 0 ? GK + (size_t)(t - 1) * np : W;
+                    GemmArgs pr{D, p, n, K, n, true, src, n, Xp, D};   // K'src
                     pr.splitk = 0;
                     gemm_f64(pr, c.buf[S_PARTIAL], s);
-                    GemmArgs up{n, p, D, K, n, false, Xp, D, U, n};   // K (K'W)
+                    GemmArgs up{n, p, D, K, n, false, Xp, D, W, n};   // W = src - K (K'src)
                     up.splitk = 0;
+                    up.sub_from = src;
                     gemm_f64(up, c.buf[S_PARTIAL], s);
-                    hipLaunchKernelGGL(k_sub, dim3(g1), dim3(256), 0, s, W, U, np);
-                    TP_HIP(hipGetLastError());
                 }
                 orth_cholqr(c, W, K + (size_t)t * np, Zt, n, p, Wsm, Xinv, Yinv, d_info, 2, 1e-14);
                 kdone = t + 1;
