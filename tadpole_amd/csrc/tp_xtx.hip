@@ -164,10 +164,12 @@ __global__ void __launch_bounds__(256) k_xtx_i8(const int8_t *__restrict__ S, in
 }
 
 // Large problems: 128 x 128 upper tiles per 8-wave workgroup (waves 2 x 4 of
-// 64 x 32, 4 x 2 MFMA tiles each), k-blocks of 64 staged through LDS
-// (double-buffered, one barrier per block) so each slice fragment is read
-// from L2 once per workgroup instead of once per wave.  LDS rows are 80 B
-// (64 B of k + 32 B pad: the b128 fragment reads of a 16-lane group hit distinct banks) per column.  Same exact arithmetic as k_xtx_i8.
+// 64 x 32, 4 x 2 MFMA tiles each), k-blocks of 128 staged through LDS
+// (double-buffered, one barrier per two MFMA k-steps) so each slice fragment
+// is read from L2 once per workgroup instead of once per wave.  LDS rows are
+// 160 B per column (128 B of k + 32 B pad: the b128 fragment reads of a
+// 16-lane group and the staging stores hit distinct banks); the two buffers
+// fill the 160 KiB.  Same exact arithmetic as k_xtx_i8.
 //
 // Tile order (whole triangle, tcol0 = 0 and tn tile columns): workgroups are
 // dealt round-robin over the 8 XCDs (blockIdx % 8); each XCD takes a contiguous
@@ -175,7 +177,7 @@ __global__ void __launch_bounds__(256) k_xtx_i8(const int8_t *__restrict__ S, in
 // column inside each), so the ~32-64 tiles one XCD holds at a time share 16
 // slice panels instead of one B panel and ~40 A panels (same tiles, same bits).
 // Sharded calls (tcol0 > 0) keep the column order.
-constexpr int XB = 128, XK = 64, XLD = 96, XST = 8;   // XLD 80 B gave 2-way conflicts in every lane group
+constexpr int XB = 128, XK = 128, XLD = 160, XST = 8;   // 160-B column stride: conflict-free b128 fragments and stores
 __device__ __forceinline__ void xtx_supertile(int L, int tn, int &bm, int &bn) {
     const int U = (tn + XST - 1) / XST;
     for (int Q = 0; Q < U; ++Q) {
@@ -225,23 +227,31 @@ __global__ void __launch_bounds__(512) k_xtx_i8_big(const int8_t *__restrict__ S
     const int wm = (w & 1) * 64, wn = (w >> 1) * 32;
     const size_t slice = (size_t)Np * Kp;
     const int ia = bm * XB, jb = bn * XB;
-    // global -> LDS: per (operand, slice) 128 columns x 64 bytes = 512 x 16 B,
-    // one 16-byte load per thread
+    // global -> LDS: per (operand, slice) 128 columns x 128 bytes of k, two
+    // 16-byte loads per thread (k bytes lk and lk + 64).  Kp is an odd multiple
+    // of 64, so the second half of the last k-block lies past it: it is read
+    // as zeros, which add nothing to the exact int32 sums.
     const int lc = t >> 2, lk = (t & 3) * 16;
-    auto gload = [&](i32x4 (&r)[2][NS], int kb) {
+    auto gload = [&](i32x4 (&r)[2][NS][2], int kb) {
+        const int ca = min(ia + lc, Np - 1), cb = min(jb + lc, Np - 1);
 #pragma unroll
-        for (int s = 0; s < NS; ++s) {
-            const int ca = min(ia + lc, Np - 1), cb = min(jb + lc, Np - 1);
-            TP_DASSERT(kb + lk + 16 <= Kp && ca >= 0 && cb >= 0);
-            r[0][s] = *(const i32x4 *)(S + s * slice + (size_t)ca * Kp + kb + lk);
-            r[1][s] = *(const i32x4 *)(S + s * slice + (size_t)cb * Kp + kb + lk);
-        }
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int k0 = kb + 64 * h + lk;
+                const bool in = kb + 64 * h < Kp;
+                TP_DASSERT(!in || (k0 + 16 <= Kp && ca >= 0 && cb >= 0));
+                r[0][s][h] = in ? *(const i32x4 *)(S + s * slice + (size_t)ca * Kp + k0) : i32x4{0, 0, 0, 0};
+                r[1][s][h] = in ? *(const i32x4 *)(S + s * slice + (size_t)cb * Kp + k0) : i32x4{0, 0, 0, 0};
+            }
     };
-    auto lstore = [&](int buf, const i32x4 (&r)[2][NS]) {
+    auto lstore = [&](int buf, const i32x4 (&r)[2][NS][2]) {
 #pragma unroll
         for (int o = 0; o < 2; ++o)
 #pragma unroll
-            for (int s = 0; s < NS; ++s) *(i32x4 *)(&Ls[buf][o][s][lc * XLD + lk]) = r[o][s];
+            for (int s = 0; s < NS; ++s)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) *(i32x4 *)(&Ls[buf][o][s][lc * XLD + 64 * h + lk]) = r[o][s][h];
     };
     i32x4 acc[NS][NS][4][2];
 #pragma unroll
@@ -252,7 +262,7 @@ __global__ void __launch_bounds__(512) k_xtx_i8_big(const int8_t *__restrict__ S
             for (int a = 0; a < 4; ++a)
 #pragma unroll
                 for (int b = 0; b < 2; ++b) acc[s][u][a][b] = i32x4{0, 0, 0, 0};
-    i32x4 rg[2][NS];
+    i32x4 rg[2][NS][2];
     gload(rg, 0);
     lstore(0, rg);
     __syncthreads();
@@ -261,24 +271,29 @@ __global__ void __launch_bounds__(512) k_xtx_i8_big(const int8_t *__restrict__ S
     for (int kb = 0; kb < Kp; kb += XK) {
         const bool more = kb + XK < Kp;
         if (more) gload(rg, kb + XK);
-        i32x4 fa[NS][4], fb[NS][2];
 #pragma unroll
-        for (int s = 0; s < NS; ++s) {
+        for (int h = 0; h < 2; ++h) {   // two MFMA k-steps of 64 per barrier
+            i32x4 fa[NS][4], fb[NS][2];
 #pragma unroll
-            for (int a = 0; a < 4; ++a) fa[s][a] = *(const i32x4 *)(&Ls[buf][0][s][(wm + 16 * a + fr) * XLD + fk]);
-#pragma unroll
-            for (int b = 0; b < 2; ++b) fb[s][b] = *(const i32x4 *)(&Ls[buf][1][s][(wn + 16 * b + fr) * XLD + fk]);
-        }
-#pragma unroll
-        for (int s = 0; s < NS; ++s)
-#pragma unroll
-            for (int u = 0; u < NS; ++u)
+            for (int s = 0; s < NS; ++s) {
 #pragma unroll
                 for (int a = 0; a < 4; ++a)
+                    fa[s][a] = *(const i32x4 *)(&Ls[buf][0][s][(wm + 16 * a + fr) * XLD + 64 * h + fk]);
 #pragma unroll
-                    for (int b = 0; b < 2; ++b)
-                        acc[s][u][a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[s][a], fb[u][b], acc[s][u][a][b],
-                                                                                0, 0, 0);
+                for (int b = 0; b < 2; ++b)
+                    fb[s][b] = *(const i32x4 *)(&Ls[buf][1][s][(wn + 16 * b + fr) * XLD + 64 * h + fk]);
+            }
+#pragma unroll
+            for (int s = 0; s < NS; ++s)
+#pragma unroll
+                for (int u = 0; u < NS; ++u)
+#pragma unroll
+                    for (int a = 0; a < 4; ++a)
+#pragma unroll
+                        for (int b = 0; b < 2; ++b)
+                            acc[s][u][a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[s][a], fb[u][b],
+                                                                                    acc[s][u][a][b], 0, 0, 0);
+        }
         if (more) lstore(buf ^ 1, rg);
         __syncthreads();
         buf ^= 1;
