@@ -630,10 +630,14 @@ __global__ void __launch_bounds__(128) k_coniss_t(SweepDev sd, double *cost0) {
 template __global__ void k_coniss_t<false, 1, false>(SweepDev, double *);
 template __global__ void k_coniss_t<false, 2, false>(SweepDev, double *);
 template __global__ void k_coniss_t<false, 3, false>(SweepDev, double *);
+template __global__ void k_coniss_t<false, 6, true>(SweepDev, double *);
+template __global__ void k_coniss_t<false, 8, true>(SweepDev, double *);
+template __global__ void k_coniss_t<false, 11, true>(SweepDev, double *);
 template __global__ void k_coniss_t<false, 16, true>(SweepDev, double *);
 template __global__ void k_coniss_t<true, 1, false>(SweepDev, double *);
 template __global__ void k_coniss_t<true, 2, false>(SweepDev, double *);
 template __global__ void k_coniss_t<true, 3, false>(SweepDev, double *);
+template __global__ void k_coniss_t<true, 6, true>(SweepDev, double *);
 template __global__ void k_coniss_t<true, 16, true>(SweepDev, double *);
 
 // ------------------------------------------------------------ CH over cuts
@@ -1065,13 +1069,20 @@ static void run_coniss(const SweepDev &sd, hipStream_t s, bool stamped, Ctx *pro
     const size_t lds = in_lds ? coniss_lds_bytes(sd.n) : kConissGlbLds;
     const int bs = (nbk + 63) / 64;   // block-minimum slots per lane
     if (!stamped && prof) kprof_begin(*prof, K_CONISS);
+    // global variant: as few block-minimum slots as the size needs (every
+    // per-slot loop of the merge chain -- the untouched minimum, the argmin
+    // ballots, the block-minimum updates -- runs over all of them)
     if (stamped) {
-        if (!in_lds) launch_coniss_bs<true, 16, true>(sd, cost0, lds, s);
+        if (!in_lds && bs <= 6) launch_coniss_bs<true, 6, true>(sd, cost0, lds, s);
+        else if (!in_lds) launch_coniss_bs<true, 16, true>(sd, cost0, lds, s);
         else if (bs == 1) launch_coniss_bs<true, 1, false>(sd, cost0, lds, s);
         else if (bs == 2) launch_coniss_bs<true, 2, false>(sd, cost0, lds, s);
         else launch_coniss_bs<true, 3, false>(sd, cost0, lds, s);
     } else {
-        if (!in_lds) launch_coniss_bs<false, 16, true>(sd, cost0, lds, s);
+        if (!in_lds && bs <= 6) launch_coniss_bs<false, 6, true>(sd, cost0, lds, s);
+        else if (!in_lds && bs <= 8) launch_coniss_bs<false, 8, true>(sd, cost0, lds, s);
+        else if (!in_lds && bs <= 11) launch_coniss_bs<false, 11, true>(sd, cost0, lds, s);
+        else if (!in_lds) launch_coniss_bs<false, 16, true>(sd, cost0, lds, s);
         else if (bs == 1) launch_coniss_bs<false, 1, false>(sd, cost0, lds, s);
         else if (bs == 2) launch_coniss_bs<false, 2, false>(sd, cost0, lds, s);
         else launch_coniss_bs<false, 3, false>(sd, cost0, lds, s);

@@ -121,4 +121,6 @@ if __name__ == "__main__":
         coniss()
     if "coniss3" in what:
         coniss(7808, 200)
+    if "coniss24" in what:   # above the LDS capacity: the global-memory variant
+        coniss(24300, 200)
 
