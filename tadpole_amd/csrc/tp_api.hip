@@ -1301,6 +1301,7 @@ void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
         case 13: p = &g_gemm_ts; break;
         case 14: p = &g_xtx_supertile; break;
         case 15: p = &g_pca_over; break;
+        case 16: p = &g_coniss_lu; break;
         default: fail(TP_ERR_ARG, "unknown knob");
         }
         if (*which == 3 && *value != 16 && *value != 32) fail(TP_ERR_ARG, "stage depth must be 16 or 32");

@@ -188,6 +188,7 @@ struct SweepDev {
 };
 // scratch of the shared CH segment statistics for ntrees trees
 extern int g_ch_dedup;        // 0: every tree computes its own segment statistics
+extern int g_coniss_lu;       // 0: the global CONISS variant keeps its links in global memory
 extern int g_ch_dedup_ucap;   // > 0: cap on the shared store (tests of the overflow path)
 size_t sweep_dedup_bytes(int n, int k, int ntrees, int seg_cap, int *hcap, int *ucap);
 void sweep_dedup_bind(SweepDev &sd, void *base, int hcap, int ucap);

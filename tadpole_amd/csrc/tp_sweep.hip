@@ -166,6 +166,22 @@ __global__ void __launch_bounds__(64) k_seed(SweepDev sd, double *cost0) {
     c0[p0 + lane] = mycost;
 }
 
+// CONISS link arrays: int (LDS variant, or global memory), or 16-bit indices in
+// LDS for the costs-in-global variant (-1 <-> 0xFFFF; n <= ~40k)
+template <bool U16> struct LinkArr {
+    int *p;
+    __device__ __forceinline__ int get(int i) const { return p[i]; }
+    __device__ __forceinline__ void set(int i, int v) const { p[i] = v; }
+};
+template <> struct LinkArr<true> {
+    unsigned short *p;
+    __device__ __forceinline__ int get(int i) const {
+        const int x = p[i];
+        return x == 0xFFFF ? -1 : x;
+    }
+    __device__ __forceinline__ void set(int i, int v) const { p[i] = (unsigned short)v; }
+};
+
 // Columns i..ld-1 of a row hold whatever the row was read from (later PCs of
 // Pt, or their sums): the last slot's term is selected to 0 there, which adds
 // fma(0, 0, acc) = acc -- the canonical sum over the first i columns.
@@ -206,7 +222,7 @@ __device__ __forceinline__ double ward_part(const double (&sa)[NS], double fa, c
 // barrier with both waves choosing was slower: B's prefetch of a2's rows then
 // has only B's own choice to hide behind, and HBM latency shows.)  Mailbox
 // words are written before one barrier and read after it.
-template <bool STAMPS, int NS, int BS, bool GLB>
+template <bool STAMPS, int NS, int BS, bool GLB, bool LU = false>
 __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, double *lds, double *mb_d,
                                              int4 *mb_i) {
     long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -229,9 +245,15 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
     // and links in global scratch behind cost0 (L2 / MALL resident); only the
     // mailbox is in LDS.  Same code path otherwise.
     const size_t cst = coniss_cost_stride(n), lst = coniss_link_stride(n);
+    // LU (with GLB): the links are 16-bit indices in LDS, the costs stay global
     double *cost = GLB ? cost0 + (size_t)ti * cst : lds;
-    int *link = GLB ? (int *)(cost0 + (size_t)sd.ntrees * cst) + (size_t)ti * 2 * lst : (int *)(cost + cst);
-    int *rn = link + lst;
+    LinkArr<LU> link, rn;
+    if constexpr (LU) {
+        link.p = (unsigned short *)lds;
+    } else {
+        link.p = GLB ? (int *)(cost0 + (size_t)sd.ntrees * cst) + (size_t)ti * 2 * lst : (int *)(cost + cst);
+    }
+    rn.p = link.p + lst;
     // dummy slots: branch-free code writes absent positions there (an exec-
     // masked `if` costs ~55 cycles on the merge chain, a select ~14)
     const int DC = nbk * 64, DL = n;
@@ -290,17 +312,17 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
     auto merge_at1 = [&](int p) {   // current links -> the pair starting at p, first level (no branches)
         Mg m;
         m.a = p;
-        m.ea = link[p];
-        m.eb = rn[p];
-        const int lsv = pin(link[p > 0 ? p - 1 : DL]);
+        m.ea = link.get(p);
+        m.eb = rn.get(p);
+        const int lsv = pin(link.get(p > 0 ? p - 1 : DL));
         m.ls = p > 0 ? lsv : -1;
         m.r = m.eb >= 0 && m.eb + 1 < n ? m.eb + 1 : -1;
         return m;
     };
     auto merge_at2 = [&](Mg &m) {   // second level: the right ends of r and rr, the cluster left of ls
-        int erv = rn[m.ea + 1 < n ? m.ea + 1 : DL];
-        int llv = link[m.ls > 0 ? m.ls - 1 : DL];
-        int rrev = rn[m.r >= 0 ? m.r : DL];
+        int erv = rn.get(m.ea + 1 < n ? m.ea + 1 : DL);
+        int llv = link.get(m.ls > 0 ? m.ls - 1 : DL);
+        int rrev = rn.get(m.r >= 0 ? m.r : DL);
         pin3(erv, llv, rrev);
         m.er = m.r >= 0 ? erv : -1;
         m.ll = m.ls > 0 ? llv : -1;
@@ -345,10 +367,13 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
             const double cp = c0[p];
             if (!GLB) cost[p] = cp;
             if (p < n) {
-                link[p] = p;
-                rn[p] = p + 1 < n ? p + 1 : -1;
+                link.set(p, p);
+                rn.set(p, p + 1 < n ? p + 1 : -1);
             }
-            if (bk == 0) link[DL + lane] = rn[DL + lane] = -1;
+            if (bk == 0) {
+                link.set(DL + lane, -1);
+                rn.set(DL + lane, -1);
+            }
             const double m = wave_min(cp);
             if (lane == (bk & 63)) {
 #pragma unroll
@@ -391,18 +416,18 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
             // branch-free: absent positions write the dummy slots
             cost[pls] = pcl;
             cost[pa_] = pcr;
-            link[a] = eb;
-            link[eb] = a;
-            rn[a] = er;
+            link.set(a, eb);
+            link.set(eb, a);
+            rn.set(a, er);
             cost[b] = QNAN;
             cost[a] = QNAN;
             cost[ls >= 0 ? ls : DC] = QNAN;
-            rn[ls >= 0 ? ls : DL] = eb;
+            rn.set(ls >= 0 ? ls : DL, eb);
             // links the two candidate merges next to m need (independent of a2:
             // issued before the argmin's reductions so their latency overlaps)
-            int m1llv = link[cur.ll > 0 ? cur.ll - 1 : DL];
-            int m2erv = rn[r >= 0 ? r : DL];
-            int m2rrev = rn[(r >= 0 && er + 1 < n) ? er + 1 : DL];
+            int m1llv = link.get(cur.ll > 0 ? cur.ll - 1 : DL);
+            int m2erv = rn.get(r >= 0 ? r : DL);
+            int m2rrev = rn.get((r >= 0 && er + 1 < n) ? er + 1 : DL);
             // refresh the three touched blocks and, concurrently, the minimum of
             // the untouched ones: four interleaved wave reductions
             const int ba = a >> 6, bb = b >> 6, bl = ls >= 0 ? (ls >> 6) : ba;
@@ -614,30 +639,32 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
 }
 
 // STAMPS: diagnostic build (see coniss_tree2).  BS: block-minimum slots (n <= 4096 BS).
-template <bool STAMPS, int BS, bool GLB>
+// LU: the global variant with its links as 16-bit indices in LDS.
+template <bool STAMPS, int BS, bool GLB, bool LU = false>
 __global__ void __launch_bounds__(128) k_coniss_t(SweepDev sd, double *cost0) {
     extern __shared__ double lds[];
     __shared__ double mb_d[4];
     __shared__ int4 mb_i[4];
     const int i = sd.tree0 + blockIdx.x + 1;
     switch ((i + 63) / 64) {
-        case 1: coniss_tree2<STAMPS, 1, BS, GLB>(sd, cost0, lds, mb_d, mb_i); break;
-        case 2: coniss_tree2<STAMPS, 2, BS, GLB>(sd, cost0, lds, mb_d, mb_i); break;
-        case 3: coniss_tree2<STAMPS, 3, BS, GLB>(sd, cost0, lds, mb_d, mb_i); break;
-        default: coniss_tree2<STAMPS, 4, BS, GLB>(sd, cost0, lds, mb_d, mb_i); break;
+        case 1: coniss_tree2<STAMPS, 1, BS, GLB, LU>(sd, cost0, lds, mb_d, mb_i); break;
+        case 2: coniss_tree2<STAMPS, 2, BS, GLB, LU>(sd, cost0, lds, mb_d, mb_i); break;
+        case 3: coniss_tree2<STAMPS, 3, BS, GLB, LU>(sd, cost0, lds, mb_d, mb_i); break;
+        default: coniss_tree2<STAMPS, 4, BS, GLB, LU>(sd, cost0, lds, mb_d, mb_i); break;
     }
 }
 template __global__ void k_coniss_t<false, 1, false>(SweepDev, double *);
 template __global__ void k_coniss_t<false, 2, false>(SweepDev, double *);
 template __global__ void k_coniss_t<false, 3, false>(SweepDev, double *);
-template __global__ void k_coniss_t<false, 6, true>(SweepDev, double *);
-template __global__ void k_coniss_t<false, 8, true>(SweepDev, double *);
+template __global__ void k_coniss_t<false, 6, true, true>(SweepDev, double *);
+template __global__ void k_coniss_t<false, 8, true, true>(SweepDev, double *);
+template __global__ void k_coniss_t<false, 11, true, true>(SweepDev, double *);
 template __global__ void k_coniss_t<false, 11, true>(SweepDev, double *);
 template __global__ void k_coniss_t<false, 16, true>(SweepDev, double *);
 template __global__ void k_coniss_t<true, 1, false>(SweepDev, double *);
 template __global__ void k_coniss_t<true, 2, false>(SweepDev, double *);
 template __global__ void k_coniss_t<true, 3, false>(SweepDev, double *);
-template __global__ void k_coniss_t<true, 6, true>(SweepDev, double *);
+template __global__ void k_coniss_t<true, 6, true, true>(SweepDev, double *);
 template __global__ void k_coniss_t<true, 16, true>(SweepDev, double *);
 
 // ------------------------------------------------------------ CH over cuts
@@ -1054,33 +1081,39 @@ static bool coniss_in_lds(int n) { return coniss_lds_bytes(n) <= 160 * 1024 - 25
 
 // seed kernel + CONISS (cost0 = initial adjacent costs, ntrees x nbk*64, then
 // the global-variant link scratch: see sweep_cost0_doubles)
-template <bool STAMPS, int BS, bool GLB>
+template <bool STAMPS, int BS, bool GLB, bool LU = false>
 static void launch_coniss_bs(const SweepDev &sd, double *cost0, size_t lds, hipStream_t s) {
-    TP_HIP(hipFuncSetAttribute((const void *)k_coniss_t<STAMPS, BS, GLB>,
+    TP_HIP(hipFuncSetAttribute((const void *)k_coniss_t<STAMPS, BS, GLB, LU>,
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL((k_coniss_t<STAMPS, BS, GLB>), dim3(sd.ntrees), dim3(128), lds, s, sd, cost0);
+    hipLaunchKernelGGL((k_coniss_t<STAMPS, BS, GLB, LU>), dim3(sd.ntrees), dim3(128), lds, s, sd, cost0);
 }
+int g_coniss_lu = 1;   // 0: the global variant keeps its links in global memory too
+
 static void run_coniss(const SweepDev &sd, hipStream_t s, bool stamped, Ctx *prof) {
     const int nbk = (sd.n + 63) / 64;
     double *cost0 = sd.cost0;
     hipLaunchKernelGGL(k_seed, dim3(sd.ntrees, nbk), dim3(64), 0, s, sd, cost0);
     TP_HIP(hipGetLastError());
     const bool in_lds = coniss_in_lds(sd.n);
-    const size_t lds = in_lds ? coniss_lds_bytes(sd.n) : kConissGlbLds;
+    // global variant: 16-bit links in LDS when they fit (costs stay global)
+    const size_t lu_bytes = coniss_link_stride(sd.n) * 4;
     const int bs = (nbk + 63) / 64;   // block-minimum slots per lane
+    const bool lu = !in_lds && g_coniss_lu && sd.n + 64 < 0xFFFF && lu_bytes <= 150 * 1024 && bs <= 11;
+    const size_t lds = in_lds ? coniss_lds_bytes(sd.n) : (lu ? lu_bytes : kConissGlbLds);
     if (!stamped && prof) kprof_begin(*prof, K_CONISS);
     // global variant: as few block-minimum slots as the size needs (every
     // per-slot loop of the merge chain -- the untouched minimum, the argmin
     // ballots, the block-minimum updates -- runs over all of them)
     if (stamped) {
-        if (!in_lds && bs <= 6) launch_coniss_bs<true, 6, true>(sd, cost0, lds, s);
+        if (lu && bs <= 6) launch_coniss_bs<true, 6, true, true>(sd, cost0, lds, s);
         else if (!in_lds) launch_coniss_bs<true, 16, true>(sd, cost0, lds, s);
         else if (bs == 1) launch_coniss_bs<true, 1, false>(sd, cost0, lds, s);
         else if (bs == 2) launch_coniss_bs<true, 2, false>(sd, cost0, lds, s);
         else launch_coniss_bs<true, 3, false>(sd, cost0, lds, s);
     } else {
-        if (!in_lds && bs <= 6) launch_coniss_bs<false, 6, true>(sd, cost0, lds, s);
-        else if (!in_lds && bs <= 8) launch_coniss_bs<false, 8, true>(sd, cost0, lds, s);
+        if (lu && bs <= 6) launch_coniss_bs<false, 6, true, true>(sd, cost0, lds, s);
+        else if (lu && bs <= 8) launch_coniss_bs<false, 8, true, true>(sd, cost0, lds, s);
+        else if (lu) launch_coniss_bs<false, 11, true, true>(sd, cost0, lds, s);
         else if (!in_lds && bs <= 11) launch_coniss_bs<false, 11, true>(sd, cost0, lds, s);
         else if (!in_lds) launch_coniss_bs<false, 16, true>(sd, cost0, lds, s);
         else if (bs == 1) launch_coniss_bs<false, 1, false>(sd, cost0, lds, s);

@@ -318,12 +318,18 @@ def _structured_pcs(n, k, seed):
     return means[seg] + 0.05 * rng.standard_normal((n, k))
 
 
+@pytest.mark.parametrize("lu", [1, 0])
 @pytest.mark.parametrize("n,k,seed", [(10600, 6, 3), (20000, 3, 4)])
-def test_sweep_bit_exact_global_variant(gpu, n, k, seed):
-    # n beyond the LDS capacity (10 200): the CONISS keeps costs and links in
-    # global memory (same code path otherwise) -- the C5 arm sizes
+def test_sweep_bit_exact_global_variant(gpu, n, k, seed, lu):
+    # n beyond the LDS capacity (10 200): the CONISS keeps its costs in global
+    # memory, its links as 16-bit indices in LDS (lu = 1, knob 16) or in global
+    # memory too (lu = 0); same code path otherwise -- the C5 arm sizes
     p = _structured_pcs(n, k, seed)
-    got = G.sweep_dev(p)
+    old = G.knob(16, lu)
+    try:
+        got = G.sweep_dev(p)
+    finally:
+        G.knob(16, old)
     ref = O.sweep(p)
     assert np.array_equal(got["n_cluster"], ref.n_cluster)
     assert np.array_equal(got["mrg_b"], ref.mrg_b)
