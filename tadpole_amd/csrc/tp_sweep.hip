@@ -242,8 +242,9 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
     const int nbk = (n + 63) / 64;
     const double QNAN = __longlong_as_double(0x7FF8000000000000LL);
     // GLB (n above the LDS capacity): costs stay in this tree's slice of cost0
-    // and links in global scratch behind cost0 (L2 / MALL resident); only the
-    // mailbox is in LDS.  Same code path otherwise.
+    // (L2 / MALL resident) and links either in LDS as 16-bit indices (LU, n up
+    // to ~38k: the link chains of merge_at stay LDS round trips) or in global
+    // scratch behind cost0.  Same code path otherwise.
     const size_t cst = coniss_cost_stride(n), lst = coniss_link_stride(n);
     // LU (with GLB): the links are 16-bit indices in LDS, the costs stay global
     double *cost = GLB ? cost0 + (size_t)ti * cst : lds;
