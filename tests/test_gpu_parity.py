@@ -319,8 +319,10 @@ def _structured_pcs(n, k, seed):
 
 
 @pytest.mark.parametrize("lu", [1, 0])
-@pytest.mark.parametrize("n,k,seed", [(10600, 6, 3), (20000, 3, 4)])
+@pytest.mark.parametrize("n,k,seed", [(10600, 6, 3), (20000, 3, 4), (38000, 2, 5), (40000, 2, 6)])
 def test_sweep_bit_exact_global_variant(gpu, n, k, seed, lu):
+    # 10.6k / 20k: 6 block-minimum slots; 38k: 11 slots with 16-bit LDS links
+    # (the largest size they fit); 40k: links in global memory whatever lu says
     # n beyond the LDS capacity (10 200): the CONISS keeps its costs in global
     # memory, its links as 16-bit indices in LDS (lu = 1, knob 16) or in global
     # memory too (lu = 0); same code path otherwise -- the C5 arm sizes
