@@ -174,6 +174,7 @@ struct SweepDev {
     int *err;           // device flag: 1 = a cut exceeded seg_cap / w_cap
     long long *stamps = nullptr;   // diagnostic builds only (k_coniss_t<true>)
     double *cost0 = nullptr;       // ntrees x roundup(n, 64) initial costs (scratch)
+    const double *pt2 = nullptr;   // CONISS: the scores with slots 0 and 1 paired (set by the launcher, inside cost0)
     // CH segment statistics shared across trees (null: every tree computes its
     // own): the finest cuts' segments [s, e) go into an open-addressing set
     // (hkeys, empty = ~0), each distinct one gets a slot of ustore (k column
@@ -202,8 +203,10 @@ __host__ __device__ inline size_t coniss_link_stride(int n) { return (size_t)n +
 // row-major scores Pt (n x k) + slack: CONISS reads whole 64-column slots of a
 // row (up to 256 columns) and masks the columns past its prefix
 inline size_t pt_doubles(int n, int k) { return (size_t)n * k + 256; }
+// + the copy of the scores with column pairs (l, l + 64) adjacent that CONISS
+// reads (n x 256, see k_pt_pairs in tp_sweep.hip)
 inline size_t sweep_cost0_doubles(int n, int ntrees) {
-    return (size_t)ntrees * (coniss_cost_stride(n) + coniss_link_stride(n));
+    return (size_t)ntrees * (coniss_cost_stride(n) + coniss_link_stride(n)) + 2 + (size_t)n * 256;
 }
 size_t sweep_sums_doubles(int n, int tree0, int ntrees);
 void blas_shutdown_all();

@@ -125,6 +125,22 @@ __device__ __forceinline__ void wave_sum2(double &u, double &v) {
 }
 
 
+// ---- scores for CONISS with column slots 0 and 1 paired: row p of 256
+// doubles, columns l and l + 64 at 2 l and 2 l + 1, columns 128..255 plain
+// after them (zero past k).  A lane then fetches its first two columns with
+// one 16-byte load; the columns a lane holds and their order are those of the
+// plain layout (same bits).  Slab rows of merged clusters use the same layout.
+__global__ void __launch_bounds__(256) k_pt_pairs(const double *Pt, int n, int ldp, int k, double *Pt2) {
+    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (size_t)n * 256) return;
+    const int p = (int)(idx >> 8), q = (int)(idx & 255);
+    const int c = q < 128 ? 64 * (q & 1) + (q >> 1) : q;
+    Pt2[idx] = c < k ? Pt[(size_t)p * ldp + c] : 0.0;
+}
+static size_t coniss_pt2_offset(int n, int ntrees) {
+    return ((size_t)ntrees * (coniss_cost_stride(n) + coniss_link_stride(n)) + 1) & ~(size_t)1;
+}
+
 // ---- initial adjacent (singleton) costs of every tree: e_j = x_j - y_j over
 // the first i score columns, cost = tot / 2 (canonical order).  One wave per
 // (tree, 64 positions).  The trees' cluster-sum slabs are not seeded: a
@@ -268,9 +284,13 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
     // singleton (its sums are its row of the shared scores Pt, which no tree
     // writes: slabs hold only merged clusters).  A knows the ends of every
     // cluster it names, so it flags singletons in what it sends B.
-    double *S = sd.sums + sums_off(n, sd.tree0, i) + lane;
-    const double *P0 = sd.Pt + lane;
-    const int ldp = sd.ldp;
+    // rows with NS >= 2: slots 0 and 1 paired (lane l: doubles 2l, 2l + 1),
+    // slots 2 and 3 plain -- in the tree's slab (stride ld) and in the shared
+    // paired copy of the scores (stride 256); NS = 1: plain rows, the scores
+    // read from Pt itself
+    double *S = sd.sums + sums_off(n, sd.tree0, i);
+    const double *PP = NS >= 2 ? sd.pt2 : sd.Pt;
+    const size_t ldpp = NS >= 2 ? 256 : (size_t)sd.ldp;
     const bool last_in = lane + 64 * (NS - 1) < i;
     int *mrg_a = sd.mrg_a + (size_t)ti * (n - 1);
     int *mrg_b = sd.mrg_b + (size_t)ti * (n - 1);
@@ -299,9 +319,16 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
     auto load_row = [&](double (&dst)[NS], int code) {
         code = __builtin_amdgcn_readfirstlane(code);
         const int p = code & (ROW_PT - 1);
-        const double *pr = (code & ROW_PT) ? P0 + (size_t)p * ldp : S + (size_t)p * ld;
+        const double *pr = (code & ROW_PT) ? PP + (size_t)p * ldpp : S + (size_t)p * ld;
+        if (NS >= 2) {
+            const double2 v = *(const double2 *)(pr + 2 * lane);
+            dst[0] = v.x;
+            dst[1] = v.y;
+        } else {
+            dst[0] = pr[lane];
+        }
 #pragma unroll
-        for (int t = 0; t < NS; ++t) dst[t] = pr[64 * t];
+        for (int t = 2; t < NS; ++t) dst[t] = pr[64 * t + lane];
     };
     auto rowc = [](int start, bool single) { return start | (single ? ROW_PT : 0); };
     // A: a merge described by (a, ea, eb, ls, r, er); b = ea + 1; ll = start of
@@ -563,10 +590,13 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
             load_row(pll, lls);
             load_row(prr, rrs);
 #pragma unroll
-            for (int t = 0; t < NS; ++t) {
-                sm[t] = sa[t] + sb[t];
-                S[(size_t)a_ * ld + 64 * t] = sm[t];
-            }
+            for (int t = 0; t < NS; ++t) sm[t] = sa[t] + sb[t];
+            if (NS >= 2)
+                *(double2 *)(S + (size_t)a_ * ld + 2 * lane) = make_double2(sm[0], sm[1]);
+            else
+                S[(size_t)a_ * ld + lane] = sm[0];
+#pragma unroll
+            for (int t = 2; t < NS; ++t) S[(size_t)a_ * ld + 64 * t + lane] = sm[t];
             if (STAMPS) {   // waits for the rows (the stamp below then counts the HBM wait)
                 double z = 0.0;
 #pragma unroll
@@ -1090,9 +1120,18 @@ static void launch_coniss_bs(const SweepDev &sd, double *cost0, size_t lds, hipS
 }
 int g_coniss_lu = 1;   // 0: the global variant keeps its links in global memory too
 
-static void run_coniss(const SweepDev &sd, hipStream_t s, bool stamped, Ctx *prof) {
+static void run_coniss(const SweepDev &sd_in, hipStream_t s, bool stamped, Ctx *prof) {
+    SweepDev sd = sd_in;
     const int nbk = (sd.n + 63) / 64;
     double *cost0 = sd.cost0;
+    if (sd.tree0 + sd.ntrees > 64) {   // trees with two or more slots read the paired copy
+        double *pt2 = cost0 + coniss_pt2_offset(sd.n, sd.ntrees);
+        const size_t cnt = (size_t)sd.n * 256;
+        hipLaunchKernelGGL(k_pt_pairs, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, sd.Pt, sd.n, sd.ldp, sd.k,
+                           pt2);
+        TP_HIP(hipGetLastError());
+        sd.pt2 = pt2;
+    }
     hipLaunchKernelGGL(k_seed, dim3(sd.ntrees, nbk), dim3(64), 0, s, sd, cost0);
     TP_HIP(hipGetLastError());
     const bool in_lds = coniss_in_lds(sd.n);
