@@ -506,7 +506,8 @@ static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_cl
         xtx_product(c, X, n, S);
         kprof_end(c, K_COR_GEMM);
     }
-    launch_cor_epilogue(S, m, n, C, c.buf[S_DIAG].as<double>(n), s);
+    double *cmean = g_cor_fused ? c.buf[S_CMEAN].as<double>(n) : nullptr;   // C's column means, for prcomp
+    launch_cor_epilogue(S, m, n, C, c.buf[S_DIAG].as<double>(n), s, cmean);
     trace_mark(s, "cor");
     tm.mark();
     // ---- prcomp (R/TADpole.R:452-453)
@@ -515,7 +516,7 @@ static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_cl
     if (k > k_cap) fail(TP_ERR_CAPACITY, "k_cap smaller than min(max_pcs, n_good)");
     double *P = c.buf[S_P].as<double>((size_t)n * k);
     double *Pt = c.buf[S_PT].as<double>(pt_doubles(n, k));
-    PcaStats ps = pca_dev(c, C, n, k, P, Pt, nullptr);
+    PcaStats ps = pca_dev(c, C, n, k, P, Pt, nullptr, cmean);
     trace_mark(s, "pca");
     tm.mark();
     // ---- find_params + final tree (R/TADpole.R:456-460)
@@ -1280,7 +1281,7 @@ extern "C" {
  * segment statistics shared across trees, 1 cap on their store (0 = automatic),
  * 2 short-K panel GEMM, 3 GEMM LDS stage depth (16 / 32), 4 register-resident
  * tridiagonalisation, 5 int8 X'X, 6 PCA degree margin, 7 XCD-aware GEMM order, ..., 14 supertile
- * order of the int8 X'X tiles. */
+ * order of the int8 X'X tiles, ..., 17 C's column means formed by the correlation epilogue. */
 void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
     guarded(status, [&] {
         int *p = nullptr;
@@ -1302,6 +1303,7 @@ void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
         case 14: p = &g_xtx_supertile; break;
         case 15: p = &g_pca_over; break;
         case 16: p = &g_coniss_lu; break;
+        case 17: p = &g_cor_fused; break;
         default: fail(TP_ERR_ARG, "unknown knob");
         }
         if (*which == 3 && *value != 16 && *value != 32) fail(TP_ERR_ARG, "stage depth must be 16 or 32");

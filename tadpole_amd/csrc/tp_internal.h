@@ -64,7 +64,7 @@ struct Ctx {
     hipStream_t cur = nullptr;      // stream used by the current call
     hipStream_t side = nullptr;     // fork-join helper stream (side_stream())
     hipEvent_t fork_ev = nullptr, join_ev = nullptr;
-    DevBuf buf[32];
+    DevBuf buf[40];   // indexed by Slot (static_assert below)
     DevBuf pinned_flag;
     void *host_pinned = nullptr;    // small pinned staging area
     size_t host_pinned_bytes = 0;
@@ -88,8 +88,9 @@ enum Slot {
     S_M = 0, S_ROWMEAN, S_DIAG, S_BAD, S_GOOD, S_NGOOD, S_X, S_COLMEAN,
     S_S, S_C, S_XC, S_XCT, S_G, S_Q, S_Z, S_W, S_SMALL, S_P, S_PT,
     S_SWEEP, S_SWEEP2, S_SCORES, S_PARTIAL, S_MISC, S_SHARD, S_SHARD2, S_DEDUP,
-    S_KRY, S_KRYG, S_KRYT, S_KRYV, S_KRYX
+    S_KRY, S_KRYG, S_KRYT, S_KRYV, S_KRYX, S_CMEAN, S_NSLOT
 };
+static_assert(S_NSLOT <= (int)(sizeof(Ctx::buf) / sizeof(Ctx::buf[0])), "Ctx::buf too small for the slots");
 
 // ---------------------------------------------------------------- kernels
 // mask / correlation / centering  (tp_prep.hip)
@@ -102,8 +103,9 @@ void launch_mask_select(const double *d_rowmean, const double *d_diag, int n0,
 void launch_gather_colmean(const double *d_M, int n0, const int *d_good, int n,
                            double *d_X, double *d_colmean, hipStream_t s);
 void launch_colmean(const double *d_A, int n, int ld, double *d_mean, hipStream_t s);
+// d_cmean != nullptr: the column means of C are formed in the same pass (k_colmean's order)
 void launch_cor_epilogue(const double *d_S, const double *d_m, int n, double *d_C, double *d_sd,
-                         hipStream_t s);
+                         hipStream_t s, double *d_cmean = nullptr);
 void launch_center(const double *d_C, const double *d_mean, int n, double *d_Xc,
                    double *d_XcT, hipStream_t s);
 
@@ -189,6 +191,7 @@ struct SweepDev {
 };
 // scratch of the shared CH segment statistics for ntrees trees
 extern int g_ch_dedup;        // 0: every tree computes its own segment statistics
+extern int g_cor_fused;        // 0: prcomp's column means by a separate pass over C
 extern int g_coniss_lu;       // 0: the global CONISS variant keeps its links in global memory
 extern int g_ch_dedup_ucap;   // > 0: cap on the shared store (tests of the overflow path)
 size_t sweep_dedup_bytes(int n, int k, int ntrees, int seg_cap, int *hcap, int *ucap);
@@ -264,7 +267,8 @@ struct PcaStats {
     int krylov_steps = 0, krylov_dim = 0;   // block Krylov path (0: G formed)
 };
 extern int g_pca_krylov_min, g_pca_krylov_block, g_pca_krylov_steps, g_pca_over;
+// d_cmean: C's column means if the caller already has them (else computed here)
 PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d_Pt,
-                 double *h_sdev);
+                 double *h_sdev, const double *d_cmean = nullptr);
 
 }  // namespace tp

@@ -496,13 +496,18 @@ static void krylov_topk(Ctx &c, const double *Xc, const double *XcT, int n, int 
     gemm_f64(pg, c.buf[S_PARTIAL], s);
 }
 
-PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d_Pt, double *h_sdev) {
+PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d_Pt, double *h_sdev,
+                 const double *d_cmean) {
     PcaStats st;
     hipStream_t s = c.cur;
-    double *mean = c.buf[S_COLMEAN].as<double>(n);
     double *Xc = c.buf[S_XC].as<double>((size_t)n * n);
     double *XcT = c.buf[S_XCT].as<double>((size_t)n * n);
-    launch_colmean(d_C, n, n, mean, s);
+    const double *mean = d_cmean;
+    if (!mean) {
+        double *cm = c.buf[S_COLMEAN].as<double>(n);
+        launch_colmean(d_C, n, n, cm, s);
+        mean = cm;
+    }
     launch_center(d_C, mean, n, Xc, XcT, s);
     double *V = c.buf[S_W].as<double>((size_t)n * k);       // n x k, descending
     std::vector<double> h_theta;

@@ -281,10 +281,50 @@ __global__ void __launch_bounds__(256) k_cor_epilogue(const double *S, const dou
     }
 }
 
-void launch_cor_epilogue(const double *d_S, const double *d_m, int n, double *d_C, double *d_sd, hipStream_t s) {
+int g_cor_fused = 1;
+
+// The same elements, one wave per column j, with C's column mean formed in the same
+// pass: the lane-strided double-double order of k_colmean (rows lane, lane + 64, ...,
+// then the wave sum), so cm[j] has k_colmean's bits and C is not read again for it.
+template <int U>
+__global__ void __launch_bounds__(256) k_cor_epilogue_mean(const double *S, const double *m, const double *sd, int n,
+                                                           double *C, double *cm) {
+    const int lane = threadIdx.x & 63;
+    const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (j >= n) return;
+    const double fn = (double)n, fn1 = (double)(n - 1), mj = m[j], sdj = sd[j];
+    const double *Sj = S + (size_t)j * n;
+    double *Cj = C + (size_t)j * n;
+    double hi = 0.0, lo = 0.0;
+    auto elem = [&](int i, double sij) {
+        const double cij = (sij - fn * (m[i] * mj)) / fn1;
+        double v = cij / (sd[i] * sdj);
+        if (isnan(v)) v = 0.0;
+        Cj[i] = v;
+        dd_add_d(hi, lo, v);
+    };
+    int r = lane;
+    for (; r + 64 * (U - 1) < n; r += 64 * U) {
+        double v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = Sj[r + 64 * u];
+#pragma unroll
+        for (int u = 0; u < U; ++u) elem(r + 64 * u, v[u]);
+    }
+    for (; r < n; r += 64) elem(r, Sj[r]);
+    wave_dd_sum(hi, lo);
+    if (lane == 0) cm[j] = dd_div_d(hi, lo, fn);
+}
+
+void launch_cor_epilogue(const double *d_S, const double *d_m, int n, double *d_C, double *d_sd, hipStream_t s,
+                         double *d_cmean) {
     hipLaunchKernelGGL(k_cor_sd, dim3((n + 255) / 256), dim3(256), 0, s, d_S, d_m, n, d_sd);
-    hipLaunchKernelGGL(k_cor_epilogue, dim3((unsigned)((n + 255) / 256), (unsigned)std::min(n, 65535)), dim3(256), 0,
-                       s, d_S, d_m, d_sd, n, d_C);
+    if (d_cmean)
+        hipLaunchKernelGGL(k_cor_epilogue_mean<8>, dim3((n + 3) / 4), dim3(256), 0, s, d_S, d_m, d_sd, n, d_C,
+                           d_cmean);
+    else
+        hipLaunchKernelGGL(k_cor_epilogue, dim3((unsigned)((n + 255) / 256), (unsigned)std::min(n, 65535)), dim3(256),
+                           0, s, d_S, d_m, d_sd, n, d_C);
     TP_HIP(hipGetLastError());
 }
 

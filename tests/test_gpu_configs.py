@@ -123,6 +123,32 @@ def test_pipeline_krylov_forced_end_to_end(gpu):
     assert np.max(np.abs(a[fin] - b[fin]) / np.abs(b[fin])) < 1e-6
 
 
+@pytest.mark.parametrize("krylov", [True, False])
+def test_cor_epilogue_fused_colmean_same_bits(gpu, krylov):
+    """C's column means formed inside the correlation epilogue (knob 17, default)
+    carry k_colmean's bits: the whole pipeline's output is bit-identical to the
+    separate pass, on both PCA paths."""
+    import tadpole_amd as tp
+    m = synth_hic(2400, SEED_BASE + 79)
+    old8 = G.knob(8, 0 if krylov else 1 << 30)
+    try:
+        runs = []
+        for fused in (1, 0):
+            old = G.knob(17, fused)
+            try:
+                runs.append(tp.TADpole(m, max_pcs=200))
+            finally:
+                G.knob(17, old)
+    finally:
+        G.knob(8, old8)
+    a, b = runs
+    assert (a.n_pcs, a.optimal_n_clusters) == (b.n_pcs, b.optimal_n_clusters)
+    assert np.array_equal(np.asarray(a.scores).view(np.uint64), np.asarray(b.scores).view(np.uint64))
+    assert a.clusters.keys() == b.clusters.keys()
+    for q in a.clusters:
+        assert np.array_equal(a.clusters[q], b.clusters[q]), q
+
+
 # ------------------------------------------------------------ arm path (C5)
 
 @pytest.mark.parametrize("name", ["arm_c5layout", "arm_early"])
