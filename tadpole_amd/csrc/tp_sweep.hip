@@ -153,31 +153,44 @@ __global__ void __launch_bounds__(64) k_seed(SweepDev sd, double *cost0) {
     double *c0 = cost0 + (size_t)ti * coniss_cost_stride(n);
     const int p0 = blockIdx.y * 64;
     const double QNAN = __longlong_as_double(0x7FF8000000000000LL);
-    double x[KMAXSLOT], y[KMAXSLOT];
+    // rows are fetched RB at a time (all their loads in flight before the first
+    // reduction): the walk over 64 positions is otherwise one load latency a step
+    constexpr int RB = 8;
+    double x[KMAXSLOT];
 #pragma unroll
     for (int t = 0; t < KMAXSLOT; ++t) {
         const int j = lane + 64 * t;
-        y[t] = (p0 < n && j < i) ? sd.Pt[(size_t)p0 * ldp + j] : 0.0;
+        x[t] = (p0 < n && j < i) ? sd.Pt[(size_t)p0 * ldp + j] : 0.0;
     }
     double mycost = QNAN;
-    for (int q = 0; q < 64; ++q) {
-        const int p = p0 + q;
-        if (p + 1 >= n) break;
+    for (int q0 = 0; q0 < 64 && p0 + q0 + 1 < n; q0 += RB) {
+        double z[RB][KMAXSLOT];
 #pragma unroll
-        for (int t = 0; t < KMAXSLOT; ++t) {
-            x[t] = y[t];
-            const int j = lane + 64 * t;
-            y[t] = j < i ? sd.Pt[(size_t)(p + 1) * ldp + j] : 0.0;
-        }
-        double acc = 0.0;
+        for (int u = 0; u < RB; ++u) {
+            const int r = p0 + q0 + u + 1;
 #pragma unroll
-        for (int t = 0; t < KMAXSLOT; ++t)
-            if (lane + 64 * t < i) {
-                double e = x[t] - y[t];
-                acc = fma(e, e, acc);
+            for (int t = 0; t < KMAXSLOT; ++t) {
+                const int j = lane + 64 * t;
+                z[u][t] = (r < n && j < i) ? sd.Pt[(size_t)r * ldp + j] : 0.0;
             }
-        double tot = wave_sum(acc);
-        if (lane == q) mycost = nan2inf(tot / 2.0);
+        }
+#pragma unroll
+        for (int u = 0; u < RB; ++u) {
+            const int q = q0 + u;
+            if (p0 + q + 1 < n) {                      // uniform over the wave
+                double acc = 0.0;
+#pragma unroll
+                for (int t = 0; t < KMAXSLOT; ++t)
+                    if (lane + 64 * t < i) {
+                        double e = x[t] - z[u][t];
+                        acc = fma(e, e, acc);
+                    }
+                double tot = wave_sum(acc);
+                if (lane == q) mycost = nan2inf(tot / 2.0);
+            }
+#pragma unroll
+            for (int t = 0; t < KMAXSLOT; ++t) x[t] = z[u][t];
+        }
     }
     c0[p0 + lane] = mycost;
 }
