@@ -154,8 +154,9 @@ __global__ void __launch_bounds__(64) k_seed(SweepDev sd, double *cost0) {
     const int p0 = blockIdx.y * 64;
     const double QNAN = __longlong_as_double(0x7FF8000000000000LL);
     // rows are fetched RB at a time (all their loads in flight before the first
-    // reduction): the walk over 64 positions is otherwise one load latency a step
-    constexpr int RB = 8;
+    // reduction; C3: RB 4 / 8 / 16 = 145 / 150 / 175 us, registers vs latency);
+    // the walk over 64 positions is otherwise one load latency a step
+    constexpr int RB = 4;
     double x[KMAXSLOT];
 #pragma unroll
     for (int t = 0; t < KMAXSLOT; ++t) {
