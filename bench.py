@@ -13,12 +13,25 @@ pipelines run one after another on one stream (N0 over one
 pipeline's wall time).  The throughput of S matrices in flight on S streams is
 reported beside it (`throughput`), never as `value`.
 
-Multi-GPU: one process per GPU (torch.distributed.run); each rank processes its
-own matrix (independent chromosomes): weak scaling, no
-data-path collective.  value = bins of all ranks / max-over-ranks time.
+Multi-GPU: one process per GPU.  `--gpus N` without a torch.distributed
+environment re-launches this script under torch.distributed.run with N ranks
+(as a child process, before anything touches the GPU) and exits with its
+code; under torch.distributed.run WORLD_SIZE must equal --gpus.  Each rank
+processes its own C3 matrix (independent chromosomes): weak
+scaling, no data-path collective, value = bins of all ranks / max-over-ranks
+time; `ranks_seen` is counted over the process group.
 --sharded: one matrix split over all ranks (RCCL all-gathers, strong scaling).
---e2e-tsv N: the north_star end-to-end line instead: TADpole() on an N-bin
+--e2e-tsv N: only the north_star end-to-end line: TADpole() on an N-bin
 tab-separated file (native parse + upload + pipeline + assembly).
+
+North-star lines (same JSON object, after the C3 headline; --no-extras skips):
+  "e2e_10k"    TADpole() on a 10 000-bin TSV file, median of 3, stage breakdown
+               (rank 0 at N=1);
+  "c5_arm"     one 24 300-bin matrix (the C5 p-arm shape) on one GPU, with its
+               parity against tests/golden/c5arm.npz (rank 0 at N=1);
+  "c4_genome"  the 23 hg19 chromosomes @25 kb through run_genome over all
+               ranks (LPT, 8 streams a GPU), parity of four chromosomes
+               against their golden fixtures.
 
 Extra fields: "roofline" for the kernel class with the largest time per
 pipeline (HIP events recorded inside the library on the stream the kernels run
@@ -95,49 +108,189 @@ def parse():
                     help="one matrix split over all ranks (SURVEY §8(e)2, C5 arms): strong scaling")
     ap.add_argument("--e2e-tsv", type=int, default=0,
                     help="end-to-end TADpole() on an N-bin TSV file (parse included) instead of the HBM bench")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the north-star lines (e2e_10k, c5_arm, c4_genome)")
+    ap.add_argument("--extras-reps", type=int, default=3)
     return ap.parse_args()
 
 
-def write_tsv(m, path):
-    """Headerless tab-separated integer matrix (read.big.matrix's input)."""
-    vmax = int(m.max())
-    table = np.array([str(v) for v in range(vmax + 1)], dtype=object)
-    mi = m.astype(np.int64)
-    with open(path, "w") as f:
-        for r in range(mi.shape[0]):
-            f.write("\t".join(table[mi[r]]))
-            f.write("\n")
+def relaunch_if_needed(args, script=None, argv=None):
+    """`--gpus N` outside torch.distributed: run N ranks under
+    torch.distributed.run as a child process (nothing here has touched the
+    GPU) and return its exit code; None when this process is a rank already.
+    ``script``/``argv`` (tests): what the ranks run instead of this file."""
+    import socket
+    import subprocess
+    if "WORLD_SIZE" in os.environ:
+        world = int(os.environ["WORLD_SIZE"])
+        if world != args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr, flush=True)
+            return 2
+        return None
+    if args.gpus <= 1:
+        return None
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", script or os.path.abspath(__file__)]
+    cmd += list(sys.argv[1:] if argv is None else argv)
+    return subprocess.call(cmd)
+
+
+STAGES = ["mask", "cor", "pca", "sweep", "total"]
+
+
+def _stages(timings):
+    return {q: round(float(timings[i]), 3) for i, q in enumerate(STAGES)}
+
+
+def run_e2e_tsv(n0, max_pcs, reps):
+    """north_star: end-to-end TADpole() on an n0-bin matrix file (native parse
+    + upload + device pipeline + host assembly), median of `reps`, and the
+    same call split into its parts (R/TADpole.R:344-349,444-497)."""
+    import tadpole_amd as tp
+    from tadpole_amd.api import _assemble, _pipeline
+    from tadpole_amd.synth import SEED_BASE, synth_hic_par, write_tsv
+    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"tadpole_e2e_{n0}_{os.getpid()}.tsv")
+    t0 = time.perf_counter()
+    size = write_tsv(synth_hic_par(n0, SEED_BASE + 3), path)
+    t_write = time.perf_counter() - t0
+    try:
+        tp.TADpole(path, max_pcs=max_pcs)            # warm-up (device context, code objects)
+        t_all, parts = [], []
+        res = None
+        for _ in range(max(1, reps)):
+            t0 = time.perf_counter()
+            res = tp.TADpole(path, max_pcs=max_pcs)
+            t_all.append(time.perf_counter() - t0)
+        for _ in range(max(1, reps)):               # the same call, piece by piece
+            t0 = time.perf_counter()
+            raw = tp.read_matrix(path)
+            t1 = time.perf_counter()
+            r = _pipeline(raw, max_pcs, 2, 0.01, 0, 0)
+            t2 = time.perf_counter()
+            _assemble(r, np.flatnonzero(r["bad"]) + 1)
+            t3 = time.perf_counter()
+            parts.append((t1 - t0, t2 - t1, t3 - t2, float(r["timings"][4]) * 1e-3))
+            del raw
+    finally:
+        os.remove(path)
+    med = float(np.median(t_all))
+    pm = np.median(np.array(parts), axis=0)
+    return {"metric": "end-to-end TADpole() seconds on an N-bin TSV file (north_star: < 1 s at 10k bins)",
+            "value": round(med, 4), "unit": "s", "higher_is_better": False, "n0": n0, "reps": len(t_all),
+            "all_s": [round(x, 4) for x in t_all], "bins_per_s": round(n0 / med, 1),
+            "breakdown_s": {"parse": round(pm[0], 4), "upload_and_device_pipeline": round(pm[1], 4),
+                            "device_pipeline": round(pm[3], 4), "host_copy_and_sync": round(pm[1] - pm[3], 4),
+                            "host_assembly": round(pm[2], 4)},
+            "tsv_bytes": size, "tsv_write_s": round(t_write, 2), "n_pcs": res.n_pcs,
+            "optimal_n_clusters": res.optimal_n_clusters, "device_stages_ms": _stages(res.timings_ms),
+            "data": "synthetic (tadpole_amd/synth.py synth_hic_par, seed 20261015+3) written as an integer TSV"}
+
+
+def _golden_check(got, z, prefix=""):
+    """Parity of a tadpole object against a committed oracle fixture: TAD
+    coordinates of every level, n_pcs, optimal_n_clusters, bad columns, merge
+    order (bit-exact) and CH scores (max relative error)."""
+    lev = z[prefix + "levels"]
+    co = z[prefix + "coords"]
+    ok = (got.n_pcs == int(z[prefix + "n_pcs"]) and got.optimal_n_clusters == int(z[prefix + "optimal_n_clusters"])
+          and set(got.clusters) == {str(int(q)) for q in lev}
+          and all(np.array_equal(got.clusters[str(int(q))], co[co[:, 0] == q][:, 1:]) for q in lev)
+          and np.array_equal(got.dendro.boundary - 1, z[prefix + "merge_b"]))
+    if (prefix + "bad_idx1") in z and got.bad_columns is not None:
+        ok = ok and np.array_equal(got.bad_columns, z[prefix + "bad_idx1"])
+    a, b = got.scores, z[prefix + "scores"]
+    fin = ~np.isnan(b)
+    rel = float(np.max(np.abs(a[fin] - b[fin]) / np.abs(b[fin]))) if a.shape == b.shape else None
+    return bool(ok and rel is not None and rel < 1e-6), rel
+
+
+def run_c5_arm(device, max_pcs, reps):
+    """One C5-arm-shape matrix (24 300 bins, the p arm of chr1 @5kb) resident
+    in HBM, pipelines one after another on one stream; parity against the
+    oracle fixture tests/golden/c5arm.npz."""
+    import torch
+    from tadpole_amd.api import TADpole
+    from tadpole_amd.synth import SEED_BASE, synth_hic_par
+    n0 = 24300
+    gold = os.path.join(HERE, "tests", "golden", "c5arm.npz")
+    host = synth_hic_par(n0, SEED_BASE + 5)
+    dm = torch.from_numpy(host).to(f"cuda:{device}")
+    del host
+    TADpole(dm, max_pcs=max_pcs, inplace=False)          # warm-up (scratch of this size)
+    ts, res = [], None
+    for _ in range(max(1, reps)):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res = TADpole(dm, max_pcs=max_pcs, inplace=True)   # clean in place: no device copy in the timing
+        ts.append(time.perf_counter() - t0)
+    del dm
+    torch.cuda.empty_cache()
+    med = float(np.median(ts))
+    out = {"n0": n0, "n_good": int(res.timings_ms[14]), "k": int(res.timings_ms[15]), "reps": len(ts),
+           "s_median": round(med, 4), "bins_per_s": round(n0 / med, 1), "stages_ms": _stages(res.timings_ms),
+           "coniss_ms": round(float(res.timings_ms[9]), 3), "xtx_ms": round(float(res.timings_ms[5]), 3),
+           "krylov_steps": int(res.timings_ms[16]), "pca_resid": float(res.timings_ms[13]),
+           "n_pcs": res.n_pcs, "optimal_n_clusters": res.optimal_n_clusters,
+           "workload": "C5 arm shape: synthetic 24300x24300 Hi-C (synth_hic_par, seed 20261015+5), max_pcs=%d, "
+                       "one GPU, resident in HBM" % max_pcs}
+    if os.path.exists(gold) and max_pcs == 200:
+        ok, rel = _golden_check(res, np.load(gold))
+        out["parity"] = {"golden_fixture": "tests/golden/c5arm.npz", "match": ok, "ch_max_rel_err": rel}
+    return out
+
+
+C4_GOLDEN = ("chr21", "chr22", "chr19", "chr1")
+
+
+def run_c4_genome(world, rank, max_pcs, reps, streams=8):
+    """C4: the 23 hg19 chromosomes @25 kb (synthetic counts of the real bin
+    numbers) through run_genome over every rank of the default process group:
+    LPT over ranks, `streams` pipelines in flight per GPU, host-resident
+    matrices (the H2D copies and the host assembly are inside the time).  Each
+    rank builds only its own chromosomes.  Median of `reps` whole runs."""
+    import torch.distributed as dist
+    from tadpole_amd.genome import lpt_assign, matrix_cost, run_genome
+    from tadpole_amd.synth import genome_bins, genome_matrix
+    sizes = genome_bins()
+    plan = lpt_assign({c: matrix_cost(sizes[c]) for c in sizes}, world)
+    t0 = time.perf_counter()
+    mats = {c: (genome_matrix(c) if c in plan[rank] else (lambda c=c: genome_matrix(c))) for c in sizes}
+    t_gen = time.perf_counter() - t0
+    run_genome(mats, sizes=sizes, streams=streams, max_pcs=max_pcs)     # warm-up (contexts, code objects)
+    walls, res = [], None
+    for _ in range(max(1, reps)):
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        res, _ = run_genome(mats, sizes=sizes, streams=streams, max_pcs=max_pcs)
+        if world > 1:
+            dist.barrier()
+        walls.append(time.perf_counter() - t0)
+    if rank != 0:
+        return None
+    bins = sum(sizes.values())
+    wall = float(np.median(walls))
+    out = {"chromosomes": len(sizes), "bins": bins, "ranks": world, "streams_per_rank": streams,
+           "wall_s_median": round(wall, 4), "all_s": [round(x, 4) for x in walls],
+           "bins_per_s": round(bins / wall, 1), "matrix_build_s_rank0": round(t_gen, 2),
+           "workload": "C4: 23 hg19 chromosomes @25 kb (synthetic, synth_hic_par), max_pcs=%d, one run_genome "
+                       "call; host-resident matrices (H2D copies and host assembly included)" % max_pcs}
+    par = {}
+    for c in C4_GOLDEN:
+        gold = os.path.join(HERE, "tests", "golden", f"genome_{c}.npz")
+        if os.path.exists(gold) and max_pcs == 200 and c in res:
+            ok, rel = _golden_check(res[c], np.load(gold))
+            par[c] = {"match": ok, "ch_max_rel_err": rel}
+    if par:
+        out["parity"] = par
+    return out
 
 
 def e2e_tsv(args):
-    """north_star: end-to-end TADpole() on a 10 000-bin matrix file."""
-    import tadpole_amd as tp
-    from tadpole_amd.synth import SEED_BASE, synth_hic
-    n0 = args.e2e_tsv
-    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"tadpole_e2e_{n0}.tsv")
-    m = synth_hic(n0, SEED_BASE + 3)
-    write_tsv(m, path)
-    size = os.path.getsize(path)
-    tp.TADpole(path, max_pcs=args.max_pcs)            # warm-up (device context, code objects)
-    t_parse, t_all = [], []
-    res = None
-    for _ in range(max(1, args.steps)):
-        t0 = time.perf_counter()
-        raw = tp.read_matrix(path)
-        t_parse.append(time.perf_counter() - t0)
-        del raw
-        t0 = time.perf_counter()
-        res = tp.TADpole(path, max_pcs=args.max_pcs)
-        t_all.append(time.perf_counter() - t0)
-    med = float(np.median(t_all))
-    stages = ["mask", "cor", "pca", "sweep", "total"]
-    out = {"metric": "end-to-end TADpole() seconds on an N-bin TSV file (north_star: < 1 s at 10k bins)",
-           "value": round(med, 4), "unit": "s", "higher_is_better": False, "n0": n0, "steps": len(t_all),
-           "tsv_bytes": size, "parse_s_median": round(float(np.median(t_parse)), 4),
-           "bins_per_s": round(n0 / med, 1), "n_pcs": res.n_pcs, "optimal_n_clusters": res.optimal_n_clusters,
-           "device_stages_ms": {q: round(float(res.timings_ms[i]), 3) for i, q in enumerate(stages)},
-           "data": "synthetic (tadpole_amd/synth.py, seed 20261015+3) written as an integer TSV"}
-    os.remove(path)
+    out = run_e2e_tsv(args.e2e_tsv, args.max_pcs, max(1, args.steps))
     line = json.dumps(out)
     print(line, flush=True)
     if args.json_out:
@@ -147,6 +300,9 @@ def e2e_tsv(args):
 
 def main():
     args = parse()
+    rc = relaunch_if_needed(args)
+    if rc is not None:
+        sys.exit(rc)
     if args.throughput_streams > 1 and not args.sharded:
         # concurrent pipelines need one hardware queue per stream (HIP's default
         # is 4 and streams sharing a queue serialise); only before HIP starts
@@ -167,8 +323,16 @@ def main():
         dist.init_process_group("gloo")
     # one GPU per rank; more ranks than GPUs (a rehearsal on a smaller box)
     # share devices round-robin
-    local = local % max(1, torch.cuda.device_count())
+    ndev = max(1, torch.cuda.device_count())
+    local = local % ndev
     torch.cuda.set_device(local)
+    seen = [(rank, local)]
+    if world > 1:
+        seen = [None] * world
+        dist.all_gather_object(seen, (rank, local))
+    if len({r for r, _ in seen}) != args.gpus:
+        raise SystemExit(f"bench.py: {len(seen)} ranks seen, --gpus {args.gpus}")
+    comm_size = None
 
     from tadpole_amd import _lib
     from tadpole_amd.api import _assemble
@@ -183,7 +347,7 @@ def main():
     if args.sharded:
         from tadpole_amd import multi
         if world > 1:
-            multi.init_comm(device=local)
+            comm_size = multi.init_comm(device=local)[1]
         flags |= _lib.TP_FLAG_SHARDED
     k_cap = max(1, min(args.max_pcs, n0))
     w_cap = n0
@@ -293,14 +457,24 @@ def main():
                "note": "S matrices in flight on S streams (own library context each); not `value`"}
         del lanes
 
+    # ---- north-star lines (C3 timing above is untouched by them)
+    extras = {}
+    if not args.no_extras and not args.sharded:
+        if world == 1:
+            extras["e2e_10k"] = run_e2e_tsv(10000, args.max_pcs, args.extras_reps)
+            extras["c5_arm"] = run_c5_arm(local, args.max_pcs, args.extras_reps)
+        c4 = run_c4_genome(world, rank, args.max_pcs, args.extras_reps)
+        if rank == 0:
+            extras["c4_genome"] = c4
+
     if rank == 0:
         value = n0 * (1 if args.sharded else world) * args.steps / elapsed
         share = 1.0 / world if args.sharded else 1.0   # sharded: this rank's part of each product
         krylov_steps, krylov_d, block = int(tm[16]), int(tm[17]), int(tm[12])
         gq_launches = max(1, int(round(tm[8])))
-        if krylov_steps:   # one record = Xc K_t and Xc'(Xc K_t): 2 x 2 N^2 p flops
+        if krylov_steps:   # one record = one product with C (C K_t or C (Xc K_t)): 2 N^2 p flops
             p = krylov_d // max(1, krylov_steps)
-            gq_flops = share * 4.0 * n * n * p
+            gq_flops = share * 2.0 * n * n * p
         else:              # one record = G Q: 2 N^2 b flops
             gq_flops = share * 2.0 * n * n * block
         ns = int(tm[18])   # int8 slices of the exact X'X (0: fp64 product)
@@ -355,6 +529,7 @@ def main():
                "dtype": "f64",
                "data": "synthetic (SURVEY.md §8(d) Hi-C generator, seed 20261015+%d" % cfg +
                        ("" if args.sharded else "+1000*rank") + ")",
+               "ranks_seen": len(seen), "devices_seen": sorted({d for _, d in seen}),
                "config": {"workload": (f"{_config_name(n0, args.max_pcs)}: synthetic {n0}x{n0} Hi-C matrix "
                                        + ("sharded over all GPUs" if args.sharded else "per GPU")
                                        + f", max_pcs={args.max_pcs}, one pipeline at a time on one stream"),
@@ -362,8 +537,11 @@ def main():
                           "parallelism": (f"one matrix over {world} GPU(s): column/row-split products, "
                                           "RCCL all-gather" if args.sharded else f"one matrix per GPU x{world}")},
                "roofline": roof}
+        if comm_size is not None:
+            out["rccl_comm_size"] = comm_size
         if thr:
             out["throughput"] = thr
+        out.update(extras)
         # parity vs the committed oracle fixture of this workload (R-faithful SVD PCA)
         par = {}
         gold = os.path.join(HERE, "tests", "golden", f"c{cfg}.npz")

@@ -58,9 +58,20 @@ enum {
                                    matrix and gets the same results            */
 
 /* ---------------------------------------------------------------- runtime */
-int  tp_version(void);                          /* ABI version, 1                */
+int  tp_version(void);                          /* ABI version, 2 (see below)    */
 int  tp_device_count(void);                     /* HIP devices visible (>=0)     */
 void tp_shutdown(void);                         /* free every device context     */
+/* Free the scratch (device memory, pinned staging) of the context the library
+ * keeps for a caller-supplied stream (*_dev entries with a non-NULL stream: one
+ * context per stream, each holding ~N^2-sized scratch).  A call still running
+ * on that stream keeps its context until it returns; the next call on the
+ * stream makes a new one.  NULL stream: TP_ERR_ARG (tp_shutdown frees the
+ * library's own stream).  Every entry locks the context it uses for the whole
+ * call, so concurrent callers of one stream (or of the library stream)
+ * serialise.  ABI 2: timings_ms of tp_pipeline / tp_pipeline_dev holds 32
+ * doubles (ABI 1: 16) -- a caller built against version 1 must pass NULL
+ * timings or a 32-double buffer. */
+void tp_release_stream(const int *device, void *stream, int *status);
 int  tp_last_error(char *buf, int len);         /* ctypes form                   */
 void tp_last_error_r(char **buf, int *len);     /* R .C form                     */
 

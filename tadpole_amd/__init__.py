@@ -21,8 +21,9 @@ def use_hw_queues(n: int = 16) -> None:
 
 from .api import (Chclust, Mat, Tadpole, TADpole, bin_index, diffT, is_na, is_r_na, load_mat,
                   mask, random_bed, read_matrix)
-from ._lib import TadpoleError
+from ._lib import TadpoleError, release_stream
 
 __all__ = ["TADpole", "load_mat", "diffT", "random_bed", "bin_index", "mask", "read_matrix",
-           "Tadpole", "Chclust", "Mat", "TadpoleError", "is_na", "is_r_na", "use_hw_queues"]
+           "Tadpole", "Chclust", "Mat", "TadpoleError", "is_na", "is_r_na", "use_hw_queues",
+           "release_stream"]
 __version__ = "0.1.0"

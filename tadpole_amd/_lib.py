@@ -19,10 +19,11 @@ TP_FLAG_ROW_MAJOR = 1
 TP_FLAG_CLEAN = 2
 TP_FLAG_NO_MASK = 4
 TP_FLAG_SHARDED = 8
+ABI_VERSION = 2   # tp_version() this binding is written for (timings_ms: 32 doubles)
 
 #: every symbol include/tadpole_hip.h declares
 EXPORTS = (
-    "tp_version", "tp_device_count", "tp_shutdown", "tp_last_error", "tp_last_error_r",
+    "tp_version", "tp_device_count", "tp_shutdown", "tp_release_stream", "tp_last_error", "tp_last_error_r",
     "tp_mask", "tp_mask_dev", "tp_cor", "tp_pca", "tp_sweep", "tp_coniss", "tp_dist", "tp_ch",
     "tp_pipeline", "tp_pipeline_dev", "tp_sweep_dev", "tp_tsv_dims", "tp_read_tsv",
     "tp_comm_unique_id", "tp_comm_init", "tp_comm_destroy", "tp_set_virtual_shards", "tp_shard_plan",
@@ -82,11 +83,14 @@ def load() -> ctypes.CDLL:
     L.tp_tsv_dims.argtypes = [_S, _I, _I, _I]
     L.tp_read_tsv.argtypes = [_S, _I, _I, _I, _I, _D, _I]
     L.tp_sweep_dev.argtypes = [_V, _I, _I, _I, _I, _V, _I, _I, _D, _I, _I, _I, _D, _D, _I]
+    L.tp_release_stream.argtypes = [_I, _V, _I]
     L.tp_comm_unique_id.argtypes = [ctypes.c_char_p, _I]
     L.tp_comm_init.argtypes = [ctypes.c_char_p, _I, _I, _I, _I]
     L.tp_comm_destroy.argtypes = [_I]
     L.tp_set_virtual_shards.argtypes = [_I, _I, _I]
     L.tp_shard_plan.argtypes = [_I, _I, _I, _I, _I]
+    if L.tp_version() != ABI_VERSION:
+        raise ImportError(f"{LIB_PATH}: ABI version {L.tp_version()}, this binding needs {ABI_VERSION} (rebuild)")
     _lib = L
     return L
 
@@ -128,3 +132,20 @@ def cint(v: int) -> ctypes.c_int:
 
 def cdbl(v: float) -> ctypes.c_double:
     return ctypes.c_double(float(v))
+
+
+def release_stream(stream, device: int = None) -> None:
+    """tp_release_stream: free the library context (scratch buffers) of a
+    caller stream -- a torch.cuda.Stream or a raw hipStream_t handle.  Safe
+    while a call on it is still running (that call keeps it until it returns).
+    The library also retires the least recently used idle stream context once
+    a device has TP_MAX_STREAM_CONTEXTS of them (default 8)."""
+    handle = int(getattr(stream, "cuda_stream", stream))
+    if device is None:
+        dev = getattr(stream, "device", None)
+        device = dev.index if getattr(dev, "index", None) is not None else 0
+    L = load()
+    st = ctypes.c_int(0)
+    L.tp_release_stream(ctypes.byref(ctypes.c_int(int(device))), ctypes.c_void_p(int(handle)), ctypes.byref(st))
+    check(st)
+

@@ -509,7 +509,7 @@ def _assemble_rle(t, dendro, levels, good1, bad_idx1) -> Tadpole:
 def TADpole(mat_file, max_pcs: int = 200, min_clusters: int = 2, bad_frac: float = 0.01,
             chr=None, start=None, end=None, resol=None, centromere_search: bool = False,
             device: int = 0, sharded: bool = False, stream=None, fixed_centromere: bool = False,
-            verbose: bool = False) -> Tadpole:
+            verbose: bool = False, inplace: bool = False) -> Tadpole:
     """``TADpole()`` (R/TADpole.R:344-501).  ``mat_file`` may be a path to a
     tab-separated matrix or an in-memory square array.  ``sharded``: split this
     matrix over the ranks of the communicator made by
@@ -518,8 +518,22 @@ def TADpole(mat_file, max_pcs: int = 200, min_clusters: int = 2, bad_frac: float
     ``fixed_centromere``: the centromere split without the reference's q-arm
     index bug (R/TADpole.R:78-80), and the single-matrix path where R would
     fail on a plain matrix (:66-70,356).  ``verbose``: R's message() lines on
-    stderr (always logged on the ``tadpole_amd`` logger)."""
-    raw = mat_file if _is_device(mat_file) else _as_matrix(mat_file)
+    stderr (always logged on the ``tadpole_amd`` logger).
+
+    A GPU-resident ``mat_file`` (a torch tensor) is left untouched: the
+    pipeline cleans (NA -> 0, forceSymmetric, R/TADpole.R:19-20) a device copy.
+    ``inplace=True`` skips that copy (N0^2 doubles of HBM) and cleans the
+    caller's float64 tensor in place.  ``stream`` contexts: see
+    ``tadpole_amd.release_stream``."""
+    if _is_device(mat_file):
+        raw = mat_file
+        if not inplace:
+            import torch
+            raw = raw.to(torch.float64).contiguous()
+            if raw.data_ptr() == mat_file.data_ptr():
+                raw = raw.clone()
+    else:
+        raw = _as_matrix(mat_file)
     shard_flag = _lib.TP_FLAG_SHARDED if sharded else 0
     if not centromere_search:
         res = _pipeline(raw, max_pcs, min_clusters, bad_frac, shard_flag, device, stream)
@@ -546,7 +560,7 @@ def TADpole(mat_file, max_pcs: int = 200, min_clusters: int = 2, bad_frac: float
             raise TypeError("$ operator is invalid for atomic vectors (no centromere split: no bad bin, or the "
                             "longest bad run touches an end of the matrix; R/TADpole.R:66-70,87-90,356)")
         return TADpole(raw, max_pcs, min_clusters, bad_frac, device=device, sharded=sharded, stream=stream,
-                       verbose=verbose)
+                       verbose=verbose, inplace=True)
     return _tadpole_arms(raw, plan, max_pcs, min_clusters, device, shard_flag, stream, verbose)
 
 

@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -122,13 +123,27 @@ void kprof_collect(Ctx &c, double *ms, int *cnt) {
 }
 
 static std::mutex g_mu;
-static Ctx *g_ctx[64] = {nullptr};
+static std::shared_ptr<Ctx> g_ctx[64];
 // contexts of caller-supplied streams: one set of scratch buffers per stream,
 // so pipelines on different streams of one device can run concurrently
-static std::vector<std::pair<hipStream_t, Ctx *>> g_sctx[64];
+static std::vector<std::pair<hipStream_t, std::shared_ptr<Ctx>>> g_sctx[64];
+// the contexts this thread's current C-ABI call holds (locked)
+static thread_local std::vector<std::shared_ptr<Ctx>> t_held;
+static unsigned long long g_tick = 0;
 
-static Ctx *new_ctx(int device) {
-    Ctx *c = new Ctx();
+// at most this many caller-stream contexts per device (env TP_MAX_STREAM_CONTEXTS,
+// default 8): a new one retires the least recently used idle one
+static size_t max_stream_ctx() {
+    static const size_t v = [] {
+        const char *e = getenv("TP_MAX_STREAM_CONTEXTS");
+        const long x = e ? atol(e) : 8;
+        return (size_t)(x < 1 ? 1 : x);
+    }();
+    return v;
+}
+
+static std::shared_ptr<Ctx> new_ctx(int device) {
+    auto c = std::make_shared<Ctx>();
     c->device = device;
     return c;
 }
@@ -138,63 +153,116 @@ Ctx &ctx_for(int device, hipStream_t stream) {
     hipError_t e = hipGetDeviceCount(&ndev);
     if (e != hipSuccess || ndev <= 0) fail(TP_ERR_HIP, "no HIP device available (libtadpole_hip has no CPU path)");
     if (device < 0 || device >= ndev || device >= 64) fail(TP_ERR_ARG, "device index out of range");
-    std::lock_guard<std::mutex> lk(g_mu);
+    std::shared_ptr<Ctx> c, retired;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        TP_HIP(hipSetDevice(device));
+        if (!g_ctx[device]) {
+            auto d = new_ctx(device);
+            TP_HIP(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+            d->owns_stream = true;
+            g_ctx[device] = d;
+        }
+        std::shared_ptr<Ctx> def = g_ctx[device];
+        if (!stream || stream == def->stream) {
+            c = def;
+        } else {
+            for (auto &pr : g_sctx[device])
+                if (pr.first == stream) c = pr.second;
+            if (!c) {
+                auto &v = g_sctx[device];
+                if (v.size() >= max_stream_ctx()) {
+                    // retire the least recently used context no call is using
+                    // (try_lock: not held; lookups need g_mu, which we hold)
+                    size_t best = v.size();
+                    for (size_t q = 0; q < v.size(); ++q)
+                        if ((best == v.size() || v[q].second->last_use < v[best].second->last_use) &&
+                            v[q].second->mu.try_lock()) {
+                            v[q].second->mu.unlock();
+                            best = q;
+                        }
+                    if (best < v.size()) {
+                        retired = std::move(v[best].second);
+                        v.erase(v.begin() + best);
+                    }
+                }
+                c = new_ctx(device);
+                c->stream = stream;
+                c->owns_stream = false;
+                v.push_back({stream, c});
+            }
+            // the communicator belongs to the device: every stream's context uses it
+            c->shard.comm = def->shard.comm;
+            c->shard.rank = def->shard.rank;
+            c->shard.nranks = def->shard.nranks;
+            c->shard.nvirt = def->shard.nvirt;
+        }
+        c->last_use = ++g_tick;
+    }
+    retired.reset();   // frees its device memory (outside the registry lock)
+    // outside the registry lock: a long call on one stream does not block
+    // lookups of the others
+    c->mu.lock();
+    t_held.push_back(c);
     TP_HIP(hipSetDevice(device));
-    if (!g_ctx[device]) {
-        Ctx *c = new_ctx(device);
-        TP_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-        c->owns_stream = true;
-        g_ctx[device] = c;
-    }
-    Ctx *def = g_ctx[device];
-    if (!stream || stream == def->stream) {
-        def->cur = def->stream;
-        return *def;
-    }
-    Ctx *c = nullptr;
-    for (auto &pr : g_sctx[device])
-        if (pr.first == stream) c = pr.second;
-    if (!c) {
-        c = new_ctx(device);
-        c->stream = stream;
-        c->owns_stream = false;
-        g_sctx[device].push_back({stream, c});
-    }
-    c->cur = stream;
-    // the communicator belongs to the device: every stream's context uses it
-    c->shard.comm = def->shard.comm;
-    c->shard.rank = def->shard.rank;
-    c->shard.nranks = def->shard.nranks;
-    c->shard.nvirt = def->shard.nvirt;
+    c->cur = c->stream;
     return *c;
 }
 
-static void free_ctx(Ctx *c) {
-    (void)hipStreamSynchronize(c->stream);
-    for (auto &b : c->buf) b.release();
-    c->pinned_flag.release();
-    if (c->host_pinned) (void)hipHostFree(c->host_pinned);
-    if (c->blas) rocblas_destroy_handle((rocblas_handle)c->blas);
-    if (c->side) {
-        (void)hipStreamSynchronize(c->side);
-        (void)hipStreamDestroy(c->side);
-        (void)hipEventDestroy(c->fork_ev);
-        (void)hipEventDestroy(c->join_ev);
+void ctx_unlock_held() {
+    // unlock in reverse order; dropping the last reference frees a context
+    // that tp_release_stream / tp_shutdown retired during the call
+    while (!t_held.empty()) {
+        std::shared_ptr<Ctx> c = std::move(t_held.back());
+        t_held.pop_back();
+        c->mu.unlock();
     }
-    if (c->owns_stream) (void)hipStreamDestroy(c->stream);
-    delete c;
+}
+
+Ctx::~Ctx() {
+    (void)hipSetDevice(device);
+    if (stream) (void)hipStreamSynchronize(stream);
+    for (auto &b : buf) b.release();
+    pinned_flag.release();
+    if (host_pinned) (void)hipHostFree(host_pinned);
+    if (blas) rocblas_destroy_handle((rocblas_handle)blas);
+    if (side) {
+        (void)hipStreamSynchronize(side);
+        (void)hipStreamDestroy(side);
+        (void)hipEventDestroy(fork_ev);
+        (void)hipEventDestroy(join_ev);
+    }
+    for (auto e : evpool) (void)hipEventDestroy(e);
+    if (owns_stream) (void)hipStreamDestroy(stream);
 }
 
 void ctx_shutdown_all() {
-    std::lock_guard<std::mutex> lk(g_mu);
-    for (int d = 0; d < 64; ++d) {
-        if (!g_ctx[d] && g_sctx[d].empty()) continue;
-        (void)hipSetDevice(d);
-        for (auto &pr : g_sctx[d]) free_ctx(pr.second);
-        g_sctx[d].clear();
-        if (g_ctx[d]) free_ctx(g_ctx[d]);
-        g_ctx[d] = nullptr;
+    std::vector<std::shared_ptr<Ctx>> dead;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        for (int d = 0; d < 64; ++d) {
+            for (auto &pr : g_sctx[d]) dead.push_back(std::move(pr.second));
+            g_sctx[d].clear();
+            if (g_ctx[d]) dead.push_back(std::move(g_ctx[d]));
+        }
     }
+    // contexts in use by another thread are freed when that call ends
+}
+
+bool ctx_release_stream(int device, hipStream_t stream) {
+    std::shared_ptr<Ctx> dead;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        if (device < 0 || device >= 64) return false;
+        auto &v = g_sctx[device];
+        for (size_t q = 0; q < v.size(); ++q)
+            if (v[q].first == stream) {
+                dead = std::move(v[q].second);
+                v.erase(v.begin() + q);
+                break;
+            }
+    }
+    return dead != nullptr;   // freed here, or by the call that still holds it
 }
 
 // ---------------------------------------------------------- host helpers
@@ -552,6 +620,9 @@ static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_cl
 }
 
 template <class F> static void guarded(int *status, F &&f) {
+    struct Unlock {
+        ~Unlock() { ctx_unlock_held(); }
+    } unlock;
     try {
         f();
         if (status) *status = TP_OK;
@@ -575,7 +646,7 @@ using namespace tp;
 
 extern "C" {
 
-int tp_version(void) { return 1; }
+int tp_version(void) { return 2; }
 
 int tp_device_count(void) {
     int n = 0;
@@ -584,6 +655,13 @@ int tp_device_count(void) {
 }
 
 void tp_shutdown(void) { ctx_shutdown_all(); }
+
+void tp_release_stream(const int *device, void *stream, int *status) {
+    guarded(status, [&] {
+        if (!stream) fail(TP_ERR_ARG, "tp_release_stream: NULL stream (the library stream is freed by tp_shutdown)");
+        (void)ctx_release_stream(dev_of(device), (hipStream_t)stream);
+    });
+}
 
 /* ------------------------------------------------------------ multi-GPU */
 void tp_comm_unique_id(char *id, int *status) {

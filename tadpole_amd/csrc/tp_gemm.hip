@@ -75,10 +75,10 @@ __device__ __forceinline__ void store_b(double (*Bs)[KB + 2], const double (&rb)
 // attribute launches; the code is the same.
 template <bool TA, int KB, int TAG = 0>
 __global__ void __launch_bounds__(256) k_gemm_f64(int M, int N, int K, const double *__restrict__ A, int lda,
-                                                  const double *__restrict__ B, int ldb, double *__restrict__ C,
+                                                  const double *__restrict__ B, int ldb, double *C,
                                                   int ldc, int store_t, int sym, int tcol0, int kchunk,
                                                   size_t part_stride, int g_xcd_order,
-                                                  const double *__restrict__ C0 = nullptr) {
+                                                  const double *C0 = nullptr) {   // C0 may alias C (no restrict)
     __shared__ double As[2][BM][KB + 2];
     __shared__ double Bs[2][BN][KB + 2];
     // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs (each
@@ -304,8 +304,8 @@ constexpr int PM = 32, PN = 64, PK = 32, PLD = PK + 2, PSETS = 3;
 template <bool TA>
 __global__ void __launch_bounds__(256) k_gemm_f64_panel(int M, int N, int K, const double *__restrict__ A, int lda,
                                                         const double *__restrict__ B, int ldb,
-                                                        double *__restrict__ C, int ldc, int store_t,
-                                                        const double *__restrict__ C0) {
+                                                        double *C, int ldc, int store_t,
+                                                        const double *C0) {   // C0 may alias C (no restrict)
     __shared__ double As[2][PM][PLD];
     __shared__ double Bs[2][PN][PLD];
     const int tm = (M + PM - 1) / PM;

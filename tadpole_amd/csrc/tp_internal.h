@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <cstddef>
 #include <cstdint>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -46,8 +47,15 @@ struct Shard {
     bool active = false;    // this call runs sharded (TP_FLAG_SHARDED)
 };
 
-// Per-device state: one stream, named scratch buffers.
+// Per-stream state: one stream, named scratch buffers.  Every C-ABI entry
+// holds the context's lock for the whole call (ctx_for takes it, the entry's
+// guard releases it), so callers sharing a stream -- or the default context --
+// serialise instead of racing on the scratch.  Contexts are reference counted:
+// tp_release_stream / tp_shutdown drop the registry's reference and the last
+// holder frees the device memory (~Ctx).
 struct Ctx {
+    ~Ctx();
+    std::recursive_mutex mu;
     Shard shard;
     bool prof = false;                  // record per-kernel events this call
     std::vector<hipEvent_t> evpool;
@@ -57,6 +65,7 @@ struct Ctx {
     int open_cls = -1;
     hipEvent_t open_ev = nullptr;
     int device = 0;
+    unsigned long long last_use = 0;   // registry tick of the last lookup (LRU retirement)
     int last_xtx_ns = 0;            // int8 slices of the last X'X product (0: fp64 MFMA product)
     hipStream_t stream = nullptr;   // library stream (or the caller's, owns_stream = false)
     bool owns_stream = false;
@@ -82,6 +91,8 @@ void kprof_begin(Ctx &c, int cls);
 void kprof_end(Ctx &c, int cls);
 void kprof_collect(Ctx &c, double *ms_per_class, int *count_per_class);
 void ctx_shutdown_all();
+bool ctx_release_stream(int device, hipStream_t stream);   // false: no context for that stream
+void ctx_unlock_held();   // end of a C-ABI call: unlock (and maybe free) the contexts it used
 
 // Scratch slots (indices into Ctx::buf) so stages can share one context.
 enum Slot {

@@ -18,6 +18,12 @@ R/TADpole.R:15-140,344-510):
   fixed, on a C5-layout matrix (centromere past the middle: the q-arm index bug
   drops nothing) and on an early-centromere matrix (the bug drops wrong bins);
 * genome: the three smallest C4 chromosomes (chr21, chr22, chr19 @25 kb).
+* large: the largest single matrices of the BASELINE configs, outputs only:
+  C4's chr1 @25 kb (9 971 bins) and a C5-arm-size matrix
+  (synth_hic_par(24300, SEED_BASE + 5), the p arm's size; the bench's c5_arm
+  line runs the same matrix).  The PCA is LAPACK dsyevr on Xc'Xc (``pca="eigh"``:
+  the same top-k subspaces as R's full SVD at a fraction of its cost); peak
+  host memory ~35 GB at 24.3k bins.
 
 control.bed / case.bed are the reference's own diffT example data
 (inst/extdata) and diffT_curve.json the breakpoints of misc/DiffT_score.png.
@@ -36,7 +42,7 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 import tadpole_oracle as O  # noqa: E402
 from tadpole_amd.synth import (SEED_BASE, early_centromere_matrix, genome_bins, genome_matrix,  # noqa: E402
-                               genome_seed, synth_hic)
+                               genome_seed, synth_hic, synth_hic_par, matrix_checksum)
 
 CASES = [("n64", 64, 20261101, 200), ("n200", 200, 20261016, 200), ("n300", 300, 20261102, 100)]
 CONFIGS = [("c2", 2000, SEED_BASE + 2), ("c3", 7808, SEED_BASE + 3)]
@@ -109,12 +115,35 @@ def genome():
         m = genome_matrix(name)
         r = O.tadpole(m, max_pcs=200, nthreads=THREADS)
         np.savez_compressed(os.path.join(HERE, f"genome_{name}.npz"), n0=genome_bins()[name],
-                            seed=genome_seed(name), max_pcs=200, **outputs(r))
+                            seed=genome_seed(name), max_pcs=200, matrix_checksum=matrix_checksum(m),
+                            **outputs(r))
         print(name, m.shape[0], r.n_pcs, r.optimal_n_clusters)
 
 
+def large():
+    for name, make, seed in (("genome_chr1", lambda: genome_matrix("chr1"), genome_seed("chr1")),
+                             ("c5arm", lambda: synth_hic_par(C5ARM_BINS, SEED_BASE + 5), SEED_BASE + 5)):
+        t0 = time.time()
+        m = make()
+        n0 = m.shape[0]
+        ck = matrix_checksum(m)
+        r = O.tadpole(m, max_pcs=200, nthreads=THREADS, pca="eigh")
+        del m
+        pcs = r.pcs
+        # the spectral gap at k (how well the top-k subspace is defined) for the tests' log
+        sv = np.linalg.norm(pcs, axis=0)
+        np.savez_compressed(os.path.join(HERE, f"{name}.npz"), n0=n0, seed=seed, max_pcs=200,
+                            pc_norms=sv, matrix_checksum=ck, **outputs(r))
+        print(name, n0, r.n_pcs, r.optimal_n_clusters, r.scores.shape, f"{time.time() - t0:.1f} s", flush=True)
+        del r
+
+
+C5ARM_BINS = 24300
+
 if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if what == "large":   # tens of minutes and ~35 GB: never part of "all"
+        large()
     for fn in (small, arms, genome, configs):
         if what in ("all", fn.__name__):
             fn()

@@ -29,7 +29,7 @@ def test_header_symbols_exported():
 
 def test_version_and_status_codes():
     L = _lib.load()
-    assert L.tp_version() == 1
+    assert L.tp_version() == 2
     txt = open(os.path.join(ROOT, "include", "tadpole_hip.h")).read()
     for name, val in [("TP_OK", 0), ("TP_ERR_ARG", 1), ("TP_ERR_HIP", 2), ("TP_ERR_NO_BSTICK", 3)]:
         assert re.search(rf"{name}\s*=\s*{val}\b", txt)

@@ -8,6 +8,11 @@ columns, n_cluster per tree, the final tree's boundary order and hclust merge
 matrix bit-exact; CH scores within 1e-6 relative (NA pattern exact); heights
 within 1e-8 relative (different PCA algorithm from LAPACK: the PC scores agree
 to ~1e-12, not bit for bit).
+
+The hclust ``merge`` comparison is oracle self-consistency: the row order of
+rioja's merge matrix is restated (hclust's hcass2 convention) in both the
+library and the oracle, and no reference-held fixture pins it (parity with R
+unpinned).
 """
 import os
 
@@ -16,7 +21,8 @@ import pytest
 
 import gpu_helpers as G
 import tadpole_oracle as O
-from tadpole_amd.synth import (SEED_BASE, early_centromere_matrix, genome_bins, genome_matrix, synth_hic)
+from tadpole_amd.synth import (SEED_BASE, early_centromere_matrix, genome_bins, genome_matrix, matrix_checksum,
+                               synth_hic, synth_hic_par)
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
@@ -207,6 +213,34 @@ def test_genome_c4_one_gpu(gpu):
     for c in ("chr21", "chr22", "chr19"):
         _check(res[c], np.load(os.path.join(GOLD, f"genome_{c}.npz")))
     print("C4 seconds per chromosome:", {c: round(s, 3) for c, s in sorted(secs.items())})
+
+
+# ------------------------------------ the largest single matrices (oracle)
+
+LARGE = {"genome_chr1": lambda: genome_matrix("chr1"),           # C4's largest chromosome, 9 971 bins
+         "c5arm": lambda: synth_hic_par(24300, SEED_BASE + 5)}   # C5's p-arm shape, 24 300 bins
+
+
+@pytest.mark.parametrize("name", sorted(LARGE))
+def test_large_golden(gpu, name):
+    """The largest single matrices of the BASELINE configs end to end against
+    the oracle (tests/golden/make_golden.py large: LAPACK dsyevr PCA, the C
+    sweep): identical n_pcs, optimal_n_clusters, bad columns, merge order and
+    every level's coordinates, CH within 1e-6 relative.  These are the sizes
+    where the dense PC tail makes CONISS near-ties likeliest
+    (R/TADpole.R:351-442,444-497)."""
+    import tadpole_amd as tp
+    z = np.load(os.path.join(GOLD, f"{name}.npz"))
+    m = LARGE[name]()
+    assert np.array_equal(matrix_checksum(m), z["matrix_checksum"])   # same input as the fixture
+    got = tp.TADpole(m, max_pcs=int(z["max_pcs"]))
+    del m
+    sv = z["pc_norms"]
+    print(f"{name}: n={int(got.timings_ms[14])} n_pcs={got.n_pcs} k*={got.optimal_n_clusters} "
+          f"pca resid {got.timings_ms[13]:.1e} krylov steps {int(got.timings_ms[16])} "
+          f"sigma_k-1/sigma_k {sv[-2] / sv[-1]:.6f}")
+    assert got.timings_ms[13] <= 1e-11
+    _check(got, z)
 
 
 # ------------------------------------------------- C5 at full size (properties)

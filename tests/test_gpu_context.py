@@ -1,0 +1,116 @@
+"""Library context lifetime and concurrency (include/tadpole_hip.h,
+tp_release_stream): one context of ~N^2 scratch per caller stream, retired
+least-recently-used past TP_MAX_STREAM_CONTEXTS (default 8) or freed by
+tadpole_amd.release_stream; every entry locks its context for the whole call,
+so callers sharing the library stream serialise instead of racing."""
+import threading
+
+import numpy as np
+import pytest
+
+from tadpole_amd.synth import synth_hic
+
+pytestmark = pytest.mark.gpu
+
+
+def _used():
+    import torch
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()     # torch caches blocks per stream: not the library's memory
+    free, total = torch.cuda.mem_get_info(0)
+    return total - free
+
+
+def _same(a, b):
+    return (a.n_pcs == b.n_pcs and a.optimal_n_clusters == b.optimal_n_clusters
+            and np.array_equal(np.asarray(a.scores).view(np.uint64), np.asarray(b.scores).view(np.uint64))
+            and a.clusters.keys() == b.clusters.keys()
+            and all(np.array_equal(a.clusters[q], b.clusters[q]) for q in a.clusters))
+
+
+def test_fresh_streams_keep_device_memory_bounded(gpu):
+    """50 TADpole(stream=new) calls: the library keeps at most 8 stream
+    contexts, so device memory stops growing; release_stream frees them."""
+    import torch
+    import tadpole_amd as tp
+    m = synth_hic(3000, 61)
+    ref = tp.TADpole(m, max_pcs=60)
+    gpu.tp_shutdown()            # earlier tests' stream contexts out of the baseline
+    base = _used()
+    streams, used = [], []
+    for i in range(50):
+        s = torch.cuda.Stream()
+        got = tp.TADpole(m, max_pcs=60, stream=s)
+        assert _same(got, ref), i
+        streams.append(s)
+        used.append(_used() - base)
+    per_ctx = max(used[0], 1)
+    print("device memory above baseline after 1, 8, 16, 50 stream calls (MB):",
+          [round(used[q] / 2**20) for q in (0, 7, 15, 49)])
+    assert max(used) <= 8 * per_ctx + (256 << 20)         # bounded by the cap, not by the 50 calls
+    assert used[-1] <= used[15] + (256 << 20)             # flat past the cap
+    for s in streams:
+        tp.release_stream(s)
+    assert _used() - base <= (256 << 20)
+
+
+def test_default_stream_callers_serialise(gpu):
+    """Two host threads on the library stream of one device (no stream given)
+    get the same results as one caller: the context lock serialises them."""
+    import tadpole_amd as tp
+    mats = [synth_hic(1500, 62), synth_hic(1700, 63)]
+    refs = [tp.TADpole(m, max_pcs=80) for m in mats]
+    out = [[None] * 3, [None] * 3]
+    errs = []
+
+    def run(w):
+        try:
+            for r in range(3):
+                out[w][r] = tp.TADpole(mats[w], max_pcs=80)
+        except Exception as e:   # noqa: BLE001
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=run, args=(w,)) for w in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    for w in range(2):
+        for r in range(3):
+            assert _same(out[w][r], refs[w]), (w, r)
+
+
+def test_release_stream_while_in_use(gpu):
+    """Releasing a stream's context while a call runs on it lets that call
+    finish (it holds the context); the next call gets a fresh one."""
+    import torch
+    import tadpole_amd as tp
+    m = synth_hic(2500, 64)
+    s = torch.cuda.Stream()
+    ref = tp.TADpole(m, max_pcs=100, stream=s)
+    res = [None]
+    t = threading.Thread(target=lambda: res.__setitem__(0, tp.TADpole(m, max_pcs=100, stream=s)))
+    t.start()
+    tp.release_stream(s)
+    t.join()
+    assert _same(res[0], ref)
+    assert _same(tp.TADpole(m, max_pcs=100, stream=s), ref)
+    tp.release_stream(s)
+
+
+def test_device_input_not_modified(gpu):
+    """TADpole() on a GPU tensor leaves the caller's tensor as it was (the
+    pipeline cleans a device copy); inplace=True cleans it in place."""
+    import torch
+    import tadpole_amd as tp
+    m = synth_hic(400, 65)
+    m[3, 10] = np.nan
+    m[20, 5] = 7.0                       # asymmetric entry (the upper triangle wins)
+    d = torch.from_numpy(m).cuda()
+    before = d.clone()
+    a = tp.TADpole(d, max_pcs=50)
+    assert torch.equal(torch.nan_to_num(d, nan=-1.0), torch.nan_to_num(before, nan=-1.0))
+    b = tp.TADpole(d, max_pcs=50, inplace=True)
+    assert _same(a, b)
+    assert not torch.isnan(d).any() and torch.equal(d, d.T)

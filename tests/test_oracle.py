@@ -199,3 +199,31 @@ def test_oracle_under_asan():
                        env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1"), timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "MISMATCH" not in r.stdout
+
+
+@pytest.mark.parametrize("name", ["genome_chr21", "genome_chr22", "genome_chr19", "genome_chr1", "c5arm"])
+def test_large_fixture_generator_pinned(name):
+    """The parallel generator (synth_hic_par) reproduces the inputs of the
+    outputs-only fixtures exactly (their matrix_checksum), for any thread count."""
+    from tadpole_amd.synth import SEED_BASE, genome_matrix, matrix_checksum, synth_hic_par
+    g = np.load(os.path.join(GOLD, f"{name}.npz"))
+    if name.startswith("genome_"):
+        m = genome_matrix(name[len("genome_"):])
+    else:
+        m = synth_hic_par(int(g["n0"]), int(g["seed"]), threads=3)
+    assert m.shape[0] == int(g["n0"])
+    assert np.array_equal(matrix_checksum(m), g["matrix_checksum"])
+
+
+def test_write_tsv_round_trip(tmp_path):
+    """The bench's TSV writer (read.big.matrix input) parses back to the matrix."""
+    from tadpole_amd.synth import synth_hic_par, write_tsv
+    m = synth_hic_par(300, 9)
+    m[5, 7] = m[7, 5] = 123456789       # wide field
+    p = tmp_path / "m.tsv"
+    nb = write_tsv(m, str(p), block_rows=7, threads=3)
+    assert nb == p.stat().st_size
+    rows = p.read_text().split("\n")
+    assert rows[-1] == "" and len(rows) == 301
+    back = np.array([[float(x) for x in r.split("\t")] for r in rows[:-1]])
+    assert np.array_equal(back, m)

@@ -6,7 +6,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 rm -rf gpurun_out/prof gpurun_out/pmc_fetch gpurun_out/pmc_write
-B="bench.py --steps ${STEPS:-5} --warmup 1 --throughput-streams 0 --no-cpu-baseline"
+B="bench.py --steps ${STEPS:-5} --warmup 1 --throughput-streams 0 --no-cpu-baseline --no-extras"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 $B --json-out gpurun_out/prof_bench.json > gpurun_out/prof_bench.log 2>&1
 rc=$?; echo "trace rc=$rc"; [ $rc -eq 0 ] || exit $rc
 cut -c1-400 gpurun_out/prof_bench.json
