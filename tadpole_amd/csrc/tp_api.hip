@@ -385,13 +385,14 @@ static SweepOut run_sweep(Ctx &c, const double *d_Pt, int n, int k, int min_clus
     sd.seg = c.buf[S_PARTIAL].as<double>((size_t)k * sd.seg_cap * (k + 1));
     sd.iseg = c.buf[S_MISC].as<int>((size_t)k * (2 * sd.seg_cap + 2) + 64) + 64;
     sd.trS = (double *)(c.buf[S_NGOOD].as<char>(64)) + 2;
-    sd.cost0 = c.buf[S_SMALL].as<double>(sweep_cost0_doubles(n, k));
+    sd.cost0 = c.buf[S_SMALL].as<double>(sweep_cost0_doubles(n, k, k));
     if (g_ch_dedup) {   // CH segment statistics shared across trees
         int hcap = 0, ucap = 0;
         const size_t bytes = sweep_dedup_bytes(n, k, k, sd.seg_cap, &hcap, &ucap);
         sweep_dedup_bind(sd, c.buf[S_DEDUP].as<char>(bytes), hcap, ucap);
     }
     TP_HIP(hipMemsetAsync(err_all, 0, (size_t)R * sizeof(int), s));
+    std::vector<SweepDev> mine;   // this rank's launched shards
     for (int r = 0; r < R; ++r) {
         const int t0 = tb[r], nt = tb[r + 1] - tb[r];
         if (!shard_mine(c, r) || nt == 0) continue;
@@ -407,6 +408,7 @@ static SweepOut run_sweep(Ctx &c, const double *d_Pt, int n, int k, int min_clus
         d.scores = sc_all + (size_t)t0 * sd.w_cap;   // ld = nt
         d.err = err_all + r;
         launch_sweep(d, s, &c);
+        mine.push_back(d);
     }
     {
         std::vector<size_t> off(R + 1);
@@ -430,11 +432,28 @@ static SweepOut run_sweep(Ctx &c, const double *d_Pt, int n, int k, int min_clus
         if (h_nc[i] < 1)
             fail(TP_ERR_NO_BSTICK, "no broken-stick level is significant for PC prefix " + std::to_string(i + 1) +
                                        " (R: invalid 'times' argument at R/TADpole.R:115)");
-    for (int r = 0; r < R; ++r)
-        if (h_err[r])
-            fail(TP_ERR_UNSUPPORTED,
-                 "a PC prefix has more than 1024 significant broken-stick levels: this build's CH kernel "
-                 "holds at most 1024 segments per cut (R's loop at R/TADpole.R:117-120 has no limit)");
+    // trees whose finest cut exceeds k_ch's 1024 LDS segments (R's loop at
+    // R/TADpole.R:117-120 has no limit): the global-memory CH kernel scores
+    // them (on the rank that owns them, before the scores are gathered)
+    for (const SweepDev &d : mine) {
+        std::vector<int> slot(d.ntrees, -1);
+        int nbig = 0, ncmax = 0;
+        for (int ti = 0; ti < d.ntrees; ++ti) {
+            const int nc = h_nc[d.tree0 + ti];
+            if (nc > d.seg_cap) {
+                slot[ti] = nbig++;
+                ncmax = std::max(ncmax, nc);
+            }
+        }
+        if (!nbig) continue;
+        const size_t sd_d = ch_glb_slot_doubles(ncmax, d.k);
+        char *big = c.buf[S_CHBIG].as<char>((size_t)nbig * sd_d * 8 + (size_t)d.ntrees * 4 + 256);
+        int *d_slot = (int *)big;
+        double *scr = (double *)(big + (((size_t)d.ntrees * 4 + 255) & ~(size_t)255));
+        TP_HIP(hipMemcpyAsync(d_slot, slot.data(), (size_t)d.ntrees * 4, hipMemcpyHostToDevice, s));
+        launch_ch_glb(d, d_slot, scr, sd_d, s);
+        TP_HIP(hipStreamSynchronize(s));   // the host slot list lives on this stack frame
+    }
     SweepOut o;
     o.w = *std::max_element(h_nc.begin(), h_nc.end());
     if (o.w > w_cap_host) fail(TP_ERR_CAPACITY, "scores capacity (w_cap) too small: need " + std::to_string(o.w));
@@ -567,14 +586,14 @@ static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_cl
     tm.mark();
     // ---- sparse_cor (R/TADpole.R:94-100,448-449)
     double *S = c.buf[S_S].as<double>((size_t)n * n);
-    double *C = c.buf[S_C].as<double>((size_t)n * n);
+    double *C = c.buf[S_C].as<double>(pca_c_doubles(n));
     {
         kprof_begin(c, K_COR_GEMM);
         trace_mark(s, "cor: start");
         xtx_product(c, X, n, S);
         kprof_end(c, K_COR_GEMM);
     }
-    double *cmean = g_cor_fused ? c.buf[S_CMEAN].as<double>(n) : nullptr;   // C's column means, for prcomp
+    double *cmean = g_cor_fused ? C + (size_t)n * n : nullptr;   // C's column means, for prcomp (C's tail)
     launch_cor_epilogue(S, m, n, C, c.buf[S_DIAG].as<double>(n), s, cmean);
     trace_mark(s, "cor");
     tm.mark();
@@ -775,7 +794,7 @@ void tp_pca(const double *C, const int *n, const int *k, const int *device, doub
         Ctx &c = ctx_for(dev_of(device));
         hipStream_t s = c.cur;
         const int N = *n, K = *k;
-        double *dC = c.buf[S_C].as<double>((size_t)N * N);
+        double *dC = c.buf[S_C].as<double>(pca_c_doubles(N));
         TP_HIP(hipMemcpyAsync(dC, C, (size_t)N * N * 8, hipMemcpyHostToDevice, s));
         double *dP = c.buf[S_P].as<double>((size_t)N * K);
         pca_dev(c, dC, N, K, dP, nullptr, sdev);
@@ -833,7 +852,7 @@ void tp_sweep_dev(const double *d_P, const int *n, const int *k, const int *min_
 void tp_coniss(const double *P, const int *n, const int *ncols, const int *device, int *merge, double *height,
                int *boundary, int *status) {
     guarded(status, [&] {
-        if (!P || !n || !ncols || *n < 2 || *ncols < 1 || *ncols > 256) fail(TP_ERR_ARG, "bad arguments");
+        if (!P || !n || !ncols || *n < 2 || *ncols < 1 || *ncols > 512) fail(TP_ERR_ARG, "bad arguments");
         Ctx &c = ctx_for(dev_of(device));
         hipStream_t s = c.cur;
         const int N = *n, K = *ncols;
@@ -856,7 +875,7 @@ void tp_coniss(const double *P, const int *n, const int *ncols, const int *devic
         sd.cost = (double *)(((uintptr_t)(sd.mrg_b + (N - 1)) + 15) & ~(uintptr_t)15);
         sd.height = sd.cost + (N - 1);
         sd.n_cluster = c.buf[S_MISC].as<int>(64);
-        sd.cost0 = c.buf[S_SMALL].as<double>(sweep_cost0_doubles(N, 1));
+        sd.cost0 = c.buf[S_SMALL].as<double>(sweep_cost0_doubles(N, 1, K));
         sd.w_cap = std::max(1, N - 1);
         // CONISS only (the CH half needs a broken-stick cut; not wanted here)
         launch_coniss_only(sd, s);
@@ -892,7 +911,7 @@ void tp_dist(const double *P, const int *n, const int *ncols, const int *device,
 void tp_ch(const double *P, const int *n, const int *k, const int *labels, const int *cn, const int *device,
            double *ch, int *status) {
     guarded(status, [&] {
-        if (!P || !n || !k || !labels || !cn || *n < 2 || *k < 1 || *k > 256 || *cn < 1 || !ch)
+        if (!P || !n || !k || !labels || !cn || *n < 2 || *k < 1 || *k > 512 || *cn < 1 || !ch)
             fail(TP_ERR_ARG, "bad arguments");
         const int N = *n, K = *k, CN = *cn;
         std::vector<int> bnd(CN + 1);
@@ -1124,7 +1143,7 @@ void tp_debug_coniss_stamps(const double *P, const int *n, const int *k, long lo
         sd.n_cluster = c.buf[S_MISC].as<int>(K + 64);
         long long *dst = (long long *)c.buf[S_SCORES].as<char>((size_t)K * 16 * 8);
         sd.stamps = dst;
-        sd.cost0 = c.buf[S_SMALL].as<double>(sweep_cost0_doubles(N, K));
+        sd.cost0 = c.buf[S_SMALL].as<double>(sweep_cost0_doubles(N, K, K));
         hipEvent_t e0, e1;
         TP_HIP(hipEventCreate(&e0));
         TP_HIP(hipEventCreate(&e1));

@@ -21,12 +21,14 @@
 namespace tp {
 
 constexpr int NB = 32;
-constexpr int BMAX = 480;
+constexpr int BMAX = 480;       // the panel in LDS
+constexpr int BMAX_BIG = 640;   // PG: the panel in global scratch (L2), b up to 640 (k <= 512)
 constexpr int NT = 512;   // threads of k_chol: 8 waves, 256 VGPRs each
 
-template <bool STAMPS>
+// PG: the 32-row panel lives in global scratch Pg (ld b + 8) instead of LDS
+template <bool STAMPS, bool PG = false>
 __global__ void __launch_bounds__(NT) k_chol_t(double *W, double *rdiag, int b, double rel, int *info,
-                                               long long *stamps) {
+                                               long long *stamps, double *Pg = nullptr) {
     long long st_acc[4] = {0, 0, 0, 0};
     long long st_t0 = STAMPS ? (long long)__builtin_amdgcn_s_memtime() : 0;
 #define TP_STAMP(ph)                                                      \
@@ -38,8 +40,11 @@ __global__ void __launch_bounds__(NT) k_chol_t(double *W, double *rdiag, int b, 
     __shared__ double D[NB][NB + 1];       // factored diagonal block U_pp
     __shared__ double rd[NB];              // 1 / diag(U_pp)
     __shared__ double prow[NB];            // pivot row broadcast (wave 0)
-    __shared__ double P[NB][BMAX + 8];     // panel U[o:o+32, o+32:b]
-    __shared__ double scl[BMAX];           // diag(W)^-1/2
+    __shared__ double Psh[PG ? 1 : NB][PG ? 1 : BMAX + 8];   // panel U[o:o+32, o+32:b]
+    __shared__ double scl[PG ? BMAX_BIG : BMAX];             // diag(W)^-1/2
+    double *const Pp = PG ? Pg : &Psh[0][0];
+    const int pld = PG ? b + 8 : BMAX + 8;
+#define P(r, c) Pp[(size_t)(r) * pld + (c)]
     const int t = threadIdx.x;
     const int T = b / NB;
     // ---- Jacobi scaling (van der Sluis): factor W' = S W S, S = diag(W)^-1/2,
@@ -130,7 +135,7 @@ __global__ void __launch_bounds__(NT) k_chol_t(double *W, double *rdiag, int b, 
             }
 #pragma unroll
             for (int r = 0; r < NB; ++r) {
-                P[r][c] = v[r];
+                P(r, c) = v[r];
                 W[(size_t)col * b + o + r] = v[r];
             }
         }
@@ -154,8 +159,8 @@ __global__ void __launch_bounds__(NT) k_chol_t(double *W, double *rdiag, int b, 
                 double ai[8], al[8];
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
-                    ai[u] = P[r][i0 + u];   // P padded: columns >= ncol read stale / zero, unused
-                    al[u] = P[r][l0 + u];
+                    ai[u] = P(r, i0 + u);   // P padded: columns >= ncol read stale / zero, unused
+                    al[u] = P(r, l0 + u);
                 }
 #pragma unroll
                 for (int u = 0; u < 8; ++u)
@@ -200,25 +205,30 @@ __global__ void __launch_bounds__(NT) k_chol_t(double *W, double *rdiag, int b, 
     if (STAMPS && t == 0)
         for (int q = 0; q < 4; ++q) stamps[q] = st_acc[q];
 #undef TP_STAMP
+#undef P
 }
-template __global__ void k_chol_t<false>(double *, double *, int, double, int *, long long *);
-template __global__ void k_chol_t<true>(double *, double *, int, double, int *, long long *);
+template __global__ void k_chol_t<false>(double *, double *, int, double, int *, long long *, double *);
+template __global__ void k_chol_t<true>(double *, double *, int, double, int *, long long *, double *);
+template __global__ void k_chol_t<false, true>(double *, double *, int, double, int *, long long *, double *);
 
 // Q = Z U^{-1}: Z, Q n x b column-major (ld n), U b x b upper (ld b),
 // rdiag = 1 / diag(U).  Workgroup = 16 rows; thread (r, c) = (t & 15, t >> 4).
-constexpr int TR = 16, TC = 16;
-__global__ void __launch_bounds__(256) k_trsm_ru(const double *Z, int n, int b, const double *U,
-                                                 const double *rdiag, double *Q) {
-    __shared__ double Qs[TR][BMAX + 1];
-    __shared__ double Ub[TC][BMAX + 1];
+// TR rows a workgroup (16; 8 for b > 480, where 16 rows of Q and U's column
+// block no longer fit the LDS together)
+constexpr int TC = 16;
+template <int TR, int BM>
+__global__ void __launch_bounds__(TR * TC) k_trsm_ru(const double *Z, int n, int b, const double *U,
+                                                     const double *rdiag, double *Q) {
+    __shared__ double Qs[TR][BM + 1];
+    __shared__ double Ub[TC][BM + 1];
     const int t = threadIdx.x;
-    const int r = t & 15, c = t >> 4;
+    const int r = t % TR, c = t / TR;
     const int row0 = blockIdx.x * TR;
     const int row = row0 + r;
     const bool live = row < n;
     for (int o = 0; o < b; o += TC) {
         // stage U[0:o+TC, o:o+TC] as Ub[c][m] = U(m, o+c)
-        for (int e = t; e < (o + TC) * TC; e += 256) {
+        for (int e = t; e < (o + TC) * TC; e += TR * TC) {
             const int m = e % (o + TC), cc = e / (o + TC);
             Ub[cc][m] = U[(size_t)(o + cc) * b + m];
         }
@@ -253,22 +263,35 @@ __global__ void __launch_bounds__(256) k_trsm_ru(const double *Z, int n, int b, 
         for (int cc = c; cc < b; cc += TC) Q[(size_t)cc * n + row] = Qs[r][cc];
 }
 
-void launch_chol(double *d_W, double *d_rdiag, int b, double rel, int *d_info, hipStream_t s) {
-    if (b % NB != 0 || b > BMAX) fail(TP_ERR_ARG, "chol: block size must be a multiple of 32, <= 480");
-    hipLaunchKernelGGL(k_chol_t<false>, dim3(1), dim3(NT), 0, s, d_W, d_rdiag, b, rel, d_info, nullptr);
+size_t chol_panel_doubles(int b) { return b > BMAX ? (size_t)NB * (b + 8) : 0; }
+void launch_chol(double *d_W, double *d_rdiag, int b, double rel, int *d_info, hipStream_t s, double *d_panel) {
+    if (b % NB != 0 || b > BMAX_BIG) fail(TP_ERR_ARG, "chol: block size must be a multiple of 32, <= 640");
+    if (b > BMAX) {
+        if (!d_panel) fail(TP_ERR_ARG, "chol: b > 480 needs panel scratch (chol_panel_doubles)");
+        hipLaunchKernelGGL((k_chol_t<false, true>), dim3(1), dim3(NT), 0, s, d_W, d_rdiag, b, rel, d_info, nullptr,
+                           d_panel);
+    } else {
+        hipLaunchKernelGGL((k_chol_t<false>), dim3(1), dim3(NT), 0, s, d_W, d_rdiag, b, rel, d_info, nullptr,
+                           nullptr);
+    }
     TP_HIP(hipGetLastError());
 }
 
 void launch_chol_stamped(double *d_W, double *d_rdiag, int b, double rel, int *d_info, long long *d_st,
                          hipStream_t s) {
-    hipLaunchKernelGGL(k_chol_t<true>, dim3(1), dim3(NT), 0, s, d_W, d_rdiag, b, rel, d_info, d_st);
+    if (b % NB != 0 || b > BMAX) fail(TP_ERR_ARG, "chol (stamped): block size must be a multiple of 32, <= 480");
+    hipLaunchKernelGGL((k_chol_t<true>), dim3(1), dim3(NT), 0, s, d_W, d_rdiag, b, rel, d_info, d_st, nullptr);
     TP_HIP(hipGetLastError());
 }
 
 void launch_trsm_ru(const double *d_Z, int n, int b, const double *d_U, const double *d_rdiag, double *d_Q,
                     hipStream_t s) {
-    if (b % TC != 0 || b > BMAX) fail(TP_ERR_ARG, "trsm: block size must be a multiple of 16, <= 480");
-    hipLaunchKernelGGL(k_trsm_ru, dim3((n + TR - 1) / TR), dim3(256), 0, s, d_Z, n, b, d_U, d_rdiag, d_Q);
+    if (b % TC != 0 || b > BMAX_BIG) fail(TP_ERR_ARG, "trsm: block size must be a multiple of 16, <= 640");
+    if (b <= BMAX)
+        hipLaunchKernelGGL((k_trsm_ru<16, BMAX>), dim3((n + 15) / 16), dim3(256), 0, s, d_Z, n, b, d_U, d_rdiag, d_Q);
+    else
+        hipLaunchKernelGGL((k_trsm_ru<8, BMAX_BIG>), dim3((n + 7) / 8), dim3(128), 0, s, d_Z, n, b, d_U, d_rdiag,
+                           d_Q);
     TP_HIP(hipGetLastError());
 }
 

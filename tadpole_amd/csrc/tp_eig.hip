@@ -1,5 +1,5 @@
 // Symmetric eigendecomposition of the small b x b Rayleigh-Ritz matrix of the
-// PCA (H = Q'GQ, b = block size, <= 512), replacing rocSOLVER dsyevd whose
+// PCA (H = Q'GQ, b = block size, <= 640), replacing rocSOLVER dsyevd whose
 // hundreds of tiny launches (latrd column by column) dominated the PCA.
 //
 //   k_sytrd_l   one 1024-thread workgroup reduces H to tridiagonal T = Q_H' H Q_H
@@ -21,7 +21,7 @@
 
 namespace tp {
 
-constexpr int EIG_BMAX = 512;
+constexpr int EIG_BMAX = 640;   // b = k + oversampling for k <= 512
 constexpr int SY_WAVES = 16;
 
 template <int QM, bool ST = false>
@@ -753,14 +753,16 @@ int g_sytrd_reg = 1;   // diagnostics switch: 0 = the L2-resident k_sytrd_l
 // 1: k_bisect + k_invit.
 void eig_sym(rocblas_handle h, double *A, int b, double *theta, double *work, int *info, hipStream_t s,
              int method) {
-    if (!eig_sym_supported(b)) fail(TP_ERR_UNSUPPORTED, "eig_sym: b > 512");
+    if (!eig_sym_supported(b)) fail(TP_ERR_UNSUPPORTED, "eig_sym: b > 640");
     double *C = work, *e = C + (size_t)b * b, *tau = e + b, *dg = tau + b, *lam = dg + b;   // lam: b + 1
     if (sytrd_reg_supported(b) && g_sytrd_reg)
         hipLaunchKernelGGL(k_sytrd_reg, dim3(1), dim3(1024), 0, s, A, b, dg, e, tau);
     else if (b <= 256)
         hipLaunchKernelGGL((k_sytrd_l<4, false>), dim3(1), dim3(1024), 0, s, A, b, dg, e, tau, (long long *)nullptr);
-    else
+    else if (b <= 512)
         hipLaunchKernelGGL((k_sytrd_l<8, false>), dim3(1), dim3(1024), 0, s, A, b, dg, e, tau, (long long *)nullptr);
+    else
+        hipLaunchKernelGGL((k_sytrd_l<10, false>), dim3(1), dim3(1024), 0, s, A, b, dg, e, tau, (long long *)nullptr);
     TP_HIP(hipGetLastError());
     if (method == 0) {
         TP_HIP(hipMemcpyAsync(theta, dg, (size_t)b * sizeof(double), hipMemcpyDeviceToDevice, s));
@@ -773,8 +775,10 @@ void eig_sym(rocblas_handle h, double *A, int b, double *theta, double *work, in
     }
     if (b <= 256)
         hipLaunchKernelGGL(k_ormtr_l<4>, dim3((b + 3) / 4), dim3(256), 0, s, A, tau, b, C);
-    else
+    else if (b <= 512)
         hipLaunchKernelGGL(k_ormtr_l<8>, dim3((b + 3) / 4), dim3(256), 0, s, A, tau, b, C);
+    else
+        hipLaunchKernelGGL(k_ormtr_l<10>, dim3((b + 3) / 4), dim3(256), 0, s, A, tau, b, C);
     TP_HIP(hipGetLastError());
     TP_HIP(hipMemcpyAsync(A, C, (size_t)b * b * sizeof(double), hipMemcpyDeviceToDevice, s));
 }
@@ -788,8 +792,10 @@ void sytrd_which(double *A, int b, double *work, int which, hipStream_t s, long 
         hipLaunchKernelGGL(k_sytrd_reg, dim3(1), dim3(1024), 0, s, A, b, dg, e, tau);
     } else if (b <= 256) {
         hipLaunchKernelGGL((k_sytrd_l<4, false>), dim3(1), dim3(1024), 0, s, A, b, dg, e, tau, (long long *)nullptr);
-    } else {
+    } else if (b <= 512) {
         hipLaunchKernelGGL((k_sytrd_l<8, false>), dim3(1), dim3(1024), 0, s, A, b, dg, e, tau, (long long *)nullptr);
+    } else {
+        hipLaunchKernelGGL((k_sytrd_l<10, false>), dim3(1), dim3(1024), 0, s, A, b, dg, e, tau, (long long *)nullptr);
     }
     TP_HIP(hipGetLastError());
 }

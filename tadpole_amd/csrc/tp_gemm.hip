@@ -523,6 +523,53 @@ __global__ void __launch_bounds__(256) k_splitk_reduce(const double *part, size_
     }
 }
 
+// The same fixed-order reduction with the rank-1 epilogue of GemmArgs::r1_*:
+// rows [0, rows) of C (ldc) = sum(i, j) - u_i sum(vrow, j), where sum(vrow, j)
+// is the value the plain reduction would store for that row (same order)
+template <int TAG = 0>
+__global__ void __launch_bounds__(256) k_splitk_reduce_r1(const double *part, size_t stride, int S, int M, int N,
+                                                          int rows, int vrow, const double *u, double *C, int ldc) {
+    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (size_t)rows * N) return;
+    const int i = (int)(idx % rows), j = (int)(idx / rows);
+    auto red = [&](size_t e) {
+        double v = part[e];
+        int z = 1;
+        for (; z + 8 <= S; z += 8) {
+            double t[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) t[q] = part[e + (size_t)(z + q) * stride];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v = v + t[q];
+        }
+        for (; z < S; ++z) v = v + part[e + (size_t)z * stride];
+        return v;
+    };
+    const double v = red((size_t)i + (size_t)j * M);
+    const double w = red((size_t)vrow + (size_t)j * M);
+    C[(size_t)i + (size_t)j * ldc] = v - (u ? u[i] * w : w);
+}
+
+// Out (rows x N, ld rows) = T(i, j) - u_i T(vrow, j), T(i, j) = T[i rs + j cs]:
+// the rank-1 epilogue on a stored product (a gathered row-major one in the
+// sharded path, rs = N, cs = 1; a column-major one, rs = 1, cs = M); same
+// arithmetic as k_splitk_reduce_r1
+__global__ void __launch_bounds__(256) k_r1_apply(const double *T, size_t rs, size_t cs, int N, int rows, int vrow,
+                                                  const double *u, double *Out) {
+    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (size_t)rows * N) return;
+    const int i = (int)(idx % rows), j = (int)(idx / rows);
+    const double v = T[(size_t)i * rs + (size_t)j * cs], w = T[(size_t)vrow * rs + (size_t)j * cs];
+    Out[idx] = v - (u ? u[i] * w : w);
+}
+void launch_r1_apply(const double *T, size_t rs, size_t cs, int N, int rows, int vrow, const double *u, double *Out,
+                     hipStream_t s) {
+    const size_t tot = (size_t)rows * N;
+    hipLaunchKernelGGL(k_r1_apply, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, T, rs, cs, N, rows, vrow, u,
+                       Out);
+    TP_HIP(hipGetLastError());
+}
+
 // Many partials of a small output (Gram matrices of CholQR, K'W of the Krylov
 // re-orthogonalisation): 64 outputs per workgroup, the partials of each split
 // over the 4 waves (wave w: z = w, w + 4, ...: ascending), the four group sums
@@ -563,6 +610,9 @@ void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s) {
     if (g.M <= 0 || g.N <= 0) return;
     if (g.sub_from && (g.sym_upper || g.store_t || g.rows))
         fail(TP_ERR_ARG, "gemm_f64: C = C0 - A'B only for plain column-major outputs");
+    if (g.r1_vrow >= 0 && (g.store_t || !g.rows || g.r1_rows > g.M || g.r1_vrow >= g.M ||
+                           !(rows_ts(g.K, g.N) && g.trans_a && !g.sym_upper && g.splitk <= 1)))
+        fail(TP_ERR_ARG, "gemm_f64: the rank-1 epilogue is for plain long-K row-shardable products");
     if (g.sym_upper && g.M != g.N) fail(TP_ERR_ARG, "sym_upper GEMM needs a square output");
     const int tm = (g.M + BM - 1) / BM, tn = (g.N + BN - 1) / BN;
     // sym_upper: upper tiles of tile columns [tc0, tc1) (a column shard)
@@ -583,7 +633,8 @@ void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s) {
         double *out = g.C;
         int ldo = g.ldc, st = g.store_t;
         size_t pstride = 0;
-        if (S > 1) {
+        const bool r1 = g.r1_vrow >= 0;
+        if (S > 1 || r1) {   // the rank-1 epilogue runs in the reduction (S = 1: a one-partial reduction)
             pstride = (size_t)g.M * g.N;
             out = work.as<double>(pstride * S);
             ldo = g.M;
@@ -597,7 +648,17 @@ void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s) {
             hipLaunchKernelGGL(k_gemm_ts<0>, grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb, out, ldo, st,
                                kchunk, pstride);
         TP_HIP(hipGetLastError());
-        if (S > 1) {
+        if (r1) {
+            const size_t tot = (size_t)g.r1_rows * g.N;
+            const dim3 rg((unsigned)((tot + 255) / 256));
+            if (g.tag == 1)
+                hipLaunchKernelGGL(k_splitk_reduce_r1<1>, rg, dim3(256), 0, s, out, pstride, S, g.M, g.N, g.r1_rows,
+                                   g.r1_vrow, g.r1_u, g.C, g.ldc);
+            else
+                hipLaunchKernelGGL(k_splitk_reduce_r1<0>, rg, dim3(256), 0, s, out, pstride, S, g.M, g.N, g.r1_rows,
+                                   g.r1_vrow, g.r1_u, g.C, g.ldc);
+            TP_HIP(hipGetLastError());
+        } else if (S > 1) {
             const size_t tot = (size_t)g.M * g.N;
             const dim3 rg((unsigned)((tot + 255) / 256));
             if (g.tag == 1)

@@ -99,7 +99,7 @@ enum Slot {
     S_M = 0, S_ROWMEAN, S_DIAG, S_BAD, S_GOOD, S_NGOOD, S_X, S_COLMEAN,
     S_S, S_C, S_XC, S_XCT, S_G, S_Q, S_Z, S_W, S_SMALL, S_P, S_PT,
     S_SWEEP, S_SWEEP2, S_SCORES, S_PARTIAL, S_MISC, S_SHARD, S_SHARD2, S_DEDUP,
-    S_KRY, S_KRYG, S_KRYT, S_KRYV, S_KRYX, S_CMEAN, S_NSLOT
+    S_KRY, S_KRYG, S_KRYT, S_KRYV, S_KRYX, S_CMEAN, S_CHBIG, S_CHOLP, S_NSLOT
 };
 static_assert(S_NSLOT <= (int)(sizeof(Ctx::buf) / sizeof(Ctx::buf[0])), "Ctx::buf too small for the slots");
 
@@ -139,12 +139,23 @@ struct GemmArgs {
     bool rows = false;           // row-shardable long-K product (rows_gemm_sharded): 128 x 64 kernel, k chunks by K
     const double *sub_from = nullptr;   // C = sub_from - A'B (plain column-major C; may alias C): same bits as
                                         // the product into a temporary and a separate subtraction
+    // rank-1 epilogue of the row-shardable long-K product (rows_ts path): rows
+    // [0, r1_rows) of C (ldc) = (A'B)[i, j] - u_i (A'B)[r1_vrow, j], u = r1_u or
+    // all ones; the M - r1_rows extra rows are computed, not stored
+    int r1_vrow = -1;
+    const double *r1_u = nullptr;
+    int r1_rows = 0;
 };
 void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s);
+void launch_r1_apply(const double *T, size_t rs, size_t cs, int N, int rows, int vrow, const double *u, double *Out,
+                     hipStream_t s);
 extern int g_gemm_panel;   // short-K tall-skinny 32 x 64 kernel enabled (default 1)
 extern int g_gemm_kb;      // LDS stage depth of the 64 x 64 kernel (16 / 32)
 extern int g_gemm_xcd;     // XCD-aware workgroup order of the 64 x 64 kernel (default 1)
-void launch_chol(double *d_W, double *d_rdiag, int b, double rel, int *d_info, hipStream_t s);
+// b <= 640 (a multiple of 32); b > 480 needs chol_panel_doubles(b) of scratch
+size_t chol_panel_doubles(int b);
+void launch_chol(double *d_W, double *d_rdiag, int b, double rel, int *d_info, hipStream_t s,
+                 double *d_panel = nullptr);
 void launch_chol_stamped(double *d_W, double *d_rdiag, int b, double rel, int *d_info, long long *d_st,
                          hipStream_t s);
 void launch_trsm_ru(const double *d_Z, int n, int b, const double *d_U, const double *d_rdiag, double *d_Q,
@@ -188,6 +199,7 @@ struct SweepDev {
     long long *stamps = nullptr;   // diagnostic builds only (k_coniss_t<true>)
     double *cost0 = nullptr;       // ntrees x roundup(n, 64) initial costs (scratch)
     const double *pt2 = nullptr;   // CONISS: the scores with slots 0 and 1 paired (set by the launcher, inside cost0)
+    int pt2_ld = 256;              // its row stride: 64 x the widest tree's slots rounded to 4 or 8
     // CH segment statistics shared across trees (null: every tree computes its
     // own): the finest cuts' segments [s, e) go into an open-addressing set
     // (hkeys, empty = ~0), each distinct one gets a slot of ustore (k column
@@ -215,17 +227,21 @@ __host__ __device__ inline size_t coniss_link_stride(int n) { return (size_t)n +
 // initial costs (ntrees x cost stride) + link scratch of the global-memory
 // CONISS variant (ntrees x 2 link strides of ints)
 // row-major scores Pt (n x k) + slack: CONISS reads whole 64-column slots of a
-// row (up to 256 columns) and masks the columns past its prefix
-inline size_t pt_doubles(int n, int k) { return (size_t)n * k + 256; }
+// row (up to 512 columns) and masks the columns past its prefix
+inline size_t pt_doubles(int n, int k) { return (size_t)n * k + 512; }
 // + the copy of the scores with column pairs (l, l + 64) adjacent that CONISS
-// reads (n x 256, see k_pt_pairs in tp_sweep.hip)
-inline size_t sweep_cost0_doubles(int n, int ntrees) {
-    return (size_t)ntrees * (coniss_cost_stride(n) + coniss_link_stride(n)) + 2 + (size_t)n * 256;
+// reads (n x 256, or n x 512 for k > 256; see k_pt_pairs in tp_sweep.hip)
+inline size_t sweep_cost0_doubles(int n, int ntrees, int k = 256) {
+    return (size_t)ntrees * (coniss_cost_stride(n) + coniss_link_stride(n)) + 2 + (size_t)n * (k > 256 ? 512 : 256);
 }
 size_t sweep_sums_doubles(int n, int tree0, int ntrees);
 void blas_shutdown_all();
 void launch_sweep(const SweepDev &sd, hipStream_t s, Ctx *prof = nullptr);
 void launch_coniss_only(const SweepDev &sd, hipStream_t s);
+// CH of the trees whose finest cut has more than 1024 segments (k_ch's LDS
+// capacity): d_slot_of[ntrees] = scratch slot or -1
+size_t ch_glb_slot_doubles(int nc, int k);
+void launch_ch_glb(const SweepDev &sd, const int *d_slot_of, double *scratch, size_t slot_doubles, hipStream_t s);
 void launch_coniss_stamped(const SweepDev &sd, hipStream_t s);
 void launch_ch_only(const double *d_Pt, int n, int ldp, int k, const int *d_bnd,
                     int cn, double *d_seg, double *d_out, hipStream_t s);
@@ -260,8 +276,14 @@ void shard_gather(Ctx &c, double *buf, const std::vector<size_t> &off);
 void shard_gather_bytes(Ctx &c, void *buf, const std::vector<size_t> &off);
 void shard_bcast_bytes(Ctx &c, void *buf, size_t bytes, int root);
 void sym_gemm_sharded(Ctx &c, GemmArgs g);
+// R1 (optional): Out (r1->rows x N, ld r1->rows) = (A'B)[i, j] - u_i (A'B)[vrow, j]
+struct R1 {
+    int vrow;
+    const double *u;   // nullptr: all ones
+    int rows;
+};
 void rows_gemm_sharded(Ctx &c, const double *A, int lda, int M, const double *B, int ldb, int N, int K,
-                       double *Out, int splitk_plain, int tag = 0);
+                       double *Out, int splitk_plain, int tag = 0, const R1 *r1 = nullptr);
 
 // exact X'X on int8 matrix cores for integer counts (tp_xtx.hip)
 extern int g_xtx_int8;
@@ -278,8 +300,11 @@ struct PcaStats {
     int krylov_steps = 0, krylov_dim = 0;   // block Krylov path (0: G formed)
 };
 extern int g_pca_krylov_min, g_pca_krylov_block, g_pca_krylov_steps, g_pca_over;
-// d_cmean: C's column means if the caller already has them (else computed here)
-PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d_Pt,
+// d_C: n x n, with room for 2n more doubles after it (the Krylov path writes
+// m = colMeans(C) and a column of ones there); d_cmean: C's column means if the
+// caller already has them (may be d_C + n n), else computed here
+inline size_t pca_c_doubles(int n) { return (size_t)n * n + 2 * (size_t)n; }
+PcaStats pca_dev(Ctx &c, double *d_C, int n, int k, double *d_P, double *d_Pt,
                  double *h_sdev, const double *d_cmean = nullptr);
 
 }  // namespace tp

@@ -108,7 +108,8 @@ static void orth_cholqr(Ctx &c, double *Z, double *Qout, double *Tmp, int n, int
             launch_chol_inv(W, Y, X + b, X, b, p == 0 ? shift : 0.0, d_info, c.cur);
             launch_trsm_frag(src, n, b, Y, X + b, dst, c.cur);
         } else {
-            launch_chol(W, X, b, p == 0 ? shift : 0.0, d_info, c.cur);
+            double *panel = b > 480 ? c.buf[S_CHOLP].as<double>(chol_panel_doubles(b)) : nullptr;
+            launch_chol(W, X, b, p == 0 ? shift : 0.0, d_info, c.cur, panel);
             launch_trsm_ru(src, n, b, W, X, dst, c.cur);
         }
         src = dst;
@@ -125,29 +126,9 @@ __global__ void k_cheb(double *Y, const double *GY, const double *Yc, const doub
     Y[t] = v;
 }
 
-// v_j = sum_i w_i Y[i, j] (w = NULL: all ones), one 256-thread workgroup per
-// column j: lane-strided partials, then the canonical wave/workgroup tree.
-// Fixed order for a given n (the same bits on every rank of a sharded run).
-__global__ void __launch_bounds__(256) k_colsum_w(const double *Y, int n, int ldy, const double *w, double *v) {
-    __shared__ double red[4];
-    const int j = blockIdx.x, t = threadIdx.x;
-    const double *y = Y + (size_t)j * ldy;
-    double acc = 0.0;
-    for (int i = t; i < n; i += 256) acc = w ? fma(w[i], y[i], acc) : acc + y[i];
-    acc = wave_sum(acc);
-    if ((t & 63) == 0) red[t >> 6] = acc;
-    __syncthreads();
-    if (t == 0) v[j] = ((red[0] + red[1]) + red[2]) + red[3];
-}
-
-// Y[i, j] -= u_i v_j (u = NULL: all ones): the rank-1 centring corrections of
-// the Krylov products (Xc = C - 1 m', C symmetric: Xc K = C K - 1 (m'K),
-// Xc'Y = C Y - m (1'Y))
-__global__ void __launch_bounds__(256) k_rank1_sub(double *Y, int n, int p, const double *u, const double *v) {
-    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= (size_t)n * p) return;
-    const int i = (int)(idx % n), j = (int)(idx / n);
-    Y[idx] = Y[idx] - (u ? u[i] * v[j] : v[j]);
+__global__ void k_fill_const(double *p, int n, double v) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
 }
 
 // |U_jj| of the last Cholesky (upper triangle of W) -> host, ascending index j
@@ -396,8 +377,8 @@ static void subspace_topk(Ctx &c, const double *A, int n, int k, const Prod &pro
 // itself and the centring is two rank-1 corrections of an n x p block.
 // Blocks K_t (n x p) in S_KRY, G K_t in S_KRYG, T = K'GK in S_KRYT, the small
 // problem's vectors in S_KRYV.
-static void krylov_topk(Ctx &c, const double *C, const double *mean, int n, int k, double *V, double *P,
-                        std::vector<double> &h_theta, PcaStats &st) {
+static void krylov_topk(Ctx &c, double *C, int n, int k, double *V, double *P, std::vector<double> &h_theta,
+                        PcaStats &st) {
     hipStream_t s = c.cur;
     const int p = g_pca_krylov_block > 0 ? g_pca_krylov_block : (k >= 128 ? 64 : 32);
     // D ~ 5k columns; denser spectra of larger matrices need more (C5 arms:
@@ -414,10 +395,9 @@ static void krylov_topk(Ctx &c, const double *C, const double *mean, int n, int 
     const unsigned g1 = (unsigned)((np + 255) / 256);
     // per-step scratch; re-fetched by every extend() because the small
     // problem (subspace_topk) grows and reallocates the same slots
-    double *W, *Zt, *Xp, *Wsm, *Xinv, *Yinv, *rv;
+    double *W, *Zt, *Xp, *Wsm, *Xinv, *Yinv;
     int *d_info;
     auto scratch = [&]() {
-        rv = c.buf[S_MISC].as<double>(64 + 2 * p) + 64;   // m'K_t, 1'(Xc K_t) (first: S_MISC may grow here)
         W = c.buf[S_Q].as<double>(np);
         Zt = c.buf[S_Z].as<double>(np);
         Xp = c.buf[S_SWEEP].as<double>((size_t)p * p * smax);
@@ -456,18 +436,16 @@ static void krylov_topk(Ctx &c, const double *C, const double *mean, int n, int 
             double *Kt = K + (size_t)t * np;
             double *GKt = GK + (size_t)t * np;
             double *XKt = XK + (size_t)t * np;
+            // [C | m | 1]' B: rows n and n + 1 of the product are m'B and 1'B,
+            // so each centring correction rides in the product's reduction
             kprof_begin(c, K_GQ_GEMM);
-            rows_gemm_sharded(c, C, n, n, Kt, n, p, n, XKt, 0, 1);      // C K_t
+            const R1 r_xk{n, nullptr, n};        // Xc K_t = C K_t - 1 (m'K_t)
+            rows_gemm_sharded(c, C, n, n + 2, Kt, n, p, n, XKt, 0, 1, &r_xk);
             kprof_end(c, K_GQ_GEMM);
-            hipLaunchKernelGGL(k_colsum_w, dim3(p), dim3(256), 0, s, Kt, n, n, mean, rv);      // m'K_t
-            hipLaunchKernelGGL(k_rank1_sub, dim3(g1), dim3(256), 0, s, XKt, n, p, (const double *)nullptr,
-                               (const double *)rv);                                           // Xc K_t
             kprof_begin(c, K_GQ_GEMM);
-            rows_gemm_sharded(c, C, n, n, XKt, n, p, n, GKt, 0, 1);     // C (Xc K_t)
+            const R1 r_gk{n + 1, C + (size_t)n * n, n};   // Xc'(Xc K_t) = C (Xc K_t) - m (1'Xc K_t)
+            rows_gemm_sharded(c, C, n, n + 2, XKt, n, p, n, GKt, 0, 1, &r_gk);
             kprof_end(c, K_GQ_GEMM);
-            hipLaunchKernelGGL(k_colsum_w, dim3(p), dim3(256), 0, s, XKt, n, n, (const double *)nullptr, rv + p);
-            hipLaunchKernelGGL(k_rank1_sub, dim3(g1), dim3(256), 0, s, GKt, n, p, mean, (const double *)(rv + p));
-            TP_HIP(hipGetLastError());                                                          // Xc'(Xc K_t)
         }
         built = std::max(built, upto);
     };
@@ -533,7 +511,7 @@ static void krylov_topk(Ctx &c, const double *C, const double *mean, int n, int 
     gemm_f64(pg, c.buf[S_PARTIAL], s);
 }
 
-PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d_Pt, double *h_sdev,
+PcaStats pca_dev(Ctx &c, double *d_C, int n, int k, double *d_P, double *d_Pt, double *h_sdev,
                  const double *d_cmean) {
     PcaStats st;
     hipStream_t s = c.cur;
@@ -549,7 +527,12 @@ PcaStats pca_dev(Ctx &c, const double *d_C, int n, int k, double *d_P, double *d
     const bool krylov = n >= g_pca_krylov_min && b_est < n;
     double *Xc = nullptr, *XcT = nullptr;
     if (krylov) {
-        krylov_topk(c, d_C, mean, n, k, V, d_P, h_theta, st);   // neither Xc nor XcT is formed
+        // C's two extra columns: m (the centring) and ones
+        double *ext = d_C + (size_t)n * n;
+        if (mean != ext) TP_HIP(hipMemcpyAsync(ext, mean, (size_t)n * sizeof(double), hipMemcpyDeviceToDevice, s));
+        hipLaunchKernelGGL(k_fill_const, dim3((n + 255) / 256), dim3(256), 0, s, ext + n, n, 1.0);
+        TP_HIP(hipGetLastError());
+        krylov_topk(c, d_C, n, k, V, d_P, h_theta, st);   // neither Xc nor XcT is formed
     } else {
         Xc = c.buf[S_XC].as<double>((size_t)n * n);
         XcT = c.buf[S_XCT].as<double>((size_t)n * n);

@@ -253,13 +253,21 @@ void xtx_product(Ctx &c, const double *X, int n, double *S) {
 // B K x N: rows of Out split in 64-row blocks, each written transposed into
 // the packed T (N x M col-major = Out row-major), gathered, transposed back.
 void rows_gemm_sharded(Ctx &c, const double *A, int lda, int M, const double *B, int ldb, int N, int K,
-                       double *Out, int splitk_plain, int tag) {
+                       double *Out, int splitk_plain, int tag, const R1 *r1) {
     if (!c.shard.active) {
-        GemmArgs g{M, N, K, A, lda, true, B, ldb, Out, M};
+        const bool fused = r1 && rows_ts(K, N) && splitk_plain <= 1;   // the epilogue rides in the reduction
+        double *dst = (r1 && !fused) ? c.buf[S_SHARD].as<double>((size_t)M * N) : Out;
+        GemmArgs g{M, N, K, A, lda, true, B, ldb, dst, fused ? r1->rows : M};
         g.splitk = splitk_plain;
         g.tag = tag;
         g.rows = true;
+        if (fused) {
+            g.r1_vrow = r1->vrow;
+            g.r1_u = r1->u;
+            g.r1_rows = r1->rows;
+        }
         gemm_f64(g, c.buf[S_PARTIAL], c.cur);
+        if (r1 && !fused) launch_r1_apply(dst, 1, (size_t)M, N, r1->rows, r1->vrow, r1->u, Out, c.cur);
         return;
     }
     const int R = shard_count(c);
@@ -280,7 +288,10 @@ void rows_gemm_sharded(Ctx &c, const double *A, int lda, int M, const double *B,
     std::vector<size_t> off(R + 1);
     for (int r = 0; r <= R; ++r) off[r] = (size_t)rb[r] * N;
     shard_gather(c, T, off);
-    launch_transpose(T, N, M, N, Out, M, c.cur);
+    if (r1)   // same element values as unsharded, then the same rank-1 arithmetic
+        launch_r1_apply(T, (size_t)N, 1, N, r1->rows, r1->vrow, r1->u, Out, c.cur);
+    else
+        launch_transpose(T, N, M, N, Out, M, c.cur);
 }
 
 }  // namespace tp

@@ -23,7 +23,12 @@
 
 namespace tp {
 
-constexpr int KMAXSLOT = 4;   // columns per lane: k <= 256
+// KS: 64-column slots per lane of the kernels that hold all k PCs (4: k <= 256,
+// 8: k <= 512, chosen per launch).  A column past k contributes nothing (its
+// slot is skipped or adds fma(0, 0, acc) = acc), so the bits for k <= 256 are
+// the same with either instance.
+constexpr int KS_MAX = 8;
+inline int ks_for(int k) { return k <= 256 ? 4 : 8; }
 constexpr int ROW_PT = 1 << 30;   // CONISS row code flag: the row is in Pt (a singleton)
 
 // pairwise tree over 64 leaves = the xor butterfly's summation tree
@@ -125,15 +130,15 @@ __device__ __forceinline__ void wave_sum2(double &u, double &v) {
 }
 
 
-// ---- scores for CONISS with column slots 0 and 1 paired: row p of 256
-// doubles, columns l and l + 64 at 2 l and 2 l + 1, columns 128..255 plain
+// ---- scores for CONISS with column slots 0 and 1 paired: row p of W (256 or
+// 512) doubles, columns l and l + 64 at 2 l and 2 l + 1, columns 128..W-1 plain
 // after them (zero past k).  A lane then fetches its first two columns with
 // one 16-byte load; the columns a lane holds and their order are those of the
 // plain layout (same bits).  Slab rows of merged clusters use the same layout.
-__global__ void __launch_bounds__(256) k_pt_pairs(const double *Pt, int n, int ldp, int k, double *Pt2) {
+__global__ void __launch_bounds__(256) k_pt_pairs(const double *Pt, int n, int ldp, int k, double *Pt2, int W) {
     const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= (size_t)n * 256) return;
-    const int p = (int)(idx >> 8), q = (int)(idx & 255);
+    if (idx >= (size_t)n * W) return;
+    const int p = (int)(idx / W), q = (int)(idx % W);
     const int c = q < 128 ? 64 * (q & 1) + (q >> 1) : q;
     Pt2[idx] = c < k ? Pt[(size_t)p * ldp + c] : 0.0;
 }
@@ -146,6 +151,7 @@ static size_t coniss_pt2_offset(int n, int ntrees) {
 // (tree, 64 positions).  The trees' cluster-sum slabs are not seeded: a
 // singleton's sums are its row of the shared scores Pt (read there by
 // k_coniss); a slab row is written only when a merge forms that cluster.
+template <int KS>
 __global__ void __launch_bounds__(64) k_seed(SweepDev sd, double *cost0) {
     const int n = sd.n, ldp = sd.ldp;
     const int ti = blockIdx.x, i = sd.tree0 + ti + 1;
@@ -157,20 +163,20 @@ __global__ void __launch_bounds__(64) k_seed(SweepDev sd, double *cost0) {
     // reduction; C3: RB 4 / 8 / 16 = 145 / 150 / 175 us, registers vs latency);
     // the walk over 64 positions is otherwise one load latency a step
     constexpr int RB = 4;
-    double x[KMAXSLOT];
+    double x[KS];
 #pragma unroll
-    for (int t = 0; t < KMAXSLOT; ++t) {
+    for (int t = 0; t < KS; ++t) {
         const int j = lane + 64 * t;
         x[t] = (p0 < n && j < i) ? sd.Pt[(size_t)p0 * ldp + j] : 0.0;
     }
     double mycost = QNAN;
     for (int q0 = 0; q0 < 64 && p0 + q0 + 1 < n; q0 += RB) {
-        double z[RB][KMAXSLOT];
+        double z[RB][KS];
 #pragma unroll
         for (int u = 0; u < RB; ++u) {
             const int r = p0 + q0 + u + 1;
 #pragma unroll
-            for (int t = 0; t < KMAXSLOT; ++t) {
+            for (int t = 0; t < KS; ++t) {
                 const int j = lane + 64 * t;
                 z[u][t] = (r < n && j < i) ? sd.Pt[(size_t)r * ldp + j] : 0.0;
             }
@@ -181,7 +187,7 @@ __global__ void __launch_bounds__(64) k_seed(SweepDev sd, double *cost0) {
             if (p0 + q + 1 < n) {                      // uniform over the wave
                 double acc = 0.0;
 #pragma unroll
-                for (int t = 0; t < KMAXSLOT; ++t)
+                for (int t = 0; t < KS; ++t)
                     if (lane + 64 * t < i) {
                         double e = x[t] - z[u][t];
                         acc = fma(e, e, acc);
@@ -190,7 +196,7 @@ __global__ void __launch_bounds__(64) k_seed(SweepDev sd, double *cost0) {
                 if (lane == q) mycost = nan2inf(tot / 2.0);
             }
 #pragma unroll
-            for (int t = 0; t < KMAXSLOT; ++t) x[t] = z[u][t];
+            for (int t = 0; t < KS; ++t) x[t] = z[u][t];
         }
     }
     c0[p0 + lane] = mycost;
@@ -300,11 +306,11 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
     // cluster it names, so it flags singletons in what it sends B.
     // rows with NS >= 2: slots 0 and 1 paired (lane l: doubles 2l, 2l + 1),
     // slots 2 and 3 plain -- in the tree's slab (stride ld) and in the shared
-    // paired copy of the scores (stride 256); NS = 1: plain rows, the scores
+    // paired copy of the scores (stride sd.pt2_ld); NS = 1: plain rows, the scores
     // read from Pt itself
     double *S = sd.sums + sums_off(n, sd.tree0, i);
     const double *PP = NS >= 2 ? sd.pt2 : sd.Pt;
-    const size_t ldpp = NS >= 2 ? 256 : (size_t)sd.ldp;
+    const size_t ldpp = NS >= 2 ? (size_t)sd.pt2_ld : (size_t)sd.ldp;
     const bool last_in = lane + 64 * (NS - 1) < i;
     int *mrg_a = sd.mrg_a + (size_t)ti * (n - 1);
     int *mrg_b = sd.mrg_b + (size_t)ti * (n - 1);
@@ -685,7 +691,8 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
 
 // STAMPS: diagnostic build (see coniss_tree2).  BS: block-minimum slots (n <= 4096 BS).
 // LU: the global variant with its links as 16-bit indices in LDS.
-template <bool STAMPS, int BS, bool GLB, bool LU = false>
+// KS: the most column slots a tree of this launch has (4: k <= 256; 8: k <= 512)
+template <bool STAMPS, int BS, bool GLB, bool LU = false, int KS = 4>
 __global__ void __launch_bounds__(128) k_coniss_t(SweepDev sd, double *cost0) {
     extern __shared__ double lds[];
     __shared__ double mb_d[4];
@@ -695,7 +702,17 @@ __global__ void __launch_bounds__(128) k_coniss_t(SweepDev sd, double *cost0) {
         case 1: coniss_tree2<STAMPS, 1, BS, GLB, LU>(sd, cost0, lds, mb_d, mb_i); break;
         case 2: coniss_tree2<STAMPS, 2, BS, GLB, LU>(sd, cost0, lds, mb_d, mb_i); break;
         case 3: coniss_tree2<STAMPS, 3, BS, GLB, LU>(sd, cost0, lds, mb_d, mb_i); break;
-        default: coniss_tree2<STAMPS, 4, BS, GLB, LU>(sd, cost0, lds, mb_d, mb_i); break;
+        case 4: coniss_tree2<STAMPS, 4, BS, GLB, LU>(sd, cost0, lds, mb_d, mb_i); break;
+        default:
+            if constexpr (KS > 4) {
+                switch ((i + 63) / 64) {
+                    case 5: coniss_tree2<STAMPS, 5, BS, GLB, LU>(sd, cost0, lds, mb_d, mb_i); break;
+                    case 6: coniss_tree2<STAMPS, 6, BS, GLB, LU>(sd, cost0, lds, mb_d, mb_i); break;
+                    case 7: coniss_tree2<STAMPS, 7, BS, GLB, LU>(sd, cost0, lds, mb_d, mb_i); break;
+                    default: coniss_tree2<STAMPS, 8, BS, GLB, LU>(sd, cost0, lds, mb_d, mb_i); break;
+                }
+            }
+            break;
     }
 }
 template __global__ void k_coniss_t<false, 1, false>(SweepDev, double *);
@@ -706,75 +723,90 @@ template __global__ void k_coniss_t<false, 8, true, true>(SweepDev, double *);
 template __global__ void k_coniss_t<false, 11, true, true>(SweepDev, double *);
 template __global__ void k_coniss_t<false, 11, true>(SweepDev, double *);
 template __global__ void k_coniss_t<false, 16, true>(SweepDev, double *);
+template __global__ void k_coniss_t<false, 32, true>(SweepDev, double *);
 template __global__ void k_coniss_t<true, 1, false>(SweepDev, double *);
 template __global__ void k_coniss_t<true, 2, false>(SweepDev, double *);
 template __global__ void k_coniss_t<true, 3, false>(SweepDev, double *);
 template __global__ void k_coniss_t<true, 6, true, true>(SweepDev, double *);
 template __global__ void k_coniss_t<true, 16, true>(SweepDev, double *);
+// k in 257..512 (R accepts any max_pcs, R/TADpole.R:344,452): trees of up to 8 slots
+template __global__ void k_coniss_t<false, 1, false, false, 8>(SweepDev, double *);
+template __global__ void k_coniss_t<false, 2, false, false, 8>(SweepDev, double *);
+template __global__ void k_coniss_t<false, 3, false, false, 8>(SweepDev, double *);
+template __global__ void k_coniss_t<false, 6, true, true, 8>(SweepDev, double *);
+template __global__ void k_coniss_t<false, 8, true, true, 8>(SweepDev, double *);
+template __global__ void k_coniss_t<false, 11, true, true, 8>(SweepDev, double *);
+template __global__ void k_coniss_t<false, 11, true, false, 8>(SweepDev, double *);
+template __global__ void k_coniss_t<false, 16, true, false, 8>(SweepDev, double *);
+template __global__ void k_coniss_t<false, 32, true, false, 8>(SweepDev, double *);
 
 // ------------------------------------------------------------ CH over cuts
 // canonical segment statistics of rows s..e, by one wave (see tpo_seg_ss)
-// RB rows per batch (RB x KMAXSLOT loads in flight); the order of the sums is
+// RB rows per batch (RB x KS loads in flight); the order of the sums is
 // the same for any RB
-template <int RB = 4>
+template <int KS, int RB = 4>
 __device__ double seg_ss_wave(const double *Pt, int ldp, int k, int s, int e, double *sumout, int lane) {
     const double fn = (double)(e - s + 1);
-    bool ok[KMAXSLOT];
-    int jj[KMAXSLOT];
+    bool ok[KS];
+    int jj[KS];
 #pragma unroll
-    for (int t = 0; t < KMAXSLOT; ++t) {
+    for (int t = 0; t < KS; ++t) {
         jj[t] = lane + 64 * t;
         ok[t] = jj[t] < k;
         if (!ok[t]) jj[t] = 0;   // safe address, value unused
     }
     // pass 1: column sums, sequential over rows per column; RB rows per step
-    // so RB x KMAXSLOT independent loads are in flight
-    double sj[KMAXSLOT] = {0.0, 0.0, 0.0, 0.0};
+    // so RB x KS independent loads are in flight
+    double sj[KS];
+#pragma unroll
+    for (int t = 0; t < KS; ++t) sj[t] = 0.0;
     int a = s;
     for (; a + RB - 1 <= e; a += RB) {
-        double x[RB][KMAXSLOT];
+        double x[RB][KS];
 #pragma unroll
         for (int r = 0; r < RB; ++r)
 #pragma unroll
-            for (int t = 0; t < KMAXSLOT; ++t) x[r][t] = Pt[(size_t)(a + r) * ldp + jj[t]];
+            for (int t = 0; t < KS; ++t) x[r][t] = Pt[(size_t)(a + r) * ldp + jj[t]];
 #pragma unroll
         for (int r = 0; r < RB; ++r)
 #pragma unroll
-            for (int t = 0; t < KMAXSLOT; ++t) sj[t] = sj[t] + x[r][t];
+            for (int t = 0; t < KS; ++t) sj[t] = sj[t] + x[r][t];
     }
     for (; a <= e; ++a)
 #pragma unroll
-        for (int t = 0; t < KMAXSLOT; ++t) sj[t] = sj[t] + Pt[(size_t)a * ldp + jj[t]];
-    double mj[KMAXSLOT], ss[KMAXSLOT] = {0.0, 0.0, 0.0, 0.0};
+        for (int t = 0; t < KS; ++t) sj[t] = sj[t] + Pt[(size_t)a * ldp + jj[t]];
+    double mj[KS], ss[KS];
 #pragma unroll
-    for (int t = 0; t < KMAXSLOT; ++t) {
+    for (int t = 0; t < KS; ++t) ss[t] = 0.0;
+#pragma unroll
+    for (int t = 0; t < KS; ++t) {
         mj[t] = sj[t] / fn;
         if (sumout && ok[t]) sumout[jj[t]] = sj[t];
     }
     a = s;
     for (; a + RB - 1 <= e; a += RB) {
-        double x[RB][KMAXSLOT];
+        double x[RB][KS];
 #pragma unroll
         for (int r = 0; r < RB; ++r)
 #pragma unroll
-            for (int t = 0; t < KMAXSLOT; ++t) x[r][t] = Pt[(size_t)(a + r) * ldp + jj[t]];
+            for (int t = 0; t < KS; ++t) x[r][t] = Pt[(size_t)(a + r) * ldp + jj[t]];
 #pragma unroll
         for (int r = 0; r < RB; ++r)
 #pragma unroll
-            for (int t = 0; t < KMAXSLOT; ++t) {
+            for (int t = 0; t < KS; ++t) {
                 double d = x[r][t] - mj[t];
                 ss[t] = fma(d, d, ss[t]);
             }
     }
     for (; a <= e; ++a)
 #pragma unroll
-        for (int t = 0; t < KMAXSLOT; ++t) {
+        for (int t = 0; t < KS; ++t) {
             double d = Pt[(size_t)a * ldp + jj[t]] - mj[t];
             ss[t] = fma(d, d, ss[t]);
         }
     double part = 0.0;
 #pragma unroll
-    for (int t = 0; t < KMAXSLOT; ++t)
+    for (int t = 0; t < KS; ++t)
         if (ok[t]) part = part + ss[t];
     return wave_sum(part);
 }
@@ -783,8 +815,9 @@ __device__ double seg_ss_wave(const double *Pt, int ldp, int k, int s, int e, do
 // of seg_ss_wave, combined in slot order through LDS exactly as its `part`:
 // same bits).  Rows stream in batches of 32 with the next batch's loads
 // issued before the current batch is summed (the pass is latency-bound).
-__global__ void __launch_bounds__(256) k_trS(const double *Pt, int n, int ldp, int k, double *out) {
-    __shared__ double ssl[KMAXSLOT][64];
+template <int KS>
+__global__ void __launch_bounds__(64 * KS) k_trS(const double *Pt, int n, int ldp, int k, double *out) {
+    __shared__ double ssl[KS][64];
     constexpr int RB = 32;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int j = lane + 64 * w;
@@ -831,7 +864,7 @@ __global__ void __launch_bounds__(256) k_trS(const double *Pt, int n, int ldp, i
     if (w == 0) {
         double part = 0.0;
 #pragma unroll
-        for (int t = 0; t < KMAXSLOT; ++t)
+        for (int t = 0; t < KS; ++t)
             if (lane + 64 * t < k) part = part + ssl[t][lane];
         const double v = wave_sum(part);
         if (lane == 0) *out = v;
@@ -911,6 +944,7 @@ __global__ void __launch_bounds__(256) k_ch_cut(SweepDev sd) {
 }
 
 // one wave per distinct segment (grid-stride): k column sums + SS
+template <int KS>
 __global__ void __launch_bounds__(256) k_ch_segstat(SweepDev sd) {
     const int lane = threadIdx.x & 63;
     const int wv = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
@@ -921,7 +955,7 @@ __global__ void __launch_bounds__(256) k_ch_segstat(SweepDev sd) {
         const unsigned long long key = sd.ukey[idx];
         const int s = (int)(key >> 32), e = (int)(unsigned)(key & 0xFFFFFFFFULL);
         double *dst = sd.ustore + (size_t)idx * (k + 1);
-        const double ss = seg_ss_wave(sd.Pt, sd.ldp, k, s, e - 1, dst, lane);
+        const double ss = seg_ss_wave<KS>(sd.Pt, sd.ldp, k, s, e - 1, dst, lane);
         if (lane == 0) dst[k] = ss;
     }
 }
@@ -953,6 +987,7 @@ void sweep_dedup_bind(SweepDev &sd, void *base, int hcap, int ucap) {
     sd.hcap = hcap;
     sd.ucap = ucap;
 }
+template <int KS>
 __global__ void __launch_bounds__(CH_THREADS) k_ch(SweepDev sd) {
     __shared__ int segs[CH_SEGMAX + 1], mbl[CH_SEGMAX];
     __shared__ int src[CH_SEGMAX];   // segment's statistics: ustore index, or -1 = this tree's scratch
@@ -995,13 +1030,13 @@ __global__ void __launch_bounds__(CH_THREADS) k_ch(SweepDev sd) {
         __syncthreads();
         for (int g = w; g < nc; g += nw)   // the store was full: the tree's own
             if (src[g] < 0) {
-                const double ss = seg_ss_wave(sd.Pt, ldp, k, segs[g], segs[g + 1] - 1, seg + (size_t)g * k, lane);
+                const double ss = seg_ss_wave<KS>(sd.Pt, ldp, k, segs[g], segs[g + 1] - 1, seg + (size_t)g * k, lane);
                 if (lane == 0) ssg[g] = ss;
             }
     } else {
         finest_cut(sd, ti, nc, mbl, segs);
         for (int g = w; g < nc; g += nw) {
-            double ss = seg_ss_wave(sd.Pt, ldp, k, segs[g], segs[g + 1] - 1, seg + (size_t)g * k, lane);
+            double ss = seg_ss_wave<KS>(sd.Pt, ldp, k, segs[g], segs[g + 1] - 1, seg + (size_t)g * k, lane);
             if (lane == 0) { ssg[g] = ss; src[g] = -1; }
         }
     }
@@ -1037,15 +1072,15 @@ __global__ void __launch_bounds__(CH_THREADS) k_ch(SweepDev sd) {
         const int ix = src[g];
         return ix >= 0 ? sd.ustore + (size_t)ix * (k + 1) : seg + (size_t)g * k;
     };
-    auto load4 = [&](double (&d)[KMAXSLOT], const double *p) {
+    auto load4 = [&](double (&d)[KS], const double *p) {
 #pragma unroll
-        for (int t = 0; t < KMAXSLOT; ++t) {
+        for (int t = 0; t < KS; ++t) {
             const int j = lane + 64 * t;
             d[t] = j < k ? p[j] : 0.0;
         }
     };
     int lev = nc - 1;
-    double A[KMAXSLOT], B[KMAXSLOT], M[KMAXSLOT], A2[KMAXSLOT], B2[KMAXSLOT];
+    double A[KS], B[KS], M[KS], A2[KS], B2[KS];
     int ga = 0, gb = 0, nx = 0;
     if (lev >= m && lev >= 1) {
         gb = gbl[lev - 1];
@@ -1078,7 +1113,7 @@ __global__ void __launch_bounds__(CH_THREADS) k_ch(SweepDev sd) {
         const double fa = (double)na, fb = (double)nbb;
         double acc = 0.0;
 #pragma unroll
-        for (int t = 0; t < KMAXSLOT; ++t) {
+        for (int t = 0; t < KS; ++t) {
             const int j = lane + 64 * t;
             if (j < k) {
                 const double t1 = A[t] * fb;
@@ -1091,7 +1126,7 @@ __global__ void __launch_bounds__(CH_THREADS) k_ch(SweepDev sd) {
         trW = trW + tot / (fa * fb * (fa + fb));
         double *DA = seg + (size_t)ga * k;   // the merged segment's sums
 #pragma unroll
-        for (int t = 0; t < KMAXSLOT; ++t) {
+        for (int t = 0; t < KS; ++t) {
             const int j = lane + 64 * t;
             M[t] = A[t] + B[t];
             if (j < k) DA[j] = M[t];
@@ -1101,7 +1136,7 @@ __global__ void __launch_bounds__(CH_THREADS) k_ch(SweepDev sd) {
                 lev == 1 ? r_nan() : ((double)(n - lev) * (trS - trW)) / ((double)(lev - 1) * trW);
         if (more) {
 #pragma unroll
-            for (int t = 0; t < KMAXSLOT; ++t) {
+            for (int t = 0; t < KS; ++t) {
                 A[t] = ga2 == ga ? M[t] : A2[t];
                 B[t] = gb2 == ga ? M[t] : B2[t];
             }
@@ -1110,6 +1145,115 @@ __global__ void __launch_bounds__(CH_THREADS) k_ch(SweepDev sd) {
             nx = nx2;
         }
     }
+}
+
+// ---- CH for trees whose finest cut exceeds k_ch's LDS capacity (more than
+// CH_SEGMAX = 1024 significant broken-stick levels; R's loop at
+// R/TADpole.R:117-120 has no limit): the same arithmetic as k_ch without the
+// shared segment store, with the cut, the level structure and the segment sums
+// in global scratch.  slot_of[ti]: the tree's scratch slot (-1: k_ch scored it).
+template <int KS>
+__global__ void __launch_bounds__(256) k_ch_glb(SweepDev sd, const int *slot_of, double *scratch,
+                                                size_t slot_doubles) {
+    const int ti = blockIdx.x;
+    const int sl = slot_of[ti];
+    if (sl < 0) return;
+    const int n = sd.n, k = sd.k, ldp = sd.ldp;
+    const int nc = sd.n_cluster[ti];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    double *base = scratch + (size_t)sl * slot_doubles;
+    double *seg = base;                                 // nc x k segment sums
+    double *ssg = seg + (size_t)nc * k;                 // nc segment SS
+    int *segs = (int *)(ssg + nc);                      // nc + 1 cut positions
+    int *mbl = segs + nc + 1, *gbl = mbl + nc, *lnk_l = gbl + nc, *lnk_r = lnk_l + nc;
+    const int ldsc = sd.ntrees;
+    double *score_row = sd.scores + ti;
+    const int m = sd.min_clusters < nc ? sd.min_clusters : nc;
+    const int *mb = sd.mrg_b + (size_t)ti * (n - 1);
+    // finest cut (as finest_cut, in global memory)
+    for (int t = threadIdx.x; t < nc - 1; t += blockDim.x) mbl[t] = mb[n - 2 - t];
+    __syncthreads();
+    for (int t = threadIdx.x; t < nc - 1; t += blockDim.x) {
+        const int bt = mbl[t];
+        int rank = 0;
+        for (int u = 0; u < nc - 1; ++u) rank += mbl[u] < bt;
+        segs[rank + 1] = bt;
+    }
+    if (threadIdx.x == 0) {
+        segs[0] = 0;
+        segs[nc] = n;
+    }
+    __syncthreads();
+    for (int g = w; g < nc; g += nw) {
+        const double ss = seg_ss_wave<KS>(sd.Pt, ldp, k, segs[g], segs[g + 1] - 1, seg + (size_t)g * k, lane);
+        if (lane == 0) ssg[g] = ss;
+    }
+    for (int t = threadIdx.x; t < nc - 1; t += blockDim.x) {
+        const int bt = mb[n - 2 - t];
+        int lo = 1, hi = nc - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (segs[mid] < bt) lo = mid + 1;
+            else hi = mid;
+        }
+        gbl[t] = lo;
+    }
+    for (int g = threadIdx.x; g < nc; g += blockDim.x) {
+        lnk_l[g] = g - 1;
+        lnk_r[g] = g + 1;
+    }
+    __syncthreads();
+    if (w != 0) return;
+    const double trS = *sd.trS;
+    double trW = 0.0;
+    for (int g = 0; g < nc; ++g) trW = trW + ssg[g];
+    if (lane == 0)
+        score_row[(size_t)(nc - 1) * ldsc] = ((double)(n - nc) * (trS - trW)) / ((double)(nc - 1) * trW);
+    for (int lev = nc - 1; lev >= m && lev >= 1; --lev) {
+        const int gb = gbl[lev - 1];
+        const int ga = lnk_l[gb];
+        const int nx = lnk_r[gb];
+        const int b = segs[gb];
+        const int na = b - segs[ga];
+        const int nbb = (nx < nc ? segs[nx] : n) - b;
+        const double fa = (double)na, fb = (double)nbb;
+        double *DA = seg + (size_t)ga * k;
+        const double *DB = seg + (size_t)gb * k;
+        double acc = 0.0, Mv[KS];
+#pragma unroll
+        for (int t = 0; t < KS; ++t) {
+            const int j = lane + 64 * t;
+            const double a = j < k ? DA[j] : 0.0, bv = j < k ? DB[j] : 0.0;
+            if (j < k) {
+                const double t1 = a * fb;
+                const double t2 = bv * fa;
+                const double e = t1 - t2;
+                acc = fma(e, e, acc);
+            }
+            Mv[t] = a + bv;
+        }
+        const double tot = wave_sum(acc);
+        trW = trW + tot / (fa * fb * (fa + fb));
+#pragma unroll
+        for (int t = 0; t < KS; ++t) {
+            const int j = lane + 64 * t;
+            if (j < k) DA[j] = Mv[t];
+        }
+        lnk_r[ga] = nx;
+        if (nx < nc) lnk_l[nx] = ga;
+        if (lane == 0)
+            score_row[(size_t)(lev - 1) * ldsc] =
+                lev == 1 ? r_nan() : ((double)(n - lev) * (trS - trW)) / ((double)(lev - 1) * trW);
+    }
+}
+
+size_t ch_glb_slot_doubles(int nc, int k) { return (size_t)nc * (k + 1) + (size_t)(5 * nc + 2) / 2 + 8; }
+void launch_ch_glb(const SweepDev &sd, const int *d_slot_of, double *scratch, size_t slot_doubles, hipStream_t s) {
+    if (ks_for(sd.k) == 4)
+        hipLaunchKernelGGL(k_ch_glb<4>, dim3(sd.ntrees), dim3(256), 0, s, sd, d_slot_of, scratch, slot_doubles);
+    else
+        hipLaunchKernelGGL(k_ch_glb<8>, dim3(sd.ntrees), dim3(256), 0, s, sd, d_slot_of, scratch, slot_doubles);
+    TP_HIP(hipGetLastError());
 }
 
 __global__ void k_fill(double *p, size_t cnt, double v) {
@@ -1121,13 +1265,22 @@ static size_t coniss_lds_bytes(int n) {   // costs, links, right ends (the mailb
     return coniss_cost_stride(n) * 8 + coniss_link_stride(n) * 8;
 }
 constexpr size_t kConissGlbLds = 16;   // nothing: the mailbox is static LDS
-constexpr int kConissMaxN = 64 * 64 * 16;             // global variant: 16 block-minimum slots
+constexpr int kConissMaxN = 64 * 64 * 32;             // global variant: up to 32 block-minimum slots
 static bool coniss_in_lds(int n) { return coniss_lds_bytes(n) <= 160 * 1024 - 256 && n <= 64 * 64 * 3; }   // 256: static mailbox
 
 // seed kernel + CONISS (cost0 = initial adjacent costs, ntrees x nbk*64, then
 // the global-variant link scratch: see sweep_cost0_doubles)
 template <bool STAMPS, int BS, bool GLB, bool LU = false>
 static void launch_coniss_bs(const SweepDev &sd, double *cost0, size_t lds, hipStream_t s) {
+    if (sd.tree0 + sd.ntrees > 256) {   // trees of 5..8 column slots
+        if constexpr (!STAMPS) {
+            TP_HIP(hipFuncSetAttribute((const void *)k_coniss_t<false, BS, GLB, LU, 8>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            hipLaunchKernelGGL((k_coniss_t<false, BS, GLB, LU, 8>), dim3(sd.ntrees), dim3(128), lds, s, sd, cost0);
+            return;
+        }
+        fail(TP_ERR_UNSUPPORTED, "stamped CONISS: at most 256 columns");
+    }
     TP_HIP(hipFuncSetAttribute((const void *)k_coniss_t<STAMPS, BS, GLB, LU>,
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL((k_coniss_t<STAMPS, BS, GLB, LU>), dim3(sd.ntrees), dim3(128), lds, s, sd, cost0);
@@ -1138,15 +1291,20 @@ static void run_coniss(const SweepDev &sd_in, hipStream_t s, bool stamped, Ctx *
     SweepDev sd = sd_in;
     const int nbk = (sd.n + 63) / 64;
     double *cost0 = sd.cost0;
+    const int ks = ks_for(sd.tree0 + sd.ntrees);   // slots of the widest tree of this launch
     if (sd.tree0 + sd.ntrees > 64) {   // trees with two or more slots read the paired copy
         double *pt2 = cost0 + coniss_pt2_offset(sd.n, sd.ntrees);
-        const size_t cnt = (size_t)sd.n * 256;
+        sd.pt2_ld = 64 * ks;
+        const size_t cnt = (size_t)sd.n * sd.pt2_ld;
         hipLaunchKernelGGL(k_pt_pairs, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, sd.Pt, sd.n, sd.ldp, sd.k,
-                           pt2);
+                           pt2, sd.pt2_ld);
         TP_HIP(hipGetLastError());
         sd.pt2 = pt2;
     }
-    hipLaunchKernelGGL(k_seed, dim3(sd.ntrees, nbk), dim3(64), 0, s, sd, cost0);
+    if (ks == 4)
+        hipLaunchKernelGGL(k_seed<4>, dim3(sd.ntrees, nbk), dim3(64), 0, s, sd, cost0);
+    else
+        hipLaunchKernelGGL(k_seed<8>, dim3(sd.ntrees, nbk), dim3(64), 0, s, sd, cost0);
     TP_HIP(hipGetLastError());
     const bool in_lds = coniss_in_lds(sd.n);
     // global variant: 16-bit links in LDS when they fit (costs stay global)
@@ -1160,7 +1318,8 @@ static void run_coniss(const SweepDev &sd_in, hipStream_t s, bool stamped, Ctx *
     // ballots, the block-minimum updates -- runs over all of them)
     if (stamped) {
         if (lu && bs <= 6) launch_coniss_bs<true, 6, true, true>(sd, cost0, lds, s);
-        else if (!in_lds) launch_coniss_bs<true, 16, true>(sd, cost0, lds, s);
+        else if (!in_lds && bs <= 16) launch_coniss_bs<true, 16, true>(sd, cost0, lds, s);
+        else if (!in_lds) fail(TP_ERR_UNSUPPORTED, "stamped CONISS: at most 65 536 bins");
         else if (bs == 1) launch_coniss_bs<true, 1, false>(sd, cost0, lds, s);
         else if (bs == 2) launch_coniss_bs<true, 2, false>(sd, cost0, lds, s);
         else launch_coniss_bs<true, 3, false>(sd, cost0, lds, s);
@@ -1169,7 +1328,8 @@ static void run_coniss(const SweepDev &sd_in, hipStream_t s, bool stamped, Ctx *
         else if (lu && bs <= 8) launch_coniss_bs<false, 8, true, true>(sd, cost0, lds, s);
         else if (lu) launch_coniss_bs<false, 11, true, true>(sd, cost0, lds, s);
         else if (!in_lds && bs <= 11) launch_coniss_bs<false, 11, true>(sd, cost0, lds, s);
-        else if (!in_lds) launch_coniss_bs<false, 16, true>(sd, cost0, lds, s);
+        else if (!in_lds && bs <= 16) launch_coniss_bs<false, 16, true>(sd, cost0, lds, s);
+        else if (!in_lds) launch_coniss_bs<false, 32, true>(sd, cost0, lds, s);   // > 65 536 bins
         else if (bs == 1) launch_coniss_bs<false, 1, false>(sd, cost0, lds, s);
         else if (bs == 2) launch_coniss_bs<false, 2, false>(sd, cost0, lds, s);
         else launch_coniss_bs<false, 3, false>(sd, cost0, lds, s);
@@ -1179,11 +1339,12 @@ static void run_coniss(const SweepDev &sd_in, hipStream_t s, bool stamped, Ctx *
 }
 
 void launch_sweep(const SweepDev &sd, hipStream_t s, Ctx *prof) {
-    if (sd.k > 64 * KMAXSLOT)
-        fail(TP_ERR_UNSUPPORTED, "min(max_pcs, n_good) > 256: this build's sweep kernels hold at most 256 PC columns "
+    if (sd.k > 64 * KS_MAX)
+        fail(TP_ERR_UNSUPPORTED, "min(max_pcs, n_good) > 512: this build's sweep kernels hold at most 512 PC columns "
                                  "per lane group (R accepts any max_pcs, R/TADpole.R:344,452)");
+    const int ks = ks_for(sd.k);
     if (sd.n < 3) fail(TP_ERR_NO_BSTICK, "fewer than 3 good bins: no broken-stick level");
-    if (sd.n > kConissMaxN) fail(TP_ERR_UNSUPPORTED, "more than 65536 bins per matrix");
+    if (sd.n > kConissMaxN) fail(TP_ERR_UNSUPPORTED, "more than 131072 bins per matrix");
     if (sd.ntrees < 1 || sd.tree0 < 0 || sd.tree0 + sd.ntrees > sd.k) fail(TP_ERR_ARG, "bad tree range");
     size_t cnt = (size_t)sd.ntrees * sd.w_cap;
     double na;
@@ -1194,7 +1355,8 @@ void launch_sweep(const SweepDev &sd, hipStream_t s, Ctx *prof) {
     hipLaunchKernelGGL(k_fill, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, sd.scores, cnt, na);
     TP_HIP(hipGetLastError());
     hipStream_t ts = prof ? side_fork(*prof) : s;
-    hipLaunchKernelGGL(k_trS, dim3(1), dim3(256), 0, ts, sd.Pt, sd.n, sd.ldp, sd.k, sd.trS);
+    if (ks == 4) hipLaunchKernelGGL(k_trS<4>, dim3(1), dim3(256), 0, ts, sd.Pt, sd.n, sd.ldp, sd.k, sd.trS);
+    else hipLaunchKernelGGL(k_trS<8>, dim3(1), dim3(512), 0, ts, sd.Pt, sd.n, sd.ldp, sd.k, sd.trS);
     TP_HIP(hipGetLastError());
     run_coniss(sd, s, false, prof);
     if (prof) side_join(*prof);
@@ -1207,12 +1369,15 @@ void launch_sweep(const SweepDev &sd, hipStream_t s, Ctx *prof) {
         TP_HIP(hipGetLastError());
         trace_mark(s, "ch_cut");
         const int g = std::max(1, std::min(256, (sd.ucap + 3) / 4));
-        hipLaunchKernelGGL(k_ch_segstat, dim3(g), dim3(256), 0, s, sd);
+        if (ks == 4) hipLaunchKernelGGL(k_ch_segstat<4>, dim3(g), dim3(256), 0, s, sd);
+        else hipLaunchKernelGGL(k_ch_segstat<8>, dim3(g), dim3(256), 0, s, sd);
         TP_HIP(hipGetLastError());
         trace_mark(s, "ch_segstat");
-        hipLaunchKernelGGL(k_ch, dim3(sd.ntrees), dim3(256), 0, s, sd);
+        if (ks == 4) hipLaunchKernelGGL(k_ch<4>, dim3(sd.ntrees), dim3(256), 0, s, sd);
+        else hipLaunchKernelGGL(k_ch<8>, dim3(sd.ntrees), dim3(256), 0, s, sd);
     } else {
-        hipLaunchKernelGGL(k_ch, dim3(sd.ntrees), dim3(CH_THREADS), 0, s, sd);
+        if (ks == 4) hipLaunchKernelGGL(k_ch<4>, dim3(sd.ntrees), dim3(CH_THREADS), 0, s, sd);
+        else hipLaunchKernelGGL(k_ch<8>, dim3(sd.ntrees), dim3(CH_THREADS), 0, s, sd);
     }
     TP_HIP(hipGetLastError());
     trace_mark(s, "ch");
@@ -1222,19 +1387,20 @@ void launch_sweep(const SweepDev &sd, hipStream_t s, Ctx *prof) {
 void launch_coniss_stamped(const SweepDev &sd, hipStream_t s) { run_coniss(sd, s, true, nullptr); }
 
 void launch_coniss_only(const SweepDev &sd, hipStream_t s) {
-    if (sd.tree0 + sd.ntrees > 64 * KMAXSLOT) fail(TP_ERR_UNSUPPORTED, "more than 256 columns");
-    if (sd.n > kConissMaxN) fail(TP_ERR_UNSUPPORTED, "more than 65536 bins per matrix");
+    if (sd.tree0 + sd.ntrees > 64 * KS_MAX) fail(TP_ERR_UNSUPPORTED, "more than 512 columns");
+    if (sd.n > kConissMaxN) fail(TP_ERR_UNSUPPORTED, "more than 131072 bins per matrix");
     run_coniss(sd, s, false, nullptr);
 }
 
 // ------------------------------------------- single calinhara (tp_ch entry)
+template <int KS>
 __global__ void __launch_bounds__(256) k_ch_single(const double *Pt, int n, int ldp, int k, const int *bnd, int cn,
                                                    double *ssg, double *trS_out, double *out) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     for (int g = w; g < cn + 1; g += 4) {
         // g == cn: the whole matrix (tr S)
         int s0 = g == cn ? 0 : bnd[g], e0 = g == cn ? n - 1 : bnd[g + 1] - 1;
-        double ss = seg_ss_wave(Pt, ldp, k, s0, e0, nullptr, lane);
+        double ss = seg_ss_wave<KS>(Pt, ldp, k, s0, e0, nullptr, lane);
         if (lane == 0) ssg[g] = ss;
     }
     __syncthreads();
@@ -1249,8 +1415,13 @@ __global__ void __launch_bounds__(256) k_ch_single(const double *Pt, int n, int 
 
 void launch_ch_only(const double *d_Pt, int n, int ldp, int k, const int *d_bnd, int cn, double *d_seg,
                     double *d_out, hipStream_t s) {
-    hipLaunchKernelGGL(k_ch_single, dim3(1), dim3(256), 0, s, d_Pt, n, ldp, k, d_bnd, cn, d_seg, d_seg + cn + 1,
-                       d_out);
+    if (k > 64 * KS_MAX) fail(TP_ERR_UNSUPPORTED, "calinhara: more than 512 columns");
+    if (k <= 256)
+        hipLaunchKernelGGL(k_ch_single<4>, dim3(1), dim3(256), 0, s, d_Pt, n, ldp, k, d_bnd, cn, d_seg,
+                           d_seg + cn + 1, d_out);
+    else
+        hipLaunchKernelGGL(k_ch_single<8>, dim3(1), dim3(256), 0, s, d_Pt, n, ldp, k, d_bnd, cn, d_seg,
+                           d_seg + cn + 1, d_out);
     TP_HIP(hipGetLastError());
 }
 

@@ -1,0 +1,387 @@
+// Microbenchmark of the Krylov product C = A'B (A k-contiguous, M = n + 2,
+// N = 64, K = n; the C3 shape by default): the library's k_gemm_ts tile
+// (128 x 64, 4 waves of 32 x 64, BK 16) against variants.  Partials only (the
+// split-K reduction is timed separately in the library).  Build:
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off tools/gemm_ts_bench.hip -o tools/gemm_ts_bench
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+#define CK(x)                                                                                  \
+    do {                                                                                       \
+        hipError_t e_ = (x);                                                                   \
+        if (e_ != hipSuccess) {                                                                \
+            fprintf(stderr, "HIP %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); \
+            exit(1);                                                                           \
+        }                                                                                      \
+    } while (0)
+
+constexpr int TSM = 128, TSN = 64;
+
+__device__ __forceinline__ int xcd_order(int total) {
+    const int xcd = (int)blockIdx.x & 7, slot = (int)blockIdx.x >> 3;
+    return xcd * (total >> 3) + min(xcd, total & 7) + slot;
+}
+
+// ---- V0: the library kernel (k_gemm_ts)
+template <int TSK>
+__global__ void __launch_bounds__(256, 2) k_v0(int M, int N, int K, const double *__restrict__ A, int lda,
+                                               const double *__restrict__ B, int ldb, double *__restrict__ C, int ldc,
+                                               int kchunk, size_t part_stride) {
+    constexpr int TSLD = TSK + 2;
+    __shared__ double As[2][TSM][TSLD];
+    __shared__ double Bs[2][TSN][TSLD];
+    const int tm = (M + TSM - 1) / TSM, tn = (N + TSN - 1) / TSN;
+    const int Lg = xcd_order((int)gridDim.x);
+    const int bn = Lg % tn, bm = (Lg / tn) % tm, z = Lg / (tn * tm);
+    const int i0 = bm * TSM, j0 = bn * TSN;
+    const int kbeg = z * kchunk, kend = min(K, kbeg + kchunk);
+    C += part_stride * z;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int wm = 32 * w;
+    const int fr = lane & 15, fk = lane >> 4;
+    d4 acc[2][4];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = (d4){0.0, 0.0, 0.0, 0.0};
+    constexpr int PA = TSM * TSK / 256, PB = TSN * TSK / 256;
+    double ra[PA], rb[PB];
+    const int lk = t % TSK, lr = t / TSK;
+    constexpr int RS = 256 / TSK;
+    auto load = [&](int k0) {
+        const int k = k0 + lk;
+        const bool kin = k < kend;
+#pragma unroll
+        for (int p = 0; p < PA; ++p) {
+            const int i = i0 + lr + RS * p;
+            ra[p] = (kin && i < M) ? A[(size_t)k + (size_t)i * lda] : 0.0;
+        }
+#pragma unroll
+        for (int p = 0; p < PB; ++p) {
+            const int j = j0 + lr + RS * p;
+            rb[p] = (kin && j < N) ? B[(size_t)k + (size_t)j * ldb] : 0.0;
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int p = 0; p < PA; ++p) As[buf][lr + RS * p][lk] = ra[p];
+#pragma unroll
+        for (int p = 0; p < PB; ++p) Bs[buf][lr + RS * p][lk] = rb[p];
+    };
+    if (kbeg < kend) {
+        load(kbeg);
+        store(0);
+    }
+    __syncthreads();
+    int buf = 0;
+    for (int k0 = kbeg; k0 < kend; k0 += TSK) {
+        const bool more = k0 + TSK < kend;
+        if (more) load(k0 + TSK);
+#pragma unroll
+        for (int kk = 0; kk < TSK; kk += 4) {
+            double af[2], bf[4];
+#pragma unroll
+            for (int a = 0; a < 2; ++a) af[a] = As[buf][wm + 16 * a + fr][kk + fk];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) bf[b] = Bs[buf][16 * b + fr][kk + fk];
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[a], bf[b], acc[a][b], 0, 0, 0);
+        }
+        if (more) store(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = i0 + wm + 16 * a + fk + 4 * r;
+                const int j = j0 + 16 * b + fr;
+                if (i < M && j < N) C[(size_t)i + (size_t)j * ldc] = acc[a][b][r];
+            }
+}
+
+// ---- V1: k sliced over the waves: every wave owns the whole 128 x 64 tile
+// (8 x 4 accumulators) for one 4-deep MFMA step of each BK-deep stage (wave w:
+// k = k0 + 4 w' .. for w' = w, w + 4, ...); 12 fragment reads per 32 MFMAs.
+// The four waves' partials are summed in wave order at the end through LDS.
+template <int TSK>
+__global__ void __launch_bounds__(256, 2) k_v1(int M, int N, int K, const double *__restrict__ A, int lda,
+                                               const double *__restrict__ B, int ldb, double *__restrict__ C, int ldc,
+                                               int kchunk, size_t part_stride) {
+    constexpr int TSLD = TSK + 2;
+    __shared__ double As[2][TSM][TSLD];
+    __shared__ double Bs[2][TSN][TSLD];
+    const int tm = (M + TSM - 1) / TSM, tn = (N + TSN - 1) / TSN;
+    const int Lg = xcd_order((int)gridDim.x);
+    const int bn = Lg % tn, bm = (Lg / tn) % tm, z = Lg / (tn * tm);
+    const int i0 = bm * TSM, j0 = bn * TSN;
+    const int kbeg = z * kchunk, kend = min(K, kbeg + kchunk);
+    C += part_stride * z;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int fr = lane & 15, fk = lane >> 4;
+    d4 acc[8][4];
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = (d4){0.0, 0.0, 0.0, 0.0};
+    constexpr int PA = TSM * TSK / 256, PB = TSN * TSK / 256;
+    double ra[PA], rb[PB];
+    const int lk = t % TSK, lr = t / TSK;
+    constexpr int RS = 256 / TSK;
+    auto load = [&](int k0) {
+        const int k = k0 + lk;
+        const bool kin = k < kend;
+#pragma unroll
+        for (int p = 0; p < PA; ++p) {
+            const int i = i0 + lr + RS * p;
+            ra[p] = (kin && i < M) ? A[(size_t)k + (size_t)i * lda] : 0.0;
+        }
+#pragma unroll
+        for (int p = 0; p < PB; ++p) {
+            const int j = j0 + lr + RS * p;
+            rb[p] = (kin && j < N) ? B[(size_t)k + (size_t)j * ldb] : 0.0;
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int p = 0; p < PA; ++p) As[buf][lr + RS * p][lk] = ra[p];
+#pragma unroll
+        for (int p = 0; p < PB; ++p) Bs[buf][lr + RS * p][lk] = rb[p];
+    };
+    if (kbeg < kend) {
+        load(kbeg);
+        store(0);
+    }
+    __syncthreads();
+    int buf = 0;
+    for (int k0 = kbeg; k0 < kend; k0 += TSK) {
+        const bool more = k0 + TSK < kend;
+        if (more) load(k0 + TSK);
+#pragma unroll
+        for (int ks = 0; ks < TSK / 16; ++ks) {
+            const int kk = 16 * ks + 4 * w + fk;
+            double bf[4];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) bf[b] = Bs[buf][16 * b + fr][kk];
+#pragma unroll
+            for (int a = 0; a < 8; ++a) {
+                const double af = As[buf][16 * a + fr][kk];
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(af, bf[b], acc[a][b], 0, 0, 0);
+            }
+        }
+        if (more) store(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+    // wave-order sum of the four partial tiles, 4 accumulator rows a pass
+    double *red = &As[0][0][0];   // 4 waves x 4 x 4 tiles x 256 doubles = 128 KiB?  no: pass of one a-row
+#pragma unroll
+    for (int a = 0; a < 8; ++a) {
+        // red[w][b][r][lane] : 4 x 4 x 4 x 64 doubles = 32 KiB
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) red[((w * 4 + b) * 4 + r) * 64 + lane] = acc[a][b][r];
+        __syncthreads();
+        // wave w sums accumulator column b = w of this a-row
+        {
+            const int b = w;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                double v = red[((0 * 4 + b) * 4 + r) * 64 + lane];
+                v = v + red[((1 * 4 + b) * 4 + r) * 64 + lane];
+                v = v + red[((2 * 4 + b) * 4 + r) * 64 + lane];
+                v = v + red[((3 * 4 + b) * 4 + r) * 64 + lane];
+                const int i = i0 + 16 * a + fk + 4 * r;
+                const int j = j0 + 16 * b + fr;
+                if (i < M && j < N) C[(size_t)i + (size_t)j * ldc] = v;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+
+// ---- V2: 4 waves as 2 (M halves of 64 rows) x 2 (k slices): wave w owns rows
+// 64 (w & 1) .. + 63 of the tile with 4 x 4 accumulators for the MFMA k-steps
+// 2 (w >> 1), 2 (w >> 1) + 1 of each 16-deep stage: 16 fragment reads per 32
+// MFMAs; the two k-slice partials are summed (slice 0 first) through LDS.
+template <int TSK>
+__global__ void __launch_bounds__(256, 2) k_v2(int M, int N, int K, const double *__restrict__ A, int lda,
+                                               const double *__restrict__ B, int ldb, double *__restrict__ C, int ldc,
+                                               int kchunk, size_t part_stride) {
+    constexpr int TSLD = TSK + 2;
+    __shared__ double As[2][TSM][TSLD];
+    __shared__ double Bs[2][TSN][TSLD];
+    const int tm = (M + TSM - 1) / TSM, tn = (N + TSN - 1) / TSN;
+    const int Lg = xcd_order((int)gridDim.x);
+    const int bn = Lg % tn, bm = (Lg / tn) % tm, z = Lg / (tn * tm);
+    const int i0 = bm * TSM, j0 = bn * TSN;
+    const int kbeg = z * kchunk, kend = min(K, kbeg + kchunk);
+    C += part_stride * z;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int wm = 64 * (w & 1), ksl = w >> 1;
+    const int fr = lane & 15, fk = lane >> 4;
+    d4 acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = (d4){0.0, 0.0, 0.0, 0.0};
+    constexpr int PA = TSM * TSK / 256, PB = TSN * TSK / 256;
+    double ra[PA], rb[PB];
+    const int lk = t % TSK, lr = t / TSK;
+    constexpr int RS = 256 / TSK;
+    auto load = [&](int k0) {
+        const int k = k0 + lk;
+        const bool kin = k < kend;
+#pragma unroll
+        for (int p = 0; p < PA; ++p) {
+            const int i = i0 + lr + RS * p;
+            ra[p] = (kin && i < M) ? A[(size_t)k + (size_t)i * lda] : 0.0;
+        }
+#pragma unroll
+        for (int p = 0; p < PB; ++p) {
+            const int j = j0 + lr + RS * p;
+            rb[p] = (kin && j < N) ? B[(size_t)k + (size_t)j * ldb] : 0.0;
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int p = 0; p < PA; ++p) As[buf][lr + RS * p][lk] = ra[p];
+#pragma unroll
+        for (int p = 0; p < PB; ++p) Bs[buf][lr + RS * p][lk] = rb[p];
+    };
+    if (kbeg < kend) {
+        load(kbeg);
+        store(0);
+    }
+    __syncthreads();
+    int buf = 0;
+    for (int k0 = kbeg; k0 < kend; k0 += TSK) {
+        const bool more = k0 + TSK < kend;
+        if (more) load(k0 + TSK);
+#pragma unroll
+        for (int ks = 0; ks < TSK / 8; ++ks) {
+            const int kk = 8 * ks + 4 * ksl + fk;
+            double af[4], bf[4];
+#pragma unroll
+            for (int a = 0; a < 4; ++a) af[a] = As[buf][wm + 16 * a + fr][kk];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) bf[b] = Bs[buf][16 * b + fr][kk];
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[a], bf[b], acc[a][b], 0, 0, 0);
+        }
+        if (more) store(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+    // slice 1 hands its partials to slice 0 through LDS (4 x 4 x 4 x 64 doubles per M half)
+    double *red = &As[0][0][0];
+    if (ksl == 1) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) red[(((w & 1) * 16 + a * 4 + b) * 4 + r) * 64 + lane] = acc[a][b][r];
+    }
+    __syncthreads();
+    if (ksl == 0) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const double v = acc[a][b][r] + red[(((w & 1) * 16 + a * 4 + b) * 4 + r) * 64 + lane];
+                    const int i = i0 + wm + 16 * a + fk + 4 * r;
+                    const int j = j0 + 16 * b + fr;
+                    if (i < M && j < N) C[(size_t)i + (size_t)j * ldc] = v;
+                }
+    }
+}
+
+__global__ void k_rand(double *p, size_t n, unsigned long long seed) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    unsigned long long z = seed + 0x9E3779B97F4A7C15ULL * (i + 1);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    z = z ^ (z >> 31);
+    p[i] = ((double)(z >> 11) * (1.0 / 9007199254740992.0)) * 2.0 - 1.0;
+}
+
+int main(int argc, char **argv) {
+    const int n = argc > 1 ? atoi(argv[1]) : 7729;
+    const int N = 64, M = n + 2, K = n;
+    const int S = std::min(8, K / 256);
+    int kchunk = ((K + S - 1) / S + 15) / 16 * 16;
+    const int SS = (K + kchunk - 1) / kchunk;
+    const int reps = 20;
+    double *A, *B, *P0, *P1;
+    CK(hipMalloc(&A, (size_t)M * K * 8));
+    CK(hipMalloc(&B, (size_t)K * N * 8));
+    const size_t pst = (size_t)M * N;
+    CK(hipMalloc(&P0, pst * SS * 8));
+    CK(hipMalloc(&P1, pst * SS * 8));
+    hipLaunchKernelGGL(k_rand, dim3((unsigned)(((size_t)M * K + 255) / 256)), dim3(256), 0, 0, A, (size_t)M * K, 1ULL);
+    hipLaunchKernelGGL(k_rand, dim3((unsigned)(((size_t)K * N + 255) / 256)), dim3(256), 0, 0, B, (size_t)K * N, 2ULL);
+    CK(hipDeviceSynchronize());
+    const int tiles = (M + TSM - 1) / TSM;
+    const dim3 grid((unsigned)(tiles * SS));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const double flops = 2.0 * M * N * (double)K;
+    auto run = [&](const char *name, auto kern, double *out) {
+        for (int r = 0; r < 3; ++r) hipLaunchKernelGGL(kern, grid, dim3(256), 0, 0, M, N, K, A, n, B, n, out, M, kchunk, pst);
+        CK(hipEventRecord(e0));
+        for (int r = 0; r < reps; ++r)
+            hipLaunchKernelGGL(kern, grid, dim3(256), 0, 0, M, N, K, A, n, B, n, out, M, kchunk, pst);
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        const double us = ms * 1e3 / reps;
+        printf("%-28s %8.1f us  %6.2f TF/s\n", name, us, flops / (us * 1e-6) / 1e12);
+    };
+    auto cmp = [&](const char *name) {
+        std::vector<double> h0(pst * SS), h1(pst * SS);
+        CK(hipMemcpy(h0.data(), P0, pst * SS * 8, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(h1.data(), P1, pst * SS * 8, hipMemcpyDeviceToHost));
+        double md = 0, mx = 0;
+        for (size_t q = 0; q < h0.size(); ++q) {
+            md = std::max(md, std::fabs(h0[q] - h1[q]));
+            mx = std::max(mx, std::fabs(h0[q]));
+        }
+        printf("   %s vs v0: max |diff| %.3e (max |v| %.3e)\n", name, md, mx);
+    };
+    printf("M=%d N=%d K=%d split=%d kchunk=%d grid=%u\n", M, N, K, SS, kchunk, grid.x);
+    run("v0 k_gemm_ts BK16", k_v0<16>, P0);
+    run("v0 BK32", k_v0<32>, P1);
+    cmp("v0 BK32");
+    run("v1 kslice BK16", k_v1<16>, P1);
+    cmp("v1 BK16");
+    run("v1 kslice BK32", k_v1<32>, P1);
+    cmp("v1 BK32");
+    run("v2 2x2 (M halves, k slices) BK16", k_v2<16>, P1);
+    cmp("v2 BK16");
+    run("v0 k_gemm_ts BK16 (again)", k_v0<16>, P0);
+    return 0;
+}
