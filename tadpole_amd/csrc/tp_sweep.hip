@@ -85,19 +85,56 @@ __device__ __forceinline__ double nan2inf(double x) { return isnan(x) ? __longlo
 // Synchronisation: the workgroup is one wave.  Every lane writes the same value
 // to each shared LDS word it updates, so no barrier is needed in the loop.
 
-// four wave minima interleaved (independent DPP chains), broadcast (lane 63)
+// four wave minima interleaved, broadcast (lane 63).  The operands are merge
+// costs: non-negative doubles, +inf, or the quiet NaN of a non-candidate, whose
+// 64-bit patterns order exactly like the values with that NaN largest -- the
+// order v_min_f64 gives (NaN ignored unless every lane holds it).  So the
+// minimum is taken on the bit patterns, high words first and then the low words
+// of the lanes that hold the smallest high word: one DPP-fused v_min_u32 per
+// step (a 64-bit step is two DPP moves and a v_min_f64).  Same result bits.
+template <int CTRL> __device__ __forceinline__ unsigned dpp_u(unsigned v) {
+    return (unsigned)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
+}
+__device__ __forceinline__ unsigned umin_(unsigned a, unsigned b) { return a < b ? a : b; }
 __device__ __forceinline__ void wave_min4(double &a, double &b, double &c, double &d) {
-#define TP_MIN4(ctl)                    \
-    a = vmin(a, dpp_d<ctl>(a));         \
-    b = vmin(b, dpp_d<ctl>(b));         \
-    c = vmin(c, dpp_d<ctl>(c));         \
-    d = vmin(d, dpp_d<ctl>(d));
-    TP_MIN4(0xB1) TP_MIN4(0x4E) TP_MIN4(0x141) TP_MIN4(0x140) TP_MIN4(0x142) TP_MIN4(0x143)
-#undef TP_MIN4
-    a = readlane_d(a, 63);
-    b = readlane_d(b, 63);
-    c = readlane_d(c, 63);
-    d = readlane_d(d, 63);
+    unsigned h[4], l[4];
+    {
+        const unsigned long long ua = (unsigned long long)__double_as_longlong(a),
+                                 ub = (unsigned long long)__double_as_longlong(b),
+                                 uc = (unsigned long long)__double_as_longlong(c),
+                                 ud = (unsigned long long)__double_as_longlong(d);
+        h[0] = (unsigned)(ua >> 32); l[0] = (unsigned)ua;
+        h[1] = (unsigned)(ub >> 32); l[1] = (unsigned)ub;
+        h[2] = (unsigned)(uc >> 32); l[2] = (unsigned)uc;
+        h[3] = (unsigned)(ud >> 32); l[3] = (unsigned)ud;
+    }
+    unsigned m[4] = {h[0], h[1], h[2], h[3]};
+#define TP_UMIN4(x, ctl)                                                             \
+    x[0] = umin_(x[0], dpp_u<ctl>(x[0]));                                            \
+    x[1] = umin_(x[1], dpp_u<ctl>(x[1]));                                            \
+    x[2] = umin_(x[2], dpp_u<ctl>(x[2]));                                            \
+    x[3] = umin_(x[3], dpp_u<ctl>(x[3]));
+    TP_UMIN4(m, 0xB1) TP_UMIN4(m, 0x4E) TP_UMIN4(m, 0x141) TP_UMIN4(m, 0x140) TP_UMIN4(m, 0x142)
+    TP_UMIN4(m, 0x143)
+    unsigned hm[4], lm[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        hm[q] = (unsigned)__builtin_amdgcn_readlane((int)m[q], 63);
+        lm[q] = h[q] == hm[q] ? l[q] : 0xFFFFFFFFu;
+    }
+    TP_UMIN4(lm, 0xB1) TP_UMIN4(lm, 0x4E) TP_UMIN4(lm, 0x141) TP_UMIN4(lm, 0x140) TP_UMIN4(lm, 0x142)
+    TP_UMIN4(lm, 0x143)
+#undef TP_UMIN4
+    double r[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)lm[q], 63);
+        r[q] = __longlong_as_double((long long)(((unsigned long long)hm[q] << 32) | lo));
+    }
+    a = r[0];
+    b = r[1];
+    c = r[2];
+    d = r[3];
 }
 
 // two wave minima interleaved, broadcast (lane 63)

@@ -317,6 +317,93 @@ __global__ void __launch_bounds__(256, 2) k_v2(int M, int N, int K, const double
     }
 }
 
+
+// ---- V3: v0 with 16-byte global loads (two consecutive k of a row per lane:
+// 8 lanes cover a row's 128 B, a wave 8 rows) and 16-byte LDS stores
+template <int TSK>
+__global__ void __launch_bounds__(256, 2) k_v3(int M, int N, int K, const double *__restrict__ A, int lda,
+                                               const double *__restrict__ B, int ldb, double *__restrict__ C, int ldc,
+                                               int kchunk, size_t part_stride) {
+    constexpr int TSLD = TSK + 2;
+    __shared__ double As[2][TSM][TSLD];
+    __shared__ double Bs[2][TSN][TSLD];
+    const int tm = (M + TSM - 1) / TSM, tn = (N + TSN - 1) / TSN;
+    const int Lg = xcd_order((int)gridDim.x);
+    const int bn = Lg % tn, bm = (Lg / tn) % tm, z = Lg / (tn * tm);
+    const int i0 = bm * TSM, j0 = bn * TSN;
+    const int kbeg = z * kchunk, kend = min(K, kbeg + kchunk);
+    C += part_stride * z;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int wm = 32 * w;
+    const int fr = lane & 15, fk = lane >> 4;
+    d4 acc[2][4];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = (d4){0.0, 0.0, 0.0, 0.0};
+    constexpr int KP = TSK / 2;                 // k pairs per row
+    constexpr int RS = 256 / KP;                // rows per pass
+    constexpr int PA = TSM / RS, PB = TSN / RS;
+    double2 ra[PA], rb[PB];
+    const int lk = t % KP, lr = t / KP;
+    auto load = [&](int k0) {
+        const int k = k0 + 2 * lk;
+        const bool kin = k < kend;   // kend even (K chunks are multiples of 16; K even checked by the host)
+#pragma unroll
+        for (int p = 0; p < PA; ++p) {
+            const int i = i0 + lr + RS * p;
+            ra[p] = (kin && i < M) ? *(const double2 *)(A + (size_t)k + (size_t)i * lda) : make_double2(0.0, 0.0);
+        }
+#pragma unroll
+        for (int p = 0; p < PB; ++p) {
+            const int j = j0 + lr + RS * p;
+            rb[p] = (kin && j < N) ? *(const double2 *)(B + (size_t)k + (size_t)j * ldb) : make_double2(0.0, 0.0);
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int p = 0; p < PA; ++p) *(double2 *)&As[buf][lr + RS * p][2 * lk] = ra[p];
+#pragma unroll
+        for (int p = 0; p < PB; ++p) *(double2 *)&Bs[buf][lr + RS * p][2 * lk] = rb[p];
+    };
+    if (kbeg < kend) {
+        load(kbeg);
+        store(0);
+    }
+    __syncthreads();
+    int buf = 0;
+    for (int k0 = kbeg; k0 < kend; k0 += TSK) {
+        const bool more = k0 + TSK < kend;
+        if (more) load(k0 + TSK);
+#pragma unroll
+        for (int kk = 0; kk < TSK; kk += 4) {
+            double af[2], bf[4];
+#pragma unroll
+            for (int a = 0; a < 2; ++a) af[a] = As[buf][wm + 16 * a + fr][kk + fk];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) bf[b] = Bs[buf][16 * b + fr][kk + fk];
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[a], bf[b], acc[a][b], 0, 0, 0);
+        }
+        if (more) store(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = i0 + wm + 16 * a + fk + 4 * r;
+                const int j = j0 + 16 * b + fr;
+                if (i < M && j < N) C[(size_t)i + (size_t)j * ldc] = acc[a][b][r];
+            }
+}
+
 __global__ void k_rand(double *p, size_t n, unsigned long long seed) {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -376,12 +463,10 @@ int main(int argc, char **argv) {
     run("v0 k_gemm_ts BK16", k_v0<16>, P0);
     run("v0 BK32", k_v0<32>, P1);
     cmp("v0 BK32");
-    run("v1 kslice BK16", k_v1<16>, P1);
-    cmp("v1 BK16");
-    run("v1 kslice BK32", k_v1<32>, P1);
-    cmp("v1 BK32");
-    run("v2 2x2 (M halves, k slices) BK16", k_v2<16>, P1);
-    cmp("v2 BK16");
+    run("v3 16-B loads BK16", k_v3<16>, P1);
+    cmp("v3 BK16");
+    run("v3 16-B loads BK32", k_v3<32>, P1);
+    cmp("v3 BK32");
     run("v0 k_gemm_ts BK16 (again)", k_v0<16>, P0);
     return 0;
 }
