@@ -581,20 +581,29 @@ static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_cl
     if (n < 3) fail(TP_ERR_NO_BSTICK, "fewer than 3 good bins after masking");
     double *X = c.buf[S_X].as<double>((size_t)n * n);
     double *m = c.buf[S_COLMEAN].as<double>(n);
-    launch_gather_colmean(d_M, n0, d_good, n, X, m, s);
+    // the gather also scans X for the exact int8 X'X (integrality, maximum,
+    // S_jj) and builds its 2-slice image: no separate passes over X for them
+    const bool prep = g_xtx_fused && g_xtx_int8 && n >= 1024 && n <= 130000;
+    GatherStats gs{};
+    if (prep) {
+        const int Kp = xtx_kp(n), Np = (n + 127) / 128 * 128;
+        char *gb = c.buf[S_GSTAT].as<char>((size_t)n * 24 + 256);
+        double *cmax = (double *)gb;
+        long long *css = (long long *)(cmax + n);
+        int *cbad = (int *)(css + n);
+        int8_t *sl = xtx_slice_buf(c, n, 2);
+        launch_gather_prep(d_M, n0, d_good, n, X, m, cmax, cbad, css, sl, Kp, Np, s);
+        gs = GatherStats{cmax, cbad, css, true};
+    } else {
+        launch_gather_colmean(d_M, n0, d_good, n, X, m, s);
+    }
     trace_mark(s, "mask");
     tm.mark();
     // ---- sparse_cor (R/TADpole.R:94-100,448-449)
-    double *S = c.buf[S_S].as<double>((size_t)n * n);
     double *C = c.buf[S_C].as<double>(pca_c_doubles(n));
-    {
-        kprof_begin(c, K_COR_GEMM);
-        trace_mark(s, "cor: start");
-        xtx_product(c, X, n, S);
-        kprof_end(c, K_COR_GEMM);
-    }
     double *cmean = g_cor_fused ? C + (size_t)n * n : nullptr;   // C's column means, for prcomp (C's tail)
-    launch_cor_epilogue(S, m, n, C, c.buf[S_DIAG].as<double>(n), s, cmean);
+    trace_mark(s, "cor: start");
+    cor_product(c, X, n, m, prep ? &gs : nullptr, nullptr, C, c.buf[S_DIAG].as<double>(n), cmean);
     trace_mark(s, "cor");
     tm.mark();
     // ---- prcomp (R/TADpole.R:452-453)
@@ -1378,7 +1387,8 @@ extern "C" {
  * segment statistics shared across trees, 1 cap on their store (0 = automatic),
  * 2 short-K panel GEMM, 3 GEMM LDS stage depth (16 / 32), 4 register-resident
  * tridiagonalisation, 5 int8 X'X, 6 PCA degree margin, 7 XCD-aware GEMM order, ..., 14 supertile
- * order of the int8 X'X tiles, ..., 17 C's column means formed by the correlation epilogue. */
+ * order of the int8 X'X tiles, ..., 17 C's column means formed by the correlation epilogue, 18 the
+ * correlation epilogue in the int8 X'X store (with the gather's statistics). */
 void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
     guarded(status, [&] {
         int *p = nullptr;
@@ -1401,6 +1411,7 @@ void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
         case 15: p = &g_pca_over; break;
         case 16: p = &g_coniss_lu; break;
         case 17: p = &g_cor_fused; break;
+        case 18: p = &g_xtx_fused; break;
         default: fail(TP_ERR_ARG, "unknown knob");
         }
         if (*which == 3 && *value != 16 && *value != 32) fail(TP_ERR_ARG, "stage depth must be 16 or 32");

@@ -99,7 +99,7 @@ enum Slot {
     S_M = 0, S_ROWMEAN, S_DIAG, S_BAD, S_GOOD, S_NGOOD, S_X, S_COLMEAN,
     S_S, S_C, S_XC, S_XCT, S_G, S_Q, S_Z, S_W, S_SMALL, S_P, S_PT,
     S_SWEEP, S_SWEEP2, S_SCORES, S_PARTIAL, S_MISC, S_SHARD, S_SHARD2, S_DEDUP,
-    S_KRY, S_KRYG, S_KRYT, S_KRYV, S_KRYX, S_CMEAN, S_CHBIG, S_CHOLP, S_NSLOT
+    S_KRY, S_KRYG, S_KRYT, S_KRYV, S_KRYX, S_CMEAN, S_CHBIG, S_CHOLP, S_SMALL2, S_GSTAT, S_NSLOT
 };
 static_assert(S_NSLOT <= (int)(sizeof(Ctx::buf) / sizeof(Ctx::buf[0])), "Ctx::buf too small for the slots");
 
@@ -114,6 +114,11 @@ void launch_mask_select(const double *d_rowmean, const double *d_diag, int n0,
 void launch_gather_colmean(const double *d_M, int n0, const int *d_good, int n,
                            double *d_X, double *d_colmean, hipStream_t s);
 void launch_colmean(const double *d_A, int n, int ld, double *d_mean, hipStream_t s);
+// the gather with what the int8 X'X needs (per-column max / non-integer flag /
+// exact sum of squares, speculative 2-slice int8 image), tp_prep.hip
+void launch_gather_prep(const double *d_M, int n0, const int *d_good, int n, double *d_X, double *d_colmean,
+                        double *d_cmax, int *d_cbad, long long *d_css, int8_t *d_sl, int Kp, int Np, hipStream_t s);
+void launch_cor_sd_ss(const long long *d_css, const double *d_m, int n, double *d_sd, hipStream_t s);
 // d_cmean != nullptr: the column means of C are formed in the same pass (k_colmean's order)
 void launch_cor_epilogue(const double *d_S, const double *d_m, int n, double *d_C, double *d_sd,
                          hipStream_t s, double *d_cmean = nullptr);
@@ -287,10 +292,28 @@ void rows_gemm_sharded(Ctx &c, const double *A, int lda, int M, const double *B,
 
 // exact X'X on int8 matrix cores for integer counts (tp_xtx.hip)
 extern int g_xtx_int8;
+extern int g_xtx_fused;
 int xtx_int_slices(Ctx &c, const double *d_X, int n);   // 0 = not integer counts (fp64 path)
 const int8_t *xtx_slices(Ctx &c, const double *d_X, int n, int ns);
 void xtx_int8_tiles(Ctx &c, const int8_t *sl, int n, int ns, double *d_S, int tc0, int tc1);   // 64-col tiles
-void xtx_int8_tiles128(Ctx &c, const int8_t *sl, int n, int ns, double *d_S, int tc0, int tc1);
+// cm / csd given: the correlation epilogue in the store (d_S receives cor)
+void xtx_int8_tiles128(Ctx &c, const int8_t *sl, int n, int ns, double *d_S, int tc0, int tc1,
+                       const double *cm = nullptr, const double *csd = nullptr);
+int xtx_kp(int n);
+int8_t *xtx_slice_buf(Ctx &c, int n, int ns);
+int xtx_int_slices_cols(Ctx &c, const double *d_cmax, const int *d_cbad, int n);
+// sparse_cor in one call (R/TADpole.R:94-100,449): C = cor(X) with NaN -> 0, and
+// C's column means into d_cmean when given.  Exact int8 X'X with the epilogue in
+// the store when the gather's statistics say X holds counts < 2^14 (and its
+// slices are already built), else X'X into d_S and the separate epilogue.
+struct GatherStats {
+    const double *cmax;
+    const int *cbad;
+    const long long *css;
+    bool slices2;   // the gather wrote the 2-slice int8 image
+};
+void cor_product(Ctx &c, const double *d_X, int n, const double *d_m, const GatherStats *gs, double *d_S,
+                 double *d_C, double *d_sd, double *d_cmean);
 // S = X'X by the exact int8 path when possible, sharded like sym_gemm_sharded
 void xtx_product(Ctx &c, const double *d_X, int n, double *d_S);
 

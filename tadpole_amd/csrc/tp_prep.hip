@@ -238,6 +238,95 @@ void launch_gather_colmean(const double *d_M, int n0, const int *d_good, int n, 
     TP_HIP(hipGetLastError());
 }
 
+// The same gather and column means, plus what the exact int8 X'X needs, in
+// the same pass over X (instead of two more passes over it: the integrality
+// scan and the slicing): per column the maximum, a flag for entries that are
+// not non-negative integers, the exact sum of squares (int64: S_jj of X'X, for
+// sd), and -- speculatively, for counts below 2^14 -- the two 7-bit int8
+// slices (column j of slice s at sl + s Np Kp + j Kp, rows zero-padded to Kp;
+// grid over Np columns: the padding columns get zero slices).
+__global__ void __launch_bounds__(256) k_gather_prep(const double *M, int n0, const int *good, int n, double *X,
+                                                     double *cm, double *cmax, int *cbad, long long *css,
+                                                     int8_t *sl, int Kp, int Np) {
+    int lane = threadIdx.x & 63;
+    int j = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (j >= Np) return;
+    const size_t slice = (size_t)Np * Kp;
+    if (j >= n) {   // padding column: zero slices
+        for (int k = lane * 4; k < Kp; k += 256) {
+            *(unsigned *)(sl + (size_t)j * Kp + k) = 0u;
+            *(unsigned *)(sl + slice + (size_t)j * Kp + k) = 0u;
+        }
+        return;
+    }
+    const double *src = M + (size_t)good[j] * n0;
+    double *dst = X + (size_t)j * n;
+    int8_t *s0 = sl + (size_t)j * Kp, *s1 = s0 + slice;
+    double hi = 0.0, lo = 0.0, mx = 0.0;
+    long long ss = 0;
+    bool bad = false;
+    auto take = [&](int a, double v) {
+        dst[a] = v;
+        dd_add_d(hi, lo, v);
+        const bool ok = v >= 0.0 && v == floor(v) && v < 2147483648.0;
+        bad |= !ok;
+        mx = fmax(mx, v);
+        const long long iv = ok ? (long long)v : 0;
+        ss += iv * iv;
+        s0[a] = (int8_t)(iv & 127);
+        s1[a] = (int8_t)((iv >> 7) & 127);
+    };
+    constexpr int U = 8;   // gathers in flight per lane (same accumulation order as k_gather_colmean)
+    int a = lane;
+    for (; a + 64 * (U - 1) < n; a += 64 * U) {
+        int gi[U];
+        double v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) gi[u] = good[a + 64 * u];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = src[gi[u]];
+#pragma unroll
+        for (int u = 0; u < U; ++u) take(a + 64 * u, v[u]);
+    }
+    for (; a < n; a += 64) take(a, src[good[a]]);
+    for (int k = n + lane; k < Kp; k += 64) {   // zero rows past n
+        s0[k] = 0;
+        s1[k] = 0;
+    }
+    wave_dd_sum(hi, lo);
+    for (int o = 32; o > 0; o >>= 1) {
+        mx = fmax(mx, __shfl_xor(mx, o, 64));
+        ss += __shfl_xor(ss, o, 64);
+    }
+    const bool anyb = __ballot(bad) != 0ULL;
+    if (lane == 0) {
+        if (cm) cm[j] = dd_div_d(hi, lo, (double)n);
+        cmax[j] = mx;
+        cbad[j] = anyb ? 1 : 0;
+        css[j] = ss;
+    }
+}
+
+void launch_gather_prep(const double *d_M, int n0, const int *d_good, int n, double *d_X, double *d_colmean,
+                        double *d_cmax, int *d_cbad, long long *d_css, int8_t *d_sl, int Kp, int Np, hipStream_t s) {
+    hipLaunchKernelGGL(k_gather_prep, dim3((Np + 3) / 4), dim3(256), 0, s, d_M, n0, d_good, n, d_X, d_colmean, d_cmax,
+                       d_cbad, d_css, d_sl, Kp, Np);
+    TP_HIP(hipGetLastError());
+}
+
+// sd[j] = sqrt(cov_jj) from the exact S_jj = sum_i x_ij^2 (k_cor_sd's expression;
+// S_jj < 2^53 is exact in a double, the value X'X's diagonal holds)
+__global__ void __launch_bounds__(256) k_cor_sd_ss(const long long *css, const double *m, int n, double *sd) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const double fn = (double)n, fn1 = (double)(n - 1);
+    sd[j] = sqrt(((double)css[j] - fn * (m[j] * m[j])) / fn1);
+}
+void launch_cor_sd_ss(const long long *d_css, const double *d_m, int n, double *d_sd, hipStream_t s) {
+    hipLaunchKernelGGL(k_cor_sd_ss, dim3((n + 255) / 256), dim3(256), 0, s, d_css, d_m, n, d_sd);
+    TP_HIP(hipGetLastError());
+}
+
 __global__ void __launch_bounds__(256) k_colmean(const double *A, int n, int ld, double *cm) {
     int lane = threadIdx.x & 63;
     int j = blockIdx.x * 4 + (threadIdx.x >> 6);

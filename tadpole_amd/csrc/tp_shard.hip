@@ -249,6 +249,44 @@ void xtx_product(Ctx &c, const double *X, int n, double *S) {
     launch_clean_symmetrize(S, n, true, c.cur);
 }
 
+int g_xtx_fused = 1;   // 0: X'X into S, then the separate correlation epilogue (A/B, tests)
+
+void cor_product(Ctx &c, const double *X, int n, const double *m, const GatherStats *gs, double *S, double *C,
+                 double *sd, double *cmean) {
+    hipStream_t s = c.cur;
+    int ns = -1;
+    if (gs && g_xtx_fused && n >= 1024) ns = xtx_int_slices_cols(c, gs->cmax, gs->cbad, n);
+    if (!(ns == 1 || ns == 2)) {
+        if (!S) S = c.buf[S_S].as<double>((size_t)n * n);
+        kprof_begin(c, K_COR_GEMM);
+        xtx_product(c, X, n, S);
+        kprof_end(c, K_COR_GEMM);
+        launch_cor_epilogue(S, m, n, C, sd, s, cmean);
+        return;
+    }
+    c.last_xtx_ns = ns;
+    // the gather's 2-slice image serves ns = 1 too (its slice 1 is zero then)
+    const int8_t *sl = gs->slices2 ? xtx_slice_buf(c, n, 2) : xtx_slices(c, X, n, ns);
+    launch_cor_sd_ss(gs->css, m, n, sd, s);
+    kprof_begin(c, K_COR_GEMM);
+    if (!c.shard.active) {
+        xtx_int8_tiles128(c, sl, n, ns, C, 0, -1, m, sd);
+    } else {
+        // 128-column tiles split by tile columns exactly as xtx_product's big path
+        const int R = shard_count(c);
+        std::vector<int> tb(R + 1);
+        shard_plan((n + 1) / 2, R, 0, tb.data());   // kind 0 counts 64-wide tiles: (n + 127) / 128 of 128
+        for (int r = 0; r < R; ++r)
+            if (shard_mine(c, r)) xtx_int8_tiles128(c, sl, n, ns, C, tb[r], tb[r + 1], m, sd);
+        std::vector<size_t> off(R + 1);
+        for (int r = 0; r <= R; ++r) off[r] = (size_t)std::min(n, tb[r] * 128) * n;
+        shard_gather(c, C, off);
+        launch_clean_symmetrize(C, n, true, s);   // lower <- upper (cor is finite: NaN -> 0 done)
+    }
+    kprof_end(c, K_COR_GEMM);
+    if (cmean) launch_colmean(C, n, n, cmean, s);   // k_cor_epilogue_mean's bits
+}
+
 // Out (M x N col-major, ld M) = A' B with A stored K x M (col-major, lda) and
 // B K x N: rows of Out split in 64-row blocks, each written transposed into
 // the packed T (N x M col-major = Out row-major), gathered, transposed back.

@@ -205,9 +205,14 @@ __device__ __forceinline__ void xtx_supertile(int L, int tn, int &bm, int &bn) {
     }
     bm = bn = 0;   // not reached for L < tn (tn + 1) / 2
 }
-template <int NS>
+// COR: the sparse_cor epilogue (R/TADpole.R:96-98,449) applied to each exact
+// S_ij before the store -- C holds cor, with k_cor_epilogue's arithmetic (same
+// bits), and S is never written or re-read.  m: column means, sd: sqrt(cov_jj).
+template <int NS, bool COR = false>
 __global__ void __launch_bounds__(512) k_xtx_i8_big(const int8_t *__restrict__ S, int n, int Kp, int Np,
-                                                    double *__restrict__ C, int tcol0, int tn_all) {
+                                                    double *__restrict__ C, int tcol0, int tn_all,
+                                                    const double *__restrict__ cm = nullptr,
+                                                    const double *__restrict__ csd = nullptr) {
     __shared__ __attribute__((aligned(16))) int8_t Ls[2][2][NS][XB * XLD];   // [buf][A/B][slice]
     int bm, bn;
     if (tn_all > 0) {
@@ -298,36 +303,73 @@ __global__ void __launch_bounds__(512) k_xtx_i8_big(const int8_t *__restrict__ S
         __syncthreads();
         buf ^= 1;
     }
+    // COR: the tile's column means and sds (128 rows, 128 columns) into LDS
+    // (the staging buffers are free after the last barrier)
+    double *pm = (double *)&Ls[0][0][0][0];   // [0,128) m rows, [128,256) m cols, [256,384) sd rows, [384,512) sd cols
+    if constexpr (COR) {
+        if (t < 128) {
+            const int i = min(ia + t, n - 1), j = min(jb + t, n - 1);
+            pm[t] = cm[i];
+            pm[128 + t] = cm[j];
+            pm[256 + t] = csd[i];
+            pm[384 + t] = csd[j];
+        }
+        __syncthreads();
+    }
+    const double fn = (double)n, fn1 = (double)(n - 1);
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
         for (int b = 0; b < 2; ++b)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int i = ia + wm + 16 * a + (lane >> 4) * 4 + r;
-                const int j = jb + wn + 16 * b + fr;
+                const int il = wm + 16 * a + (lane >> 4) * 4 + r, jl = wn + 16 * b + fr;
+                const int i = ia + il;
+                const int j = jb + jl;
                 if (i >= n || j >= n || i > j) continue;
                 long long v = 0;
 #pragma unroll
                 for (int s = 0; s < NS; ++s)
 #pragma unroll
                     for (int u = 0; u < NS; ++u) v += (long long)acc[s][u][a][b][r] << (7 * (s + u));
-                const double d = (double)v;
+                double d = (double)v;
+                if constexpr (COR) {   // k_cor_epilogue's expression, element (i, j); (j, i) is the same value
+                    const double cij = (d - fn * (pm[il] * pm[128 + jl])) / fn1;
+                    d = cij / (pm[256 + il] * pm[384 + jl]);
+                    if (isnan(d)) d = 0.0;
+                }
                 C[(size_t)i + (size_t)j * n] = d;
                 C[(size_t)j + (size_t)i * n] = d;
             }
 }
 
-// Decide the path for X (n x n, col-major, device): 0 = fp64, else the slice count.
-int xtx_int_slices(Ctx &c, const double *d_X, int n) {
-    if (g_xtx_int8 == 0 || n > 130000) return 0;
-    unsigned long long *mb = (unsigned long long *)c.buf[S_SHARD2].as<char>(64);
-    int *flag = (int *)(mb + 1);
-    TP_HIP(hipMemsetAsync(mb, 0, 16, c.cur));
-    const size_t cnt = (size_t)n * n;
-    const unsigned g = (unsigned)std::max<size_t>(1, std::min<size_t>(2048, (cnt / 2 + 255) / 256));
-    hipLaunchKernelGGL(k_int_scan, dim3(g), dim3(256), 0, c.cur, d_X, cnt, mb, flag);
-    TP_HIP(hipGetLastError());
+// the gather's per-column maxima / flags -> the k_int_scan result format
+__global__ void __launch_bounds__(256) k_colflags(const double *cmax, const int *cbad, int n,
+                                                  unsigned long long *maxbits, int *notint) {
+    __shared__ double wm[4];
+    __shared__ int wb[4];
+    double m = 0.0;
+    int bad = 0;
+    for (int j = threadIdx.x; j < n; j += 256) {
+        m = fmax(m, cmax[j]);
+        bad |= cbad[j];
+    }
+    for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
+    const int anyb = __ballot(bad != 0) != 0ULL;
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        wm[w] = m;
+        wb[w] = anyb;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const double mm = fmax(fmax(wm[0], wm[1]), fmax(wm[2], wm[3]));
+        *maxbits = (unsigned long long)__double_as_longlong(mm);
+        *notint = wb[0] | wb[1] | wb[2] | wb[3];
+    }
+}
+
+static int slices_for(Ctx &c, unsigned long long *mb) {
     unsigned long long h[2] = {0, 0};
     unsigned long long *ph = (unsigned long long *)c.pinned(16);   // pinned: no staged copy
     TP_HIP(hipMemcpyAsync(ph, mb, 16, hipMemcpyDeviceToHost, c.cur));
@@ -342,18 +384,48 @@ int xtx_int_slices(Ctx &c, const double *d_X, int n) {
     return 0;
 }
 
+// Decide the path for X (n x n, col-major, device): 0 = fp64, else the slice count.
+int xtx_int_slices(Ctx &c, const double *d_X, int n) {
+    if (g_xtx_int8 == 0 || n > 130000) return 0;
+    unsigned long long *mb = (unsigned long long *)c.buf[S_SHARD2].as<char>(64);
+    int *flag = (int *)(mb + 1);
+    TP_HIP(hipMemsetAsync(mb, 0, 16, c.cur));
+    const size_t cnt = (size_t)n * n;
+    const unsigned g = (unsigned)std::max<size_t>(1, std::min<size_t>(2048, (cnt / 2 + 255) / 256));
+    hipLaunchKernelGGL(k_int_scan, dim3(g), dim3(256), 0, c.cur, d_X, cnt, mb, flag);
+    TP_HIP(hipGetLastError());
+    return slices_for(c, mb);
+}
+
+int xtx_kp(int n);
+// The same decision from the gather's per-column statistics (k_gather_prep)
+int xtx_int_slices_cols(Ctx &c, const double *d_cmax, const int *d_cbad, int n) {
+    if (g_xtx_int8 == 0 || n > 130000) return 0;
+    unsigned long long *mb = (unsigned long long *)c.buf[S_SMALL2].as<char>(64);
+    int *flag = (int *)(mb + 1);
+    hipLaunchKernelGGL(k_colflags, dim3(1), dim3(256), 0, c.cur, d_cmax, d_cbad, n, mb, flag);
+    TP_HIP(hipGetLastError());
+    return slices_for(c, mb);
+}
+
 // Slice column stride: whole 64-byte k-blocks, an ODD number of them, so
 // consecutive columns do not all start on the same HBM channel / L2 set (a
 // power-of-two stride such as 2048 B at n = 2000 ran 3x slower).
-static int xtx_kp(int n) {
+int xtx_kp(int n) {
     const int blocks = (n + 63) / 64;
     return 64 * (blocks | 1);
 }
 
+// the slice buffer (device scratch, valid until the next call); its first 64
+// bytes hold k_int_scan's result
+int8_t *xtx_slice_buf(Ctx &c, int n, int ns) {
+    const int Kp = xtx_kp(n), Np = (n + 127) / 128 * 128;
+    return c.buf[S_SHARD2].as<int8_t>((size_t)ns * Np * Kp + 64) + 64;
+}
 // int8 slices of X (device scratch, valid until the next call)
 const int8_t *xtx_slices(Ctx &c, const double *d_X, int n, int ns) {
     const int Kp = xtx_kp(n), Np = (n + 127) / 128 * 128;
-    int8_t *sl = c.buf[S_SHARD2].as<int8_t>((size_t)ns * Np * Kp + 64) + 64;
+    int8_t *sl = xtx_slice_buf(c, n, ns);
     dim3 g((unsigned)((Kp / 4 + 255) / 256), (unsigned)Np);
     hipLaunchKernelGGL(k_slice_i8, g, dim3(256), 0, c.cur, d_X, n, Kp, Np, ns, sl);
     TP_HIP(hipGetLastError());
@@ -365,7 +437,8 @@ int g_xtx_supertile = 1;
 // S (n x n) = X'X exactly on the upper tiles of tile columns [tc0, tc1) and
 // their mirrors, from ns slices.
 // 128-column tiles [tc0, tc1) (tile units of 128) by the LDS-staged kernel
-void xtx_int8_tiles128(Ctx &c, const int8_t *sl, int n, int ns, double *d_S, int tc0, int tc1) {
+void xtx_int8_tiles128(Ctx &c, const int8_t *sl, int n, int ns, double *d_S, int tc0, int tc1, const double *cm,
+                       const double *csd) {
     const int Kp = xtx_kp(n), Np = (n + 127) / 128 * 128;
     const int tn = Np / 128;
     tc0 = std::max(0, tc0);
@@ -373,10 +446,17 @@ void xtx_int8_tiles128(Ctx &c, const int8_t *sl, int n, int ns, double *d_S, int
     if (tc1 <= tc0) return;
     const unsigned nb = (unsigned)((long)tc1 * (tc1 + 1) / 2 - (long)tc0 * (tc0 + 1) / 2);
     const int tn_all = (tc0 == 0 && tc1 == tn && g_xtx_supertile) ? tn : 0;
-    if (ns == 1)
-        hipLaunchKernelGGL(k_xtx_i8_big<1>, dim3(nb), dim3(512), 0, c.cur, sl, n, Kp, Np, d_S, tc0, tn_all);
+    const bool cor = cm != nullptr;
+    if (ns == 1 && !cor)
+        hipLaunchKernelGGL((k_xtx_i8_big<1>), dim3(nb), dim3(512), 0, c.cur, sl, n, Kp, Np, d_S, tc0, tn_all, cm, csd);
+    else if (ns == 2 && !cor)
+        hipLaunchKernelGGL((k_xtx_i8_big<2>), dim3(nb), dim3(512), 0, c.cur, sl, n, Kp, Np, d_S, tc0, tn_all, cm, csd);
+    else if (ns == 1)
+        hipLaunchKernelGGL((k_xtx_i8_big<1, true>), dim3(nb), dim3(512), 0, c.cur, sl, n, Kp, Np, d_S, tc0, tn_all, cm,
+                           csd);
     else if (ns == 2)
-        hipLaunchKernelGGL(k_xtx_i8_big<2>, dim3(nb), dim3(512), 0, c.cur, sl, n, Kp, Np, d_S, tc0, tn_all);
+        hipLaunchKernelGGL((k_xtx_i8_big<2, true>), dim3(nb), dim3(512), 0, c.cur, sl, n, Kp, Np, d_S, tc0, tn_all, cm,
+                           csd);
     else fail(TP_ERR_ARG, "xtx_int8_tiles128: 1..2 slices");
     TP_HIP(hipGetLastError());
 }

@@ -155,6 +155,34 @@ def test_cor_epilogue_fused_colmean_same_bits(gpu, krylov):
         assert np.array_equal(a.clusters[q], b.clusters[q]), q
 
 
+@pytest.mark.parametrize("case", ["counts", "large_counts", "real"])
+def test_cor_in_xtx_store_same_bits(gpu, case):
+    """The correlation epilogue applied in the int8 X'X store with the gather's
+    column statistics (knob 18, default) gives the bits of X'X into S plus the
+    separate epilogue -- on counts (the fused path), on counts >= 2^14 (3
+    slices: the fallback) and on non-integer data (the fp64 product)."""
+    import tadpole_amd as tp
+    m = synth_hic(2100, SEED_BASE + 80)
+    if case == "large_counts":
+        m = m * 7.0                        # maxima past 2^14
+    elif case == "real":
+        m = m * 0.37                       # not integers
+    runs = []
+    for fused in (1, 0):
+        old = G.knob(18, fused)
+        try:
+            runs.append(tp.TADpole(m, max_pcs=150))
+        finally:
+            G.knob(18, old)
+    a, b = runs
+    assert (a.n_pcs, a.optimal_n_clusters) == (b.n_pcs, b.optimal_n_clusters)
+    assert np.array_equal(np.asarray(a.scores).view(np.uint64), np.asarray(b.scores).view(np.uint64))
+    assert a.clusters.keys() == b.clusters.keys()
+    for q in a.clusters:
+        assert np.array_equal(a.clusters[q], b.clusters[q]), q
+    assert np.array_equal(a.dendro.height.view(np.uint64), b.dendro.height.view(np.uint64))
+
+
 # ------------------------------------------------------------ arm path (C5)
 
 @pytest.mark.parametrize("name", ["arm_c5layout", "arm_early"])
