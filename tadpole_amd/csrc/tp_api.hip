@@ -1412,6 +1412,7 @@ void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
         case 16: p = &g_coniss_lu; break;
         case 17: p = &g_cor_fused; break;
         case 18: p = &g_xtx_fused; break;
+        case 19: p = &g_pca_cheb_fused; break;
         default: fail(TP_ERR_ARG, "unknown knob");
         }
         if (*which == 3 && *value != 16 && *value != 32) fail(TP_ERR_ARG, "stage depth must be 16 or 32");

@@ -570,6 +570,40 @@ void launch_r1_apply(const double *T, size_t rs, size_t cs, int N, int rows, int
     TP_HIP(hipGetLastError());
 }
 
+// The fixed-order reduction with the affine epilogue of GemmArgs::affine:
+// C = a sum + b Y [+ c Z] (the Chebyshev step; Y, Z share C's layout)
+__global__ void __launch_bounds__(256) k_splitk_reduce_af(const double *part, size_t stride, int S, int M, int N,
+                                                          double *C, int ldc, double a, double b, double c,
+                                                          const double *Y, const double *Z) {
+    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (size_t)M * N) return;
+    const int i = (int)(idx % M), j = (int)(idx / M);
+    double v = part[idx];
+    int z = 1;
+    for (; z + 8 <= S; z += 8) {
+        double t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t[u] = part[idx + (size_t)(z + u) * stride];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v = v + t[u];
+    }
+    for (; z < S; ++z) v = v + part[idx + (size_t)z * stride];
+    const size_t ci = (size_t)i + (size_t)j * ldc;
+    double w = a * v + b * Y[ci];
+    if (Z) w = w + c * Z[ci];
+    C[ci] = w;
+}
+// in place on a stored product (S = 1): same arithmetic
+__global__ void __launch_bounds__(256) k_affine_inplace(int M, int N, double *C, int ldc, double a, double b, double c,
+                                                        const double *Y, const double *Z) {
+    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (size_t)M * N) return;
+    const size_t ci = (size_t)(idx % M) + (size_t)(idx / M) * ldc;
+    double w = a * C[ci] + b * Y[ci];
+    if (Z) w = w + c * Z[ci];
+    C[ci] = w;
+}
+
 // Many partials of a small output (Gram matrices of CholQR, K'W of the Krylov
 // re-orthogonalisation): 64 outputs per workgroup, the partials of each split
 // over the 4 waves (wave w: z = w, w + 4, ...: ascending), the four group sums
@@ -614,6 +648,9 @@ void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s) {
                            !(rows_ts(g.K, g.N) && g.trans_a && !g.sym_upper && g.splitk <= 1)))
         fail(TP_ERR_ARG, "gemm_f64: the rank-1 epilogue is for plain long-K row-shardable products");
     if (g.sym_upper && g.M != g.N) fail(TP_ERR_ARG, "sym_upper GEMM needs a square output");
+    if (g.affine && (g.sym_upper || g.store_t || g.sub_from || g.rows || g.r1_vrow >= 0 || !g.af_y ||
+                     g.af_y == g.C || g.af_z == g.C))
+        fail(TP_ERR_ARG, "gemm_f64: the affine epilogue is for plain column-major products into a separate C");
     const int tm = (g.M + BM - 1) / BM, tn = (g.N + BN - 1) / BN;
     // sym_upper: upper tiles of tile columns [tc0, tc1) (a column shard)
     const int tc0 = g.sym_upper ? std::max(0, g.tcol0) : 0;
@@ -681,7 +718,7 @@ void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s) {
         // non-symmetric: >= 240 tiles of 128 means >= 960 of 64, where the auto
         // split-K policy below picks no split either (same bits)
         const bool want = g.sym_upper ? g.big_cols : (g.splitk <= 1 && nb2 >= 240 && g.K >= 512);
-        if (want && !g.sub_from) {
+        if (want && !g.sub_from && !g.affine) {
             if (g.sym_upper && c1 <= c0) return;
             if (g.trans_a)
                 hipLaunchKernelGGL(k_gemm_f64_big<true>, dim3((unsigned)nb2), dim3(256), 0, s, g.M, g.N, g.K, g.A,
@@ -698,7 +735,7 @@ void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s) {
     // (K < 512 only: with full K a wave per SIMD issues an f64 MFMA every ~150
     // cycles at best -- tools/mfma_rate.hip -- and the split-K 64 x 64 grid
     // with two workgroups a CU is faster)
-    if (g_gemm_panel && !g.sym_upper && g.splitk <= 1 && nblk < 192 && g.N <= 512 && g.K < 512) {
+    if (g_gemm_panel && !g.sym_upper && !g.affine && g.splitk <= 1 && nblk < 192 && g.N <= 512 && g.K < 512) {
         const long np = (long)((g.M + PM - 1) / PM) * ((g.N + PN - 1) / PN);
         if (np >= 128) {
             if (g.trans_a)
@@ -766,7 +803,17 @@ void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s) {
                            out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride, g_gemm_xcd, S == 1 ? g.sub_from : nullptr);
     }
     TP_HIP(hipGetLastError());
-    if (S > 1) {
+    if (g.affine) {
+        const size_t tot = (size_t)g.M * g.N;
+        const dim3 rg((unsigned)((tot + 255) / 256));
+        if (S > 1)
+            hipLaunchKernelGGL(k_splitk_reduce_af, rg, dim3(256), 0, s, out, pstride, S, g.M, g.N, g.C, g.ldc, g.af_a,
+                               g.af_b, g.af_c, g.af_y, g.af_z);
+        else
+            hipLaunchKernelGGL(k_affine_inplace, rg, dim3(256), 0, s, g.M, g.N, g.C, g.ldc, g.af_a, g.af_b, g.af_c,
+                               g.af_y, g.af_z);
+        TP_HIP(hipGetLastError());
+    } else if (S > 1) {
         size_t tot = (size_t)g.M * g.N;
         const dim3 rg((unsigned)((tot + 255) / 256));
         if (S >= 16 && tot <= ((size_t)1 << 18))

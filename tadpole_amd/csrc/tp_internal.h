@@ -150,6 +150,12 @@ struct GemmArgs {
     int r1_vrow = -1;
     const double *r1_u = nullptr;
     int r1_rows = 0;
+    // affine epilogue (the Chebyshev three-term step): C = af_a (A'B) + af_b af_y
+    // [+ af_c af_z], elementwise over C's column-major layout (ldc), in the
+    // split-K reduction; plain (not sym/store_t/sub_from/rows) products only
+    bool affine = false;
+    double af_a = 1.0, af_b = 0.0, af_c = 0.0;
+    const double *af_y = nullptr, *af_z = nullptr;
 };
 void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s);
 void launch_r1_apply(const double *T, size_t rs, size_t cs, int N, int rows, int vrow, const double *u, double *Out,
@@ -205,6 +211,7 @@ struct SweepDev {
     double *cost0 = nullptr;       // ntrees x roundup(n, 64) initial costs (scratch)
     const double *pt2 = nullptr;   // CONISS: the scores with slots 0 and 1 paired (set by the launcher, inside cost0)
     int pt2_ld = 256;              // its row stride: 64 x the widest tree's slots rounded to 4 or 8
+    const double *pt4 = nullptr;   // CONISS, trees of exactly 4 slots: slots (0,1) and (2,3) paired, row stride 256
     // CH segment statistics shared across trees (null: every tree computes its
     // own): the finest cuts' segments [s, e) go into an open-addressing set
     // (hkeys, empty = ~0), each distinct one gets a slot of ustore (k column
@@ -235,9 +242,11 @@ __host__ __device__ inline size_t coniss_link_stride(int n) { return (size_t)n +
 // row (up to 512 columns) and masks the columns past its prefix
 inline size_t pt_doubles(int n, int k) { return (size_t)n * k + 512; }
 // + the copy of the scores with column pairs (l, l + 64) adjacent that CONISS
-// reads (n x 256, or n x 512 for k > 256; see k_pt_pairs in tp_sweep.hip)
+// reads (n x 256, or n x 512 for k > 256; see k_pt_pairs in tp_sweep.hip),
+// + the fully paired copy the 4-slot trees read (n x 256, when k > 192)
 inline size_t sweep_cost0_doubles(int n, int ntrees, int k = 256) {
-    return (size_t)ntrees * (coniss_cost_stride(n) + coniss_link_stride(n)) + 2 + (size_t)n * (k > 256 ? 512 : 256);
+    return (size_t)ntrees * (coniss_cost_stride(n) + coniss_link_stride(n)) + 2 + (size_t)n * (k > 256 ? 512 : 256) +
+           (k > 192 ? (size_t)n * 256 : 0);
 }
 size_t sweep_sums_doubles(int n, int tree0, int ntrees);
 void blas_shutdown_all();
@@ -323,6 +332,7 @@ struct PcaStats {
     int krylov_steps = 0, krylov_dim = 0;   // block Krylov path (0: G formed)
 };
 extern int g_pca_krylov_min, g_pca_krylov_block, g_pca_krylov_steps, g_pca_over;
+extern int g_pca_cheb_fused;   // Krylov small problem: Chebyshev step in the T Y reduction (default 1)
 // d_C: n x n, with room for 2n more doubles after it (the Krylov path writes
 // m = colMeans(C) and a column of ones there); d_cmean: C's column means if the
 // caller already has them (may be d_C + n n), else computed here

@@ -141,9 +141,14 @@ int g_pca_margin = 0;     // extra Chebyshev degrees over the planned count (the
 int g_pca_krylov_min = 4096;   // N at which the block Krylov path replaces forming G (0: always, huge: never)
 int g_pca_krylov_block = 0;    // Krylov block p (0: 64 for k >= 128, else 32)
 int g_pca_over = 0;            // subspace oversampling b - k (0: max(32, k / 4), b rounded to 32; else rounded to 16)
+int g_pca_cheb_fused = 1;     // Krylov small problem: the Chebyshev step in the T Y product's reduction (0: k_cheb)
 int g_pca_krylov_steps = 0;    // Krylov steps s before the first check (0: ceil(5 k / p))
 
 using Prod = std::function<void(const double *, double *)>;
+// Out = a (A Y) + b Yc [+ c Yp]: the product with the Chebyshev step in its
+// epilogue (same arithmetic as k_cheb on a stored A Y)
+using ProdAff = std::function<void(const double *Y, double *Out, double a, double b, const double *Yc, double c,
+                                   const double *Yp)>;
 
 // Top-k eigenpairs of a symmetric n x n operator by Chebyshev-filtered block
 // subspace iteration.  prod(Y, Out): Out = A Y (n x b, ld n).  A (n x n, ld n)
@@ -151,7 +156,8 @@ using Prod = std::function<void(const double *, double *)>;
 // vectors, descending; h_theta: ascending Ritz values of the last Rayleigh-Ritz
 // problem.  Scratch: S_Q S_Z S_SWEEP S_SWEEP2 S_SMALL S_MISC (+ S_PARTIAL).
 static void subspace_topk(Ctx &c, const double *A, int n, int k, const Prod &prod, double *V,
-                          std::vector<double> &h_theta, PcaStats &st, uint64_t seed, int margin = 0) {
+                          std::vector<double> &h_theta, PcaStats &st, uint64_t seed, int margin = 0,
+                          const ProdAff *paff = nullptr) {
     hipStream_t s = c.cur;
     const int over = g_pca_over > 0 ? g_pca_over : std::max(32, k / 4);
     const int rnd = g_pca_over > 0 ? 16 : 32;
@@ -212,13 +218,21 @@ static void subspace_topk(Ctx &c, const double *A, int n, int k, const Prod &pro
         const size_t cnt = (size_t)n * b;
         const unsigned grid = (unsigned)((cnt + 255) / 256);
         double *prev = Q, *cur = T, *gy = Z, *nxt = Yb;
-        prod(Q, gy);
-        hipLaunchKernelGGL(k_cheb, dim3(grid), dim3(256), 0, s, cur, gy, Q, (const double *)nullptr, cnt,
-                           1.0 / hh, -e / hh, 0.0);
+        if (paff) {
+            (*paff)(Q, cur, 1.0 / hh, -e / hh, Q, 0.0, nullptr);
+        } else {
+            prod(Q, gy);
+            hipLaunchKernelGGL(k_cheb, dim3(grid), dim3(256), 0, s, cur, gy, Q, (const double *)nullptr, cnt,
+                               1.0 / hh, -e / hh, 0.0);
+        }
         for (int j = 1; j < m; ++j) {
-            prod(cur, gy);
-            hipLaunchKernelGGL(k_cheb, dim3(grid), dim3(256), 0, s, nxt, gy, cur, prev, cnt, 2.0 / hh,
-                               -2.0 * e / hh, -1.0);
+            if (paff) {
+                (*paff)(cur, nxt, 2.0 / hh, -2.0 * e / hh, cur, -1.0, prev);
+            } else {
+                prod(cur, gy);
+                hipLaunchKernelGGL(k_cheb, dim3(grid), dim3(256), 0, s, nxt, gy, cur, prev, cnt, 2.0 / hh,
+                                   -2.0 * e / hh, -1.0);
+            }
             double *old = prev;
             prev = cur;
             cur = nxt;
@@ -467,10 +481,22 @@ static void krylov_topk(Ctx &c, double *C, int n, int k, double *V, double *P, s
             g.splitk = 0;
             gemm_f64(g, c.buf[S_PARTIAL], s);
         };
+        ProdAff taff = [&](const double *Y, double *Out, double a, double b, const double *Yc, double cc,
+                           const double *Yp) {
+            GemmArgs g{D, sst.block, D, Tm, D, true, Y, D, Out, D};
+            g.splitk = 0;
+            g.affine = true;
+            g.af_a = a;
+            g.af_b = b;
+            g.af_y = Yc;
+            g.af_c = cc;
+            g.af_z = Yp;
+            gemm_f64(g, c.buf[S_PARTIAL], s);
+        };
         // +2 planned degrees: a product with T costs ~1.5 % of a Rayleigh-Ritz
         // round (one-workgroup tridiagonalisation) that a near miss of the
         // residual check would add
-        subspace_topk(c, Tm, D, k, tprod, Vs, h_theta, sst, 0x5EEDULL + (uint64_t)D, 2);
+        subspace_topk(c, Tm, D, k, tprod, Vs, h_theta, sst, 0x5EEDULL + (uint64_t)D, 2, g_pca_cheb_fused ? &taff : nullptr);
         // V = K Y, G V = (G K) Y; residuals in the n-dimensional space
         GemmArgs vg{n, k, D, K, n, false, Vs, D, V, n};
         vg.splitk = 0;

@@ -172,11 +172,15 @@ __device__ __forceinline__ void wave_sum2(double &u, double &v) {
 // after them (zero past k).  A lane then fetches its first two columns with
 // one 16-byte load; the columns a lane holds and their order are those of the
 // plain layout (same bits).  Slab rows of merged clusters use the same layout.
-__global__ void __launch_bounds__(256) k_pt_pairs(const double *Pt, int n, int ldp, int k, double *Pt2, int W) {
+// full: slots 2 and 3 paired as well (W = 256, the copy the 4-slot trees read:
+// two 16-byte loads a lane per row).  An odd slot count keeps its last slot
+// plain (a paired last slot would be read at a 16-byte stride).
+__global__ void __launch_bounds__(256) k_pt_pairs(const double *Pt, int n, int ldp, int k, double *Pt2, int W,
+                                                  int full) {
     const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= (size_t)n * W) return;
     const int p = (int)(idx / W), q = (int)(idx % W);
-    const int c = q < 128 ? 64 * (q & 1) + (q >> 1) : q;
+    const int c = (q < 128 || (full && q < 256)) ? (q & ~127) + 64 * (q & 1) + ((q & 127) >> 1) : q;
     Pt2[idx] = c < k ? Pt[(size_t)p * ldp + c] : 0.0;
 }
 static size_t coniss_pt2_offset(int n, int ntrees) {
@@ -345,9 +349,11 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
     // slots 2 and 3 plain -- in the tree's slab (stride ld) and in the shared
     // paired copy of the scores (stride sd.pt2_ld); NS = 1: plain rows, the scores
     // read from Pt itself
+    // NS = 4: slots (2, 3) paired too, slab rows and the shared copy sd.pt4
+    constexpr bool P4 = NS == 4;
     double *S = sd.sums + sums_off(n, sd.tree0, i);
-    const double *PP = NS >= 2 ? sd.pt2 : sd.Pt;
-    const size_t ldpp = NS >= 2 ? (size_t)sd.pt2_ld : (size_t)sd.ldp;
+    const double *PP = P4 ? sd.pt4 : (NS >= 2 ? sd.pt2 : sd.Pt);
+    const size_t ldpp = P4 ? (size_t)256 : (NS >= 2 ? (size_t)sd.pt2_ld : (size_t)sd.ldp);
     const bool last_in = lane + 64 * (NS - 1) < i;
     int *mrg_a = sd.mrg_a + (size_t)ti * (n - 1);
     int *mrg_b = sd.mrg_b + (size_t)ti * (n - 1);
@@ -384,8 +390,14 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
         } else {
             dst[0] = pr[lane];
         }
+        if (P4) {
+            const double2 v = *(const double2 *)(pr + 128 + 2 * lane);
+            dst[2] = v.x;
+            dst[3] = v.y;
+        } else {
 #pragma unroll
-        for (int t = 2; t < NS; ++t) dst[t] = pr[64 * t + lane];
+            for (int t = 2; t < NS; ++t) dst[t] = pr[64 * t + lane];
+        }
     };
     auto rowc = [](int start, bool single) { return start | (single ? ROW_PT : 0); };
     // A: a merge described by (a, ea, eb, ls, r, er); b = ea + 1; ll = start of
@@ -652,8 +664,12 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
                 *(double2 *)(S + (size_t)a_ * ld + 2 * lane) = make_double2(sm[0], sm[1]);
             else
                 S[(size_t)a_ * ld + lane] = sm[0];
+            if (P4) {
+                *(double2 *)(S + (size_t)a_ * ld + 128 + 2 * lane) = make_double2(sm[2], sm[3]);
+            } else {
 #pragma unroll
-            for (int t = 2; t < NS; ++t) S[(size_t)a_ * ld + 64 * t + lane] = sm[t];
+                for (int t = 2; t < NS; ++t) S[(size_t)a_ * ld + 64 * t + lane] = sm[t];
+            }
             if (STAMPS) {   // waits for the rows (the stamp below then counts the HBM wait)
                 double z = 0.0;
 #pragma unroll
@@ -1334,9 +1350,17 @@ static void run_coniss(const SweepDev &sd_in, hipStream_t s, bool stamped, Ctx *
         sd.pt2_ld = 64 * ks;
         const size_t cnt = (size_t)sd.n * sd.pt2_ld;
         hipLaunchKernelGGL(k_pt_pairs, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, sd.Pt, sd.n, sd.ldp, sd.k,
-                           pt2, sd.pt2_ld);
+                           pt2, sd.pt2_ld, 0);
         TP_HIP(hipGetLastError());
         sd.pt2 = pt2;
+        if (sd.tree0 + sd.ntrees > 192 && sd.tree0 < 256) {   // 4-slot trees: the fully paired copy
+            double *pt4 = pt2 + cnt;
+            const size_t c4 = (size_t)sd.n * 256;
+            hipLaunchKernelGGL(k_pt_pairs, dim3((unsigned)((c4 + 255) / 256)), dim3(256), 0, s, sd.Pt, sd.n, sd.ldp,
+                               sd.k, pt4, 256, 1);
+            TP_HIP(hipGetLastError());
+            sd.pt4 = pt4;
+        }
     }
     if (ks == 4)
         hipLaunchKernelGGL(k_seed<4>, dim3(sd.ntrees, nbk), dim3(64), 0, s, sd, cost0);

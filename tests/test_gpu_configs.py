@@ -183,6 +183,25 @@ def test_cor_in_xtx_store_same_bits(gpu, case):
     assert np.array_equal(a.dendro.height.view(np.uint64), b.dendro.height.view(np.uint64))
 
 
+def test_cheb_in_product_reduction_same_bits(gpu):
+    """The Chebyshev three-term step applied in the split-K reduction of the
+    Krylov small problem's T Y product (knob 19, default) gives the bits of the
+    stored product plus k_cheb: the same arithmetic on the same reduced value."""
+    import tadpole_amd as tp
+    m = synth_hic(4200, SEED_BASE + 81)      # n >= 4096: the block Krylov path
+    runs = []
+    for fused in (1, 0):
+        old = G.knob(19, fused)
+        try:
+            runs.append(tp.TADpole(m, max_pcs=120))
+        finally:
+            G.knob(19, old)
+    a, b = runs
+    assert a.timings_ms[16] > 0                       # the Krylov path ran
+    assert np.array_equal(np.asarray(a.scores).view(np.uint64), np.asarray(b.scores).view(np.uint64))
+    assert np.array_equal(a.dendro.height.view(np.uint64), b.dendro.height.view(np.uint64))   # PC-score bits
+
+
 # ------------------------------------------------------------ arm path (C5)
 
 @pytest.mark.parametrize("name", ["arm_c5layout", "arm_early"])
