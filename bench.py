@@ -368,9 +368,12 @@ def main():
     lane0 = Lane(0)
     torch.cuda.synchronize()
 
+    host_t = {"call": 0.0, "assemble": 0.0, "n": 0}   # wall of the C call / of the host assembly
+
     def step(lane, want_timings=True):
         b, dev_m, stream = lane.bufs, lane.dev_m, lane.stream
         outs = [I(0) for _ in range(6)]
+        tc0 = time.perf_counter()
         n_good, k, w, n_pcs, n_clusters, st = outs
         L.tp_pipeline_dev(ctypes.c_void_p(dev_m.data_ptr()), ctypes.byref(I(n0)), ctypes.byref(I(args.max_pcs)),
                           ctypes.byref(I(args.min_clusters)), ctypes.byref(ctypes.c_double(0.01)),
@@ -382,6 +385,7 @@ def main():
                           _lib.ip(b["boundary"]), _lib.dp(b["timings"]) if want_timings else None,
                           ctypes.byref(st))
         _lib.check(st)
+        tc1 = time.perf_counter()
         n = n_good.value
         kk, ww = k.value, w.value
         res = dict(bad=b["bad"].astype(bool), good=b["good"][:n].copy(), k=kk, w=ww,
@@ -389,7 +393,11 @@ def main():
                    n_clusters=n_clusters.value,
                    merge=b["merge"][:2 * (n - 1)].reshape(2, n - 1).T.copy(), height=b["height"][:n - 1].copy(),
                    boundary=b["boundary"][:n - 1].copy(), timings=b["timings"].copy())
-        return _assemble(res, np.flatnonzero(res["bad"]) + 1)
+        out = _assemble(res, np.flatnonzero(res["bad"]) + 1)
+        host_t["call"] += tc1 - tc0
+        host_t["assemble"] += time.perf_counter() - tc1
+        host_t["n"] += 1
+        return out
 
     for _ in range(args.warmup):
         step(lane0)
@@ -403,6 +411,7 @@ def main():
     # library records HIP events per kernel class on that stream
     tms = []
     barrier()
+    host_t.update(call=0.0, assemble=0.0, n=0)
     t0 = time.perf_counter()
     last = None
     for _ in range(args.steps):
@@ -416,6 +425,10 @@ def main():
         elapsed = float(t.item())
     tm = np.mean(np.stack(tms), axis=0)
     n, k = int(tm[14]), int(tm[15])
+    nh = max(1, host_t["n"])
+    host_ms = {"c_call": round(host_t["call"] / nh * 1e3, 3), "device_stages": round(float(tm[4]), 3),
+               "c_call_minus_device": round(host_t["call"] / nh * 1e3 - float(tm[4]), 3),
+               "python_assembly": round(host_t["assemble"] / nh * 1e3, 3)}
 
     # ---- throughput with S matrices in flight (not `value`)
     thr = None
@@ -536,7 +549,7 @@ def main():
                           "n0": n0, "n_good": n, "k": k, "max_pcs": args.max_pcs,
                           "parallelism": (f"one matrix over {world} GPU(s): column/row-split products, "
                                           "RCCL all-gather" if args.sharded else f"one matrix per GPU x{world}")},
-               "roofline": roof}
+               "roofline": roof, "host_ms_per_step": host_ms}
         if comm_size is not None:
             out["rccl_comm_size"] = comm_size
         if thr:

@@ -424,7 +424,7 @@ static SweepOut run_sweep(Ctx &c, const double *d_Pt, int n, int k, int min_clus
     {
         int *pi = (int *)c.pinned((size_t)(k + R) * sizeof(int));   // nc_all and err_all are contiguous
         TP_HIP(hipMemcpyAsync(pi, nc_all, (size_t)(k + R) * sizeof(int), hipMemcpyDeviceToHost, s));
-        TP_HIP(hipStreamSynchronize(s));
+        stream_sync(c, s);
         memcpy(h_nc.data(), pi, k * sizeof(int));
         memcpy(h_err.data(), pi + k, R * sizeof(int));
     }
@@ -452,7 +452,7 @@ static SweepOut run_sweep(Ctx &c, const double *d_Pt, int n, int k, int min_clus
         double *scr = (double *)(big + (((size_t)d.ntrees * 4 + 255) & ~(size_t)255));
         TP_HIP(hipMemcpyAsync(d_slot, slot.data(), (size_t)d.ntrees * 4, hipMemcpyHostToDevice, s));
         launch_ch_glb(d, d_slot, scr, sd_d, s);
-        TP_HIP(hipStreamSynchronize(s));   // the host slot list lives on this stack frame
+        stream_sync(c, s);   // the host slot list lives on this stack frame
     }
     SweepOut o;
     o.w = *std::max_element(h_nc.begin(), h_nc.end());
@@ -474,7 +474,7 @@ static SweepOut run_sweep(Ctx &c, const double *d_Pt, int n, int k, int min_clus
             TP_HIP(hipMemcpyAsync(ps + (size_t)t0 * o.w, sc_all + (size_t)t0 * sd.w_cap,
                                   (size_t)nt * o.w * sizeof(double), hipMemcpyDeviceToHost, s));
         }
-        TP_HIP(hipStreamSynchronize(s));
+        stream_sync(c, s);
         for (int r = 0; r < R; ++r) {
             const int t0 = tb[r], nt = tb[r + 1] - tb[r];
             const double *blk = ps + (size_t)t0 * o.w;
@@ -508,7 +508,7 @@ static SweepOut run_sweep(Ctx &c, const double *d_Pt, int n, int k, int min_clus
         TP_HIP(hipMemcpyAsync(all_cost->data(), cost, rec * 8, hipMemcpyDeviceToHost, s));
         TP_HIP(hipMemcpyAsync(all_h->data(), hgt, rec * 8, hipMemcpyDeviceToHost, s));
     }
-    TP_HIP(hipStreamSynchronize(s));
+    stream_sync(c, s);
     memcpy(ma.data(), pa, (n - 1) * sizeof(int));
     memcpy(mb.data(), pb, (n - 1) * sizeof(int));
     memcpy(he.data(), ph, (n - 1) * sizeof(double));
@@ -535,10 +535,16 @@ static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_cl
     Timer tm(timings != nullptr, s);
     // TP_FLAG_SHARDED: this call splits its products over the ranks of the
     // device's communicator (or its virtual shards); reset on every exit
+    // (a sharded call that throws aborts the communicator: its peers then
+    // leave their collectives through their deadline, see stream_sync)
     struct ShardScope {
         Ctx &c;
-        ShardScope(Ctx &cc, bool on) : c(cc) { c.shard.active = on; }
-        ~ShardScope() { c.shard.active = false; }
+        int pending;
+        ShardScope(Ctx &cc, bool on) : c(cc), pending(std::uncaught_exceptions()) { c.shard.active = on; }
+        ~ShardScope() {
+            if (c.shard.active && c.shard.comm && std::uncaught_exceptions() > pending) comm_abort(c);
+            c.shard.active = false;
+        }
     } shard_scope(c, (flags & TP_FLAG_SHARDED) != 0);
     c.prof = timings != nullptr;
     c.recs.clear();
@@ -557,7 +563,7 @@ static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_cl
         for (int q = 0; q < n0; ++q) iota[q] = q;
         TP_HIP(hipMemcpyAsync(d_good, iota.data(), n0 * sizeof(int), hipMemcpyHostToDevice, s));
         TP_HIP(hipMemsetAsync(d_bad, 0, n0 * sizeof(int), s));
-        TP_HIP(hipStreamSynchronize(s));
+        stream_sync(c, s);
         n = n0;
     } else {
         launch_rowmean_diag(d_M, n0, rm, dg, s);
@@ -571,7 +577,7 @@ static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_cl
         TP_HIP(hipMemcpyAsync(pi + 2 * n0, d_ng, sizeof(int), hipMemcpyDeviceToHost, s));
         if (bad) TP_HIP(hipMemcpyAsync(pi, d_bad, n0 * sizeof(int), hipMemcpyDeviceToHost, s));
         if (good_idx) TP_HIP(hipMemcpyAsync(pi + n0, d_good, n0 * sizeof(int), hipMemcpyDeviceToHost, s));
-        TP_HIP(hipStreamSynchronize(s));
+        stream_sync(c, s);
         if (!(flags & TP_FLAG_NO_MASK)) n = pi[2 * n0];
         if (bad) memcpy(bad, pi, n0 * sizeof(int));
         if (good_idx) memcpy(good_idx, pi + n0, (size_t)n * sizeof(int));
@@ -600,19 +606,44 @@ static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_cl
     trace_mark(s, "mask");
     tm.mark();
     // ---- sparse_cor (R/TADpole.R:94-100,448-449)
-    double *C = c.buf[S_C].as<double>(pca_c_doubles(n));
-    double *cmean = g_cor_fused ? C + (size_t)n * n : nullptr;   // C's column means, for prcomp (C's tail)
+    const int k = std::min(max_pcs, n);
+    // C5 (one matrix over R > 1 shards, Krylov PCA, int8-exact X'X): C stays
+    // row-sharded -- shard r computes and keeps only the columns (= rows, C is
+    // symmetric) its Krylov products read, so C is never gathered; with real
+    // ranks a rank allocates only its slab
+    CorSlab slab;
+    bool use_slab = false;
+    {
+        const int R = shard_count(c);
+        const int b_est = std::min(n, ((k + std::max(32, k / 4) + 31) / 32) * 32);
+        if (g_shard_slab && c.shard.active && R > 1 && prep && n >= g_pca_krylov_min && b_est < n) {
+            const int ns = xtx_int_slices_cols(c, gs.cmax, gs.cbad, n);
+            if (ns == 1 || ns == 2) {
+                use_slab = true;
+                slab.ns = ns;
+                slab.rb.resize(R + 1);
+                shard_plan(n + 2, R, 1, slab.rb.data());   // rows_gemm_sharded's row plan over [C | m | 1]
+                slab.narrow = c.shard.comm != nullptr;
+            }
+        }
+    }
+    const int sc0 = use_slab && slab.narrow ? slab.rb[c.shard.rank] : 0;
+    const int sc1 = use_slab && slab.narrow ? slab.rb[c.shard.rank + 1] : -1;
+    double *C = use_slab && slab.narrow ? c.buf[S_C].as<double>((size_t)n * (sc1 - sc0) + 64)
+                                        : c.buf[S_C].as<double>(pca_c_doubles(n));
+    // C's column means, for prcomp (C's tail, or the [m | 1] buffer of a slab)
+    double *cmean = use_slab ? c.buf[S_MEXT].as<double>(2 * (size_t)n) : (g_cor_fused ? C + (size_t)n * n : nullptr);
     trace_mark(s, "cor: start");
-    cor_product(c, X, n, m, prep ? &gs : nullptr, nullptr, C, c.buf[S_DIAG].as<double>(n), cmean);
+    cor_product(c, X, n, m, prep ? &gs : nullptr, nullptr, C, c.buf[S_DIAG].as<double>(n), cmean,
+                use_slab ? &slab : nullptr);
     trace_mark(s, "cor");
     tm.mark();
     // ---- prcomp (R/TADpole.R:452-453)
-    const int k = std::min(max_pcs, n);
     o.k = k;
     if (k > k_cap) fail(TP_ERR_CAPACITY, "k_cap smaller than min(max_pcs, n_good)");
     double *P = c.buf[S_P].as<double>((size_t)n * k);
     double *Pt = c.buf[S_PT].as<double>(pt_doubles(n, k));
-    PcaStats ps = pca_dev(c, C, n, k, P, Pt, nullptr, cmean);
+    PcaStats ps = pca_dev(c, C, n, k, P, Pt, nullptr, cmean, sc0, sc1);
     trace_mark(s, "pca");
     tm.mark();
     // ---- find_params + final tree (R/TADpole.R:456-460)
@@ -1413,6 +1444,11 @@ void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
         case 17: p = &g_cor_fused; break;
         case 18: p = &g_xtx_fused; break;
         case 19: p = &g_pca_cheb_fused; break;
+        case 20: p = &g_pca_ckrylov; break;
+        case 21: p = &g_ckry_chunk; break;
+        case 22: p = &g_ckry_steps; break;
+        case 23: p = &g_gemm_ts32; break;
+        case 24: p = &g_shard_slab; break;
         default: fail(TP_ERR_ARG, "unknown knob");
         }
         if (*which == 3 && *value != 16 && *value != 32) fail(TP_ERR_ARG, "stage depth must be 16 or 32");

@@ -406,32 +406,35 @@ int g_gemm_panel = 1;   // 0: tall-skinny products take the split-K 64 x 64 path
 // registers during the MFMAs, split-K chunks for a grid of ~2 workgroups a
 // CU.  Same k order as k_gemm_f64 (steps of 4 within blocks of 16): for the
 // same chunking the bits are those of the 64 x 64 kernel.
+// TN = 32 (the C-Krylov blocks): a 128 x 32 tile, each wave 32 x 32 (2 x 2
+// accumulators); same k order, so the bits of a column do not depend on TN.
 constexpr int TSM = 128, TSN = 64, TSK = 16, TSLD = TSK + 2;
-template <int TAG>
+template <int TAG, int TN = TSN>
 __global__ void __launch_bounds__(256, 2) k_gemm_ts(int M, int N, int K, const double *__restrict__ A, int lda,
                                                     const double *__restrict__ B, int ldb, double *__restrict__ C,
                                                     int ldc, int store_t, int kchunk, size_t part_stride) {
+    constexpr int NB = TN / 16;   // accumulator columns per wave
     __shared__ double As[2][TSM][TSLD];
-    __shared__ double Bs[2][TSN][TSLD];
-    const int tm = (M + TSM - 1) / TSM, tn = (N + TSN - 1) / TSN;
+    __shared__ double Bs[2][TN][TSLD];
+    const int tm = (M + TSM - 1) / TSM, tn = (N + TN - 1) / TN;
     // XCD-aware order (see k_gemm_f64): the column tiles of one row panel and
     // its neighbours run on one XCD and share the A panel in its L2
     const int total = (int)gridDim.x;
     const int xcd = (int)blockIdx.x & 7, slot = (int)blockIdx.x >> 3;
     const int Lg = xcd * (total >> 3) + min(xcd, total & 7) + slot;
     const int bn = Lg % tn, bm = (Lg / tn) % tm, z = Lg / (tn * tm);
-    const int i0 = bm * TSM, j0 = bn * TSN;
+    const int i0 = bm * TSM, j0 = bn * TN;
     const int kbeg = z * kchunk, kend = min(K, kbeg + kchunk);
     C += part_stride * z;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int wm = 32 * w;
     const int fr = lane & 15, fk = lane >> 4;
-    d4 acc[2][4];
+    d4 acc[2][NB];
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) acc[a][b] = (d4){0.0, 0.0, 0.0, 0.0};
-    double ra[8], rb[4];
+        for (int b = 0; b < NB; ++b) acc[a][b] = (d4){0.0, 0.0, 0.0, 0.0};
+    double ra[8], rb[NB];
     // thread t loads k = t & 15 of rows (t >> 4) + 16 p: 16 lanes read 128
     // contiguous bytes of one row
     const int lk = t & 15, lr = t >> 4;
@@ -444,7 +447,7 @@ __global__ void __launch_bounds__(256, 2) k_gemm_ts(int M, int N, int K, const d
             ra[p] = (kin && i < M) ? A[(size_t)k + (size_t)i * lda] : 0.0;
         }
 #pragma unroll
-        for (int p = 0; p < 4; ++p) {
+        for (int p = 0; p < NB; ++p) {
             const int j = j0 + lr + 16 * p;
             rb[p] = (kin && j < N) ? B[(size_t)k + (size_t)j * ldb] : 0.0;
         }
@@ -453,7 +456,7 @@ __global__ void __launch_bounds__(256, 2) k_gemm_ts(int M, int N, int K, const d
 #pragma unroll
         for (int p = 0; p < 8; ++p) As[buf][lr + 16 * p][lk] = ra[p];
 #pragma unroll
-        for (int p = 0; p < 4; ++p) Bs[buf][lr + 16 * p][lk] = rb[p];
+        for (int p = 0; p < NB; ++p) Bs[buf][lr + 16 * p][lk] = rb[p];
     };
     if (kbeg < kend) {
         load(kbeg);
@@ -466,15 +469,15 @@ __global__ void __launch_bounds__(256, 2) k_gemm_ts(int M, int N, int K, const d
         if (more) load(k0 + TSK);
 #pragma unroll
         for (int kk = 0; kk < TSK; kk += 4) {
-            double af[2], bf[4];
+            double af[2], bf[NB];
 #pragma unroll
             for (int a = 0; a < 2; ++a) af[a] = As[buf][wm + 16 * a + fr][kk + fk];
 #pragma unroll
-            for (int b = 0; b < 4; ++b) bf[b] = Bs[buf][16 * b + fr][kk + fk];
+            for (int b = 0; b < NB; ++b) bf[b] = Bs[buf][16 * b + fr][kk + fk];
 #pragma unroll
             for (int a = 0; a < 2; ++a)
 #pragma unroll
-                for (int b = 0; b < 4; ++b)
+                for (int b = 0; b < NB; ++b)
                     acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[a], bf[b], acc[a][b], 0, 0, 0);
         }
         if (more) store(buf ^ 1);
@@ -484,7 +487,7 @@ __global__ void __launch_bounds__(256, 2) k_gemm_ts(int M, int N, int K, const d
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b)
+        for (int b = 0; b < NB; ++b)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int i = i0 + wm + 16 * a + fk + 4 * r;
@@ -495,6 +498,7 @@ __global__ void __launch_bounds__(256, 2) k_gemm_ts(int M, int N, int K, const d
             }
 }
 int g_gemm_ts = 8;   // k_gemm_ts: most k chunks (0: off -> the 64 x 64 split-K kernel)
+int g_gemm_ts32 = 8;   // the same for the 32-column tile (a function of K alone: shards agree)
 
 // Fixed-order split-K reduction: C = sum_{z=0..S-1} part[z] (column-major M x N),
 // z ascending; loads issued 8 at a time (S is a runtime count: one dependent
@@ -660,11 +664,12 @@ void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s) {
     // long-K tall-skinny A'B (Xc products of the PCA): 128 x 64 tiles, before
     // any other choice -- a row shard must take the same kernel and k chunks
     if (g.rows && rows_ts(g.K, g.N) && g.trans_a && !g.sym_upper && (g.splitk <= 0 || g.splitk == 1)) {
-        const long tiles = (long)((g.M + TSM - 1) / TSM) * ((g.N + TSN - 1) / TSN);
+        const int tnw = g.N <= 32 ? 32 : TSN;   // tile width: 32 for the C-Krylov blocks
+        const long tiles = (long)((g.M + TSM - 1) / TSM) * ((g.N + tnw - 1) / tnw);
         // the k chunks depend on K alone (not on M): a row shard of the
         // product (tp_shard.hip) then sums every element in the same order
         int S = 1;
-        if (g.splitk <= 0) S = std::max(1, std::min(g_gemm_ts, g.K / 256));
+        if (g.splitk <= 0) S = std::max(1, std::min(tnw == 32 ? g_gemm_ts32 : g_gemm_ts, g.K / 256));
         int kchunk = ((g.K + S - 1) / S + TSK - 1) / TSK * TSK;
         S = (g.K + kchunk - 1) / kchunk;
         double *out = g.C;
@@ -678,7 +683,10 @@ void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s) {
             st = 0;
         }
         const dim3 grid((unsigned)(tiles * S));
-        if (g.tag == 1)
+        if (tnw == 32)
+            hipLaunchKernelGGL((k_gemm_ts<1, 32>), grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb, out,
+                               ldo, st, kchunk, pstride);
+        else if (g.tag == 1)
             hipLaunchKernelGGL(k_gemm_ts<1>, grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb, out, ldo, st,
                                kchunk, pstride);
         else

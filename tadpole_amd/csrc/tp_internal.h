@@ -99,7 +99,8 @@ enum Slot {
     S_M = 0, S_ROWMEAN, S_DIAG, S_BAD, S_GOOD, S_NGOOD, S_X, S_COLMEAN,
     S_S, S_C, S_XC, S_XCT, S_G, S_Q, S_Z, S_W, S_SMALL, S_P, S_PT,
     S_SWEEP, S_SWEEP2, S_SCORES, S_PARTIAL, S_MISC, S_SHARD, S_SHARD2, S_DEDUP,
-    S_KRY, S_KRYG, S_KRYT, S_KRYV, S_KRYX, S_CMEAN, S_CHBIG, S_CHOLP, S_SMALL2, S_GSTAT, S_NSLOT
+    S_KRY, S_KRYG, S_KRYT, S_KRYV, S_KRYX, S_CMEAN, S_CHBIG, S_CHOLP, S_SMALL2, S_GSTAT, S_XTXT, S_MEXT, S_KRYA,
+    S_NSLOT
 };
 static_assert(S_NSLOT <= (int)(sizeof(Ctx::buf) / sizeof(Ctx::buf[0])), "Ctx::buf too small for the slots");
 
@@ -114,6 +115,7 @@ void launch_mask_select(const double *d_rowmean, const double *d_diag, int n0,
 void launch_gather_colmean(const double *d_M, int n0, const int *d_good, int n,
                            double *d_X, double *d_colmean, hipStream_t s);
 void launch_colmean(const double *d_A, int n, int ld, double *d_mean, hipStream_t s);
+void launch_colmean_cols(const double *d_A, int n, int ncols, int ld, double *d_mean, hipStream_t s);
 // the gather with what the int8 X'X needs (per-column max / non-integer flag /
 // exact sum of squares, speculative 2-slice int8 image), tp_prep.hip
 void launch_gather_prep(const double *d_M, int n0, const int *d_good, int n, double *d_X, double *d_colmean,
@@ -180,6 +182,7 @@ constexpr int kCholInvMax = 256;
 extern int g_chol_inv_waves;
 extern int g_gemm_splitk;
 extern int g_gemm_ts;
+extern int g_gemm_ts32;
 extern int g_xtx_supertile;   // int8 X'X: XCD-contiguous supertile order of the 128 x 128 tiles (0: columns)
 // row-shardable products that take the 128 x 64 kernel with k chunks fixed by K
 // (tp_gemm.hip); shards and the unsharded call must agree on it
@@ -283,6 +286,10 @@ void tsv_read(const char *path, int nrow, int ncol, int nthreads, bool row_major
 void comm_unique_id(char *id128);
 void comm_init(Ctx &c, const char *id128, int nranks, int rank);
 void comm_destroy(Ctx &c);
+// host waits of a call that may be sharded: bounded and abort-on-failure with a
+// live communicator (see tp_shard.hip), hipStreamSynchronize otherwise
+void stream_sync(Ctx &c, hipStream_t s);
+void comm_abort(Ctx &c);
 int shard_count(const Ctx &c);
 bool shard_mine(const Ctx &c, int r);
 void shard_plan(int n, int R, int kind, int *bounds);
@@ -296,18 +303,24 @@ struct R1 {
     const double *u;   // nullptr: all ones
     int rows;
 };
+// a_col0: A points at column a_col0 of the logical K x M matrix (a rank's
+// column slab of C: its shard's rows are the only ones it reads)
 void rows_gemm_sharded(Ctx &c, const double *A, int lda, int M, const double *B, int ldb, int N, int K,
-                       double *Out, int splitk_plain, int tag = 0, const R1 *r1 = nullptr);
+                       double *Out, int splitk_plain, int tag = 0, const R1 *r1 = nullptr, int a_col0 = 0);
 
 // exact X'X on int8 matrix cores for integer counts (tp_xtx.hip)
 extern int g_xtx_int8;
 extern int g_xtx_fused;
+extern int g_shard_slab;   // 1: C5 shards keep C row-sharded (column slabs), 0: C gathered whole
 int xtx_int_slices(Ctx &c, const double *d_X, int n);   // 0 = not integer counts (fp64 path)
 const int8_t *xtx_slices(Ctx &c, const double *d_X, int n, int ns);
 void xtx_int8_tiles(Ctx &c, const int8_t *sl, int n, int ns, double *d_S, int tc0, int tc1);   // 64-col tiles
 // cm / csd given: the correlation epilogue in the store (d_S receives cor)
 void xtx_int8_tiles128(Ctx &c, const int8_t *sl, int n, int ns, double *d_S, int tc0, int tc1,
                        const double *cm = nullptr, const double *csd = nullptr);
+// columns [c0, c1) only, into d_slab (ld n, column c0 first): the C5 row-sharded C
+void xtx_int8_slab128(Ctx &c, const int8_t *sl, int n, int ns, double *d_slab, int c0, int c1,
+                      const double *cm = nullptr, const double *csd = nullptr);
 int xtx_kp(int n);
 int8_t *xtx_slice_buf(Ctx &c, int n, int ns);
 int xtx_int_slices_cols(Ctx &c, const double *d_cmax, const int *d_cbad, int n);
@@ -321,8 +334,17 @@ struct GatherStats {
     const long long *css;
     bool slices2;   // the gather wrote the 2-slice int8 image
 };
+// C5 row-sharded C (one matrix over R ranks on the Krylov path): shard r owns
+// columns [rb[r], rb[r+1]) of [C | m | 1] (rb: rows_gemm_sharded's row plan
+// over n + 2); narrow: d_C holds only this rank's columns (column rb[rank]
+// first), else all of them (virtual shards)
+struct CorSlab {
+    int ns = 0;
+    std::vector<int> rb;
+    bool narrow = false;
+};
 void cor_product(Ctx &c, const double *d_X, int n, const double *d_m, const GatherStats *gs, double *d_S,
-                 double *d_C, double *d_sd, double *d_cmean);
+                 double *d_C, double *d_sd, double *d_cmean, const CorSlab *slab = nullptr);
 // S = X'X by the exact int8 path when possible, sharded like sym_gemm_sharded
 void xtx_product(Ctx &c, const double *d_X, int n, double *d_S);
 
@@ -333,11 +355,21 @@ struct PcaStats {
 };
 extern int g_pca_krylov_min, g_pca_krylov_block, g_pca_krylov_steps, g_pca_over;
 extern int g_pca_cheb_fused;   // Krylov small problem: Chebyshev step in the T Y reduction (default 1)
+extern int g_pca_ckrylov;      // 1: block Krylov in C (tp_krylov.hip), 0: in G (tp_pca.hip)
+extern int g_ckry_chunk;       // rows per Z partial of the C-Krylov orthogonalisation
+extern int g_ckry_steps;       // C-Krylov blocks before the first check (0: from k and n)
+// the top k eigenpairs of a D x D projected matrix (tp_pca.hip)
+void small_topk_T(Ctx &c, double *Tm, int D, int k, double *Vs, std::vector<double> &h_theta, PcaStats &sst);
+// false: an orthogonalisation pass broke down (the caller takes the G path)
+bool krylov_c_topk(Ctx &c, double *C, int c_col0, const double *mext, int n, int k, double *V, double *P,
+                   std::vector<double> &h_theta, PcaStats &st);
 // d_C: n x n, with room for 2n more doubles after it (the Krylov path writes
 // m = colMeans(C) and a column of ones there); d_cmean: C's column means if the
 // caller already has them (may be d_C + n n), else computed here
 inline size_t pca_c_doubles(int n) { return (size_t)n * n + 2 * (size_t)n; }
+// c_col0 / c_col1: d_C holds only columns [c_col0, c_col1) of [C | m | 1] (a
+// C5 rank's slab, Krylov path; -1: all of them, with room for the two extra)
 PcaStats pca_dev(Ctx &c, double *d_C, int n, int k, double *d_P, double *d_Pt,
-                 double *h_sdev, const double *d_cmean = nullptr);
+                 double *h_sdev, const double *d_cmean = nullptr, int c_col0 = 0, int c_col1 = -1);
 
 }  // namespace tp

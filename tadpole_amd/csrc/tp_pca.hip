@@ -183,7 +183,7 @@ static void subspace_topk(Ctx &c, const double *A, int n, int k, const Prod &pro
         TP_HIP(hipGetLastError());
         h_theta.resize(n);
         TP_HIP(hipMemcpyAsync(h_theta.data(), theta, n * sizeof(double), hipMemcpyDeviceToHost, s));
-        TP_HIP(hipStreamSynchronize(s));
+        stream_sync(c, s);
         trace_mark(s, "pca: exact eig");
         st.iters = 0;
         st.resid = 0.0;
@@ -265,7 +265,7 @@ static void subspace_topk(Ctx &c, const double *A, int n, int k, const Prod &pro
         std::vector<double> dg(b);
         hipLaunchKernelGGL(k_diag, dim3((b + 255) / 256), dim3(256), 0, s, Wsm, b, resid);
         TP_HIP(hipMemcpyAsync(dg.data(), resid, b * sizeof(double), hipMemcpyDeviceToHost, s));
-        TP_HIP(hipStreamSynchronize(s));
+        stream_sync(c, s);
         for (double &x : dg) x = std::sqrt(x);
         const double l1 = dg[0], lk = dg[k - 1], lb = dg[b - 1];
         cut = lb;
@@ -347,7 +347,7 @@ static void subspace_topk(Ctx &c, const double *A, int n, int k, const Prod &pro
         TP_HIP(hipGetLastError());
         TP_HIP(hipMemcpyAsync(h_res.data(), resid, k * sizeof(double), hipMemcpyDeviceToHost, s));
         TP_HIP(hipMemcpyAsync(h_theta.data(), theta, b * sizeof(double), hipMemcpyDeviceToHost, s));
-        TP_HIP(hipStreamSynchronize(s));
+        stream_sync(c, s);
         const double th1 = std::fabs(h_theta[b - 1]);
         double worst = 0.0;
         for (int j = 0; j < k; ++j) worst = std::max(worst, h_res[j] / (th1 > 0 ? th1 : 1.0));
@@ -385,14 +385,42 @@ static void subspace_topk(Ctx &c, const double *A, int n, int k, const Prod &pro
     TP_HIP(hipMemcpyAsync(V, Q, (size_t)n * k * sizeof(double), hipMemcpyDeviceToDevice, s));
 }
 
+// The projected problem of the Krylov paths: the top k eigenpairs of T (D x
+// D, symmetric, ld D) by the subspace iteration above (products with T are
+// D x D GEMMs, the Chebyshev step in their split-K reduction).  Vs: D x k.
+void small_topk_T(Ctx &c, double *Tm, int D, int k, double *Vs, std::vector<double> &h_theta, PcaStats &sst) {
+    hipStream_t s = c.cur;
+    Prod tprod = [&](const double *Y, double *Out) {
+        GemmArgs g{D, sst.block, D, Tm, D, true, Y, D, Out, D};
+        g.splitk = 0;
+        gemm_f64(g, c.buf[S_PARTIAL], s);
+    };
+    ProdAff taff = [&](const double *Y, double *Out, double a, double b, const double *Yc, double cc,
+                       const double *Yp) {
+        GemmArgs g{D, sst.block, D, Tm, D, true, Y, D, Out, D};
+        g.splitk = 0;
+        g.affine = true;
+        g.af_a = a;
+        g.af_b = b;
+        g.af_y = Yc;
+        g.af_c = cc;
+        g.af_z = Yp;
+        gemm_f64(g, c.buf[S_PARTIAL], s);
+    };
+    // +2 planned degrees: a product with T costs ~1.5 % of a Rayleigh-Ritz
+    // round (one-workgroup tridiagonalisation) that a near miss of the
+    // residual check would add
+    subspace_topk(c, Tm, D, k, tprod, Vs, h_theta, sst, 0x5EEDULL + (uint64_t)D, 2, g_pca_cheb_fused ? &taff : nullptr);
+}
+
 // Block Krylov path (see the file comment): V (n x k) = top-k eigenvectors of
 // G = Xc'Xc without forming G, or Xc: C is symmetric, so with m = colMeans(C)
 // Xc K = C K - 1 (m'K) and Xc'Y = C Y - m (1'Y) -- both products stream C
 // itself and the centring is two rank-1 corrections of an n x p block.
 // Blocks K_t (n x p) in S_KRY, G K_t in S_KRYG, T = K'GK in S_KRYT, the small
 // problem's vectors in S_KRYV.
-static void krylov_topk(Ctx &c, double *C, int n, int k, double *V, double *P, std::vector<double> &h_theta,
-                        PcaStats &st) {
+static void krylov_topk(Ctx &c, double *C, int c_col0, const double *mext, int n, int k, double *V, double *P,
+                        std::vector<double> &h_theta, PcaStats &st) {
     hipStream_t s = c.cur;
     const int p = g_pca_krylov_block > 0 ? g_pca_krylov_block : (k >= 128 ? 64 : 32);
     // D ~ 5k columns; denser spectra of larger matrices need more (C5 arms:
@@ -454,11 +482,11 @@ static void krylov_topk(Ctx &c, double *C, int n, int k, double *V, double *P, s
             // so each centring correction rides in the product's reduction
             kprof_begin(c, K_GQ_GEMM);
             const R1 r_xk{n, nullptr, n};        // Xc K_t = C K_t - 1 (m'K_t)
-            rows_gemm_sharded(c, C, n, n + 2, Kt, n, p, n, XKt, 0, 1, &r_xk);
+            rows_gemm_sharded(c, C, n, n + 2, Kt, n, p, n, XKt, 0, 1, &r_xk, c_col0);
             kprof_end(c, K_GQ_GEMM);
             kprof_begin(c, K_GQ_GEMM);
-            const R1 r_gk{n + 1, C + (size_t)n * n, n};   // Xc'(Xc K_t) = C (Xc K_t) - m (1'Xc K_t)
-            rows_gemm_sharded(c, C, n, n + 2, XKt, n, p, n, GKt, 0, 1, &r_gk);
+            const R1 r_gk{n + 1, mext, n};   // Xc'(Xc K_t) = C (Xc K_t) - m (1'Xc K_t)
+            rows_gemm_sharded(c, C, n, n + 2, XKt, n, p, n, GKt, 0, 1, &r_gk, c_col0);
             kprof_end(c, K_GQ_GEMM);
         }
         built = std::max(built, upto);
@@ -476,27 +504,7 @@ static void krylov_topk(Ctx &c, double *C, int n, int k, double *V, double *P, s
         gemm_f64(tg, c.buf[S_PARTIAL], s);
         double *Vs = c.buf[S_KRYV].as<double>((size_t)D * k);
         PcaStats sst;
-        Prod tprod = [&](const double *Y, double *Out) {
-            GemmArgs g{D, sst.block, D, Tm, D, true, Y, D, Out, D};
-            g.splitk = 0;
-            gemm_f64(g, c.buf[S_PARTIAL], s);
-        };
-        ProdAff taff = [&](const double *Y, double *Out, double a, double b, const double *Yc, double cc,
-                           const double *Yp) {
-            GemmArgs g{D, sst.block, D, Tm, D, true, Y, D, Out, D};
-            g.splitk = 0;
-            g.affine = true;
-            g.af_a = a;
-            g.af_b = b;
-            g.af_y = Yc;
-            g.af_c = cc;
-            g.af_z = Yp;
-            gemm_f64(g, c.buf[S_PARTIAL], s);
-        };
-        // +2 planned degrees: a product with T costs ~1.5 % of a Rayleigh-Ritz
-        // round (one-workgroup tridiagonalisation) that a near miss of the
-        // residual check would add
-        subspace_topk(c, Tm, D, k, tprod, Vs, h_theta, sst, 0x5EEDULL + (uint64_t)D, 2, g_pca_cheb_fused ? &taff : nullptr);
+        small_topk_T(c, Tm, D, k, Vs, h_theta, sst);
         // V = K Y, G V = (G K) Y; residuals in the n-dimensional space
         GemmArgs vg{n, k, D, K, n, false, Vs, D, V, n};
         vg.splitk = 0;
@@ -512,7 +520,7 @@ static void krylov_topk(Ctx &c, double *C, int n, int k, double *V, double *P, s
         hipLaunchKernelGGL(k_resid, dim3((k + 3) / 4), dim3(256), 0, s, GV, V, dth, n, bs, k, resid);
         TP_HIP(hipGetLastError());
         TP_HIP(hipMemcpyAsync(h_res.data(), resid, k * sizeof(double), hipMemcpyDeviceToHost, s));
-        TP_HIP(hipStreamSynchronize(s));
+        stream_sync(c, s);
         const double th1 = std::fabs(h_theta[bs - 1]);
         double worst = 0.0;
         for (int j = 0; j < k; ++j) worst = std::max(worst, h_res[j] / (th1 > 0 ? th1 : 1.0));
@@ -538,7 +546,7 @@ static void krylov_topk(Ctx &c, double *C, int n, int k, double *V, double *P, s
 }
 
 PcaStats pca_dev(Ctx &c, double *d_C, int n, int k, double *d_P, double *d_Pt, double *h_sdev,
-                 const double *d_cmean) {
+                 const double *d_cmean, int c_col0, int c_col1) {
     PcaStats st;
     hipStream_t s = c.cur;
     const double *mean = d_cmean;
@@ -552,13 +560,26 @@ PcaStats pca_dev(Ctx &c, double *d_C, int n, int k, double *d_P, double *d_Pt, d
     const int b_est = std::min(n, ((k + std::max(32, k / 4) + 31) / 32) * 32);
     const bool krylov = n >= g_pca_krylov_min && b_est < n;
     double *Xc = nullptr, *XcT = nullptr;
+    if (c_col0 != 0 && !krylov) fail(TP_ERR_ARG, "pca_dev: a column slab of C needs the Krylov path");
     if (krylov) {
-        // C's two extra columns: m (the centring) and ones
-        double *ext = d_C + (size_t)n * n;
-        if (mean != ext) TP_HIP(hipMemcpyAsync(ext, mean, (size_t)n * sizeof(double), hipMemcpyDeviceToDevice, s));
-        hipLaunchKernelGGL(k_fill_const, dim3((n + 255) / 256), dim3(256), 0, s, ext + n, n, 1.0);
+        // [m | 1] (the centring's rank-1 terms) for every rank, and as columns
+        // n, n + 1 of [C | m | 1] (the products' extra rows m'B, 1'B) where
+        // this rank holds them (all of C, or the last rank's slab)
+        double *mext = c.buf[S_MEXT].as<double>(2 * (size_t)n);
+        if (mean != mext) TP_HIP(hipMemcpyAsync(mext, mean, (size_t)n * sizeof(double), hipMemcpyDeviceToDevice, s));
+        hipLaunchKernelGGL(k_fill_const, dim3((n + 255) / 256), dim3(256), 0, s, mext + n, n, 1.0);
         TP_HIP(hipGetLastError());
-        krylov_topk(c, d_C, n, k, V, d_P, h_theta, st);   // neither Xc nor XcT is formed
+        const int cend = c_col1 < 0 ? n + 2 : c_col1;
+        if (c_col0 <= n && cend >= n + 2)
+            TP_HIP(hipMemcpyAsync(d_C + (size_t)(n - c_col0) * n, mext, 2 * (size_t)n * sizeof(double),
+                                  hipMemcpyDeviceToDevice, s));
+        // neither Xc nor XcT is formed; the Krylov space of C (tp_krylov.hip),
+        // or of G when an orthogonalisation pass of that path breaks down
+        if (!g_pca_ckrylov || !krylov_c_topk(c, d_C, c_col0, mext, n, k, V, d_P, h_theta, st)) {
+            h_theta.clear();
+            st = PcaStats{};
+            krylov_topk(c, d_C, c_col0, mext, n, k, V, d_P, h_theta, st);
+        }
     } else {
         Xc = c.buf[S_XC].as<double>((size_t)n * n);
         XcT = c.buf[S_XCT].as<double>((size_t)n * n);

@@ -327,10 +327,10 @@ void launch_cor_sd_ss(const long long *d_css, const double *d_m, int n, double *
     TP_HIP(hipGetLastError());
 }
 
-__global__ void __launch_bounds__(256) k_colmean(const double *A, int n, int ld, double *cm) {
+__global__ void __launch_bounds__(256) k_colmean(const double *A, int n, int ncols, int ld, double *cm) {
     int lane = threadIdx.x & 63;
     int j = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (j >= n) return;
+    if (j >= ncols) return;
     const double *src = A + (size_t)j * ld;
     double hi = 0.0, lo = 0.0;
     dd_col_acc<8>(src, n, lane, hi, lo);
@@ -339,7 +339,12 @@ __global__ void __launch_bounds__(256) k_colmean(const double *A, int n, int ld,
 }
 
 void launch_colmean(const double *d_A, int n, int ld, double *d_mean, hipStream_t s) {
-    hipLaunchKernelGGL(k_colmean, dim3((n + 3) / 4), dim3(256), 0, s, d_A, n, ld, d_mean);
+    launch_colmean_cols(d_A, n, n, ld, d_mean, s);
+}
+// means of ncols columns of n rows (a column slab of C): the same per-column bits
+void launch_colmean_cols(const double *d_A, int n, int ncols, int ld, double *d_mean, hipStream_t s) {
+    if (ncols <= 0) return;
+    hipLaunchKernelGGL(k_colmean, dim3((ncols + 3) / 4), dim3(256), 0, s, d_A, n, ncols, ld, d_mean);
     TP_HIP(hipGetLastError());
 }
 

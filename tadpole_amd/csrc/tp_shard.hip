@@ -27,8 +27,10 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <rccl/rccl.h>
@@ -48,6 +50,8 @@ struct Rccl {
     decltype(&ncclGroupStart) gstart = nullptr;
     decltype(&ncclGroupEnd) gend = nullptr;
     decltype(&ncclGetErrorString) errstr = nullptr;
+    decltype(&ncclCommAbort) abort = nullptr;
+    decltype(&ncclCommGetAsyncError) async_err = nullptr;
 };
 static Rccl g_rccl;
 
@@ -68,6 +72,8 @@ static Rccl &rccl() {
     TP_SYM(gstart, "ncclGroupStart")
     TP_SYM(gend, "ncclGroupEnd")
     TP_SYM(errstr, "ncclGetErrorString")
+    TP_SYM(abort, "ncclCommAbort")
+    TP_SYM(async_err, "ncclCommGetAsyncError")
 #undef TP_SYM
     g_rccl = r;
     return g_rccl;
@@ -105,6 +111,58 @@ void comm_destroy(Ctx &c) {
     c.shard.comm = nullptr;
     c.shard.rank = 0;
     c.shard.nranks = 1;
+}
+
+// ------------------------------------------------- failure containment
+// A rank that fails inside a sharded call leaves its peers waiting in a
+// collective.  Sharded calls therefore never block in hipStreamSynchronize:
+// stream_sync polls the stream, the communicator's asynchronous error and a
+// deadline (TP_SHARD_TIMEOUT_S, default 300 s), and on either aborts the
+// communicator (ncclCommAbort) and fails the call; a rank whose own host code
+// throws aborts it too (comm_abort from the pipeline's scope guard).  Peers
+// then leave their collectives through their own deadline instead of hanging.
+static double shard_timeout_s() {
+    static const double v = [] {
+        const char *e = getenv("TP_SHARD_TIMEOUT_S");
+        const double x = e ? atof(e) : 300.0;
+        return x > 0 ? x : 300.0;
+    }();
+    return v;
+}
+
+void comm_abort(Ctx &c) {
+    if (!c.shard.comm) return;
+    (void)rccl().abort((ncclComm_t)c.shard.comm);
+    c.shard.comm = nullptr;
+    c.shard.rank = 0;
+    c.shard.nranks = 1;
+}
+
+void stream_sync(Ctx &c, hipStream_t s) {
+    if (!(c.shard.active && c.shard.comm)) {
+        TP_HIP(hipStreamSynchronize(s));
+        return;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const hipError_t e = hipStreamQuery(s);
+        if (e == hipSuccess) return;
+        if (e != hipErrorNotReady) {
+            comm_abort(c);
+            TP_HIP(e);
+        }
+        ncclResult_t ae = ncclSuccess;
+        if (rccl().async_err((ncclComm_t)c.shard.comm, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
+            comm_abort(c);
+            fail(TP_ERR_HIP, std::string("RCCL asynchronous error in a sharded call: ") + rccl().errstr(ae) +
+                                 " (communicator aborted)");
+        }
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > shard_timeout_s()) {
+            comm_abort(c);
+            fail(TP_ERR_HIP, "sharded call timed out waiting for its peers (TP_SHARD_TIMEOUT_S); communicator aborted");
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
 }
 
 // -------------------------------------------------------------- planning
@@ -249,11 +307,36 @@ void xtx_product(Ctx &c, const double *X, int n, double *S) {
     launch_clean_symmetrize(S, n, true, c.cur);
 }
 
-int g_xtx_fused = 1;   // 0: X'X into S, then the separate correlation epilogue (A/B, tests)
+int g_xtx_fused = 1;
+int g_shard_slab = 1;   // 0: X'X into S, then the separate correlation epilogue (A/B, tests)
 
 void cor_product(Ctx &c, const double *X, int n, const double *m, const GatherStats *gs, double *S, double *C,
-                 double *sd, double *cmean) {
+                 double *sd, double *cmean, const CorSlab *slab) {
     hipStream_t s = c.cur;
+    if (slab) {
+        // C5 row-sharded C: each shard computes only its columns (the tiles of
+        // xtx_int8_slab128: same tiles and arithmetic, so the same bits) and
+        // their means; the n means are gathered, C itself never is
+        if (!gs || !gs->slices2 || !cmean || !(slab->ns == 1 || slab->ns == 2))
+            fail(TP_ERR_ARG, "cor_product: the column slab needs the gather's int8 image and the means buffer");
+        c.last_xtx_ns = slab->ns;
+        const int8_t *sl = xtx_slice_buf(c, n, 2);
+        launch_cor_sd_ss(gs->css, m, n, sd, s);
+        const int R = (int)slab->rb.size() - 1;
+        kprof_begin(c, K_COR_GEMM);
+        for (int r = 0; r < R; ++r) {
+            if (!shard_mine(c, r)) continue;
+            const int c0 = std::min(n, slab->rb[r]), c1 = std::min(n, slab->rb[r + 1]);
+            double *dst = slab->narrow ? C : C + (size_t)c0 * n;
+            xtx_int8_slab128(c, sl, n, slab->ns, dst, c0, c1, m, sd);
+            launch_colmean_cols(dst, n, c1 - c0, n, cmean + c0, s);
+        }
+        kprof_end(c, K_COR_GEMM);
+        std::vector<size_t> off(R + 1);
+        for (int r = 0; r <= R; ++r) off[r] = (size_t)std::min(n, slab->rb[r]);
+        shard_gather(c, cmean, off);
+        return;
+    }
     int ns = -1;
     if (gs && g_xtx_fused && n >= 1024) ns = xtx_int_slices_cols(c, gs->cmax, gs->cbad, n);
     if (!(ns == 1 || ns == 2)) {
@@ -291,8 +374,9 @@ void cor_product(Ctx &c, const double *X, int n, const double *m, const GatherSt
 // B K x N: rows of Out split in 64-row blocks, each written transposed into
 // the packed T (N x M col-major = Out row-major), gathered, transposed back.
 void rows_gemm_sharded(Ctx &c, const double *A, int lda, int M, const double *B, int ldb, int N, int K,
-                       double *Out, int splitk_plain, int tag, const R1 *r1) {
+                       double *Out, int splitk_plain, int tag, const R1 *r1, int a_col0) {
     if (!c.shard.active) {
+        if (a_col0 != 0) fail(TP_ERR_ARG, "rows_gemm_sharded: a column slab needs the sharded schedule");
         const bool fused = r1 && rows_ts(K, N) && splitk_plain <= 1;   // the epilogue rides in the reduction
         double *dst = (r1 && !fused) ? c.buf[S_SHARD].as<double>((size_t)M * N) : Out;
         GemmArgs g{M, N, K, A, lda, true, B, ldb, dst, fused ? r1->rows : M};
@@ -314,7 +398,9 @@ void rows_gemm_sharded(Ctx &c, const double *A, int lda, int M, const double *B,
     double *T = c.buf[S_SHARD].as<double>((size_t)M * N);
     for (int r = 0; r < R; ++r) {
         if (!shard_mine(c, r) || rb[r + 1] <= rb[r]) continue;
-        GemmArgs g{rb[r + 1] - rb[r], N, K, A + (size_t)rb[r] * lda, lda, true, B, ldb, T + (size_t)rb[r] * N, N};
+        if (rb[r] < a_col0) fail(TP_ERR_ARG, "rows_gemm_sharded: shard rows outside this rank's slab");
+        GemmArgs g{rb[r + 1] - rb[r], N, K, A + (size_t)(rb[r] - a_col0) * lda, lda, true, B, ldb,
+                   T + (size_t)rb[r] * N, N};
         g.store_t = true;
         // long-K products (128 x 64 kernel): k chunks fixed by K, the same bits
         // as unsharded; otherwise no split (chunks would follow the shard's tiles)

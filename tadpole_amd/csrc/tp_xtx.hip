@@ -23,6 +23,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <vector>
 
 namespace tp {
 
@@ -208,14 +209,24 @@ __device__ __forceinline__ void xtx_supertile(int L, int tn, int &bm, int &bn) {
 // COR: the sparse_cor epilogue (R/TADpole.R:96-98,449) applied to each exact
 // S_ij before the store -- C holds cor, with k_cor_epilogue's arithmetic (same
 // bits), and S is never written or re-read.  m: column means, sd: sqrt(cov_jj).
+// Column slab (tiles != nullptr, C5 row-sharded C): workgroup b computes the
+// upper tile tiles[b] and stores only the elements whose column lies in
+// [c0, c1), at C[row + (col - c0) n] -- the same tiles and arithmetic as the
+// whole matrix, so a slab holds exactly those columns' bits.
 template <int NS, bool COR = false>
 __global__ void __launch_bounds__(512) k_xtx_i8_big(const int8_t *__restrict__ S, int n, int Kp, int Np,
                                                     double *__restrict__ C, int tcol0, int tn_all,
                                                     const double *__restrict__ cm = nullptr,
-                                                    const double *__restrict__ csd = nullptr) {
+                                                    const double *__restrict__ csd = nullptr,
+                                                    const int2 *__restrict__ tiles = nullptr, int c0 = 0,
+                                                    int c1 = 0x7fffffff) {
     __shared__ __attribute__((aligned(16))) int8_t Ls[2][2][NS][XB * XLD];   // [buf][A/B][slice]
     int bm, bn;
-    if (tn_all > 0) {
+    if (tiles) {
+        const int2 tl = tiles[blockIdx.x];
+        bm = tl.x;
+        bn = tl.y;
+    } else if (tn_all > 0) {
         const int total = tn_all * (tn_all + 1) / 2;
         const int xcd = (int)blockIdx.x & 7, slot = (int)blockIdx.x >> 3;
         xtx_supertile(xcd * (total >> 3) + min(xcd, total & 7) + slot, tn_all, bm, bn);
@@ -338,8 +349,8 @@ __global__ void __launch_bounds__(512) k_xtx_i8_big(const int8_t *__restrict__ S
                     d = cij / (pm[256 + il] * pm[384 + jl]);
                     if (isnan(d)) d = 0.0;
                 }
-                C[(size_t)i + (size_t)j * n] = d;
-                C[(size_t)j + (size_t)i * n] = d;
+                if (j >= c0 && j < c1) C[(size_t)i + (size_t)(j - c0) * n] = d;
+                if (i >= c0 && i < c1) C[(size_t)j + (size_t)(i - c0) * n] = d;
             }
 }
 
@@ -373,7 +384,7 @@ static int slices_for(Ctx &c, unsigned long long *mb) {
     unsigned long long h[2] = {0, 0};
     unsigned long long *ph = (unsigned long long *)c.pinned(16);   // pinned: no staged copy
     TP_HIP(hipMemcpyAsync(ph, mb, 16, hipMemcpyDeviceToHost, c.cur));
-    TP_HIP(hipStreamSynchronize(c.cur));
+    stream_sync(c, c.cur);
     memcpy(h, ph, 16);
     if ((int)h[1]) return 0;
     double mx;
@@ -459,6 +470,42 @@ void xtx_int8_tiles128(Ctx &c, const int8_t *sl, int n, int ns, double *d_S, int
                            csd);
     else fail(TP_ERR_ARG, "xtx_int8_tiles128: 1..2 slices");
     TP_HIP(hipGetLastError());
+}
+
+// Columns [c0, c1) of S (or of cor with cm / csd) into d_slab (ld n, column c0
+// first): every upper 128-tile that holds an element of those columns or of
+// their mirror rows -- (P, Q) with Q in the slab's tile columns, or P in them
+// and Q past them.
+void xtx_int8_slab128(Ctx &c, const int8_t *sl, int n, int ns, double *d_slab, int c0, int c1, const double *cm,
+                      const double *csd) {
+    if (c1 <= c0) return;
+    const int Kp = xtx_kp(n), Np = (n + 127) / 128 * 128;
+    const int tn = Np / 128, T0 = c0 / 128, T1 = (c1 + 127) / 128;
+    std::vector<int2> tl;
+    for (int q = T0; q < T1; ++q)
+        for (int p = 0; p <= q; ++p) tl.push_back(make_int2(p, q));
+    for (int p = T0; p < T1; ++p)
+        for (int q = T1; q < tn; ++q) tl.push_back(make_int2(p, q));
+    int2 *d_tl = c.buf[S_XTXT].as<int2>(tl.size());
+    TP_HIP(hipMemcpyAsync(d_tl, tl.data(), tl.size() * sizeof(int2), hipMemcpyHostToDevice, c.cur));
+    const unsigned nb = (unsigned)tl.size();
+    const bool cor = cm != nullptr;
+    if (ns == 1 && !cor)
+        hipLaunchKernelGGL((k_xtx_i8_big<1>), dim3(nb), dim3(512), 0, c.cur, sl, n, Kp, Np, d_slab, 0, 0, cm, csd, d_tl,
+                           c0, c1);
+    else if (ns == 2 && !cor)
+        hipLaunchKernelGGL((k_xtx_i8_big<2>), dim3(nb), dim3(512), 0, c.cur, sl, n, Kp, Np, d_slab, 0, 0, cm, csd, d_tl,
+                           c0, c1);
+    else if (ns == 1)
+        hipLaunchKernelGGL((k_xtx_i8_big<1, true>), dim3(nb), dim3(512), 0, c.cur, sl, n, Kp, Np, d_slab, 0, 0, cm, csd,
+                           d_tl, c0, c1);
+    else if (ns == 2)
+        hipLaunchKernelGGL((k_xtx_i8_big<2, true>), dim3(nb), dim3(512), 0, c.cur, sl, n, Kp, Np, d_slab, 0, 0, cm, csd,
+                           d_tl, c0, c1);
+    else fail(TP_ERR_ARG, "xtx_int8_slab128: 1..2 slices");
+    TP_HIP(hipGetLastError());
+    // the host tile list must outlive the asynchronous copy
+    stream_sync(c, c.cur);
 }
 
 void xtx_int8_tiles(Ctx &c, const int8_t *sl, int n, int ns, double *d_S, int tc0, int tc1) {

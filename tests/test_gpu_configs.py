@@ -77,11 +77,12 @@ def test_config_c3_from_hbm(gpu):
     _check(got, z)
 
 
-@pytest.mark.parametrize("forced", [True, False])
-def test_pca_krylov_path_vs_lapack(gpu, forced):
-    """The block Krylov PCA (G never formed) against LAPACK's SVD on a matrix
-    below its default size threshold (forced) and the G path on the same
-    matrix: every prefix subspace the sweep uses agrees."""
+@pytest.mark.parametrize("forced,space", [(True, "C"), (True, "G"), (False, "C")])
+def test_pca_krylov_path_vs_lapack(gpu, forced, space):
+    """The block Krylov PCA (G never formed; Krylov space of C, the default,
+    or of G: knob 20) against LAPACK's SVD on a matrix below its default size
+    threshold (forced) and the G-formed path on the same matrix: every prefix
+    subspace the sweep uses agrees."""
     n0 = 2600
     m = synth_hic(n0, SEED_BASE + 77)
     cm = O.clean_symmetrize(m)
@@ -89,10 +90,12 @@ def test_pca_krylov_path_vs_lapack(gpu, forced):
     g = np.flatnonzero(~obad)
     c = O.sparse_cor(cm[np.ix_(g, g)])
     old = G.knob(8, 0 if forced else 1 << 30)
+    old20 = G.knob(20, 1 if space == "C" else 0)
     try:
         p, _ = G.pca(c, 200)
     finally:
         G.knob(8, old)
+        G.knob(20, old20)
     op = O.prcomp_x(c, 200)
     s = np.sign(np.sum(p * op, axis=0))
     s[s == 0] = 1
@@ -109,15 +112,19 @@ def test_pca_krylov_path_vs_lapack(gpu, forced):
         assert np.abs(proj(p, i) - proj(op, i)).max() < 1e-7, i
 
 
-def test_pipeline_krylov_forced_end_to_end(gpu):
-    """A whole TADpole() through the Krylov PCA at a size the oracle runs live."""
+@pytest.mark.parametrize("space", ["C", "G"])
+def test_pipeline_krylov_forced_end_to_end(gpu, space):
+    """A whole TADpole() through the Krylov PCA (in C or in G) at a size the
+    oracle runs live."""
     import tadpole_amd as tp
     m = synth_hic(2400, SEED_BASE + 78)
     old = G.knob(8, 0)
+    old20 = G.knob(20, 1 if space == "C" else 0)
     try:
         got = tp.TADpole(m, max_pcs=200)
     finally:
         G.knob(8, old)
+        G.knob(20, old20)
     assert got.timings_ms[16] > 0          # the Krylov path ran
     ref = O.tadpole(m, max_pcs=200)
     assert (got.n_pcs, got.optimal_n_clusters) == (ref.n_pcs, ref.optimal_n_clusters)

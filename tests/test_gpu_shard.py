@@ -45,6 +45,36 @@ def test_virtual_shards_bit_identical(gpu, n0, seed):
         _same(tp.TADpole(m, max_pcs=200), ref)
 
 
+def test_virtual_shards_row_sharded_c(gpu):
+    """C5's row-sharded C (knob 24, default): on the Krylov path each shard
+    computes only its columns of C (the int8 X'X tiles that touch them) and
+    their means, and the Krylov products read only those columns -- C is never
+    gathered.  Bit-identical to the gathered schedule (knob 24 = 0) and to one
+    shard, for both Krylov spaces (knob 20)."""
+    import gpu_helpers as G
+    m = synth_hic(2600, 35)
+    old8 = G.knob(8, 0)            # the Krylov path at this size
+    try:
+        for space in (0, 1):
+            old20 = G.knob(20, space)
+            try:
+                multi.set_virtual_shards(1)
+                ref = tp.TADpole(m, max_pcs=160, sharded=True)
+                assert ref.timings_ms[16] > 0
+                for slab in (1, 0):
+                    old24 = G.knob(24, slab)
+                    try:
+                        multi.set_virtual_shards(3)
+                        _same(tp.TADpole(m, max_pcs=160, sharded=True), ref)
+                    finally:
+                        G.knob(24, old24)
+            finally:
+                G.knob(20, old20)
+                multi.set_virtual_shards(1)
+    finally:
+        G.knob(8, old8)
+
+
 def test_virtual_shards_centromere_arms(gpu):
     m = synth_hic(700, 33, centromere=True)
     try:
