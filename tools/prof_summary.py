@@ -22,7 +22,7 @@ OUT = os.path.join(ROOT, "gpurun_out")
 # runs; per prefix the variant with the largest total time in the trace is taken
 # (the CONISS block size and the GEMM tile are chosen per problem size)
 CLASSES = {"coniss": ["tp::k_coniss_t<false,"],
-           "ch": ["tp::k_ch_cut", "tp::k_ch_segstat", "tp::k_ch("],
+           "ch": ["tp::k_ch_cut", "tp::k_ch_segstat", "tp::k_ch<"],
            "xtx_gemm": ["tp::k_xtx_i8_big<"]}
 
 
