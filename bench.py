@@ -35,7 +35,9 @@ North-star lines (same JSON object, after the C3 headline; --no-extras skips):
 
 Extra fields: "roofline" for the kernel class with the largest time per
 pipeline (HIP events recorded inside the library on the stream the kernels run
-on, averaged over the timed steps), "cpu_baseline" (the CPU oracle on this
+on, averaged over the timed steps; the Krylov products' class, 32 launches a
+pipeline, from a few untimed pipelines after them, since an event per launch
+costs ~0.4 ms a pipeline), "cpu_baseline" (the CPU oracle on this
 host, rank 0, N=1), "parity" (rank 0's result vs the committed oracle fixture
 and vs the CPU oracle run on the same matrix).
 """
@@ -407,8 +409,18 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
+    def fine_events(on):
+        """knob 25: HIP events around every Krylov product (off in the timed
+        region: each hipEventRecord opens a few-us gap on the stream, ~0.4 ms
+        over a pipeline's 32 products)."""
+        old, st = I(0), I(0)
+        L.tp_debug_knob(ctypes.byref(I(25)), ctypes.byref(I(1 if on else 0)), ctypes.byref(old), ctypes.byref(st))
+        _lib.check(st)
+
     # ---- timed region: K pipelines, one after another, on one stream; the
-    # library records HIP events per kernel class on that stream
+    # library records HIP events per stage and around its one-launch kernel
+    # classes (int8 X'X, CONISS, CH) on that stream
+    fine_events(False)
     tms = []
     barrier()
     host_t.update(call=0.0, assemble=0.0, n=0)
@@ -423,12 +435,19 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    host_call = dict(host_t)
     tm = np.mean(np.stack(tms), axis=0)
+    # the Krylov products' class (32 launches a pipeline) from separate
+    # untimed pipelines with their events on
+    fine_events(True)
+    tmf = np.mean(np.stack([step(lane0).timings_ms for _ in range(max(2, min(5, args.steps)))]), axis=0)
+    torch.cuda.synchronize()
+    tm[7], tm[8] = tmf[7], tmf[8]
     n, k = int(tm[14]), int(tm[15])
-    nh = max(1, host_t["n"])
-    host_ms = {"c_call": round(host_t["call"] / nh * 1e3, 3), "device_stages": round(float(tm[4]), 3),
-               "c_call_minus_device": round(host_t["call"] / nh * 1e3 - float(tm[4]), 3),
-               "python_assembly": round(host_t["assemble"] / nh * 1e3, 3)}
+    nh = max(1, host_call["n"])
+    host_ms = {"c_call": round(host_call["call"] / nh * 1e3, 3), "device_stages": round(float(tm[4]), 3),
+               "c_call_minus_device": round(host_call["call"] / nh * 1e3 - float(tm[4]), 3),
+               "python_assembly": round(host_call["assemble"] / nh * 1e3, 3)}
 
     # ---- throughput with S matrices in flight (not `value`)
     thr = None

@@ -208,6 +208,18 @@ void tp_pipeline_dev(const double *d_M, const int *n0, const int *max_pcs,
                      int *merge, double *height, int *boundary,
                      double *timings_ms, int *status);
 
+/* ------------------------------------------------------------ tad coords */
+/* The TAD start/end coordinates of several cut levels of the final tree at
+ * once: R/TADpole.R:470-488 (cutree(dendro, kk) per significant level, the
+ * labels placed on c(good, bad) order, rle runs -> rows (start, end)).
+ * boundary[n-1]: as tp_pipeline returns it (first n_good-1 entries, n =
+ * n_good), pos[n]: the 1-based coordinate of each kept bin in the full
+ * matrix, levels[nlev]: each in 1..n.  out: sum(levels) rows of two int64
+ * (start, end), row-major, level after level in `levels` order.  Host only. */
+void tp_level_coords(const int *boundary, const int *n, const int *levels,
+                     const int *nlev, const long long *pos, long long *out,
+                     int *status);
+
 /* Device-resident stage entry points for tests and benches (d_* = device). */
 void tp_sweep_dev(const double *d_P, const int *n, const int *k,
                   const int *min_clusters, const int *device, void *stream,

@@ -27,6 +27,7 @@ EXPORTS = (
     "tp_mask", "tp_mask_dev", "tp_cor", "tp_pca", "tp_sweep", "tp_coniss", "tp_dist", "tp_ch",
     "tp_pipeline", "tp_pipeline_dev", "tp_sweep_dev", "tp_tsv_dims", "tp_read_tsv",
     "tp_comm_unique_id", "tp_comm_init", "tp_comm_destroy", "tp_set_virtual_shards", "tp_shard_plan",
+    "tp_level_coords",
 )
 
 
@@ -41,6 +42,7 @@ _lib = None
 _I = ctypes.POINTER(ctypes.c_int)
 _D = ctypes.POINTER(ctypes.c_double)
 _V = ctypes.c_void_p
+_LL = ctypes.POINTER(ctypes.c_longlong)
 
 
 def load() -> ctypes.CDLL:
@@ -89,6 +91,7 @@ def load() -> ctypes.CDLL:
     L.tp_comm_destroy.argtypes = [_I]
     L.tp_set_virtual_shards.argtypes = [_I, _I, _I]
     L.tp_shard_plan.argtypes = [_I, _I, _I, _I, _I]
+    L.tp_level_coords.argtypes = [_I, _I, _I, _I, _LL, _LL, _I]
     if L.tp_version() != ABI_VERSION:
         raise ImportError(f"{LIB_PATH}: ABI version {L.tp_version()}, this binding needs {ABI_VERSION} (rebuild)")
     _lib = L
@@ -113,8 +116,14 @@ def ip(x):
         return None
     if isinstance(x, ctypes.c_int):
         return ctypes.pointer(x)
-    assert x.dtype == np.int32 and x.flags["C_CONTIGUOUS"] or x.flags["F_CONTIGUOUS"]
+    assert x.dtype == np.int32 and (x.flags["C_CONTIGUOUS"] or x.flags["F_CONTIGUOUS"])
     return x.ctypes.data_as(_I)
+
+
+def llp(x):
+    """long long* to a contiguous int64 ndarray."""
+    assert x.dtype == np.int64 and x.flags["C_CONTIGUOUS"]
+    return x.ctypes.data_as(_LL)
 
 
 def dp(x):

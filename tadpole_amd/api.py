@@ -465,30 +465,24 @@ def _assemble(res, bad_idx1) -> Tadpole:
 
 def _all_level_coords(boundary, n, levels, pos):
     """``_level_coords`` of every level at once (the cuts are nested: the cut
-    into kk clusters is the cut into kk - 1 plus boundary[n - kk]): one sort of
-    the deepest level's boundaries, each level's subset taken in that order."""
-    levels = np.asarray(levels, np.int64)
+    into kk clusters is the cut into kk - 1 plus boundary[n - kk]): one stable
+    sort of the deepest level's boundaries in the library
+    (``tp_level_coords``), each level's rows a view of one int64 block."""
+    levels = np.ascontiguousarray(levels, np.int32)
     if len(levels) == 0:
         return []
-    L = int(levels.max())
-    B = boundary[n - L:] if L > 1 else boundary[:0]          # boundary[n - L + j] joins at kk >= L - j
-    order = np.argsort(B, kind="stable")
-    vals = B[order] - 1
-    joins = (L - np.arange(len(B)))[order]
-    M = joins[None, :] <= levels[:, None]                   # level x sorted boundary
-    lev_i, col = np.nonzero(M)                              # row-major: each level's boundaries ascending
-    b = vals[col]
-    cnt = levels - 1
-    off = np.concatenate([[0], np.cumsum(levels)])          # level l occupies rows off[l] .. off[l+1]-1
+    bnd = np.ascontiguousarray(boundary[:max(n - 1, 0)], np.int32)
+    pos = np.ascontiguousarray(pos, np.int64)
+    off = np.zeros(len(levels) + 1, np.int64)
+    np.cumsum(levels, out=off[1:])
     out = np.empty((int(off[-1]), 2), np.int64)
-    out[off[:-1], 0] = pos[0]
-    out[off[1:] - 1, 1] = pos[n - 1]
-    first = np.concatenate([[0], np.cumsum(cnt)])[:-1]
-    rank = np.arange(len(b)) - np.repeat(first, cnt)        # position of each boundary within its level
-    rows = off[lev_i] + rank
-    out[rows + 1, 0] = pos[b]
-    out[rows, 1] = pos[b - 1]
-    return [out[off[l]:off[l + 1]] for l in range(len(levels))]
+    st = _lib.cint(0)
+    L = _lib.load()
+    L.tp_level_coords(_lib.ip(bnd) if n > 1 else None, ctypes.byref(_lib.cint(n)), _lib.ip(levels),
+                      ctypes.byref(_lib.cint(len(levels))), _lib.llp(pos), _lib.llp(out), ctypes.byref(st))
+    _lib.check(st)
+    offl = off.tolist()
+    return [out[offl[l]:offl[l + 1]] for l in range(len(levels))]
 
 
 def _assemble_rle(t, dendro, levels, good1, bad_idx1) -> Tadpole:

@@ -96,8 +96,9 @@ static hipEvent_t next_event(Ctx &c) {
     }
     return c.evpool[c.evnext++];
 }
+int g_kprof_fine = 1;
 void kprof_begin(Ctx &c, int cls) {
-    if (!c.prof) return;
+    if (!c.prof || (cls == K_GQ_GEMM && !g_kprof_fine)) return;
     c.open_cls = cls;
     c.open_ev = next_event(c);
     TP_HIP(hipEventRecord(c.open_ev, c.cur));
@@ -271,17 +272,23 @@ bool ctx_release_stream(int device, hipStream_t stream) {
 static void select_params(const double *scores, int k, int w, int *n_pcs, int *n_clusters) {
     int best = -1;
     double bestv = 0.0;
-    for (int i = 0; i < k; ++i) {
-        long double s = 0.0L;
-        int cnt = 0;
-        for (int j = 0; j < w; ++j) {
-            double v = scores[(size_t)i + (size_t)j * k];
+    // row sums in R's rowMeans order (j ascending per row, long double), but
+    // walked column by column: k independent accumulation chains over
+    // contiguous memory instead of one strided chain per row
+    std::vector<long double> s(k, 0.0L);
+    std::vector<int> cnt(k, 0);
+    for (int j = 0; j < w; ++j) {
+        const double *col = scores + (size_t)j * k;
+        for (int i = 0; i < k; ++i) {
+            const double v = col[i];
             if (std::isnan(v)) continue;
-            s += v;
-            ++cnt;
+            s[i] += v;
+            ++cnt[i];
         }
-        if (cnt == 0) continue;                    // NaN row mean: skipped by which.max
-        double mean = (double)(s / cnt);
+    }
+    for (int i = 0; i < k; ++i) {
+        if (cnt[i] == 0) continue;                 // NaN row mean: skipped by which.max
+        double mean = (double)(s[i] / cnt[i]);
         if (std::isnan(mean)) continue;
         if (best < 0 || mean > bestv) { best = i; bestv = mean; }
     }
@@ -463,27 +470,34 @@ static SweepOut run_sweep(Ctx &c, const double *d_Pt, int n, int k, int min_clus
         for (int r = 0; r <= R; ++r) off[r] = (size_t)tb[r] * sd.w_cap;
         shard_gather(c, sc_all, off);   // whole blocks (each rank's w may differ)
     }
-    std::vector<double> h_sc((size_t)k * o.w);
-    {
-        // every shard's block (nt x w at offset t0 * w_cap, ld nt) in one
-        // pinned buffer, one sync, then reordered to k x w
-        double *ps = (double *)c.pinned((size_t)k * o.w * sizeof(double));
-        for (int r = 0; r < R; ++r) {
-            const int t0 = tb[r], nt = tb[r + 1] - tb[r];
-            if (nt == 0) continue;
-            TP_HIP(hipMemcpyAsync(ps + (size_t)t0 * o.w, sc_all + (size_t)t0 * sd.w_cap,
-                                  (size_t)nt * o.w * sizeof(double), hipMemcpyDeviceToHost, s));
-        }
-        stream_sync(c, s);
+    // scores and the chosen tree's records are read straight out of the
+    // context's pinned staging (no fresh host vectors: a k x w vector is a
+    // new mmap per call, ~0.1 ms of page faults)
+    const size_t sc_bytes = (size_t)k * o.w * sizeof(double);
+    const size_t mrec_off = (sc_bytes * (R > 1 ? 2 : 1) + 255) & ~(size_t)255;
+    char *pin = (char *)c.pinned(mrec_off + (size_t)(n - 1) * 16);
+    double *ps = (double *)pin;
+    const double *h_sc = ps;
+    for (int r = 0; r < R; ++r) {
+        const int t0 = tb[r], nt = tb[r + 1] - tb[r];
+        if (nt == 0) continue;
+        TP_HIP(hipMemcpyAsync(ps + (size_t)t0 * o.w, sc_all + (size_t)t0 * sd.w_cap,
+                              (size_t)nt * o.w * sizeof(double), hipMemcpyDeviceToHost, s));
+    }
+    stream_sync(c, s);
+    if (R > 1) {
+        // every shard's block (nt x w at offset t0 * w, ld nt) reordered to k x w
+        double *sc = ps + (size_t)k * o.w;
         for (int r = 0; r < R; ++r) {
             const int t0 = tb[r], nt = tb[r + 1] - tb[r];
             const double *blk = ps + (size_t)t0 * o.w;
             for (int j = 0; j < o.w; ++j)
-                for (int ti = 0; ti < nt; ++ti) h_sc[(size_t)(t0 + ti) + (size_t)j * k] = blk[(size_t)ti + (size_t)j * nt];
+                for (int ti = 0; ti < nt; ++ti) sc[(size_t)(t0 + ti) + (size_t)j * k] = blk[(size_t)ti + (size_t)j * nt];
         }
+        h_sc = sc;
     }
-    if (scores) memcpy(scores, h_sc.data(), h_sc.size() * sizeof(double));
-    select_params(h_sc.data(), k, o.w, &o.n_pcs, &o.n_clusters);
+    if (scores) memcpy(scores, h_sc, sc_bytes);
+    select_params(h_sc, k, o.w, &o.n_pcs, &o.n_clusters);
     const int t = o.n_pcs - 1;
     {
         int owner = 0;
@@ -492,9 +506,7 @@ static SweepOut run_sweep(Ctx &c, const double *d_Pt, int n, int k, int min_clus
         shard_bcast_bytes(c, mrg_b + (size_t)t * (n - 1), (size_t)(n - 1) * 4, owner);
         shard_bcast_bytes(c, hgt + (size_t)t * (n - 1), (size_t)(n - 1) * 8, owner);
     }
-    std::vector<int> ma(n - 1), mb(n - 1);
-    std::vector<double> he(n - 1);
-    char *pm = (char *)c.pinned((size_t)(n - 1) * 16);   // a, b (ints), then heights (8-byte aligned)
+    char *pm = pin + mrec_off;   // a, b (ints), then heights (8-byte aligned)
     int *pa = (int *)pm, *pb = pa + (n - 1);
     double *ph = (double *)(pm + (size_t)(n - 1) * 8);
     TP_HIP(hipMemcpyAsync(pa, mrg_a + (size_t)t * (n - 1), (n - 1) * sizeof(int), hipMemcpyDeviceToHost, s));
@@ -509,13 +521,10 @@ static SweepOut run_sweep(Ctx &c, const double *d_Pt, int n, int k, int min_clus
         TP_HIP(hipMemcpyAsync(all_h->data(), hgt, rec * 8, hipMemcpyDeviceToHost, s));
     }
     stream_sync(c, s);
-    memcpy(ma.data(), pa, (n - 1) * sizeof(int));
-    memcpy(mb.data(), pb, (n - 1) * sizeof(int));
-    memcpy(he.data(), ph, (n - 1) * sizeof(double));
-    if (merge) encode_merge(ma.data(), mb.data(), n, merge);
-    if (height) memcpy(height, he.data(), (n - 1) * sizeof(double));
+    if (merge) encode_merge(pa, pb, n, merge);
+    if (height) memcpy(height, ph, (n - 1) * sizeof(double));
     if (boundary)
-        for (int q = 0; q < n - 1; ++q) boundary[q] = mb[q] + 1;
+        for (int q = 0; q < n - 1; ++q) boundary[q] = pb[q] + 1;
     return o;
 }
 
@@ -1026,6 +1035,47 @@ void tp_pipeline_dev(const double *d_M, const int *n0, const int *max_pcs, const
     });
 }
 
+/* R/TADpole.R:470-488 for every level at once: the cuts of the constrained
+ * tree are nested (the cut into kk clusters is the cut into kk - 1 plus
+ * boundary[n - kk]), so one stable sort of the deepest level's boundaries
+ * gives every level's boundaries in order.  Host-only (no device). */
+void tp_level_coords(const int *boundary, const int *n, const int *levels, const int *nlev, const long long *pos,
+                     long long *out, int *status) {
+    guarded(status, [&] {
+        if (!n || *n < 1 || !nlev || *nlev < 0 || (*nlev && (!levels || !pos || !out)) || (*n > 1 && !boundary))
+            fail(TP_ERR_ARG, "tp_level_coords: bad arguments");
+        const int N = *n, NL = *nlev;
+        int L = 1;
+        for (int l = 0; l < NL; ++l) {
+            if (levels[l] < 1 || levels[l] > N) fail(TP_ERR_ARG, "tp_level_coords: level outside 1..n");
+            L = std::max(L, levels[l]);
+        }
+        // B[j] = boundary[n - L + j] (j < L - 1) joins the cut at level L - j
+        std::vector<std::pair<int, int>> vb;   // (boundary, join level), stable by boundary
+        vb.reserve(L - 1);
+        for (int j = 0; j < L - 1; ++j) {
+            const int v = boundary[N - L + j];
+            if (v < 2 || v > N) fail(TP_ERR_ARG, "tp_level_coords: boundary outside 2..n");
+            vb.push_back({v, L - j});
+        }
+        std::stable_sort(vb.begin(), vb.end(),
+                         [](const std::pair<int, int> &a, const std::pair<int, int> &b) { return a.first < b.first; });
+        long long *o = out;
+        for (int l = 0; l < NL; ++l) {
+            const int kk = levels[l];
+            o[0] = pos[0];
+            for (const auto &e : vb) {
+                if (e.second > kk) continue;
+                o[1] = pos[e.first - 2];   // the run before the boundary ends at bin v - 1
+                o += 2;
+                o[0] = pos[e.first - 1];   // the next starts at bin v
+            }
+            o[1] = pos[N - 1];
+            o += 2;
+        }
+    });
+}
+
 
 /* ---- diagnostics (not part of include/tadpole_hip.h) -------------------- */
 
@@ -1419,7 +1469,8 @@ extern "C" {
  * 2 short-K panel GEMM, 3 GEMM LDS stage depth (16 / 32), 4 register-resident
  * tridiagonalisation, 5 int8 X'X, 6 PCA degree margin, 7 XCD-aware GEMM order, ..., 14 supertile
  * order of the int8 X'X tiles, ..., 17 C's column means formed by the correlation epilogue, 18 the
- * correlation epilogue in the int8 X'X store (with the gather's statistics). */
+ * correlation epilogue in the int8 X'X store (with the gather's statistics), ..., 25 events around
+ * every Krylov product when timings are requested (0: stage and one-launch classes only). */
 void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
     guarded(status, [&] {
         int *p = nullptr;
@@ -1449,6 +1500,7 @@ void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
         case 22: p = &g_ckry_steps; break;
         case 23: p = &g_gemm_ts32; break;
         case 24: p = &g_shard_slab; break;
+        case 25: p = &g_kprof_fine; break;
         default: fail(TP_ERR_ARG, "unknown knob");
         }
         if (*which == 3 && *value != 16 && *value != 32) fail(TP_ERR_ARG, "stage depth must be 16 or 32");

@@ -311,6 +311,7 @@ void rows_gemm_sharded(Ctx &c, const double *A, int lda, int M, const double *B,
 // exact X'X on int8 matrix cores for integer counts (tp_xtx.hip)
 extern int g_xtx_int8;
 extern int g_xtx_fused;
+extern int g_kprof_fine;   // 0: no per-launch Krylov product events (they open gaps on the stream)
 extern int g_shard_slab;   // 1: C5 shards keep C row-sharded (column slabs), 0: C gathered whole
 int xtx_int_slices(Ctx &c, const double *d_X, int n);   // 0 = not integer counts (fp64 path)
 const int8_t *xtx_slices(Ctx &c, const double *d_X, int n, int ns);
@@ -352,6 +353,7 @@ extern int g_pca_margin;   // extra Chebyshev degrees over the planned count (de
 struct PcaStats {
     int iters = 0; double resid = 0; double rate = 0; int block = 0; int blocks = 0;
     int krylov_steps = 0, krylov_dim = 0;   // block Krylov path (0: G formed)
+    const double *d_theta = nullptr;        // device copy of h_theta (valid until the next small problem)
 };
 extern int g_pca_krylov_min, g_pca_krylov_block, g_pca_krylov_steps, g_pca_over;
 extern int g_pca_cheb_fused;   // Krylov small problem: Chebyshev step in the T Y reduction (default 1)

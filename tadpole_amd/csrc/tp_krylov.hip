@@ -200,10 +200,9 @@ bool krylov_c_topk(Ctx &c, double *C, int c_col0, const double *mext, int n, int
         gg.splitk = 0;
         gemm_f64(gg, c.buf[S_PARTIAL], s);
         const int bs = (int)h_theta.size();
-        double *dth = c.buf[S_MISC].as<double>(64 + 2 * bs + k) + 64;
-        double *resid = dth + bs;
-        TP_HIP(hipMemcpyAsync(dth, h_theta.data(), bs * sizeof(double), hipMemcpyHostToDevice, s));
-        hipLaunchKernelGGL(k_resid_c, dim3(k), dim3(256), 0, s, GV, V, ab, mext, dth, n, bs, k, resid);
+        // the small problem's Ritz values are still on the device (S_SMALL)
+        double *resid = c.buf[S_MISC].as<double>(64 + 2 * (size_t)bs + k) + 64 + bs;
+        hipLaunchKernelGGL(k_resid_c, dim3(k), dim3(256), 0, s, GV, V, ab, mext, sst.d_theta, n, bs, k, resid);
         TP_HIP(hipGetLastError());
         int hinfo = 0;
         {

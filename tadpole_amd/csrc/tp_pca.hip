@@ -32,6 +32,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 
 #include "tp_common.cuh"
 #include "tp_internal.h"
@@ -195,8 +196,11 @@ static void subspace_topk(Ctx &c, const double *A, int n, int k, const Prod &pro
         hipLaunchKernelGGL(k_select_rev, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, E, n, k, V);
         TP_HIP(hipGetLastError());
         h_theta.resize(n);
-        TP_HIP(hipMemcpyAsync(h_theta.data(), theta, n * sizeof(double), hipMemcpyDeviceToHost, s));
+        double *pn = (double *)c.pinned((size_t)n * sizeof(double));
+        TP_HIP(hipMemcpyAsync(pn, theta, n * sizeof(double), hipMemcpyDeviceToHost, s));
         stream_sync(c, s);
+        memcpy(h_theta.data(), pn, n * sizeof(double));
+        st.d_theta = theta;
         trace_mark(s, "pca: exact eig");
         st.iters = 0;
         st.resid = 0.0;
@@ -277,8 +281,10 @@ static void subspace_topk(Ctx &c, const double *A, int n, int k, const Prod &pro
     {
         std::vector<double> dg(b);
         hipLaunchKernelGGL(k_diag, dim3((b + 255) / 256), dim3(256), 0, s, Wsm, b, resid);
-        TP_HIP(hipMemcpyAsync(dg.data(), resid, b * sizeof(double), hipMemcpyDeviceToHost, s));
+        double *pn = (double *)c.pinned((size_t)b * sizeof(double));
+        TP_HIP(hipMemcpyAsync(pn, resid, b * sizeof(double), hipMemcpyDeviceToHost, s));
         stream_sync(c, s);
+        memcpy(dg.data(), pn, b * sizeof(double));
         for (double &x : dg) x = std::sqrt(x);
         const double l1 = dg[0], lk = dg[k - 1], lb = dg[b - 1];
         cut = lb;
@@ -358,9 +364,17 @@ static void subspace_topk(Ctx &c, const double *A, int n, int k, const Prod &pro
         std::swap(Q, T);
         hipLaunchKernelGGL(k_resid, dim3(k), dim3(256), 0, s, Yb, Q, theta, n, b, k, resid);
         TP_HIP(hipGetLastError());
-        TP_HIP(hipMemcpyAsync(h_res.data(), resid, k * sizeof(double), hipMemcpyDeviceToHost, s));
-        TP_HIP(hipMemcpyAsync(h_theta.data(), theta, b * sizeof(double), hipMemcpyDeviceToHost, s));
-        stream_sync(c, s);
+        {
+            // one pinned staging, one sync (pageable read-backs each stage
+            // and synchronise on their own)
+            double *pn = (double *)c.pinned((size_t)(k + b) * sizeof(double));
+            TP_HIP(hipMemcpyAsync(pn, resid, k * sizeof(double), hipMemcpyDeviceToHost, s));
+            TP_HIP(hipMemcpyAsync(pn + k, theta, b * sizeof(double), hipMemcpyDeviceToHost, s));
+            stream_sync(c, s);
+            memcpy(h_res.data(), pn, k * sizeof(double));
+            memcpy(h_theta.data(), pn + k, b * sizeof(double));
+        }
+        st.d_theta = theta;
         const double th1 = std::fabs(h_theta[b - 1]);
         double worst = 0.0;
         for (int j = 0; j < k; ++j) worst = std::max(worst, h_res[j] / (th1 > 0 ? th1 : 1.0));
@@ -527,13 +541,21 @@ static void krylov_topk(Ctx &c, double *C, int c_col0, const double *mext, int n
         gg.splitk = 0;
         gemm_f64(gg, c.buf[S_PARTIAL], s);
         const int bs = (int)h_theta.size();
-        double *dth = c.buf[S_MISC].as<double>(64 + 2 * bs + k) + 64;
-        double *resid = dth + bs;
-        TP_HIP(hipMemcpyAsync(dth, h_theta.data(), bs * sizeof(double), hipMemcpyHostToDevice, s));
-        hipLaunchKernelGGL(k_resid, dim3(k), dim3(256), 0, s, GV, V, dth, n, bs, k, resid);
+        // the small problem's Ritz values are still on the device (S_SMALL)
+        double *resid = c.buf[S_MISC].as<double>(64 + 2 * (size_t)bs + k) + 64 + bs;
+        hipLaunchKernelGGL(k_resid, dim3(k), dim3(256), 0, s, GV, V, sst.d_theta, n, bs, k, resid);
         TP_HIP(hipGetLastError());
-        TP_HIP(hipMemcpyAsync(h_res.data(), resid, k * sizeof(double), hipMemcpyDeviceToHost, s));
+        double *pn = (double *)c.pinned((size_t)k * sizeof(double));
+        TP_HIP(hipMemcpyAsync(pn, resid, k * sizeof(double), hipMemcpyDeviceToHost, s));
+        // scores P = Xc V = (Xc K) Y: an n x D by D x k product instead of
+        // another pass over Xc (2 n D k flops, not 2 n^2 k), queued before the
+        // residual check so the device has work while the host waits for it
+        // (recomputed if the check extends the space)
+        GemmArgs pg{n, k, D, XK, n, false, Vs, D, P, n};
+        pg.splitk = 0;
+        gemm_f64(pg, c.buf[S_PARTIAL], s);
         stream_sync(c, s);
+        memcpy(h_res.data(), pn, k * sizeof(double));
         const double th1 = std::fabs(h_theta[bs - 1]);
         double worst = 0.0;
         for (int j = 0; j < k; ++j) worst = std::max(worst, h_res[j] / (th1 > 0 ? th1 : 1.0));
@@ -550,12 +572,6 @@ static void krylov_topk(Ctx &c, double *C, int c_col0, const double *mext, int n
         steps = std::min(smax, steps + 4);
     }
     if (!(st.resid <= 1e-8)) fail(TP_ERR_NUMERIC, "PCA block Krylov iteration did not converge");
-    // scores P = Xc V = (Xc K) Y: an n x D by D x k product instead of another
-    // pass over Xc (2 n D k flops, not 2 n^2 k)
-    GemmArgs pg{n, k, st.krylov_dim, XK, n, false, c.buf[S_KRYV].as<double>((size_t)st.krylov_dim * k),
-                st.krylov_dim, P, n};
-    pg.splitk = 0;
-    gemm_f64(pg, c.buf[S_PARTIAL], s);
 }
 
 PcaStats pca_dev(Ctx &c, double *d_C, int n, int k, double *d_P, double *d_Pt, double *h_sdev,

@@ -9,7 +9,7 @@ import pandas as pd
 import pytest
 
 import tadpole_oracle as O
-from tadpole_amd import api
+from tadpole_amd import _lib, api
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
@@ -73,6 +73,21 @@ def test_vectorised_assembly_equals_literal_rle(seed):
         assert set(fast.clusters) == set(slow.clusters)
         for q in fast.clusters:
             assert np.array_equal(fast.clusters[q], slow.clusters[q]), (q, b is None)
+
+
+def test_level_coords_rejects_bad_arguments():
+    # tp_level_coords (host-only C-ABI): levels outside 1..n and boundaries
+    # outside 2..n fail with TP_ERR_ARG instead of reading out of bounds
+    n = 6
+    pos = np.arange(1, n + 1, dtype=np.int64)
+    with pytest.raises(_lib.TadpoleError) as e:
+        api._all_level_coords(np.array([2, 3, 4, 5, 6]), n, [n + 1], pos)
+    assert e.value.status == _lib.TP_ERR_ARG
+    with pytest.raises(_lib.TadpoleError) as e:
+        api._all_level_coords(np.array([2, 3, 1, 5, 6]), n, [4], pos)
+    assert e.value.status == _lib.TP_ERR_ARG
+    assert [c.tolist() for c in api._all_level_coords(np.array([4, 2, 6, 3, 5]), n, [1, 3], pos)] == \
+        [[[1, 6]], [[1, 2], [3, 4], [5, 6]]]
 
 
 def test_assembly_without_bad_columns_branch():
