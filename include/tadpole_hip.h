@@ -13,6 +13,7 @@
  *   dist(pcs)            R/TADpole.R:108,460              -> tp_dist
  *   calinhara(x, cutree) R/TADpole.R:117-120              -> tp_ch
  *   the whole seam       R/TADpole.R:348-349,444-468      -> tp_pipeline
+ *   cutree/rle coords    R/TADpole.R:470-488              -> tp_level_coords
  *
  * Calling convention (so R's .C() can bind every entry without R headers, and
  * Python ctypes in the tests): every argument is a pointer; matrices are
@@ -214,11 +215,12 @@ void tp_pipeline_dev(const double *d_M, const int *n0, const int *max_pcs,
  * labels placed on c(good, bad) order, rle runs -> rows (start, end)).
  * boundary[n-1]: as tp_pipeline returns it (first n_good-1 entries, n =
  * n_good), pos[n]: the 1-based coordinate of each kept bin in the full
- * matrix, levels[nlev]: each in 1..n.  out: sum(levels) rows of two int64
- * (start, end), row-major, level after level in `levels` order.  Host only. */
+ * matrix, levels[nlev]: each in 1..n.  out: sum(levels) rows of two ints
+ * (start, end), row-major, level after level in `levels` order.  Host only
+ * (R: .C("tp_level_coords", boundary, n, levels, nlev, pos, out = integer(2 *
+ * sum(levels)), status = integer(1))). */
 void tp_level_coords(const int *boundary, const int *n, const int *levels,
-                     const int *nlev, const long long *pos, long long *out,
-                     int *status);
+                     const int *nlev, const int *pos, int *out, int *status);
 
 /* Device-resident stage entry points for tests and benches (d_* = device). */
 void tp_sweep_dev(const double *d_P, const int *n, const int *k,

@@ -42,7 +42,6 @@ _lib = None
 _I = ctypes.POINTER(ctypes.c_int)
 _D = ctypes.POINTER(ctypes.c_double)
 _V = ctypes.c_void_p
-_LL = ctypes.POINTER(ctypes.c_longlong)
 
 
 def load() -> ctypes.CDLL:
@@ -91,7 +90,7 @@ def load() -> ctypes.CDLL:
     L.tp_comm_destroy.argtypes = [_I]
     L.tp_set_virtual_shards.argtypes = [_I, _I, _I]
     L.tp_shard_plan.argtypes = [_I, _I, _I, _I, _I]
-    L.tp_level_coords.argtypes = [_I, _I, _I, _I, _LL, _LL, _I]
+    L.tp_level_coords.argtypes = [_I, _I, _I, _I, _I, _I, _I]
     if L.tp_version() != ABI_VERSION:
         raise ImportError(f"{LIB_PATH}: ABI version {L.tp_version()}, this binding needs {ABI_VERSION} (rebuild)")
     _lib = L
@@ -119,11 +118,6 @@ def ip(x):
     assert x.dtype == np.int32 and (x.flags["C_CONTIGUOUS"] or x.flags["F_CONTIGUOUS"])
     return x.ctypes.data_as(_I)
 
-
-def llp(x):
-    """long long* to a contiguous int64 ndarray."""
-    assert x.dtype == np.int64 and x.flags["C_CONTIGUOUS"]
-    return x.ctypes.data_as(_LL)
 
 
 def dp(x):

@@ -472,15 +472,15 @@ def _all_level_coords(boundary, n, levels, pos):
     if len(levels) == 0:
         return []
     bnd = np.ascontiguousarray(boundary[:max(n - 1, 0)], np.int32)
-    pos = np.ascontiguousarray(pos, np.int64)
+    pos32 = np.ascontiguousarray(pos, np.int32)
     off = np.zeros(len(levels) + 1, np.int64)
     np.cumsum(levels, out=off[1:])
-    out = np.empty((int(off[-1]), 2), np.int64)
+    out = np.empty((int(off[-1]), 2), np.int32)
     st = _lib.cint(0)
-    L = _lib.load()
-    L.tp_level_coords(_lib.ip(bnd) if n > 1 else None, ctypes.byref(_lib.cint(n)), _lib.ip(levels),
-                      ctypes.byref(_lib.cint(len(levels))), _lib.llp(pos), _lib.llp(out), ctypes.byref(st))
+    _lib.load().tp_level_coords(_lib.ip(bnd), ctypes.byref(_lib.cint(n)), _lib.ip(levels),
+                                ctypes.byref(_lib.cint(len(levels))), _lib.ip(pos32), _lib.ip(out), ctypes.byref(st))
     _lib.check(st)
+    out = out.astype(np.int64)
     offl = off.tolist()
     return [out[offl[l]:offl[l + 1]] for l in range(len(levels))]
 

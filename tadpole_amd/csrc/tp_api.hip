@@ -1039,8 +1039,8 @@ void tp_pipeline_dev(const double *d_M, const int *n0, const int *max_pcs, const
  * tree are nested (the cut into kk clusters is the cut into kk - 1 plus
  * boundary[n - kk]), so one stable sort of the deepest level's boundaries
  * gives every level's boundaries in order.  Host-only (no device). */
-void tp_level_coords(const int *boundary, const int *n, const int *levels, const int *nlev, const long long *pos,
-                     long long *out, int *status) {
+void tp_level_coords(const int *boundary, const int *n, const int *levels, const int *nlev, const int *pos, int *out,
+                     int *status) {
     guarded(status, [&] {
         if (!n || *n < 1 || !nlev || *nlev < 0 || (*nlev && (!levels || !pos || !out)) || (*n > 1 && !boundary))
             fail(TP_ERR_ARG, "tp_level_coords: bad arguments");
@@ -1060,7 +1060,7 @@ void tp_level_coords(const int *boundary, const int *n, const int *levels, const
         }
         std::stable_sort(vb.begin(), vb.end(),
                          [](const std::pair<int, int> &a, const std::pair<int, int> &b) { return a.first < b.first; });
-        long long *o = out;
+        int *o = out;
         for (int l = 0; l < NL; ++l) {
             const int kk = levels[l];
             o[0] = pos[0];
