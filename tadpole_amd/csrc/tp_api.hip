@@ -1470,7 +1470,8 @@ extern "C" {
  * tridiagonalisation, 5 int8 X'X, 6 PCA degree margin, 7 XCD-aware GEMM order, ..., 14 supertile
  * order of the int8 X'X tiles, ..., 17 C's column means formed by the correlation epilogue, 18 the
  * correlation epilogue in the int8 X'X store (with the gather's statistics), ..., 25 events around
- * every Krylov product when timings are requested (0: stage and one-launch classes only). */
+ * every Krylov product when timings are requested (0: stage and one-launch classes only), 26 products
+ * with the block-tridiagonal Krylov projection T skip its zero blocks (0: dense GEMM). */
 void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
     guarded(status, [&] {
         int *p = nullptr;
@@ -1501,6 +1502,7 @@ void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
         case 23: p = &g_gemm_ts32; break;
         case 24: p = &g_shard_slab; break;
         case 25: p = &g_kprof_fine; break;
+        case 26: p = &g_pca_band; break;
         default: fail(TP_ERR_ARG, "unknown knob");
         }
         if (*which == 3 && *value != 16 && *value != 32) fail(TP_ERR_ARG, "stage depth must be 16 or 32");

@@ -73,7 +73,7 @@ struct Ctx {
     hipStream_t cur = nullptr;      // stream used by the current call
     hipStream_t side = nullptr;     // fork-join helper stream (side_stream())
     hipEvent_t fork_ev = nullptr, join_ev = nullptr;
-    DevBuf buf[40];   // indexed by Slot (static_assert below)
+    DevBuf buf[48];   // indexed by Slot (static_assert below)
     DevBuf pinned_flag;
     void *host_pinned = nullptr;    // small pinned staging area
     size_t host_pinned_bytes = 0;
@@ -100,6 +100,7 @@ enum Slot {
     S_S, S_C, S_XC, S_XCT, S_G, S_Q, S_Z, S_W, S_SMALL, S_P, S_PT,
     S_SWEEP, S_SWEEP2, S_SCORES, S_PARTIAL, S_MISC, S_SHARD, S_SHARD2, S_DEDUP,
     S_KRY, S_KRYG, S_KRYT, S_KRYV, S_KRYX, S_CMEAN, S_CHBIG, S_CHOLP, S_SMALL2, S_GSTAT, S_XTXT, S_MEXT, S_KRYA,
+    S_KRYH,
     S_NSLOT
 };
 static_assert(S_NSLOT <= (int)(sizeof(Ctx::buf) / sizeof(Ctx::buf[0])), "Ctx::buf too small for the slots");
@@ -361,7 +362,11 @@ extern int g_pca_ckrylov;      // 1: block Krylov in C (tp_krylov.hip), 0: in G 
 extern int g_ckry_chunk;       // rows per Z partial of the C-Krylov orthogonalisation
 extern int g_ckry_steps;       // C-Krylov blocks before the first check (0: from k and n)
 // the top k eigenpairs of a D x D projected matrix (tp_pca.hip)
-void small_topk_T(Ctx &c, double *Tm, int D, int k, double *Vs, std::vector<double> &h_theta, PcaStats &sst);
+// band_p > 0: T is block tridiagonal with band_p x band_p blocks (products
+// with it skip the zero blocks when g_pca_band)
+void small_topk_T(Ctx &c, double *Tm, int D, int k, double *Vs, std::vector<double> &h_theta, PcaStats &sst,
+                  int band_p = 0);
+extern int g_pca_band;
 // false: an orthogonalisation pass broke down (the caller takes the G path)
 bool krylov_c_topk(Ctx &c, double *C, int c_col0, const double *mext, int n, int k, double *V, double *P,
                    std::vector<double> &h_theta, PcaStats &st);

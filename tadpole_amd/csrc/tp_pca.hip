@@ -140,6 +140,72 @@ __global__ void k_cheb(double *Y, const double *GY, const double *Yc, const doub
     Y[t] = v;
 }
 
+typedef double d4b __attribute__((ext_vector_type(4)));
+
+// Out = a (T Y) + bc Yc [+ cc Yp] (AFF) or T Y, for T symmetric and block
+// tridiagonal with p x p blocks (the block Krylov projection, D x D, ld D),
+// Y, Out, Yc, Yp D x b (ld D).  One workgroup per (block row, 16 columns):
+// p / 16 waves, each a 16 x 16 tile over the <= 3p columns of T its block row
+// touches (f64 MFMA 16x16x4); the tile goes through LDS so the epilogue reads
+// and writes whole column segments.  2 D (3p) b flops instead of 2 D^2 b.
+template <bool AFF>
+__global__ void __launch_bounds__(256) k_band_ty(const double *__restrict__ T, const double *__restrict__ Y,
+                                                  double *Out, int D, int p, double a, double bc, const double *Yc,
+                                                  double cc, const double *Yp) {
+    __shared__ double tile[64][17];
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63, fr = l & 15, fk = l >> 4;
+    const int ib = blockIdx.x, c0 = blockIdx.y * 16;
+    const int r0 = ib * p + 16 * w;
+    const int k0 = max(0, (ib - 1) * p), k1 = min(D, (ib + 2) * p);
+    const double *tp = T + (size_t)(r0 + fr) + (size_t)fk * D;   // T[r0 + fr][k + fk]
+    const double *yp = Y + (size_t)fk + (size_t)(c0 + fr) * D;   // Y[k + fk][c0 + fr]
+    d4b acc = (d4b){0.0, 0.0, 0.0, 0.0};
+    for (int k = k0; k < k1; k += 32) {   // p is a multiple of 32
+        double af[8], bf[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            af[u] = tp[(size_t)(k + 4 * u) * D];
+            bf[u] = yp[k + 4 * u];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(af[u], bf[u], acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) tile[16 * w + fk + 4 * r][fr] = acc[r];
+    __syncthreads();
+    // column c0 + j, rows ib p + q + e p / 4 (4p threads cover p x 16; 16
+    // consecutive lanes a 128-byte column segment)
+    const int j = threadIdx.x / (p / 4), q = threadIdx.x % (p / 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int rl = q + e * (p / 4);
+        const size_t idx = (size_t)(ib * p + rl) + (size_t)(c0 + j) * D;
+        double v = tile[rl][j];
+        if (AFF) {
+            v = a * v + bc * Yc[idx];
+            if (Yp) v = v + cc * Yp[idx];
+        }
+        Out[idx] = v;
+    }
+}
+
+// T (D x D, ld D) from the Krylov CGS2 coefficients H1 + H2 (ld Dm): block
+// (bi, bj) with bi < bj from column block bj, mirrored below the diagonal,
+// diagonal blocks symmetrised, blocks off the tridiagonal band zero
+__global__ void k_assemble_T(const double *H1, const double *H2, int Dm, int D, int p, double *T) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (size_t)D * D) return;
+    const int i = (int)(t % D), j = (int)(t / D);
+    const int bi = i / p, bj = j / p;
+    const size_t a = (size_t)i + (size_t)j * Dm, b = (size_t)j + (size_t)i * Dm;
+    double v;
+    if (bi + 1 < bj || bj + 1 < bi) v = 0.0;   // K_i'G K_j = 0 for |i - j| > 1 (rounding left out)
+    else if (bi < bj) v = H1[a] + H2[a];
+    else if (bi > bj) v = H1[b] + H2[b];
+    else v = 0.5 * ((H1[a] + H2[a]) + (H1[b] + H2[b]));
+    T[t] = v;
+}
+
 __global__ void k_fill_const(double *p, int n, double v) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) p[i] = v;
@@ -415,15 +481,35 @@ static void subspace_topk(Ctx &c, const double *A, int n, int k, const Prod &pro
 // The projected problem of the Krylov paths: the top k eigenpairs of T (D x
 // D, symmetric, ld D) by the subspace iteration above (products with T are
 // D x D GEMMs, the Chebyshev step in their split-K reduction).  Vs: D x k.
-void small_topk_T(Ctx &c, double *Tm, int D, int k, double *Vs, std::vector<double> &h_theta, PcaStats &sst) {
+int g_pca_band = 1;
+
+static void band_ty(const double *T, const double *Y, double *Out, int D, int b, int p, bool aff, double a, double bc,
+                    const double *Yc, double cc, const double *Yp, hipStream_t s) {
+    if (p % 32 || p > 64 || D % p || b % 16) fail(TP_ERR_ARG, "band_ty: p must be 32 or 64, D a multiple of p, b of 16");
+    const dim3 grid(D / p, b / 16);
+    if (aff) hipLaunchKernelGGL(k_band_ty<true>, grid, dim3(4 * p), 0, s, T, Y, Out, D, p, a, bc, Yc, cc, Yp);
+    else hipLaunchKernelGGL(k_band_ty<false>, grid, dim3(4 * p), 0, s, T, Y, Out, D, p, 0.0, 0.0, nullptr, 0.0, nullptr);
+    TP_HIP(hipGetLastError());
+}
+
+void small_topk_T(Ctx &c, double *Tm, int D, int k, double *Vs, std::vector<double> &h_theta, PcaStats &sst, int band_p) {
     hipStream_t s = c.cur;
+    const bool band = band_p > 0 && g_pca_band;
     Prod tprod = [&](const double *Y, double *Out) {
+        if (band) {
+            band_ty(Tm, Y, Out, D, sst.block, band_p, false, 0, 0, nullptr, 0, nullptr, s);
+            return;
+        }
         GemmArgs g{D, sst.block, D, Tm, D, true, Y, D, Out, D};
         g.splitk = 0;
         gemm_f64(g, c.buf[S_PARTIAL], s);
     };
     ProdAff taff = [&](const double *Y, double *Out, double a, double b, const double *Yc, double cc,
                        const double *Yp) {
+        if (band) {
+            band_ty(Tm, Y, Out, D, sst.block, band_p, true, a, b, Yc, cc, Yp, s);
+            return;
+        }
         GemmArgs g{D, sst.block, D, Tm, D, true, Y, D, Out, D};
         g.splitk = 0;
         g.affine = true;
@@ -462,14 +548,20 @@ static void krylov_topk(Ctx &c, double *C, int c_col0, const double *mext, int n
     double *XK = c.buf[S_KRYX].as<double>((size_t)n * p * smax);   // Xc K_t: the scores come from it
     const size_t np = (size_t)n * p;
     const unsigned g1 = (unsigned)((np + 255) / 256);
+    // The CGS2 coefficients of both passes, H1 and H2 (Dm x Dm each, ld Dm):
+    // column block t - 1 holds K'(G K_{t-1}) and K'W1 of step t, so their sum
+    // is T's column block t - 1 above and on the diagonal (G K_{t-1} = K (H1 +
+    // H2) + K_t R with K_t orthogonal to K): T = K'GK without its own product
+    const int Dm = p * smax;
+    double *H1 = c.buf[S_KRYH].as<double>(2 * (size_t)Dm * Dm);
+    double *H2 = H1 + (size_t)Dm * Dm;
     // per-step scratch; re-fetched by every extend() because the small
     // problem (subspace_topk) grows and reallocates the same slots
-    double *W, *Zt, *Xp, *Wsm, *Xinv, *Yinv;
+    double *W, *Zt, *Wsm, *Xinv, *Yinv;
     int *d_info;
     auto scratch = [&]() {
         W = c.buf[S_Q].as<double>(np);
         Zt = c.buf[S_Z].as<double>(np);
-        Xp = c.buf[S_SWEEP].as<double>((size_t)p * p * smax);
         Wsm = c.buf[S_SMALL].as<double>((size_t)3 * p * p + 2 * p + 64);
         Xinv = Wsm + (size_t)p * p;
         Yinv = Xinv + (size_t)p * p;
@@ -491,10 +583,11 @@ static void krylov_topk(Ctx &c, double *C, int c_col0, const double *mext, int n
                 const int D = t * p;
                 for (int pass = 0; pass < 2; ++pass) {
                     const double *src = pass == 0 ? GK + (size_t)(t - 1) * np : W;
-                    GemmArgs pr{D, p, n, K, n, true, src, n, Xp, D};   // K'src
+                    double *Hc = (pass == 0 ? H1 : H2) + (size_t)(t - 1) * p * Dm;   // column block t - 1
+                    GemmArgs pr{D, p, n, K, n, true, src, n, Hc, Dm};   // K'src
                     pr.splitk = 0;
                     gemm_f64(pr, c.buf[S_PARTIAL], s);
-                    GemmArgs up{n, p, D, K, n, false, Xp, D, W, n};   // W = src - K (K'src)
+                    GemmArgs up{n, p, D, K, n, false, Hc, Dm, W, n};   // W = src - K (K'src)
                     up.splitk = 0;
                     up.sub_from = src;
                     gemm_f64(up, c.buf[S_PARTIAL], s);
@@ -523,15 +616,24 @@ static void krylov_topk(Ctx &c, double *C, int c_col0, const double *mext, int n
         extend(steps);
         const int D = steps * p;
         trace_mark(s, "pca: krylov");
-        // T = K'GK (upper tiles, mirrored), then its top k eigenpairs
+        // T = K'GK from the CGS2 coefficients; the last column block (no
+        // step after it) by one K'(G K_{s-1}) product
+        {
+            GemmArgs lg{D, p, n, K, n, true, GK + (size_t)(steps - 1) * np, n, H1 + (size_t)(steps - 1) * p * Dm, Dm};
+            lg.splitk = 0;
+            gemm_f64(lg, c.buf[S_PARTIAL], s);
+            TP_HIP(hipMemset2DAsync(H2 + (size_t)(steps - 1) * p * Dm, (size_t)Dm * sizeof(double), 0,
+                                    (size_t)D * sizeof(double), p, s));
+        }
         double *Tm = c.buf[S_KRYT].as<double>((size_t)D * D);
-        GemmArgs tg{D, D, n, K, n, true, GK, n, Tm, D};
-        tg.sym_upper = true;
-        tg.splitk = 0;
-        gemm_f64(tg, c.buf[S_PARTIAL], s);
+        {
+            const size_t cnt = (size_t)D * D;
+            hipLaunchKernelGGL(k_assemble_T, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, H1, H2, Dm, D, p, Tm);
+            TP_HIP(hipGetLastError());
+        }
         double *Vs = c.buf[S_KRYV].as<double>((size_t)D * k);
         PcaStats sst;
-        small_topk_T(c, Tm, D, k, Vs, h_theta, sst);
+        small_topk_T(c, Tm, D, k, Vs, h_theta, sst, p);
         // V = K Y, G V = (G K) Y; residuals in the n-dimensional space
         GemmArgs vg{n, k, D, K, n, false, Vs, D, V, n};
         vg.splitk = 0;
