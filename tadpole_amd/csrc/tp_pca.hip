@@ -143,44 +143,49 @@ __global__ void k_cheb(double *Y, const double *GY, const double *Yc, const doub
 typedef double d4b __attribute__((ext_vector_type(4)));
 
 // Out = a (T Y) + bc Yc [+ cc Yp] (AFF) or T Y, for T symmetric and block
-// tridiagonal with p x p blocks (the block Krylov projection, D x D, ld D),
+// tridiagonal with P x P blocks (the block Krylov projection, D x D, ld D),
 // Y, Out, Yc, Yp D x b (ld D).  One workgroup per (block row, 16 columns):
-// p / 16 waves, each a 16 x 16 tile over the <= 3p columns of T its block row
-// touches (f64 MFMA 16x16x4); the tile goes through LDS so the epilogue reads
-// and writes whole column segments.  2 D (3p) b flops instead of 2 D^2 b.
-template <bool AFF>
-__global__ void __launch_bounds__(256) k_band_ty(const double *__restrict__ T, const double *__restrict__ Y,
-                                                  double *Out, int D, int p, double a, double bc, const double *Yc,
-                                                  double cc, const double *Yp) {
-    __shared__ double tile[64][17];
+// 3 x P / 16 waves, wave (kb, rw) a 16 x 16 tile of rows rw over T's block
+// column ib - 1 + kb, all of its loads issued at once (one memory latency per
+// product, not one per k step); the three partial tiles are summed in LDS in
+// a fixed order and the epilogue reads and writes whole column segments.
+// 2 D (3P) b flops instead of 2 D^2 b.
+template <bool AFF, int P>
+__global__ void __launch_bounds__(12 * P) k_band_ty(const double *__restrict__ T, const double *__restrict__ Y,
+                                                     double *Out, int D, double a, double bc, const double *Yc,
+                                                     double cc, const double *Yp) {
+    constexpr int NRW = P / 16;   // row waves per block column
+    __shared__ double tile[3][P][17];
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63, fr = l & 15, fk = l >> 4;
+    const int rw = w % NRW, kb = w / NRW;
     const int ib = blockIdx.x, c0 = blockIdx.y * 16;
-    const int r0 = ib * p + 16 * w;
-    const int k0 = max(0, (ib - 1) * p), k1 = min(D, (ib + 2) * p);
-    const double *tp = T + (size_t)(r0 + fr) + (size_t)fk * D;   // T[r0 + fr][k + fk]
-    const double *yp = Y + (size_t)fk + (size_t)(c0 + fr) * D;   // Y[k + fk][c0 + fr]
+    const int r0 = ib * P + 16 * rw;
+    const int kc = ib - 1 + kb;   // T's block column
     d4b acc = (d4b){0.0, 0.0, 0.0, 0.0};
-    for (int k = k0; k < k1; k += 32) {   // p is a multiple of 32
-        double af[8], bf[8];
+    if (kc >= 0 && kc * P < D) {
+        const double *tp = T + (size_t)(r0 + fr) + (size_t)(kc * P + fk) * D;   // T[r0 + fr][k + fk]
+        const double *yp = Y + (size_t)(kc * P + fk) + (size_t)(c0 + fr) * D;   // Y[k + fk][c0 + fr]
+        double af[P / 4], bf[P / 4];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            af[u] = tp[(size_t)(k + 4 * u) * D];
-            bf[u] = yp[k + 4 * u];
+        for (int u = 0; u < P / 4; ++u) {
+            af[u] = tp[(size_t)(4 * u) * D];
+            bf[u] = yp[4 * u];
         }
 #pragma unroll
-        for (int u = 0; u < 8; ++u) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(af[u], bf[u], acc, 0, 0, 0);
+        for (int u = 0; u < P / 4; ++u) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(af[u], bf[u], acc, 0, 0, 0);
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) tile[16 * w + fk + 4 * r][fr] = acc[r];
+    for (int r = 0; r < 4; ++r) tile[kb][16 * rw + fk + 4 * r][fr] = acc[r];
     __syncthreads();
-    // column c0 + j, rows ib p + q + e p / 4 (4p threads cover p x 16; 16
-    // consecutive lanes a 128-byte column segment)
-    const int j = threadIdx.x / (p / 4), q = threadIdx.x % (p / 4);
+    if (threadIdx.x >= 4 * P) return;
+    // column c0 + j, rows ib P + q + e P / 4 (16 consecutive lanes a 128-byte
+    // column segment)
+    const int j = threadIdx.x / (P / 4), q = threadIdx.x % (P / 4);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-        const int rl = q + e * (p / 4);
-        const size_t idx = (size_t)(ib * p + rl) + (size_t)(c0 + j) * D;
-        double v = tile[rl][j];
+        const int rl = q + e * (P / 4);
+        const size_t idx = (size_t)(ib * P + rl) + (size_t)(c0 + j) * D;
+        double v = (tile[0][rl][j] + tile[1][rl][j]) + tile[2][rl][j];
         if (AFF) {
             v = a * v + bc * Yc[idx];
             if (Yp) v = v + cc * Yp[idx];
@@ -486,9 +491,14 @@ int g_pca_band = 1;
 static void band_ty(const double *T, const double *Y, double *Out, int D, int b, int p, bool aff, double a, double bc,
                     const double *Yc, double cc, const double *Yp, hipStream_t s) {
     if (p % 32 || p > 64 || D % p || b % 16) fail(TP_ERR_ARG, "band_ty: p must be 32 or 64, D a multiple of p, b of 16");
-    const dim3 grid(D / p, b / 16);
-    if (aff) hipLaunchKernelGGL(k_band_ty<true>, grid, dim3(4 * p), 0, s, T, Y, Out, D, p, a, bc, Yc, cc, Yp);
-    else hipLaunchKernelGGL(k_band_ty<false>, grid, dim3(4 * p), 0, s, T, Y, Out, D, p, 0.0, 0.0, nullptr, 0.0, nullptr);
+    const dim3 grid(D / p, b / 16), blk(12 * p);
+    if (p == 64) {
+        if (aff) hipLaunchKernelGGL((k_band_ty<true, 64>), grid, blk, 0, s, T, Y, Out, D, a, bc, Yc, cc, Yp);
+        else hipLaunchKernelGGL((k_band_ty<false, 64>), grid, blk, 0, s, T, Y, Out, D, 0.0, 0.0, nullptr, 0.0, nullptr);
+    } else {
+        if (aff) hipLaunchKernelGGL((k_band_ty<true, 32>), grid, blk, 0, s, T, Y, Out, D, a, bc, Yc, cc, Yp);
+        else hipLaunchKernelGGL((k_band_ty<false, 32>), grid, blk, 0, s, T, Y, Out, D, 0.0, 0.0, nullptr, 0.0, nullptr);
+    }
     TP_HIP(hipGetLastError());
 }
 
