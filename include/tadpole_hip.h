@@ -109,6 +109,13 @@ void tp_shard_plan(const int *n, const int *nranks, const int *kind,
 void tp_tsv_dims(const char **path, int *nrow, int *ncol, int *status);
 void tp_read_tsv(const char **path, const int *nrow, const int *ncol,
                  const int *nthreads, const int *flags, double *out, int *status);
+/* The same parse straight into device memory: d_out (nrow x ncol, row-major,
+ * on `device`) filled through the library's pinned staging in row blocks, each
+ * block's copy queued on `stream` while the next block is parsed (the upload
+ * hides under the parse).  Returns once the copies are complete. */
+void tp_read_tsv_dev(const char **path, const int *nrow, const int *ncol,
+                     const int *nthreads, const int *device, void *stream,
+                     double *d_out, int *status);
 
 /* ------------------------------------------------------------------- mask */
 /* R/TADpole.R:19-20 (NA->0, forceSymmetric(uplo='U')), :35-37 (rowMeans, diag==0,

@@ -126,8 +126,36 @@ def read_matrix(mat_file, nthreads: int = 0) -> np.ndarray:
     return out
 
 
+def _read_to_device(mat_file, device: int, stream=None):
+    """A matrix file parsed straight into a new float64 device tensor
+    (``tp_read_tsv_dev``: row blocks through the library's pinned staging, each
+    block's upload overlapping the parse of the next).  TADpole(path) never
+    returns the matrix, so the pipeline may clean this copy in place."""
+    L = _lib.load()
+    if L.tp_device_count() <= 0:
+        raise _lib.TadpoleError(_lib.TP_ERR_HIP, "no HIP device: there is no CPU path")
+    import torch
+    path = ctypes.c_char_p(os.fsencode(os.fspath(mat_file)))
+    nr, nc, st = cint(0), cint(0), cint(0)
+    L.tp_tsv_dims(ctypes.byref(path), ctypes.byref(nr), ctypes.byref(nc), ctypes.byref(st))
+    _lib.check(st)
+    d = torch.empty((nr.value, nc.value), dtype=torch.float64, device=f"cuda:{device}")
+    if d.numel():
+        s = stream if stream is not None else torch.cuda.current_stream(device)
+        th = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+        L.tp_read_tsv_dev(ctypes.byref(path), ctypes.byref(nr), ctypes.byref(nc), ctypes.byref(cint(min(th, 64))),
+                          ctypes.byref(cint(device)), ctypes.c_void_p(s.cuda_stream), ctypes.c_void_p(d.data_ptr()),
+                          ctypes.byref(st))
+        _lib.check(st)
+    return d
+
+
+def _is_path(mat) -> bool:
+    return isinstance(mat, (str, bytes)) or hasattr(mat, "__fspath__")
+
+
 def _as_matrix(mat) -> np.ndarray:
-    if isinstance(mat, (str, bytes)) or hasattr(mat, "__fspath__"):
+    if _is_path(mat):
         return read_matrix(mat)
     m = np.asarray(mat, dtype=np.float64)
     if m.ndim != 2 or m.shape[0] != m.shape[1]:
@@ -526,6 +554,8 @@ def TADpole(mat_file, max_pcs: int = 200, min_clusters: int = 2, bad_frac: float
             raw = raw.to(torch.float64).contiguous()
             if raw.data_ptr() == mat_file.data_ptr():
                 raw = raw.clone()
+    elif _is_path(mat_file):
+        raw = _read_to_device(mat_file, device, stream)   # ours: cleaned in place on the device
     else:
         raw = _as_matrix(mat_file)
     shard_flag = _lib.TP_FLAG_SHARDED if sharded else 0

@@ -1352,6 +1352,25 @@ void tp_read_tsv(const char **path, const int *nrow, const int *ncol, const int 
         tp::tsv_read(*path, *nrow, *ncol, th, flags && (*flags & TP_FLAG_ROW_MAJOR), out);
     });
 }
+
+void tp_read_tsv_dev(const char **path, const int *nrow, const int *ncol, const int *nthreads, const int *device,
+                     void *stream, double *d_out, int *status) {
+    guarded(status, [&] {
+        if (!path || !*path || !nrow || !ncol || !d_out || *nrow < 0 || *ncol < 0) fail(TP_ERR_ARG, "null argument");
+        const int th = (nthreads && *nthreads > 0) ? *nthreads : (int)std::max(1u, std::thread::hardware_concurrency());
+        Ctx &c = ctx_for(dev_of(device), (hipStream_t)stream);
+        const size_t ld = (size_t)*ncol;
+        // the context's pinned staging (kept across calls): each parsed row
+        // block is copied to the device while the next one is parsed
+        double *stage = (double *)c.pinned(std::max<size_t>(1, (size_t)*nrow * ld) * sizeof(double));
+        tp::tsv_read_rows(*path, *nrow, *ncol, th, stage, 8, [&](size_t r0, size_t r1) {
+            if (r1 > r0)
+                TP_HIP(hipMemcpyAsync(d_out + r0 * ld, stage + r0 * ld, (r1 - r0) * ld * sizeof(double),
+                                      hipMemcpyHostToDevice, c.cur));
+        });
+        stream_sync(c, c.cur);   // the staging is reused by the next call on this context
+    });
+}
 }  // extern "C"
 
 extern "C" {

@@ -8,6 +8,7 @@
 #include <cstdint>
 #include <mutex>
 #include <string>
+#include <functional>
 #include <vector>
 
 #include "../../include/tadpole_hip.h"
@@ -282,6 +283,9 @@ void eig_sym(rocblas_handle h, double *A, int b, double *theta, double *work, in
 // tp_io.hip: native reader of read.big.matrix(sep = '\t') files (host code)
 void tsv_dims(const char *path, int *nrow, int *ncol);
 void tsv_read(const char *path, int nrow, int ncol, int nthreads, bool row_major, double *out);
+// row-major, in row blocks, on_block(r0, r1) as each block completes
+void tsv_read_rows(const char *path, int nrow, int ncol, int nthreads, double *out, int nblocks,
+                   const std::function<void(size_t, size_t)> &on_block);
 
 // sharding (tp_shard.hip)
 void comm_unique_id(char *id128);

@@ -413,6 +413,41 @@ def test_pipeline_file_input_and_nan(gpu, tmp_path):
     assert (got.n_pcs, got.optimal_n_clusters) == (ref.n_pcs, ref.optimal_n_clusters)
 
 
+def test_read_tsv_dev_blocks_equal_host_parse(gpu, tmp_path):
+    # tp_read_tsv_dev (parse in 8 row blocks on 4 threads, each block's upload
+    # overlapping the next block's parse) gives the host parser's bits: reals,
+    # NA, a short line padded with NaN, CRLF line ends
+    import ctypes
+    import torch
+    from tadpole_amd import _lib, read_matrix
+    rng = np.random.default_rng(7)
+    n = 400
+    m = rng.standard_normal((n, n)) * 1e3
+    lines = ["\t".join(f"{v:.17g}" for v in row) for row in m]
+    lines[5] = lines[5].replace(lines[5].split("\t")[7], "NA", 1)
+    lines[9] = "\t".join(lines[9].split("\t")[:n - 3])
+    f = tmp_path / "blocks.tsv"
+    f.write_bytes(("\r\n".join(lines) + "\r\n").encode())
+    host = read_matrix(str(f))
+    assert np.isnan(host[5, 7]) and np.all(np.isnan(host[9, n - 3:]))
+    d = torch.full((n, n), -1.0, dtype=torch.float64, device="cuda:0")
+    st = ctypes.c_int(0)
+    path = ctypes.c_char_p(str(f).encode())
+    s = torch.cuda.current_stream(0)
+    gpu.tp_read_tsv_dev(ctypes.byref(path), ctypes.byref(ctypes.c_int(n)), ctypes.byref(ctypes.c_int(n)),
+                        ctypes.byref(ctypes.c_int(4)), ctypes.byref(ctypes.c_int(0)), ctypes.c_void_p(s.cuda_stream),
+                        ctypes.c_void_p(d.data_ptr()), ctypes.byref(st))
+    _lib.check(st)
+    got = d.cpu().numpy()
+    assert np.array_equal(got.view(np.uint64)[~np.isnan(host)], host.view(np.uint64)[~np.isnan(host)])
+    assert np.array_equal(np.isnan(got), np.isnan(host))
+    # wrong row count: an argument error, not a partial matrix
+    gpu.tp_read_tsv_dev(ctypes.byref(path), ctypes.byref(ctypes.c_int(n + 1)), ctypes.byref(ctypes.c_int(n)),
+                        ctypes.byref(ctypes.c_int(4)), ctypes.byref(ctypes.c_int(0)), ctypes.c_void_p(s.cuda_stream),
+                        ctypes.c_void_p(d.data_ptr()), ctypes.byref(st))
+    assert st.value == _lib.TP_ERR_ARG
+
+
 def test_pipeline_errors(gpu):
     import tadpole_amd as tp
     with pytest.raises(tp.TadpoleError):

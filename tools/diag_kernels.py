@@ -65,7 +65,7 @@ def coniss(n0=2000, k=200):
     nb = {8: "rec read", 9: "row wait+sums", 10: "ward+records", 11: "wait X", 14: "prefetch", 15: "wait Y"}
     print(f"coniss n={n} k={k}: stamped kernel {ms.value:.3f} ms ({ms.value * 1e3 / (n - 1):.2f} us/merge)",
           flush=True)
-    for i in (0, 63, 127, k - 1):
+    for i in (0, 63, 127, 128, 160, 191, 192, k - 1):
         print(f"  tree {i + 1:3d}: A " + ", ".join(f"{v} {s[i, q]:.0f}" for q, v in na.items()) +
               f" (sum {sum(s[i, q] for q in na):.0f})", flush=True)
         print(f"            B " + ", ".join(f"{v} {s[i, q]:.0f}" for q, v in nb.items()) +
