@@ -481,13 +481,21 @@ def _assemble(res, bad_idx1) -> Tadpole:
         names = np.concatenate([good1, np.asarray(bad_idx1)]).astype(np.float64)
         if not np.all(np.diff(good1.astype(np.float64)) > 0):
             return _assemble_rle(t, dendro, levels, good1, bad_idx1)
-        order = np.argsort(names, kind="stable")
-        rank = np.empty(len(names), np.int64)
-        rank[order] = np.arange(1, len(names) + 1)
-        pos = rank[:n]
-    bnd = np.asarray(res["boundary"], np.int64)
-    for kk, co in zip(levels, _all_level_coords(bnd, n, levels, pos)):
-        t.clusters[str(int(kk))] = co
+        tot = len(names)
+        seen = np.zeros(tot + 1, bool)
+        ok = names.min() >= 1 and names.max() <= tot
+        if ok:
+            seen[names.astype(np.int64)] = True
+        if ok and seen[1:].all():
+            # the names are 1..N (a full matrix's good + bad bins): the rank of
+            # each good bin in order(c(good, bad)) is its own name
+            pos = good1.astype(np.int64)
+        else:
+            order = np.argsort(names, kind="stable")
+            rank = np.empty(tot, np.int64)
+            rank[order] = np.arange(1, tot + 1)
+            pos = rank[:n]
+    t.clusters.update(zip(map(str, levels.tolist()), _all_level_coords(res["boundary"], n, levels, pos)))
     return t
 
 
