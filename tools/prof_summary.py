@@ -38,7 +38,9 @@ def short(name):
 def main():
     tag = sys.argv[1]
     bench = json.load(open(os.path.join(OUT, "prof_bench.json")))
-    steps = bench["steps"] + bench["warmup"]              # timed + warmup pipelines
+    # timed + warmup pipelines + the untimed ones bench.py runs after the timed
+    # region with per-product events on (max(2, min(5, steps)))
+    steps = bench["steps"] + bench["warmup"] + max(2, min(5, bench["steps"]))
     stats = list(csv.DictReader(open(os.path.join(OUT, "prof", "run_kernel_stats.csv"))))
     shutil.copy(os.path.join(OUT, "prof", "run_kernel_stats.csv"),
                 os.path.join(ROOT, "profiles", f"{tag}_kernel_stats.csv"))
