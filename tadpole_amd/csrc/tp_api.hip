@@ -1506,7 +1506,8 @@ extern "C" {
  * order of the int8 X'X tiles, ..., 17 C's column means formed by the correlation epilogue, 18 the
  * correlation epilogue in the int8 X'X store (with the gather's statistics), ..., 25 events around
  * every Krylov product when timings are requested (0: stage and one-launch classes only), 26 products
- * with the block-tridiagonal Krylov projection T skip its zero blocks (0: dense GEMM). */
+ * with the block-tridiagonal Krylov projection T skip its zero blocks (0: dense GEMM), 28 the
+ * Krylov CGS2's first pass against the last two blocks only (0: against every block). */
 void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
     guarded(status, [&] {
         int *p = nullptr;
@@ -1538,6 +1539,7 @@ void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
         case 24: p = &g_shard_slab; break;
         case 25: p = &g_kprof_fine; break;
         case 26: p = &g_pca_band; break;
+        case 28: p = &g_krylov_local; break;
         default: fail(TP_ERR_ARG, "unknown knob");
         }
         if (*which == 3 && *value != 16 && *value != 32) fail(TP_ERR_ARG, "stage depth must be 16 or 32");

@@ -371,6 +371,7 @@ extern int g_ckry_steps;       // C-Krylov blocks before the first check (0: fro
 void small_topk_T(Ctx &c, double *Tm, int D, int k, double *Vs, std::vector<double> &h_theta, PcaStats &sst,
                   int band_p = 0);
 extern int g_pca_band;
+extern int g_krylov_local;   // Krylov CGS pass 0 against the last two blocks (1) or all (0)
 // false: an orthogonalisation pass broke down (the caller takes the G path)
 bool krylov_c_topk(Ctx &c, double *C, int c_col0, const double *mext, int n, int k, double *V, double *P,
                    std::vector<double> &h_theta, PcaStats &st);

@@ -487,6 +487,7 @@ static void subspace_topk(Ctx &c, const double *A, int n, int k, const Prod &pro
 // D, symmetric, ld D) by the subspace iteration above (products with T are
 // D x D GEMMs, the Chebyshev step in their split-K reduction).  Vs: D x k.
 int g_pca_band = 1;
+int g_krylov_local = 1;   // CGS pass 0 against the last two Krylov blocks only (0: every block)
 
 static void band_ty(const double *T, const double *Y, double *Out, int D, int b, int p, bool aff, double a, double bc,
                     const double *Yc, double cc, const double *Yp, hipStream_t s) {
@@ -591,13 +592,21 @@ static void krylov_topk(Ctx &c, double *C, int c_col0, const double *mext, int n
                 // K_t: G K_{t-1} re-orthogonalised twice against K_0..K_{t-1} (CGS2), CholQR2.
                 // W = src - K (K'src) in the product's epilogue (src = G K_{t-1}, then W)
                 const int D = t * p;
+                // Pass 0 against the last two blocks only (knob 28): G K_{t-1}
+                // lies in span(K_{t-2}, K_{t-1}, K_t) in exact arithmetic, so
+                // the older blocks' coefficients are rounding-level, and pass
+                // 1 (against every block) removes them -- local
+                // orthogonalisation + full reorthogonalisation, half the
+                // streaming of K.  T's band needs only those two blocks of H1.
                 for (int pass = 0; pass < 2; ++pass) {
                     const double *src = pass == 0 ? GK + (size_t)(t - 1) * np : W;
-                    double *Hc = (pass == 0 ? H1 : H2) + (size_t)(t - 1) * p * Dm;   // column block t - 1
-                    GemmArgs pr{D, p, n, K, n, true, src, n, Hc, Dm};   // K'src
+                    const int D0 = (pass == 0 && g_krylov_local) ? std::max(0, (t - 2) * p) : 0;
+                    double *Hc = (pass == 0 ? H1 : H2) + (size_t)(t - 1) * p * Dm + D0;   // column block t - 1
+                    const double *Kc = K + (size_t)D0 * n;
+                    GemmArgs pr{D - D0, p, n, Kc, n, true, src, n, Hc, Dm};   // K'src
                     pr.splitk = 0;
                     gemm_f64(pr, c.buf[S_PARTIAL], s);
-                    GemmArgs up{n, p, D, K, n, false, Hc, Dm, W, n};   // W = src - K (K'src)
+                    GemmArgs up{n, p, D - D0, Kc, n, false, Hc, Dm, W, n};   // W = src - K (K'src)
                     up.splitk = 0;
                     up.sub_from = src;
                     gemm_f64(up, c.buf[S_PARTIAL], s);
