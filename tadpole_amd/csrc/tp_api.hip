@@ -1507,7 +1507,8 @@ extern "C" {
  * correlation epilogue in the int8 X'X store (with the gather's statistics), ..., 25 events around
  * every Krylov product when timings are requested (0: stage and one-launch classes only), 26 products
  * with the block-tridiagonal Krylov projection T skip its zero blocks (0: dense GEMM), 28 the
- * Krylov CGS2's first pass against the last two blocks only (0: against every block). */
+ * Krylov CGS2's first pass against the last two blocks only (0: against every block), 29 CholQR
+ * Gram matrices of 64-column blocks by k_gram64 (0: the split-K GEMM; same bits). */
 void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
     guarded(status, [&] {
         int *p = nullptr;
@@ -1540,6 +1541,7 @@ void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
         case 25: p = &g_kprof_fine; break;
         case 26: p = &g_pca_band; break;
         case 28: p = &g_krylov_local; break;
+        case 29: p = &g_gram64; break;
         default: fail(TP_ERR_ARG, "unknown knob");
         }
         if (*which == 3 && *value != 16 && *value != 32) fail(TP_ERR_ARG, "stage depth must be 16 or 32");

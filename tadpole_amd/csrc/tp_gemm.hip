@@ -644,6 +644,36 @@ __global__ void __launch_bounds__(256) k_splitk_reduce4(const double *part, size
 }
 int g_gemm_splitk = 1;   // auto split-K policy: 1 = deep splits for few-tile long-K products, 0 = round-1 policy
 
+// Split-K plan of the 64 x 64 kernel (shared with k_gram64, which must chunk
+// K exactly as that kernel would to give the same bits).
+static void split_plan(const GemmArgs &g, long nblk, int &S, int &kchunk) {
+    S = g.splitk;
+    if (S < 1) {
+        // auto: fill the 256 CUs when the output has few tiles and K is long
+        S = 1;
+        if (nblk < 192 && g.K >= 512) S = (int)std::min<long>(8, std::max<long>(1, (384 + nblk - 1) / nblk));
+        S = std::min(S, std::max(1, g.K / 128));
+        if (g_gemm_splitk && nblk <= 64 && g.K >= 512) {
+            // few output tiles, long K (Gram matrices Z'Z, the Krylov K'W, T Y):
+            // one k-chunk is otherwise a long chain of dependent stages on a
+            // quarter of the chip.  ~1024 workgroups, chunks of >= 8 stages
+            // (>= 4 for a single tile), partials bounded by ~1/64 of the
+            // operand bytes the product streams.
+            const int kmin = nblk <= 4 ? 64 : 128;
+            long s2 = std::min<long>(g.K / kmin, (1024 + nblk - 1) / nblk);
+            const double outb = 8.0 * g.M * g.N;
+            const double budget = std::max(16.0e6, 8.0 * g.M * (double)g.N * g.K / 64.0);
+            s2 = std::min<long>(s2, (long)(budget / outb));
+            s2 = std::min<long>(s2, 128);
+            if (s2 > S) S = (int)s2;
+        }
+    }
+    kchunk = ((g.K + S - 1) / S + BK - 1) / BK * BK;   // multiple of 16 for either stage depth
+    if (kchunk < BK) kchunk = BK;
+    S = (g.K + kchunk - 1) / kchunk;
+    if (S < 1) S = 1;
+}
+
 void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s) {
     if (g.M <= 0 || g.N <= 0) return;
     if (g.sub_from && (g.sym_upper || g.store_t || g.rows))
@@ -756,31 +786,8 @@ void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s) {
             return;
         }
     }
-    int S = g.splitk;
-    if (S < 1) {
-        // auto: fill the 256 CUs when the output has few tiles and K is long
-        S = 1;
-        if (nblk < 192 && g.K >= 512) S = (int)std::min<long>(8, std::max<long>(1, (384 + nblk - 1) / nblk));
-        S = std::min(S, std::max(1, g.K / 128));
-        if (g_gemm_splitk && nblk <= 64 && g.K >= 512) {
-            // few output tiles, long K (Gram matrices Z'Z, the Krylov K'W, T Y):
-            // one k-chunk is otherwise a long chain of dependent stages on a
-            // quarter of the chip.  ~1024 workgroups, chunks of >= 8 stages
-            // (>= 4 for a single tile), partials bounded by ~1/64 of the
-            // operand bytes the product streams.
-            const int kmin = nblk <= 4 ? 64 : 128;
-            long s2 = std::min<long>(g.K / kmin, (1024 + nblk - 1) / nblk);
-            const double outb = 8.0 * g.M * g.N;
-            const double budget = std::max(16.0e6, 8.0 * g.M * (double)g.N * g.K / 64.0);
-            s2 = std::min<long>(s2, (long)(budget / outb));
-            s2 = std::min<long>(s2, 128);
-            if (s2 > S) S = (int)s2;
-        }
-    }
-    int kchunk = ((g.K + S - 1) / S + BK - 1) / BK * BK;   // multiple of 16 for either stage depth
-    if (kchunk < BK) kchunk = BK;
-    S = (g.K + kchunk - 1) / kchunk;
-    if (S < 1) S = 1;
+    int S = 0, kchunk = 0;
+    split_plan(g, nblk, S, kchunk);
     // 1-D grid of tiles x k chunks (the kernel maps it XCD-aware)
     dim3 grid((unsigned)(nblk * S), 1, 1);
     double *out = g.C;
@@ -836,5 +843,82 @@ void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s) {
         TP_HIP(hipGetLastError());
     }
 }
+
+// ---------------------------------------------------------------------------
+// Gram matrix Z'Z of a tall 64-column block (the Krylov CholQR Gram matrices):
+// the 64 x 64 kernel's split-K chunks, but each workgroup stages its whole
+// chunk of rows in LDS once (both operands read from it, one load latency, no
+// stage barriers) and computes all 16 tiles.  Same chunks as split_plan gives
+// the 64 x 64 kernel, k ascending in steps of 4 from the chunk start with the
+// last stage zero-padded to 16 rows, and the same partial layout: the partials
+// -- and after the same reduction, the Gram matrix -- are bit-identical.
+constexpr int GRM = 128;   // most rows of a chunk
+__global__ void __launch_bounds__(256) k_gram64(const double *__restrict__ Z, int n, int ldz, int kchunk,
+                                                double *__restrict__ part, size_t pstride) {
+    __shared__ double Zs[GRM][65];
+    const int z = blockIdx.x;
+    const int k0 = z * kchunk, k1 = min(n, k0 + kchunk);
+    const int rows16 = ((k1 - k0) + 15) & ~15;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    // lane = row (64 consecutive doubles of a column per load), wave w =
+    // columns w, w + 4, ...
+#pragma unroll 4
+    for (int c = w; c < 64; c += 4) {
+        const double *zc = Z + (size_t)c * ldz;
+        for (int r = lane; r < rows16; r += 64) {
+            const int k = k0 + r;
+            Zs[r][c] = k < k1 ? zc[k] : 0.0;
+        }
+    }
+    __syncthreads();
+    const int fr = lane & 15, fk = lane >> 4;
+    d4 acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = (d4){0.0, 0.0, 0.0, 0.0};
+    for (int k = 0; k < rows16; k += 4) {
+        const double af = Zs[k + fk][16 * w + fr];   // A[i][k] = Z[k][i]
+        double bf[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bf[j] = Zs[k + fk][16 * j + fr];   // B[k][j] = Z[k][j]
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af, bf[j], acc[j], 0, 0, 0);
+    }
+    double *P = part + pstride * z;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) P[(size_t)(16 * w + fk + 4 * r) + (size_t)(16 * j + fr) * 64] = acc[j][r];
+}
+int g_gram64 = 0;   // CholQR Gram of 64-column blocks by k_gram64 (0: the 64 x 64 split-K kernel; same bits)
+
+bool gram64(const double *Z, int n, int ldz, double *W, DevBuf &work, hipStream_t s) {
+    if (!g_gram64 || n < 1) return false;
+    GemmArgs g{64, 64, n, Z, ldz, true, Z, ldz, W, 64};
+    g.sym_upper = true;
+    g.splitk = 0;
+    int S = 0, kchunk = 0;
+    split_plan(g, 1, S, kchunk);
+    if (kchunk > GRM) return false;
+    double *out = W;
+    size_t pstride = 0;
+    if (S > 1) {
+        pstride = (size_t)64 * 64;
+        out = work.as<double>(pstride * S);
+    }
+    hipLaunchKernelGGL(k_gram64, dim3((unsigned)S), dim3(256), 0, s, Z, n, ldz, kchunk, out, pstride);
+    TP_HIP(hipGetLastError());
+    if (S > 1) {   // the reduction gemm_f64 would run
+        const size_t tot = (size_t)64 * 64;
+        if (S >= 16)
+            hipLaunchKernelGGL(k_splitk_reduce4, dim3((unsigned)((tot + 63) / 64)), dim3(256), 0, s, out, pstride, S, 64,
+                               64, W, 64, 0, (const double *)nullptr);
+        else
+            hipLaunchKernelGGL(k_splitk_reduce<0>, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, out, pstride,
+                               S, 64, 64, W, 64, 0, (const double *)nullptr);
+        TP_HIP(hipGetLastError());
+    }
+    return true;
+}
+
 
 }  // namespace tp

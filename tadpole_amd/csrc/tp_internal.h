@@ -185,6 +185,10 @@ extern int g_chol_inv_waves;
 extern int g_gemm_splitk;
 extern int g_gemm_ts;
 extern int g_gemm_ts32;
+extern int g_gram64;
+// Z'Z (64 x 64, ld 64) of an n x 64 block by k_gram64, bit-identical to the
+// symmetric split-K GEMM; false: not applicable (the caller runs gemm_f64)
+bool gram64(const double *Z, int n, int ldz, double *W, DevBuf &work, hipStream_t s);
 extern int g_xtx_supertile;   // int8 X'X: XCD-contiguous supertile order of the 128 x 128 tiles (0: columns)
 // row-shardable products that take the 128 x 64 kernel with k chunks fixed by K
 // (tp_gemm.hip); shards and the unsharded call must agree on it

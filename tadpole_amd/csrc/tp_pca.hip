@@ -116,7 +116,7 @@ static void orth_cholqr(Ctx &c, double *Z, double *Qout, double *Tmp, int n, int
         GemmArgs g{b, b, n, src, n, true, src, n, W, b};
         g.sym_upper = true;
         g.splitk = 0;   // auto: deep split for few-tile Gram matrices (tp_gemm.hip)
-        gemm_f64(g, c.buf[S_PARTIAL], c.cur);
+        if (!(b == 64 && gram64(src, n, n, W, c.buf[S_PARTIAL], c.cur))) gemm_f64(g, c.buf[S_PARTIAL], c.cur);
         double *dst = ((passes - 1 - p) % 2 == 0) ? Qout : Tmp;   // last pass lands in Qout
         if (b <= kCholInvMax && b % 16 == 0) {
             launch_chol_inv(W, Y, X + b, X, b, p == 0 ? shift : 0.0, d_info, c.cur);

@@ -115,6 +115,28 @@ def test_pca_krylov_path_vs_lapack(gpu, forced, space):
         assert np.abs(proj(p, i) - proj(op, i)).max() < 1e-7, i
 
 
+def test_gram64_same_bits_as_split_k_gemm(gpu):
+    """The CholQR Gram matrices of the Krylov blocks by k_gram64 (knob 29) and
+    by the 64 x 64 split-K GEMM give the same bits: the whole Krylov PCA's
+    scores are identical."""
+    n0 = 2600
+    m = synth_hic(n0, SEED_BASE + 79)
+    cm = O.clean_symmetrize(m)
+    obad, _, _ = O.bad_mask(cm, 0.01)
+    g = np.flatnonzero(~obad)
+    c = O.sparse_cor(cm[np.ix_(g, g)])
+    old8 = G.knob(8, 0)
+    old29 = G.knob(29, 1)
+    try:
+        p1, _ = G.pca(c, 200)
+        G.knob(29, 0)
+        p0, _ = G.pca(c, 200)
+    finally:
+        G.knob(8, old8)
+        G.knob(29, old29)
+    assert np.array_equal(p1.view(np.uint64), p0.view(np.uint64))
+
+
 @pytest.mark.parametrize("space", ["C", "G"])
 def test_pipeline_krylov_forced_end_to_end(gpu, space):
     """A whole TADpole() through the Krylov PCA (in C or in G) at a size the
