@@ -31,7 +31,12 @@ North-star lines (same JSON object, after the C3 headline; --no-extras skips):
                parity against tests/golden/c5arm.npz (rank 0 at N=1);
   "c4_genome"  the 23 hg19 chromosomes @25 kb through run_genome over all
                ranks (LPT, 8 streams a GPU), parity of four chromosomes
-               against their golden fixtures.
+               against their golden fixtures;
+  "c5_full"    BASELINE config 5: TADpole(centromere_search=TRUE) on the
+               49 851-bin chr1 @5kb matrix, one GPU at N=1 (plus a one-rank
+               RCCL sharded run checked bit for bit), every arm sharded over
+               all ranks at N > 1 (--no-c5 skips), parity against
+               tests/golden/c5full.npz.
 
 Extra fields: "roofline" for the kernel class with the largest time per
 pipeline (HIP events recorded inside the library on the stream the kernels run
@@ -113,6 +118,7 @@ def parse():
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the north-star lines (e2e_10k, c5_arm, c4_genome)")
     ap.add_argument("--extras-reps", type=int, default=3)
+    ap.add_argument("--no-c5", action="store_true", help="skip the c5_full line (49 851-bin config 5)")
     return ap.parse_args()
 
 
@@ -141,6 +147,11 @@ def relaunch_if_needed(args, script=None, argv=None):
 
 
 STAGES = ["mask", "cor", "pca", "sweep", "total"]
+
+
+def torch_device() -> int:
+    import torch
+    return torch.cuda.current_device()
 
 
 def _stages(timings):
@@ -261,16 +272,20 @@ def run_c4_genome(world, rank, max_pcs, reps, streams=8):
     t0 = time.perf_counter()
     mats = {c: (genome_matrix(c) if c in plan[rank] else (lambda c=c: genome_matrix(c))) for c in sizes}
     t_gen = time.perf_counter() - t0
+    from tadpole_amd import _lib
     run_genome(mats, sizes=sizes, streams=streams, max_pcs=max_pcs)     # warm-up (contexts, code objects)
-    walls, res = [], None
+    walls, res, rep_secs = [], None, []
+    ctx0 = _lib.context_stats(torch_device())[1]
     for _ in range(max(1, reps)):
         if world > 1:
             dist.barrier()
         t0 = time.perf_counter()
-        res, _ = run_genome(mats, sizes=sizes, streams=streams, max_pcs=max_pcs)
+        res, secs = run_genome(mats, sizes=sizes, streams=streams, max_pcs=max_pcs)
         if world > 1:
             dist.barrier()
         walls.append(time.perf_counter() - t0)
+        rep_secs.append(secs)
+    ctx_new = _lib.context_stats(torch_device())[1] - ctx0
     if rank != 0:
         return None
     bins = sum(sizes.values())
@@ -278,6 +293,10 @@ def run_c4_genome(world, rank, max_pcs, reps, streams=8):
     out = {"chromosomes": len(sizes), "bins": bins, "ranks": world, "streams_per_rank": streams,
            "wall_s_median": round(wall, 4), "all_s": [round(x, 4) for x in walls],
            "bins_per_s": round(bins / wall, 1), "matrix_build_s_rank0": round(t_gen, 2),
+           # seconds of each chromosome's TADpole() call (every rank's, gathered) per timed rep,
+           # and the library contexts rank 0 created during the timed reps (0: the stream pool reuses them)
+           "chrom_s_per_rep": [{c: round(v, 4) for c, v in sorted(sc.items())} for sc in rep_secs],
+           "contexts_created_in_timed_reps_rank0": ctx_new,
            "workload": "C4: 23 hg19 chromosomes @25 kb (synthetic, synth_hic_par), max_pcs=%d, one run_genome "
                        "call; host-resident matrices (H2D copies and host assembly included)" % max_pcs}
     par = {}
@@ -287,6 +306,161 @@ def run_c4_genome(world, rank, max_pcs, reps, streams=8):
             ok, rel = _golden_check(res[c], np.load(gold))
             par[c] = {"match": ok, "ch_max_rel_err": rel}
     if par:
+        out["parity"] = par
+    return out
+
+
+C5_BINS = 49851
+C5_CHUNK_ROWS = 4096
+
+
+def _c5_resident(world, rank, local):
+    """BASELINE config 5's matrix (chr1 @5kb: synth_hic_par(49 851, seed
+    20261015+5, centromere=True), the input of tests/golden/c5full.npz) resident
+    in HBM on every rank.  Rank 0 draws it on the host and checks its checksum
+    against the fixture; with several ranks it travels to the others over the
+    gloo control group in row chunks (4096 rows = 1.6 GB at a time: a rank
+    other than 0 never holds more than one chunk on the host, and no GPU
+    collective is involved).  Setup, outside every timing."""
+    import torch
+    import torch.distributed as dist
+    from tadpole_amd.synth import SEED_BASE, matrix_checksum, synth_hic_par
+    n0 = C5_BINS
+    info = {}
+    dm = torch.empty((n0, n0), dtype=torch.float64, device=f"cuda:{local}")
+    host = None
+    if rank == 0:
+        t0 = time.perf_counter()
+        host = synth_hic_par(n0, SEED_BASE + 5, centromere=True)
+        info["matrix_build_s"] = round(time.perf_counter() - t0, 2)
+        gold = os.path.join(HERE, "tests", "golden", "c5full.npz")
+        if os.path.exists(gold):
+            info["matrix_checksum_match"] = bool(np.array_equal(matrix_checksum(host),
+                                                                np.load(gold)["matrix_checksum"]))
+    t0 = time.perf_counter()
+    distribute_rows(host, n0, world, rank, lambda r0, r1, t: dm[r0:r1].copy_(t))
+    torch.cuda.synchronize()
+    info["distribute_s"] = round(time.perf_counter() - t0, 2)
+    del host
+    return dm, info
+
+
+def distribute_rows(host, n0, world, rank, sink, chunk_rows=C5_CHUNK_ROWS):
+    """Rank 0's n0 x n0 host matrix to every rank, row chunk by row chunk:
+    sink(r0, r1, rows) receives rows [r0, r1) as a CPU tensor on each rank
+    (broadcast over the default -- gloo -- group when world > 1)."""
+    import torch
+    import torch.distributed as dist
+    for r0 in range(0, n0, chunk_rows):
+        r1 = min(n0, r0 + chunk_rows)
+        if world > 1:
+            buf = (torch.from_numpy(np.ascontiguousarray(host[r0:r1])) if rank == 0
+                   else torch.empty((r1 - r0, n0), dtype=torch.float64))
+            dist.broadcast(buf, src=0)
+        else:
+            buf = torch.from_numpy(np.ascontiguousarray(host[r0:r1]))
+        sink(r0, r1, buf)
+
+
+def c5_mode(world):
+    """How the c5_full line runs at this rank count: one GPU unsharded (plus a
+    one-rank RCCL check), or every arm sharded over all ranks."""
+    return "sharded" if world > 1 else "one_gpu"
+
+
+def run_c5_full(world, rank, local, max_pcs, reps):
+    """BASELINE config 5 end to end: TADpole(centromere_search=TRUE) on the
+    49 851-bin chr1 @5kb matrix resident in HBM (R/TADpole.R:58-85,351-442:
+    mask, centromere split, the p (~24.3k bins) and q (~21.3k, bug-compatible)
+    arms, merging_arms).  One GPU: the plain pipeline per arm.  N ranks: every
+    arm's products split over all ranks through the library's RCCL
+    communicator (column slabs of C, row-split Krylov products, tree-split
+    sweep), the time the max over ranks.  Parity: bit-exact
+    TAD coordinates / merge order / n_pcs / optimal_n_clusters of both arms
+    and merging_arms, CH <= 1e-6, against tests/golden/c5full.npz (the CPU
+    oracle on the same matrix); one GPU also checks a one-rank sharded run
+    against the unsharded one bit for bit."""
+    import torch
+    import torch.distributed as dist
+    from tadpole_amd import multi
+    from tadpole_amd.api import TADpole
+    dm, info = _c5_resident(world, rank, local)
+    sharded = c5_mode(world) == "sharded"
+    comm_size = None
+    if sharded:
+        comm_size = multi.init_comm(device=local)[1]
+
+    def once():
+        return TADpole(dm, max_pcs=max_pcs, centromere_search=True, sharded=sharded, inplace=True)
+
+    try:
+        once()                                     # warm-up (scratch of these sizes)
+        ts, res = [], None
+        for _ in range(max(1, reps)):
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            res = once()
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t0
+            if world > 1:
+                t = torch.tensor([el], dtype=torch.float64)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                el = float(t.item())
+            ts.append(el)
+        one_rank = None
+        if world == 1:
+            # the sharded schedule through a real one-rank RCCL communicator
+            # must give the unsharded bits
+            uid = multi.comm_unique_id()
+            multi._lib_init(uid, 1, 0, local)
+            try:
+                sh = TADpole(dm, max_pcs=max_pcs, centromere_search=True, sharded=True, inplace=True)
+            finally:
+                multi.destroy_comm(local)
+            one_rank = bool(np.array_equal(sh.merging_arms, res.merging_arms) and all(
+                np.array_equal(getattr(sh, a).scores.view(np.uint64), getattr(res, a).scores.view(np.uint64))
+                and np.array_equal(getattr(sh, a).dendro.boundary, getattr(res, a).dendro.boundary)
+                and np.array_equal(getattr(sh, a).dendro.height.view(np.uint64),
+                                   getattr(res, a).dendro.height.view(np.uint64))
+                for a in ("p", "q")))
+    finally:
+        if sharded:
+            multi.destroy_comm(local)
+        del dm
+        torch.cuda.empty_cache()
+    if rank != 0:
+        return None
+    med = float(np.median(ts))
+    out = {"n0": C5_BINS, "ranks": world, "reps": len(ts), "s_median": round(med, 4),
+           "all_s": [round(x, 4) for x in ts], "bins_per_s": round(C5_BINS / med, 1),
+           "workload": ("C5: chr1 @5kb shape, synthetic 49851x49851 Hi-C (synth_hic_par, seed 20261015+5, "
+                        "centromere run at [0.4875, 0.572) N0), TADpole(centromere_search=TRUE) bug-compatible, "
+                        "max_pcs=%d, resident in HBM, " % max_pcs +
+                        (f"every arm sharded over {world} GPUs (RCCL)" if sharded else "one GPU")),
+           "arms": {}}
+    out.update(info)
+    if comm_size is not None:
+        out["rccl_comm_size"] = comm_size
+    if one_rank is not None:
+        out["sharded_1rank_bit_identical"] = one_rank
+    for a in ("p", "q"):
+        r = getattr(res, a)
+        out["arms"][a] = {"n": int(r.timings_ms[14]), "k": int(r.timings_ms[15]), "stages_ms": _stages(r.timings_ms),
+                          "xtx_ms": round(float(r.timings_ms[5]), 3), "coniss_ms": round(float(r.timings_ms[9]), 3),
+                          "krylov_steps": int(r.timings_ms[16]), "pca_resid": float(r.timings_ms[13]),
+                          "n_pcs": r.n_pcs, "optimal_n_clusters": r.optimal_n_clusters}
+    gold = os.path.join(HERE, "tests", "golden", "c5full.npz")
+    if os.path.exists(gold) and max_pcs == 200:
+        z = np.load(gold)
+        par = {"golden_fixture": "tests/golden/c5full.npz",
+               "merging_arms_match": bool(np.array_equal(res.merging_arms, z["bug_merging_arms"]))}
+        for a in ("p", "q"):
+            ok, rel = _golden_check(getattr(res, a), z, f"bug_{a}_")
+            par[a] = {"match": ok and np.array_equal(getattr(res, a).dendro.label_ids, z[f"bug_{a}_names"]),
+                      "ch_max_rel_err": rel}
+        par["match"] = bool(par["merging_arms_match"] and par["p"]["match"] and par["q"]["match"])
         out["parity"] = par
     return out
 
@@ -310,6 +484,9 @@ def main():
         # is 4 and streams sharing a queue serialise); only before HIP starts
         if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:
             os.environ["GPU_MAX_HW_QUEUES"] = "16"
+    # a first-time collective hang in a sharded line fails that line within a
+    # minute (the library's watchdog aborts its communicator), not the run
+    os.environ.setdefault("TP_SHARD_TIMEOUT_S", "60")
     if args.e2e_tsv:
         return e2e_tsv(args)
     import torch
@@ -320,9 +497,12 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         # control only (barriers, the max of the elapsed times, the sharded
-        # path's RCCL id): no data-path collective, so gloo over TCP
+        # path's RCCL id, the C5 matrix's distribution): no data-path
+        # collective, so gloo over TCP; a bounded timeout, so a rank that died
+        # ends the run instead of parking the others for gloo's default 30 min
+        import datetime
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo")
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=300))
     # one GPU per rank; more ranks than GPUs (a rehearsal on a smaller box)
     # share devices round-robin
     ndev = max(1, torch.cuda.device_count())
@@ -498,6 +678,13 @@ def main():
         c4 = run_c4_genome(world, rank, args.max_pcs, args.extras_reps)
         if rank == 0:
             extras["c4_genome"] = c4
+        if not args.no_c5:
+            try:
+                c5 = run_c5_full(world, rank, local, args.max_pcs, args.extras_reps)
+            except Exception as e:   # noqa: BLE001 -- reported in the line; the C3 headline stands
+                c5 = {"error": f"{type(e).__name__}: {e}"}
+            if rank == 0:
+                extras["c5_full"] = c5
 
     if rank == 0:
         value = n0 * (1 if args.sharded else world) * args.steps / elapsed

@@ -73,6 +73,11 @@ void tp_shutdown(void);                         /* free every device context    
  * doubles (ABI 1: 16) -- a caller built against version 1 must pass NULL
  * timings or a 32-double buffer. */
 void tp_release_stream(const int *device, void *stream, int *status);
+/* Context bookkeeping of `device`: live = caller-stream contexts kept now,
+ * created = contexts (the library stream's included) made since the library
+ * was loaded.  A caller that reuses its streams creates none after the first
+ * call on each (tadpole_amd.genome's persistent stream pool is tested so). */
+void tp_context_stats(const int *device, int *live, int *created, int *status);
 int  tp_last_error(char *buf, int len);         /* ctypes form                   */
 void tp_last_error_r(char **buf, int *len);     /* R .C form                     */
 

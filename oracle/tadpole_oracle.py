@@ -79,12 +79,31 @@ def _ip(a):
 
 # ---------------------------------------------------------------- load_mat ---
 
-def clean_symmetrize(mat: np.ndarray) -> np.ndarray:
-    """``R/TADpole.R:19-20``: NA/NaN -> 0, then ``forceSymmetric(uplo='U')``."""
-    m = np.array(mat, dtype=np.float64, copy=True)
-    m[np.isnan(m)] = 0.0
-    iu = np.triu_indices(m.shape[0], 1)
-    m.T[iu] = m[iu]
+def clean_symmetrize(mat: np.ndarray, inplace: bool = False) -> np.ndarray:
+    """``R/TADpole.R:19-20``: NA/NaN -> 0, then ``forceSymmetric(uplo='U')``.
+    ``inplace`` (a C-contiguous float64 array, the 49 851-bin C5 fixture):
+    the same assignments in row blocks, no N^2 index arrays or copy."""
+    if not inplace:
+        m = np.array(mat, dtype=np.float64, copy=True)
+        m[np.isnan(m)] = 0.0
+        iu = np.triu_indices(m.shape[0], 1)
+        m.T[iu] = m[iu]
+        return m
+    m = mat
+    if m.dtype != np.float64 or not m.flags["C_CONTIGUOUS"]:
+        raise ValueError("inplace clean_symmetrize needs a C-contiguous float64 array")
+    n = m.shape[0]
+    blk = 256
+    for r0 in range(0, n, blk):
+        r1 = min(n, r0 + blk)
+        rows = m[r0:r1]
+        rows[np.isnan(rows)] = 0.0
+    for r0 in range(0, n, blk):        # lower (row > col) <- upper (col, row)
+        r1 = min(n, r0 + blk)
+        m[r0:r1, :r0] = m[:r0, r0:r1].T
+        sub = m[r0:r1, r0:r1]
+        il = np.tril_indices(r1 - r0, -1)
+        sub[il] = sub.T[il]
     return m
 
 
@@ -407,7 +426,7 @@ def _r_drop(n: int, neg) -> np.ndarray:
     return np.setdiff1d(np.arange(n), drop)
 
 
-def load_mat_arms(mat: np.ndarray, bad_frac: float = 0.01, fixed: bool = False):
+def load_mat_arms(mat: np.ndarray, bad_frac: float = 0.01, fixed: bool = False, inplace: bool = False):
     """``load_mat(..., centromere_search=TRUE)`` (``R/TADpole.R:15-92``)
     without plots.  Returns ``("matrix", x, names1, bad_idx1)`` when there is no
     bad bin or the longest bad run touches an end (``:66-70``), else
@@ -416,8 +435,9 @@ def load_mat_arms(mat: np.ndarray, bad_frac: float = 0.01, fixed: bool = False):
     Bug-compatible by default: the q-arm bad bins are removed with their
     ORIGINAL indices as positions in the arm-local matrix (``:78-80``), so an
     index inside the arm's length drops the wrong bin and one beyond it is
-    ignored.  ``fixed=True`` removes them at their arm-local positions."""
-    m = clean_symmetrize(mat)
+    ignored.  ``fixed=True`` removes them at their arm-local positions.
+    ``inplace``: clean ``mat`` itself (see ``clean_symmetrize``)."""
+    m = clean_symmetrize(mat, inplace)
     n0 = m.shape[0]
     bad, _, _ = bad_mask(m, bad_frac)
     idx = np.flatnonzero(bad) + 1
@@ -451,23 +471,38 @@ class ArmsResult:
 
 
 def tadpole_arms(mat: np.ndarray, max_pcs: int = 200, min_clusters: int = 2,
-                 bad_frac: float = 0.01, fixed: bool = False, nthreads: int = 0):
+                 bad_frac: float = 0.01, fixed: bool = False, nthreads: int = 0, pca: str = "svd"):
     """``TADpole(..., centromere_search=TRUE)`` (``R/TADpole.R:351-442``).
     Returns an ``ArmsResult``; when ``load_mat`` returned a plain matrix R
     fails at ``mat$centromer`` (``:356``): bug-compatible mode raises, fixed
     mode runs the single-matrix path instead."""
-    kind, *rest = load_mat_arms(mat, bad_frac, fixed)
-    if kind == "matrix":
+    loaded = load_mat_arms(mat, bad_frac, fixed)
+    if loaded[0] == "matrix":
         if not fixed:
             raise TypeError("$ operator is invalid for atomic vectors")
-        return tadpole(mat, max_pcs, min_clusters, bad_frac, nthreads=nthreads)
-    arms, cen = rest
+        return tadpole(mat, max_pcs, min_clusters, bad_frac, nthreads=nthreads, pca=pca)
+    return arms_from_loaded(loaded, max_pcs, min_clusters, nthreads, pca)
+
+
+def arms_from_loaded(loaded, max_pcs: int = 200, min_clusters: int = 2, nthreads: int = 0,
+                     pca: str = "svd", log=None) -> "ArmsResult":
+    """The arm loop and arm merge of ``R/TADpole.R:357-442`` on the output of
+    ``load_mat_arms`` (split out so a caller can free the full matrix first).
+    Each arm's matrix is dropped from ``loaded`` once its result exists."""
+    kind, arms, cen = loaded
+    if kind != "arms":
+        raise ValueError("arms_from_loaded needs load_mat_arms' arm split")
     out = {}
     parts = []
     for arm in ("p", "q"):
         x, names, bad_arm = arms[arm]
-        r = _core(x, names, bad_arm, max_pcs, min_clusters, "dd", nthreads)
+        arms[arm] = (None, names, bad_arm)
+        r = _core(x, names, bad_arm, max_pcs, min_clusters, "dd", nthreads, pca=pca)
+        del x
+        r.cor = None
         out[arm] = r
+        if log:
+            log(arm, r)
         parts += [r.fixed_opt, np.zeros(len(cen))]
     allv = np.concatenate(parts)[:-len(cen)]
     lens, v = rle(allv)

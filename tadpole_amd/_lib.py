@@ -27,7 +27,7 @@ EXPORTS = (
     "tp_mask", "tp_mask_dev", "tp_cor", "tp_pca", "tp_sweep", "tp_coniss", "tp_dist", "tp_ch",
     "tp_pipeline", "tp_pipeline_dev", "tp_sweep_dev", "tp_tsv_dims", "tp_read_tsv",
     "tp_comm_unique_id", "tp_comm_init", "tp_comm_destroy", "tp_set_virtual_shards", "tp_shard_plan",
-    "tp_level_coords", "tp_read_tsv_dev",
+    "tp_level_coords", "tp_read_tsv_dev", "tp_context_stats",
 )
 
 
@@ -92,6 +92,7 @@ def load() -> ctypes.CDLL:
     L.tp_shard_plan.argtypes = [_I, _I, _I, _I, _I]
     L.tp_level_coords.argtypes = [_I, _I, _I, _I, _I, _I, _I]
     L.tp_read_tsv_dev.argtypes = [_S, _I, _I, _I, _I, _V, _V, _I]
+    L.tp_context_stats.argtypes = [_I, _I, _I, _I]
     if L.tp_version() != ABI_VERSION:
         raise ImportError(f"{LIB_PATH}: ABI version {L.tp_version()}, this binding needs {ABI_VERSION} (rebuild)")
     _lib = L
@@ -153,3 +154,13 @@ def release_stream(stream, device: int = None) -> None:
     L.tp_release_stream(ctypes.byref(ctypes.c_int(int(device))), ctypes.c_void_p(int(handle)), ctypes.byref(st))
     check(st)
 
+
+def context_stats(device: int = 0):
+    """tp_context_stats: (caller-stream contexts kept now, contexts created on
+    ``device`` since the library was loaded)."""
+    L = load()
+    live, created, st = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
+    L.tp_context_stats(ctypes.byref(ctypes.c_int(int(device))), ctypes.byref(live), ctypes.byref(created),
+                       ctypes.byref(st))
+    check(st)
+    return live.value, created.value

@@ -22,8 +22,14 @@
 namespace tp {
 
 static thread_local std::string g_err;
+// status of the last fail() on this thread (-1: none since the last reset):
+// lets a sharded call's scope guard tell data errors from device failures
+static thread_local int t_fail_status = -1;
 
-void fail(int status, const std::string &msg) { throw Error{status, msg}; }
+void fail(int status, const std::string &msg) {
+    t_fail_status = status;
+    throw Error{status, msg};
+}
 
 // TP_TRACE_SYNC=1 (debugging hangs): synchronise and report at stage marks
 void trace_mark(hipStream_t s, const char *what) {
@@ -123,11 +129,19 @@ void kprof_collect(Ctx &c, double *ms, int *cnt) {
     c.evnext = 0;
 }
 
-static std::mutex g_mu;
-static std::shared_ptr<Ctx> g_ctx[64];
+// The registry lives on the heap and is never destroyed: contexts are freed by
+// tp_shutdown / tp_release_stream / LRU retirement, never by static
+// destructors at process exit (after the HIP runtime may be gone).
+static std::mutex &g_mu = *new std::mutex;
+static std::shared_ptr<Ctx> *const g_ctx = new std::shared_ptr<Ctx>[64];
 // contexts of caller-supplied streams: one set of scratch buffers per stream,
 // so pipelines on different streams of one device can run concurrently
-static std::vector<std::pair<hipStream_t, std::shared_ptr<Ctx>>> g_sctx[64];
+static std::vector<std::pair<hipStream_t, std::shared_ptr<Ctx>>> *const g_sctx =
+    new std::vector<std::pair<hipStream_t, std::shared_ptr<Ctx>>>[64];
+// one sharded call at a time per device: an RCCL communicator is not for
+// concurrent use from several streams, and an abort must not free it under
+// another call
+static std::mutex *const g_comm_mu = new std::mutex[64];
 // the contexts this thread's current C-ABI call holds (locked)
 static thread_local std::vector<std::shared_ptr<Ctx>> t_held;
 static unsigned long long g_tick = 0;
@@ -143,10 +157,20 @@ static size_t max_stream_ctx() {
     return v;
 }
 
+static int g_created[64];   // contexts made per device (under g_mu)
+
 static std::shared_ptr<Ctx> new_ctx(int device) {
     auto c = std::make_shared<Ctx>();
     c->device = device;
+    ++g_created[device];
     return c;
+}
+
+static void ctx_stats(int device, int *live, int *created) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (device < 0 || device >= 64) fail(TP_ERR_ARG, "device index out of range");
+    *live = (int)g_sctx[device].size();
+    *created = g_created[device];
 }
 
 Ctx &ctx_for(int device, hipStream_t stream) {
@@ -197,6 +221,7 @@ Ctx &ctx_for(int device, hipStream_t stream) {
             c->shard.rank = def->shard.rank;
             c->shard.nranks = def->shard.nranks;
             c->shard.nvirt = def->shard.nvirt;
+            c->shard.dead = def->shard.dead;
         }
         c->last_use = ++g_tick;
     }
@@ -208,6 +233,41 @@ Ctx &ctx_for(int device, hipStream_t stream) {
     TP_HIP(hipSetDevice(device));
     c->cur = c->stream;
     return *c;
+}
+
+void shard_lease_begin(Ctx &c) {
+    g_comm_mu[c.device].lock();
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        const std::shared_ptr<Ctx> &def = g_ctx[c.device];
+        if (def && def.get() != &c) {
+            c.shard.comm = def->shard.comm;
+            c.shard.rank = def->shard.rank;
+            c.shard.nranks = def->shard.nranks;
+            c.shard.nvirt = def->shard.nvirt;
+            c.shard.dead = def->shard.dead;
+        }
+    }
+    if (c.shard.dead && !c.shard.comm) {
+        g_comm_mu[c.device].unlock();
+        fail(TP_ERR_HIP, "sharded call: this device's RCCL communicator was aborted after an earlier failure; "
+                         "make a new one (tp_comm_init / tadpole_amd.multi.init_comm) first");
+    }
+}
+
+void shard_lease_end(Ctx &c) { g_comm_mu[c.device].unlock(); }
+
+bool ctx_comm_retire(Ctx &c, void *comm) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    const std::shared_ptr<Ctx> &def = g_ctx[c.device];
+    if (!def || def->shard.comm != comm) return false;   // already retired (or replaced by tp_comm_init)
+    def->shard.comm = nullptr;
+    def->shard.rank = 0;
+    def->shard.nranks = 1;
+    def->shard.dead = true;
+    // idle stream contexts keep a stale copy until their next lookup / lease,
+    // both of which re-copy it from the device's context
+    return true;
 }
 
 void ctx_unlock_held() {
@@ -222,7 +282,9 @@ void ctx_unlock_held() {
 
 Ctx::~Ctx() {
     (void)hipSetDevice(device);
-    if (stream) (void)hipStreamSynchronize(stream);
+    // a caller's stream may already be destroyed: every C-ABI call that queued
+    // work on it synchronised before returning, and hipFree waits for the device
+    if (stream && owns_stream) (void)hipStreamSynchronize(stream);
     for (auto &b : buf) b.release();
     pinned_flag.release();
     if (host_pinned) (void)hipHostFree(host_pinned);
@@ -234,6 +296,8 @@ Ctx::~Ctx() {
         (void)hipEventDestroy(join_ev);
     }
     for (auto e : evpool) (void)hipEventDestroy(e);
+    for (auto e : ring_ev)
+        if (e) (void)hipEventDestroy(e);
     if (owns_stream) (void)hipStreamDestroy(stream);
 }
 
@@ -559,16 +623,30 @@ static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_cl
     if (!(bad_frac >= 0.0 && bad_frac <= 1.0)) fail(TP_ERR_ARG, "bad_frac must be in [0, 1]");
     Timer tm(timings != nullptr, s);
     // TP_FLAG_SHARDED: this call splits its products over the ranks of the
-    // device's communicator (or its virtual shards); reset on every exit
-    // (a sharded call that throws aborts the communicator: its peers then
-    // leave their collectives through their deadline, see stream_sync)
+    // device's communicator (or its virtual shards), holding the device's
+    // communicator lease for the whole call; reset on every exit.  A sharded
+    // call that fails on a device / RCCL error (or anything that is not one of
+    // the data errors below) aborts the communicator: its peers then leave
+    // their collectives through their deadline (see stream_sync).  Data errors
+    // (bad arguments, no broken-stick level, capacity, no convergence) come
+    // from the replicated inputs and hit every rank at the same point, so the
+    // communicator stays usable.
     struct ShardScope {
         Ctx &c;
         int pending;
-        ShardScope(Ctx &cc, bool on) : c(cc), pending(std::uncaught_exceptions()) { c.shard.active = on; }
+        bool on;
+        ShardScope(Ctx &cc, bool sharded) : c(cc), pending(std::uncaught_exceptions()), on(sharded) {
+            if (on) shard_lease_begin(c);
+            t_fail_status = -1;
+            c.shard.active = on;
+        }
         ~ShardScope() {
-            if (c.shard.active && c.shard.comm && std::uncaught_exceptions() > pending) comm_abort(c);
+            const bool data_error = t_fail_status == TP_ERR_ARG || t_fail_status == TP_ERR_NO_BSTICK ||
+                                    t_fail_status == TP_ERR_CAPACITY || t_fail_status == TP_ERR_NUMERIC ||
+                                    t_fail_status == TP_ERR_UNSUPPORTED;
+            if (c.shard.active && c.shard.comm && std::uncaught_exceptions() > pending && !data_error) comm_abort(c);
             c.shard.active = false;
+            if (on) shard_lease_end(c);
         }
     } shard_scope(c, (flags & TP_FLAG_SHARDED) != 0);
     c.prof = timings != nullptr;
@@ -747,6 +825,13 @@ void tp_release_stream(const int *device, void *stream, int *status) {
     });
 }
 
+void tp_context_stats(const int *device, int *live, int *created, int *status) {
+    guarded(status, [&] {
+        if (!live || !created) fail(TP_ERR_ARG, "tp_context_stats: NULL argument");
+        ctx_stats(dev_of(device), live, created);
+    });
+}
+
 /* ------------------------------------------------------------ multi-GPU */
 void tp_comm_unique_id(char *id, int *status) {
     guarded(status, [&] { comm_unique_id(id); });
@@ -756,13 +841,19 @@ void tp_comm_init(const char *id, const int *nranks, const int *rank, const int 
     guarded(status, [&] {
         if (!id || !nranks || !rank) fail(TP_ERR_ARG, "tp_comm_init: NULL argument");
         Ctx &c = ctx_for(dev_of(device));
+        std::lock_guard<std::mutex> lease(g_comm_mu[c.device]);   // no sharded call is using the old one
         comm_init(c, id, *nranks, *rank);
     });
 }
 
 void tp_comm_destroy(const int *device) {
     int st = 0;
-    guarded(&st, [&] { comm_destroy(ctx_for(dev_of(device))); });
+    guarded(&st, [&] {
+        Ctx &c = ctx_for(dev_of(device));
+        std::lock_guard<std::mutex> lease(g_comm_mu[c.device]);
+        comm_destroy(c);
+        c.shard.dead = false;   // destroyed on purpose: the next sharded call runs on virtual shards / one rank
+    });
 }
 
 void tp_set_virtual_shards(const int *device, const int *nvirt, int *status) {
@@ -1376,14 +1467,30 @@ void tp_read_tsv_dev(const char **path, const int *nrow, const int *ncol, const 
         const int th = (nthreads && *nthreads > 0) ? *nthreads : (int)std::max(1u, std::thread::hardware_concurrency());
         Ctx &c = ctx_for(dev_of(device), (hipStream_t)stream);
         const size_t ld = (size_t)*ncol;
-        // the context's pinned staging (kept across calls): each parsed row
-        // block is copied to the device while the next one is parsed
-        double *stage = (double *)c.pinned(std::max<size_t>(1, (size_t)*nrow * ld) * sizeof(double));
-        tp::tsv_read_rows(*path, *nrow, *ncol, th, stage, 8, [&](size_t r0, size_t r1) {
-            if (r1 > r0)
-                TP_HIP(hipMemcpyAsync(d_out + r0 * ld, stage + r0 * ld, (r1 - r0) * ld * sizeof(double),
-                                      hipMemcpyHostToDevice, c.cur));
-        });
+        // a ring of 3 pinned row-block slots (~16 MB each, the context's pinned
+        // staging, kept across calls): each parsed block is copied to the device
+        // while the next ones are parsed, and a slot is refilled once its copy
+        // is done -- the staging is 3 blocks, not the matrix
+        constexpr int kSlots = 3;
+        static_assert(kSlots <= (int)(sizeof(c.ring_ev) / sizeof(c.ring_ev[0])), "Ctx::ring_ev too small");
+        for (int q = 0; q < kSlots; ++q)
+            if (!c.ring_ev[q]) TP_HIP(hipEventCreateWithFlags(&c.ring_ev[q], hipEventDisableTiming));
+        hipEvent_t *ev = c.ring_ev;
+        tp::tsv_read_rows(
+            *path, *nrow, *ncol, th, (size_t)16 << 20, kSlots,
+            [&](size_t slot_rows) { return (double *)c.pinned(kSlots * slot_rows * ld * sizeof(double)); },
+            [&](size_t r0, size_t r1, const double *rows, int slot) {
+                if (r1 > r0)
+                    TP_HIP(hipMemcpyAsync(d_out + r0 * ld, rows, (r1 - r0) * ld * sizeof(double),
+                                          hipMemcpyHostToDevice, c.cur));
+                TP_HIP(hipEventRecord(ev[slot], c.cur));
+            },
+            [&](int slot) {   // a ~16 MB copy (< 1 ms): poll with short sleeps, no spinning
+                hipError_t q;
+                while ((q = hipEventQuery(ev[slot])) == hipErrorNotReady)
+                    std::this_thread::sleep_for(std::chrono::microseconds(20));
+                TP_HIP(q);
+            });
         stream_sync(c, c.cur);   // the staging is reused by the next call on this context
     });
 }
@@ -1508,7 +1615,8 @@ extern "C" {
  * every Krylov product when timings are requested (0: stage and one-launch classes only), 26 products
  * with the block-tridiagonal Krylov projection T skip its zero blocks (0: dense GEMM), 28 the
  * Krylov CGS2's first pass against the last two blocks only (0: against every block), 29 CholQR
- * Gram matrices of 64-column blocks by k_gram64 (0: the split-K GEMM; same bits). */
+ * Gram matrices of 64-column blocks by k_gram64 (0: the split-K GEMM; same bits), 30 the next N
+ * sharded waits with a live communicator fail as device errors (failure-containment tests). */
 void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
     guarded(status, [&] {
         int *p = nullptr;
@@ -1542,6 +1650,7 @@ void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
         case 26: p = &g_pca_band; break;
         case 28: p = &g_krylov_local; break;
         case 29: p = &g_gram64; break;
+        case 30: p = &g_shard_inject; break;
         default: fail(TP_ERR_ARG, "unknown knob");
         }
         if (*which == 3 && *value != 16 && *value != 32) fail(TP_ERR_ARG, "stage depth must be 16 or 32");

@@ -46,6 +46,7 @@ struct Shard {
     int rank = 0, nranks = 1;
     int nvirt = 1;          // test hook: virtual shards on one device (no comm)
     bool active = false;    // this call runs sharded (TP_FLAG_SHARDED)
+    bool dead = false;      // the device's communicator was aborted after a failure (until tp_comm_init)
 };
 
 // Per-stream state: one stream, named scratch buffers.  Every C-ABI entry
@@ -78,6 +79,7 @@ struct Ctx {
     DevBuf pinned_flag;
     void *host_pinned = nullptr;    // small pinned staging area
     size_t host_pinned_bytes = 0;
+    hipEvent_t ring_ev[4] = {};     // tp_read_tsv_dev: one event per staging-ring slot
     void *pinned(size_t b);
 };
 
@@ -94,6 +96,14 @@ void kprof_collect(Ctx &c, double *ms_per_class, int *count_per_class);
 void ctx_shutdown_all();
 bool ctx_release_stream(int device, hipStream_t stream);   // false: no context for that stream
 void ctx_unlock_held();   // end of a C-ABI call: unlock (and maybe free) the contexts it used
+// sharded calls: exclusive use of the device's communicator for the call, with
+// the context's copy of it refreshed from the device's (shard_lease_begin
+// fails when the communicator was aborted); shard_lease_end releases it
+void shard_lease_begin(Ctx &c);
+void shard_lease_end(Ctx &c);
+// the device's communicator `comm` failed: the device forgets it (and
+// remembers that it died); true for the one caller that must ncclCommAbort it
+bool ctx_comm_retire(Ctx &c, void *comm);
 
 // Scratch slots (indices into Ctx::buf) so stages can share one context.
 enum Slot {
@@ -287,9 +297,14 @@ void eig_sym(rocblas_handle h, double *A, int b, double *theta, double *work, in
 // tp_io.hip: native reader of read.big.matrix(sep = '\t') files (host code)
 void tsv_dims(const char *path, int *nrow, int *ncol);
 void tsv_read(const char *path, int nrow, int ncol, int nthreads, bool row_major, double *out);
-// row-major, in row blocks, on_block(r0, r1) as each block completes
-void tsv_read_rows(const char *path, int nrow, int ncol, int nthreads, double *out, int nblocks,
-                   const std::function<void(size_t, size_t)> &on_block);
+// row-major, in row blocks of ~block_bytes of doubles through a ring of nslots
+// staging slots (alloc(slot_rows) -> nslots x slot_rows x ncol doubles):
+// on_block(r0, r1, rows, slot) as each block completes; slot_free(slot) must
+// return only when the slot may be overwritten (see tp_io.hip)
+void tsv_read_rows(const char *path, int nrow, int ncol, int nthreads, size_t block_bytes, int nslots,
+                   const std::function<double *(size_t)> &alloc,
+                   const std::function<void(size_t, size_t, const double *, int)> &on_block,
+                   const std::function<void(int)> &slot_free);
 
 // sharding (tp_shard.hip)
 void comm_unique_id(char *id128);
@@ -299,6 +314,7 @@ void comm_destroy(Ctx &c);
 // live communicator (see tp_shard.hip), hipStreamSynchronize otherwise
 void stream_sync(Ctx &c, hipStream_t s);
 void comm_abort(Ctx &c);
+extern int g_shard_inject;   // test hook: the next N sharded waits fail as device errors
 int shard_count(const Ctx &c);
 bool shard_mine(const Ctx &c, int r);
 void shard_plan(int n, int R, int kind, int *bounds);

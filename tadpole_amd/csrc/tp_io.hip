@@ -18,6 +18,8 @@
 #include <algorithm>
 #include <atomic>
 #include <charconv>
+#include <condition_variable>
+#include <mutex>
 #include <cmath>
 #include <cstring>
 #include <string>
@@ -233,21 +235,29 @@ void tsv_read(const char *path, int nrow, int ncol, int nthreads, bool row_major
     }
 }
 
-// Row-major parse into `out` in nblocks row blocks: on_block(r0, r1) runs on
-// the calling thread as soon as rows [r0, r1) are complete, while the worker
-// threads parse the later blocks (thread t takes byte range t of every block,
-// block after block).  Lets a caller overlap each block's upload with the
-// parse of the next.  Errors (a line with too many fields) are raised after
-// the last block.
-void tsv_read_rows(const char *path, int nrow, int ncol, int nthreads, double *out, int nblocks,
-                   const std::function<void(size_t, size_t)> &on_block) {
+// Row-major parse in row blocks of about block_bytes of text each, through a
+// ring of `nslots` staging slots: alloc(slot_rows) returns nslots x slot_rows
+// x ncol doubles (called once, after the line count); block b is parsed into
+// slot b % nslots (row r at (r - r0) * ncol), and on_block(r0, r1, rows, slot)
+// runs on the calling thread as soon as it is complete, while the worker
+// threads parse the next blocks (thread t takes byte range t of every block,
+// block after block).  A slot is written again only after slot_free(slot)
+// returned on the calling thread (the caller waits there for its upload of
+// the slot), so the staging is nslots blocks, not the matrix.  Errors (a line
+// with too many fields) are raised after the last block.
+void tsv_read_rows(const char *path, int nrow, int ncol, int nthreads, size_t block_bytes, int nslots,
+                   const std::function<double *(size_t)> &alloc,
+                   const std::function<void(size_t, size_t, const double *, int)> &on_block,
+                   const std::function<void(int)> &slot_free) {
     Mapped m(path);
     const size_t e = content_end(m);
     if (nrow == 0 || ncol == 0) return;
     int T = std::max(1, std::min(nthreads, 64));
-    int NB = std::max(1, nblocks);
+    const int S = std::max(2, nslots);
+    const size_t dbytes = (size_t)nrow * (size_t)ncol * sizeof(double);
+    int NB = (int)std::min<size_t>(4096, std::max<size_t>(2 * (size_t)S, dbytes / std::max<size_t>(block_bytes, 65536) + 1));
     if (e < (size_t)T * NB * 65536) T = 1;
-    if (e < (size_t)NB * 65536) NB = 1;
+    if (e < (size_t)NB * 65536) NB = std::max<int>(1, (int)(e / 65536));
     const int Q = NB * T;
     std::vector<size_t> start(Q + 1);
     start[0] = 0;
@@ -270,20 +280,36 @@ void tsv_read_rows(const char *path, int nrow, int ncol, int nthreads, double *o
     std::vector<size_t> row0(Q + 1, 0);
     for (int q = 0; q < Q; ++q) row0[q + 1] = row0[q] + rows[q];
     if (row0[Q] != (size_t)nrow) fail(TP_ERR_ARG, "row count changed while reading (or wrong nrow)");
+    size_t slot_rows = 1;
+    for (int b = 0; b < NB; ++b) slot_rows = std::max(slot_rows, row0[(size_t)(b + 1) * T] - row0[(size_t)b * T]);
+    double *ring = alloc(slot_rows);
     std::vector<long> bad_line(T, -1);
-    std::vector<std::atomic<int>> done(NB);
-    for (auto &d : done) d.store(0);
+    // blocking hand-offs (no spinning: on a CPU-quota'd host, spinning
+    // waiters steal the parse's time slices): workers wait for their block's
+    // slot, the calling thread for each block's completion
+    std::mutex mu;
+    std::condition_variable cv_work, cv_main;
+    std::vector<int> done(NB, 0);
+    int writable = std::min(NB, S);   // blocks [0, writable) may be written
+    bool stop = false;
     std::vector<std::thread> th;
     for (int t = 0; t < T; ++t)
         th.emplace_back([&, t] {
             for (int b = 0; b < NB; ++b) {
+                {
+                    std::unique_lock<std::mutex> lk(mu);
+                    cv_work.wait(lk, [&] { return stop || b < writable; });
+                    if (b >= writable) return;
+                }
                 const int q = b * T + t;
                 const char *p = m.p + start[q], *end = m.p + start[q + 1];
                 size_t r = row0[q];
+                const size_t rb0 = row0[(size_t)b * T];
+                double *slot = ring + (size_t)(b % S) * slot_rows * (size_t)ncol;
                 while (p < end) {
                     const char *nl = (const char *)memchr(p, '\n', (size_t)(end - p));
                     const char *le = nl ? nl : end;
-                    double *row = out + r * (size_t)ncol;
+                    double *row = slot + (r - rb0) * (size_t)ncol;
                     int c = 0;
                     const char *f = p;
                     while (true) {
@@ -301,19 +327,44 @@ void tsv_read_rows(const char *path, int nrow, int ncol, int nthreads, double *o
                     ++r;
                     p = nl ? nl + 1 : end;
                 }
-                done[b].fetch_add(1, std::memory_order_release);
+                bool last;
+                {
+                    std::lock_guard<std::mutex> lk(mu);
+                    last = ++done[b] == T;
+                }
+                if (last) cv_main.notify_one();
             }
         });
-    struct Join {   // the workers finish even when on_block throws
+    struct Join {   // the workers finish even when on_block / slot_free throws
         std::vector<std::thread> &th;
+        std::mutex &mu;
+        std::condition_variable &cv;
+        bool &stop;
         ~Join() {
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                stop = true;
+            }
+            cv.notify_all();
             for (auto &x : th)
                 if (x.joinable()) x.join();
         }
-    } join{th};
+    } join{th, mu, cv_work, stop};
     for (int b = 0; b < NB; ++b) {
-        while (done[b].load(std::memory_order_acquire) < T) std::this_thread::yield();
-        on_block(row0[(size_t)b * T], row0[(size_t)(b + 1) * T]);
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv_main.wait(lk, [&] { return done[b] == T; });
+        }
+        on_block(row0[(size_t)b * T], row0[(size_t)(b + 1) * T], ring + (size_t)(b % S) * slot_rows * (size_t)ncol,
+                 b % S);
+        if (b + S < NB) {   // block b + S reuses this slot once its upload is done
+            slot_free(b % S);
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                writable = b + S + 1;
+            }
+            cv_work.notify_all();
+        }
     }
     for (auto &x : th) x.join();
     for (int t = 0; t < T; ++t)

@@ -101,6 +101,7 @@ void comm_init(Ctx &c, const char *id128, int nranks, int rank) {
     c.shard.comm = comm;
     c.shard.rank = rank;
     c.shard.nranks = nranks;
+    c.shard.dead = false;
 }
 
 void comm_destroy(Ctx &c) {
@@ -130,18 +131,33 @@ static double shard_timeout_s() {
     return v;
 }
 
+// The communicator belongs to the device (every stream's context copies it):
+// the device's registry entry forgets it first, so no later call -- and no
+// tp_comm_destroy -- touches the aborted communicator, and exactly one caller
+// aborts it.
 void comm_abort(Ctx &c) {
-    if (!c.shard.comm) return;
-    (void)rccl().abort((ncclComm_t)c.shard.comm);
+    void *comm = c.shard.comm;
+    if (!comm) return;
+    const bool owner = ctx_comm_retire(c, comm);
     c.shard.comm = nullptr;
     c.shard.rank = 0;
     c.shard.nranks = 1;
+    c.shard.dead = true;
+    if (owner) (void)rccl().abort((ncclComm_t)comm);
 }
+
+int g_shard_inject = 0;   // test hook (knob 30): the next N sharded waits fail as a device error
 
 void stream_sync(Ctx &c, hipStream_t s) {
     if (!(c.shard.active && c.shard.comm)) {
         TP_HIP(hipStreamSynchronize(s));
         return;
+    }
+    if (g_shard_inject > 0) {
+        --g_shard_inject;
+        TP_HIP(hipStreamSynchronize(s));
+        comm_abort(c);
+        fail(TP_ERR_HIP, "injected device failure in a sharded call (knob 30); communicator aborted");
     }
     const auto t0 = std::chrono::steady_clock::now();
     for (;;) {

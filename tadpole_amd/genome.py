@@ -12,8 +12,33 @@ from __future__ import annotations
 
 import heapq
 import os
+import queue
+import threading
 import time
 from typing import Callable, Dict, List, Mapping, Optional, Sequence, Tuple
+
+# persistent per-(device, width) pools: a worker executor and `width` HIP
+# streams handed out one per running chromosome.  The library keeps one
+# context (~N^2 of scratch) per caller stream, so reusing the same streams
+# call after call reuses those contexts instead of building fresh ones (and
+# retiring old ones) inside every run_genome call.
+_POOLS: Dict[Tuple[int, int], tuple] = {}
+_POOLS_LOCK = threading.Lock()
+
+
+def _stream_pool(device: int, width: int):
+    key = (device, width)
+    with _POOLS_LOCK:
+        pool = _POOLS.get(key)
+        if pool is None:
+            import torch
+            from concurrent.futures import ThreadPoolExecutor
+            free = queue.SimpleQueue()
+            for _ in range(width):
+                free.put(torch.cuda.Stream(device=f"cuda:{device}"))
+            pool = (ThreadPoolExecutor(max_workers=width, thread_name_prefix=f"tadpole-genome{device}"), free)
+            _POOLS[key] = pool
+    return pool
 
 
 def lpt_assign(costs: Mapping[str, float], n_workers: int) -> List[List[str]]:
@@ -91,23 +116,20 @@ def run_genome(matrices: Mapping[str, object], sizes: Optional[Mapping[str, int]
 
         if streams > 1 and len(plan[rank]) > 1:
             # this rank's chromosomes, up to `streams` in flight on one GPU (one
-            # HIP stream and library context each): the latency-bound stages of
-            # a pipeline leave most CUs idle.  (Hardware queues: see
-            # tadpole_amd.use_hw_queues.)
-            import threading
-            from concurrent.futures import ThreadPoolExecutor
-
-            import torch
-            tls = threading.local()
+            # HIP stream and library context each, from the persistent pool):
+            # the latency-bound stages of a pipeline leave most CUs idle.
+            # (Hardware queues: see tadpole_amd.use_hw_queues.)
+            ex, free = _stream_pool(local, streams)
 
             def run_stream(name, m, device):
-                if getattr(tls, "stream", None) is None:
-                    tls.stream = torch.cuda.Stream(device=f"cuda:{device}")
-                return TADpole(m, device=device, stream=tls.stream, **tadpole_kwargs)
+                s = free.get()
+                try:
+                    return TADpole(m, device=device, stream=s, **tadpole_kwargs)
+                finally:
+                    free.put(s)
 
-            with ThreadPoolExecutor(max_workers=streams) as ex:
-                for f in [ex.submit(one, name, run_stream) for name in plan[rank]]:
-                    f.result()
+            for f in [ex.submit(one, name, run_stream) for name in plan[rank]]:
+                f.result()
         else:
             for name in plan[rank]:
                 one(name, runner)

@@ -177,16 +177,21 @@ def matrix_checksum(m: np.ndarray) -> np.ndarray:
     """Two exact integers that pin a count matrix's values (the committed large
     fixtures store them instead of the matrix): the sum of the counts and
     sum (row + 1) (column + 1) m mod 2^61 - 1 (exact Python integers)."""
+    from concurrent.futures import ThreadPoolExecutor
+    import os
     n = m.shape[0]
     P = (1 << 61) - 1
     w = np.arange(n, dtype=np.int64) + 1
-    total = 0
-    acc = 0
-    for r0 in range(0, n, 1024):
+
+    def part(r0):   # exact integers per 1024-row block; summed in Python ints
         blk = np.asarray(m[r0:r0 + 1024], np.float64).astype(np.int64)
-        total += int(blk.sum())
-        rows = (blk * w[None, :]).sum(axis=1)      # < 2^43 per row at counts < 2^13, n < 2^15
-        acc += sum(int(v) * (r0 + q + 1) for q, v in enumerate(rows))
+        rows = (blk * w[None, :]).sum(axis=1)      # < 2^43 per row at counts < 2^13, n < 2^16
+        return int(blk.sum()), sum(int(v) * (r0 + q + 1) for q, v in enumerate(rows))
+
+    with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1)) as ex:
+        parts = list(ex.map(part, range(0, n, 1024)))
+    total = sum(p[0] for p in parts)
+    acc = sum(p[1] for p in parts)
     return np.array([total, acc % P], np.int64)
 
 

@@ -139,11 +139,46 @@ def large():
 
 
 C5ARM_BINS = 24300
+C5_BINS = 49851
+
+
+def c5full():
+    """BASELINE config 5 at full size: synth_hic_par(49 851, SEED_BASE + 5,
+    centromere=True) -- chr1 @5kb -- through TADpole(centromere_search=TRUE)
+    (R/TADpole.R:58-85,351-442), bug-compatible (the q arm keeps its bad bins,
+    :78-80) and with the PCA by LAPACK dsyevr.  Outputs only (+ the matrix
+    checksum).  The 19.9 GB matrix is cleaned in place and freed before the
+    arms run (peak ~35 GB)."""
+    t0 = time.time()
+    m = synth_hic_par(C5_BINS, SEED_BASE + 5, centromere=True)
+    ck = matrix_checksum(m)
+    print("c5 matrix", f"{time.time() - t0:.1f} s", ck, flush=True)
+    loaded = O.load_mat_arms(m, 0.01, fixed=False, inplace=True)
+    del m
+    out = {"n0": C5_BINS, "seed": SEED_BASE + 5, "max_pcs": 200, "matrix_checksum": ck}
+
+    def log(arm, r):
+        print("c5 arm", arm, len(r.good_idx1), r.n_pcs, r.optimal_n_clusters, r.scores.shape,
+              f"{time.time() - t0:.1f} s", flush=True)
+
+    a = O.arms_from_loaded(loaded, max_pcs=200, nthreads=THREADS, pca="eigh", log=log)
+    out["bug_merging_arms"] = a.merging_arms
+    out["bug_centromere"] = a.centromere
+    for arm in ("p", "q"):
+        r = getattr(a, arm)
+        out.update(outputs(r, f"bug_{arm}_"))
+        out[f"bug_{arm}_names"] = np.asarray(r.good_idx1, np.int32)
+        out[f"bug_{arm}_pc_norms"] = np.linalg.norm(r.pcs, axis=0)
+    np.savez_compressed(os.path.join(HERE, "c5full.npz"), **out)
+    print("c5full", len(a.merging_arms), f"{time.time() - t0:.1f} s", flush=True)
+
 
 if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
     if what == "large":   # tens of minutes and ~35 GB: never part of "all"
         large()
+    if what == "c5full":  # ~1 h and ~35 GB: never part of "all"
+        c5full()
     for fn in (small, arms, genome, configs):
         if what in ("all", fn.__name__):
             fn()

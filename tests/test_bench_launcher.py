@@ -64,3 +64,44 @@ def test_bench_cli_refuses_mismatch():
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], env=env,
                        capture_output=True, text=True, timeout=120)
     assert p.returncode == 2 and "WORLD_SIZE=3" in p.stderr
+
+
+def _dist_worker(rank, world, port, out):
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n0 = 37
+    host = np.arange(n0 * n0, dtype=np.float64).reshape(n0, n0) if rank == 0 else None
+    got = torch.full((n0, n0), -1.0, dtype=torch.float64)
+    bench.distribute_rows(host, n0, world, rank, lambda r0, r1, t: got[r0:r1].copy_(t), chunk_rows=8)
+    want = torch.arange(n0 * n0, dtype=torch.float64).reshape(n0, n0)
+    out.put((rank, bool(torch.equal(got, want)), bench.c5_mode(world)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_c5_full_multi_rank_path_gloo():
+    """The c5_full line at world 2 (what `bench.py --gpus 2` selects): the
+    sharded mode, and the C5 matrix reaching every rank intact through the
+    chunked gloo broadcast (rank 0 holds the only host copy)."""
+    import socket
+    import torch.multiprocessing as mp
+    import bench
+    assert bench.c5_mode(1) == "one_gpu" and bench.c5_mode(8) == "sharded"
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_dist_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(60)
+    assert res == [(0, True, "sharded"), (1, True, "sharded")]

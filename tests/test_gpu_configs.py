@@ -338,56 +338,47 @@ def _nested(clusters):
         prev = starts
 
 
-def test_c5_full_size_sharded_bit_identical(gpu):
-    """C5 (chr1 @5kb shape, 49 851 bins, centromere_search=TRUE): the arms
-    (~24.3k and ~21.3k bins) split over 8 virtual shards give the bits of the
-    unsplit schedule; the PCA residual bound holds at full size; the levels
-    nest.  The matrix is generated in HBM (torch, seeded) and stays there."""
+def test_c5_full_golden_and_sharded_bit_identical(gpu):
+    """BASELINE config 5 at full size (chr1 @5kb shape: synth_hic_par(49 851,
+    SEED_BASE + 5, centromere=True), the CPU-generated matrix of
+    tests/golden/c5full.npz): TADpole(centromere_search=TRUE), bug-compatible
+    (the q arm keeps its ~100 zeroed bins: constant columns, NaN -> 0 in cor,
+    identical PC rows, exact CONISS ties), against the CPU oracle --
+    merging_arms, and per arm n_pcs, optimal_n_clusters, bit-exact merge
+    order and every level's coordinates, CH within 1e-6 relative
+    (R/TADpole.R:58-85,351-442).  The same matrix split over 8 virtual shards
+    (the C5 schedule: column slabs of C, row-split Krylov products, tree-split
+    sweep) gives the unsharded bits; the levels nest."""
     import torch
     import tadpole_amd as tp
-    n0 = 49851
-    gen = torch.Generator(device="cuda").manual_seed(SEED_BASE + 5)
-    idx = torch.arange(n0, device="cuda", dtype=torch.float64)
-    m = torch.empty((n0, n0), dtype=torch.float64, device="cuda")
-    blk = 2048
-    for r0 in range(0, n0, blk):
-        r1 = min(n0, r0 + blk)
-        e = 1000.0 / (1.0 + (idx[r0:r1, None] - idx[None, :]).abs())
-        m[r0:r1] = torch.poisson(e, generator=gen)
-        del e
-    for r0 in range(0, n0, blk):          # mirror the upper triangle (upper wins)
-        r1 = min(n0, r0 + blk)
-        m[r0:r1, :r0] = m[:r0, r0:r1].T
-        m[r0:r1, r0:r1] = torch.triu(m[r0:r1, r0:r1]) + torch.triu(m[r0:r1, r0:r1], 1).T
-    a, b = int(0.4875 * n0), int(0.572 * n0)
-    m[a:b, :] = 0
-    m[:, a:b] = 0
-    z = torch.randint(0, n0, (250,), generator=gen, device="cuda")
-    m[z, :] = 0
-    m[:, z] = 0
     from tadpole_amd import multi
-    outs = []
-    for v in (1, 8):
-        multi.set_virtual_shards(v)
-        try:
-            outs.append(tp.TADpole(m.clone(), max_pcs=200, centromere_search=True, sharded=True))
-        finally:
-            multi.set_virtual_shards(1)
+    z = np.load(os.path.join(GOLD, "c5full.npz"))
+    m = synth_hic_par(int(z["n0"]), int(z["seed"]), centromere=True)
+    assert np.array_equal(matrix_checksum(m), z["matrix_checksum"])   # same input as the fixture
+    dm = torch.from_numpy(m).cuda()
     del m
-    torch.cuda.empty_cache()
-    g1, g8 = outs
-    assert np.array_equal(g1.merging_arms, g8.merging_arms)
+    got = tp.TADpole(dm, max_pcs=200, centromere_search=True, inplace=True)
+    assert np.array_equal(got.merging_arms, z["bug_merging_arms"])
     for arm in ("p", "q"):
-        x, y = getattr(g1, arm), getattr(g8, arm)
+        sub = getattr(got, arm)
+        sv = z[f"bug_{arm}_pc_norms"]
+        print(f"C5 arm {arm}: n={int(sub.timings_ms[14])} n_pcs={sub.n_pcs} k*={sub.optimal_n_clusters} "
+              f"pca resid {sub.timings_ms[13]:.1e} sigma_k-1/sigma_k {sv[-2] / sv[-1]:.6f}")
+        assert sub.timings_ms[13] <= 1e-11
+        assert np.array_equal(sub.dendro.label_ids, z[f"bug_{arm}_names"])
+        _check(sub, z, f"bug_{arm}_", bad=False)
+        _nested(sub.clusters)
+    multi.set_virtual_shards(8)
+    try:
+        g8 = tp.TADpole(dm, max_pcs=200, centromere_search=True, sharded=True, inplace=True)
+    finally:
+        multi.set_virtual_shards(1)
+    del dm
+    torch.cuda.empty_cache()
+    assert np.array_equal(g8.merging_arms, got.merging_arms)
+    for arm in ("p", "q"):
+        x, y = getattr(got, arm), getattr(g8, arm)
         assert (x.n_pcs, x.optimal_n_clusters) == (y.n_pcs, y.optimal_n_clusters)
         assert np.array_equal(x.scores.view(np.uint64), y.scores.view(np.uint64))
         assert np.array_equal(x.dendro.boundary, y.dendro.boundary)
         assert np.array_equal(x.dendro.height.view(np.uint64), y.dendro.height.view(np.uint64))
-        assert x.timings_ms[13] <= 1e-11 and y.timings_ms[13] <= 1e-11
-        _nested(x.clusters)
-        print(f"C5 arm {arm}: n={int(x.timings_ms[14])} n_pcs={x.n_pcs} k*={x.optimal_n_clusters} "
-              f"pca resid {x.timings_ms[13]:.1e}")
-    c = g1.merging_arms
-    # bug-compatible: the q arm keeps its bad bins AND re-inserts them as zeros
-    # (duplicate names, R/TADpole.R:78-80,413-423), so coordinates may run past N0
-    assert np.all(c[:, 0] <= c[:, 1]) and np.all(c[1:, 0] > c[:-1, 1])

@@ -114,3 +114,20 @@ def test_device_input_not_modified(gpu):
     b = tp.TADpole(d, max_pcs=50, inplace=True)
     assert _same(a, b)
     assert not torch.isnan(d).any() and torch.equal(d, d.T)
+
+
+def test_run_genome_reuses_stream_contexts(gpu):
+    """Consecutive run_genome calls draw their streams from a persistent pool,
+    so the second call creates no library context (no N^2 scratch allocated
+    or retired inside it) and gives bit-identical results."""
+    from tadpole_amd import _lib
+    from tadpole_amd.genome import run_genome
+    mats = {f"c{i}": synth_hic(600 + 40 * i, 70 + i) for i in range(6)}
+    a, _ = run_genome(mats, streams=4, max_pcs=60)
+    live0, made0 = _lib.context_stats(0)
+    b, _ = run_genome(mats, streams=4, max_pcs=60)
+    live1, made1 = _lib.context_stats(0)
+    assert made1 == made0, (made0, made1)
+    assert live1 == live0
+    for c in mats:
+        assert _same(a[c], b[c]), c

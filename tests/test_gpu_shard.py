@@ -138,3 +138,73 @@ def test_genome_driver_streams(gpu):
     res, secs = run_genome(mats, streams=3, max_pcs=80)
     for name, m in mats.items():
         _same(res[name], tp.TADpole(m, max_pcs=80))
+
+
+def _one_rank_comm():
+    import ctypes
+    from tadpole_amd import _lib
+    uid = multi.comm_unique_id()
+    L = _lib.load()
+    st = ctypes.c_int(0)
+    L.tp_comm_init(uid, ctypes.byref(ctypes.c_int(1)), ctypes.byref(ctypes.c_int(0)),
+                   ctypes.byref(ctypes.c_int(0)), ctypes.byref(st))
+    _lib.check(st)
+
+
+def test_sharded_failure_on_caller_stream_aborts_device_communicator(gpu):
+    """A device failure inside a sharded call on a caller stream (injected:
+    knob 30) aborts the DEVICE's communicator, not just that stream
+    context's copy: the next sharded call on any stream fails loudly (no
+    silent unsharded run, no use of the freed communicator), tp_comm_destroy
+    does not free it a second time, and a new communicator works again."""
+    import torch
+    import gpu_helpers as G
+    from tadpole_amd._lib import TadpoleError, TP_ERR_HIP
+    m = synth_hic(500, 36)
+    multi.set_virtual_shards(1)
+    ref = tp.TADpole(m, max_pcs=80, sharded=True)
+    ref_u = tp.TADpole(m, max_pcs=80)
+    _one_rank_comm()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    try:
+        _same(tp.TADpole(m, max_pcs=80, sharded=True, stream=s1), ref)   # s1's context copies the comm
+        G.knob(30, 1)
+        with pytest.raises(TadpoleError) as e:
+            tp.TADpole(m, max_pcs=80, sharded=True, stream=s1)
+        assert e.value.status == TP_ERR_HIP and "injected" in str(e.value)
+        for s in (s1, s2, None):      # the device's communicator is gone for every stream
+            with pytest.raises(TadpoleError) as e:
+                tp.TADpole(m, max_pcs=80, sharded=True, stream=s)
+            assert "aborted" in str(e.value)
+        _same(tp.TADpole(m, max_pcs=80, stream=s2), ref_u)                # unsharded calls are unaffected
+    finally:
+        G.knob(30, 0)
+        multi.destroy_comm(0)          # no second free of the aborted communicator
+    _same(tp.TADpole(m, max_pcs=80, sharded=True, stream=s1), ref)       # destroyed on purpose: one shard
+    _one_rank_comm()
+    try:
+        _same(tp.TADpole(m, max_pcs=80, sharded=True, stream=s2), ref)
+    finally:
+        multi.destroy_comm(0)
+    tp.release_stream(s1)
+    tp.release_stream(s2)
+
+
+def test_sharded_data_error_keeps_communicator(gpu):
+    """A data error in a sharded call (fewer than 3 good bins: every rank
+    sees it at the same point) fails that call only; the communicator stays
+    alive and the next sharded call runs on it."""
+    from tadpole_amd._lib import TadpoleError, TP_ERR_NO_BSTICK
+    m = synth_hic(400, 37)
+    multi.set_virtual_shards(1)
+    ref = tp.TADpole(m, max_pcs=60, sharded=True)
+    bad = np.zeros((50, 50))
+    bad[0, 0] = bad[1, 1] = 5.0
+    _one_rank_comm()
+    try:
+        with pytest.raises(TadpoleError) as e:
+            tp.TADpole(bad, max_pcs=10, sharded=True)
+        assert e.value.status == TP_ERR_NO_BSTICK
+        _same(tp.TADpole(m, max_pcs=60, sharded=True), ref)
+    finally:
+        multi.destroy_comm(0)
