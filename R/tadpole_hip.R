@@ -1,3 +1,16 @@
+# Copyright (C) the TADpole authors (3DGenomes/TADpole, GPL-3) and the
+# tadpole_amd authors.
+#
+# This file is part of a GPU backend for the TADpole R package.  Parts of it
+# restate the reference's R code (R/TADpole.R) so that TADpole_hip() is a
+# drop-in for TADpole(); like the reference (DESCRIPTION: License GPL-3) it is
+# free software: you can redistribute it and/or modify it under the terms of
+# the GNU General Public License as published by the Free Software Foundation,
+# either version 3 of the License, or (at your option) any later version.
+# It is distributed WITHOUT ANY WARRANTY; without even the implied warranty of
+# MERCHANTABILITY or FITNESS FOR A PARTICULAR PURPOSE.  See the GNU General
+# Public License (https://www.gnu.org/licenses/gpl-3.0.html) for details.
+#
 # tadpole_hip.R -- R host side of libtadpole_hip.so (the MI355X engine) for the
 # 3DGenomes/TADpole package.  Drop this file into the package's R/ directory:
 # TADpole_hip() is TADpole() (R/TADpole.R:344-501) with the hot path -- mask,

@@ -563,7 +563,12 @@ def TADpole(mat_file, max_pcs: int = 200, min_clusters: int = 2, bad_frac: float
             if raw.data_ptr() == mat_file.data_ptr():
                 raw = raw.clone()
     elif _is_path(mat_file):
-        raw = _read_to_device(mat_file, device, stream)   # ours: cleaned in place on the device
+        try:
+            import torch  # noqa: F401  (device memory for the direct-to-device parse)
+        except ImportError:   # R-like hosts without torch: the host parse, then tp_pipeline
+            raw = read_matrix(mat_file)
+        else:
+            raw = _read_to_device(mat_file, device, stream)   # ours: cleaned in place on the device
     else:
         raw = _as_matrix(mat_file)
     shard_flag = _lib.TP_FLAG_SHARDED if sharded else 0
