@@ -601,17 +601,50 @@ def TADpole(mat_file, max_pcs: int = 200, min_clusters: int = 2, bad_frac: float
     return _tadpole_arms(raw, plan, max_pcs, min_clusters, device, shard_flag, stream, verbose)
 
 
+_ARM_STREAMS: Dict[int, tuple] = {}
+
+
+def _arm_streams(device: int):
+    """Two persistent HIP streams per device for the concurrent arms (the
+    library keeps one context per stream: reusing them reuses its scratch)."""
+    s = _ARM_STREAMS.get(device)
+    if s is None:
+        import torch
+        s = _ARM_STREAMS[device] = (torch.cuda.Stream(device=f"cuda:{device}"),
+                                    torch.cuda.Stream(device=f"cuda:{device}"))
+    return s
+
+
+def _arms_concurrent(raw, shard_flag: int, stream) -> bool:
+    """The two arms are independent matrices (R/TADpole.R:357-432 runs them
+    one after the other): on one GPU they run on two streams at once, so one
+    arm's latency-bound CONISS sweep (~200 of 256 CUs, mostly idle SIMDs)
+    overlaps the other arm's MFMA-bound correlation and PCA.  Not for sharded
+    calls (one communicator per device serialises them) or when the caller
+    chose the stream."""
+    if shard_flag or stream is not None or os.environ.get("TADPOLE_ARMS_SERIAL") == "1":
+        return False
+    try:
+        import torch
+    except ImportError:
+        return False
+    return torch.cuda.is_available()
+
+
 def _tadpole_arms(raw, plan, max_pcs, min_clusters, device, shard_flag: int = 0, stream=None,
                   verbose: bool = False) -> Tadpole:
     """R/TADpole.R:351-442 (arm loop and arm merge).  Each arm is the raw
     principal submatrix of its kept bins; NA->0 and forceSymmetric(uplo='U')
     commute with taking it, so the device cleans it (TP_FLAG_NO_MASK: the arm
-    matrices are correlated as given, R/TADpole.R:362)."""
+    matrices are correlated as given, R/TADpole.R:362).  On one GPU the two
+    arms run concurrently on two streams (``_arms_concurrent``); results and
+    R's message() lines are those of the sequential loop, in its order."""
     tad = Tadpole()
     centromer = plan["centromere"]
-    fixed_arms: List[np.ndarray] = []
-    for arm in ("p", "q"):
-        _message(f"Processing arm {arm}", verbose)
+    if _is_device(raw):
+        device = raw.device.index if raw.device.index is not None else device
+
+    def run_arm(arm, arm_stream):
         names, bad_cols = plan[arm]
         if _is_device(raw):   # already cleaned by tp_mask_dev
             import torch
@@ -621,10 +654,27 @@ def _tadpole_arms(raw, plan, max_pcs, min_clusters, device, shard_flag: int = 0,
         else:
             sub = raw[np.ix_(names - 1, names - 1)]
             clean = 0
-        res = _pipeline(sub, max_pcs, min_clusters, 0.0, _lib.TP_FLAG_NO_MASK | clean | shard_flag, device, stream)
+        res = _pipeline(sub, max_pcs, min_clusters, 0.0, _lib.TP_FLAG_NO_MASK | clean | shard_flag, device,
+                        arm_stream)
         del sub
         res["good"] = names.astype(np.int32)   # rownames inherited from the full matrix
-        sub_t = _assemble(res, np.asarray(bad_cols))
+        return _assemble(res, np.asarray(bad_cols))
+
+    if _arms_concurrent(raw, shard_flag, stream):
+        from concurrent.futures import ThreadPoolExecutor
+        sp, sq = _arm_streams(device)
+        with ThreadPoolExecutor(max_workers=2) as ex:
+            fut = {"p": ex.submit(run_arm, "p", sp), "q": ex.submit(run_arm, "q", sq)}
+            subs = {arm: fut[arm].result() for arm in ("p", "q")}
+    else:
+        subs = {}
+        for arm in ("p", "q"):
+            subs[arm] = run_arm(arm, stream)
+    fixed_arms: List[np.ndarray] = []
+    for arm in ("p", "q"):
+        names, bad_cols = plan[arm]
+        sub_t = subs[arm]
+        _message(f"Processing arm {arm}", verbose)
         _message(f"Optimal number of PCs: {sub_t.n_pcs}", verbose)
         _message(f"Optimal number of clusters: {sub_t.optimal_n_clusters}", verbose)
         setattr(tad, arm, sub_t)

@@ -1422,7 +1422,7 @@ void tp_debug_eigsym(const double *H, const int *b, const int *method, double *t
         Ctx &c = ctx_for(0);
         hipStream_t s = c.cur;
         const int B = *b;
-        if (!tp::eig_sym_supported(B)) fail(TP_ERR_UNSUPPORTED, "b > 512");
+        if (!tp::eig_sym_supported(B)) fail(TP_ERR_UNSUPPORTED, "b > 640 (EIG_BMAX)");
         rocblas_handle h;
         if (rocblas_create_handle(&h) != rocblas_status_success) fail(TP_ERR_HIP, "handle");
         (void)rocblas_set_stream(h, s);
@@ -1611,12 +1611,14 @@ extern "C" {
  * 2 short-K panel GEMM, 3 GEMM LDS stage depth (16 / 32), 4 register-resident
  * tridiagonalisation, 5 int8 X'X, 6 PCA degree margin, 7 XCD-aware GEMM order, ..., 14 supertile
  * order of the int8 X'X tiles, ..., 17 C's column means formed by the correlation epilogue, 18 the
- * correlation epilogue in the int8 X'X store (with the gather's statistics), ..., 25 events around
+ * correlation epilogue in the int8 X'X store (with the gather's statistics), ..., 20 the PCA's block
+ * Krylov space: 1 of C, 0 of G, -1 (default) of C from knob 31's bin count on, ..., 25 events around
  * every Krylov product when timings are requested (0: stage and one-launch classes only), 26 products
  * with the block-tridiagonal Krylov projection T skip its zero blocks (0: dense GEMM), 28 the
  * Krylov CGS2's first pass against the last two blocks only (0: against every block), 29 CholQR
  * Gram matrices of 64-column blocks by k_gram64 (0: the split-K GEMM; same bits), 30 the next N
- * sharded waits with a live communicator fail as device errors (failure-containment tests). */
+ * sharded waits with a live communicator fail as device errors (failure-containment tests), 31 the
+ * bins from which knob 20 = -1 (default) takes the Krylov space of C. */
 void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
     guarded(status, [&] {
         int *p = nullptr;
@@ -1651,6 +1653,7 @@ void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
         case 28: p = &g_krylov_local; break;
         case 29: p = &g_gram64; break;
         case 30: p = &g_shard_inject; break;
+        case 31: p = &g_ckry_min; break;
         default: fail(TP_ERR_ARG, "unknown knob");
         }
         if (*which == 3 && *value != 16 && *value != 32) fail(TP_ERR_ARG, "stage depth must be 16 or 32");

@@ -382,7 +382,8 @@ struct PcaStats {
 };
 extern int g_pca_krylov_min, g_pca_krylov_block, g_pca_krylov_steps, g_pca_over;
 extern int g_pca_cheb_fused;   // Krylov small problem: Chebyshev step in the T Y reduction (default 1)
-extern int g_pca_ckrylov;      // 1: block Krylov in C (tp_krylov.hip), 0: in G (tp_pca.hip)
+extern int g_pca_ckrylov;      // 1: block Krylov in C (tp_krylov.hip), 0: in G (tp_pca.hip), -1: C from g_ckry_min
+extern int g_ckry_min;         // bins from which the automatic choice takes the Krylov space of C
 extern int g_ckry_chunk;       // rows per Z partial of the C-Krylov orthogonalisation
 extern int g_ckry_steps;       // C-Krylov blocks before the first check (0: from k and n)
 // the top k eigenpairs of a D x D projected matrix (tp_pca.hip)

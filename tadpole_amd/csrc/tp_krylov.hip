@@ -69,7 +69,13 @@ __global__ void k_start_block(double *Q, int n, uint64_t seed) {
 // split-K reduction over n, its reduce, the small step and the apply: ~75 us,
 // latency-bound) cost 5.1 ms against the G path's 3.3 ms: PCA 14.9 vs 14.1 ms
 // (profiles/r03b_*).  Kept, tested, behind knob 20.
-int g_pca_ckrylov = 0;        // 1: Krylov in C (this file), 0: Krylov in G (tp_pca.hip)
+// 1: Krylov in C (this file), 0: Krylov in G (tp_pca.hip), -1: C from
+// g_ckry_min bins on.  Measured (round 4, MI355X, PCA ms G vs C): 10k bins
+// 18.3 vs 18.1, 24.3k bins 96.0 vs 77.3 -- the C space halves the product
+// flops, and above ~10k bins that outweighs its costlier orthogonalisation
+// (at C3, 7.7k bins, the G space is ~0.8 ms faster)
+int g_pca_ckrylov = -1;
+int g_ckry_min = 10000;
 int g_ckry_chunk = 256;       // rows per Z partial of the PIP passes
 int g_ckry_steps = 0;         // blocks s before the first check (0: from k and n)
 

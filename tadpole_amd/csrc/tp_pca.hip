@@ -725,7 +725,8 @@ PcaStats pca_dev(Ctx &c, double *d_C, int n, int k, double *d_P, double *d_Pt, d
                                   hipMemcpyDeviceToDevice, s));
         // neither Xc nor XcT is formed; the Krylov space of C (tp_krylov.hip),
         // or of G when an orthogonalisation pass of that path breaks down
-        if (!g_pca_ckrylov || !krylov_c_topk(c, d_C, c_col0, mext, n, k, V, d_P, h_theta, st)) {
+        const bool cspace = g_pca_ckrylov > 0 || (g_pca_ckrylov < 0 && n >= g_ckry_min);
+        if (!cspace || !krylov_c_topk(c, d_C, c_col0, mext, n, k, V, d_P, h_theta, st)) {
             h_theta.clear();
             st = PcaStats{};
             krylov_topk(c, d_C, c_col0, mext, n, k, V, d_P, h_theta, st);

@@ -10,10 +10,10 @@ HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [HERE, os.path.join(HERE, "tests")]
 import gpu_helpers as G  # noqa: E402
 import tadpole_amd as tp  # noqa: E402
-from tadpole_amd.synth import synth_hic  # noqa: E402
+from tadpole_amd.synth import synth_hic, synth_hic_par  # noqa: E402
 
 n0 = int(sys.argv[1])
-m = synth_hic(n0, 20261017)
+m = synth_hic(n0, 20261017) if n0 < 8000 else synth_hic_par(n0, 20261017)
 tp.TADpole(m, max_pcs=200)   # warm-up (contexts, code objects)
 for cfg in sys.argv[2:]:
     sets = [tuple(int(v) for v in kv.split("=")) for kv in cfg.split(",") if kv]

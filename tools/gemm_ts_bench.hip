@@ -404,6 +404,94 @@ __global__ void __launch_bounds__(256, 2) k_v3(int M, int N, int K, const double
             }
 }
 
+// ---- V5: parametrised: TM rows per workgroup (4 waves of TM/4 rows x 64
+// columns), BK-deep stages, NBUF LDS buffers (1: register prefetch, two
+// barriers a stage), OCC workgroups a CU (launch bounds)
+template <int TM, int BK, int NBUF, int OCC>
+__global__ void __launch_bounds__(256, OCC) k_v5(int M, int N, int K, const double *__restrict__ A, int lda,
+                                                 const double *__restrict__ B, int ldb, double *__restrict__ C,
+                                                 int ldc, int kchunk, size_t part_stride) {
+    constexpr int LD = BK + 2;
+    constexpr int WA = TM / 64;   // 16-row accumulator tiles per wave
+    __shared__ double As[NBUF][TM][LD];
+    __shared__ double Bs[NBUF][TSN][LD];
+    const int tm = (M + TM - 1) / TM, tn = (N + TSN - 1) / TSN;
+    const int Lg = xcd_order((int)gridDim.x);
+    const int bn = Lg % tn, bm = (Lg / tn) % tm, z = Lg / (tn * tm);
+    const int i0 = bm * TM, j0 = bn * TSN;
+    const int kbeg = z * kchunk, kend = min(K, kbeg + kchunk);
+    C += part_stride * z;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int wm = (TM / 4) * w;
+    const int fr = lane & 15, fk = lane >> 4;
+    d4 acc[WA][4];
+#pragma unroll
+    for (int a = 0; a < WA; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = (d4){0.0, 0.0, 0.0, 0.0};
+    constexpr int PA = TM * BK / 256, PB = TSN * BK / 256;
+    double ra[PA], rb[PB];
+    const int lk = t % BK, lr = t / BK;
+    constexpr int RS = 256 / BK;
+    auto load = [&](int k0) {
+        const int k = k0 + lk;
+        const bool kin = k < kend;
+#pragma unroll
+        for (int p = 0; p < PA; ++p) {
+            const int i = i0 + lr + RS * p;
+            ra[p] = (kin && i < M) ? A[(size_t)k + (size_t)i * lda] : 0.0;
+        }
+#pragma unroll
+        for (int p = 0; p < PB; ++p) {
+            const int j = j0 + lr + RS * p;
+            rb[p] = (kin && j < N) ? B[(size_t)k + (size_t)j * ldb] : 0.0;
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int p = 0; p < PA; ++p) As[buf][lr + RS * p][lk] = ra[p];
+#pragma unroll
+        for (int p = 0; p < PB; ++p) Bs[buf][lr + RS * p][lk] = rb[p];
+    };
+    if (kbeg < kend) {
+        load(kbeg);
+        store(0);
+    }
+    __syncthreads();
+    int buf = 0;
+    for (int k0 = kbeg; k0 < kend; k0 += BK) {
+        const bool more = k0 + BK < kend;
+        if (more) load(k0 + BK);
+#pragma unroll
+        for (int kk = 0; kk < BK; kk += 4) {
+            double af[WA], bf[4];
+#pragma unroll
+            for (int a = 0; a < WA; ++a) af[a] = As[buf][wm + 16 * a + fr][kk + fk];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) bf[b] = Bs[buf][16 * b + fr][kk + fk];
+#pragma unroll
+            for (int a = 0; a < WA; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[a], bf[b], acc[a][b], 0, 0, 0);
+        }
+        if (NBUF == 1) __syncthreads();
+        if (more) store(NBUF == 1 ? 0 : buf ^ 1);
+        __syncthreads();
+        if (NBUF == 2) buf ^= 1;
+    }
+#pragma unroll
+    for (int a = 0; a < WA; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = i0 + wm + 16 * a + fk + 4 * r;
+                const int j = j0 + 16 * b + fr;
+                if (i < M && j < N) C[(size_t)i + (size_t)j * ldc] = acc[a][b][r];
+            }
+}
+
 __global__ void k_rand(double *p, size_t n, unsigned long long seed) {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -417,26 +505,25 @@ __global__ void k_rand(double *p, size_t n, unsigned long long seed) {
 int main(int argc, char **argv) {
     const int n = argc > 1 ? atoi(argv[1]) : 7729;
     const int N = 64, M = n + 2, K = n;
-    const int S = std::min(8, K / 256);
-    int kchunk = ((K + S - 1) / S + 15) / 16 * 16;
-    const int SS = (K + kchunk - 1) / kchunk;
     const int reps = 20;
     double *A, *B, *P0, *P1;
     CK(hipMalloc(&A, (size_t)M * K * 8));
     CK(hipMalloc(&B, (size_t)K * N * 8));
     const size_t pst = (size_t)M * N;
-    CK(hipMalloc(&P0, pst * SS * 8));
-    CK(hipMalloc(&P1, pst * SS * 8));
+    const int SMAX = 32;
+    CK(hipMalloc(&P0, pst * SMAX * 8));
+    CK(hipMalloc(&P1, pst * SMAX * 8));
     hipLaunchKernelGGL(k_rand, dim3((unsigned)(((size_t)M * K + 255) / 256)), dim3(256), 0, 0, A, (size_t)M * K, 1ULL);
     hipLaunchKernelGGL(k_rand, dim3((unsigned)(((size_t)K * N + 255) / 256)), dim3(256), 0, 0, B, (size_t)K * N, 2ULL);
     CK(hipDeviceSynchronize());
-    const int tiles = (M + TSM - 1) / TSM;
-    const dim3 grid((unsigned)(tiles * SS));
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     const double flops = 2.0 * M * N * (double)K;
-    auto run = [&](const char *name, auto kern, double *out) {
+    auto run = [&](const char *name, auto kern, int TM, int S, double *out) {
+        int kchunk = ((K + S - 1) / S + 15) / 16 * 16;
+        const int SS = (K + kchunk - 1) / kchunk;
+        const dim3 grid((unsigned)(((M + TM - 1) / TM) * SS));
         for (int r = 0; r < 3; ++r) hipLaunchKernelGGL(kern, grid, dim3(256), 0, 0, M, N, K, A, n, B, n, out, M, kchunk, pst);
         CK(hipEventRecord(e0));
         for (int r = 0; r < reps; ++r)
@@ -446,27 +533,24 @@ int main(int argc, char **argv) {
         float ms = 0;
         CK(hipEventElapsedTime(&ms, e0, e1));
         const double us = ms * 1e3 / reps;
-        printf("%-28s %8.1f us  %6.2f TF/s\n", name, us, flops / (us * 1e-6) / 1e12);
+        printf("%-34s S=%2d grid=%5u %8.1f us  %6.2f TF/s\n", name, SS, grid.x, us, flops / (us * 1e-6) / 1e12);
+        fflush(stdout);
     };
-    auto cmp = [&](const char *name) {
-        std::vector<double> h0(pst * SS), h1(pst * SS);
-        CK(hipMemcpy(h0.data(), P0, pst * SS * 8, hipMemcpyDeviceToHost));
-        CK(hipMemcpy(h1.data(), P1, pst * SS * 8, hipMemcpyDeviceToHost));
-        double md = 0, mx = 0;
-        for (size_t q = 0; q < h0.size(); ++q) {
-            md = std::max(md, std::fabs(h0[q] - h1[q]));
-            mx = std::max(mx, std::fabs(h0[q]));
-        }
-        printf("   %s vs v0: max |diff| %.3e (max |v| %.3e)\n", name, md, mx);
-    };
-    printf("M=%d N=%d K=%d split=%d kchunk=%d grid=%u\n", M, N, K, SS, kchunk, grid.x);
-    run("v0 k_gemm_ts BK16", k_v0<16>, P0);
-    run("v0 BK32", k_v0<32>, P1);
-    cmp("v0 BK32");
-    run("v3 16-B loads BK16", k_v3<16>, P1);
-    cmp("v3 BK16");
-    run("v3 16-B loads BK32", k_v3<32>, P1);
-    cmp("v3 BK32");
-    run("v0 k_gemm_ts BK16 (again)", k_v0<16>, P0);
+    printf("M=%d N=%d K=%d\n", M, N, K);
+    run("v0 k_gemm_ts BK16", k_v0<16>, 128, 8, P0);
+    run("v0 k_gemm_ts BK16", k_v0<16>, 128, 16, P0);
+    run("v5 TM128 BK16 NBUF1 OCC3", k_v5<128, 16, 1, 3>, 128, 8, P1);
+    run("v5 TM128 BK16 NBUF1 OCC3", k_v5<128, 16, 1, 3>, 128, 16, P1);
+    run("v5 TM128 BK16 NBUF1 OCC4", k_v5<128, 16, 1, 4>, 128, 16, P1);
+    run("v5 TM128 BK8 NBUF2 OCC4", k_v5<128, 8, 2, 4>, 128, 16, P1);
+    run("v5 TM128 BK8 NBUF2 OCC3", k_v5<128, 8, 2, 3>, 128, 16, P1);
+    run("v5 TM64 BK16 NBUF2 OCC4", k_v5<64, 16, 2, 4>, 64, 8, P1);
+    run("v5 TM64 BK16 NBUF2 OCC4", k_v5<64, 16, 2, 4>, 64, 16, P1);
+    run("v5 TM128 BK16 NBUF2 OCC2", k_v5<128, 16, 2, 2>, 128, 8, P1);
+    run("v5 TM128 BK32 NBUF1 OCC2", k_v5<128, 32, 1, 2>, 128, 8, P1);
+    run("v5 TM128 BK32 NBUF1 OCC3", k_v5<128, 32, 1, 3>, 128, 16, P1);
+    run("v5 TM256 BK16 NBUF1 OCC2", k_v5<256, 16, 1, 2>, 256, 16, P1);
+    run("v5 TM256 BK8 NBUF2 OCC2", k_v5<256, 8, 2, 2>, 256, 16, P1);
+    run("v0 k_gemm_ts BK16 (again)", k_v0<16>, 128, 8, P0);
     return 0;
 }
