@@ -78,6 +78,14 @@ void tp_release_stream(const int *device, void *stream, int *status);
  * was loaded.  A caller that reuses its streams creates none after the first
  * call on each (tadpole_amd.genome's persistent stream pool is tested so). */
 void tp_context_stats(const int *device, int *live, int *created, int *status);
+/* Attach a host word to the context of (device, stream) (NULL detaches):
+ * every later tp_pipeline / tp_pipeline_dev on that context stores its stage
+ * there as it goes -- 0 started, 1 mask read back, 2 correlation queued,
+ * 3 PCA finished and the sweep about to be queued, 4 returned (success or
+ * failure) -- with release ordering, so another host thread can poll it to
+ * overlap work with this pipeline's later stages (the centromere arms: one
+ * arm's correlation and PCA under the other arm's CONISS sweep). */
+void tp_progress_attach(const int *device, void *stream, int *progress, int *status);
 int  tp_last_error(char *buf, int len);         /* ctypes form                   */
 void tp_last_error_r(char **buf, int *len);     /* R .C form                     */
 

@@ -661,11 +661,33 @@ def _tadpole_arms(raw, plan, max_pcs, min_clusters, device, shard_flag: int = 0,
         return _assemble(res, np.asarray(bad_cols))
 
     if _arms_concurrent(raw, shard_flag, stream):
+        # the q arm starts when the p arm's PCA is done (the library's
+        # progress word for p's stream): q's correlation and PCA (MFMA-bound,
+        # the whole chip) then run under p's CONISS sweep (latency-bound, one
+        # workgroup per tree), and the two sweeps do not compete for LDS
+        import time
         from concurrent.futures import ThreadPoolExecutor
         sp, sq = _arm_streams(device)
-        with ThreadPoolExecutor(max_workers=2) as ex:
-            fut = {"p": ex.submit(run_arm, "p", sp), "q": ex.submit(run_arm, "q", sq)}
-            subs = {arm: fut[arm].result() for arm in ("p", "q")}
+        L = _lib.load()
+        prog = np.zeros(1, np.int32)
+        st = cint(0)
+        L.tp_progress_attach(ctypes.byref(cint(device)), ctypes.c_void_p(sp.cuda_stream),
+                             prog.ctypes.data_as(ctypes.c_void_p), ctypes.byref(st))
+        _lib.check(st)
+        try:
+            with ThreadPoolExecutor(max_workers=2) as ex:
+                fp = ex.submit(run_arm, "p", sp)
+
+                def run_q():
+                    while prog[0] < 3 and not fp.done():
+                        time.sleep(2e-4)
+                    return run_arm("q", sq)
+
+                fq = ex.submit(run_q)
+                subs = {"p": fp.result(), "q": fq.result()}
+        finally:
+            L.tp_progress_attach(ctypes.byref(cint(device)), ctypes.c_void_p(sp.cuda_stream), None,
+                                 ctypes.byref(st))
     else:
         subs = {}
         for arm in ("p", "q"):

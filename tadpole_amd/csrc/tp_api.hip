@@ -13,9 +13,6 @@
 #include <thread>
 #include <vector>
 
-#include <rocblas/rocblas.h>
-#include <rocsolver/rocsolver.h>
-
 #include "../../include/tadpole_hip.h"
 #include "tp_internal.h"
 
@@ -288,7 +285,6 @@ Ctx::~Ctx() {
     for (auto &b : buf) b.release();
     pinned_flag.release();
     if (host_pinned) (void)hipHostFree(host_pinned);
-    if (blas) rocblas_destroy_handle((rocblas_handle)blas);
     if (side) {
         (void)hipStreamSynchronize(side);
         (void)hipStreamDestroy(side);
@@ -652,6 +648,17 @@ static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_cl
     c.prof = timings != nullptr;
     c.recs.clear();
     c.evnext = 0;
+    // the caller's progress word (tp_progress_attach): 0 started, 1 mask read
+    // back, 2 correlation queued, 3 PCA done (its last read-back) and the sweep
+    // about to be queued, 4 done -- set on every exit too (a failure reads 4)
+    struct Progress {
+        int *p;
+        void set(int v) {
+            if (p) __atomic_store_n(p, v, __ATOMIC_RELEASE);
+        }
+        ~Progress() { set(4); }
+    } progress{c.progress};
+    progress.set(0);
     tm.mark();
     // ---- load_mat cleaning + mask + subset (R/TADpole.R:19-20,35-37,88-89)
     if (!(flags & TP_FLAG_CLEAN)) launch_clean_symmetrize(d_M, n0, !(flags & TP_FLAG_ROW_MAJOR), s);
@@ -687,6 +694,7 @@ static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_cl
     }
     PipeOut o;
     o.n_good = n;
+    progress.set(1);
     if (n < 3) fail(TP_ERR_NO_BSTICK, "fewer than 3 good bins after masking");
     double *X = c.buf[S_X].as<double>((size_t)n * n);
     double *m = c.buf[S_COLMEAN].as<double>(n);
@@ -741,6 +749,7 @@ static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_cl
                 use_slab ? &slab : nullptr);
     trace_mark(s, "cor");
     tm.mark();
+    progress.set(2);
     // ---- prcomp (R/TADpole.R:452-453)
     o.k = k;
     if (k > k_cap) fail(TP_ERR_CAPACITY, "k_cap smaller than min(max_pcs, n_good)");
@@ -750,6 +759,7 @@ static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_cl
     trace_mark(s, "pca");
     tm.mark();
     // ---- find_params + final tree (R/TADpole.R:456-460)
+    progress.set(3);
     o.sw = run_sweep(c, Pt, n, k, min_clusters, w_cap, n_cluster, scores, merge, height, boundary);
     tm.mark();
     if (good_idx)
@@ -822,6 +832,13 @@ void tp_release_stream(const int *device, void *stream, int *status) {
     guarded(status, [&] {
         if (!stream) fail(TP_ERR_ARG, "tp_release_stream: NULL stream (the library stream is freed by tp_shutdown)");
         (void)ctx_release_stream(dev_of(device), (hipStream_t)stream);
+    });
+}
+
+void tp_progress_attach(const int *device, void *stream, int *progress, int *status) {
+    guarded(status, [&] {
+        Ctx &c = ctx_for(dev_of(device), (hipStream_t)stream);
+        c.progress = progress;
     });
 }
 
@@ -1008,7 +1025,7 @@ void tp_sweep_dev(const double *d_P, const int *n, const int *k, const int *min_
 void tp_coniss(const double *P, const int *n, const int *ncols, const int *device, int *merge, double *height,
                int *boundary, int *status) {
     guarded(status, [&] {
-        if (!P || !n || !ncols || *n < 2 || *ncols < 1 || *ncols > 512) fail(TP_ERR_ARG, "bad arguments");
+        if (!P || !n || !ncols || *n < 2 || *ncols < 1 || *ncols > 1024) fail(TP_ERR_ARG, "bad arguments");
         Ctx &c = ctx_for(dev_of(device));
         hipStream_t s = c.cur;
         const int N = *n, K = *ncols;
@@ -1067,7 +1084,7 @@ void tp_dist(const double *P, const int *n, const int *ncols, const int *device,
 void tp_ch(const double *P, const int *n, const int *k, const int *labels, const int *cn, const int *device,
            double *ch, int *status) {
     guarded(status, [&] {
-        if (!P || !n || !k || !labels || !cn || *n < 2 || *k < 1 || *k > 512 || *cn < 1 || !ch)
+        if (!P || !n || !k || !labels || !cn || *n < 2 || *k < 1 || *k > 1024 || *cn < 1 || !ch)
             fail(TP_ERR_ARG, "bad arguments");
         const int N = *n, K = *k, CN = *cn;
         std::vector<int> bnd(CN + 1);
@@ -1358,84 +1375,29 @@ void tp_debug_coniss_stamps(const double *P, const int *n, const int *k, long lo
 }
 
 
-/* rocSOLVER symmetric eigensolvers on a b x b matrix: ms[0] syevd, ms[1]
- * syevj, ms[2] syevdj; ev_out (b x 3) eigenvalues of each. */
-void tp_debug_eig(const double *H, const int *b, double *ms, double *ev_out, int *status) {
-    guarded(status, [&] {
-        Ctx &c = ctx_for(0);
-        hipStream_t s = c.cur;
-        const int B = *b;
-        rocblas_handle h;
-        if (rocblas_create_handle(&h) != rocblas_status_success) fail(TP_ERR_HIP, "handle");
-        (void)rocblas_set_stream(h, s);
-        double *dA = c.buf[S_SMALL].as<double>((size_t)B * B + 4 * B + 64);
-        double *dW = dA + (size_t)B * B, *dE = dW + B, *dRes = dE + B;
-        int *info = c.buf[S_MISC].as<int>(64);
-        int *nsw = info + 8;
-        hipEvent_t e0, e1;
-        TP_HIP(hipEventCreate(&e0));
-        TP_HIP(hipEventCreate(&e1));
-        double *dWork = c.buf[S_PARTIAL].as<double>((size_t)B * B + 4 * B + 64);
-        for (int which = 0; which < 5; ++which) {
-            float best = 1e30f;
-            for (int rep = 0; rep < 3; ++rep) {
-                TP_HIP(hipMemcpyAsync(dA, H, (size_t)B * B * 8, hipMemcpyHostToDevice, s));
-                TP_HIP(hipEventRecord(e0, s));
-                rocblas_status st = rocblas_status_success;
-                if (which == 0)
-                    st = rocsolver_dsyevd(h, rocblas_evect_original, rocblas_fill_upper, B, dA, B, dW, dE, info);
-                else if (which == 1)
-                    st = rocsolver_dsyevj(h, rocblas_esort_ascending, rocblas_evect_original, rocblas_fill_upper, B,
-                                          dA, B, 1e-14, dRes, 20, nsw, dW, info);
-                else if (which == 2)
-                    st = rocsolver_dsyevdj(h, rocblas_evect_original, rocblas_fill_upper, B, dA, B, dW, info);
-                else
-                    tp::eig_sym(h, dA, B, dW, dWork, info, s, which - 3);
-                TP_HIP(hipEventRecord(e1, s));
-                TP_HIP(hipEventSynchronize(e1));
-                if (st != rocblas_status_success) { best = -1; break; }
-                float t = 0;
-                TP_HIP(hipEventElapsedTime(&t, e0, e1));
-                best = std::min(best, t);
-            }
-            ms[which] = best;
-            TP_HIP(hipMemcpy(ev_out + (size_t)which * B, dW, B * 8, hipMemcpyDeviceToHost));
-            if (which == 4) {   // eigenvectors of the custom path: ev_out[5B ..) = V (B x B)
-                TP_HIP(hipMemcpy(ev_out + (size_t)5 * B, dA, (size_t)B * B * 8, hipMemcpyDeviceToHost));
-            }
-        }
-        (void)hipEventDestroy(e0);
-        (void)hipEventDestroy(e1);
-        (void)rocblas_destroy_handle(h);
-    });
-}
-
 }  // extern "C"
 
 extern "C" {
 // Test hook for the PCA's Rayleigh-Ritz eigensolver (tp_eig.hip, not part of the
-// reference-facing ABI): H (b x b, column-major, symmetric) -> theta ascending,
-// V eigenvectors (columns).  method 0: sytrd + rocSOLVER dstedc, 1: sytrd +
-// bisection + inverse iteration (the product path).
+// reference-facing ABI): H (b x b, column-major, symmetric, b <= 1280) -> theta
+// ascending, V eigenvectors (columns): tridiagonalisation + bisection + inverse
+// iteration (the product path; *method is ignored -- the rocSOLVER dstedc
+// variant of earlier builds is gone).
 void tp_debug_eigsym(const double *H, const int *b, const int *method, double *theta, double *V, int *status) {
     guarded(status, [&] {
         Ctx &c = ctx_for(0);
         hipStream_t s = c.cur;
         const int B = *b;
-        if (!tp::eig_sym_supported(B)) fail(TP_ERR_UNSUPPORTED, "b > 640 (EIG_BMAX)");
-        rocblas_handle h;
-        if (rocblas_create_handle(&h) != rocblas_status_success) fail(TP_ERR_HIP, "handle");
-        (void)rocblas_set_stream(h, s);
+        (void)method;
+        if (!tp::eig_sym_supported(B)) fail(TP_ERR_UNSUPPORTED, "b > 1280 (EIG_BMAX)");
         double *dA = c.buf[S_SMALL].as<double>((size_t)B * B + B + 64);
         double *dW = dA + (size_t)B * B;
         double *dWork = c.buf[S_PARTIAL].as<double>((size_t)B * B + 4 * B + 64);
-        int *info = c.buf[S_MISC].as<int>(64);
         TP_HIP(hipMemcpyAsync(dA, H, (size_t)B * B * 8, hipMemcpyHostToDevice, s));
-        tp::eig_sym(h, dA, B, dW, dWork, info, s, *method);
+        tp::eig_sym(dA, B, dW, dWork, s);
         TP_HIP(hipMemcpyAsync(theta, dW, (size_t)B * 8, hipMemcpyDeviceToHost, s));
         TP_HIP(hipMemcpyAsync(V, dA, (size_t)B * B * 8, hipMemcpyDeviceToHost, s));
         TP_HIP(hipStreamSynchronize(s));
-        (void)rocblas_destroy_handle(h);
     });
 }
 }  // extern "C"

@@ -22,7 +22,7 @@ namespace tp {
 
 constexpr int NB = 32;
 constexpr int BMAX = 480;       // the panel in LDS
-constexpr int BMAX_BIG = 640;   // PG: the panel in global scratch (L2), b up to 640 (k <= 512)
+constexpr int BMAX_BIG = 1280;  // PG: the panel in global scratch (L2), b up to 1280 (k <= 1024)
 constexpr int NT = 512;   // threads of k_chol: 8 waves, 256 VGPRs each
 
 // PG: the 32-row panel lives in global scratch Pg (ld b + 8) instead of LDS
@@ -263,9 +263,57 @@ __global__ void __launch_bounds__(TR * TC) k_trsm_ru(const double *Z, int n, int
         for (int cc = c; cc < b; cc += TC) Q[(size_t)cc * n + row] = Qs[r][cc];
 }
 
+// b > 640: the same solve with U's column block staged in chunks of CH rows
+// (Ub for a whole column block of U no longer fits the LDS beside Q's rows)
+template <int TR, int BM, int CH>
+__global__ void __launch_bounds__(TR * TC) k_trsm_ru_big(const double *Z, int n, int b, const double *U,
+                                                         const double *rdiag, double *Q) {
+    __shared__ double Qs[TR][BM + 1];
+    __shared__ double Ub[TC][CH + 1];
+    const int t = threadIdx.x;
+    const int r = t % TR, c = t / TR;
+    const int row = blockIdx.x * TR + r;
+    const bool live = row < n;
+    for (int o = 0; o < b; o += TC) {
+        double acc = live ? Z[(size_t)(o + c) * n + row] : 0.0;
+        for (int m0 = 0; m0 < o; m0 += CH) {   // rows m0 .. m0 + mlen - 1 of U's column block o
+            const int mlen = min(CH, o - m0);
+            __syncthreads();
+            for (int e = t; e < mlen * TC; e += TR * TC) {
+                const int mm = e % mlen, cc = e / mlen;
+                Ub[cc][mm] = U[(size_t)(o + cc) * b + m0 + mm];
+            }
+            __syncthreads();
+            for (int m = 0; m < mlen; ++m) acc = acc - Qs[r][m0 + m] * Ub[c][m];
+        }
+        __syncthreads();
+        for (int e = t; e < TC * TC; e += TR * TC) {   // the diagonal block U[o:o+TC, o:o+TC]
+            const int mm = e % TC, cc = e / TC;
+            Ub[cc][mm] = U[(size_t)(o + cc) * b + o + mm];
+        }
+        Qs[r][o + c] = acc;
+        __syncthreads();
+        if (c == 0) {
+            double q[TC];
+#pragma unroll
+            for (int cc = 0; cc < TC; ++cc) {
+                double v = Qs[r][o + cc];
+#pragma unroll
+                for (int c2 = 0; c2 < cc; ++c2) v = v - q[c2] * Ub[cc][c2];
+                q[cc] = v * rdiag[o + cc];
+            }
+#pragma unroll
+            for (int cc = 0; cc < TC; ++cc) Qs[r][o + cc] = q[cc];
+        }
+        __syncthreads();
+    }
+    if (live)
+        for (int cc = c; cc < b; cc += TC) Q[(size_t)cc * n + row] = Qs[r][cc];
+}
+
 size_t chol_panel_doubles(int b) { return b > BMAX ? (size_t)NB * (b + 8) : 0; }
 void launch_chol(double *d_W, double *d_rdiag, int b, double rel, int *d_info, hipStream_t s, double *d_panel) {
-    if (b % NB != 0 || b > BMAX_BIG) fail(TP_ERR_ARG, "chol: block size must be a multiple of 32, <= 640");
+    if (b % NB != 0 || b > BMAX_BIG) fail(TP_ERR_ARG, "chol: block size must be a multiple of 32, <= 1280");
     if (b > BMAX) {
         if (!d_panel) fail(TP_ERR_ARG, "chol: b > 480 needs panel scratch (chol_panel_doubles)");
         hipLaunchKernelGGL((k_chol_t<false, true>), dim3(1), dim3(NT), 0, s, d_W, d_rdiag, b, rel, d_info, nullptr,
@@ -286,12 +334,14 @@ void launch_chol_stamped(double *d_W, double *d_rdiag, int b, double rel, int *d
 
 void launch_trsm_ru(const double *d_Z, int n, int b, const double *d_U, const double *d_rdiag, double *d_Q,
                     hipStream_t s) {
-    if (b % TC != 0 || b > BMAX_BIG) fail(TP_ERR_ARG, "trsm: block size must be a multiple of 16, <= 640");
+    if (b % TC != 0 || b > BMAX_BIG) fail(TP_ERR_ARG, "trsm: block size must be a multiple of 16, <= 1280");
     if (b <= BMAX)
         hipLaunchKernelGGL((k_trsm_ru<16, BMAX>), dim3((n + 15) / 16), dim3(256), 0, s, d_Z, n, b, d_U, d_rdiag, d_Q);
+    else if (b <= 640)
+        hipLaunchKernelGGL((k_trsm_ru<8, 640>), dim3((n + 7) / 8), dim3(128), 0, s, d_Z, n, b, d_U, d_rdiag, d_Q);
     else
-        hipLaunchKernelGGL((k_trsm_ru<8, BMAX_BIG>), dim3((n + 7) / 8), dim3(128), 0, s, d_Z, n, b, d_U, d_rdiag,
-                           d_Q);
+        hipLaunchKernelGGL((k_trsm_ru_big<8, BMAX_BIG, 256>), dim3((n + 7) / 8), dim3(128), 0, s, d_Z, n, b, d_U,
+                           d_rdiag, d_Q);
     TP_HIP(hipGetLastError());
 }
 

@@ -1,6 +1,6 @@
 // Symmetric eigendecomposition of the small b x b Rayleigh-Ritz matrix of the
-// PCA (H = Q'GQ, b = block size, <= 640), replacing rocSOLVER dsyevd whose
-// hundreds of tiny launches (latrd column by column) dominated the PCA.
+// PCA (H = Q'GQ, b = block size, <= 1280: k <= 1024), the library's own
+// kernels only (a rocSOLVER dsyevd spent hundreds of tiny launches in latrd).
 //
 //   k_sytrd_l   one 1024-thread workgroup reduces H to tridiagonal T = Q_H' H Q_H
 //               (Householder, LAPACK dsytd2 'L' conventions: reflector j has
@@ -10,23 +10,26 @@
 //               p = A22 v of step j+1: one read + one write of the trailing
 //               matrix per step (L2-resident), column dots by wave reductions,
 //               row dots in per-lane registers (lane owns rows r = 64q + lane).
-//   rocsolver_dstedc  eigenpairs of T (divide and conquer)
+//   k_sytrd_reg the same with the matrix in registers (b <= 256).
+//   k_bisect / k_invit  eigenpairs of T (Sturm bisection, inverse iteration).
 //   k_ormtr_l   C <- Q_H C: one wave per column of C, reflectors applied in
 //               reverse order with the column held in registers.
-#include <rocblas/rocblas.h>
-#include <rocsolver/rocsolver.h>
-
 #include "tp_common.cuh"
 #include "tp_internal.h"
 
 namespace tp {
 
-constexpr int EIG_BMAX = 640;   // b = k + oversampling for k <= 512
+constexpr int EIG_BMAX = 1280;   // b = k + oversampling for k <= 1024
 constexpr int SY_WAVES = 16;
 
+// QM = rows per lane (b <= 64 QM).  NPR rows of per-wave partials in LDS: 16
+// (one per wave) up to QM = 10; for QM = 20 (b <= 1280) 8, the waves of the
+// upper half adding theirs to the lower half's rows in a second round.
 template <int QM, bool ST = false>
 __global__ void __launch_bounds__(1024) k_sytrd_l(double *A, int b, double *d, double *e, double *tau,
                                                   long long *stamps = nullptr) {
+    constexpr int BM = 64 * QM;
+    constexpr int NPR = QM > 10 ? 8 : SY_WAVES;
     long long sacc[4] = {0, 0, 0, 0};
     long long st0 = ST ? (long long)__builtin_amdgcn_s_memtime() : 0;
 #define SY_STAMP(ph)                                                      \
@@ -35,14 +38,14 @@ __global__ void __launch_bounds__(1024) k_sytrd_l(double *A, int b, double *d, d
         sacc[ph] += _t - st0;                                             \
         st0 = _t;                                                         \
     }
-    __shared__ double V[2][EIG_BMAX], W[2][EIG_BMAX], PC[EIG_BMAX];
-    __shared__ double PRW[SY_WAVES][EIG_BMAX];
+    __shared__ double V[2][BM], W[2][BM], PC[BM];
+    __shared__ double PRW[NPR][BM];
     __shared__ double RED[SY_WAVES + 8];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     double vold[QM], wold[QM], vnew[QM], prow[QM], nxt[QM];
 #pragma unroll
     for (int q = 0; q < QM; ++q) vold[q] = wold[q] = nxt[q] = 0.0;
-    for (int r = t; r < EIG_BMAX; r += 1024) V[1][r] = W[1][r] = V[0][r] = W[0][r] = 0.0;
+    for (int r = t; r < BM; r += 1024) V[1][r] = W[1][r] = V[0][r] = W[0][r] = 0.0;
     __syncthreads();
 
     for (int j = 0; j + 2 < b; ++j) {
@@ -154,18 +157,34 @@ __global__ void __launch_bounds__(1024) k_sytrd_l(double *A, int b, double *d, d
                 if (lane == 0 && c < b) PC[c] = ps;
             }
         }
+        if (NPR == SY_WAVES || wv < NPR) {
 #pragma unroll
-        for (int q = 0; q < QM; ++q) PRW[wv][64 * q + lane] = prow[q];
+            for (int q = 0; q < QM; ++q) PRW[wv][64 * q + lane] = prow[q];
+        }
+        if (NPR < SY_WAVES) {
+            __syncthreads();
+            if (wv >= NPR) {
+#pragma unroll
+                for (int q = 0; q < QM; ++q) PRW[wv - NPR][64 * q + lane] += prow[q];
+            }
+        }
         __syncthreads();
         SY_STAMP(1);
-        // ---- (d) p = tau A22 v, alpha2 = -tau/2 p'v, w = p + alpha2 v
-        double p = 0.0, pv = 0.0;
-        if (t < b && t >= j + 1) {
-            double s = PC[t];
+        // ---- (d) p = tau A22 v, alpha2 = -tau/2 p'v, w = p + alpha2 v (rows
+        //      t, t + 1024, ... of this thread)
+        constexpr int RT = (BM + 1023) / 1024;
+        double p[RT], pv = 0.0;
 #pragma unroll
-            for (int w = 0; w < SY_WAVES; ++w) s = s + PRW[w][t];
-            p = tj * s;
-            pv = p * V[P][t];
+        for (int u = 0; u < RT; ++u) {
+            const int rr = t + 1024 * u;
+            p[u] = 0.0;
+            if (rr < b && rr >= j + 1) {
+                double s = PC[rr];
+#pragma unroll
+                for (int w = 0; w < NPR; ++w) s = s + PRW[w][rr];
+                p[u] = tj * s;
+                pv = fma(p[u], V[P][rr], pv);
+            }
         }
         pv = wave_sum(pv);
         if (lane == 0) RED[wv] = pv;
@@ -174,7 +193,11 @@ __global__ void __launch_bounds__(1024) k_sytrd_l(double *A, int b, double *d, d
 #pragma unroll
         for (int w = 0; w < SY_WAVES; ++w) dot = dot + RED[w];
         const double alpha2 = -0.5 * tj * dot;
-        if (t < EIG_BMAX) W[P][t] = (t < b && t >= j + 1) ? fma(alpha2, V[P][t], p) : 0.0;
+#pragma unroll
+        for (int u = 0; u < RT; ++u) {
+            const int rr = t + 1024 * u;
+            if (rr < BM) W[P][rr] = (rr < b && rr >= j + 1) ? fma(alpha2, V[P][rr], p[u]) : 0.0;
+        }
         __syncthreads();
 #pragma unroll
         for (int q = 0; q < QM; ++q) {
@@ -589,7 +612,7 @@ __device__ __forceinline__ int sturm_count(const double *sd, const double *se2, 
 // lam[idx] = idx-th smallest eigenvalue (midpoint of a ~2-ulp bracket);
 // lam[b] = ||T|| bound (Gershgorin), written by block 0.
 __global__ void __launch_bounds__(256) k_bisect(const double *d, const double *e, int b, double *lam) {
-    __shared__ double sd[EIG_BMAX], se[EIG_BMAX], red[32];
+    __shared__ double sd[EIG_BMAX], se[EIG_BMAX], red[32];   // 20 KB at EIG_BMAX = 1280
     const TriNorm tn = tri_bounds(d, e, b, sd, se, red);
     for (int i = threadIdx.x; i + 1 < b; i += blockDim.x) se[i] = se[i] * se[i];   // e^2 for the counts
     __syncthreads();
@@ -625,19 +648,21 @@ __device__ __forceinline__ double hash_unit(unsigned int m, unsigned int i) {
 }
 
 // Z (b x b, column m = eigenvector m), theta[m] = Rayleigh quotient.  dd holds
-// the reciprocal pivots of U.
-__global__ void __launch_bounds__(256) k_invit(const double *d, const double *e, int b, const double *lam,
-                                               double *Z, double *theta) {
-    __shared__ double sd[EIG_BMAX], se[EIG_BMAX];
-    __shared__ double dd[4][EIG_BMAX], du[4][EIG_BMAX], du2[4][EIG_BMAX], dl[4][EIG_BMAX], xv[4][EIG_BMAX];
-    __shared__ unsigned char swp[4][EIG_BMAX];
+// the reciprocal pivots of U.  NV vectors (waves) per workgroup, b <= BM: 4 for
+// b <= 640, 1 above (the LU factors of one vector take 5 BM doubles of LDS).
+template <int BM, int NV>
+__global__ void __launch_bounds__(64 * NV) k_invit(const double *d, const double *e, int b, const double *lam,
+                                                   double *Z, double *theta) {
+    __shared__ double sd[BM], se[BM];
+    __shared__ double dd[NV][BM], du[NV][BM], du2[NV][BM], dl[NV][BM], xv[NV][BM];
+    __shared__ unsigned char swp[NV][BM];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    for (int i = t; i < b; i += 256) {
+    for (int i = t; i < b; i += 64 * NV) {
         sd[i] = d[i];
         se[i] = i + 1 < b ? e[i] : 0.0;
     }
     __syncthreads();
-    const int idx = blockIdx.x * 4 + wv;
+    const int idx = blockIdx.x * NV + wv;
     if (idx >= b) return;
     const double tnorm = lam[b];
     const double eps = 2.220446049250313e-16;
@@ -740,20 +765,16 @@ __global__ void __launch_bounds__(256) k_invit(const double *d, const double *e,
     }
 }
 
-static void rb_ok(rocblas_status st, const char *what) {
-    if (st != rocblas_status_success) fail(TP_ERR_HIP, std::string("rocSOLVER failure in ") + what);
-}
-
 bool eig_sym_supported(int b) { return b >= 1 && b <= EIG_BMAX; }
 int g_sytrd_reg = 1;   // diagnostics switch: 0 = the L2-resident k_sytrd_l
 
 // In place: A (b x b, lower triangle of a symmetric matrix) <- eigenvectors,
-// theta <- eigenvalues ascending.  work: >= b*b + 4*b + 8 doubles; info: device
-// int (dstedc path).  method 0: rocSOLVER dstedc for the tridiagonal stage,
-// 1: k_bisect + k_invit.
-void eig_sym(rocblas_handle h, double *A, int b, double *theta, double *work, int *info, hipStream_t s,
-             int method) {
-    if (!eig_sym_supported(b)) fail(TP_ERR_UNSUPPORTED, "eig_sym: b > 640");
+// theta <- eigenvalues ascending, b <= EIG_BMAX (1280: k <= 1024).  work: >=
+// b*b + 4*b + 8 doubles.  Tridiagonalisation (register-resident for b <= 256 a
+// multiple of 16, else L2-resident), Sturm bisection + inverse iteration,
+// back-transformation -- the library's own kernels only (no rocSOLVER).
+void eig_sym(double *A, int b, double *theta, double *work, hipStream_t s) {
+    if (!eig_sym_supported(b)) fail(TP_ERR_UNSUPPORTED, "eig_sym: b > 1280 (EIG_BMAX)");
     double *C = work, *e = C + (size_t)b * b, *tau = e + b, *dg = tau + b, *lam = dg + b;   // lam: b + 1
     if (sytrd_reg_supported(b) && g_sytrd_reg)
         hipLaunchKernelGGL(k_sytrd_reg, dim3(1), dim3(1024), 0, s, A, b, dg, e, tau);
@@ -761,24 +782,28 @@ void eig_sym(rocblas_handle h, double *A, int b, double *theta, double *work, in
         hipLaunchKernelGGL((k_sytrd_l<4, false>), dim3(1), dim3(1024), 0, s, A, b, dg, e, tau, (long long *)nullptr);
     else if (b <= 512)
         hipLaunchKernelGGL((k_sytrd_l<8, false>), dim3(1), dim3(1024), 0, s, A, b, dg, e, tau, (long long *)nullptr);
-    else
+    else if (b <= 640)
         hipLaunchKernelGGL((k_sytrd_l<10, false>), dim3(1), dim3(1024), 0, s, A, b, dg, e, tau, (long long *)nullptr);
+    else
+        hipLaunchKernelGGL((k_sytrd_l<20, false>), dim3(1), dim3(1024), 0, s, A, b, dg, e, tau, (long long *)nullptr);
     TP_HIP(hipGetLastError());
-    if (method == 0) {
-        TP_HIP(hipMemcpyAsync(theta, dg, (size_t)b * sizeof(double), hipMemcpyDeviceToDevice, s));
-        rb_ok(rocsolver_dstedc(h, rocblas_evect_tridiagonal, b, theta, e, C, b, info), "dstedc");
-    } else {
+    {
         const unsigned g = (unsigned)((b + 3) / 4);
         hipLaunchKernelGGL(k_bisect, dim3(g), dim3(256), 0, s, dg, e, b, lam);
-        hipLaunchKernelGGL(k_invit, dim3(g), dim3(256), 0, s, dg, e, b, lam, C, theta);
+        if (b <= 640)
+            hipLaunchKernelGGL((k_invit<640, 4>), dim3(g), dim3(256), 0, s, dg, e, b, lam, C, theta);
+        else
+            hipLaunchKernelGGL((k_invit<EIG_BMAX, 1>), dim3((unsigned)b), dim3(64), 0, s, dg, e, b, lam, C, theta);
         TP_HIP(hipGetLastError());
     }
     if (b <= 256)
         hipLaunchKernelGGL(k_ormtr_l<4>, dim3((b + 3) / 4), dim3(256), 0, s, A, tau, b, C);
     else if (b <= 512)
         hipLaunchKernelGGL(k_ormtr_l<8>, dim3((b + 3) / 4), dim3(256), 0, s, A, tau, b, C);
-    else
+    else if (b <= 640)
         hipLaunchKernelGGL(k_ormtr_l<10>, dim3((b + 3) / 4), dim3(256), 0, s, A, tau, b, C);
+    else
+        hipLaunchKernelGGL(k_ormtr_l<20>, dim3((b + 3) / 4), dim3(256), 0, s, A, tau, b, C);
     TP_HIP(hipGetLastError());
     TP_HIP(hipMemcpyAsync(A, C, (size_t)b * b * sizeof(double), hipMemcpyDeviceToDevice, s));
 }

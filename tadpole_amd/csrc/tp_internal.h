@@ -1,8 +1,6 @@
 // Internal declarations shared by the HIP translation units of libtadpole_hip.
 // Nothing here is part of the C ABI (include/tadpole_hip.h is).
 #pragma once
-#include <rocblas/rocblas.h>
-
 #include <hip/hip_runtime.h>
 #include <cstddef>
 #include <cstdint>
@@ -71,7 +69,6 @@ struct Ctx {
     int last_xtx_ns = 0;            // int8 slices of the last X'X product (0: fp64 MFMA product)
     hipStream_t stream = nullptr;   // library stream (or the caller's, owns_stream = false)
     bool owns_stream = false;
-    void *blas = nullptr;           // rocblas_handle of this context (lazily created)
     hipStream_t cur = nullptr;      // stream used by the current call
     hipStream_t side = nullptr;     // fork-join helper stream (side_stream())
     hipEvent_t fork_ev = nullptr, join_ev = nullptr;
@@ -80,6 +77,7 @@ struct Ctx {
     void *host_pinned = nullptr;    // small pinned staging area
     size_t host_pinned_bytes = 0;
     hipEvent_t ring_ev[4] = {};     // tp_read_tsv_dev: one event per staging-ring slot
+    int *progress = nullptr;        // tp_progress_attach: host word, the pipeline's stage (1 mask .. 4 done)
     void *pinned(size_t b);
 };
 
@@ -177,7 +175,7 @@ void launch_r1_apply(const double *T, size_t rs, size_t cs, int N, int rows, int
 extern int g_gemm_panel;   // short-K tall-skinny 32 x 64 kernel enabled (default 1)
 extern int g_gemm_kb;      // LDS stage depth of the 64 x 64 kernel (16 / 32)
 extern int g_gemm_xcd;     // XCD-aware workgroup order of the 64 x 64 kernel (default 1)
-// b <= 640 (a multiple of 32); b > 480 needs chol_panel_doubles(b) of scratch
+// b <= 1280 (a multiple of 32); b > 480 needs chol_panel_doubles(b) of scratch
 size_t chol_panel_doubles(int b);
 void launch_chol(double *d_W, double *d_rdiag, int b, double rel, int *d_info, hipStream_t s,
                  double *d_panel = nullptr);
@@ -258,17 +256,16 @@ __host__ __device__ inline size_t coniss_link_stride(int n) { return (size_t)n +
 // initial costs (ntrees x cost stride) + link scratch of the global-memory
 // CONISS variant (ntrees x 2 link strides of ints)
 // row-major scores Pt (n x k) + slack: CONISS reads whole 64-column slots of a
-// row (up to 512 columns) and masks the columns past its prefix
-inline size_t pt_doubles(int n, int k) { return (size_t)n * k + 512; }
+// row (up to 1024 columns) and masks the columns past its prefix
+inline size_t pt_doubles(int n, int k) { return (size_t)n * k + 1024; }
 // + the copy of the scores with column pairs (l, l + 64) adjacent that CONISS
-// reads (n x 256, or n x 512 for k > 256; see k_pt_pairs in tp_sweep.hip),
-// + the fully paired copy the 4-slot trees read (n x 256, when k > 192)
+// reads (n x 64 KS: 256, 512 for k > 256, 1024 for k > 512; see k_pt_pairs in
+// tp_sweep.hip), + the fully paired copy the 4-slot trees read (n x 256, when k > 192)
 inline size_t sweep_cost0_doubles(int n, int ntrees, int k = 256) {
-    return (size_t)ntrees * (coniss_cost_stride(n) + coniss_link_stride(n)) + 2 + (size_t)n * (k > 256 ? 512 : 256) +
-           (k > 192 ? (size_t)n * 256 : 0);
+    return (size_t)ntrees * (coniss_cost_stride(n) + coniss_link_stride(n)) + 2 +
+           (size_t)n * (k > 512 ? 1024 : (k > 256 ? 512 : 256)) + (k > 192 ? (size_t)n * 256 : 0);
 }
 size_t sweep_sums_doubles(int n, int tree0, int ntrees);
-void blas_shutdown_all();
 void launch_sweep(const SweepDev &sd, hipStream_t s, Ctx *prof = nullptr);
 void launch_coniss_only(const SweepDev &sd, hipStream_t s);
 // CH of the trees whose finest cut has more than 1024 segments (k_ch's LDS
@@ -282,17 +279,15 @@ void launch_dist(const double *d_P, int n, int ldp, int ncols, double *d_d, hipS
 void launch_transpose(const double *d_A, int rows, int cols, int lda, double *d_T, int ldt,
                       hipStream_t s);
 
-// PCA (tp_pca.cpp): P (n x k col-major, ld n) and Pt (n x k row-major) from C.
-// Symmetric eigendecomposition for b <= 512 (tp_eig.hip): A (b x b, lower
+// PCA (tp_pca.hip): P (n x k col-major, ld n) and Pt (n x k row-major) from C.
+// Symmetric eigendecomposition for b <= 1280 (tp_eig.hip): A (b x b, lower
 // triangle) <- eigenvectors, theta <- ascending eigenvalues.  work >= b*b + 4b + 8.
-// method 0: tridiagonal stage by rocSOLVER dstedc, 1: bisection + inverse iteration.
 bool eig_sym_supported(int b);
 extern int g_sytrd_reg;
 void sytrd_stamped(double *A, int b, double *work, long long *d_stamps, hipStream_t s);
 void sytrd_which(double *A, int b, double *work, int which, hipStream_t s,
                  long long *d_stamps = nullptr);   // work: 3b (e, tau, d)
-void eig_sym(rocblas_handle h, double *A, int b, double *theta, double *work, int *info, hipStream_t s,
-             int method = 1);
+void eig_sym(double *A, int b, double *theta, double *work, hipStream_t s);
 
 // tp_io.hip: native reader of read.big.matrix(sep = '\t') files (host code)
 void tsv_dims(const char *path, int *nrow, int *ncol);

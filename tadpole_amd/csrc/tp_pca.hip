@@ -22,9 +22,6 @@
 // ||G v - theta v|| <= tol * theta_1 (checked in the N-dimensional space), and
 // the scores are P = Xc V_k (fp64 MFMA GEMM).  When N <= b the Ritz problem is
 // G itself (exact full eigendecomposition).
-#include <rocblas/rocblas.h>
-#include <rocsolver/rocsolver.h>
-
 #include <algorithm>
 #include <cmath>
 #include <functional>
@@ -39,22 +36,6 @@
 
 namespace tp {
 
-static void rb_check(rocblas_status st, const char *what) {
-    if (st != rocblas_status_success) fail(TP_ERR_HIP, std::string("rocBLAS/rocSOLVER failure in ") + what);
-}
-
-static rocblas_handle blas_for(Ctx &c) {
-    if (!c.blas) {
-        rocblas_handle h;
-        rb_check(rocblas_create_handle(&h), "rocblas_create_handle");
-        c.blas = h;
-    }
-    rocblas_handle h = (rocblas_handle)c.blas;
-    rb_check(rocblas_set_stream(h, c.cur), "rocblas_set_stream");
-    return h;
-}
-
-void blas_shutdown_all() {}   // handles are per context (freed with it)
 
 // deterministic pseudo-random start block, uniform in (-1, 1)
 __global__ void k_rand_block(double *Q, int n, int b, uint64_t seed) {
@@ -250,19 +231,13 @@ static void subspace_topk(Ctx &c, const double *A, int n, int k, const Prod &pro
     st.block = b;
     if (b >= n) {
         // exact: eigendecomposition of A itself (small n)
-        rocblas_handle h = blas_for(c);
         b = n;
         int *d_info = c.buf[S_MISC].as<int>(64);
         double *theta = c.buf[S_SMALL].as<double>((size_t)n + 64);
         double *E = c.buf[S_Z].as<double>((size_t)n * n);
         TP_HIP(hipMemcpyAsync(E, A, (size_t)n * n * sizeof(double), hipMemcpyDeviceToDevice, s));
-        double *offbuf = c.buf[S_Q].as<double>((size_t)n + 64);
-        if (eig_sym_supported(n))
-            eig_sym(h, E, n, theta, c.buf[S_PARTIAL].as<double>((size_t)n * n + 4 * n + 64), d_info, s);
-        else
-            rb_check(rocsolver_dsyevd(h, rocblas_evect_original, rocblas_fill_upper, n, E, n, theta, offbuf,
-                                      d_info),
-                     "dsyevd");
+        (void)d_info;
+        eig_sym(E, n, theta, c.buf[S_PARTIAL].as<double>((size_t)n * n + 4 * n + 64), s);   // n <= b <= 1280
         size_t tot = (size_t)n * k;
         hipLaunchKernelGGL(k_select_rev, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, E, n, k, V);
         TP_HIP(hipGetLastError());
@@ -403,7 +378,6 @@ static void subspace_topk(Ctx &c, const double *A, int n, int k, const Prod &pro
     }
     std::vector<double> h_res(k);
     h_theta.resize(b);
-    rocblas_handle h = blas_for(c);
     for (int round = 0; round < 6; ++round) {
         // Rayleigh-Ritz: orthonormalise tightly, H = Q'AQ, eigen-decompose, rotate
         // Q is orthonormal to ~kappa^2 eps after the last one-pass CholQR:
@@ -415,12 +389,7 @@ static void subspace_topk(Ctx &c, const double *A, int n, int k, const Prod &pro
         hq.sym_upper = true;
         hq.splitk = std::max(1, std::min(32, n / 128));
         gemm_f64(hq, c.buf[S_PARTIAL], s);
-        if (eig_sym_supported(b))
-            eig_sym(h, Wsm, b, theta, c.buf[S_PARTIAL].as<double>((size_t)b * b + 4 * b + 64), d_info, s);
-        else
-            rb_check(rocsolver_dsyevd(h, rocblas_evect_original, rocblas_fill_upper, b, Wsm, b, theta, offd,
-                                      d_info),
-                     "dsyevd(RR)");
+        eig_sym(Wsm, b, theta, c.buf[S_PARTIAL].as<double>((size_t)b * b + 4 * b + 64), s);
         size_t tot = (size_t)b * b;
         hipLaunchKernelGGL(k_select_rev, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, Wsm, b, b, Xinv);
         // rotate: V = Q X (into T); A V = (A Q) X = Z X for the residuals of

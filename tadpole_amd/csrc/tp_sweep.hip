@@ -24,11 +24,11 @@
 namespace tp {
 
 // KS: 64-column slots per lane of the kernels that hold all k PCs (4: k <= 256,
-// 8: k <= 512, chosen per launch).  A column past k contributes nothing (its
+// 8: k <= 512, 16: k <= 1024, chosen per launch).  A column past k contributes nothing (its
 // slot is skipped or adds fma(0, 0, acc) = acc), so the bits for k <= 256 are
 // the same with either instance.
-constexpr int KS_MAX = 8;
-inline int ks_for(int k) { return k <= 256 ? 4 : 8; }
+constexpr int KS_MAX = 16;
+inline int ks_for(int k) { return k <= 256 ? 4 : (k <= 512 ? 8 : 16); }
 constexpr int ROW_PT = 1 << 30;   // CONISS row code flag: the row is in Pt (a singleton)
 
 // pairwise tree over 64 leaves = the xor butterfly's summation tree
@@ -299,6 +299,28 @@ __device__ __forceinline__ double ward_part(const double (&sa)[NS], double fa, c
 // barrier with both waves choosing was slower: B's prefetch of a2's rows then
 // has only B's own choice to hide behind, and HBM latency shows.)  Mailbox
 // words are written before one barrier and read after it.
+// Build switches (A/B builds of the merge loop; the product uses the defaults):
+// TP_CONISS_BMI    block argmin positions kept in registers beside the block
+//                  minima (the speculative argmin reads no block of costs)
+// TP_CONISS_LDSBAR LDS-only barriers X and Y (global loads stay in flight)
+// TP_CONISS_GLBPF  costs-in-global variant: the next merge's three cost blocks
+//                  loaded right after the choice, patched at the merge's start
+#ifndef TP_CONISS_BMI
+#define TP_CONISS_BMI 0
+#endif
+#ifndef TP_CONISS_LDSBAR
+#define TP_CONISS_LDSBAR 0
+#endif
+#ifndef TP_CONISS_GLBPF
+#define TP_CONISS_GLBPF 0
+#endif
+__device__ __forceinline__ void coniss_bar() {
+#if TP_CONISS_LDSBAR
+    lds_barrier();
+#else
+    __syncthreads();
+#endif
+}
 template <bool STAMPS, int NS, int BS, bool GLB, bool LU = false>
 __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, double *lds, double *mb_d,
                                              int4 *mb_i) {
@@ -314,6 +336,8 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
     const int ti = blockIdx.x;
     const int i = sd.tree0 + ti + 1;
     constexpr int ld = NS * 64;
+    constexpr bool kBmi = TP_CONISS_BMI != 0;
+    constexpr bool kPf = GLB && TP_CONISS_GLBPF != 0;
     const int lane = threadIdx.x & 63;
     const bool waveA = __builtin_amdgcn_readfirstlane((int)threadIdx.x) < 64;   // wave-uniform: a scalar branch
     const int nbk = (n + 63) / 64;
@@ -362,6 +386,9 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
     const double *c0 = cost0 + (size_t)ti * cst;
 
     double bmr[BS];
+    // bmi: the leftmost position holding each block's minimum (kept with bmr,
+    // so the speculative argmin reads no block of costs)
+    int bmi[BS];
     auto argmin_pos = [&](double vmin) -> int {
         if (isnan(vmin)) return -1;
         int blk = 0;
@@ -454,11 +481,22 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
         nv = c2 ? cr : nv;
     };
     Mg cur = {0, 0, 0, -1, -1, -1, -1, -1};
+    // GLB: the next merge's three touched cost blocks, loaded one merge ahead
+    double nva = QNAN, nvb = QNAN, nvl = QNAN;
+    auto prefetch_blocks = [&](const Mg &m) {
+        const int ba = m.a >> 6, bb = (m.ea + 1) >> 6, bl = m.ls >= 0 ? (m.ls >> 6) : ba;
+        nva = cost[ba * 64 + lane];
+        nvb = cost[bb * 64 + lane];
+        nvl = cost[bl * 64 + lane];
+    };
     double c = 0.0, pcl = QNAN, pcr = QNAN;
     int pls = DC, pa_ = DC;   // A: where the previous merge's new costs go (applied at the next merge's start)
     if (waveA) {
 #pragma unroll
-        for (int q = 0; q < BS; ++q) bmr[q] = QNAN;
+        for (int q = 0; q < BS; ++q) {
+            bmr[q] = QNAN;
+            bmi[q] = DC;
+        }
         for (int bk = 0; bk < nbk; ++bk) {
             const int p = bk * 64 + lane;
             const double cp = c0[p];
@@ -472,14 +510,20 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
                 rn.set(DL + lane, -1);
             }
             const double m = wave_min(cp);
+            const unsigned long long mm = __ballot(cp == m);
+            const int mpos = mm ? bk * 64 + (int)__builtin_ctzll(mm) : DC;
             if (lane == (bk & 63)) {
 #pragma unroll
                 for (int q = 0; q < BS; ++q)
-                    if (q == (bk >> 6)) bmr[q] = m;
+                    if (q == (bk >> 6)) {
+                        bmr[q] = m;
+                        bmi[q] = mpos;
+                    }
             }
         }
         c = gmin();
         cur = merge_at(argmin_pos(c));
+        if constexpr (kPf) prefetch_blocks(cur);
         const Rec rc = make_rec(cur, 0);
         mb_i[0] = rc.x;
         mb_i[1] = rc.y;
@@ -528,9 +572,25 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
             // refresh the three touched blocks and, concurrently, the minimum of
             // the untouched ones: four interleaved wave reductions
             const int ba = a >> 6, bb = b >> 6, bl = ls >= 0 ? (ls >> 6) : ba;
-            const double va = cost[ba * 64 + lane];
-            const double vb = cost[bb * 64 + lane];
-            const double vl = cost[bl * 64 + lane];
+            double va, vb, vl;
+            if constexpr (kPf) {
+                // the three blocks were loaded after the previous merge's choice
+                // (still in flight across barrier Y: LDS-only barriers); patch
+                // the positions this merge's writes above changed
+                auto patch = [&](double v, int blk) {
+                    const int p = blk * 64 + lane;
+                    v = p == pls ? pcl : v;
+                    v = p == pa_ ? pcr : v;
+                    return (p == b || p == a || (ls >= 0 && p == ls)) ? QNAN : v;
+                };
+                va = patch(nva, ba);
+                vb = patch(nvb, bb);
+                vl = patch(nvl, bl);
+            } else {
+                va = cost[ba * 64 + lane];
+                vb = cost[bb * 64 + lane];
+                vl = cost[bl * 64 + lane];
+            }
             double rest = QNAN;
 #pragma unroll
             for (int q = 0; q < BS; ++q) {
@@ -540,23 +600,55 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
             TP_STAMP(6);
             double ma = va, mb = vb, ml = vl, mr = rest;
             wave_min4(ma, mb, ml, mr);
+            int a2 = -1;
+            double v2;
+            if constexpr (kBmi) {
+                // the refreshed blocks' leftmost minimum positions (NaN block: none)
+                const unsigned long long xa = __ballot(va == ma), xb = __ballot(vb == mb), xl = __ballot(vl == ml);
+                const int pma = xa ? ba * 64 + (int)__builtin_ctzll(xa) : DC;
+                const int pmb = xb ? bb * 64 + (int)__builtin_ctzll(xb) : DC;
+                const int pml = xl ? bl * 64 + (int)__builtin_ctzll(xl) : DC;
 #pragma unroll
-            for (int q = 0; q < BS; ++q) {
-                bmr[q] = (lane == (ba & 63) && q == (ba >> 6)) ? ma : bmr[q];
-                bmr[q] = (lane == (bb & 63) && q == (bb >> 6)) ? mb : bmr[q];
-                bmr[q] = (lane == (bl & 63) && q == (bl >> 6)) ? ml : bmr[q];
-            }
-            const double v2 = vmin(vmin(mr, ma), vmin(mb, ml));
-            // leftmost position holding v2: its block from the block minima, then
-            // the block's words (v2 NaN: no ballot matches, a2 = -1)
-            int blk = 0;
+                for (int q = 0; q < BS; ++q) {
+                    const bool ia = lane == (ba & 63) && q == (ba >> 6);
+                    const bool ib = lane == (bb & 63) && q == (bb >> 6);
+                    const bool il = lane == (bl & 63) && q == (bl >> 6);
+                    bmr[q] = ia ? ma : bmr[q];
+                    bmi[q] = ia ? pma : bmi[q];
+                    bmr[q] = ib ? mb : bmr[q];
+                    bmi[q] = ib ? pmb : bmi[q];
+                    bmr[q] = il ? ml : bmr[q];
+                    bmi[q] = il ? pml : bmi[q];
+                }
+                v2 = vmin(vmin(mr, ma), vmin(mb, ml));
+                // leftmost position holding v2: the lowest block whose minimum is
+                // v2, then that block's leftmost minimum position, kept in bmi (v2
+                // NaN: no ballot matches, a2 = -1)
 #pragma unroll
-            for (int q = BS - 1; q >= 0; --q) {
-                const unsigned long long m = __ballot(bmr[q] == v2);
-                blk = m ? 64 * q + (int)__builtin_ctzll(m) : blk;
+                for (int q = BS - 1; q >= 0; --q) {
+                    const unsigned long long m = __ballot(bmr[q] == v2);
+                    const int pq = __builtin_amdgcn_readlane(bmi[q], m ? (int)__builtin_ctzll(m) : 0);
+                    a2 = m ? pq : a2;
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < BS; ++q) {
+                    bmr[q] = (lane == (ba & 63) && q == (ba >> 6)) ? ma : bmr[q];
+                    bmr[q] = (lane == (bb & 63) && q == (bb >> 6)) ? mb : bmr[q];
+                    bmr[q] = (lane == (bl & 63) && q == (bl >> 6)) ? ml : bmr[q];
+                }
+                v2 = vmin(vmin(mr, ma), vmin(mb, ml));
+                // leftmost position holding v2: its block from the block minima,
+                // then the block's words (v2 NaN: no ballot matches, a2 = -1)
+                int blk = 0;
+#pragma unroll
+                for (int q = BS - 1; q >= 0; --q) {
+                    const unsigned long long m = __ballot(bmr[q] == v2);
+                    blk = m ? 64 * q + (int)__builtin_ctzll(m) : blk;
+                }
+                const unsigned long long mv = __ballot(cost[blk * 64 + lane] == v2);
+                a2 = mv ? blk * 64 + (int)__builtin_ctzll(mv) : -1;
             }
-            const unsigned long long mv = __ballot(cost[blk * 64 + lane] == v2);
-            const int a2 = mv ? blk * 64 + (int)__builtin_ctzll(mv) : -1;
             TP_STAMP(7);
             // ---- the three possible next merges (post-update links); a2's
             //      clusters go to B at once (its row prefetch starts before X)
@@ -582,7 +674,7 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
             m2.ll = cur.ll;
             m2.rre = m2rrev;
             TP_STAMP(0);
-            __syncthreads();   // X
+            coniss_bar();   // X (LDS-only by default: global loads stay in flight)
             TP_STAMP(1);
             // ---- the choice
             const double cl = mb_d[0], cr = mb_d[1];
@@ -600,6 +692,7 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
             cur.ll = sel(m0.ll, m1.ll, m2.ll);
             cur.rre = sel(m0.rre, m1.rre, m2.rre);
             c = nv;
+            if constexpr (kPf) prefetch_blocks(cur);
             {
                 const Rec rc = make_rec(cur, c2 ? 2 : (c1 ? 1 : 0));
                 mb_i[0] = rc.x;
@@ -609,19 +702,38 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
             }
             // block minima absorb the new costs now (the LDS words follow at the
             // next merge's start, before its refresh reads them)
+            if constexpr (kBmi) {
 #pragma unroll
-            for (int q = 0; q < BS; ++q) {
-                const double tr = vmin(bmr[q], cr);
-                bmr[q] = (lane == (ba & 63) && q == (ba >> 6)) ? tr : bmr[q];
-                const double tl = vmin(bmr[q], cl);
-                bmr[q] = (ls >= 0 && lane == (bl & 63) && q == (bl >> 6)) ? tl : bmr[q];
+                for (int q = 0; q < BS; ++q) {
+                    // (value, position) lexicographic minimum: the block keeps its
+                    // leftmost minimum position (a NaN cost -- no right neighbour
+                    // -- changes nothing; a NaN block minimum takes the new cost)
+                    const bool ia = lane == (ba & 63) && q == (ba >> 6);
+                    const bool tr =
+                        ia && ((cr < bmr[q]) || (cr == bmr[q] && a < bmi[q]) || (bmr[q] != bmr[q] && cr == cr));
+                    bmr[q] = tr ? cr : bmr[q];
+                    bmi[q] = tr ? a : bmi[q];
+                    const bool il = ls >= 0 && lane == (bl & 63) && q == (bl >> 6);
+                    const bool tl =
+                        il && ((cl < bmr[q]) || (cl == bmr[q] && ls < bmi[q]) || (bmr[q] != bmr[q] && cl == cl));
+                    bmr[q] = tl ? cl : bmr[q];
+                    bmi[q] = tl ? ls : bmi[q];
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < BS; ++q) {
+                    const double tr = vmin(bmr[q], cr);
+                    bmr[q] = (lane == (ba & 63) && q == (ba >> 6)) ? tr : bmr[q];
+                    const double tl = vmin(bmr[q], cl);
+                    bmr[q] = (ls >= 0 && lane == (bl & 63) && q == (bl >> 6)) ? tl : bmr[q];
+                }
             }
             pcl = cl;
             pcr = cr;
             pls = ls >= 0 ? ls : DC;
             pa_ = a;
             TP_STAMP(2);
-            __syncthreads();   // Y
+            coniss_bar();   // Y
             TP_STAMP(3);
         } else {
             // ---- this merge's rows from the previous merge's prefetch
@@ -695,7 +807,7 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
             mcost[s] = cc;
             height[s] = h;
             TP_STAMP(2);
-            __syncthreads();   // X
+            coniss_bar();   // X (LDS-only by default: global loads stay in flight)
             TP_STAMP(3);
             // ---- prefetch a2's rows for the next merge
             const int4 p0 = mb_i[3];
@@ -707,7 +819,7 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
             r2p = p0.w;
             aprev = a_;
             TP_STAMP(6);
-            __syncthreads();   // Y
+            coniss_bar();   // Y
             TP_STAMP(7);
         }
     }
@@ -762,7 +874,21 @@ __global__ void __launch_bounds__(128) k_coniss_t(SweepDev sd, double *cost0) {
                     case 5: coniss_tree2<STAMPS, 5, BS, GLB, LU>(sd, cost0, lds, mb_d, mb_i); break;
                     case 6: coniss_tree2<STAMPS, 6, BS, GLB, LU>(sd, cost0, lds, mb_d, mb_i); break;
                     case 7: coniss_tree2<STAMPS, 7, BS, GLB, LU>(sd, cost0, lds, mb_d, mb_i); break;
-                    default: coniss_tree2<STAMPS, 8, BS, GLB, LU>(sd, cost0, lds, mb_d, mb_i); break;
+                    case 8: coniss_tree2<STAMPS, 8, BS, GLB, LU>(sd, cost0, lds, mb_d, mb_i); break;
+                    default:
+                        if constexpr (KS > 8) {
+                            switch ((i + 63) / 64) {
+                                case 9: coniss_tree2<STAMPS, 9, BS, GLB, LU>(sd, cost0, lds, mb_d, mb_i); break;
+                                case 10: coniss_tree2<STAMPS, 10, BS, GLB, LU>(sd, cost0, lds, mb_d, mb_i); break;
+                                case 11: coniss_tree2<STAMPS, 11, BS, GLB, LU>(sd, cost0, lds, mb_d, mb_i); break;
+                                case 12: coniss_tree2<STAMPS, 12, BS, GLB, LU>(sd, cost0, lds, mb_d, mb_i); break;
+                                case 13: coniss_tree2<STAMPS, 13, BS, GLB, LU>(sd, cost0, lds, mb_d, mb_i); break;
+                                case 14: coniss_tree2<STAMPS, 14, BS, GLB, LU>(sd, cost0, lds, mb_d, mb_i); break;
+                                case 15: coniss_tree2<STAMPS, 15, BS, GLB, LU>(sd, cost0, lds, mb_d, mb_i); break;
+                                default: coniss_tree2<STAMPS, 16, BS, GLB, LU>(sd, cost0, lds, mb_d, mb_i); break;
+                            }
+                        }
+                        break;
                 }
             }
             break;
@@ -792,6 +918,16 @@ template __global__ void k_coniss_t<false, 11, true, true, 8>(SweepDev, double *
 template __global__ void k_coniss_t<false, 11, true, false, 8>(SweepDev, double *);
 template __global__ void k_coniss_t<false, 16, true, false, 8>(SweepDev, double *);
 template __global__ void k_coniss_t<false, 32, true, false, 8>(SweepDev, double *);
+// k in 513..1024: trees of up to 16 slots
+template __global__ void k_coniss_t<false, 1, false, false, 16>(SweepDev, double *);
+template __global__ void k_coniss_t<false, 2, false, false, 16>(SweepDev, double *);
+template __global__ void k_coniss_t<false, 3, false, false, 16>(SweepDev, double *);
+template __global__ void k_coniss_t<false, 6, true, true, 16>(SweepDev, double *);
+template __global__ void k_coniss_t<false, 8, true, true, 16>(SweepDev, double *);
+template __global__ void k_coniss_t<false, 11, true, true, 16>(SweepDev, double *);
+template __global__ void k_coniss_t<false, 11, true, false, 16>(SweepDev, double *);
+template __global__ void k_coniss_t<false, 16, true, false, 16>(SweepDev, double *);
+template __global__ void k_coniss_t<false, 32, true, false, 16>(SweepDev, double *);
 
 // ------------------------------------------------------------ CH over cuts
 // canonical segment statistics of rows s..e, by one wave (see tpo_seg_ss)
@@ -1304,8 +1440,10 @@ size_t ch_glb_slot_doubles(int nc, int k) { return (size_t)nc * (k + 1) + (size_
 void launch_ch_glb(const SweepDev &sd, const int *d_slot_of, double *scratch, size_t slot_doubles, hipStream_t s) {
     if (ks_for(sd.k) == 4)
         hipLaunchKernelGGL(k_ch_glb<4>, dim3(sd.ntrees), dim3(256), 0, s, sd, d_slot_of, scratch, slot_doubles);
-    else
+    else if (ks_for(sd.k) == 8)
         hipLaunchKernelGGL(k_ch_glb<8>, dim3(sd.ntrees), dim3(256), 0, s, sd, d_slot_of, scratch, slot_doubles);
+    else
+        hipLaunchKernelGGL(k_ch_glb<16>, dim3(sd.ntrees), dim3(256), 0, s, sd, d_slot_of, scratch, slot_doubles);
     TP_HIP(hipGetLastError());
 }
 
@@ -1325,6 +1463,15 @@ static bool coniss_in_lds(int n) { return coniss_lds_bytes(n) <= 160 * 1024 - 25
 // the global-variant link scratch: see sweep_cost0_doubles)
 template <bool STAMPS, int BS, bool GLB, bool LU = false>
 static void launch_coniss_bs(const SweepDev &sd, double *cost0, size_t lds, hipStream_t s) {
+    if (sd.tree0 + sd.ntrees > 512) {   // trees of 9..16 column slots
+        if constexpr (!STAMPS) {
+            TP_HIP(hipFuncSetAttribute((const void *)k_coniss_t<false, BS, GLB, LU, 16>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            hipLaunchKernelGGL((k_coniss_t<false, BS, GLB, LU, 16>), dim3(sd.ntrees), dim3(128), lds, s, sd, cost0);
+            return;
+        }
+        fail(TP_ERR_UNSUPPORTED, "stamped CONISS: at most 256 columns");
+    }
     if (sd.tree0 + sd.ntrees > 256) {   // trees of 5..8 column slots
         if constexpr (!STAMPS) {
             TP_HIP(hipFuncSetAttribute((const void *)k_coniss_t<false, BS, GLB, LU, 8>,
@@ -1364,8 +1511,10 @@ static void run_coniss(const SweepDev &sd_in, hipStream_t s, bool stamped, Ctx *
     }
     if (ks == 4)
         hipLaunchKernelGGL(k_seed<4>, dim3(sd.ntrees, nbk), dim3(64), 0, s, sd, cost0);
-    else
+    else if (ks == 8)
         hipLaunchKernelGGL(k_seed<8>, dim3(sd.ntrees, nbk), dim3(64), 0, s, sd, cost0);
+    else
+        hipLaunchKernelGGL(k_seed<16>, dim3(sd.ntrees, nbk), dim3(64), 0, s, sd, cost0);
     TP_HIP(hipGetLastError());
     const bool in_lds = coniss_in_lds(sd.n);
     // global variant: 16-bit links in LDS when they fit (costs stay global)
@@ -1401,8 +1550,8 @@ static void run_coniss(const SweepDev &sd_in, hipStream_t s, bool stamped, Ctx *
 
 void launch_sweep(const SweepDev &sd, hipStream_t s, Ctx *prof) {
     if (sd.k > 64 * KS_MAX)
-        fail(TP_ERR_UNSUPPORTED, "min(max_pcs, n_good) > 512: this build's sweep kernels hold at most 512 PC columns "
-                                 "per lane group (R accepts any max_pcs, R/TADpole.R:344,452)");
+        fail(TP_ERR_UNSUPPORTED, "min(max_pcs, n_good) > 1024: this build's sweep kernels hold at most 1024 PC "
+                                 "columns per lane group (R accepts any max_pcs, R/TADpole.R:344,452)");
     const int ks = ks_for(sd.k);
     if (sd.n < 3) fail(TP_ERR_NO_BSTICK, "fewer than 3 good bins: no broken-stick level");
     if (sd.n > kConissMaxN) fail(TP_ERR_UNSUPPORTED, "more than 131072 bins per matrix");
@@ -1417,7 +1566,8 @@ void launch_sweep(const SweepDev &sd, hipStream_t s, Ctx *prof) {
     TP_HIP(hipGetLastError());
     hipStream_t ts = prof ? side_fork(*prof) : s;
     if (ks == 4) hipLaunchKernelGGL(k_trS<4>, dim3(1), dim3(256), 0, ts, sd.Pt, sd.n, sd.ldp, sd.k, sd.trS);
-    else hipLaunchKernelGGL(k_trS<8>, dim3(1), dim3(512), 0, ts, sd.Pt, sd.n, sd.ldp, sd.k, sd.trS);
+    else if (ks == 8) hipLaunchKernelGGL(k_trS<8>, dim3(1), dim3(512), 0, ts, sd.Pt, sd.n, sd.ldp, sd.k, sd.trS);
+    else hipLaunchKernelGGL(k_trS<16>, dim3(1), dim3(1024), 0, ts, sd.Pt, sd.n, sd.ldp, sd.k, sd.trS);
     TP_HIP(hipGetLastError());
     run_coniss(sd, s, false, prof);
     if (prof) side_join(*prof);
@@ -1431,14 +1581,17 @@ void launch_sweep(const SweepDev &sd, hipStream_t s, Ctx *prof) {
         trace_mark(s, "ch_cut");
         const int g = std::max(1, std::min(256, (sd.ucap + 3) / 4));
         if (ks == 4) hipLaunchKernelGGL(k_ch_segstat<4>, dim3(g), dim3(256), 0, s, sd);
-        else hipLaunchKernelGGL(k_ch_segstat<8>, dim3(g), dim3(256), 0, s, sd);
+        else if (ks == 8) hipLaunchKernelGGL(k_ch_segstat<8>, dim3(g), dim3(256), 0, s, sd);
+        else hipLaunchKernelGGL(k_ch_segstat<16>, dim3(g), dim3(256), 0, s, sd);
         TP_HIP(hipGetLastError());
         trace_mark(s, "ch_segstat");
         if (ks == 4) hipLaunchKernelGGL(k_ch<4>, dim3(sd.ntrees), dim3(256), 0, s, sd);
-        else hipLaunchKernelGGL(k_ch<8>, dim3(sd.ntrees), dim3(256), 0, s, sd);
+        else if (ks == 8) hipLaunchKernelGGL(k_ch<8>, dim3(sd.ntrees), dim3(256), 0, s, sd);
+        else hipLaunchKernelGGL(k_ch<16>, dim3(sd.ntrees), dim3(256), 0, s, sd);
     } else {
         if (ks == 4) hipLaunchKernelGGL(k_ch<4>, dim3(sd.ntrees), dim3(CH_THREADS), 0, s, sd);
-        else hipLaunchKernelGGL(k_ch<8>, dim3(sd.ntrees), dim3(CH_THREADS), 0, s, sd);
+        else if (ks == 8) hipLaunchKernelGGL(k_ch<8>, dim3(sd.ntrees), dim3(CH_THREADS), 0, s, sd);
+        else hipLaunchKernelGGL(k_ch<16>, dim3(sd.ntrees), dim3(CH_THREADS), 0, s, sd);
     }
     TP_HIP(hipGetLastError());
     trace_mark(s, "ch");
@@ -1448,7 +1601,7 @@ void launch_sweep(const SweepDev &sd, hipStream_t s, Ctx *prof) {
 void launch_coniss_stamped(const SweepDev &sd, hipStream_t s) { run_coniss(sd, s, true, nullptr); }
 
 void launch_coniss_only(const SweepDev &sd, hipStream_t s) {
-    if (sd.tree0 + sd.ntrees > 64 * KS_MAX) fail(TP_ERR_UNSUPPORTED, "more than 512 columns");
+    if (sd.tree0 + sd.ntrees > 64 * KS_MAX) fail(TP_ERR_UNSUPPORTED, "more than 1024 columns");
     if (sd.n > kConissMaxN) fail(TP_ERR_UNSUPPORTED, "more than 131072 bins per matrix");
     run_coniss(sd, s, false, nullptr);
 }
@@ -1476,12 +1629,15 @@ __global__ void __launch_bounds__(256) k_ch_single(const double *Pt, int n, int 
 
 void launch_ch_only(const double *d_Pt, int n, int ldp, int k, const int *d_bnd, int cn, double *d_seg,
                     double *d_out, hipStream_t s) {
-    if (k > 64 * KS_MAX) fail(TP_ERR_UNSUPPORTED, "calinhara: more than 512 columns");
+    if (k > 64 * KS_MAX) fail(TP_ERR_UNSUPPORTED, "calinhara: more than 1024 columns");
     if (k <= 256)
         hipLaunchKernelGGL(k_ch_single<4>, dim3(1), dim3(256), 0, s, d_Pt, n, ldp, k, d_bnd, cn, d_seg,
                            d_seg + cn + 1, d_out);
-    else
+    else if (k <= 512)
         hipLaunchKernelGGL(k_ch_single<8>, dim3(1), dim3(256), 0, s, d_Pt, n, ldp, k, d_bnd, cn, d_seg,
+                           d_seg + cn + 1, d_out);
+    else
+        hipLaunchKernelGGL(k_ch_single<16>, dim3(1), dim3(256), 0, s, d_Pt, n, ldp, k, d_bnd, cn, d_seg,
                            d_seg + cn + 1, d_out);
     TP_HIP(hipGetLastError());
 }

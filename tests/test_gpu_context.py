@@ -131,3 +131,46 @@ def test_run_genome_reuses_stream_contexts(gpu):
     assert live1 == live0
     for c in mats:
         assert _same(a[c], b[c]), c
+
+
+def test_progress_word_reports_stages(gpu):
+    """tp_progress_attach: a host word the pipeline on that stream's context
+    advances 0 -> 1 (mask read back) -> 2 (correlation queued) -> 3 (PCA done)
+    -> 4 (returned), polled from another thread while the call runs (what the
+    concurrent centromere arms use to start the q arm under the p arm's sweep)."""
+    import ctypes
+    import time
+    import torch
+    from tadpole_amd import _lib
+    m = synth_hic(2500, 66)
+    s = torch.cuda.Stream()
+    L = _lib.load()
+    prog = np.full(1, -1, np.int32)
+    st = ctypes.c_int(0)
+    L.tp_progress_attach(ctypes.byref(ctypes.c_int(0)), ctypes.c_void_p(s.cuda_stream),
+                         prog.ctypes.data_as(ctypes.c_void_p), ctypes.byref(st))
+    _lib.check(st)
+    seen, done = [], [False]
+
+    def run():
+        try:
+            import tadpole_amd as tp
+            tp.TADpole(m, max_pcs=100, stream=s)
+        finally:
+            done[0] = True
+
+    th = threading.Thread(target=run)
+    th.start()
+    while not done[0]:
+        v = int(prog[0])
+        if not seen or seen[-1] != v:
+            seen.append(v)
+        time.sleep(5e-5)
+    th.join()
+    seen.append(int(prog[0]))
+    L.tp_progress_attach(ctypes.byref(ctypes.c_int(0)), ctypes.c_void_p(s.cuda_stream), None, ctypes.byref(st))
+    _lib.check(st)
+    vals = [v for v in seen if v >= 0]
+    assert vals == sorted(vals) and vals[-1] == 4 and 3 in vals, seen
+    import tadpole_amd as tp
+    tp.release_stream(s)

@@ -1,9 +1,9 @@
 """R-legal inputs past the round-2 build's limits (R accepts any max_pcs,
 R/TADpole.R:344,452; the CH loop at :117-120 has no level limit):
 
-* k = min(max_pcs, N) up to 512 in the sweep kernels (column-slot templates),
-  with the PCA's Rayleigh-Ritz block up to 640 on the library's own
-  eigensolver (rocSOLVER never enters the pipeline);
+* k = min(max_pcs, N) up to 1024 in the sweep kernels (column-slot templates
+  of 4, 8 and 16 slots), with the PCA's Rayleigh-Ritz block up to 1280 on the
+  library's own eigensolver and CholQR (the library links no rocSOLVER);
 * more than 1024 significant broken-stick levels (k_ch_glb, the global-memory
   CH kernel for cuts past k_ch's LDS capacity);
 * more than 65 536 bins in CONISS (32 block-minimum slots).
@@ -56,11 +56,11 @@ def hier_pcs(levels, k, seed=1):
     return p
 
 
-@pytest.mark.parametrize("k", [300, 400, 512])
+@pytest.mark.parametrize("k", [300, 400, 512, 600, 1024])
 def test_sweep_k_above_256_bit_exact(gpu, k):
-    """Trees of 5..8 column slots (the KS = 8 instances of CONISS, k_seed,
-    k_trS, the CH kernels) against the oracle, bit for bit."""
-    p = _segment_pcs(900, k, 40 + k)
+    """Trees of 5..8 and 9..16 column slots (the KS = 8 / 16 instances of
+    CONISS, k_seed, k_trS, the CH kernels) against the oracle, bit for bit."""
+    p = _segment_pcs(max(900, k + 100), k, 40 + k)
     got = G.sweep_dev(p)
     ref = O.sweep(p)
     _same_sweep(got, ref)
@@ -117,10 +117,13 @@ def _check_pipeline(got, ref):
     assert np.max(np.abs(a[fin] - b[fin]) / np.abs(b[fin])) < 1e-6
 
 
-@pytest.mark.parametrize("max_pcs", [300, 480])
+@pytest.mark.parametrize("max_pcs", [300, 480, 600])
 def test_pipeline_max_pcs_above_256(gpu, max_pcs):
-    """TADpole(max_pcs = 300 / 480) end to end against the oracle (LAPACK SVD):
-    Rayleigh-Ritz blocks of 384 / 608 on the library's eigensolver."""
+    """TADpole(max_pcs = 300 / 480 / 600) end to end against the oracle
+    (LAPACK SVD): Rayleigh-Ritz blocks of 384 / 608 / 768 on the library's
+    eigensolver (768: the b > 640 kernels -- k_sytrd_l<20>, one-vector
+    k_invit, the chunked k_trsm_ru_big); R accepts any max_pcs
+    (R/TADpole.R:344,452)."""
     import tadpole_amd as tp
     m = synth_hic(1400, 900 + max_pcs)
     got = tp.TADpole(m, max_pcs=max_pcs)
@@ -138,3 +141,13 @@ def test_pipeline_krylov_max_pcs_300(gpu):
     assert got.timings_ms[13] <= 1e-11
     ref = O.tadpole(m, max_pcs=300, nthreads=16, pca="eigh")
     _check_pipeline(got, ref)
+
+
+def test_sweep_k_above_1024_unsupported(gpu):
+    """k > 1024 is refused with TP_ERR_UNSUPPORTED (a clear error, not a
+    silent truncation)."""
+    from tadpole_amd._lib import TadpoleError, TP_ERR_UNSUPPORTED
+    p = _segment_pcs(1200, 1030, 3)
+    with pytest.raises(TadpoleError) as e:
+        G.sweep_dev(p)
+    assert e.value.status == TP_ERR_UNSUPPORTED

@@ -137,7 +137,8 @@ def _spectrum(kind, b, rng):
 @pytest.mark.parametrize("b,kind", [(1, "graded"), (2, "indefinite"), (3, "graded"), (5, "clustered"),
                                     (64, "graded"), (200, "rankdef"), (256, "graded"), (256, "clustered"),
                                     (16, "graded"), (240, "clustered"), (208, "rankdef"),
-                                    (300, "graded"), (512, "graded")])
+                                    (300, "graded"), (512, "graded"), (640, "clustered"),
+                                    (768, "graded"), (1000, "rankdef"), (1280, "clustered")])
 def test_eigsym(gpu, b, kind):
     rng = np.random.default_rng(b * 7 + len(kind))
     ev = _spectrum(kind, b, rng)

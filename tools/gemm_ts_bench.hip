@@ -407,29 +407,30 @@ __global__ void __launch_bounds__(256, 2) k_v3(int M, int N, int K, const double
 // ---- V5: parametrised: TM rows per workgroup (4 waves of TM/4 rows x 64
 // columns), BK-deep stages, NBUF LDS buffers (1: register prefetch, two
 // barriers a stage), OCC workgroups a CU (launch bounds)
-template <int TM, int BK, int NBUF, int OCC>
+template <int TM, int BK, int NBUF, int OCC, int TN = TSN>
 __global__ void __launch_bounds__(256, OCC) k_v5(int M, int N, int K, const double *__restrict__ A, int lda,
                                                  const double *__restrict__ B, int ldb, double *__restrict__ C,
                                                  int ldc, int kchunk, size_t part_stride) {
     constexpr int LD = BK + 2;
     constexpr int WA = TM / 64;   // 16-row accumulator tiles per wave
+    constexpr int NBF = TN / 16;
     __shared__ double As[NBUF][TM][LD];
-    __shared__ double Bs[NBUF][TSN][LD];
-    const int tm = (M + TM - 1) / TM, tn = (N + TSN - 1) / TSN;
+    __shared__ double Bs[NBUF][TN][LD];
+    const int tm = (M + TM - 1) / TM, tn = (N + TN - 1) / TN;
     const int Lg = xcd_order((int)gridDim.x);
     const int bn = Lg % tn, bm = (Lg / tn) % tm, z = Lg / (tn * tm);
-    const int i0 = bm * TM, j0 = bn * TSN;
+    const int i0 = bm * TM, j0 = bn * TN;
     const int kbeg = z * kchunk, kend = min(K, kbeg + kchunk);
     C += part_stride * z;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int wm = (TM / 4) * w;
     const int fr = lane & 15, fk = lane >> 4;
-    d4 acc[WA][4];
+    d4 acc[WA][NBF];
 #pragma unroll
     for (int a = 0; a < WA; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) acc[a][b] = (d4){0.0, 0.0, 0.0, 0.0};
-    constexpr int PA = TM * BK / 256, PB = TSN * BK / 256;
+        for (int b = 0; b < NBF; ++b) acc[a][b] = (d4){0.0, 0.0, 0.0, 0.0};
+    constexpr int PA = TM * BK / 256, PB = TN * BK / 256;
     double ra[PA], rb[PB];
     const int lk = t % BK, lr = t / BK;
     constexpr int RS = 256 / BK;
@@ -464,15 +465,15 @@ __global__ void __launch_bounds__(256, OCC) k_v5(int M, int N, int K, const doub
         if (more) load(k0 + BK);
 #pragma unroll
         for (int kk = 0; kk < BK; kk += 4) {
-            double af[WA], bf[4];
+            double af[WA], bf[NBF];
 #pragma unroll
             for (int a = 0; a < WA; ++a) af[a] = As[buf][wm + 16 * a + fr][kk + fk];
 #pragma unroll
-            for (int b = 0; b < 4; ++b) bf[b] = Bs[buf][16 * b + fr][kk + fk];
+            for (int b = 0; b < NBF; ++b) bf[b] = Bs[buf][16 * b + fr][kk + fk];
 #pragma unroll
             for (int a = 0; a < WA; ++a)
 #pragma unroll
-                for (int b = 0; b < 4; ++b)
+                for (int b = 0; b < NBF; ++b)
                     acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[a], bf[b], acc[a][b], 0, 0, 0);
         }
         if (NBUF == 1) __syncthreads();
@@ -483,7 +484,7 @@ __global__ void __launch_bounds__(256, OCC) k_v5(int M, int N, int K, const doub
 #pragma unroll
     for (int a = 0; a < WA; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b)
+        for (int b = 0; b < NBF; ++b)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int i = i0 + wm + 16 * a + fk + 4 * r;
@@ -504,7 +505,7 @@ __global__ void k_rand(double *p, size_t n, unsigned long long seed) {
 
 int main(int argc, char **argv) {
     const int n = argc > 1 ? atoi(argv[1]) : 7729;
-    const int N = 64, M = n + 2, K = n;
+    const int N = argc > 2 ? atoi(argv[2]) : 64, M = n + 2, K = n;
     const int reps = 20;
     double *A, *B, *P0, *P1;
     CK(hipMalloc(&A, (size_t)M * K * 8));
@@ -537,20 +538,21 @@ int main(int argc, char **argv) {
         fflush(stdout);
     };
     printf("M=%d N=%d K=%d\n", M, N, K);
-    run("v0 k_gemm_ts BK16", k_v0<16>, 128, 8, P0);
-    run("v0 k_gemm_ts BK16", k_v0<16>, 128, 16, P0);
-    run("v5 TM128 BK16 NBUF1 OCC3", k_v5<128, 16, 1, 3>, 128, 8, P1);
-    run("v5 TM128 BK16 NBUF1 OCC3", k_v5<128, 16, 1, 3>, 128, 16, P1);
-    run("v5 TM128 BK16 NBUF1 OCC4", k_v5<128, 16, 1, 4>, 128, 16, P1);
-    run("v5 TM128 BK8 NBUF2 OCC4", k_v5<128, 8, 2, 4>, 128, 16, P1);
-    run("v5 TM128 BK8 NBUF2 OCC3", k_v5<128, 8, 2, 3>, 128, 16, P1);
-    run("v5 TM64 BK16 NBUF2 OCC4", k_v5<64, 16, 2, 4>, 64, 8, P1);
-    run("v5 TM64 BK16 NBUF2 OCC4", k_v5<64, 16, 2, 4>, 64, 16, P1);
-    run("v5 TM128 BK16 NBUF2 OCC2", k_v5<128, 16, 2, 2>, 128, 8, P1);
-    run("v5 TM128 BK32 NBUF1 OCC2", k_v5<128, 32, 1, 2>, 128, 8, P1);
-    run("v5 TM128 BK32 NBUF1 OCC3", k_v5<128, 32, 1, 3>, 128, 16, P1);
-    run("v5 TM256 BK16 NBUF1 OCC2", k_v5<256, 16, 1, 2>, 256, 16, P1);
-    run("v5 TM256 BK8 NBUF2 OCC2", k_v5<256, 8, 2, 2>, 256, 16, P1);
-    run("v0 k_gemm_ts BK16 (again)", k_v0<16>, 128, 8, P0);
+    if (N == 64) {
+        run("v0 k_gemm_ts BK16", k_v0<16>, 128, 8, P0);
+        run("v5 TM128 BK16 NBUF2 OCC2", k_v5<128, 16, 2, 2>, 128, 8, P1);
+        run("v5 TM128 BK32 NBUF1 OCC2", k_v5<128, 32, 1, 2>, 128, 8, P1);
+        run("v5 TM64 BK16 NBUF2 OCC4", k_v5<64, 16, 2, 4>, 64, 8, P1);
+        run("v0 k_gemm_ts BK16 (again)", k_v0<16>, 128, 8, P0);
+    } else {
+        run("v5 TM128 TN32 BK16 NBUF2 OCC2 (lib)", k_v5<128, 16, 2, 2, 32>, 128, 8, P0);
+        run("v5 TM128 TN32 BK16 NBUF2 OCC3", k_v5<128, 16, 2, 3, 32>, 128, 8, P1);
+        run("v5 TM256 TN32 BK16 NBUF2 OCC2", k_v5<256, 16, 2, 2, 32>, 256, 8, P1);
+        run("v5 TM256 TN32 BK16 NBUF2 OCC2", k_v5<256, 16, 2, 2, 32>, 256, 16, P1);
+        run("v5 TM256 TN32 BK8 NBUF2 OCC2", k_v5<256, 8, 2, 2, 32>, 256, 16, P1);
+        run("v5 TM256 TN32 BK32 NBUF1 OCC2", k_v5<256, 32, 1, 2, 32>, 256, 8, P1);
+        run("v5 TM128 TN32 BK32 NBUF2 OCC2", k_v5<128, 32, 2, 2, 32>, 128, 8, P1);
+        run("v5 TM128 TN32 BK16 NBUF2 OCC2 (lib, again)", k_v5<128, 16, 2, 2, 32>, 128, 8, P0);
+    }
     return 0;
 }
