@@ -1522,7 +1522,9 @@ void tp_debug_sytrd2(const double *H, const int *b, const int *which, double *ms
 
 extern "C" {
 /* S = X'X (n x n, column-major in and out) by mode 0 = fp64 MFMA GEMM, 1 = the
- * int8-exact path (fails with TP_ERR_ARG when X is not non-negative integer
+ * int8-exact path with 64-column tiles, 2 = the 128-column tile kernels of the
+ * pipeline (knob 32 picks the LDS-DMA or the register-staged one; counts below
+ * 16384) (fails with TP_ERR_ARG when X is not non-negative integer
  * counts below 2^21); *slices = slices used (0 for fp64); ms = mean of 3. */
 void tp_debug_xtx(const double *X, const int *n, const int *mode, double *S, int *slices, double *ms,
                   int *status) {
@@ -1534,9 +1536,10 @@ void tp_debug_xtx(const double *X, const int *n, const int *mode, double *S, int
         double *dS = c.buf[S_S].as<double>((size_t)N * N);
         TP_HIP(hipMemcpyAsync(dX, X, (size_t)N * N * 8, hipMemcpyHostToDevice, s));
         int ns = 0;
-        if (*mode == 1) {
+        if (*mode >= 1) {
             ns = xtx_int_slices(c, dX, N);
             if (ns == 0) fail(TP_ERR_ARG, "X is not non-negative integer counts < 2^21");
+            if (*mode == 2 && ns > 2) fail(TP_ERR_ARG, "128-tile kernels: counts < 16384");
         }
         hipEvent_t e0, e1;
         TP_HIP(hipEventCreate(&e0));
@@ -1546,7 +1549,8 @@ void tp_debug_xtx(const double *X, const int *n, const int *mode, double *S, int
             TP_HIP(hipEventRecord(e0, s));
             if (ns) {
                 const int8_t *sl = xtx_slices(c, dX, N, ns);
-                xtx_int8_tiles(c, sl, N, ns, dS, 0, -1);
+                if (*mode == 2) xtx_int8_tiles128(c, sl, N, ns, dS, 0, -1, nullptr, nullptr);
+                else xtx_int8_tiles(c, sl, N, ns, dS, 0, -1);
             } else {
                 GemmArgs g{N, N, N, dX, N, true, dX, N, dS, N};
                 g.sym_upper = true;
@@ -1616,6 +1620,8 @@ void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
         case 29: p = &g_gram64; break;
         case 30: p = &g_shard_inject; break;
         case 31: p = &g_ckry_min; break;
+        case 32: p = &g_xtx_glds; break;
+        case 33: p = &g_ckry_local; break;
         default: fail(TP_ERR_ARG, "unknown knob");
         }
         if (*which == 3 && *value != 16 && *value != 32) fail(TP_ERR_ARG, "stage depth must be 16 or 32");

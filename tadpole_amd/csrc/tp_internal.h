@@ -197,6 +197,7 @@ extern int g_gram64;
 // Z'Z (64 x 64, ld 64) of an n x 64 block by k_gram64, bit-identical to the
 // symmetric split-K GEMM; false: not applicable (the caller runs gemm_f64)
 bool gram64(const double *Z, int n, int ldz, double *W, DevBuf &work, hipStream_t s);
+extern int g_xtx_glds;        // int8 X'X: LDS-DMA ring kernel (0: register-staged k_xtx_i8_big)
 extern int g_xtx_supertile;   // int8 X'X: XCD-contiguous supertile order of the 128 x 128 tiles (0: columns)
 // row-shardable products that take the 128 x 64 kernel with k chunks fixed by K
 // (tp_gemm.hip); shards and the unsharded call must agree on it
@@ -379,6 +380,7 @@ extern int g_pca_krylov_min, g_pca_krylov_block, g_pca_krylov_steps, g_pca_over;
 extern int g_pca_cheb_fused;   // Krylov small problem: Chebyshev step in the T Y reduction (default 1)
 extern int g_pca_ckrylov;      // 1: block Krylov in C (tp_krylov.hip), 0: in G (tp_pca.hip), -1: C from g_ckry_min
 extern int g_ckry_min;         // bins from which the automatic choice takes the Krylov space of C
+extern int g_ckry_local;   // C-space Krylov: local first orthogonalisation pass (knob 33)
 extern int g_ckry_chunk;       // rows per Z partial of the C-Krylov orthogonalisation
 extern int g_ckry_steps;       // C-Krylov blocks before the first check (0: from k and n)
 // the top k eigenpairs of a D x D projected matrix (tp_pca.hip)

@@ -78,6 +78,7 @@ int g_pca_ckrylov = -1;
 int g_ckry_min = 10000;
 int g_ckry_chunk = 256;       // rows per Z partial of the PIP passes
 int g_ckry_steps = 0;         // blocks s before the first check (0: from k and n)
+int g_ckry_local = 1;         // first BCGS-PIP pass against K_0, K_{t-2}, K_{t-1} only (knob 33)
 
 // One BCGS-PIP pass of block slot `D / KP` (columns D..D+KP-1 of Kb, n x KP):
 // W0 is the block to orthonormalise against Kb's first D columns (W0 may be
@@ -86,24 +87,37 @@ struct PipScratch {
     double *part, *Z, *hh, *Ri, *apart;
     int *info;
 };
+// local >= 4: the pass runs against K_0 and the two blocks before slot `local`
+// only (a local first pass, see krylov_c_topk); the result still lands in
+// slot D / KP = local.
 static void pip_pass(Ctx &c, double *Kb, int n, int D, const double *W0, const PipScratch &ps, double shift,
-                     int lowdin = 0) {
+                     int lowdin = 0, int local = 0) {
     hipStream_t s = c.cur;
+    double *out = Kb + (size_t)D * n;
+    const double *Kt = nullptr;
+    int Dh = -1;
+    if (local >= 4) {
+        Kt = Kb + (size_t)(local - 2) * KP * n;
+        Dh = KP;
+        D = 3 * KP;
+    }
     const int ldz = D + KP;
     const int chunk = std::max(64, g_ckry_chunk);
     const int S = (n + chunk - 1) / chunk;
     const int dt = (ldz + PZ_COLS - 1) / PZ_COLS;
     const size_t pstride = (size_t)ldz * KP;
-    hipLaunchKernelGGL(k_pipz, dim3((unsigned)(dt * S)), dim3(256), 0, s, Kb, D, W0, n, chunk, ps.part, pstride);
+    hipLaunchKernelGGL(k_pipz, dim3((unsigned)(dt * S)), dim3(256), 0, s, Kb, D, W0, n, chunk, ps.part, pstride, Kt,
+                       Dh);
     const int nsl = (ldz + PR - 1) / PR, nh = (D + PR - 1) / PR;
     hipLaunchKernelGGL(k_pipr, dim3((unsigned)nsl), dim3(256), 0, s, ps.part, pstride, S, D, ps.Z, ps.hh);
     hipLaunchKernelGGL(k_pips<3>, dim3(1), dim3(512), 0, s, ps.Z, D, ps.hh, nh, shift, ps.Ri, ps.info, lowdin);
     const int tiles = (n + PA_ROWS - 1) / PA_ROWS;
     if (D > 0)
-        hipLaunchKernelGGL(k_pipa, dim3((unsigned)(tiles * PA_SPLIT)), dim3(256), 0, s, Kb, D, n, ps.Z, ps.apart);
+        hipLaunchKernelGGL(k_pipa, dim3((unsigned)(tiles * PA_SPLIT)), dim3(256), 0, s, Kb, D, n, ps.Z, ps.apart, Kt,
+                           Dh);
     else
         TP_HIP(hipMemsetAsync(ps.apart, 0, (size_t)tiles * PA_SPLIT * PA_ROWS * KP * 8, s));
-    hipLaunchKernelGGL(k_pipc, dim3((unsigned)tiles), dim3(256), 0, s, ps.apart, ps.Ri, n, W0, Kb + (size_t)D * n);
+    hipLaunchKernelGGL(k_pipc, dim3((unsigned)tiles), dim3(256), 0, s, ps.apart, ps.Ri, n, W0, out);
     TP_HIP(hipGetLastError());
 }
 
@@ -155,7 +169,12 @@ bool krylov_c_topk(Ctx &c, double *C, int c_col0, const double *mext, int n, int
         for (int t = nprod; t <= upto; ++t) {
             if (t >= 1) {
                 const int D = t * KP;
-                pip_pass(c, K, n, D, Pb + (size_t)(t - 1) * np, ps, 1e-14);
+                // Xc K_{t-1} = C K_{t-1} - 1 (m'K_{t-1}) lies in span(K_0, K_{t-2},
+                // K_{t-1}, K_t) in exact arithmetic (C symmetric: the block
+                // Lanczos recurrence; 1 is in span K_0), so the first pass runs
+                // against those blocks only and the second, against every block,
+                // removes the rounding-level rest (knob 33)
+                pip_pass(c, K, n, D, Pb + (size_t)(t - 1) * np, ps, 1e-14, 0, g_ckry_local ? t : 0);
                 pip_pass(c, K, n, D, K + (size_t)D * n, ps, 0.0, 1);   // Gram ~ I + 1e-13: Lowdin
             }
             double *Kt = K + (size_t)t * np, *Pt = Pb + (size_t)t * np;

@@ -16,8 +16,11 @@ constexpr int KP = 32;   // Krylov block width of this path
 // 16-row stages with three stages of register prefetch in flight (the loads
 // are L2 / MALL latency-bound, not bandwidth-bound).
 constexpr int PZ_COLS = 64;
+// Local passes: the first Dh columns come from K, the remaining D - Dh from
+// Kt (Dh < 0: all D from K).
 __global__ void __launch_bounds__(256) k_pipz(const double *__restrict__ K, int D, const double *__restrict__ W, int n,
-                                              int chunk, double *__restrict__ part, size_t pstride) {
+                                              int chunk, double *__restrict__ part, size_t pstride,
+                                              const double *__restrict__ Kt = nullptr, int Dh = -1) {
     __shared__ double As[2][PZ_COLS][18];
     __shared__ double Bs[2][KP][18];
     const int ldz = D + KP;
@@ -28,8 +31,10 @@ __global__ void __launch_bounds__(256) k_pipz(const double *__restrict__ K, int 
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int fr = lane & 15, fk = lane >> 4;
     const int lk = t & 15, lc = t >> 4;   // k row within the stage, column group
+    const int dh = Dh < 0 ? D : Dh;
     auto colp = [&](int col) -> const double * {
-        return col < D ? K + (size_t)col * n : (col < ldz ? W + (size_t)(col - D) * n : nullptr);
+        return col < dh ? K + (size_t)col * n
+                        : (col < D ? Kt + (size_t)(col - dh) * n : (col < ldz ? W + (size_t)(col - D) * n : nullptr));
     };
     const double *pa[4];
 #pragma unroll
@@ -281,8 +286,10 @@ __global__ void __launch_bounds__(512) k_pips(const double *__restrict__ Z, int 
 // staged through LDS in 32-deep chunks, K fragments straight from global
 // memory.  part: [tile][z] 64 x 32 row-major.
 constexpr int PA_ROWS = 64, PA_SPLIT = 4, PA_KC = 32;
+// (Kt, Dh: as k_pipz; Dh a multiple of PA_KC)
 __global__ void __launch_bounds__(256) k_pipa(const double *__restrict__ K, int D, int n, const double *__restrict__ Z,
-                                              double *__restrict__ part) {
+                                              double *__restrict__ part, const double *__restrict__ Kt = nullptr,
+                                              int Dh = -1) {
     __shared__ double Hs[2][KP][PA_KC + 2];
     const int ldz = D + KP;
     const int tile = blockIdx.x / PA_SPLIT, z = blockIdx.x % PA_SPLIT;
@@ -297,6 +304,7 @@ __global__ void __launch_bounds__(256) k_pipa(const double *__restrict__ K, int 
     // H chunk: thread t loads column t >> 3, k (t & 7) * 4 + u
     const int hc = t >> 3, hk = (t & 7) * 4;
     double rh[4], ra[8];
+    const int dh = Dh < 0 ? D : Dh;
     auto load = [&](int ch) {
         const int k0 = ch * PA_KC;
 #pragma unroll
@@ -304,10 +312,11 @@ __global__ void __launch_bounds__(256) k_pipa(const double *__restrict__ K, int 
             const int k = k0 + hk + u;
             rh[u] = k < D ? Z[(size_t)k + (size_t)hc * ldz] : 0.0;
         }
+        const double *Kc = k0 < dh ? K + (size_t)k0 * n : Kt + (size_t)(k0 - dh) * n;   // uniform per chunk
 #pragma unroll
         for (int s2 = 0; s2 < 8; ++s2) {
             const int k = k0 + 4 * s2 + fk;
-            ra[s2] = k < D ? K[(size_t)row + (size_t)k * n] : 0.0;
+            ra[s2] = k < D ? Kc[(size_t)row + (size_t)(4 * s2 + fk) * n] : 0.0;
         }
     };
     auto store = [&](int buf) {

@@ -354,6 +354,232 @@ __global__ void __launch_bounds__(512) k_xtx_i8_big(const int8_t *__restrict__ S
             }
 }
 
+// k_xtx_i8_glds: the same tiles, tile order, waves and exact arithmetic as
+// k_xtx_i8_big, with the slices staged by LDS-DMA (global_load_lds_dwordx4)
+// into a ring of 64-deep k-blocks (5 stages of 32 KiB for 2 slices): no VGPR round trip and no
+// ds_write pass (k_xtx_i8_big's 64 KiB of b128 stores per k-block ran
+// between its MFMA blocks), all but two stages in flight across each raw barrier
+// (counted vmcnt, never 0 in the loop).  A stage holds, per (operand,
+// slice), 8 chunks of 1 KiB = 16 columns x 64 k-bytes -- one MFMA operand
+// fragment each.  A DMA writes its chunk lane-linearly, so the bank swizzle
+// goes on the source address: lane p of the chunk loads column p >> 2, k
+// bytes 16 ((p & 3) ^ sw) .. +16 with sw = ((p >> 4) & 2); the fragment read of
+// (row fr, k quarter kc) is then at slot 4 fr + (kc ^ ((fr >> 2) & 2)), which
+// puts every ds_read_b128 lane group on 16 distinct 16-byte bank slots.
+#ifndef TP_XG_STAGES2
+#define TP_XG_STAGES2 5   // ring stages for 2 slices (32 KiB each: 160 KiB)
+#endif
+#ifndef TP_XG_STAGES1
+#define TP_XG_STAGES1 8   // ring stages for 1 slice (16 KiB each)
+#endif
+__device__ __forceinline__ void glds16(const void *g, void *l) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)g,
+                                     (__attribute__((address_space(3))) void *)l, 16, 0, 0);
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// wait until at most `later` (<= MAXL) stages of CPW DMAs each are outstanding
+template <int CPW, int MAXL>
+__device__ __forceinline__ void wait_stages(int later) {
+    if constexpr (MAXL <= 0) {
+        wait_vm<0>();
+    } else {
+        if (later >= MAXL) wait_vm<MAXL * CPW>();
+        else wait_stages<CPW, MAXL - 1>(later);
+    }
+}
+template <int NS, bool COR = false>
+__global__ void __launch_bounds__(512) k_xtx_i8_glds(const int8_t *__restrict__ S, int n, int Kp, int Np,
+                                                     double *__restrict__ C, int tcol0, int tn_all,
+                                                     const double *__restrict__ cm = nullptr,
+                                                     const double *__restrict__ csd = nullptr,
+                                                     const int2 *__restrict__ tiles = nullptr, int c0 = 0,
+                                                     int c1 = 0x7fffffff) {
+    constexpr int CH = 2 * NS * 8;         // 1 KiB chunks per stage
+    constexpr int CPW = CH / 8;            // chunks per wave per stage
+    constexpr int STAGE = CH * 1024;
+    constexpr int XG_STAGES = NS == 2 ? TP_XG_STAGES2 : TP_XG_STAGES1;
+    __shared__ __attribute__((aligned(16))) int8_t L[XG_STAGES * STAGE];   // the only LDS object (DMA waits)
+    int bm, bn;
+    if (tiles) {
+        const int2 tl = tiles[blockIdx.x];
+        bm = tl.x;
+        bn = tl.y;
+    } else if (tn_all > 0) {
+        const int total = tn_all * (tn_all + 1) / 2;
+        const int xcd = (int)blockIdx.x & 7, slot = (int)blockIdx.x >> 3;
+        xtx_supertile(xcd * (total >> 3) + min(xcd, total & 7) + slot, tn_all, bm, bn);
+    } else {
+        int id = blockIdx.x;
+        bn = tcol0;
+        while (id > bn) {
+            id -= bn + 1;
+            ++bn;
+        }
+        bm = id;
+    }
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int wm = (w & 1) * 64, wn = (w >> 1) * 32;
+    const size_t slice = (size_t)Np * Kp;
+    const int ia = bm * XB, jb = bn * XB;
+    // this lane's DMA sources: chunk c = w + 8 i -> operand o = c / (8 NS),
+    // slice (c / 8) % NS, column group c % 8 = w; one per-lane base (operand A,
+    // slice 0) plus a wave-uniform offset per chunk
+    const int8_t *vsrc;
+    {
+        const int pc = lane >> 2, pk = (lane & 3) ^ ((lane >> 4) & 2);
+        TP_DASSERT(ia + 16 * w + pc < Np && jb + 16 * w + pc < Np);
+        vsrc = S + (size_t)(ia + 16 * w + pc) * Kp + 16 * pk;
+    }
+    auto chunk_off = [&](int i) -> size_t {
+        const int c = w + 8 * i, o = c / (8 * NS), s = (c >> 3) % NS;
+        return (size_t)s * slice + (o ? (size_t)(jb - ia) * Kp : 0);
+    };
+    const int nk = Kp / 64;
+    auto issue = [&](int k) {   // stage k into ring slot k % XG_STAGES
+        int8_t *dst = L + (k % XG_STAGES) * STAGE;
+#pragma unroll
+        for (int i = 0; i < CPW; ++i) {
+#ifdef TP_XG_DIAG_NODMA   // diagnostic builds only (timing of the MFMA side alone; wrong results)
+            if (k < XG_STAGES)
+#endif
+            glds16(vsrc + chunk_off(i) + (size_t)64 * k, dst + (w + 8 * i) * 1024);
+        }
+    };
+    i32x4 acc[NS][NS][4][2];
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int u = 0; u < NS; ++u)
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b) acc[s][u][a][b] = i32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < XG_STAGES - 1; ++k)
+        if (k < nk) issue(k);
+    const int fr = lane & 15, kc = lane >> 4;
+    const int roff = (4 * fr + (kc ^ ((fr >> 2) & 2))) * 16;
+    // Fragments of stage k + 1 are read while the MFMAs of stage k run, so the
+    // LDS read burst after each barrier is off the MFMA chain.  One slice:
+    // two register sets.  Two slices (128 accumulator registers): one set,
+    // each fragment re-read right after its last MFMA of the step, in the
+    // product order (0,0) (1,0) | b0 | (0,1) | a0 | (1,1) | a1 b1.
+    struct Frag {
+        i32x4 a[NS][4], b[NS][2];
+    };
+    auto rd_a = [&](Frag &f, int k, int s) {
+        const int8_t *Lb = L + (k % XG_STAGES) * STAGE + roff;
+#pragma unroll
+        for (int a = 0; a < 4; ++a) f.a[s][a] = *(const i32x4 *)(Lb + (s * 8 + (wm >> 4) + a) * 1024);
+    };
+    auto rd_b = [&](Frag &f, int k, int s) {
+        const int8_t *Lb = L + (k % XG_STAGES) * STAGE + roff;
+#pragma unroll
+        for (int b = 0; b < 2; ++b) f.b[s][b] = *(const i32x4 *)(Lb + ((NS + s) * 8 + (wn >> 4) + b) * 1024);
+    };
+    auto read_frags = [&](Frag &f, int k) {
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            rd_a(f, k, s);
+            rd_b(f, k, s);
+        }
+    };
+    auto prod = [&](const Frag &f, int s, int u) {
+#ifdef TP_XG_DIAG_NOMFMA   // diagnostic builds only (timing of the load side alone; wrong results)
+        return;
+#endif
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+                acc[s][u][a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(f.a[s][a], f.b[u][b], acc[s][u][a][b], 0, 0, 0);
+    };
+    // step k: stage k + 1 has landed everywhere (this wave's DMAs by the
+    // counted wait, the others' by the barrier) and stage k - 1's slot, read
+    // at step k - 2, is refilled with stage k + XG_STAGES - 1
+    auto sync_issue = [&](int k) {
+        wait_stages<CPW, XG_STAGES - 3>(nk - 2 - k);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (k + XG_STAGES - 1 < nk) issue(k + XG_STAGES - 1);
+    };
+    wait_stages<CPW, XG_STAGES - 2>(nk - 1);
+    __builtin_amdgcn_s_barrier();
+    if constexpr (NS == 1) {
+        Frag f0, f1;
+        read_frags(f0, 0);
+        auto step = [&](int k, Frag &cur, Frag &nxt) {
+            sync_issue(k);
+            if (k + 1 < nk) read_frags(nxt, k + 1);
+            prod(cur, 0, 0);
+        };
+        int k = 0;
+        for (; k + 1 < nk; k += 2) {
+            step(k, f0, f1);
+            step(k + 1, f1, f0);
+        }
+        if (k < nk) step(k, f0, f1);
+    } else {
+        static_assert(NS == 2, "1 or 2 slices");
+        Frag f;
+        read_frags(f, 0);
+        for (int k = 0; k < nk; ++k) {
+            sync_issue(k);
+            const bool more = k + 1 < nk;
+            prod(f, 0, 0);
+            prod(f, 1, 0);
+            if (more) rd_b(f, k + 1, 0);
+            prod(f, 0, 1);
+            if (more) rd_a(f, k + 1, 0);
+            prod(f, 1, 1);
+            if (more) {
+                rd_a(f, k + 1, 1);
+                rd_b(f, k + 1, 1);
+            }
+        }
+    }
+    __syncthreads();   // the ring is free: the epilogue's column statistics reuse it
+    double *pm = (double *)L;   // [0,128) m rows, [128,256) m cols, [256,384) sd rows, [384,512) sd cols
+    if constexpr (COR) {
+        if (t < 128) {
+            const int i = min(ia + t, n - 1), j = min(jb + t, n - 1);
+            pm[t] = cm[i];
+            pm[128 + t] = cm[j];
+            pm[256 + t] = csd[i];
+            pm[384 + t] = csd[j];
+        }
+        __syncthreads();
+    }
+    const double fn = (double)n, fn1 = (double)(n - 1);
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int il = wm + 16 * a + (lane >> 4) * 4 + r, jl = wn + 16 * b + fr;
+                const int i = ia + il;
+                const int j = jb + jl;
+                if (i >= n || j >= n || i > j) continue;
+                long long v = 0;
+#pragma unroll
+                for (int s = 0; s < NS; ++s)
+#pragma unroll
+                    for (int u = 0; u < NS; ++u) v += (long long)acc[s][u][a][b][r] << (7 * (s + u));
+                double d = (double)v;
+                if constexpr (COR) {
+                    const double cij = (d - fn * (pm[il] * pm[128 + jl])) / fn1;
+                    d = cij / (pm[256 + il] * pm[384 + jl]);
+                    if (isnan(d)) d = 0.0;
+                }
+                if (j >= c0 && j < c1) C[(size_t)i + (size_t)(j - c0) * n] = d;
+                if (i >= c0 && i < c1) C[(size_t)j + (size_t)(i - c0) * n] = d;
+            }
+}
+
 // the gather's per-column maxima / flags -> the k_int_scan result format
 __global__ void __launch_bounds__(256) k_colflags(const double *cmax, const int *cbad, int n,
                                                   unsigned long long *maxbits, int *notint) {
@@ -444,6 +670,27 @@ const int8_t *xtx_slices(Ctx &c, const double *d_X, int n, int ns) {
 }
 
 int g_xtx_supertile = 1;
+int g_xtx_glds = 1;   // 0: k_xtx_i8_big (register-staged), 1: k_xtx_i8_glds (knob 32)
+
+template <int NS, bool COR>
+static void launch_xtx128_t(Ctx &c, unsigned nb, const int8_t *sl, int n, int Kp, int Np, double *d_S, int tc0,
+                            int tn_all, const double *cm, const double *csd, const int2 *d_tl, int c0, int c1) {
+    if (g_xtx_glds)
+        hipLaunchKernelGGL((k_xtx_i8_glds<NS, COR>), dim3(nb), dim3(512), 0, c.cur, sl, n, Kp, Np, d_S, tc0, tn_all,
+                           cm, csd, d_tl, c0, c1);
+    else
+        hipLaunchKernelGGL((k_xtx_i8_big<NS, COR>), dim3(nb), dim3(512), 0, c.cur, sl, n, Kp, Np, d_S, tc0, tn_all,
+                           cm, csd, d_tl, c0, c1);
+}
+static void launch_xtx128(Ctx &c, int ns, unsigned nb, const int8_t *sl, int n, int Kp, int Np, double *d_S, int tc0,
+                          int tn_all, const double *cm, const double *csd, const int2 *d_tl, int c0, int c1) {
+    const bool cor = cm != nullptr;
+    if (ns == 1 && !cor) launch_xtx128_t<1, false>(c, nb, sl, n, Kp, Np, d_S, tc0, tn_all, cm, csd, d_tl, c0, c1);
+    else if (ns == 2 && !cor) launch_xtx128_t<2, false>(c, nb, sl, n, Kp, Np, d_S, tc0, tn_all, cm, csd, d_tl, c0, c1);
+    else if (ns == 1) launch_xtx128_t<1, true>(c, nb, sl, n, Kp, Np, d_S, tc0, tn_all, cm, csd, d_tl, c0, c1);
+    else if (ns == 2) launch_xtx128_t<2, true>(c, nb, sl, n, Kp, Np, d_S, tc0, tn_all, cm, csd, d_tl, c0, c1);
+    else fail(TP_ERR_ARG, "xtx_int8 (128-tiles): 1..2 slices");
+}
 
 // S (n x n) = X'X exactly on the upper tiles of tile columns [tc0, tc1) and
 // their mirrors, from ns slices.
@@ -457,18 +704,7 @@ void xtx_int8_tiles128(Ctx &c, const int8_t *sl, int n, int ns, double *d_S, int
     if (tc1 <= tc0) return;
     const unsigned nb = (unsigned)((long)tc1 * (tc1 + 1) / 2 - (long)tc0 * (tc0 + 1) / 2);
     const int tn_all = (tc0 == 0 && tc1 == tn && g_xtx_supertile) ? tn : 0;
-    const bool cor = cm != nullptr;
-    if (ns == 1 && !cor)
-        hipLaunchKernelGGL((k_xtx_i8_big<1>), dim3(nb), dim3(512), 0, c.cur, sl, n, Kp, Np, d_S, tc0, tn_all, cm, csd);
-    else if (ns == 2 && !cor)
-        hipLaunchKernelGGL((k_xtx_i8_big<2>), dim3(nb), dim3(512), 0, c.cur, sl, n, Kp, Np, d_S, tc0, tn_all, cm, csd);
-    else if (ns == 1)
-        hipLaunchKernelGGL((k_xtx_i8_big<1, true>), dim3(nb), dim3(512), 0, c.cur, sl, n, Kp, Np, d_S, tc0, tn_all, cm,
-                           csd);
-    else if (ns == 2)
-        hipLaunchKernelGGL((k_xtx_i8_big<2, true>), dim3(nb), dim3(512), 0, c.cur, sl, n, Kp, Np, d_S, tc0, tn_all, cm,
-                           csd);
-    else fail(TP_ERR_ARG, "xtx_int8_tiles128: 1..2 slices");
+    launch_xtx128(c, ns, nb, sl, n, Kp, Np, d_S, tc0, tn_all, cm, csd, nullptr, 0, 0x7fffffff);
     TP_HIP(hipGetLastError());
 }
 
@@ -489,20 +725,7 @@ void xtx_int8_slab128(Ctx &c, const int8_t *sl, int n, int ns, double *d_slab, i
     int2 *d_tl = c.buf[S_XTXT].as<int2>(tl.size());
     TP_HIP(hipMemcpyAsync(d_tl, tl.data(), tl.size() * sizeof(int2), hipMemcpyHostToDevice, c.cur));
     const unsigned nb = (unsigned)tl.size();
-    const bool cor = cm != nullptr;
-    if (ns == 1 && !cor)
-        hipLaunchKernelGGL((k_xtx_i8_big<1>), dim3(nb), dim3(512), 0, c.cur, sl, n, Kp, Np, d_slab, 0, 0, cm, csd, d_tl,
-                           c0, c1);
-    else if (ns == 2 && !cor)
-        hipLaunchKernelGGL((k_xtx_i8_big<2>), dim3(nb), dim3(512), 0, c.cur, sl, n, Kp, Np, d_slab, 0, 0, cm, csd, d_tl,
-                           c0, c1);
-    else if (ns == 1)
-        hipLaunchKernelGGL((k_xtx_i8_big<1, true>), dim3(nb), dim3(512), 0, c.cur, sl, n, Kp, Np, d_slab, 0, 0, cm, csd,
-                           d_tl, c0, c1);
-    else if (ns == 2)
-        hipLaunchKernelGGL((k_xtx_i8_big<2, true>), dim3(nb), dim3(512), 0, c.cur, sl, n, Kp, Np, d_slab, 0, 0, cm, csd,
-                           d_tl, c0, c1);
-    else fail(TP_ERR_ARG, "xtx_int8_slab128: 1..2 slices");
+    launch_xtx128(c, ns, nb, sl, n, Kp, Np, d_slab, 0, 0, cm, csd, d_tl, c0, c1);
     TP_HIP(hipGetLastError());
     // the host tile list must outlive the asynchronous copy
     stream_sync(c, c.cur);

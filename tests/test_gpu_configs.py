@@ -77,11 +77,13 @@ def test_config_c3_from_hbm(gpu):
     _check(got, z)
 
 
-@pytest.mark.parametrize("forced,space", [(True, "C"), (True, "G"), (True, "G-full-cgs"), (False, "G")])
+@pytest.mark.parametrize("forced,space", [(True, "C"), (True, "C-full-pip"), (True, "G"), (True, "G-full-cgs"),
+                                          (False, "G")])
 def test_pca_krylov_path_vs_lapack(gpu, forced, space):
     """The block Krylov PCA (G never formed; Krylov space of G, the default,
     or of C: knob 20; G with the first CGS pass against every block instead of
-    the last two: knob 28) against LAPACK's SVD on a matrix below its default
+    the last two: knob 28; C with the first PIP pass against every block
+    instead of K_0 and the last two: knob 33) against LAPACK's SVD on a matrix below its default
     size threshold (forced) and the G-formed path on the same matrix: every
     prefix subspace the sweep uses agrees."""
     n0 = 2600
@@ -91,14 +93,16 @@ def test_pca_krylov_path_vs_lapack(gpu, forced, space):
     g = np.flatnonzero(~obad)
     c = O.sparse_cor(cm[np.ix_(g, g)])
     old = G.knob(8, 0 if forced else 1 << 30)
-    old20 = G.knob(20, 1 if space == "C" else 0)
+    old20 = G.knob(20, 1 if space.startswith("C") else 0)
     old28 = G.knob(28, 0 if space == "G-full-cgs" else 1)
+    old33 = G.knob(33, 0 if space == "C-full-pip" else 1)
     try:
         p, _ = G.pca(c, 200)
     finally:
         G.knob(8, old)
         G.knob(20, old20)
         G.knob(28, old28)
+        G.knob(33, old33)
     op = O.prcomp_x(c, 200)
     s = np.sign(np.sum(p * op, axis=0))
     s[s == 0] = 1

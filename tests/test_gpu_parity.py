@@ -500,6 +500,25 @@ def test_xtx_int8_exact(gpu, n, maxv, slices):
     print(f"xtx n={n} slices={ns}: int8 {ms * 1e3:.1f} us, fp64 {ms64 * 1e3:.1f} us")
 
 
+@pytest.mark.parametrize("glds", [1, 0])
+@pytest.mark.parametrize("n,maxv,slices", [(1100, 120, 1), (1500, 16000, 2), (2000, 127, 1), (4100, 9000, 2),
+                                           (1025, 300, 2)])
+def test_xtx_int8_tiles128_exact(gpu, n, maxv, slices, glds):
+    """The pipeline's 128-column tile kernels (the LDS-DMA ring, knob 32 = 1,
+    and the register-staged one): exact X'X at ragged n, both slice counts."""
+    rng = np.random.default_rng(n * 3 + maxv)
+    x = rng.integers(0, maxv, size=(n, n)).astype(np.float64)
+    x[0, 0] = maxv - 1
+    old = G.knob(32, glds)
+    try:
+        S, ns, ms, st = _xtx(gpu, x, 2)
+    finally:
+        G.knob(32, old)
+    assert st == 0 and ns == slices
+    assert np.array_equal(S, _exact_xtx(x))
+    print(f"xtx128 n={n} slices={ns} glds={glds}: {ms * 1e3:.1f} us")
+
+
 @pytest.mark.parametrize("n,maxv", [(515, 16000), (1100, 9000), (1100, 120)])
 def test_xtx_int8_exact_fresh_context(gpu, n, maxv):
     """Regression for the out-of-bounds slice reads fixed in 5295f4f (64-tile

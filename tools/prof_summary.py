@@ -23,7 +23,7 @@ OUT = os.path.join(ROOT, "gpurun_out")
 # (the CONISS block size and the GEMM tile are chosen per problem size)
 CLASSES = {"coniss": ["tp::k_coniss_t<false,"],
            "ch": ["tp::k_ch_cut", "tp::k_ch_segstat", "tp::k_ch<"],
-           "xtx_gemm": ["tp::k_xtx_i8_big<"]}
+           "xtx_gemm": ["tp::k_xtx_i8_"]}
 
 
 def pick(stats, prefix):
