@@ -661,33 +661,37 @@ def _tadpole_arms(raw, plan, max_pcs, min_clusters, device, shard_flag: int = 0,
         return _assemble(res, np.asarray(bad_cols))
 
     if _arms_concurrent(raw, shard_flag, stream):
-        # the q arm starts when the p arm's PCA is done (the library's
-        # progress word for p's stream): q's correlation and PCA (MFMA-bound,
-        # the whole chip) then run under p's CONISS sweep (latency-bound, one
-        # workgroup per tree), and the two sweeps do not compete for LDS
+        # both arms start at once (0.305 s for C5 on one MI355X, 0.33 s one
+        # after the other).  TADPOLE_ARMS_Q_AT=s (1..3) holds q back until p's
+        # progress word reaches stage s (2: p's correlation queued, 3: p's
+        # sweep): measured slower (0.32-0.34 s at s = 3: q's int8 X'X, 160 KiB
+        # of LDS a workgroup, cannot share a CU with p's CONISS trees).
         import time
         from concurrent.futures import ThreadPoolExecutor
         sp, sq = _arm_streams(device)
-        L = _lib.load()
+        q_at = int(os.environ.get("TADPOLE_ARMS_Q_AT", "0"))
+        L = _lib.load() if q_at > 0 else None
         prog = np.zeros(1, np.int32)
         st = cint(0)
-        L.tp_progress_attach(ctypes.byref(cint(device)), ctypes.c_void_p(sp.cuda_stream),
-                             prog.ctypes.data_as(ctypes.c_void_p), ctypes.byref(st))
-        _lib.check(st)
+        if L is not None:
+            L.tp_progress_attach(ctypes.byref(cint(device)), ctypes.c_void_p(sp.cuda_stream),
+                                 prog.ctypes.data_as(ctypes.c_void_p), ctypes.byref(st))
+            _lib.check(st)
         try:
             with ThreadPoolExecutor(max_workers=2) as ex:
                 fp = ex.submit(run_arm, "p", sp)
 
                 def run_q():
-                    while prog[0] < 3 and not fp.done():
+                    while q_at > 0 and prog[0] < q_at and not fp.done():
                         time.sleep(2e-4)
                     return run_arm("q", sq)
 
                 fq = ex.submit(run_q)
                 subs = {"p": fp.result(), "q": fq.result()}
         finally:
-            L.tp_progress_attach(ctypes.byref(cint(device)), ctypes.c_void_p(sp.cuda_stream), None,
-                                 ctypes.byref(st))
+            if L is not None:
+                L.tp_progress_attach(ctypes.byref(cint(device)), ctypes.c_void_p(sp.cuda_stream), None,
+                                     ctypes.byref(st))
     else:
         subs = {}
         for arm in ("p", "q"):
