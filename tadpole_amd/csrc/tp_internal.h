@@ -109,7 +109,7 @@ enum Slot {
     S_S, S_C, S_XC, S_XCT, S_G, S_Q, S_Z, S_W, S_SMALL, S_P, S_PT,
     S_SWEEP, S_SWEEP2, S_SCORES, S_PARTIAL, S_MISC, S_SHARD, S_SHARD2, S_DEDUP,
     S_KRY, S_KRYG, S_KRYT, S_KRYV, S_KRYX, S_CMEAN, S_CHBIG, S_CHOLP, S_SMALL2, S_GSTAT, S_XTXT, S_MEXT, S_KRYA,
-    S_KRYH,
+    S_KRYH, S_XNZ,
     S_NSLOT
 };
 static_assert(S_NSLOT <= (int)(sizeof(Ctx::buf) / sizeof(Ctx::buf[0])), "Ctx::buf too small for the slots");
@@ -197,6 +197,7 @@ extern int g_gram64;
 // Z'Z (64 x 64, ld 64) of an n x 64 block by k_gram64, bit-identical to the
 // symmetric split-K GEMM; false: not applicable (the caller runs gemm_f64)
 bool gram64(const double *Z, int n, int ldz, double *W, DevBuf &work, hipStream_t s);
+extern int g_xtx_nz;          // int8 X'X (LDS-DMA kernel): skip the high slice's zero blocks
 extern int g_xtx_glds;        // int8 X'X: LDS-DMA ring kernel (0: register-staged k_xtx_i8_big)
 extern int g_xtx_supertile;   // int8 X'X: XCD-contiguous supertile order of the 128 x 128 tiles (0: columns)
 // row-shardable products that take the 128 x 64 kernel with k chunks fixed by K

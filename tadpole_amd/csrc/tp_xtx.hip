@@ -380,6 +380,28 @@ template <int N>
 __device__ __forceinline__ void wait_vm() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
+// wait until at most n (0..16) of this wave's vector-memory operations are outstanding
+__device__ __forceinline__ void wait_vm_dyn(int n) {
+    switch (n) {
+        case 0: wait_vm<0>(); break;
+        case 1: wait_vm<1>(); break;
+        case 2: wait_vm<2>(); break;
+        case 3: wait_vm<3>(); break;
+        case 4: wait_vm<4>(); break;
+        case 5: wait_vm<5>(); break;
+        case 6: wait_vm<6>(); break;
+        case 7: wait_vm<7>(); break;
+        case 8: wait_vm<8>(); break;
+        case 9: wait_vm<9>(); break;
+        case 10: wait_vm<10>(); break;
+        case 11: wait_vm<11>(); break;
+        case 12: wait_vm<12>(); break;
+        case 13: wait_vm<13>(); break;
+        case 14: wait_vm<14>(); break;
+        case 15: wait_vm<15>(); break;
+        default: wait_vm<16>(); break;
+    }
+}
 // wait until at most `later` (<= MAXL) stages of CPW DMAs each are outstanding
 template <int CPW, int MAXL>
 __device__ __forceinline__ void wait_stages(int later) {
@@ -396,7 +418,8 @@ __global__ void __launch_bounds__(512) k_xtx_i8_glds(const int8_t *__restrict__ 
                                                      const double *__restrict__ cm = nullptr,
                                                      const double *__restrict__ csd = nullptr,
                                                      const int2 *__restrict__ tiles = nullptr, int c0 = 0,
-                                                     int c1 = 0x7fffffff) {
+                                                     int c1 = 0x7fffffff, const unsigned *__restrict__ nzw = nullptr,
+                                                     int NW = 0) {
     constexpr int CH = 2 * NS * 8;         // 1 KiB chunks per stage
     constexpr int CPW = CH / 8;            // chunks per wave per stage
     constexpr int STAGE = CH * 1024;
@@ -438,10 +461,33 @@ __global__ void __launch_bounds__(512) k_xtx_i8_glds(const int8_t *__restrict__ 
         return (size_t)s * slice + (o ? (size_t)(jb - ia) * Kp : 0);
     };
     const int nk = Kp / 64;
+    // Two slices: the high slice X1 of raw Hi-C counts is zero outside a band
+    // around the diagonal (C3: 3 % of the 128-column x 64-k blocks hold a count
+    // >= 128), so a stage loads and multiplies X1's chunks only where its
+    // block-nonzero map (k_slice_nz) has the bit: a1 / b1 for the A / B
+    // operand.  Skipped products are exactly zero: same sums, same bits.
+    // Lane j holds word j of the tile row's and tile column's maps.
+    unsigned za = ~0u, zb = ~0u;
+    if (NS == 2 && nzw != nullptr) {
+        za = lane < NW ? nzw[(size_t)bm * NW + lane] : 0u;
+        zb = lane < NW ? nzw[(size_t)bn * NW + lane] : 0u;
+    }
+    auto hi_a = [&](int k) -> bool {
+        return NS == 2 && ((__builtin_amdgcn_readlane((int)za, k >> 5) >> (k & 31)) & 1);
+    };
+    auto hi_b = [&](int k) -> bool {
+        return NS == 2 && ((__builtin_amdgcn_readlane((int)zb, k >> 5) >> (k & 31)) & 1);
+    };
+    auto dmas = [&](int k) -> int {   // DMAs per wave of stage k
+        return NS == 2 ? 2 + (int)hi_a(k) + (int)hi_b(k) : CPW;
+    };
     auto issue = [&](int k) {   // stage k into ring slot k % XG_STAGES
         int8_t *dst = L + (k % XG_STAGES) * STAGE;
+        const bool ha = hi_a(k), hb = hi_b(k);
 #pragma unroll
         for (int i = 0; i < CPW; ++i) {
+            // NS = 2: i = 0 A0, 1 A1, 2 B0, 3 B1
+            if (NS == 2 && ((i == 1 && !ha) || (i == 3 && !hb))) continue;
 #ifdef TP_XG_DIAG_NODMA   // diagnostic builds only (timing of the MFMA side alone; wrong results)
             if (k < XG_STAGES)
 #endif
@@ -500,13 +546,21 @@ __global__ void __launch_bounds__(512) k_xtx_i8_glds(const int8_t *__restrict__ 
     // step k: stage k + 1 has landed everywhere (this wave's DMAs by the
     // counted wait, the others' by the barrier) and stage k - 1's slot, read
     // at step k - 2, is refilled with stage k + XG_STAGES - 1
+    // this wave's DMAs of the stages after `upto` that are issued by step k
+    auto later_dmas = [&](int upto, int last) {
+        int c = 0;
+        for (int j = upto + 1; j <= min(last, nk - 1); ++j) c += dmas(j);
+        return c;
+    };
     auto sync_issue = [&](int k) {
-        wait_stages<CPW, XG_STAGES - 3>(nk - 2 - k);
+        if constexpr (NS == 2) wait_vm_dyn(later_dmas(k + 1, k + XG_STAGES - 2));
+        else wait_stages<CPW, XG_STAGES - 3>(nk - 2 - k);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         if (k + XG_STAGES - 1 < nk) issue(k + XG_STAGES - 1);
     };
-    wait_stages<CPW, XG_STAGES - 2>(nk - 1);
+    if constexpr (NS == 2) wait_vm_dyn(later_dmas(0, XG_STAGES - 2));
+    else wait_stages<CPW, XG_STAGES - 2>(nk - 1);
     __builtin_amdgcn_s_barrier();
     if constexpr (NS == 1) {
         Frag f0, f1;
@@ -525,19 +579,23 @@ __global__ void __launch_bounds__(512) k_xtx_i8_glds(const int8_t *__restrict__ 
     } else {
         static_assert(NS == 2, "1 or 2 slices");
         Frag f;
-        read_frags(f, 0);
+        rd_a(f, 0, 0);
+        rd_b(f, 0, 0);
+        if (hi_a(0)) rd_a(f, 0, 1);
+        if (hi_b(0)) rd_b(f, 0, 1);
         for (int k = 0; k < nk; ++k) {
             sync_issue(k);
             const bool more = k + 1 < nk;
+            const bool ha = hi_a(k), hb = hi_b(k);
             prod(f, 0, 0);
-            prod(f, 1, 0);
+            if (ha) prod(f, 1, 0);
             if (more) rd_b(f, k + 1, 0);
-            prod(f, 0, 1);
+            if (hb) prod(f, 0, 1);
             if (more) rd_a(f, k + 1, 0);
-            prod(f, 1, 1);
+            if (ha && hb) prod(f, 1, 1);
             if (more) {
-                rd_a(f, k + 1, 1);
-                rd_b(f, k + 1, 1);
+                if (hi_a(k + 1)) rd_a(f, k + 1, 1);
+                if (hi_b(k + 1)) rd_b(f, k + 1, 1);
             }
         }
     }
@@ -671,13 +729,49 @@ const int8_t *xtx_slices(Ctx &c, const double *d_X, int n, int ns) {
 
 int g_xtx_supertile = 1;
 int g_xtx_glds = 1;   // 0: k_xtx_i8_big (register-staged), 1: k_xtx_i8_glds (knob 32)
+int g_xtx_nz = 1;     // 1: k_xtx_i8_glds skips the high slice's zero blocks (knob 34)
+
+// Block-nonzero map of the high slice (slice 1): bit kb & 31 of word
+// nzw[cb * NW + kb / 32] is set when any byte of columns 128 cb .. + 127, k
+// bytes 64 kb .. + 63 is nonzero.  Workgroup (cb, word): thread t reads
+// column t / 2, 32-byte half t % 2 of each of the word's 32 k-blocks.
+__global__ void __launch_bounds__(256) k_slice_nz(const int8_t *__restrict__ S1, int Kp, int NW,
+                                                  unsigned *__restrict__ nzw) {
+    __shared__ unsigned red[4];
+    const int cb = blockIdx.x, wd = blockIdx.y, t = threadIdx.x;
+    const int nk = Kp / 64;
+    const int8_t *col = S1 + (size_t)(cb * 128 + (t >> 1)) * Kp + 32 * (t & 1);
+    unsigned m = 0;
+#pragma unroll 4
+    for (int b = 0; b < 32; ++b) {
+        const int kb = wd * 32 + b;
+        if (kb >= nk) break;
+        const int4 *p = (const int4 *)(col + (size_t)64 * kb);
+        const int4 x = p[0], y = p[1];
+        const bool nz = (x.x | x.y | x.z | x.w | y.x | y.y | y.z | y.w) != 0;
+        m |= nz ? (1u << b) : 0u;
+    }
+    for (int o = 32; o > 0; o >>= 1) m |= (unsigned)__shfl_xor((int)m, o, 64);
+    if ((t & 63) == 0) red[t >> 6] = m;
+    __syncthreads();
+    if (t == 0) nzw[(size_t)cb * NW + wd] = red[0] | red[1] | red[2] | red[3];
+}
 
 template <int NS, bool COR>
 static void launch_xtx128_t(Ctx &c, unsigned nb, const int8_t *sl, int n, int Kp, int Np, double *d_S, int tc0,
                             int tn_all, const double *cm, const double *csd, const int2 *d_tl, int c0, int c1) {
-    if (g_xtx_glds)
+    if (g_xtx_glds) {
+        unsigned *nzw = nullptr;
+        const int NW = (Kp / 64 + 31) / 32;
+        if (NS == 2 && g_xtx_nz) {
+            if (NW > 64) fail(TP_ERR_ARG, "xtx_int8: k blocks past the 64-word nonzero map");
+            nzw = c.buf[S_XNZ].as<unsigned>((size_t)(Np / 128) * NW);
+            hipLaunchKernelGGL(k_slice_nz, dim3((unsigned)(Np / 128), (unsigned)NW), dim3(256), 0, c.cur,
+                               sl + (size_t)Np * Kp, Kp, NW, nzw);
+        }
         hipLaunchKernelGGL((k_xtx_i8_glds<NS, COR>), dim3(nb), dim3(512), 0, c.cur, sl, n, Kp, Np, d_S, tc0, tn_all,
-                           cm, csd, d_tl, c0, c1);
+                           cm, csd, d_tl, c0, c1, nzw, NW);
+    }
     else
         hipLaunchKernelGGL((k_xtx_i8_big<NS, COR>), dim3(nb), dim3(512), 0, c.cur, sl, n, Kp, Np, d_S, tc0, tn_all,
                            cm, csd, d_tl, c0, c1);

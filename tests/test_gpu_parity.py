@@ -519,6 +519,32 @@ def test_xtx_int8_tiles128_exact(gpu, n, maxv, slices, glds):
     print(f"xtx128 n={n} slices={ns} glds={glds}: {ms * 1e3:.1f} us")
 
 
+@pytest.mark.parametrize("nzmap", [1, 0])
+@pytest.mark.parametrize("n", [1100, 3000, 4100])
+def test_xtx_int8_tiles128_sparse_high_slice(gpu, n, nzmap):
+    """Counts >= 128 only in a band around the diagonal and at a few scattered
+    entries (raw Hi-C): the LDS-DMA kernel skips the high slice's all-zero
+    128 x 64 blocks (knob 34) and the product stays exact."""
+    rng = np.random.default_rng(n)
+    x = rng.integers(0, 128, size=(n, n)).astype(np.float64)
+    i = np.arange(n)
+    for d in range(-5, 6):
+        j = i + d
+        ok = (j >= 0) & (j < n)
+        x[i[ok], j[ok]] = rng.integers(128, 16000, size=int(ok.sum()))
+    r, c = rng.integers(0, n, 40), rng.integers(0, n, 40)
+    x[r, c] = 15000
+    old32, old34 = G.knob(32, 1), G.knob(34, nzmap)
+    try:
+        S, ns, ms, st = _xtx(gpu, x, 2)
+    finally:
+        G.knob(32, old32)
+        G.knob(34, old34)
+    assert st == 0 and ns == 2
+    assert np.array_equal(S, _exact_xtx(x))
+    print(f"xtx128 sparse-high n={n} nzmap={nzmap}: {ms * 1e3:.1f} us")
+
+
 @pytest.mark.parametrize("n,maxv", [(515, 16000), (1100, 9000), (1100, 120)])
 def test_xtx_int8_exact_fresh_context(gpu, n, maxv):
     """Regression for the out-of-bounds slice reads fixed in 5295f4f (64-tile

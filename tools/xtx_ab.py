@@ -1,7 +1,7 @@
 """X'X kernel A/B: time of the pipeline's 128-column int8 tile kernels
 (tp_debug_xtx mode 2, mean of 3) with knob 32 = 0 (register-staged) and 1
 (LDS-DMA ring) on a synthetic count matrix, and bitwise equality of the two.
-python tools/xtx_ab.py N [maxv]"""
+python tools/xtx_ab.py N [maxv (0: synthetic Hi-C)] [knob=value ...]"""
 import ctypes
 import os
 import sys
@@ -14,9 +14,16 @@ import gpu_helpers as G  # noqa: E402
 from tadpole_amd import _lib  # noqa: E402
 
 n = int(sys.argv[1])
-maxv = int(sys.argv[2]) if len(sys.argv) > 2 else 9000
+maxv = int(sys.argv[2]) if len(sys.argv) > 2 else 9000   # 0: a synthetic Hi-C matrix
+knobs = [tuple(int(v) for v in kv.split("=")) for kv in sys.argv[3:]]   # which=value, set for both arms
 L = _lib.load()
-x = np.asfortranarray(np.random.default_rng(n).integers(0, maxv, size=(n, n)).astype(np.float64))
+if maxv == 0:
+    from tadpole_amd.synth import synth_hic, synth_hic_par
+    x = np.asfortranarray(synth_hic(n, 20261017) if n < 8000 else synth_hic_par(n, 20261017))
+else:
+    x = np.asfortranarray(np.random.default_rng(n).integers(0, maxv, size=(n, n)).astype(np.float64))
+for w, v in knobs:
+    G.knob(w, v)
 D = ctypes.POINTER(ctypes.c_double)
 out = {}
 for glds in (0, 1, 0, 1):
