@@ -76,7 +76,7 @@ __global__ void k_start_block(double *Q, int n, uint64_t seed) {
 // (at C3, 7.7k bins, the G space is ~0.8 ms faster)
 int g_pca_ckrylov = -1;
 int g_ckry_min = 10000;
-int g_ckry_chunk = 256;       // rows per Z partial of the PIP passes
+int g_ckry_chunk = 0;         // rows per Z partial of the PIP passes (0: from n and D, see pip_chunk)
 int g_ckry_steps = 0;         // blocks s before the first check (0: from k and n)
 int g_ckry_local = 1;         // first BCGS-PIP pass against K_0, K_{t-2}, K_{t-1} only (knob 33)
 
@@ -90,6 +90,14 @@ struct PipScratch {
 // local >= 4: the pass runs against K_0 and the two blocks before slot `local`
 // only (a local first pass, see krylov_c_topk); the result still lands in
 // slot D / KP = local.
+// Rows per Z partial: ~1024 workgroups of k_pipz (dt column tiles x n /
+// chunk row chunks), 512 to 1024 rows (fewer partials for k_pipr to sum; 24.3k
+// bins, PCA: fixed 256 rows 74.5 ms, 512 73.4, 768 73.3, 1024 73.7)
+static int pip_chunk(int n, int dt) {
+    if (g_ckry_chunk > 0) return std::max(64, g_ckry_chunk);
+    const long want = ((long)n * dt / 1024 + 63) / 64 * 64;
+    return (int)std::max<long>(512, std::min<long>(1024, want));
+}
 static void pip_pass(Ctx &c, double *Kb, int n, int D, const double *W0, const PipScratch &ps, double shift,
                      int lowdin = 0, int local = 0) {
     hipStream_t s = c.cur;
@@ -102,9 +110,9 @@ static void pip_pass(Ctx &c, double *Kb, int n, int D, const double *W0, const P
         D = 3 * KP;
     }
     const int ldz = D + KP;
-    const int chunk = std::max(64, g_ckry_chunk);
-    const int S = (n + chunk - 1) / chunk;
     const int dt = (ldz + PZ_COLS - 1) / PZ_COLS;
+    const int chunk = pip_chunk(n, dt);
+    const int S = (n + chunk - 1) / chunk;
     const size_t pstride = (size_t)ldz * KP;
     hipLaunchKernelGGL(k_pipz, dim3((unsigned)(dt * S)), dim3(256), 0, s, Kb, D, W0, n, chunk, ps.part, pstride, Kt,
                        Dh);
@@ -122,7 +130,8 @@ static void pip_pass(Ctx &c, double *Kb, int n, int D, const double *W0, const P
 }
 
 size_t ckry_partial_doubles(int n, int dmax) {
-    const int chunk = std::max(64, g_ckry_chunk);
+    // the most partials any pass needs: the smallest chunk is the floor's
+    const int chunk = g_ckry_chunk > 0 ? std::max(64, g_ckry_chunk) : 512;
     return (size_t)((n + chunk - 1) / chunk) * (size_t)(dmax + KP) * KP;
 }
 
@@ -137,6 +146,11 @@ bool krylov_c_topk(Ctx &c, double *C, int c_col0, const double *mext, int n, int
     if (n > 12000) steps += (int)std::ceil(12.0 * std::log2((double)n / 12000.0));   // 24k: 45 (44 measured)
     if (g_ckry_steps > 0) steps = g_ckry_steps;
     steps = std::max(1, steps);
+    // T = K'GK is block pentadiagonal in the 32-column blocks (G = C Pc C,
+    // C K_t in span K_{t-1..t+1}, the rank-1 centring term in K_0, K_1): with
+    // an even block count it is block TRIdiagonal in 64-column blocks, so the
+    // small problem's products with T are banded (k_band_ty, as the G path)
+    if (g_pca_band) steps += steps & 1;
     const int smax = std::max(steps, std::min(steps + 48, (n / 2) / KP));
     steps = std::min(steps, smax);
     const size_t np = (size_t)n * KP;
@@ -195,11 +209,18 @@ bool krylov_c_topk(Ctx &c, double *C, int c_col0, const double *mext, int n, int
         double *Tm = c.buf[S_KRYT].as<double>((size_t)D * D);
         GemmArgs tg{D, D, n, Pb, n, true, Pb, n, Tm, D};   // T = P'P
         tg.sym_upper = true;
-        tg.splitk = 0;
+        {
+            // a few hundred 64 x 64 upper tiles over K = n: split K so ~1000
+            // workgroups run (one k chunk a tile ran 2.2 ms at 24.3k bins, D 1472)
+            const long nt = (long)((D + 63) / 64) * ((D + 63) / 64 + 1) / 2;
+            tg.splitk = n >= 4096 ? (int)std::max<long>(1, std::min<long>(8, (1024 + nt - 1) / nt)) : 0;
+        }
         gemm_f64(tg, c.buf[S_PARTIAL], s);
         double *Vs = c.buf[S_KRYV].as<double>((size_t)D * k);
         PcaStats sst;
-        small_topk_T(c, Tm, D, k, Vs, h_theta, sst);
+        // banded products when T is block tridiagonal in 64-column blocks (its
+        // entries off the band are rounding-level and are not read)
+        small_topk_T(c, Tm, D, k, Vs, h_theta, sst, (g_pca_band && D % 64 == 0) ? 64 : 0);
         // V = K Y, scores Xc V = P Y
         GemmArgs vg{n, k, D, K, n, false, Vs, D, V, n};
         vg.splitk = 0;
