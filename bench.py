@@ -364,8 +364,13 @@ def distribute_rows(host, n0, world, rank, sink, chunk_rows=C5_CHUNK_ROWS):
 
 def c5_mode(world):
     """How the c5_full line runs at this rank count: one GPU unsharded (plus a
-    one-rank RCCL check), or every arm sharded over all ranks."""
-    return "sharded" if world > 1 else "one_gpu"
+    one-rank RCCL check), every arm sharded over all ranks, or skipped when
+    ranks share a GPU (a rehearsal with more ranks than devices: RCCL needs
+    one device per rank)."""
+    if world == 1:
+        return "one_gpu"
+    import torch
+    return "sharded" if torch.cuda.device_count() >= world else "skipped"
 
 
 def run_c5_full(world, rank, local, max_pcs, reps):
@@ -678,7 +683,10 @@ def main():
         c4 = run_c4_genome(world, rank, args.max_pcs, args.extras_reps)
         if rank == 0:
             extras["c4_genome"] = c4
-        if not args.no_c5:
+        if not args.no_c5 and c5_mode(world) == "skipped":
+            if rank == 0:
+                extras["c5_full"] = {"skipped": "ranks share a GPU (RCCL needs one device per rank)"}
+        elif not args.no_c5:
             try:
                 c5 = run_c5_full(world, rank, local, args.max_pcs, args.extras_reps)
             except Exception as e:   # noqa: BLE001 -- reported in the line; the C3 headline stands

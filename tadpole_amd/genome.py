@@ -84,6 +84,13 @@ def run_genome(matrices: Mapping[str, object], sizes: Optional[Mapping[str, int]
     world = dist.get_world_size() if dist_on else 1
     rank = dist.get_rank() if dist_on else 0
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    try:   # ranks beyond the visible GPUs wrap onto them (as bench.py's ranks do)
+        import torch
+        nd = torch.cuda.device_count()
+        if nd > 0:
+            local %= nd
+    except ImportError:
+        pass
     if sizes is None:
         sizes = {}
         for name, m in matrices.items():

@@ -84,14 +84,21 @@ def _dist_worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def test_c5_full_multi_rank_path_gloo():
+def test_c5_full_multi_rank_path_gloo(monkeypatch):
     """The c5_full line at world 2 (what `bench.py --gpus 2` selects): the
-    sharded mode, and the C5 matrix reaching every rank intact through the
-    chunked gloo broadcast (rank 0 holds the only host copy)."""
+    sharded mode with a device per rank (skipped when ranks would share a
+    GPU), and the C5 matrix reaching every rank intact through the chunked
+    gloo broadcast (rank 0 holds the only host copy)."""
     import socket
+    import torch
     import torch.multiprocessing as mp
     import bench
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
     assert bench.c5_mode(1) == "one_gpu" and bench.c5_mode(8) == "sharded"
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
+    assert bench.c5_mode(2) == "skipped"
+    monkeypatch.undo()
+    want_mode = "sharded" if torch.cuda.device_count() >= 2 else "skipped"
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -104,4 +111,4 @@ def test_c5_full_multi_rank_path_gloo():
     res = sorted(q.get(timeout=120) for _ in ps)
     for p in ps:
         p.join(60)
-    assert res == [(0, True, "sharded"), (1, True, "sharded")]
+    assert res == [(0, True, want_mode), (1, True, want_mode)]
