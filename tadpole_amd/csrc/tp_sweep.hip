@@ -314,6 +314,12 @@ __device__ __forceinline__ double ward_part(const double (&sa)[NS], double fa, c
 #ifndef TP_CONISS_GLBPF
 #define TP_CONISS_GLBPF 0
 #endif
+// TP_CONISS_EPF    the sums wave prefetches a2's rows before barrier X when the
+//                  structure wave has already published them (sequence word
+//                  mb_d[3]), instead of after X
+#ifndef TP_CONISS_EPF
+#define TP_CONISS_EPF 0
+#endif
 __device__ __forceinline__ void coniss_bar() {
 #if TP_CONISS_LDSBAR
     lds_barrier();
@@ -338,6 +344,7 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
     constexpr int ld = NS * 64;
     constexpr bool kBmi = TP_CONISS_BMI != 0;
     constexpr bool kPf = GLB && TP_CONISS_GLBPF != 0;
+    constexpr bool kEpf = TP_CONISS_EPF != 0;
     const int lane = threadIdx.x & 63;
     const bool waveA = __builtin_amdgcn_readfirstlane((int)threadIdx.x) < 64;   // wave-uniform: a scalar branch
     const int nbk = (n + 63) / 64;
@@ -529,6 +536,7 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
         mb_i[1] = rc.y;
         mb_i[2] = rc.z;
         mb_d[2] = c;
+        mb_d[3] = -1.0;
     }
     __syncthreads();
     // B's registers
@@ -662,6 +670,9 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
                 mb_i[3] = make_int4(rowc(m0.a, m0.ea == m0.a), rowc(bs2, m0.eb == bs2),
                                     m0.ls >= 0 ? rowc(m0.ls, m0.ls == m0.a - 1) : -1,
                                     m0.r >= 0 ? rowc(m0.r, m0.er == m0.r) : -1);
+                // after the rows (LDS operations of one wave complete in order):
+                // a reader that sees s also sees this merge's rows
+                if constexpr (kEpf) mb_d[3] = (double)s;
             }
             Mg m1;   // ls | m
             m1.a = ls; m1.ea = a - 1; m1.eb = eb; m1.ls = cur.ll; m1.r = r; m1.er = er;
@@ -789,6 +800,15 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
                 asm volatile("" ::"v"(z));
             }
             TP_STAMP(1);
+            // a2's rows: if A has already published them for this merge, their
+            // loads go out now (the Ward work below hides the LDS round trip)
+            // rather than after X -- ~a Ward step and a barrier earlier
+            double seqv = -2.0;
+            int4 p0e = make_int4(0, 0, 0, 0);
+            if constexpr (kEpf) {
+                seqv = mb_d[3];
+                p0e = mb_i[3];
+            }
             const double fm = (double)nm, fl = (double)nl, fr = (double)nr;
             double ul = ward_part<NS>(sl, fl, sm, fm, last_in);
             double ur = ward_part<NS>(sm, fm, sr, fr, last_in);
@@ -801,6 +821,19 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
             h = h + cc;
             mb_d[0] = cl;
             mb_d[1] = cr;
+            bool early = false;
+            if constexpr (kEpf) {
+                if (seqv == (double)s) {
+                    load_row(pa, p0e.x);
+                    load_row(pb, p0e.y);
+                    load_row(pl, p0e.z >= 0 ? p0e.z : p0e.x);
+                    load_row(pr, p0e.w >= 0 ? p0e.w : p0e.x);
+                    ls2p = p0e.z;
+                    r2p = p0e.w;
+                    aprev = a_;
+                    early = true;
+                }
+            }
             // every lane stores the same words (one request each; no exec mask)
             mrg_a[s] = a_;
             mrg_b[s] = b_;
@@ -809,15 +842,17 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
             TP_STAMP(2);
             coniss_bar();   // X (LDS-only by default: global loads stay in flight)
             TP_STAMP(3);
-            // ---- prefetch a2's rows for the next merge
-            const int4 p0 = mb_i[3];
-            load_row(pa, p0.x);
-            load_row(pb, p0.y);
-            load_row(pl, p0.z >= 0 ? p0.z : p0.x);
-            load_row(pr, p0.w >= 0 ? p0.w : p0.x);
-            ls2p = p0.z;
-            r2p = p0.w;
-            aprev = a_;
+            // ---- prefetch a2's rows for the next merge (unless done before X)
+            if (!early) {
+                const int4 p0 = mb_i[3];
+                load_row(pa, p0.x);
+                load_row(pb, p0.y);
+                load_row(pl, p0.z >= 0 ? p0.z : p0.x);
+                load_row(pr, p0.w >= 0 ? p0.w : p0.x);
+                ls2p = p0.z;
+                r2p = p0.w;
+                aprev = a_;
+            }
             TP_STAMP(6);
             coniss_bar();   // Y
             TP_STAMP(7);
