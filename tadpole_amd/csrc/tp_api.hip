@@ -1623,6 +1623,7 @@ void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
         case 32: p = &g_xtx_glds; break;
         case 33: p = &g_ckry_local; break;
         case 34: p = &g_xtx_nz; break;
+        case 35: p = &g_gemm_ts_pf2; break;
         default: fail(TP_ERR_ARG, "unknown knob");
         }
         if (*which == 3 && *value != 16 && *value != 32) fail(TP_ERR_ARG, "stage depth must be 16 or 32");

@@ -409,7 +409,7 @@ int g_gemm_panel = 1;   // 0: tall-skinny products take the split-K 64 x 64 path
 // TN = 32 (the C-Krylov blocks): a 128 x 32 tile, each wave 32 x 32 (2 x 2
 // accumulators); same k order, so the bits of a column do not depend on TN.
 constexpr int TSM = 128, TSN = 64, TSK = 16, TSLD = TSK + 2;
-template <int TAG, int TN = TSN>
+template <int TAG, int TN = TSN, bool PF2 = false>
 __global__ void __launch_bounds__(256, 2) k_gemm_ts(int M, int N, int K, const double *__restrict__ A, int lda,
                                                     const double *__restrict__ B, int ldb, double *__restrict__ C,
                                                     int ldc, int store_t, int kchunk, size_t part_stride) {
@@ -458,15 +458,7 @@ __global__ void __launch_bounds__(256, 2) k_gemm_ts(int M, int N, int K, const d
 #pragma unroll
         for (int p = 0; p < NB; ++p) Bs[buf][lr + 16 * p][lk] = rb[p];
     };
-    if (kbeg < kend) {
-        load(kbeg);
-        store(0);
-    }
-    __syncthreads();
-    int buf = 0;
-    for (int k0 = kbeg; k0 < kend; k0 += TSK) {
-        const bool more = k0 + TSK < kend;
-        if (more) load(k0 + TSK);
+    auto mfma_stage = [&](int buf) {
 #pragma unroll
         for (int kk = 0; kk < TSK; kk += 4) {
             double af[2], bf[NB];
@@ -480,9 +472,75 @@ __global__ void __launch_bounds__(256, 2) k_gemm_ts(int M, int N, int K, const d
                 for (int b = 0; b < NB; ++b)
                     acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[a], bf[b], acc[a][b], 0, 0, 0);
         }
-        if (more) store(buf ^ 1);
+    };
+    if constexpr (PF2) {
+        // two stages of register prefetch in two register sets used in turn
+        // (twice the loads in flight: the 32-column products stream C at
+        // ~4.5 TB/s with 8 flop a byte); same k order, same bits
+        double xa[2][8], xb[2][NB];
+        // branch-free loads (clamped addresses; out-of-range values times a 0/1
+        // factor -- finite operands, so exactly +-0, which adds nothing: a select
+        // on the loaded value makes hipcc branch around each load and drain
+        // vmcnt per element), issued every step: the compiler then counts them
+        // instead of draining the queue at each LDS store
+        auto load_to = [&](double (&ta)[8], double (&tb)[NB], int k0) {
+            const int k = k0 + lk;
+            const bool kin = k < kend;
+            const size_t kc = (size_t)min(k, K - 1);
+#pragma unroll
+            for (int p = 0; p < 8; ++p) {
+                const int i = i0 + lr + 16 * p;
+                const double f = (kin && i < M) ? 1.0 : 0.0;
+                ta[p] = A[kc + (size_t)min(i, M - 1) * lda] * f;
+            }
+#pragma unroll
+            for (int p = 0; p < NB; ++p) {
+                const int j = j0 + lr + 16 * p;
+                const double f = (kin && j < N) ? 1.0 : 0.0;
+                tb[p] = B[kc + (size_t)min(j, N - 1) * ldb] * f;
+            }
+        };
+        auto store_from = [&](const double (&ta)[8], const double (&tb)[NB], int buf) {
+#pragma unroll
+            for (int p = 0; p < 8; ++p) As[buf][lr + 16 * p][lk] = ta[p];
+#pragma unroll
+            for (int p = 0; p < NB; ++p) Bs[buf][lr + 16 * p][lk] = tb[p];
+        };
+        load_to(xa[0], xb[0], kbeg);
+        store_from(xa[0], xb[0], 0);
+        load_to(xa[1], xb[1], kbeg + TSK);
         __syncthreads();
-        buf ^= 1;
+        int buf = 0;
+        // stage k (in LDS buf) computes while set `nxt` holds stage k + TSK and
+        // set `cur` (stage k, already stored) takes stage k + 2 TSK
+        auto step = [&](int k0, double (&ca)[8], double (&cb)[NB], double (&na)[8], double (&nb)[NB]) {
+            load_to(ca, cb, k0 + 2 * TSK);   // past kend: zeros, never stored
+            mfma_stage(buf);
+            store_from(na, nb, buf ^ 1);     // past kend: zeros into the buffer no later stage reads
+            lds_barrier();   // LDS-only: the loads of stage k0 + 2 TSK stay in flight across it
+            buf ^= 1;
+        };
+        int k0 = kbeg;
+        for (; k0 + TSK < kend; k0 += 2 * TSK) {
+            step(k0, xa[0], xb[0], xa[1], xb[1]);
+            step(k0 + TSK, xa[1], xb[1], xa[0], xb[0]);
+        }
+        if (k0 < kend) step(k0, xa[0], xb[0], xa[1], xb[1]);
+    } else {
+        if (kbeg < kend) {
+            load(kbeg);
+            store(0);
+        }
+        __syncthreads();
+        int buf = 0;
+        for (int k0 = kbeg; k0 < kend; k0 += TSK) {
+            const bool more = k0 + TSK < kend;
+            if (more) load(k0 + TSK);
+            mfma_stage(buf);
+            if (more) store(buf ^ 1);
+            __syncthreads();
+            buf ^= 1;
+        }
     }
 #pragma unroll
     for (int a = 0; a < 2; ++a)
@@ -499,6 +557,7 @@ __global__ void __launch_bounds__(256, 2) k_gemm_ts(int M, int N, int K, const d
 }
 int g_gemm_ts = 8;   // k_gemm_ts: most k chunks (0: off -> the 64 x 64 split-K kernel)
 int g_gemm_ts32 = 8;   // the same for the 32-column tile (a function of K alone: shards agree)
+int g_gemm_ts_pf2 = 0;   // 32-column tile: two stages of register prefetch (same bits; knob 35)
 
 // Fixed-order split-K reduction: C = sum_{z=0..S-1} part[z] (column-major M x N),
 // z ascending; loads issued 8 at a time (S is a runtime count: one dependent
@@ -713,7 +772,10 @@ void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s) {
             st = 0;
         }
         const dim3 grid((unsigned)(tiles * S));
-        if (tnw == 32)
+        if (tnw == 32 && g_gemm_ts_pf2)
+            hipLaunchKernelGGL((k_gemm_ts<1, 32, true>), grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb,
+                               out, ldo, st, kchunk, pstride);
+        else if (tnw == 32)
             hipLaunchKernelGGL((k_gemm_ts<1, 32>), grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb, out,
                                ldo, st, kchunk, pstride);
         else if (g.tag == 1)

@@ -191,6 +191,7 @@ void launch_trsm_ru(const double *d_Z, int n, int b, const double *d_U, const do
 constexpr int kCholInvMax = 256;
 extern int g_chol_inv_waves;
 extern int g_gemm_splitk;
+extern int g_gemm_ts_pf2;   // 32-column long-K product: two stages of register prefetch
 extern int g_gemm_ts;
 extern int g_gemm_ts32;
 extern int g_gram64;

@@ -386,3 +386,22 @@ def test_c5_full_golden_and_sharded_bit_identical(gpu):
         assert np.array_equal(x.scores.view(np.uint64), y.scores.view(np.uint64))
         assert np.array_equal(x.dendro.boundary, y.dendro.boundary)
         assert np.array_equal(x.dendro.height.view(np.uint64), y.dendro.height.view(np.uint64))
+
+
+def test_gemm_ts_two_stage_prefetch_same_bits(gpu):
+    """The 32-column long-K product with two register prefetch stages (knob
+    35) keeps the k order: the whole C-space Krylov PCA (10 400 bins) gives the
+    same bits."""
+    import tadpole_amd as tp
+    from tadpole_amd.synth import synth_hic_par
+    m = synth_hic_par(10400, SEED_BASE + 81)
+    old = G.knob(35, 0)
+    try:
+        a = tp.TADpole(m, max_pcs=200)
+        G.knob(35, 1)
+        b = tp.TADpole(m, max_pcs=200)
+    finally:
+        G.knob(35, old)
+    assert a.timings_ms[16] > 0          # the Krylov path ran
+    assert np.array_equal(a.scores.view(np.uint64), b.scores.view(np.uint64))
+    assert np.array_equal(a.dendro.height.view(np.uint64), b.dendro.height.view(np.uint64))
