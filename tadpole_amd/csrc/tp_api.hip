@@ -696,12 +696,14 @@ static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_cl
     o.n_good = n;
     progress.set(1);
     if (n < 3) fail(TP_ERR_NO_BSTICK, "fewer than 3 good bins after masking");
-    double *X = c.buf[S_X].as<double>((size_t)n * n);
     double *m = c.buf[S_COLMEAN].as<double>(n);
     // the gather also scans X for the exact int8 X'X (integrality, maximum,
-    // S_jj) and builds its 2-slice image: no separate passes over X for them
+    // S_jj) and builds its 2-slice image: no separate passes over X for them,
+    // and X itself is written only if the fp64 product turns out to be needed
+    // (non-integer counts: cor_product gathers it then)
     const bool prep = g_xtx_fused && g_xtx_int8 && n >= 1024 && n <= 130000;
     GatherStats gs{};
+    double *X = nullptr;
     if (prep) {
         const int Kp = xtx_kp(n), Np = (n + 127) / 128 * 128;
         char *gb = c.buf[S_GSTAT].as<char>((size_t)n * 24 + 256);
@@ -709,9 +711,10 @@ static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_cl
         long long *css = (long long *)(cmax + n);
         int *cbad = (int *)(css + n);
         int8_t *sl = xtx_slice_buf(c, n, 2);
-        launch_gather_prep(d_M, n0, d_good, n, X, m, cmax, cbad, css, sl, Kp, Np, s);
-        gs = GatherStats{cmax, cbad, css, true};
+        launch_gather_prep(d_M, n0, d_good, n, nullptr, m, cmax, cbad, css, sl, Kp, Np, s);
+        gs = GatherStats{cmax, cbad, css, true, d_M, n0, d_good};
     } else {
+        X = c.buf[S_X].as<double>((size_t)n * n);
         launch_gather_colmean(d_M, n0, d_good, n, X, m, s);
     }
     trace_mark(s, "mask");

@@ -357,6 +357,11 @@ struct GatherStats {
     const int *cbad;
     const long long *css;
     bool slices2;   // the gather wrote the 2-slice int8 image
+    // the gather's source, for X on demand (the gather skipped writing it):
+    // cor_product runs k_gather_colmean into S_X when the fp64 product is needed
+    const double *M = nullptr;
+    int n0 = 0;
+    const int *good = nullptr;
 };
 // C5 row-sharded C (one matrix over R ranks on the Krylov path): shard r owns
 // columns [rb[r], rb[r+1]) of [C | m | 1] (rb: rows_gemm_sharded's row plan

@@ -244,7 +244,9 @@ void launch_gather_colmean(const double *d_M, int n0, const int *d_good, int n, 
 // not non-negative integers, the exact sum of squares (int64: S_jj of X'X, for
 // sd), and -- speculatively, for counts below 2^14 -- the two 7-bit int8
 // slices (column j of slice s at sl + s Np Kp + j Kp, rows zero-padded to Kp;
-// grid over Np columns: the padding columns get zero slices).
+// grid over Np columns: the padding columns get zero slices).  X may be null:
+// the int8 X'X never reads it, so the pipeline writes X only if the counts turn
+// out not to be integers (k_gather_colmean, same column means).
 __global__ void __launch_bounds__(256) k_gather_prep(const double *M, int n0, const int *good, int n, double *X,
                                                      double *cm, double *cmax, int *cbad, long long *css,
                                                      int8_t *sl, int Kp, int Np) {
@@ -260,13 +262,13 @@ __global__ void __launch_bounds__(256) k_gather_prep(const double *M, int n0, co
         return;
     }
     const double *src = M + (size_t)good[j] * n0;
-    double *dst = X + (size_t)j * n;
+    double *dst = X ? X + (size_t)j * n : nullptr;   // X == nullptr: not written (int8 path)
     int8_t *s0 = sl + (size_t)j * Kp, *s1 = s0 + slice;
     double hi = 0.0, lo = 0.0, mx = 0.0;
     long long ss = 0;
     bool bad = false;
     auto take = [&](int a, double v) {
-        dst[a] = v;
+        if (dst) dst[a] = v;
         dd_add_d(hi, lo, v);
         const bool ok = v >= 0.0 && v == floor(v) && v < 2147483648.0;
         bad |= !ok;

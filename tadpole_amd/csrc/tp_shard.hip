@@ -356,6 +356,12 @@ void cor_product(Ctx &c, const double *X, int n, const double *m, const GatherSt
     int ns = -1;
     if (gs && g_xtx_fused && n >= 1024) ns = xtx_int_slices_cols(c, gs->cmax, gs->cbad, n);
     if (!(ns == 1 || ns == 2)) {
+        if (!X) {   // the gather skipped X (int8 path expected): gather it now, same means
+            if (!gs || !gs->M) fail(TP_ERR_ARG, "cor_product: no X and no gather source");
+            double *Xg = c.buf[S_X].as<double>((size_t)n * n);
+            launch_gather_colmean(gs->M, gs->n0, gs->good, n, Xg, const_cast<double *>(m), s);
+            X = Xg;
+        }
         if (!S) S = c.buf[S_S].as<double>((size_t)n * n);
         kprof_begin(c, K_COR_GEMM);
         xtx_product(c, X, n, S);
@@ -365,6 +371,7 @@ void cor_product(Ctx &c, const double *X, int n, const double *m, const GatherSt
     }
     c.last_xtx_ns = ns;
     // the gather's 2-slice image serves ns = 1 too (its slice 1 is zero then)
+    if (!gs->slices2 && !X) fail(TP_ERR_ARG, "cor_product: no X and no int8 image");
     const int8_t *sl = gs->slices2 ? xtx_slice_buf(c, n, 2) : xtx_slices(c, X, n, ns);
     launch_cor_sd_ss(gs->css, m, n, sd, s);
     kprof_begin(c, K_COR_GEMM);

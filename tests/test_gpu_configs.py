@@ -405,3 +405,26 @@ def test_gemm_ts_two_stage_prefetch_same_bits(gpu):
     assert a.timings_ms[16] > 0          # the Krylov path ran
     assert np.array_equal(a.scores.view(np.uint64), b.scores.view(np.uint64))
     assert np.array_equal(a.dendro.height.view(np.uint64), b.dendro.height.view(np.uint64))
+
+
+def test_non_integer_counts_gather_x_on_demand(gpu):
+    """The fused gather writes X only for the fp64 correlation product: a
+    balanced (non-integer) matrix above the int8 size threshold takes the fp64
+    path through the on-demand gather and gives the bits of the plain gather
+    (knob 5 = 0: no int8 prep at all), and the oracle's TADs."""
+    import tadpole_amd as tp
+    m = synth_hic(1500, SEED_BASE + 83).astype(np.float64)
+    rng = np.random.default_rng(5)
+    w = rng.uniform(0.5, 1.5, m.shape[0])
+    m = m * w[:, None] * w[None, :]                     # balanced-style weights: not integers
+    a = tp.TADpole(m, max_pcs=100)
+    old = G.knob(5, 0)
+    try:
+        b = tp.TADpole(m, max_pcs=100)
+    finally:
+        G.knob(5, old)
+    assert np.array_equal(a.scores.view(np.uint64), b.scores.view(np.uint64))
+    ref = O.tadpole(m, max_pcs=100)
+    assert (a.n_pcs, a.optimal_n_clusters) == (ref.n_pcs, ref.optimal_n_clusters)
+    for q, v in ref.clusters.items():
+        assert np.array_equal(a.clusters[str(q)], v), q
