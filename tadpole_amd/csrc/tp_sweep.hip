@@ -299,40 +299,16 @@ __device__ __forceinline__ double ward_part(const double (&sa)[NS], double fa, c
 // barrier with both waves choosing was slower: B's prefetch of a2's rows then
 // has only B's own choice to hide behind, and HBM latency shows.)  Mailbox
 // words are written before one barrier and read after it.
-// Build switches (A/B builds of the merge loop; the product uses the defaults):
-// TP_CONISS_BMI    block argmin positions kept in registers beside the block
-//                  minima (the speculative argmin reads no block of costs)
-// TP_CONISS_LDSBAR LDS-only barriers X and Y (global loads stay in flight)
-// TP_CONISS_GLBPF  costs-in-global variant: the next merge's three cost blocks
-//                  loaded right after the choice, patched at the merge's start
-#ifndef TP_CONISS_BMI
-#define TP_CONISS_BMI 0
-#endif
-#ifndef TP_CONISS_LDSBAR
-#define TP_CONISS_LDSBAR 0
-#endif
-#ifndef TP_CONISS_GLBPF
-#define TP_CONISS_GLBPF 0
-#endif
-// TP_CONISS_EPF    the sums wave prefetches a2's rows before barrier X when the
-//                  structure wave has already published them (sequence word
-//                  mb_d[3]), instead of after X
-#ifndef TP_CONISS_EPF
-#define TP_CONISS_EPF 0
-#endif
+// Variants built and measured slower (in git history): block
+// argmin positions in registers, LDS-only barriers, the global variant's next
+// cost blocks prefetched after the choice, a2's rows prefetched before X.
+// Build switch:
 // TP_CONISS_RECB   global variant: the sums wave keeps the merge records (a, b,
 //                  cost, height) of 64 merges in registers (lane s % 64) and
 //                  stores them once per 64 merges, instead of four stores a merge
 #ifndef TP_CONISS_RECB
 #define TP_CONISS_RECB 1
 #endif
-__device__ __forceinline__ void coniss_bar() {
-#if TP_CONISS_LDSBAR
-    lds_barrier();
-#else
-    __syncthreads();
-#endif
-}
 template <bool STAMPS, int NS, int BS, bool GLB, bool LU = false>
 __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, double *lds, double *mb_d,
                                              int4 *mb_i) {
@@ -348,13 +324,10 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
     const int ti = blockIdx.x;
     const int i = sd.tree0 + ti + 1;
     constexpr int ld = NS * 64;
-    constexpr bool kBmi = TP_CONISS_BMI != 0;
-    constexpr bool kPf = GLB && TP_CONISS_GLBPF != 0;
-    constexpr bool kEpf = TP_CONISS_EPF != 0;
-    // measured: 24.3k bins (global variant) 46.8 -> 46.1 ms, C3 (LDS) 9.90 -> 10.09 ms
-    constexpr bool kRecb = GLB && TP_CONISS_RECB != 0;
     const int lane = threadIdx.x & 63;
     const bool waveA = __builtin_amdgcn_readfirstlane((int)threadIdx.x) < 64;   // wave-uniform: a scalar branch
+    // measured: 24.3k bins (global variant) 46.8 -> 46.1 ms, C3 (LDS) 9.90 -> 10.09 ms
+    constexpr bool kRecb = GLB && TP_CONISS_RECB != 0;
     const int nbk = (n + 63) / 64;
     const double QNAN = __longlong_as_double(0x7FF8000000000000LL);
     // GLB (n above the LDS capacity): costs stay in this tree's slice of cost0
@@ -401,9 +374,6 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
     const double *c0 = cost0 + (size_t)ti * cst;
 
     double bmr[BS];
-    // bmi: the leftmost position holding each block's minimum (kept with bmr,
-    // so the speculative argmin reads no block of costs)
-    int bmi[BS];
     auto argmin_pos = [&](double vmin) -> int {
         if (isnan(vmin)) return -1;
         int blk = 0;
@@ -496,22 +466,11 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
         nv = c2 ? cr : nv;
     };
     Mg cur = {0, 0, 0, -1, -1, -1, -1, -1};
-    // GLB: the next merge's three touched cost blocks, loaded one merge ahead
-    double nva = QNAN, nvb = QNAN, nvl = QNAN;
-    auto prefetch_blocks = [&](const Mg &m) {
-        const int ba = m.a >> 6, bb = (m.ea + 1) >> 6, bl = m.ls >= 0 ? (m.ls >> 6) : ba;
-        nva = cost[ba * 64 + lane];
-        nvb = cost[bb * 64 + lane];
-        nvl = cost[bl * 64 + lane];
-    };
     double c = 0.0, pcl = QNAN, pcr = QNAN;
     int pls = DC, pa_ = DC;   // A: where the previous merge's new costs go (applied at the next merge's start)
     if (waveA) {
 #pragma unroll
-        for (int q = 0; q < BS; ++q) {
-            bmr[q] = QNAN;
-            bmi[q] = DC;
-        }
+        for (int q = 0; q < BS; ++q) bmr[q] = QNAN;
         for (int bk = 0; bk < nbk; ++bk) {
             const int p = bk * 64 + lane;
             const double cp = c0[p];
@@ -525,26 +484,19 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
                 rn.set(DL + lane, -1);
             }
             const double m = wave_min(cp);
-            const unsigned long long mm = __ballot(cp == m);
-            const int mpos = mm ? bk * 64 + (int)__builtin_ctzll(mm) : DC;
             if (lane == (bk & 63)) {
 #pragma unroll
                 for (int q = 0; q < BS; ++q)
-                    if (q == (bk >> 6)) {
-                        bmr[q] = m;
-                        bmi[q] = mpos;
-                    }
+                    if (q == (bk >> 6)) bmr[q] = m;
             }
         }
         c = gmin();
         cur = merge_at(argmin_pos(c));
-        if constexpr (kPf) prefetch_blocks(cur);
         const Rec rc = make_rec(cur, 0);
         mb_i[0] = rc.x;
         mb_i[1] = rc.y;
         mb_i[2] = rc.z;
         mb_d[2] = c;
-        mb_d[3] = -1.0;
     }
     __syncthreads();
     // B's registers
@@ -590,25 +542,9 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
             // refresh the three touched blocks and, concurrently, the minimum of
             // the untouched ones: four interleaved wave reductions
             const int ba = a >> 6, bb = b >> 6, bl = ls >= 0 ? (ls >> 6) : ba;
-            double va, vb, vl;
-            if constexpr (kPf) {
-                // the three blocks were loaded after the previous merge's choice
-                // (still in flight across barrier Y: LDS-only barriers); patch
-                // the positions this merge's writes above changed
-                auto patch = [&](double v, int blk) {
-                    const int p = blk * 64 + lane;
-                    v = p == pls ? pcl : v;
-                    v = p == pa_ ? pcr : v;
-                    return (p == b || p == a || (ls >= 0 && p == ls)) ? QNAN : v;
-                };
-                va = patch(nva, ba);
-                vb = patch(nvb, bb);
-                vl = patch(nvl, bl);
-            } else {
-                va = cost[ba * 64 + lane];
-                vb = cost[bb * 64 + lane];
-                vl = cost[bl * 64 + lane];
-            }
+            const double va = cost[ba * 64 + lane];
+            const double vb = cost[bb * 64 + lane];
+            const double vl = cost[bl * 64 + lane];
             double rest = QNAN;
 #pragma unroll
             for (int q = 0; q < BS; ++q) {
@@ -618,55 +554,23 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
             TP_STAMP(6);
             double ma = va, mb = vb, ml = vl, mr = rest;
             wave_min4(ma, mb, ml, mr);
-            int a2 = -1;
-            double v2;
-            if constexpr (kBmi) {
-                // the refreshed blocks' leftmost minimum positions (NaN block: none)
-                const unsigned long long xa = __ballot(va == ma), xb = __ballot(vb == mb), xl = __ballot(vl == ml);
-                const int pma = xa ? ba * 64 + (int)__builtin_ctzll(xa) : DC;
-                const int pmb = xb ? bb * 64 + (int)__builtin_ctzll(xb) : DC;
-                const int pml = xl ? bl * 64 + (int)__builtin_ctzll(xl) : DC;
 #pragma unroll
-                for (int q = 0; q < BS; ++q) {
-                    const bool ia = lane == (ba & 63) && q == (ba >> 6);
-                    const bool ib = lane == (bb & 63) && q == (bb >> 6);
-                    const bool il = lane == (bl & 63) && q == (bl >> 6);
-                    bmr[q] = ia ? ma : bmr[q];
-                    bmi[q] = ia ? pma : bmi[q];
-                    bmr[q] = ib ? mb : bmr[q];
-                    bmi[q] = ib ? pmb : bmi[q];
-                    bmr[q] = il ? ml : bmr[q];
-                    bmi[q] = il ? pml : bmi[q];
-                }
-                v2 = vmin(vmin(mr, ma), vmin(mb, ml));
-                // leftmost position holding v2: the lowest block whose minimum is
-                // v2, then that block's leftmost minimum position, kept in bmi (v2
-                // NaN: no ballot matches, a2 = -1)
-#pragma unroll
-                for (int q = BS - 1; q >= 0; --q) {
-                    const unsigned long long m = __ballot(bmr[q] == v2);
-                    const int pq = __builtin_amdgcn_readlane(bmi[q], m ? (int)__builtin_ctzll(m) : 0);
-                    a2 = m ? pq : a2;
-                }
-            } else {
-#pragma unroll
-                for (int q = 0; q < BS; ++q) {
-                    bmr[q] = (lane == (ba & 63) && q == (ba >> 6)) ? ma : bmr[q];
-                    bmr[q] = (lane == (bb & 63) && q == (bb >> 6)) ? mb : bmr[q];
-                    bmr[q] = (lane == (bl & 63) && q == (bl >> 6)) ? ml : bmr[q];
-                }
-                v2 = vmin(vmin(mr, ma), vmin(mb, ml));
-                // leftmost position holding v2: its block from the block minima,
-                // then the block's words (v2 NaN: no ballot matches, a2 = -1)
-                int blk = 0;
-#pragma unroll
-                for (int q = BS - 1; q >= 0; --q) {
-                    const unsigned long long m = __ballot(bmr[q] == v2);
-                    blk = m ? 64 * q + (int)__builtin_ctzll(m) : blk;
-                }
-                const unsigned long long mv = __ballot(cost[blk * 64 + lane] == v2);
-                a2 = mv ? blk * 64 + (int)__builtin_ctzll(mv) : -1;
+            for (int q = 0; q < BS; ++q) {
+                bmr[q] = (lane == (ba & 63) && q == (ba >> 6)) ? ma : bmr[q];
+                bmr[q] = (lane == (bb & 63) && q == (bb >> 6)) ? mb : bmr[q];
+                bmr[q] = (lane == (bl & 63) && q == (bl >> 6)) ? ml : bmr[q];
             }
+            const double v2 = vmin(vmin(mr, ma), vmin(mb, ml));
+            // leftmost position holding v2: its block from the block minima, then
+            // the block's words (v2 NaN: no ballot matches, a2 = -1)
+            int blk = 0;
+#pragma unroll
+            for (int q = BS - 1; q >= 0; --q) {
+                const unsigned long long m = __ballot(bmr[q] == v2);
+                blk = m ? 64 * q + (int)__builtin_ctzll(m) : blk;
+            }
+            const unsigned long long mv = __ballot(cost[blk * 64 + lane] == v2);
+            const int a2 = mv ? blk * 64 + (int)__builtin_ctzll(mv) : -1;
             TP_STAMP(7);
             // ---- the three possible next merges (post-update links); a2's
             //      clusters go to B at once (its row prefetch starts before X)
@@ -680,9 +584,6 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
                 mb_i[3] = make_int4(rowc(m0.a, m0.ea == m0.a), rowc(bs2, m0.eb == bs2),
                                     m0.ls >= 0 ? rowc(m0.ls, m0.ls == m0.a - 1) : -1,
                                     m0.r >= 0 ? rowc(m0.r, m0.er == m0.r) : -1);
-                // after the rows (LDS operations of one wave complete in order):
-                // a reader that sees s also sees this merge's rows
-                if constexpr (kEpf) mb_d[3] = (double)s;
             }
             Mg m1;   // ls | m
             m1.a = ls; m1.ea = a - 1; m1.eb = eb; m1.ls = cur.ll; m1.r = r; m1.er = er;
@@ -695,7 +596,7 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
             m2.ll = cur.ll;
             m2.rre = m2rrev;
             TP_STAMP(0);
-            coniss_bar();   // X (LDS-only by default: global loads stay in flight)
+            __syncthreads();   // X
             TP_STAMP(1);
             // ---- the choice
             const double cl = mb_d[0], cr = mb_d[1];
@@ -713,7 +614,6 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
             cur.ll = sel(m0.ll, m1.ll, m2.ll);
             cur.rre = sel(m0.rre, m1.rre, m2.rre);
             c = nv;
-            if constexpr (kPf) prefetch_blocks(cur);
             {
                 const Rec rc = make_rec(cur, c2 ? 2 : (c1 ? 1 : 0));
                 mb_i[0] = rc.x;
@@ -723,38 +623,19 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
             }
             // block minima absorb the new costs now (the LDS words follow at the
             // next merge's start, before its refresh reads them)
-            if constexpr (kBmi) {
 #pragma unroll
-                for (int q = 0; q < BS; ++q) {
-                    // (value, position) lexicographic minimum: the block keeps its
-                    // leftmost minimum position (a NaN cost -- no right neighbour
-                    // -- changes nothing; a NaN block minimum takes the new cost)
-                    const bool ia = lane == (ba & 63) && q == (ba >> 6);
-                    const bool tr =
-                        ia && ((cr < bmr[q]) || (cr == bmr[q] && a < bmi[q]) || (bmr[q] != bmr[q] && cr == cr));
-                    bmr[q] = tr ? cr : bmr[q];
-                    bmi[q] = tr ? a : bmi[q];
-                    const bool il = ls >= 0 && lane == (bl & 63) && q == (bl >> 6);
-                    const bool tl =
-                        il && ((cl < bmr[q]) || (cl == bmr[q] && ls < bmi[q]) || (bmr[q] != bmr[q] && cl == cl));
-                    bmr[q] = tl ? cl : bmr[q];
-                    bmi[q] = tl ? ls : bmi[q];
-                }
-            } else {
-#pragma unroll
-                for (int q = 0; q < BS; ++q) {
-                    const double tr = vmin(bmr[q], cr);
-                    bmr[q] = (lane == (ba & 63) && q == (ba >> 6)) ? tr : bmr[q];
-                    const double tl = vmin(bmr[q], cl);
-                    bmr[q] = (ls >= 0 && lane == (bl & 63) && q == (bl >> 6)) ? tl : bmr[q];
-                }
+            for (int q = 0; q < BS; ++q) {
+                const double tr = vmin(bmr[q], cr);
+                bmr[q] = (lane == (ba & 63) && q == (ba >> 6)) ? tr : bmr[q];
+                const double tl = vmin(bmr[q], cl);
+                bmr[q] = (ls >= 0 && lane == (bl & 63) && q == (bl >> 6)) ? tl : bmr[q];
             }
             pcl = cl;
             pcr = cr;
             pls = ls >= 0 ? ls : DC;
             pa_ = a;
             TP_STAMP(2);
-            coniss_bar();   // Y
+            __syncthreads();   // Y
             TP_STAMP(3);
         } else {
             // ---- this merge's rows from the previous merge's prefetch
@@ -810,15 +691,6 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
                 asm volatile("" ::"v"(z));
             }
             TP_STAMP(1);
-            // a2's rows: if A has already published them for this merge, their
-            // loads go out now (the Ward work below hides the LDS round trip)
-            // rather than after X -- ~a Ward step and a barrier earlier
-            double seqv = -2.0;
-            int4 p0e = make_int4(0, 0, 0, 0);
-            if constexpr (kEpf) {
-                seqv = mb_d[3];
-                p0e = mb_i[3];
-            }
             const double fm = (double)nm, fl = (double)nl, fr = (double)nr;
             double ul = ward_part<NS>(sl, fl, sm, fm, last_in);
             double ur = ward_part<NS>(sm, fm, sr, fr, last_in);
@@ -831,19 +703,6 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
             h = h + cc;
             mb_d[0] = cl;
             mb_d[1] = cr;
-            bool early = false;
-            if constexpr (kEpf) {
-                if (seqv == (double)s) {
-                    load_row(pa, p0e.x);
-                    load_row(pb, p0e.y);
-                    load_row(pl, p0e.z >= 0 ? p0e.z : p0e.x);
-                    load_row(pr, p0e.w >= 0 ? p0e.w : p0e.x);
-                    ls2p = p0e.z;
-                    r2p = p0e.w;
-                    aprev = a_;
-                    early = true;
-                }
-            }
             // every lane stores the same words (one request each; no exec mask)
             if constexpr (kRecb) {
                 const bool mine = lane == (s & 63);
@@ -867,21 +726,19 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
                 height[s] = h;
             }
             TP_STAMP(2);
-            coniss_bar();   // X (LDS-only by default: global loads stay in flight)
+            __syncthreads();   // X
             TP_STAMP(3);
-            // ---- prefetch a2's rows for the next merge (unless done before X)
-            if (!early) {
-                const int4 p0 = mb_i[3];
-                load_row(pa, p0.x);
-                load_row(pb, p0.y);
-                load_row(pl, p0.z >= 0 ? p0.z : p0.x);
-                load_row(pr, p0.w >= 0 ? p0.w : p0.x);
-                ls2p = p0.z;
-                r2p = p0.w;
-                aprev = a_;
-            }
+            // ---- prefetch a2's rows for the next merge
+            const int4 p0 = mb_i[3];
+            load_row(pa, p0.x);
+            load_row(pb, p0.y);
+            load_row(pl, p0.z >= 0 ? p0.z : p0.x);
+            load_row(pr, p0.w >= 0 ? p0.w : p0.x);
+            ls2p = p0.z;
+            r2p = p0.w;
+            aprev = a_;
             TP_STAMP(6);
-            coniss_bar();   // Y
+            __syncthreads();   // Y
             TP_STAMP(7);
         }
     }
