@@ -740,7 +740,10 @@ def main():
                             for q in kern},
                 "xtx": {"int8_slices": ns,
                         "fp64_equivalent_tflops": (round(share * float(n) ** 3 / (tm[5] * 1e-3) / 1e12, 2)
-                                                   if tm[5] > 0 else None)},
+                                                   if tm[5] > 0 else None),
+                        "note": ("xtx_gemm counts the ns^2 slice products whole (dense-equivalent int8 ops); "
+                                 "the kernel skips the high slice's all-zero 128x64 blocks (raw counts >= 128 "
+                                 "sit near the diagonal), so it executes fewer") if ns == 2 else None},
                 "stages_ms": {"mask": round(tm[0], 3), "cor": round(tm[1], 3), "pca": round(tm[2], 3),
                               "sweep": round(tm[3], 3), "total": round(tm[4], 3)},
                 "pca": {"path": "block Krylov (G never formed)" if krylov_steps else "G = Xc'Xc + subspace iteration",
