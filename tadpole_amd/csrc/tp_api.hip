@@ -292,6 +292,7 @@ Ctx::~Ctx() {
         (void)hipEventDestroy(join_ev);
     }
     for (auto e : evpool) (void)hipEventDestroy(e);
+    if (sync_ev) (void)hipEventDestroy(sync_ev);
     for (auto e : ring_ev)
         if (e) (void)hipEventDestroy(e);
     if (owns_stream) (void)hipStreamDestroy(stream);
@@ -572,7 +573,6 @@ static SweepOut run_sweep(Ctx &c, const double *d_Pt, int n, int k, int min_clus
         }
         h_sc = sc;
     }
-    if (scores) memcpy(scores, h_sc, sc_bytes);
     select_params(h_sc, k, o.w, &o.n_pcs, &o.n_clusters);
     const int t = o.n_pcs - 1;
     {
@@ -596,6 +596,9 @@ static SweepOut run_sweep(Ctx &c, const double *d_Pt, int n, int k, int min_clus
         TP_HIP(hipMemcpyAsync(all_cost->data(), cost, rec * 8, hipMemcpyDeviceToHost, s));
         TP_HIP(hipMemcpyAsync(all_h->data(), hgt, rec * 8, hipMemcpyDeviceToHost, s));
     }
+    // the caller's score matrix is filled while the chosen tree's records are
+    // in flight (different parts of the pinned staging)
+    if (scores) memcpy(scores, h_sc, sc_bytes);
     stream_sync(c, s);
     if (merge) encode_merge(pa, pb, n, merge);
     if (height) memcpy(height, ph, (n - 1) * sizeof(double));

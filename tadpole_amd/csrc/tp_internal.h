@@ -77,6 +77,7 @@ struct Ctx {
     void *host_pinned = nullptr;    // small pinned staging area
     size_t host_pinned_bytes = 0;
     hipEvent_t ring_ev[4] = {};     // tp_read_tsv_dev: one event per staging-ring slot
+    hipEvent_t sync_ev = nullptr;   // event_sync: a read-back point with more work queued behind it
     int *progress = nullptr;        // tp_progress_attach: host word, the pipeline's stage (1 mask .. 4 done)
     void *pinned(size_t b);
 };
@@ -311,6 +312,12 @@ void comm_destroy(Ctx &c);
 // host waits of a call that may be sharded: bounded and abort-on-failure with a
 // live communicator (see tp_shard.hip), hipStreamSynchronize otherwise
 void stream_sync(Ctx &c, hipStream_t s);
+// Record the context's sync event on s (behind the work queued so far); then
+// event_sync waits for that point only, so work queued after the record keeps
+// the device busy while the host reads the results (sharded: same watchdog as
+// stream_sync)
+void event_mark(Ctx &c, hipStream_t s);
+void event_sync(Ctx &c);
 void comm_abort(Ctx &c);
 extern int g_shard_inject;   // test hook: the next N sharded waits fail as device errors
 int shard_count(const Ctx &c);

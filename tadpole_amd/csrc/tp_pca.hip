@@ -637,14 +637,16 @@ static void krylov_topk(Ctx &c, double *C, int c_col0, const double *mext, int n
         TP_HIP(hipGetLastError());
         double *pn = (double *)c.pinned((size_t)k * sizeof(double));
         TP_HIP(hipMemcpyAsync(pn, resid, k * sizeof(double), hipMemcpyDeviceToHost, s));
+        event_mark(c, s);
         // scores P = Xc V = (Xc K) Y: an n x D by D x k product instead of
-        // another pass over Xc (2 n D k flops, not 2 n^2 k), queued before the
-        // residual check so the device has work while the host waits for it
-        // (recomputed if the check extends the space)
+        // another pass over Xc (2 n D k flops, not 2 n^2 k), queued behind the
+        // residual read-back so the device has work while the host checks it
+        // (recomputed if the check extends the space); the host waits for the
+        // read-back only, and queues the sweep while the product runs
         GemmArgs pg{n, k, D, XK, n, false, Vs, D, P, n};
         pg.splitk = 0;
         gemm_f64(pg, c.buf[S_PARTIAL], s);
-        stream_sync(c, s);
+        event_sync(c);
         memcpy(h_res.data(), pn, k * sizeof(double));
         const double th1 = std::fabs(h_theta[bs - 1]);
         double worst = 0.0;

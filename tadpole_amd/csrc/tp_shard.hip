@@ -181,6 +181,38 @@ void stream_sync(Ctx &c, hipStream_t s) {
     }
 }
 
+void event_mark(Ctx &c, hipStream_t s) {
+    if (!c.sync_ev) TP_HIP(hipEventCreateWithFlags(&c.sync_ev, hipEventDisableTiming));
+    TP_HIP(hipEventRecord(c.sync_ev, s));
+}
+
+void event_sync(Ctx &c) {
+    if (!(c.shard.active && c.shard.comm)) {
+        TP_HIP(hipEventSynchronize(c.sync_ev));
+        return;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const hipError_t e = hipEventQuery(c.sync_ev);
+        if (e == hipSuccess) return;
+        if (e != hipErrorNotReady) {
+            comm_abort(c);
+            TP_HIP(e);
+        }
+        ncclResult_t ae = ncclSuccess;
+        if (rccl().async_err((ncclComm_t)c.shard.comm, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
+            comm_abort(c);
+            fail(TP_ERR_HIP, std::string("RCCL asynchronous error in a sharded call: ") + rccl().errstr(ae) +
+                                 " (communicator aborted)");
+        }
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > shard_timeout_s()) {
+            comm_abort(c);
+            fail(TP_ERR_HIP, "sharded call timed out waiting for its peers (TP_SHARD_TIMEOUT_S); communicator aborted");
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+}
+
 // -------------------------------------------------------------- planning
 int shard_count(const Ctx &c) {
     if (!c.shard.active) return 1;
