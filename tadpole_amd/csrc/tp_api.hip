@@ -1263,6 +1263,56 @@ void tp_debug_chol(const double *W, const int *b, const double *rel, const int *
     });
 }
 
+/* Out = A'B (A: K x M col-major, B: K x N, N = 64, K >= 64) by the
+ * int8-digit product (rows_gemm_sharded's path, rank-1 epilogue against row
+ * vrow = M - 1) into O8 and by the fp64 k_gemm_ts path into O64 (M - 1 rows
+ * each, ld M - 1); ms[0..1] the two products' device time. */
+void tp_debug_prod_i8(const double *A, const int *K, const int *M, const double *B, const int *N, double *O8,
+                      double *O64, double *ms, int *status) {
+    guarded(status, [&] {
+        Ctx &c = ctx_for(0);
+        hipStream_t s = c.cur;
+        const int k = *K, m = *M, nn = *N;
+        if (!prod_i8_ok(k, nn) || m < 2) fail(TP_ERR_ARG, "prod_i8: N must be 64 and K >= 64");
+        double *dA = c.buf[S_C].as<double>((size_t)k * m);
+        double *dB = c.buf[S_Q].as<double>((size_t)k * nn);
+        double *dO = c.buf[S_Z].as<double>(2 * (size_t)(m - 1) * nn);
+        TP_HIP(hipMemcpyAsync(dA, A, (size_t)k * m * 8, hipMemcpyHostToDevice, s));
+        TP_HIP(hipMemcpyAsync(dB, B, (size_t)k * nn * 8, hipMemcpyHostToDevice, s));
+        ProdDigits pd;
+        prod_digits_build(c, dA, k, k, m, 0, pd);
+        const R1 r1{m - 1, nullptr, m - 1};
+        hipEvent_t e0, e1, e2;
+        TP_HIP(hipEventCreate(&e0));
+        TP_HIP(hipEventCreate(&e1));
+        TP_HIP(hipEventCreate(&e2));
+        float t8 = 0, t64 = 0;
+        for (int r = 0; r < 4; ++r) {
+            TP_HIP(hipEventRecord(e0, s));
+            rows_gemm_sharded(c, dA, k, m, dB, k, nn, k, dO, 0, 1, &r1, 0, &pd);
+            TP_HIP(hipEventRecord(e1, s));
+            rows_gemm_sharded(c, dA, k, m, dB, k, nn, k, dO + (size_t)(m - 1) * nn, 0, 1, &r1, 0, nullptr);
+            TP_HIP(hipEventRecord(e2, s));
+            TP_HIP(hipEventSynchronize(e2));
+            float a = 0, b = 0;
+            TP_HIP(hipEventElapsedTime(&a, e0, e1));
+            TP_HIP(hipEventElapsedTime(&b, e1, e2));
+            if (r) {   // the first round loads the code objects
+                t8 += a;
+                t64 += b;
+            }
+        }
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        (void)hipEventDestroy(e2);
+        ms[0] = t8 / 3;
+        ms[1] = t64 / 3;
+        TP_HIP(hipMemcpyAsync(O8, dO, (size_t)(m - 1) * nn * 8, hipMemcpyDeviceToHost, s));
+        TP_HIP(hipMemcpyAsync(O64, dO + (size_t)(m - 1) * nn, (size_t)(m - 1) * nn * 8, hipMemcpyDeviceToHost, s));
+        TP_HIP(hipStreamSynchronize(s));
+    });
+}
+
 /* CholQR kernels for b <= 256 on Z = I: k_chol_inv + k_trsm_frag give
  * Y = U^{-1} (W = U'U, S-scaled, + rel on the scaled diagonal); diag[b] =
  * diag(U).  ms[0] chol kernel (the product's choice of waves), ms[1] info,
@@ -1590,7 +1640,8 @@ extern "C" {
  * Krylov CGS2's first pass against the last two blocks only (0: against every block), 29 CholQR
  * Gram matrices of 64-column blocks by k_gram64 (0: the split-K GEMM; same bits), 30 the next N
  * sharded waits with a live communicator fail as device errors (failure-containment tests), 31 the
- * bins from which knob 20 = -1 (default) takes the Krylov space of C. */
+ * bins from which knob 20 = -1 (default) takes the Krylov space of C, ..., 36 the Krylov products with
+ * C on the int8 MFMA from 7-digit images (0: the fp64 k_gemm_ts). */
 void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
     guarded(status, [&] {
         int *p = nullptr;
@@ -1630,6 +1681,7 @@ void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
         case 33: p = &g_ckry_local; break;
         case 34: p = &g_xtx_nz; break;
         case 35: p = &g_gemm_ts_pf2; break;
+        case 36: p = &g_prod_i8; break;
         default: fail(TP_ERR_ARG, "unknown knob");
         }
         if (*which == 3 && *value != 16 && *value != 32) fail(TP_ERR_ARG, "stage depth must be 16 or 32");

@@ -633,6 +633,23 @@ void launch_r1_apply(const double *T, size_t rs, size_t cs, int N, int rows, int
     TP_HIP(hipGetLastError());
 }
 
+// The two reductions above for partials made elsewhere (the int8-digit
+// products, tp_prod_i8.hip): the same kernels and summation order
+void launch_splitk_reduce_r1(const double *part, size_t stride, int S, int M, int N, int rows, int vrow,
+                             const double *u, double *C, int ldc, hipStream_t s) {
+    const size_t tot = (size_t)rows * N;
+    hipLaunchKernelGGL(k_splitk_reduce_r1<1>, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, part, stride, S, M,
+                       N, rows, vrow, u, C, ldc);
+    TP_HIP(hipGetLastError());
+}
+void launch_splitk_reduce(const double *part, size_t stride, int S, int M, int N, double *C, int ldc, int store_t,
+                          hipStream_t s) {
+    const size_t tot = (size_t)M * N;
+    hipLaunchKernelGGL(k_splitk_reduce<1>, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, part, stride, S, M, N,
+                       C, ldc, store_t, (const double *)nullptr);
+    TP_HIP(hipGetLastError());
+}
+
 // The fixed-order reduction with the affine epilogue of GemmArgs::affine:
 // C = a sum + b Y [+ c Z] (the Chebyshev step; Y, Z share C's layout)
 __global__ void __launch_bounds__(256) k_splitk_reduce_af(const double *part, size_t stride, int S, int M, int N,

@@ -110,7 +110,7 @@ enum Slot {
     S_S, S_C, S_XC, S_XCT, S_G, S_Q, S_Z, S_W, S_SMALL, S_P, S_PT,
     S_SWEEP, S_SWEEP2, S_SCORES, S_PARTIAL, S_MISC, S_SHARD, S_SHARD2, S_DEDUP,
     S_KRY, S_KRYG, S_KRYT, S_KRYV, S_KRYX, S_CMEAN, S_CHBIG, S_CHOLP, S_SMALL2, S_GSTAT, S_XTXT, S_MEXT, S_KRYA,
-    S_KRYH, S_XNZ,
+    S_KRYH, S_XNZ, S_PDIGA, S_PDIGB,
     S_NSLOT
 };
 static_assert(S_NSLOT <= (int)(sizeof(Ctx::buf) / sizeof(Ctx::buf[0])), "Ctx::buf too small for the slots");
@@ -173,6 +173,10 @@ struct GemmArgs {
 void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s);
 void launch_r1_apply(const double *T, size_t rs, size_t cs, int N, int rows, int vrow, const double *u, double *Out,
                      hipStream_t s);
+void launch_splitk_reduce_r1(const double *part, size_t stride, int S, int M, int N, int rows, int vrow,
+                             const double *u, double *C, int ldc, hipStream_t s);
+void launch_splitk_reduce(const double *part, size_t stride, int S, int M, int N, double *C, int ldc, int store_t,
+                          hipStream_t s);
 extern int g_gemm_panel;   // short-K tall-skinny 32 x 64 kernel enabled (default 1)
 extern int g_gemm_kb;      // LDS stage depth of the 64 x 64 kernel (16 / 32)
 extern int g_gemm_xcd;     // XCD-aware workgroup order of the 64 x 64 kernel (default 1)
@@ -335,8 +339,25 @@ struct R1 {
 };
 // a_col0: A points at column a_col0 of the logical K x M matrix (a rank's
 // column slab of C: its shard's rows are the only ones it reads)
+// int8-digit image of A's columns for the long-K products (tp_prod_i8.hip):
+// columns [col0, col0 + cols) of the logical A, digit s of local column i at
+// d + s slice + i Kp, its scale 2^(e - 54) at rs[i]
+struct ProdDigits {
+    const int8_t *d = nullptr;
+    const double *rs = nullptr;
+    size_t slice = 0;
+    int Kp = 0, col0 = 0, cols = 0;
+};
+extern int g_prod_i8;
+bool prod_i8_ok(int K, int N);
+void prod_digits_build(Ctx &c, const double *A, int lda, int K, int cols, int col0, ProdDigits &pd);
+int prod_i8_partials(Ctx &c, const ProdDigits &pd, int r0, int M, const double *B, int ldb, int N, int K,
+                     DevBuf &work, double **part);
+// pd (optional): A's digit image; the product then runs on the int8 MFMA
+// (same k chunks for every shard) when prod_i8_ok(K, N)
 void rows_gemm_sharded(Ctx &c, const double *A, int lda, int M, const double *B, int ldb, int N, int K,
-                       double *Out, int splitk_plain, int tag = 0, const R1 *r1 = nullptr, int a_col0 = 0);
+                       double *Out, int splitk_plain, int tag = 0, const R1 *r1 = nullptr, int a_col0 = 0,
+                       const ProdDigits *pd = nullptr);
 
 // exact X'X on int8 matrix cores for integer counts (tp_xtx.hip)
 extern int g_xtx_int8;
@@ -406,7 +427,7 @@ extern int g_pca_band;
 extern int g_krylov_local;   // Krylov CGS pass 0 against the last two blocks (1) or all (0)
 // false: an orthogonalisation pass broke down (the caller takes the G path)
 bool krylov_c_topk(Ctx &c, double *C, int c_col0, const double *mext, int n, int k, double *V, double *P,
-                   std::vector<double> &h_theta, PcaStats &st);
+                   std::vector<double> &h_theta, PcaStats &st, const ProdDigits *pd = nullptr);
 // d_C: n x n, with room for 2n more doubles after it (the Krylov path writes
 // m = colMeans(C) and a column of ones there); d_cmean: C's column means if the
 // caller already has them (may be d_C + n n), else computed here

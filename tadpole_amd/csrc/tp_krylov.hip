@@ -138,7 +138,7 @@ size_t ckry_partial_doubles(int n, int dmax) {
 // the small problem and the n-space check (tp_pca.hip)
 
 bool krylov_c_topk(Ctx &c, double *C, int c_col0, const double *mext, int n, int k, double *V, double *P,
-                   std::vector<double> &h_theta, PcaStats &st) {
+                   std::vector<double> &h_theta, PcaStats &st, const ProdDigits *pd) {
     hipStream_t s = c.cur;
     // blocks before the first check: D ~ 5.28 k (C3 / 10k: 33 blocks of 32 for
     // k = 200), more for the denser spectra of larger matrices
@@ -194,7 +194,7 @@ bool krylov_c_topk(Ctx &c, double *C, int c_col0, const double *mext, int n, int
             double *Kt = K + (size_t)t * np, *Pt = Pb + (size_t)t * np;
             kprof_begin(c, K_GQ_GEMM);
             const R1 r_xk{n, nullptr, n};   // Xc K_t = C K_t - 1 (m'K_t)
-            rows_gemm_sharded(c, C, n, n + 2, Kt, n, KP, n, Pt, 0, 1, &r_xk, c_col0);
+            rows_gemm_sharded(c, C, n, n + 2, Kt, n, KP, n, Pt, 0, 1, &r_xk, c_col0, pd);
             kprof_end(c, K_GQ_GEMM);
         }
         nprod = std::max(nprod, upto + 1);

@@ -512,10 +512,12 @@ void small_topk_T(Ctx &c, double *Tm, int D, int k, double *Vs, std::vector<doub
 // itself and the centring is two rank-1 corrections of an n x p block.
 // Blocks K_t (n x p) in S_KRY, G K_t in S_KRYG, T = K'GK in S_KRYT, the small
 // problem's vectors in S_KRYV.
+static int krylov_block(int k) { return g_pca_krylov_block > 0 ? g_pca_krylov_block : (k >= 128 ? 64 : 32); }
+
 static void krylov_topk(Ctx &c, double *C, int c_col0, const double *mext, int n, int k, double *V, double *P,
-                        std::vector<double> &h_theta, PcaStats &st) {
+                        std::vector<double> &h_theta, PcaStats &st, const ProdDigits *pd) {
     hipStream_t s = c.cur;
-    const int p = g_pca_krylov_block > 0 ? g_pca_krylov_block : (k >= 128 ? 64 : 32);
+    const int p = krylov_block(k);
     // D ~ 5k columns; denser spectra of larger matrices need more (C5 arms:
     // +4 steps at 24k bins)
     int steps = (5 * k + p - 1) / p;
@@ -590,11 +592,11 @@ static void krylov_topk(Ctx &c, double *C, int c_col0, const double *mext, int n
             // so each centring correction rides in the product's reduction
             kprof_begin(c, K_GQ_GEMM);
             const R1 r_xk{n, nullptr, n};        // Xc K_t = C K_t - 1 (m'K_t)
-            rows_gemm_sharded(c, C, n, n + 2, Kt, n, p, n, XKt, 0, 1, &r_xk, c_col0);
+            rows_gemm_sharded(c, C, n, n + 2, Kt, n, p, n, XKt, 0, 1, &r_xk, c_col0, pd);
             kprof_end(c, K_GQ_GEMM);
             kprof_begin(c, K_GQ_GEMM);
             const R1 r_gk{n + 1, mext, n};   // Xc'(Xc K_t) = C (Xc K_t) - m (1'Xc K_t)
-            rows_gemm_sharded(c, C, n, n + 2, XKt, n, p, n, GKt, 0, 1, &r_gk, c_col0);
+            rows_gemm_sharded(c, C, n, n + 2, XKt, n, p, n, GKt, 0, 1, &r_gk, c_col0, pd);
             kprof_end(c, K_GQ_GEMM);
         }
         built = std::max(built, upto);
@@ -696,11 +698,19 @@ PcaStats pca_dev(Ctx &c, double *d_C, int n, int k, double *d_P, double *d_Pt, d
                                   hipMemcpyDeviceToDevice, s));
         // neither Xc nor XcT is formed; the Krylov space of C (tp_krylov.hip),
         // or of G when an orthogonalisation pass of that path breaks down
+        // the int8-digit image of this rank's columns of [C | m | 1] for the
+        // ~32 products with it (tp_prod_i8.hip)
         const bool cspace = g_pca_ckrylov > 0 || (g_pca_ckrylov < 0 && n >= g_ckry_min);
-        if (!cspace || !krylov_c_topk(c, d_C, c_col0, mext, n, k, V, d_P, h_theta, st)) {
+        ProdDigits pdg;
+        const ProdDigits *pd = nullptr;
+        if (g_prod_i8 > 0 && !cspace && prod_i8_ok(n, krylov_block(k))) {
+            prod_digits_build(c, d_C, n, n, cend - c_col0, c_col0, pdg);
+            pd = &pdg;
+        }
+        if (!cspace || !krylov_c_topk(c, d_C, c_col0, mext, n, k, V, d_P, h_theta, st, pd)) {
             h_theta.clear();
             st = PcaStats{};
-            krylov_topk(c, d_C, c_col0, mext, n, k, V, d_P, h_theta, st);
+            krylov_topk(c, d_C, c_col0, mext, n, k, V, d_P, h_theta, st, pd);
         }
     } else {
         Xc = c.buf[S_XC].as<double>((size_t)n * n);

@@ -1,0 +1,290 @@
+// The PCA's long-K products Out = A'B (A = [C | m | 1], K = n rows, M = n + 2
+// columns; B = an n x 32 / n x 64 Krylov block) on the int8 MFMA instead of
+// the fp64 one (R/TADpole.R:453, prcomp's products; tp_pca.hip, tp_krylov.hip).
+//
+// Every column of A and of B is cut into seven balanced base-256 digits of a
+// 54-bit fixed-point image scaled by a power of two per column:
+//   x = 2^(e - 54) sum_{s=0..6} d_s 256^(6 - s),  d_s in [-128, 127],
+// |x| < 2^e (e from the column's largest |x|), so the image differs from x by
+// at most 2^(e - 55) -- below half an fp64 ulp of the column's largest entry.
+// A'B is then sum over digit pairs (s, t) of 256^(12 - s - t) D_s'E_t, each
+// D_s'E_t an exact int32 MFMA product (|sum| <= kchunk 2^14 per pair).  Pairs
+// with s + t <= 6 are kept (28 of 49), grouped by u = s + t into seven int32
+// accumulators (<= 7 pairs each: kchunk <= 16384 keeps them below 2^31); the
+// dropped pairs weigh <= 256^-7 of the leading one.  The seven sums are
+// combined in fp64 (smallest weight first) and scaled by the two columns'
+// powers of two.  Relative to sum_k |A_ki||B_kj| the result is within ~2^-52
+// of the exact product: the rounding level of the fp64 product it replaces,
+// at 28 int8 MFMAs of 16 x 16 x 64 (2^20 ops at 16 cycles each) for what the
+// fp64 16 x 16 x 4 MFMA does in 16 launches of 2^11 flops -- 2.3x less MFMA
+// time for the same output.
+//
+// A's digits are formed once per PCA (A is fixed over all ~32 products); B's
+// per product.  The product kernel writes fp64 split-K partials that the
+// fp64 path's fixed-order reductions (with the rank-1 centring epilogue) sum:
+// k chunks depend on K alone, so a row shard computes every element with the
+// same bits as the whole product.
+#include <algorithm>
+#include <cmath>
+
+#include "tp_common.cuh"
+#include "tp_internal.h"
+
+namespace tp {
+
+// knob 36: the int8-digit products in the G-space Krylov path.  Off: exact to
+// ~3e-17 of sum |A||B| (test_prod_i8_digit_product) but slower than the fp64
+// k_gemm_ts at C3 (k_pd_prod 215 us against 188 us a product, + 20 us of B
+// digits)
+int g_prod_i8 = 0;
+
+constexpr int PD_DIG = 7;   // digits per value
+typedef int pd_i32x4 __attribute__((ext_vector_type(4)));
+
+// Digits of one column per workgroup: column c of X (K values, ld ldx) ->
+// D[s slice + c Kp + k] (k < Kp; zero past K and for c >= cols), the column
+// scale 2^(e - 54) into scale[c] (NaN for a non-finite column, so the product
+// is NaN as the fp64 one would be).
+__global__ void __launch_bounds__(256) k_pd_digits(const double *__restrict__ X, int ldx, int K, int cols, int Kp,
+                                                   size_t slice, int8_t *__restrict__ D, double *__restrict__ scale) {
+    __shared__ double red[4];
+    const int c = blockIdx.x;
+    const int t = threadIdx.x;
+    const double *x = X + (size_t)c * ldx;
+    const bool live = c < cols;
+    double mx = 0.0;
+    if (live)
+        for (int k = t; k < K; k += 256) mx = fmax(mx, fabs(x[k]));
+    // NaN-propagating max: fmax drops NaN, so flag non-finite values apart
+    bool bad = false;
+    if (live)
+        for (int k = t; k < K; k += 256) bad |= !isfinite(x[k]);
+    mx = bad ? INFINITY : mx;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
+    if ((t & 63) == 0) red[t >> 6] = mx;
+    __syncthreads();
+    mx = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+    int e = 0;
+    if (mx > 0.0 && isfinite(mx)) (void)frexp(mx, &e);   // mx < 2^e
+    const double sc = ldexp(1.0, 54 - e);
+    if (t == 0) scale[c] = !live ? 0.0 : (isfinite(mx) ? ldexp(1.0, e - 54) : NAN);
+    int8_t *d = D + (size_t)c * Kp;
+    for (int k0 = 4 * t; k0 < Kp; k0 += 1024) {
+        long long q[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int k = k0 + u;
+            const double v = (live && k < K && isfinite(mx)) ? x[k] : 0.0;
+            q[u] = llrint(v * sc);   // |q| <= 2^54
+        }
+        unsigned w[PD_DIG];
+#pragma unroll
+        for (int s = 0; s < PD_DIG; ++s) w[s] = 0u;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            long long r = q[u];
+#pragma unroll
+            for (int s = PD_DIG - 1; s >= 1; --s) {   // least significant first, balanced
+                const long long dd = (long long)(int8_t)(r & 0xFF);
+                w[s] |= ((unsigned)(dd & 0xFF)) << (8 * u);
+                r = (r - dd) >> 8;
+            }
+            w[0] |= ((unsigned)(r & 0xFF)) << (8 * u);   // |r| <= 64
+        }
+#pragma unroll
+        for (int s = 0; s < PD_DIG; ++s) *(unsigned *)(d + (size_t)s * slice + k0) = w[s];
+    }
+}
+
+// Out partials: rows [0, M) of A'B from the digit images Da (column i of A at
+// Da + i Kp, digit s at + s sla) and Db (N = 32 NWC columns).  4 waves, wave w
+// a 32 x 32 output block (2 x 2 MFMA tiles, seven accumulators each); the
+// workgroup covers 32 (4 / NWC) rows x N columns; blockIdx -> (row tile, k
+// chunk) dealt XCD-contiguously.  Each 64-byte k step of both digit images
+// (7 x 64 rows each) is staged through LDS (80-byte rows: the 16-lane b128
+// fragment reads spread over the banks), double-buffered: the global loads of
+// step k + 1 are issued before step k's 112 MFMAs a wave and written to the
+// other buffer after them (one barrier a step).  ~143 KB of LDS: one
+// workgroup a CU.
+constexpr int PD_LD = 80;                        // LDS row stride (bytes)
+#ifndef TP_PD_NBUF
+#define TP_PD_NBUF 2   // 1: one LDS buffer, two workgroups a CU (spills; measured slower)
+#endif
+template <int NWC>
+__global__ void __launch_bounds__(256, 3 - TP_PD_NBUF) k_pd_prod(const int8_t *__restrict__ Da, size_t sla, int Kp, int M,
+                                                    const int8_t *__restrict__ Db, size_t slb,
+                                                    const double *__restrict__ rs, const double *__restrict__ cs,
+                                                    double *__restrict__ part, size_t pstride, int kchunk) {
+    constexpr int NWR = 4 / NWC, TMR = 32 * NWR, TN = 32 * NWC;
+    extern __shared__ __attribute__((aligned(16))) int8_t pd_lds[];
+    const int tm = (M + TMR - 1) / TMR;
+    const int total = (int)gridDim.x;
+    const int xcd = (int)blockIdx.x & 7, slot = (int)blockIdx.x >> 3;
+    const int Lg = xcd * (total >> 3) + min(xcd, total & 7) + slot;
+    const int bm = Lg % tm, z = Lg / tm;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int wr = w % NWR, wc = w / NWR;
+    const int fr = lane & 15, fk = (lane >> 4) * 16;
+    const int kbeg = z * kchunk, kend = min(Kp, kbeg + kchunk);
+    TP_DASSERT(Kp % 64 == 0 && kchunk % 64 == 0 && kend - kbeg >= 64);
+    pd_i32x4 acc[PD_DIG][2][2];
+#pragma unroll
+    for (int u = 0; u < PD_DIG; ++u)
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b) acc[u][a][b] = pd_i32x4{0, 0, 0, 0};
+    // staging: thread t moves 16 bytes (k quarter t & 3) of row t >> 2 of every
+    // digit; A rows bm TMR + r (r < TMR, TMR / 64 chunks), B columns r < TN.
+    // A's rows past M read the zero-padded image (its columns are padded to
+    // 128 + a multiple of 128).
+    constexpr int RA = TMR / 64, RB = TN / 64 > 0 ? TN / 64 : 1;
+    const int sr = t >> 2, sk = (t & 3) * 16;
+    const int8_t *ga = Da + (size_t)(bm * TMR + sr) * Kp + sk;
+    const int8_t *gb = Db + (size_t)sr * Kp + sk;
+    const bool bl = sr < TN;   // TN = 32: half the threads stage B
+    pd_i32x4 ra[PD_DIG][RA], rb[PD_DIG][RB];
+    auto gload = [&](int kb) {
+#pragma unroll
+        for (int s = 0; s < PD_DIG; ++s) {
+#pragma unroll
+            for (int q = 0; q < RA; ++q) ra[s][q] = *(const pd_i32x4 *)(ga + s * sla + (size_t)q * 64 * Kp + kb);
+#pragma unroll
+            for (int q = 0; q < RB; ++q)
+                rb[s][q] = bl ? *(const pd_i32x4 *)(gb + s * slb + (size_t)q * 64 * Kp + kb) : pd_i32x4{0, 0, 0, 0};
+        }
+    };
+    // LDS: stage buffer = [A digits: PD_DIG x 64 RA rows][B digits: PD_DIG x 64 RB rows], PD_LD bytes a row
+    constexpr int ASZ = PD_DIG * 64 * RA * PD_LD;
+    auto lstore = [&](int buf) {
+        int8_t *L = pd_lds + buf * (ASZ + PD_DIG * 64 * RB * PD_LD);
+#pragma unroll
+        for (int s = 0; s < PD_DIG; ++s) {
+#pragma unroll
+            for (int q = 0; q < RA; ++q) *(pd_i32x4 *)(L + ((s * RA + q) * 64 + sr) * PD_LD + sk) = ra[s][q];
+#pragma unroll
+            for (int q = 0; q < RB; ++q)
+                if (bl) *(pd_i32x4 *)(L + ASZ + ((s * RB + q) * 64 + sr) * PD_LD + sk) = rb[s][q];
+        }
+    };
+    auto mstep = [&](int buf) {
+        const int8_t *L = pd_lds + buf * (ASZ + PD_DIG * 64 * RB * PD_LD);
+        // local row r of A (r < TMR) at (r / 64) * 64 + r % 64 == r in the
+        // [s][q][64] order: row (s RA + r / 64) 64 + r % 64 = s 64 RA + r
+        pd_i32x4 fb[PD_DIG][2];
+#pragma unroll
+        for (int tt = 0; tt < PD_DIG; ++tt)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+                fb[tt][b] = *(const pd_i32x4 *)(L + ASZ + (tt * 64 * RB + 32 * wc + 16 * b + fr) * PD_LD + fk);
+#pragma unroll
+        for (int s0 = 0; s0 < PD_DIG; ++s0) {
+            pd_i32x4 fa[2];
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+                fa[a] = *(const pd_i32x4 *)(L + (s0 * 64 * RA + 32 * wr + 16 * a + fr) * PD_LD + fk);
+#pragma unroll
+            for (int tt = 0; tt + s0 < PD_DIG; ++tt)
+#pragma unroll
+                for (int a = 0; a < 2; ++a)
+#pragma unroll
+                    for (int b = 0; b < 2; ++b)
+                        acc[s0 + tt][a][b] =
+                            __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[a], fb[tt][b], acc[s0 + tt][a][b], 0, 0, 0);
+        }
+    };
+    gload(kbeg);
+    lstore(0);
+    __syncthreads();
+    int buf = 0;
+    for (int kb = kbeg; kb < kend; kb += 64) {
+        const bool more = kb + 64 < kend;
+        if (more) gload(kb + 64);
+        mstep(buf);
+        if (TP_PD_NBUF == 1) __syncthreads();   // one buffer: two workgroups a CU overlap each other's waits
+        if (more) lstore(TP_PD_NBUF == 1 ? buf : buf ^ 1);
+        __syncthreads();
+        if (TP_PD_NBUF == 2) buf ^= 1;
+    }
+    const int i0 = bm * TMR + 32 * wr, j0 = 32 * wc;
+    double *P = part + pstride * z;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = i0 + 16 * a + (lane >> 4) * 4 + r;
+                const int j = j0 + 16 * b + fr;
+                if (i >= M) continue;
+                // weight of u: 256^(12 - u) 2^-108 -> 2^(-12 - 8u), times the scales
+                double v = 0.0;
+#pragma unroll
+                for (int u = PD_DIG - 1; u >= 0; --u) v += (double)acc[u][a][b][r] * ldexp(1.0, 96 - 8 * u);
+                P[(size_t)i + (size_t)j * M] = (v * rs[i]) * cs[j];
+            }
+}
+
+// two stages of both digit images
+static size_t pd_lds_bytes(int nwc) {
+    const int ra = 128 / nwc / 64, rb = std::max(1, 32 * nwc / 64);
+    return (size_t)TP_PD_NBUF * PD_DIG * 64 * (ra + rb) * PD_LD;
+}
+
+// k chunks from K alone (shards agree); <= 16384 rows a chunk (accumulator range)
+#ifndef TP_PD_KDIV
+#define TP_PD_KDIV 1024
+#endif
+static int pd_kchunk(int Kp) {
+    const int S = std::max(1, std::min(16, Kp / TP_PD_KDIV));
+    int kc = ((Kp + S - 1) / S + 63) / 64 * 64;
+    return std::min(kc, 16384);
+}
+
+// N = 64 (the G-space Krylov blocks); the 32-column tile's A stage (128 rows)
+// would not fit two stages in LDS
+bool prod_i8_ok(int K, int N) { return N == 64 && K >= 64; }
+
+void prod_digits_build(Ctx &c, const double *A, int lda, int K, int cols, int col0, ProdDigits &pd) {
+    hipStream_t s = c.cur;
+    pd.Kp = (K + 63) / 64 * 64;
+    pd.col0 = col0;
+    pd.cols = cols;
+    // + 128: a shard's row tiles (from any row) stay inside the padded image
+    const int cp = (cols + 127) / 128 * 128 + 128;
+    pd.slice = (size_t)cp * pd.Kp;
+    char *base = c.buf[S_PDIGA].as<char>(PD_DIG * pd.slice + (size_t)cp * sizeof(double) + 256);
+    pd.d = (int8_t *)base;
+    pd.rs = (double *)(base + (PD_DIG * pd.slice + 255) / 256 * 256);
+    hipLaunchKernelGGL(k_pd_digits, dim3((unsigned)cp), dim3(256), 0, s, A, lda, K, cols, pd.Kp, pd.slice,
+                       (int8_t *)pd.d, (double *)pd.rs);
+    TP_HIP(hipGetLastError());
+}
+
+// partials of rows [r0, r0 + M) (global column indices of A) of A'B into
+// `work`: returns the chunk count; pstride = M N
+int prod_i8_partials(Ctx &c, const ProdDigits &pd, int r0, int M, const double *B, int ldb, int N, int K,
+                     DevBuf &work, double **part) {
+    hipStream_t s = c.cur;
+    if (!prod_i8_ok(K, N) || (K + 63) / 64 * 64 != pd.Kp || r0 < pd.col0 || r0 + M > pd.col0 + pd.cols)
+        fail(TP_ERR_ARG, "prod_i8: rows outside the digit image, or an unsupported block");
+    const size_t slb = (size_t)N * pd.Kp;
+    char *bb = c.buf[S_PDIGB].as<char>(PD_DIG * slb + (size_t)N * sizeof(double) + 256);
+    int8_t *Db = (int8_t *)bb;
+    double *cs = (double *)(bb + (PD_DIG * slb + 255) / 256 * 256);
+    hipLaunchKernelGGL(k_pd_digits, dim3((unsigned)N), dim3(256), 0, s, B, ldb, K, N, pd.Kp, slb, Db, cs);
+    const int kc = pd_kchunk(pd.Kp);
+    const int S = (pd.Kp + kc - 1) / kc;
+    const size_t pstride = (size_t)M * N;
+    *part = work.as<double>(pstride * S);
+    const int8_t *Da = pd.d + (size_t)(r0 - pd.col0) * pd.Kp;
+    const double *rs = pd.rs + (r0 - pd.col0);
+    const int tm = (M + 63) / 64;
+    hipLaunchKernelGGL(k_pd_prod<2>, dim3((unsigned)(tm * S)), dim3(256), pd_lds_bytes(2), s, Da, pd.slice, pd.Kp, M,
+                       Db, slb, rs, cs, *part, pstride, kc);
+    TP_HIP(hipGetLastError());
+    return S;
+}
+
+}  // namespace tp

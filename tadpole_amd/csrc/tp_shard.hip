@@ -429,9 +429,16 @@ void cor_product(Ctx &c, const double *X, int n, const double *m, const GatherSt
 // B K x N: rows of Out split in 64-row blocks, each written transposed into
 // the packed T (N x M col-major = Out row-major), gathered, transposed back.
 void rows_gemm_sharded(Ctx &c, const double *A, int lda, int M, const double *B, int ldb, int N, int K,
-                       double *Out, int splitk_plain, int tag, const R1 *r1, int a_col0) {
+                       double *Out, int splitk_plain, int tag, const R1 *r1, int a_col0, const ProdDigits *pd) {
+    const bool i8 = pd && pd->d && prod_i8_ok(K, N) && splitk_plain <= 1;
     if (!c.shard.active) {
         if (a_col0 != 0) fail(TP_ERR_ARG, "rows_gemm_sharded: a column slab needs the sharded schedule");
+        if (i8 && r1) {   // int8-digit partials, then the fp64 path's rank-1 reduction
+            double *part = nullptr;
+            const int S = prod_i8_partials(c, *pd, 0, M, B, ldb, N, K, c.buf[S_PARTIAL], &part);
+            launch_splitk_reduce_r1(part, (size_t)M * N, S, M, N, r1->rows, r1->vrow, r1->u, Out, r1->rows, c.cur);
+            return;
+        }
         const bool fused = r1 && rows_ts(K, N) && splitk_plain <= 1;   // the epilogue rides in the reduction
         double *dst = (r1 && !fused) ? c.buf[S_SHARD].as<double>((size_t)M * N) : Out;
         GemmArgs g{M, N, K, A, lda, true, B, ldb, dst, fused ? r1->rows : M};
@@ -454,6 +461,13 @@ void rows_gemm_sharded(Ctx &c, const double *A, int lda, int M, const double *B,
     for (int r = 0; r < R; ++r) {
         if (!shard_mine(c, r) || rb[r + 1] <= rb[r]) continue;
         if (rb[r] < a_col0) fail(TP_ERR_ARG, "rows_gemm_sharded: shard rows outside this rank's slab");
+        if (i8) {   // the same k chunks as unsharded: the same element bits
+            const int Mr = rb[r + 1] - rb[r];
+            double *part = nullptr;
+            const int S = prod_i8_partials(c, *pd, rb[r], Mr, B, ldb, N, K, c.buf[S_PARTIAL], &part);
+            launch_splitk_reduce(part, (size_t)Mr * N, S, Mr, N, T + (size_t)rb[r] * N, N, 1, c.cur);
+            continue;
+        }
         GemmArgs g{rb[r + 1] - rb[r], N, K, A + (size_t)(rb[r] - a_col0) * lda, lda, true, B, ldb,
                    T + (size_t)rb[r] * N, N};
         g.store_t = true;

@@ -66,6 +66,21 @@ def test_config_golden(gpu, name):
     assert got.timings_ms[13] <= 1e-11
 
 
+def test_config_c3_golden_int8_products(gpu):
+    """C3 with the Krylov products on the int8 MFMA (7-digit images of C and of
+    each block, knob 36): the golden's n_pcs, clusters, merge order and every
+    level, CH within 1e-6."""
+    import tadpole_amd as tp
+    z = np.load(os.path.join(GOLD, "c3.npz"))
+    m = synth_hic(int(z["n0"]), int(z["seed"]))
+    old = G.knob(36, 1)
+    try:
+        got = tp.TADpole(m, max_pcs=200)
+    finally:
+        G.knob(36, old)
+    _check(got, z)
+
+
 def test_config_c3_from_hbm(gpu):
     """C3 with the matrix already resident in HBM (a torch tensor: the bench's
     input form) gives the same result as from host memory."""
@@ -78,12 +93,13 @@ def test_config_c3_from_hbm(gpu):
 
 
 @pytest.mark.parametrize("forced,space", [(True, "C"), (True, "C-full-pip"), (True, "G"), (True, "G-full-cgs"),
-                                          (False, "G")])
+                                          (True, "G-int8"), (False, "G")])
 def test_pca_krylov_path_vs_lapack(gpu, forced, space):
     """The block Krylov PCA (G never formed; Krylov space of G, the default,
     or of C: knob 20; G with the first CGS pass against every block instead of
     the last two: knob 28; C with the first PIP pass against every block
-    instead of K_0 and the last two: knob 33) against LAPACK's SVD on a matrix below its default
+    instead of K_0 and the last two: knob 33; G with the products on the int8
+    MFMA from 7-digit images: knob 36) against LAPACK's SVD on a matrix below its default
     size threshold (forced) and the G-formed path on the same matrix: every
     prefix subspace the sweep uses agrees."""
     n0 = 2600
@@ -96,6 +112,7 @@ def test_pca_krylov_path_vs_lapack(gpu, forced, space):
     old20 = G.knob(20, 1 if space.startswith("C") else 0)
     old28 = G.knob(28, 0 if space == "G-full-cgs" else 1)
     old33 = G.knob(33, 0 if space == "C-full-pip" else 1)
+    old36 = G.knob(36, 1 if space == "G-int8" else 0)
     try:
         p, _ = G.pca(c, 200)
     finally:
@@ -103,6 +120,7 @@ def test_pca_krylov_path_vs_lapack(gpu, forced, space):
         G.knob(20, old20)
         G.knob(28, old28)
         G.knob(33, old33)
+        G.knob(36, old36)
     op = O.prcomp_x(c, 200)
     s = np.sign(np.sum(p * op, axis=0))
     s[s == 0] = 1

@@ -661,3 +661,39 @@ def test_gemm_rows_kernel_row_independent(gpu, M, N, K):
     ref = A.T @ B
     assert np.abs(c - ref).max() <= 1e-13 * np.abs(ref).max() * np.sqrt(K)
     print(f"rows gemm {M}x{N}x{K}: {t * 1e3:.1f} us, {2.0 * M * N * K / t / 1e9:.1f} TF/s")
+
+
+@pytest.mark.parametrize("K,M,N", [(4100, 302, 64), (7808, 130, 64), (4160, 9, 64)])
+def test_prod_i8_digit_product(gpu, K, M, N):
+    """The Krylov products on the int8 MFMA (7-digit images, knob 36) against
+    an 80-bit reference of the same A'B with the rank-1 epilogue: within
+    1e-14 of sum |A||B| elementwise, as accurate as the fp64 k_gemm_ts path.
+    Columns with a non-unit scale, a zero column and a column of ones (the
+    [C | m | 1] layout) ride along."""
+    import ctypes
+    rng = np.random.default_rng(K + M + N)
+    A = rng.uniform(-1, 1, size=(K, M))
+    A[:, 3] *= 1e-5
+    A[:, 5] = 0.0
+    A[:, 7] *= 37.5
+    A[:, M - 1] = 1.0
+    B = rng.standard_normal((K, N)) / np.sqrt(K)
+    B[:, 1] *= 1e6
+    Af, Bf = np.asfortranarray(A), np.asfortranarray(B)
+    O8 = np.zeros((M - 1, N), order="F")
+    O64 = np.zeros((M - 1, N), order="F")
+    ms = np.zeros(2)
+    st = ctypes.c_int(0)
+    D = ctypes.POINTER(ctypes.c_double)
+    I = lambda v: ctypes.byref(ctypes.c_int(v))  # noqa: E731
+    gpu.tp_debug_prod_i8(Af.ctypes.data_as(D), I(K), I(M), Bf.ctypes.data_as(D), I(N), O8.ctypes.data_as(D),
+                         O64.ctypes.data_as(D), ms.ctypes.data_as(D), ctypes.byref(st))
+    assert st.value == 0
+    P = A.astype(np.longdouble).T @ B.astype(np.longdouble)
+    ref = (P[:M - 1] - P[M - 1]).astype(np.float64)
+    absP = np.abs(A).T @ np.abs(B)
+    bound = absP[:M - 1] + absP[M - 1]
+    e8 = float(np.max(np.abs(O8 - ref) / bound))
+    e64 = float(np.max(np.abs(O64 - ref) / bound))
+    print(f"prod_i8 K={K} M={M} N={N}: int8 {ms[0] * 1e3:.1f} us err {e8:.2e} | fp64 {ms[1] * 1e3:.1f} us err {e64:.2e}")
+    assert e8 < 1e-14

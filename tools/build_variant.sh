@@ -11,7 +11,7 @@ base=$(basename "$src" .hip)
 /opt/rocm/bin/hipcc $FLAGS $defs -c "$C/$src" -o "$C/build/${base}_$tag.o"
 objs=""
 for o in "$C"/build/*.o; do
-  case "$(basename "$o")" in tp_*_*.o) continue;; esac
+  [ -f "$C/$(basename "$o" .o).hip" ] || continue   # other variants' objects
   [ "$(basename "$o" .o)" = "$base" ] && o="$C/build/${base}_$tag.o"
   objs="$objs $o"
 done
