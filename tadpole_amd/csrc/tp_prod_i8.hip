@@ -34,12 +34,40 @@ namespace tp {
 
 // knob 36: the int8-digit products in the G-space Krylov path.  Off: exact to
 // ~3e-17 of sum |A||B| (test_prod_i8_digit_product) but slower than the fp64
-// k_gemm_ts at C3 (k_pd_prod 215 us against 188 us a product, + 20 us of B
-// digits)
+// k_gemm_ts at C3 (222 us a product with the block's digits and the reduction,
+// against 200 us)
 int g_prod_i8 = 0;
 
 constexpr int PD_DIG = 7;   // digits per value
 typedef int pd_i32x4 __attribute__((ext_vector_type(4)));
+
+// Digits of x[k0..k0+3] (zero past K or when !ok): one 4-byte word per digit
+__device__ __forceinline__ void pd_digits4(const double *__restrict__ x, int K, int k0, bool ok, double sc,
+                                           int8_t *__restrict__ d, size_t slice) {
+    long long q[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int k = k0 + u;
+        const double v = (ok && k < K) ? x[k] : 0.0;
+        q[u] = llrint(v * sc);   // |q| <= 2^54
+    }
+    unsigned w[PD_DIG];
+#pragma unroll
+    for (int s = 0; s < PD_DIG; ++s) w[s] = 0u;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        long long r = q[u];
+#pragma unroll
+        for (int s = PD_DIG - 1; s >= 1; --s) {   // least significant first, balanced
+            const long long dd = (long long)(int8_t)(r & 0xFF);
+            w[s] |= ((unsigned)(dd & 0xFF)) << (8 * u);
+            r = (r - dd) >> 8;
+        }
+        w[0] |= ((unsigned)(r & 0xFF)) << (8 * u);   // |r| <= 64
+    }
+#pragma unroll
+    for (int s = 0; s < PD_DIG; ++s) *(unsigned *)(d + (size_t)s * slice + k0) = w[s];
+}
 
 // Digits of one column per workgroup: column c of X (K values, ld ldx) ->
 // D[s slice + c Kp + k] (k < Kp; zero past K and for c >= cols), the column
@@ -70,31 +98,48 @@ __global__ void __launch_bounds__(256) k_pd_digits(const double *__restrict__ X,
     const double sc = ldexp(1.0, 54 - e);
     if (t == 0) scale[c] = !live ? 0.0 : (isfinite(mx) ? ldexp(1.0, e - 54) : NAN);
     int8_t *d = D + (size_t)c * Kp;
-    for (int k0 = 4 * t; k0 < Kp; k0 += 1024) {
-        long long q[4];
+    for (int k0 = 4 * t; k0 < Kp; k0 += 1024) pd_digits4(x, K, k0, live && isfinite(mx), sc, d, slice);
+}
+
+// The same digits for a few columns (a Krylov block, N = 64): the column's
+// largest |x| from per-1024-row partial maxima (k_pd_colmax), one workgroup
+// per 1024 rows of a column -- 64 x (Kp / 1024) workgroups instead of 64.
+__global__ void __launch_bounds__(256) k_pd_colmax(const double *__restrict__ X, int ldx, int K, int SL,
+                                                   double *__restrict__ pmax) {
+    __shared__ double red[4];
+    const int c = blockIdx.x / SL, sl = blockIdx.x % SL;
+    const int t = threadIdx.x;
+    const double *x = X + (size_t)c * ldx;
+    double mx = 0.0;
+    bool bad = false;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int k = k0 + u;
-            const double v = (live && k < K && isfinite(mx)) ? x[k] : 0.0;
-            q[u] = llrint(v * sc);   // |q| <= 2^54
+    for (int u = 0; u < 4; ++u) {
+        const int k = sl * 1024 + 4 * t + u;
+        if (k < K) {
+            const double v = x[k];
+            mx = fmax(mx, fabs(v));
+            bad |= !isfinite(v);
         }
-        unsigned w[PD_DIG];
-#pragma unroll
-        for (int s = 0; s < PD_DIG; ++s) w[s] = 0u;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            long long r = q[u];
-#pragma unroll
-            for (int s = PD_DIG - 1; s >= 1; --s) {   // least significant first, balanced
-                const long long dd = (long long)(int8_t)(r & 0xFF);
-                w[s] |= ((unsigned)(dd & 0xFF)) << (8 * u);
-                r = (r - dd) >> 8;
-            }
-            w[0] |= ((unsigned)(r & 0xFF)) << (8 * u);   // |r| <= 64
-        }
-#pragma unroll
-        for (int s = 0; s < PD_DIG; ++s) *(unsigned *)(d + (size_t)s * slice + k0) = w[s];
     }
+    mx = bad ? INFINITY : mx;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
+    if ((t & 63) == 0) red[t >> 6] = mx;
+    __syncthreads();
+    if (t == 0) pmax[blockIdx.x] = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+}
+__global__ void __launch_bounds__(256) k_pd_digits_sl(const double *__restrict__ X, int ldx, int K, int Kp, int SL,
+                                                      const double *__restrict__ pmax, size_t slice,
+                                                      int8_t *__restrict__ D, double *__restrict__ scale) {
+    const int c = blockIdx.x / SL, sl = blockIdx.x % SL;
+    const int t = threadIdx.x;
+    double mx = 0.0;
+    for (int q = 0; q < SL; ++q) mx = fmax(mx, pmax[c * SL + q]);
+    int e = 0;
+    if (mx > 0.0 && isfinite(mx)) (void)frexp(mx, &e);
+    if (sl == 0 && t == 0) scale[c] = isfinite(mx) ? ldexp(1.0, e - 54) : NAN;
+    const int k0 = sl * 1024 + 4 * t;
+    if (k0 < Kp) pd_digits4(X + (size_t)c * ldx, K, k0, isfinite(mx), ldexp(1.0, 54 - e), D + (size_t)c * Kp, slice);
 }
 
 // Out partials: rows [0, M) of A'B from the digit images Da (column i of A at
@@ -194,19 +239,66 @@ __global__ void __launch_bounds__(256, 3 - TP_PD_NBUF) k_pd_prod(const int8_t *_
                             __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[a], fb[tt][b], acc[s0 + tt][a][b], 0, 0, 0);
         }
     };
+#if TP_PD_NBUF == 2
+    // two staging register sets, two k steps of loads in flight (HBM latency
+    // under load is ~2 steps of MFMAs); loads past the chunk re-read its last
+    // step (clamped, unconditional: the compiler counts them) and land in the
+    // buffer no later step reads
+    const int T = (kend - kbeg) / 64;
+    pd_i32x4 xa[PD_DIG][RA], xb[PD_DIG][RB];
+    auto gload2 = [&](pd_i32x4 (&ta)[PD_DIG][RA], pd_i32x4 (&tb)[PD_DIG][RB], int st) {
+        const int kb = kbeg + 64 * min(st, T - 1);
+#pragma unroll
+        for (int s = 0; s < PD_DIG; ++s) {
+#pragma unroll
+            for (int q = 0; q < RA; ++q) ta[s][q] = *(const pd_i32x4 *)(ga + s * sla + (size_t)q * 64 * Kp + kb);
+#pragma unroll
+            for (int q = 0; q < RB; ++q) tb[s][q] = *(const pd_i32x4 *)(gb + s * slb + (size_t)q * 64 * Kp + kb);
+        }
+    };
+    auto lstore2 = [&](const pd_i32x4 (&ta)[PD_DIG][RA], const pd_i32x4 (&tb)[PD_DIG][RB], int bf) {
+        int8_t *L = pd_lds + bf * (ASZ + PD_DIG * 64 * RB * PD_LD);
+#pragma unroll
+        for (int s = 0; s < PD_DIG; ++s) {
+#pragma unroll
+            for (int q = 0; q < RA; ++q) *(pd_i32x4 *)(L + ((s * RA + q) * 64 + sr) * PD_LD + sk) = ta[s][q];
+#pragma unroll
+            for (int q = 0; q < RB; ++q) *(pd_i32x4 *)(L + ASZ + ((s * RB + q) * 64 + sr) * PD_LD + sk) = tb[s][q];
+        }
+    };
+    static_assert(TN == 64, "two-step prefetch: every thread stages B (TN = 64)");
+    (void)gload;
+    (void)lstore;
+    gload2(ra, rb, 0);
+    lstore2(ra, rb, 0);
+    gload2(ra, rb, 1);
+    gload2(xa, xb, 2);
+    __syncthreads();
+    for (int st = 0;; st += 2) {
+        mstep(0);                // step st
+        lstore2(ra, rb, 1);      // step st + 1
+        __syncthreads();
+        gload2(ra, rb, st + 3);
+        if (st + 1 >= T) break;
+        mstep(1);                // step st + 1
+        lstore2(xa, xb, 0);      // step st + 2
+        __syncthreads();
+        gload2(xa, xb, st + 4);
+        if (st + 2 >= T) break;
+    }
+#else
     gload(kbeg);
     lstore(0);
     __syncthreads();
-    int buf = 0;
     for (int kb = kbeg; kb < kend; kb += 64) {
         const bool more = kb + 64 < kend;
         if (more) gload(kb + 64);
-        mstep(buf);
-        if (TP_PD_NBUF == 1) __syncthreads();   // one buffer: two workgroups a CU overlap each other's waits
-        if (more) lstore(TP_PD_NBUF == 1 ? buf : buf ^ 1);
+        mstep(0);
+        __syncthreads();   // one buffer: two workgroups a CU overlap each other's waits
+        if (more) lstore(0);
         __syncthreads();
-        if (TP_PD_NBUF == 2) buf ^= 1;
     }
+#endif
     const int i0 = bm * TMR + 32 * wr, j0 = 32 * wc;
     double *P = part + pstride * z;
 #pragma unroll
@@ -270,10 +362,15 @@ int prod_i8_partials(Ctx &c, const ProdDigits &pd, int r0, int M, const double *
     if (!prod_i8_ok(K, N) || (K + 63) / 64 * 64 != pd.Kp || r0 < pd.col0 || r0 + M > pd.col0 + pd.cols)
         fail(TP_ERR_ARG, "prod_i8: rows outside the digit image, or an unsupported block");
     const size_t slb = (size_t)N * pd.Kp;
-    char *bb = c.buf[S_PDIGB].as<char>(PD_DIG * slb + (size_t)N * sizeof(double) + 256);
+    char *bb = c.buf[S_PDIGB].as<char>(PD_DIG * slb + 256 + 512 * sizeof(double) +
+                                        (size_t)N * ((pd.Kp + 1023) / 1024) * sizeof(double));
     int8_t *Db = (int8_t *)bb;
     double *cs = (double *)(bb + (PD_DIG * slb + 255) / 256 * 256);
-    hipLaunchKernelGGL(k_pd_digits, dim3((unsigned)N), dim3(256), 0, s, B, ldb, K, N, pd.Kp, slb, Db, cs);
+    const int SL = (pd.Kp + 1023) / 1024;
+    double *pmax = (double *)(bb + (PD_DIG * slb + 255) / 256 * 256 + 512 * sizeof(double));
+    hipLaunchKernelGGL(k_pd_colmax, dim3((unsigned)(N * SL)), dim3(256), 0, s, B, ldb, K, SL, pmax);
+    hipLaunchKernelGGL(k_pd_digits_sl, dim3((unsigned)(N * SL)), dim3(256), 0, s, B, ldb, K, pd.Kp, SL, pmax, slb, Db,
+                       cs);
     const int kc = pd_kchunk(pd.Kp);
     const int S = (pd.Kp + kc - 1) / kc;
     const size_t pstride = (size_t)M * N;
