@@ -32,10 +32,10 @@
 
 namespace tp {
 
-// knob 36: the int8-digit products in the G-space Krylov path.  Off: exact to
-// ~3e-17 of sum |A||B| (test_prod_i8_digit_product) but slower than the fp64
-// k_gemm_ts at C3 (222 us a product with the block's digits and the reduction,
-// against 200 us)
+// knob 36: the int8-digit products in the G-space Krylov path.  Off: within
+// ~1e-15 of sum |A||B| (test_prod_i8_digit_product), the C3 products 6.12 ms
+// against 6.42 for the fp64 k_gemm_ts, but C's digit image costs 0.27 ms a
+// pipeline: no net gain at C3
 int g_prod_i8 = 0;
 
 constexpr int PD_DIG = 7;   // digits per value
@@ -153,6 +153,11 @@ __global__ void __launch_bounds__(256) k_pd_digits_sl(const double *__restrict__
 // other buffer after them (one barrier a step).  ~143 KB of LDS: one
 // workgroup a CU.
 constexpr int PD_LD = 80;                        // LDS row stride (bytes)
+#ifndef TP_PD_ADIG
+#define TP_PD_ADIG 6   // digits of A read by the product (6: without the (6, 0) pair, A to 2^-49 of its column
+                       // maximum: C3 products 6.63 -> 6.12 ms, errors 3e-17 -> 5e-16..9e-16 of sum |A||B|)
+#endif
+constexpr int PD_ADIG = TP_PD_ADIG;
 #ifndef TP_PD_NBUF
 #define TP_PD_NBUF 2   // 1: one LDS buffer, two workgroups a CU (spills; measured slower)
 #endif
@@ -201,7 +206,7 @@ __global__ void __launch_bounds__(256, 3 - TP_PD_NBUF) k_pd_prod(const int8_t *_
         }
     };
     // LDS: stage buffer = [A digits: PD_DIG x 64 RA rows][B digits: PD_DIG x 64 RB rows], PD_LD bytes a row
-    constexpr int ASZ = PD_DIG * 64 * RA * PD_LD;
+    constexpr int ASZ = PD_ADIG * 64 * RA * PD_LD;
     auto lstore = [&](int buf) {
         int8_t *L = pd_lds + buf * (ASZ + PD_DIG * 64 * RB * PD_LD);
 #pragma unroll
@@ -224,7 +229,7 @@ __global__ void __launch_bounds__(256, 3 - TP_PD_NBUF) k_pd_prod(const int8_t *_
             for (int b = 0; b < 2; ++b)
                 fb[tt][b] = *(const pd_i32x4 *)(L + ASZ + (tt * 64 * RB + 32 * wc + 16 * b + fr) * PD_LD + fk);
 #pragma unroll
-        for (int s0 = 0; s0 < PD_DIG; ++s0) {
+        for (int s0 = 0; s0 < PD_ADIG; ++s0) {
             pd_i32x4 fa[2];
 #pragma unroll
             for (int a = 0; a < 2; ++a)
@@ -251,7 +256,8 @@ __global__ void __launch_bounds__(256, 3 - TP_PD_NBUF) k_pd_prod(const int8_t *_
 #pragma unroll
         for (int s = 0; s < PD_DIG; ++s) {
 #pragma unroll
-            for (int q = 0; q < RA; ++q) ta[s][q] = *(const pd_i32x4 *)(ga + s * sla + (size_t)q * 64 * Kp + kb);
+            for (int q = 0; q < RA; ++q)
+                if (s < PD_ADIG) ta[s][q] = *(const pd_i32x4 *)(ga + s * sla + (size_t)q * 64 * Kp + kb);
 #pragma unroll
             for (int q = 0; q < RB; ++q) tb[s][q] = *(const pd_i32x4 *)(gb + s * slb + (size_t)q * 64 * Kp + kb);
         }
@@ -261,7 +267,8 @@ __global__ void __launch_bounds__(256, 3 - TP_PD_NBUF) k_pd_prod(const int8_t *_
 #pragma unroll
         for (int s = 0; s < PD_DIG; ++s) {
 #pragma unroll
-            for (int q = 0; q < RA; ++q) *(pd_i32x4 *)(L + ((s * RA + q) * 64 + sr) * PD_LD + sk) = ta[s][q];
+            for (int q = 0; q < RA; ++q)
+                if (s < PD_ADIG) *(pd_i32x4 *)(L + ((s * RA + q) * 64 + sr) * PD_LD + sk) = ta[s][q];
 #pragma unroll
             for (int q = 0; q < RB; ++q) *(pd_i32x4 *)(L + ASZ + ((s * RB + q) * 64 + sr) * PD_LD + sk) = tb[s][q];
         }
@@ -321,12 +328,12 @@ __global__ void __launch_bounds__(256, 3 - TP_PD_NBUF) k_pd_prod(const int8_t *_
 // two stages of both digit images
 static size_t pd_lds_bytes(int nwc) {
     const int ra = 128 / nwc / 64, rb = std::max(1, 32 * nwc / 64);
-    return (size_t)TP_PD_NBUF * PD_DIG * 64 * (ra + rb) * PD_LD;
+    return (size_t)TP_PD_NBUF * 64 * (PD_ADIG * ra + PD_DIG * rb) * PD_LD;
 }
 
 // k chunks from K alone (shards agree); <= 16384 rows a chunk (accumulator range)
 #ifndef TP_PD_KDIV
-#define TP_PD_KDIV 1024
+#define TP_PD_KDIV 960   // C3: 8 k chunks, 984 workgroups (~4 full rounds of one a CU; 1024: 7, 861)
 #endif
 static int pd_kchunk(int Kp) {
     const int S = std::max(1, std::min(16, Kp / TP_PD_KDIV));
