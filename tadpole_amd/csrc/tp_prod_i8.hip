@@ -1,6 +1,6 @@
 // The PCA's long-K products Out = A'B (A = [C | m | 1], K = n rows, M = n + 2
-// columns; B = an n x 32 / n x 64 Krylov block) on the int8 MFMA instead of
-// the fp64 one (R/TADpole.R:453, prcomp's products; tp_pca.hip, tp_krylov.hip).
+// columns; B = an n x 64 Krylov block of the G-space path) on the int8 MFMA
+// instead of the fp64 one (R/TADpole.R:453, prcomp's products; tp_pca.hip).
 //
 // Every column of A and of B is cut into seven balanced base-256 digits of a
 // 54-bit fixed-point image scaled by a power of two per column:
@@ -9,14 +9,15 @@
 // at most 2^(e - 55) -- below half an fp64 ulp of the column's largest entry.
 // A'B is then sum over digit pairs (s, t) of 256^(12 - s - t) D_s'E_t, each
 // D_s'E_t an exact int32 MFMA product (|sum| <= kchunk 2^14 per pair).  Pairs
-// with s + t <= 6 are kept (28 of 49), grouped by u = s + t into seven int32
+// with s + t <= 6 are kept, grouped by u = s + t into seven int32
 // accumulators (<= 7 pairs each: kchunk <= 16384 keeps them below 2^31); the
-// dropped pairs weigh <= 256^-7 of the leading one.  The seven sums are
-// combined in fp64 (smallest weight first) and scaled by the two columns'
-// powers of two.  Relative to sum_k |A_ki||B_kj| the result is within ~2^-52
-// of the exact product: the rounding level of the fp64 product it replaces,
-// at 28 int8 MFMAs of 16 x 16 x 64 (2^20 ops at 16 cycles each) for what the
-// fp64 16 x 16 x 4 MFMA does in 16 launches of 2^11 flops -- 2.3x less MFMA
+// dropped pairs weigh <= 256^-7 of the leading one.  The product reads
+// TP_PD_ADIG of A's digits: 7 (28 pairs) is within ~5e-17 of sum |A_ki||B_kj|,
+// the rounding level of the fp64 product; 6 (27 pairs, the default) drops the
+// (6, 0) pair and A's last 8 bits, ~1e-15.  The seven sums are combined in
+// fp64 (smallest weight first) and scaled by the two columns' powers of two.
+// 27 int8 MFMAs of 16 x 16 x 64 (2^20 ops, 16 cycles each) produce what 16
+// fp64 16 x 16 x 4 MFMAs (2^11 flops each) do at 64 cycles: 2.4x less MFMA
 // time for the same output.
 //
 // A's digits are formed once per PCA (A is fixed over all ~32 products); B's
