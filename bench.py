@@ -705,12 +705,15 @@ def main():
         else:              # one record = G Q: 2 N^2 b flops
             gq_flops = share * 2.0 * n * n * block
         ns = int(tm[18])   # int8 slices of the exact X'X (0: fp64 product)
+        pairs = int(tm[19])   # int8 digit pairs of each product with C (0: fp64 products)
         kern = {   # class: (ms per pipeline, bound, launches per pipeline, algorithmic work per launch, peak)
             # X'X: ns^2 slice products of N^3 int8 ops each (upper tiles: N^2/2 outputs x N MACs x 2)
             "xtx_gemm": ((tm[5], "mfma", 1, share * ns * ns * float(n) ** 3, INT8_MFMA_PEAK_TOPS) if ns else
                          (tm[5], "mfma", 1, share * float(n) ** 3, FP64_MFMA_PEAK_TFLOPS)),
             "xcxc_gemm": (tm[6], "mfma", 1, share * float(n) ** 3, FP64_MFMA_PEAK_TFLOPS),
-            "gq_gemm": (tm[7], "mfma", gq_launches, gq_flops, FP64_MFMA_PEAK_TFLOPS),
+            # products with C on the int8 MFMA: `pairs` digit products of 2 N^2 p int8 ops each
+            "gq_gemm": ((tm[7], "mfma", gq_launches, gq_flops * pairs, INT8_MFMA_PEAK_TOPS) if pairs else
+                        (tm[7], "mfma", gq_launches, gq_flops, FP64_MFMA_PEAK_TFLOPS)),
             "coniss": (tm[9], "hbm", 1, 40.0 * (n - 1) * k * (k + 1) / 2.0, HBM_PEAK_GBS),   # 5 sum rows/merge
             "ch": (tm[10], "hbm", 1, 16.0 * n * k, HBM_PEAK_GBS),   # the scores twice (segment statistics shared by the trees)
         }
@@ -722,7 +725,7 @@ def main():
             if not avg_ms > 0:   # a class this path does not run (e.g. G = Xc'Xc on the Krylov path)
                 return float("nan"), peak, "TFLOP/s" if bound == "mfma" else "GB/s", avg_ms
             if bound == "mfma":
-                unit = "TOP/s (int8)" if (q == "xtx_gemm" and ns) else "TFLOP/s"
+                unit = "TOP/s (int8)" if ((q == "xtx_gemm" and ns) or (q == "gq_gemm" and pairs)) else "TFLOP/s"
                 return per_launch / (avg_ms * 1e-3) / 1e12, peak, unit, avg_ms
             return per_launch / (avg_ms * 1e-3) / 1e9, peak, "GB/s", avg_ms
 
@@ -744,6 +747,12 @@ def main():
                         "note": ("xtx_gemm counts the ns^2 slice products whole (dense-equivalent int8 ops); "
                                  "the kernel skips the high slice's all-zero 128x64 blocks (raw counts >= 128 "
                                  "sit near the diagonal), so it executes fewer") if ns == 2 else None},
+                "gq": {"int8_digit_pairs": pairs,
+                       "fp64_equivalent_tflops": (round(gq_flops * gq_launches / (tm[7] * 1e-3) / 1e12, 2)
+                                                  if tm[7] > 0 else None),
+                       "note": ("the products with C on the int8 MFMA from digit images (6 digits of C, 7 of "
+                                "the block, pairs s + t <= 6; tp_prod_i8.hip); achieved counts the int8 ops")
+                       if pairs else None},
                 "stages_ms": {"mask": round(tm[0], 3), "cor": round(tm[1], 3), "pca": round(tm[2], 3),
                               "sweep": round(tm[3], 3), "total": round(tm[4], 3)},
                 "pca": {"path": "block Krylov (G never formed)" if krylov_steps else "G = Xc'Xc + subspace iteration",

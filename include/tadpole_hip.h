@@ -209,7 +209,8 @@ void tp_ch(const double *P, const int *n, const int *k, const int *labels,
  *   count [9] CONISS [10] CH, and [11] PCA Chebyshev degrees [12] block
  *   [13] residual [14] n_good [15] k [16] Krylov steps (0: G formed)
  *   [17] Krylov dimension D [18] int8 slices of the exact X'X
- *   product (0: fp64 MFMA product); [19..31] reserved, written 0). */
+ *   product (0: fp64 MFMA product) [19] int8 digit pairs of each Krylov
+ *   product with C (0: fp64 MFMA products); [20..31] reserved, written 0). */
 void tp_pipeline(const double *M, const int *n0, const int *max_pcs,
                  const int *min_clusters, const double *bad_frac,
                  const int *flags, const int *device, const int *k_cap,

@@ -791,7 +791,8 @@ static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_cl
         timings[16] = ps.krylov_steps;
         timings[17] = ps.krylov_dim;
         timings[18] = c.last_xtx_ns;
-        for (int q = 19; q < 32; ++q) timings[q] = 0.0;
+        timings[19] = ps.prod_pairs;
+        for (int q = 20; q < 32; ++q) timings[q] = 0.0;
     }
     c.prof = false;
     return o;

@@ -350,6 +350,7 @@ struct ProdDigits {
 };
 extern int g_prod_i8;
 bool prod_i8_ok(int K, int N);
+int prod_i8_pairs();   // digit pairs one int8 product sums (27 with six digits of A)
 void prod_digits_build(Ctx &c, const double *A, int lda, int K, int cols, int col0, ProdDigits &pd);
 int prod_i8_partials(Ctx &c, const ProdDigits &pd, int r0, int M, const double *B, int ldb, int N, int K,
                      DevBuf &work, double **part);
@@ -409,6 +410,7 @@ extern int g_pca_margin;   // extra Chebyshev degrees over the planned count (de
 struct PcaStats {
     int iters = 0; double resid = 0; double rate = 0; int block = 0; int blocks = 0;
     int krylov_steps = 0, krylov_dim = 0;   // block Krylov path (0: G formed)
+    int prod_pairs = 0;                     // int8 digit pairs of the products with C (0: fp64 products)
     const double *d_theta = nullptr;        // device copy of h_theta (valid until the next small problem)
 };
 extern int g_pca_krylov_min, g_pca_krylov_block, g_pca_krylov_steps, g_pca_over;

@@ -711,6 +711,7 @@ PcaStats pca_dev(Ctx &c, double *d_C, int n, int k, double *d_P, double *d_Pt, d
             h_theta.clear();
             st = PcaStats{};
             krylov_topk(c, d_C, c_col0, mext, n, k, V, d_P, h_theta, st, pd);
+            st.prod_pairs = pd ? prod_i8_pairs() : 0;
         }
     } else {
         Xc = c.buf[S_XC].as<double>((size_t)n * n);

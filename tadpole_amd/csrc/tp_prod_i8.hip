@@ -33,18 +33,28 @@
 
 namespace tp {
 
-// knob 36: the int8-digit products in the G-space Krylov path.  Off: within
-// ~1e-15 of sum |A||B| (test_prod_i8_digit_product), the C3 products 6.12 ms
-// against 6.42 for the fp64 k_gemm_ts, but C's digit image costs 0.27 ms a
-// pipeline: no net gain at C3
-int g_prod_i8 = 0;
+// knob 36: the int8-digit products in the G-space Krylov path (0: the fp64
+// k_gemm_ts).  Within ~1e-15 of sum |A||B| (test_prod_i8_digit_product); the
+// 32 C3 products 5.3 ms against 6.4
+int g_prod_i8 = 1;
 
 constexpr int PD_DIG = 7;   // digits per value
 typedef int pd_i32x4 __attribute__((ext_vector_type(4)));
 
-// Digits of x[k0..k0+3] (zero past K or when !ok): one 4-byte word per digit
+// Digit image layout (both operands): 64 columns x 64 k bytes per block, the
+// PD_DIG digit blocks of one (column tile, k step) contiguous --
+//   ((c / 64) nsteps + k / 64) PD_DIG 4096 + s 4096 + (c % 64) 64 + k % 64
+// -- so a workgroup's k step of A (64 rows, six digits) is one contiguous 24 KB
+// read (DRAM pages streamed, not 64-byte pieces of 384 columns).
+constexpr int PD_BLK = 4096;
+__device__ __forceinline__ size_t pd_off(int c, int k, int nsteps) {
+    return ((size_t)(c >> 6) * nsteps + (k >> 6)) * (PD_DIG * PD_BLK) + (size_t)(c & 63) * 64 + (k & 63);
+}
+
+// Digits of x[k0..k0+3] (zero past K or when !ok): one 4-byte word per digit,
+// digit s at d + s PD_BLK (d = the image at pd_off(c, k0))
 __device__ __forceinline__ void pd_digits4(const double *__restrict__ x, int K, int k0, bool ok, double sc,
-                                           int8_t *__restrict__ d, size_t slice) {
+                                           int8_t *__restrict__ d) {
     long long q[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -67,15 +77,15 @@ __device__ __forceinline__ void pd_digits4(const double *__restrict__ x, int K, 
         w[0] |= ((unsigned)(r & 0xFF)) << (8 * u);   // |r| <= 64
     }
 #pragma unroll
-    for (int s = 0; s < PD_DIG; ++s) *(unsigned *)(d + (size_t)s * slice + k0) = w[s];
+    for (int s = 0; s < PD_DIG; ++s) *(unsigned *)(d + (size_t)s * PD_BLK) = w[s];
 }
 
 // Digits of one column per workgroup: column c of X (K values, ld ldx) ->
-// D[s slice + c Kp + k] (k < Kp; zero past K and for c >= cols), the column
+// the image at pd_off(c, k) (k < Kp; zero past K and for c >= cols), the column
 // scale 2^(e - 54) into scale[c] (NaN for a non-finite column, so the product
 // is NaN as the fp64 one would be).
 __global__ void __launch_bounds__(256) k_pd_digits(const double *__restrict__ X, int ldx, int K, int cols, int Kp,
-                                                   size_t slice, int8_t *__restrict__ D, double *__restrict__ scale) {
+                                                   int8_t *__restrict__ D, double *__restrict__ scale) {
     __shared__ double red[4];
     const int c = blockIdx.x;
     const int t = threadIdx.x;
@@ -98,9 +108,53 @@ __global__ void __launch_bounds__(256) k_pd_digits(const double *__restrict__ X,
     if (mx > 0.0 && isfinite(mx)) (void)frexp(mx, &e);   // mx < 2^e
     const double sc = ldexp(1.0, 54 - e);
     if (t == 0) scale[c] = !live ? 0.0 : (isfinite(mx) ? ldexp(1.0, e - 54) : NAN);
-    int8_t *d = D + (size_t)c * Kp;
-    for (int k0 = 4 * t; k0 < Kp; k0 += 1024) pd_digits4(x, K, k0, live && isfinite(mx), sc, d, slice);
+    const int nsteps = Kp / 64;
+    for (int k0 = 4 * t; k0 < Kp; k0 += 1024) pd_digits4(x, K, k0, live && isfinite(mx), sc, D + pd_off(c, k0, nsteps));
 }
+
+// The same, for K <= 1024 IT: the column is read once (values kept in
+// registers across the max and the digits), thread t holding k = 1024 i + 4 t
+// .. + 3 -- one HBM pass over C instead of two (the second pass of k_pd_digits
+// misses L2 at C3: 1.87 GB moved for 0.9 GB of data)
+template <int IT>
+__global__ void __launch_bounds__(256) k_pd_digits_reg(const double *__restrict__ X, int ldx, int K, int cols, int Kp,
+                                                       int8_t *__restrict__ D, double *__restrict__ scale) {
+    __shared__ double red[4];
+    const int c = blockIdx.x;
+    const int t = threadIdx.x;
+    const double *x = X + (size_t)c * ldx;
+    const bool live = c < cols;
+    double v[IT][4];
+    double mx = 0.0;
+    bool bad = false;
+#pragma unroll
+    for (int i = 0; i < IT; ++i)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int k = 1024 * i + 4 * t + u;
+            v[i][u] = (live && k < K) ? x[k] : 0.0;
+            mx = fmax(mx, fabs(v[i][u]));
+            bad |= !isfinite(v[i][u]);
+        }
+    mx = bad ? INFINITY : mx;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
+    if ((t & 63) == 0) red[t >> 6] = mx;
+    __syncthreads();
+    mx = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+    int e = 0;
+    if (mx > 0.0 && isfinite(mx)) (void)frexp(mx, &e);   // mx < 2^e
+    const double sc = ldexp(1.0, 54 - e);
+    if (t == 0) scale[c] = !live ? 0.0 : (isfinite(mx) ? ldexp(1.0, e - 54) : NAN);
+    const bool ok = live && isfinite(mx);
+    const int nsteps = Kp / 64;
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+        const int k0 = 1024 * i + 4 * t;
+        if (k0 < Kp) pd_digits4(v[i], 4, 0, ok, sc, D + pd_off(c, k0, nsteps));
+    }
+}
+constexpr int PD_REG_IT = 8;   // register path up to K = 8192
 
 // The same digits for a few columns (a Krylov block, N = 64): the column's
 // largest |x| from per-1024-row partial maxima (k_pd_colmax), one workgroup
@@ -130,8 +184,8 @@ __global__ void __launch_bounds__(256) k_pd_colmax(const double *__restrict__ X,
     if (t == 0) pmax[blockIdx.x] = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
 }
 __global__ void __launch_bounds__(256) k_pd_digits_sl(const double *__restrict__ X, int ldx, int K, int Kp, int SL,
-                                                      const double *__restrict__ pmax, size_t slice,
-                                                      int8_t *__restrict__ D, double *__restrict__ scale) {
+                                                      const double *__restrict__ pmax, int8_t *__restrict__ D,
+                                                      double *__restrict__ scale) {
     const int c = blockIdx.x / SL, sl = blockIdx.x % SL;
     const int t = threadIdx.x;
     double mx = 0.0;
@@ -140,44 +194,40 @@ __global__ void __launch_bounds__(256) k_pd_digits_sl(const double *__restrict__
     if (mx > 0.0 && isfinite(mx)) (void)frexp(mx, &e);
     if (sl == 0 && t == 0) scale[c] = isfinite(mx) ? ldexp(1.0, e - 54) : NAN;
     const int k0 = sl * 1024 + 4 * t;
-    if (k0 < Kp) pd_digits4(X + (size_t)c * ldx, K, k0, isfinite(mx), ldexp(1.0, 54 - e), D + (size_t)c * Kp, slice);
+    if (k0 < Kp) pd_digits4(X + (size_t)c * ldx, K, k0, isfinite(mx), ldexp(1.0, 54 - e), D + pd_off(c, k0, Kp / 64));
 }
 
-// Out partials: rows [0, M) of A'B from the digit images Da (column i of A at
-// Da + i Kp, digit s at + s sla) and Db (N = 32 NWC columns).  4 waves, wave w
-// a 32 x 32 output block (2 x 2 MFMA tiles, seven accumulators each); the
-// workgroup covers 32 (4 / NWC) rows x N columns; blockIdx -> (row tile, k
-// chunk) dealt XCD-contiguously.  Each 64-byte k step of both digit images
-// (7 x 64 rows each) is staged through LDS (80-byte rows: the 16-lane b128
-// fragment reads spread over the banks), double-buffered: the global loads of
-// step k + 1 are issued before step k's 112 MFMAs a wave and written to the
-// other buffer after them (one barrier a step).  ~143 KB of LDS: one
-// workgroup a CU.
+// Out partials: rows [0, M) of A'B from the digit images Da (A's column tiles
+// from row 0 of Out on) and Db (the block's 64 columns), both in the pd_off
+// layout.  4 waves in 2 x 2, wave w a 32 x 32 output block (2 x 2 MFMA tiles,
+// seven accumulators each): 64 rows x 64 columns a workgroup; blockIdx ->
+// (row tile, k chunk) dealt XCD-contiguously.  Each 64-byte k step of both
+// images (PD_ADIG x 4 KB of A, 7 x 4 KB of B, each a contiguous run) is
+// staged through LDS (80-byte rows: the 16-lane b128 fragment reads spread
+// over the banks), double-buffered, with two k steps of loads in flight in two
+// register sets (one barrier a step; ~143 KB of LDS: one workgroup a CU).
 constexpr int PD_LD = 80;                        // LDS row stride (bytes)
 #ifndef TP_PD_ADIG
 #define TP_PD_ADIG 6   // digits of A read by the product (6: without the (6, 0) pair, A to 2^-49 of its column
                        // maximum: C3 products 6.63 -> 6.12 ms, errors 3e-17 -> 5e-16..9e-16 of sum |A||B|)
 #endif
 constexpr int PD_ADIG = TP_PD_ADIG;
-#ifndef TP_PD_NBUF
-#define TP_PD_NBUF 2   // 1: one LDS buffer, two workgroups a CU (spills; measured slower)
-#endif
-template <int NWC>
-__global__ void __launch_bounds__(256, 3 - TP_PD_NBUF) k_pd_prod(const int8_t *__restrict__ Da, size_t sla, int Kp, int M,
-                                                    const int8_t *__restrict__ Db, size_t slb,
-                                                    const double *__restrict__ rs, const double *__restrict__ cs,
-                                                    double *__restrict__ part, size_t pstride, int kchunk) {
-    constexpr int NWR = 4 / NWC, TMR = 32 * NWR, TN = 32 * NWC;
+constexpr int PD_ASZ = PD_ADIG * 64 * PD_LD, PD_BUF = PD_ASZ + PD_DIG * 64 * PD_LD;
+__global__ void __launch_bounds__(256, 1) k_pd_prod(const int8_t *__restrict__ Da, int Kp, int M,
+                                                    const int8_t *__restrict__ Db, const double *__restrict__ rs,
+                                                    const double *__restrict__ cs, double *__restrict__ part,
+                                                    size_t pstride, int kchunk) {
     extern __shared__ __attribute__((aligned(16))) int8_t pd_lds[];
-    const int tm = (M + TMR - 1) / TMR;
+    const int tm = (M + 63) / 64;
     const int total = (int)gridDim.x;
     const int xcd = (int)blockIdx.x & 7, slot = (int)blockIdx.x >> 3;
     const int Lg = xcd * (total >> 3) + min(xcd, total & 7) + slot;
     const int bm = Lg % tm, z = Lg / tm;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const int wr = w % NWR, wc = w / NWR;
+    const int wr = w & 1, wc = w >> 1;
     const int fr = lane & 15, fk = (lane >> 4) * 16;
     const int kbeg = z * kchunk, kend = min(Kp, kbeg + kchunk);
+    const int nsteps = Kp / 64;
     TP_DASSERT(Kp % 64 == 0 && kchunk % 64 == 0 && kend - kbeg >= 64);
     pd_i32x4 acc[PD_DIG][2][2];
 #pragma unroll
@@ -186,55 +236,44 @@ __global__ void __launch_bounds__(256, 3 - TP_PD_NBUF) k_pd_prod(const int8_t *_
         for (int a = 0; a < 2; ++a)
 #pragma unroll
             for (int b = 0; b < 2; ++b) acc[u][a][b] = pd_i32x4{0, 0, 0, 0};
-    // staging: thread t moves 16 bytes (k quarter t & 3) of row t >> 2 of every
-    // digit; A rows bm TMR + r (r < TMR, TMR / 64 chunks), B columns r < TN.
-    // A's rows past M read the zero-padded image (its columns are padded to
-    // 128 + a multiple of 128).
-    constexpr int RA = TMR / 64, RB = TN / 64 > 0 ? TN / 64 : 1;
+    // staging: thread t moves bytes 16 t .. 16 t + 15 of every 4 KB digit block
+    // (row t / 4, k quarter t % 4) of the step
     const int sr = t >> 2, sk = (t & 3) * 16;
-    const int8_t *ga = Da + (size_t)(bm * TMR + sr) * Kp + sk;
-    const int8_t *gb = Db + (size_t)sr * Kp + sk;
-    const bool bl = sr < TN;   // TN = 32: half the threads stage B
-    pd_i32x4 ra[PD_DIG][RA], rb[PD_DIG][RB];
-    auto gload = [&](int kb) {
+    const int8_t *ga = Da + (size_t)bm * nsteps * (PD_DIG * PD_BLK) + 16 * t;
+    const int8_t *gb = Db + 16 * t;
+    const int T = (kend - kbeg) / 64, st0 = kbeg / 64;
+    pd_i32x4 ra[PD_DIG], rb[PD_DIG], xa[PD_DIG], xb[PD_DIG];
+    // loads past the chunk re-read its last step (clamped, unconditional: the
+    // compiler counts them) and land in the buffer no later step reads
+    auto gload = [&](pd_i32x4 (&ta)[PD_DIG], pd_i32x4 (&tb)[PD_DIG], int st) {
+        const size_t o = (size_t)(st0 + min(st, T - 1)) * (PD_DIG * PD_BLK);
 #pragma unroll
         for (int s = 0; s < PD_DIG; ++s) {
-#pragma unroll
-            for (int q = 0; q < RA; ++q) ra[s][q] = *(const pd_i32x4 *)(ga + s * sla + (size_t)q * 64 * Kp + kb);
-#pragma unroll
-            for (int q = 0; q < RB; ++q)
-                rb[s][q] = bl ? *(const pd_i32x4 *)(gb + s * slb + (size_t)q * 64 * Kp + kb) : pd_i32x4{0, 0, 0, 0};
+            if (s < PD_ADIG) ta[s] = *(const pd_i32x4 *)(ga + o + s * PD_BLK);
+            tb[s] = *(const pd_i32x4 *)(gb + o + s * PD_BLK);
         }
     };
-    // LDS: stage buffer = [A digits: PD_DIG x 64 RA rows][B digits: PD_DIG x 64 RB rows], PD_LD bytes a row
-    constexpr int ASZ = PD_ADIG * 64 * RA * PD_LD;
-    auto lstore = [&](int buf) {
-        int8_t *L = pd_lds + buf * (ASZ + PD_DIG * 64 * RB * PD_LD);
+    auto lstore = [&](const pd_i32x4 (&ta)[PD_DIG], const pd_i32x4 (&tb)[PD_DIG], int bf) {
+        int8_t *L = pd_lds + bf * PD_BUF;
 #pragma unroll
         for (int s = 0; s < PD_DIG; ++s) {
-#pragma unroll
-            for (int q = 0; q < RA; ++q) *(pd_i32x4 *)(L + ((s * RA + q) * 64 + sr) * PD_LD + sk) = ra[s][q];
-#pragma unroll
-            for (int q = 0; q < RB; ++q)
-                if (bl) *(pd_i32x4 *)(L + ASZ + ((s * RB + q) * 64 + sr) * PD_LD + sk) = rb[s][q];
+            if (s < PD_ADIG) *(pd_i32x4 *)(L + (s * 64 + sr) * PD_LD + sk) = ta[s];
+            *(pd_i32x4 *)(L + PD_ASZ + (s * 64 + sr) * PD_LD + sk) = tb[s];
         }
     };
-    auto mstep = [&](int buf) {
-        const int8_t *L = pd_lds + buf * (ASZ + PD_DIG * 64 * RB * PD_LD);
-        // local row r of A (r < TMR) at (r / 64) * 64 + r % 64 == r in the
-        // [s][q][64] order: row (s RA + r / 64) 64 + r % 64 = s 64 RA + r
+    auto mstep = [&](int bf) {
+        const int8_t *L = pd_lds + bf * PD_BUF;
         pd_i32x4 fb[PD_DIG][2];
 #pragma unroll
         for (int tt = 0; tt < PD_DIG; ++tt)
 #pragma unroll
             for (int b = 0; b < 2; ++b)
-                fb[tt][b] = *(const pd_i32x4 *)(L + ASZ + (tt * 64 * RB + 32 * wc + 16 * b + fr) * PD_LD + fk);
+                fb[tt][b] = *(const pd_i32x4 *)(L + PD_ASZ + (tt * 64 + 32 * wc + 16 * b + fr) * PD_LD + fk);
 #pragma unroll
         for (int s0 = 0; s0 < PD_ADIG; ++s0) {
             pd_i32x4 fa[2];
 #pragma unroll
-            for (int a = 0; a < 2; ++a)
-                fa[a] = *(const pd_i32x4 *)(L + (s0 * 64 * RA + 32 * wr + 16 * a + fr) * PD_LD + fk);
+            for (int a = 0; a < 2; ++a) fa[a] = *(const pd_i32x4 *)(L + (s0 * 64 + 32 * wr + 16 * a + fr) * PD_LD + fk);
 #pragma unroll
             for (int tt = 0; tt + s0 < PD_DIG; ++tt)
 #pragma unroll
@@ -245,69 +284,24 @@ __global__ void __launch_bounds__(256, 3 - TP_PD_NBUF) k_pd_prod(const int8_t *_
                             __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[a], fb[tt][b], acc[s0 + tt][a][b], 0, 0, 0);
         }
     };
-#if TP_PD_NBUF == 2
-    // two staging register sets, two k steps of loads in flight (HBM latency
-    // under load is ~2 steps of MFMAs); loads past the chunk re-read its last
-    // step (clamped, unconditional: the compiler counts them) and land in the
-    // buffer no later step reads
-    const int T = (kend - kbeg) / 64;
-    pd_i32x4 xa[PD_DIG][RA], xb[PD_DIG][RB];
-    auto gload2 = [&](pd_i32x4 (&ta)[PD_DIG][RA], pd_i32x4 (&tb)[PD_DIG][RB], int st) {
-        const int kb = kbeg + 64 * min(st, T - 1);
-#pragma unroll
-        for (int s = 0; s < PD_DIG; ++s) {
-#pragma unroll
-            for (int q = 0; q < RA; ++q)
-                if (s < PD_ADIG) ta[s][q] = *(const pd_i32x4 *)(ga + s * sla + (size_t)q * 64 * Kp + kb);
-#pragma unroll
-            for (int q = 0; q < RB; ++q) tb[s][q] = *(const pd_i32x4 *)(gb + s * slb + (size_t)q * 64 * Kp + kb);
-        }
-    };
-    auto lstore2 = [&](const pd_i32x4 (&ta)[PD_DIG][RA], const pd_i32x4 (&tb)[PD_DIG][RB], int bf) {
-        int8_t *L = pd_lds + bf * (ASZ + PD_DIG * 64 * RB * PD_LD);
-#pragma unroll
-        for (int s = 0; s < PD_DIG; ++s) {
-#pragma unroll
-            for (int q = 0; q < RA; ++q)
-                if (s < PD_ADIG) *(pd_i32x4 *)(L + ((s * RA + q) * 64 + sr) * PD_LD + sk) = ta[s][q];
-#pragma unroll
-            for (int q = 0; q < RB; ++q) *(pd_i32x4 *)(L + ASZ + ((s * RB + q) * 64 + sr) * PD_LD + sk) = tb[s][q];
-        }
-    };
-    static_assert(TN == 64, "two-step prefetch: every thread stages B (TN = 64)");
-    (void)gload;
-    (void)lstore;
-    gload2(ra, rb, 0);
-    lstore2(ra, rb, 0);
-    gload2(ra, rb, 1);
-    gload2(xa, xb, 2);
+    gload(ra, rb, 0);
+    lstore(ra, rb, 0);
+    gload(ra, rb, 1);
+    gload(xa, xb, 2);
     __syncthreads();
     for (int st = 0;; st += 2) {
         mstep(0);                // step st
-        lstore2(ra, rb, 1);      // step st + 1
+        lstore(ra, rb, 1);       // step st + 1
         __syncthreads();
-        gload2(ra, rb, st + 3);
+        gload(ra, rb, st + 3);
         if (st + 1 >= T) break;
         mstep(1);                // step st + 1
-        lstore2(xa, xb, 0);      // step st + 2
+        lstore(xa, xb, 0);       // step st + 2
         __syncthreads();
-        gload2(xa, xb, st + 4);
+        gload(xa, xb, st + 4);
         if (st + 2 >= T) break;
     }
-#else
-    gload(kbeg);
-    lstore(0);
-    __syncthreads();
-    for (int kb = kbeg; kb < kend; kb += 64) {
-        const bool more = kb + 64 < kend;
-        if (more) gload(kb + 64);
-        mstep(0);
-        __syncthreads();   // one buffer: two workgroups a CU overlap each other's waits
-        if (more) lstore(0);
-        __syncthreads();
-    }
-#endif
-    const int i0 = bm * TMR + 32 * wr, j0 = 32 * wc;
+    const int i0 = bm * 64 + 32 * wr, j0 = 32 * wc;
     double *P = part + pstride * z;
 #pragma unroll
     for (int a = 0; a < 2; ++a)
@@ -326,12 +320,6 @@ __global__ void __launch_bounds__(256, 3 - TP_PD_NBUF) k_pd_prod(const int8_t *_
             }
 }
 
-// two stages of both digit images
-static size_t pd_lds_bytes(int nwc) {
-    const int ra = 128 / nwc / 64, rb = std::max(1, 32 * nwc / 64);
-    return (size_t)TP_PD_NBUF * 64 * (PD_ADIG * ra + PD_DIG * rb) * PD_LD;
-}
-
 // k chunks from K alone (shards agree); <= 16384 rows a chunk (accumulator range)
 #ifndef TP_PD_KDIV
 #define TP_PD_KDIV 960   // C3: 8 k chunks, 984 workgroups (~4 full rounds of one a CU; 1024: 7, 861)
@@ -342,8 +330,13 @@ static int pd_kchunk(int Kp) {
     return std::min(kc, 16384);
 }
 
-// N = 64 (the G-space Krylov blocks); the 32-column tile's A stage (128 rows)
-// would not fit two stages in LDS
+int prod_i8_pairs() {
+    int n = 0;
+    for (int a = 0; a < PD_ADIG; ++a) n += PD_DIG - a;
+    return n;
+}
+
+// N = 64 (the G-space Krylov blocks; the kernel's workgroup is 64 x 64)
 bool prod_i8_ok(int K, int N) { return N == 64 && K >= 64; }
 
 void prod_digits_build(Ctx &c, const double *A, int lda, int K, int cols, int col0, ProdDigits &pd) {
@@ -351,14 +344,19 @@ void prod_digits_build(Ctx &c, const double *A, int lda, int K, int cols, int co
     pd.Kp = (K + 63) / 64 * 64;
     pd.col0 = col0;
     pd.cols = cols;
-    // + 128: a shard's row tiles (from any row) stay inside the padded image
-    const int cp = (cols + 127) / 128 * 128 + 128;
-    pd.slice = (size_t)cp * pd.Kp;
+    // whole 64-column tiles (zero past cols); a product's row tiles start on a
+    // tile (prod_i8_partials)
+    const int cp = (cols + 63) / 64 * 64;
+    pd.slice = (size_t)cp * pd.Kp;   // bytes of one digit over the image
     char *base = c.buf[S_PDIGA].as<char>(PD_DIG * pd.slice + (size_t)cp * sizeof(double) + 256);
     pd.d = (int8_t *)base;
     pd.rs = (double *)(base + (PD_DIG * pd.slice + 255) / 256 * 256);
-    hipLaunchKernelGGL(k_pd_digits, dim3((unsigned)cp), dim3(256), 0, s, A, lda, K, cols, pd.Kp, pd.slice,
-                       (int8_t *)pd.d, (double *)pd.rs);
+    if (pd.Kp <= 1024 * PD_REG_IT)
+        hipLaunchKernelGGL(k_pd_digits_reg<PD_REG_IT>, dim3((unsigned)cp), dim3(256), 0, s, A, lda, K, cols, pd.Kp,
+                           (int8_t *)pd.d, (double *)pd.rs);
+    else
+        hipLaunchKernelGGL(k_pd_digits, dim3((unsigned)cp), dim3(256), 0, s, A, lda, K, cols, pd.Kp, (int8_t *)pd.d,
+                           (double *)pd.rs);
     TP_HIP(hipGetLastError());
 }
 
@@ -367,8 +365,9 @@ void prod_digits_build(Ctx &c, const double *A, int lda, int K, int cols, int co
 int prod_i8_partials(Ctx &c, const ProdDigits &pd, int r0, int M, const double *B, int ldb, int N, int K,
                      DevBuf &work, double **part) {
     hipStream_t s = c.cur;
-    if (!prod_i8_ok(K, N) || (K + 63) / 64 * 64 != pd.Kp || r0 < pd.col0 || r0 + M > pd.col0 + pd.cols)
-        fail(TP_ERR_ARG, "prod_i8: rows outside the digit image, or an unsupported block");
+    if (!prod_i8_ok(K, N) || (K + 63) / 64 * 64 != pd.Kp || r0 < pd.col0 || r0 + M > pd.col0 + pd.cols ||
+        (r0 - pd.col0) % 64)
+        fail(TP_ERR_ARG, "prod_i8: rows outside the digit image or off its 64-column tiles, or an unsupported block");
     const size_t slb = (size_t)N * pd.Kp;
     char *bb = c.buf[S_PDIGB].as<char>(PD_DIG * slb + 256 + 512 * sizeof(double) +
                                         (size_t)N * ((pd.Kp + 1023) / 1024) * sizeof(double));
@@ -376,18 +375,23 @@ int prod_i8_partials(Ctx &c, const ProdDigits &pd, int r0, int M, const double *
     double *cs = (double *)(bb + (PD_DIG * slb + 255) / 256 * 256);
     const int SL = (pd.Kp + 1023) / 1024;
     double *pmax = (double *)(bb + (PD_DIG * slb + 255) / 256 * 256 + 512 * sizeof(double));
-    hipLaunchKernelGGL(k_pd_colmax, dim3((unsigned)(N * SL)), dim3(256), 0, s, B, ldb, K, SL, pmax);
-    hipLaunchKernelGGL(k_pd_digits_sl, dim3((unsigned)(N * SL)), dim3(256), 0, s, B, ldb, K, pd.Kp, SL, pmax, slb, Db,
-                       cs);
+    if (pd.Kp <= 1024 * PD_REG_IT) {   // one launch, the block read once
+        hipLaunchKernelGGL(k_pd_digits_reg<PD_REG_IT>, dim3((unsigned)N), dim3(256), 0, s, B, ldb, K, N, pd.Kp, Db,
+                           cs);
+    } else {
+        hipLaunchKernelGGL(k_pd_colmax, dim3((unsigned)(N * SL)), dim3(256), 0, s, B, ldb, K, SL, pmax);
+        hipLaunchKernelGGL(k_pd_digits_sl, dim3((unsigned)(N * SL)), dim3(256), 0, s, B, ldb, K, pd.Kp, SL, pmax, Db,
+                           cs);
+    }
     const int kc = pd_kchunk(pd.Kp);
     const int S = (pd.Kp + kc - 1) / kc;
     const size_t pstride = (size_t)M * N;
     *part = work.as<double>(pstride * S);
-    const int8_t *Da = pd.d + (size_t)(r0 - pd.col0) * pd.Kp;
+    const int8_t *Da = pd.d + (size_t)(r0 - pd.col0) * pd.Kp * PD_DIG;   // whole tiles: 64 columns x Kp x PD_DIG
     const double *rs = pd.rs + (r0 - pd.col0);
     const int tm = (M + 63) / 64;
-    hipLaunchKernelGGL(k_pd_prod<2>, dim3((unsigned)(tm * S)), dim3(256), pd_lds_bytes(2), s, Da, pd.slice, pd.Kp, M,
-                       Db, slb, rs, cs, *part, pstride, kc);
+    hipLaunchKernelGGL(k_pd_prod, dim3((unsigned)(tm * S)), dim3(256), (size_t)2 * PD_BUF, s, Da, pd.Kp, M, Db, rs,
+                       cs, *part, pstride, kc);
     TP_HIP(hipGetLastError());
     return S;
 }

@@ -430,7 +430,8 @@ void cor_product(Ctx &c, const double *X, int n, const double *m, const GatherSt
 // the packed T (N x M col-major = Out row-major), gathered, transposed back.
 void rows_gemm_sharded(Ctx &c, const double *A, int lda, int M, const double *B, int ldb, int N, int K,
                        double *Out, int splitk_plain, int tag, const R1 *r1, int a_col0, const ProdDigits *pd) {
-    const bool i8 = pd && pd->d && prod_i8_ok(K, N) && splitk_plain <= 1;
+    // int8 digits: row shards (the rows plan's 64-row blocks) start on the image's 64-column tiles
+    const bool i8 = pd && pd->d && prod_i8_ok(K, N) && splitk_plain <= 1 && pd->col0 % 64 == 0;
     if (!c.shard.active) {
         if (a_col0 != 0) fail(TP_ERR_ARG, "rows_gemm_sharded: a column slab needs the sharded schedule");
         if (i8 && r1) {   // int8-digit partials, then the fp64 path's rank-1 reduction

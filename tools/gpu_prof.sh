@@ -11,7 +11,7 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
 rc=$?; echo "trace rc=$rc"; [ $rc -eq 0 ] || exit $rc
 cut -c1-400 gpurun_out/prof_bench.json
 [ -n "$TRACE_ONLY" ] && exit 0
-RX="k_coniss|k_gemm|k_splitk|k_ch|k_seed|k_xtx|k_cor|k_mask|k_sytrd|k_trS"
+RX="k_coniss|k_gemm|k_splitk|k_ch|k_seed|k_xtx|k_cor|k_mask|k_sytrd|k_trS|k_pd_"
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$RX" --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 $B > gpurun_out/pmc_fetch.log 2>&1
 rc=$?; echo "fetch rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$RX" --output-format csv -d gpurun_out/pmc_write -o run -- python3 $B > gpurun_out/pmc_write.log 2>&1
