@@ -213,7 +213,10 @@ constexpr int PD_LD = 80;                        // LDS row stride (bytes)
 #endif
 constexpr int PD_ADIG = TP_PD_ADIG;
 constexpr int PD_ASZ = PD_ADIG * 64 * PD_LD, PD_BUF = PD_ASZ + PD_DIG * 64 * PD_LD;
-__global__ void __launch_bounds__(256, 1) k_pd_prod(const int8_t *__restrict__ Da, int Kp, int M,
+// NB = 1: one LDS buffer (66.5 KB), one step of loads ahead, two workgroups a
+// CU (each one's MFMAs run under the other's waits)
+template <int NB>
+__global__ void __launch_bounds__(256, 3 - NB) k_pd_prod(const int8_t *__restrict__ Da, int Kp, int M,
                                                     const int8_t *__restrict__ Db, const double *__restrict__ rs,
                                                     const double *__restrict__ cs, double *__restrict__ part,
                                                     size_t pstride, int kchunk) {
@@ -284,22 +287,37 @@ __global__ void __launch_bounds__(256, 1) k_pd_prod(const int8_t *__restrict__ D
                             __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[a], fb[tt][b], acc[s0 + tt][a][b], 0, 0, 0);
         }
     };
-    gload(ra, rb, 0);
-    lstore(ra, rb, 0);
-    gload(ra, rb, 1);
-    gload(xa, xb, 2);
-    __syncthreads();
-    for (int st = 0;; st += 2) {
-        mstep(0);                // step st
-        lstore(ra, rb, 1);       // step st + 1
+    if constexpr (NB == 1) {
+        (void)xa;
+        (void)xb;
+        gload(ra, rb, 0);
+        lstore(ra, rb, 0);
         __syncthreads();
-        gload(ra, rb, st + 3);
-        if (st + 1 >= T) break;
-        mstep(1);                // step st + 1
-        lstore(xa, xb, 0);       // step st + 2
+        for (int st = 0; st < T; ++st) {
+            gload(ra, rb, st + 1);
+            mstep(0);
+            __syncthreads();
+            lstore(ra, rb, 0);
+            __syncthreads();
+        }
+    } else {
+        gload(ra, rb, 0);
+        lstore(ra, rb, 0);
+        gload(ra, rb, 1);
+        gload(xa, xb, 2);
         __syncthreads();
-        gload(xa, xb, st + 4);
-        if (st + 2 >= T) break;
+        for (int st = 0;; st += 2) {
+            mstep(0);                // step st
+            lstore(ra, rb, 1);       // step st + 1
+            __syncthreads();
+            gload(ra, rb, st + 3);
+            if (st + 1 >= T) break;
+            mstep(1);                // step st + 1
+            lstore(xa, xb, 0);       // step st + 2
+            __syncthreads();
+            gload(xa, xb, st + 4);
+            if (st + 2 >= T) break;
+        }
     }
     const int i0 = bm * 64 + 32 * wr, j0 = 32 * wc;
     double *P = part + pstride * z;
@@ -390,8 +408,12 @@ int prod_i8_partials(Ctx &c, const ProdDigits &pd, int r0, int M, const double *
     const int8_t *Da = pd.d + (size_t)(r0 - pd.col0) * pd.Kp * PD_DIG;   // whole tiles: 64 columns x Kp x PD_DIG
     const double *rs = pd.rs + (r0 - pd.col0);
     const int tm = (M + 63) / 64;
-    hipLaunchKernelGGL(k_pd_prod, dim3((unsigned)(tm * S)), dim3(256), (size_t)2 * PD_BUF, s, Da, pd.Kp, M, Db, rs,
-                       cs, *part, pstride, kc);
+    if (g_prod_i8 == 2)   // A/B: one buffer, two workgroups a CU
+        hipLaunchKernelGGL(k_pd_prod<1>, dim3((unsigned)(tm * S)), dim3(256), (size_t)PD_BUF, s, Da, pd.Kp, M, Db, rs,
+                           cs, *part, pstride, kc);
+    else
+        hipLaunchKernelGGL(k_pd_prod<2>, dim3((unsigned)(tm * S)), dim3(256), (size_t)2 * PD_BUF, s, Da, pd.Kp, M, Db,
+                           rs, cs, *part, pstride, kc);
     TP_HIP(hipGetLastError());
     return S;
 }
