@@ -1642,8 +1642,8 @@ extern "C" {
  * Gram matrices of 64-column blocks by k_gram64 (0: the split-K GEMM; same bits), 30 the next N
  * sharded waits with a live communicator fail as device errors (failure-containment tests), 31 the
  * bins from which knob 20 = -1 (default) takes the Krylov space of C, ..., 36 the Krylov products with
- * C on the int8 MFMA from digit images (1, default; 2: the one-buffer two-workgroup kernel; 0: the fp64
- * k_gemm_ts). */
+ * C on the int8 MFMA from digit images (1, default: one LDS buffer, two workgroups a CU; 2: the
+ * double-buffered one-workgroup kernel; 0: the fp64 k_gemm_ts). */
 void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
     guarded(status, [&] {
         int *p = nullptr;

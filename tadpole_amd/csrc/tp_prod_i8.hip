@@ -34,8 +34,9 @@
 namespace tp {
 
 // knob 36: the int8-digit products in the G-space Krylov path (0: the fp64
-// k_gemm_ts).  Within ~1e-15 of sum |A||B| (test_prod_i8_digit_product); the
-// 32 C3 products 5.3 ms against 6.4
+// k_gemm_ts; 2: the double-buffered kernel).  Within ~1e-15 of sum |A||B|
+// (test_prod_i8_digit_product); the 32 C3 products 4.6 ms against 6.3
+// 
 int g_prod_i8 = 1;
 
 constexpr int PD_DIG = 7;   // digits per value
@@ -120,7 +121,10 @@ template <int IT>
 __global__ void __launch_bounds__(256) k_pd_digits_reg(const double *__restrict__ X, int ldx, int K, int cols, int Kp,
                                                        int8_t *__restrict__ D, double *__restrict__ scale) {
     __shared__ double red[4];
-    const int c = blockIdx.x;
+    // adjacent columns on one XCD (workgroups are dealt round-robin over the 8):
+    // columns c and c + 1 fill the two halves of each 128-byte line of the image
+    // in the same L2 (gridDim.x is a multiple of 64)
+    const int c = (int)(blockIdx.x & 7) * (int)(gridDim.x >> 3) + (int)(blockIdx.x >> 3);
     const int t = threadIdx.x;
     const double *x = X + (size_t)c * ldx;
     const bool live = c < cols;
@@ -408,12 +412,14 @@ int prod_i8_partials(Ctx &c, const ProdDigits &pd, int r0, int M, const double *
     const int8_t *Da = pd.d + (size_t)(r0 - pd.col0) * pd.Kp * PD_DIG;   // whole tiles: 64 columns x Kp x PD_DIG
     const double *rs = pd.rs + (r0 - pd.col0);
     const int tm = (M + 63) / 64;
-    if (g_prod_i8 == 2)   // A/B: one buffer, two workgroups a CU
-        hipLaunchKernelGGL(k_pd_prod<1>, dim3((unsigned)(tm * S)), dim3(256), (size_t)PD_BUF, s, Da, pd.Kp, M, Db, rs,
-                           cs, *part, pstride, kc);
-    else
+    // one LDS buffer, two workgroups a CU: the 32 C3 products 4.57 ms against
+    // 5.35 for the double-buffered one-workgroup form (knob 36 = 2, A/B)
+    if (g_prod_i8 == 2)
         hipLaunchKernelGGL(k_pd_prod<2>, dim3((unsigned)(tm * S)), dim3(256), (size_t)2 * PD_BUF, s, Da, pd.Kp, M, Db,
                            rs, cs, *part, pstride, kc);
+    else
+        hipLaunchKernelGGL(k_pd_prod<1>, dim3((unsigned)(tm * S)), dim3(256), (size_t)PD_BUF, s, Da, pd.Kp, M, Db, rs,
+                           cs, *part, pstride, kc);
     TP_HIP(hipGetLastError());
     return S;
 }
