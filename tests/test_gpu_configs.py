@@ -66,14 +66,16 @@ def test_config_golden(gpu, name):
     assert got.timings_ms[13] <= 1e-11
 
 
-def test_config_c3_golden_int8_products(gpu):
-    """C3 with the Krylov products on the int8 MFMA (7-digit images of C and of
-    each block, knob 36): the golden's n_pcs, clusters, merge order and every
-    level, CH within 1e-6."""
+@pytest.mark.parametrize("prod", [0, 2])
+def test_config_c3_golden_product_paths(gpu, prod):
+    """C3 with the Krylov products on the paths the default does not take
+    (knob 36: 0 the fp64 k_gemm_ts, 2 the double-buffered int8-digit kernel;
+    the default, the one-buffer int8 kernel, is test_config_golden): the
+    golden's n_pcs, clusters, merge order and every level, CH within 1e-6."""
     import tadpole_amd as tp
     z = np.load(os.path.join(GOLD, "c3.npz"))
     m = synth_hic(int(z["n0"]), int(z["seed"]))
-    old = G.knob(36, 1)
+    old = G.knob(36, prod)
     try:
         got = tp.TADpole(m, max_pcs=200)
     finally:
@@ -112,7 +114,7 @@ def test_pca_krylov_path_vs_lapack(gpu, forced, space):
     old20 = G.knob(20, 1 if space.startswith("C") else 0)
     old28 = G.knob(28, 0 if space == "G-full-cgs" else 1)
     old33 = G.knob(33, 0 if space == "C-full-pip" else 1)
-    old36 = G.knob(36, 1 if space == "G-int8" else 0)
+    old36 = G.knob(36, 1 if space == "G-int8" else 0)   # the other spaces on the fp64 products
     try:
         p, _ = G.pca(c, 200)
     finally:
