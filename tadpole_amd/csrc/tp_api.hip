@@ -1536,7 +1536,7 @@ void tp_debug_sytrd(const double *H, const int *b, double *ms, long long *stamps
         float t = 0;
         TP_HIP(hipEventElapsedTime(&t, e0, e1));
         *ms = t;
-        TP_HIP(hipMemcpy(stamps, dst, 3 * sizeof(long long), hipMemcpyDeviceToHost));
+        TP_HIP(hipMemcpy(stamps, dst, 4 * sizeof(long long), hipMemcpyDeviceToHost));
         (void)hipEventDestroy(e0);
         (void)hipEventDestroy(e1);
     });
@@ -1684,6 +1684,7 @@ void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
         case 34: p = &g_xtx_nz; break;
         case 35: p = &g_gemm_ts_pf2; break;
         case 36: p = &g_prod_i8; break;
+        case 37: p = &g_sytrd32; break;
         default: fail(TP_ERR_ARG, "unknown knob");
         }
         if (*which == 3 && *value != 16 && *value != 32) fail(TP_ERR_ARG, "stage depth must be 16 or 32");

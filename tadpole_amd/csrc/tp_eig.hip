@@ -486,6 +486,312 @@ __global__ void __launch_bounds__(1024) k_sytrd_reg(double *A, int b, double *d,
 }
 bool sytrd_reg_supported(int b) { return b >= 16 && b <= 256 && b % 16 == 0; }
 
+// ---------------------------------------------------------------------------
+// k_sytrd32: the same reduction and outputs (LAPACK dsytd2 'L'), b <= 256,
+// with the upper triangle in registers as 32 x 32 tiles and three barriers a
+// step.  Built to cut the per-step cost of k_sytrd_reg (~14 k cycles: the
+// 16 x 16 tiles need a 16-lane reduction per tile row, and wave 0 alone forms
+// the reflector and assembles p in long LDS chains while 15 waves wait).
+//
+// Lane l of a tile holds the 4 x 4 block rows 4 ra .. 4 ra + 3, columns
+// 4 cb .. 4 cb + 3 (ra = l & 7, cb = l >> 3), so a tile's row partials of
+// p = A v reduce over lane bits 3..5 (row_ror:8, permlane16/32 swaps) and
+// its column partials over bits 0..2 (quad perms, one swizzle), each as a
+// reduce-scatter: 4 values -> 1 over three levels, 4 exchanges instead of 12.
+// The 36 tiles of b = 256 are dealt round-robin to 12 waves in the order
+// (tile row descending, column ascending): at every step the live tiles
+// (tile row >= j / 32) are a prefix of that order, so each wave's live tiles
+// are a prefix of its slots and the work stays balanced as it shrinks.
+// Step j:
+//   1. every wave forms the reflector from row j (published in LDS) -- no
+//      barrier between the reflector and the product; wave 0 stores it and v;
+//   2. per live tile, row and column partials of A v          -> LDS, B1
+//   3. waves 0..3 sum the partials of p (fixed order), tau, p'v -> LDS, B2
+//   4. w = p - (tau/2)(p'v) v; every live tile A -= v w' + w v'; the owners
+//      of row j + 1 publish it                                         B0
+// ST: diagnostic build with s_memtime stamps (phases 1..4 of wave 0).
+// ---------------------------------------------------------------------------
+constexpr int S32_W = 12;      // waves
+constexpr int S32_SL = 3;      // tiles a wave: 36 of b = 256 over 12 waves
+
+__device__ __forceinline__ double swap16_sum(double a, double b) {   // even rows: a + a[l^16]; odd: b + b[l^16]
+    auto lo = __builtin_amdgcn_permlane16_swap(__double2loint(a), __double2loint(b), false, false);
+    auto hi = __builtin_amdgcn_permlane16_swap(__double2hiint(a), __double2hiint(b), false, false);
+    return __hiloint2double(hi[0], lo[0]) + __hiloint2double(hi[1], lo[1]);
+}
+__device__ __forceinline__ double swap32_sum(double a, double b) {   // lanes < 32: a + a[l^32]; else b + b[l^32]
+    auto lo = __builtin_amdgcn_permlane32_swap(__double2loint(a), __double2loint(b), false, false);
+    auto hi = __builtin_amdgcn_permlane32_swap(__double2hiint(a), __double2hiint(b), false, false);
+    return __hiloint2double(hi[0], lo[0]) + __hiloint2double(hi[1], lo[1]);
+}
+__device__ __forceinline__ double swz_xor4(double v) {   // v[l ^ 4] (ds_swizzle bitmask mode)
+    const int lo = __builtin_amdgcn_ds_swizzle(__double2loint(v), 0x101F);
+    const int hi = __builtin_amdgcn_ds_swizzle(__double2hiint(v), 0x101F);
+    return __hiloint2double(hi, lo);
+}
+
+// 1 / x by the hardware reciprocal and two Newton steps (within an ulp or
+// two: a reflector's scale and tau need no correct rounding)
+__device__ __forceinline__ double rcp_nr(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    r = r * fma(-x, r, 2.0);
+    return r * fma(-x, r, 2.0);
+}
+
+template <bool ST>
+__global__ void __launch_bounds__(64 * S32_W) k_sytrd32(double *A, int b, double *d, double *e, double *tau,
+                                                         long long *stamps) {
+    __shared__ double xrow[256], vs[256], ps[256];
+    __shared__ double rowp[8][8][32];   // [I][K][row of block I]: row partials of tile (I, K)
+    __shared__ double colp[8][8][32];   // [I][K][column of block K]: column partials of tile (I, K), I < K
+    __shared__ double pvp[4], fin[2];
+    long long sacc[4] = {0, 0, 0, 0};
+    long long st0 = ST ? (long long)__builtin_amdgcn_s_memtime() : 0;
+#define S32_STAMP(ph)                                                     \
+    if (ST) {                                                             \
+        long long _t = (long long)__builtin_amdgcn_s_memtime();           \
+        sacc[ph] += _t - st0;                                             \
+        st0 = _t;                                                         \
+    }
+    const int t = threadIdx.x, l = t & 63;
+    const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int ra = l & 7, cb = l >> 3;
+    const int bp = (b + 31) & ~31, T = bp >> 5;
+    const int ntile = T * (T + 1) / 2;
+    // slot s of wave w: list index s * S32_W + w, list = tile rows descending,
+    // columns ascending; row I holds indices [N(I+1), N(I)), N(I) = (T-I)(T-I+1)/2
+    int tI[S32_SL], tK[S32_SL];
+#pragma unroll
+    for (int s = 0; s < S32_SL; ++s) {
+        int id = s * S32_W + w, I = T - 1, cnt = 1;
+        if (id < ntile) {
+            while (id >= cnt) {
+                id -= cnt;
+                --I;
+                ++cnt;
+            }
+            tI[s] = __builtin_amdgcn_readfirstlane(I);
+            tK[s] = __builtin_amdgcn_readfirstlane(I + id);
+        } else {
+            tI[s] = -1;
+            tK[s] = -1;
+        }
+    }
+    // re-materialised at each use: keeps per-slot addresses from being hoisted
+    // out of the step loop (and spilled)
+#define S32_I(s) sy_opaque(tI[s])
+#define S32_K(s) sy_opaque(tK[s])
+    for (int q = t; q < 256; q += 64 * S32_W) xrow[q] = vs[q] = ps[q] = 0.0;
+    for (int q = t; q < 8 * 8 * 32; q += 64 * S32_W) (&rowp[0][0][0])[q] = (&colp[0][0][0])[q] = 0.0;
+    __syncthreads();
+    double x[S32_SL][4][4];
+#pragma unroll
+    for (int s = 0; s < S32_SL; ++s)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int R = 32 * tI[s] + 4 * ra + i, C = 32 * tK[s] + 4 * cb + k;
+                x[s][i][k] = (tI[s] >= 0 && R < b && C < b) ? A[(size_t)min(R, C) * b + max(R, C)] : 0.0;
+            }
+    // row 0 -> LDS (tile row 0 = the tail of the list)
+#pragma unroll
+    for (int s = 0; s < S32_SL; ++s)
+        if (tI[s] == 0 && ra == 0)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) xrow[32 * tK[s] + 4 * cb + k] = x[s][0][k];
+    __syncthreads();   // every load of A done before reflectors overwrite it
+    const bool h0 = l & 1, h1 = l & 2, h3 = l & 8, h4 = l & 16;
+
+    for (int j = 0; j + 2 < b; ++j) {
+        const int J = j >> 5;
+        const int nlive = (T - J) * (T - J + 1) / 2;
+        // ---- 1. reflector (dlarfg) from row j, every wave: v for this lane's
+        //      four positions -> LDS (every wave writes the same words; a wave
+        //      then reads back its own writes, in order: no barrier)
+        double xv[4];
+        {
+            const double2 a0 = *(const double2 *)&xrow[4 * l], a1 = *(const double2 *)&xrow[4 * l + 2];
+            xv[0] = a0.x; xv[1] = a0.y; xv[2] = a1.x; xv[3] = a1.y;
+        }
+        const double alpha = xrow[j + 1];
+        double sq[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) sq[u] = (4 * l + u >= j + 2 && 4 * l + u < b) ? xv[u] * xv[u] : 0.0;
+        const double xnorm2 = wave_sum((sq[0] + sq[1]) + (sq[2] + sq[3]));
+        double beta, tj, scale;
+        if (xnorm2 == 0.0) {
+            beta = alpha;
+            tj = 0.0;
+            scale = 0.0;
+        } else {
+            beta = -copysign(sqrt(fma(alpha, alpha, xnorm2)), alpha);
+            tj = (beta - alpha) * rcp_nr(beta);
+            scale = rcp_nr(alpha - beta);
+        }
+        double vv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int c = 4 * l + u;
+            vv[u] = c == j + 1 ? 1.0 : ((c > j + 1 && c < b) ? xv[u] * scale : 0.0);
+        }
+        *(double2 *)&vs[4 * l] = make_double2(vv[0], vv[1]);
+        *(double2 *)&vs[4 * l + 2] = make_double2(vv[2], vv[3]);
+        if (w == 0) {
+            // column j of A below the diagonal <- v (rows <= j + 1 get 0 / 1:
+            // the reflector's implicit entries, never read back; every input
+            // element was loaded before the loop)
+            if (4 * l + 3 < b && (b & 1) == 0) {
+                *(double2 *)&A[(size_t)j * b + 4 * l] = make_double2(vv[0], vv[1]);
+                *(double2 *)&A[(size_t)j * b + 4 * l + 2] = make_double2(vv[2], vv[3]);
+            } else {
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (4 * l + u < b) A[(size_t)j * b + 4 * l + u] = vv[u];
+            }
+            if (l == 0) {
+                d[j] = xrow[j];
+                e[j] = beta;
+                tau[j] = tj;
+            }
+        }
+        S32_STAMP(0);
+        // ---- 2. partials of A v over the live tiles
+#pragma unroll
+        for (int s = 0; s < S32_SL; ++s) {
+            if (s * S32_W + w < nlive) {
+                const int I = S32_I(s), K = S32_K(s);
+                const int r0 = 32 * I + 4 * ra, c0 = 32 * K + 4 * cb;
+                double vr[4], vc[4];
+                {
+                    const double2 a0 = *(const double2 *)&vs[r0], a1 = *(const double2 *)&vs[r0 + 2];
+                    const double2 b0 = *(const double2 *)&vs[c0], b1 = *(const double2 *)&vs[c0 + 2];
+                    vr[0] = a0.x; vr[1] = a0.y; vr[2] = a1.x; vr[3] = a1.y;
+                    vc[0] = b0.x; vc[1] = b0.y; vc[2] = b1.x; vc[3] = b1.y;
+                }
+                double rp[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    rp[i] = fma(x[s][i][3], vc[3], fma(x[s][i][2], vc[2], fma(x[s][i][1], vc[1], x[s][i][0] * vc[0])));
+                {   // reduce-scatter over cb (lane bits 3, 4, 5)
+                    const double s0 = h3 ? rp[0] : rp[2], s1 = h3 ? rp[1] : rp[3];
+                    const double k0 = h3 ? rp[2] : rp[0], k1 = h3 ? rp[3] : rp[1];
+                    const double t0 = k0 + dpp_d<0x128>(s0), t1 = k1 + dpp_d<0x128>(s1);
+                    const double u = swap16_sum(t0, t1);
+                    const double tot = swap32_sum(u, u);
+                    if (l < 32) rowp[I][K][4 * ra + (h3 ? 2 : 0) + (h4 ? 1 : 0)] = tot;
+                }
+                if (I != K) {
+                    double cp[4];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        cp[k] = fma(x[s][3][k], vr[3], fma(x[s][2][k], vr[2], fma(x[s][1][k], vr[1], x[s][0][k] * vr[0])));
+                    // reduce-scatter over ra (lane bits 0, 1, 2)
+                    const double s0 = h0 ? cp[0] : cp[2], s1 = h0 ? cp[1] : cp[3];
+                    const double k0 = h0 ? cp[2] : cp[0], k1 = h0 ? cp[3] : cp[1];
+                    const double t0 = k0 + dpp_d<0xB1>(s0), t1 = k1 + dpp_d<0xB1>(s1);
+                    const double sx = h1 ? t0 : t1, kx = h1 ? t1 : t0;
+                    const double u = kx + dpp_d<0x4E>(sx);
+                    const double tot = u + swz_xor4(u);
+                    if ((l & 4) == 0) colp[I][K][4 * cb + (h0 ? 2 : 0) + (h1 ? 1 : 0)] = tot;
+                }
+            }
+        }
+        lds_barrier();   // B1
+        S32_STAMP(1);
+        // ---- 3. p = tau A22 v (0 at c <= j), p'v: waves 0..3, one position a
+        //      lane; the T - J terms of block m in a fixed order (row partials of
+        //      tiles (m, m..T-1), then column partials of tiles (J..m-1, m)),
+        //      all loads issued at once
+        if (w < 4) {
+            const int c = 64 * w + l, m = c >> 5, r = c & 31;
+            double tv[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int K = m + q, I = J + (q - (T - m));
+                tv[q] = K < T ? rowp[m][K][r] : (I < m ? colp[I & 7][m][r] : 0.0);
+            }
+            const double sum = ((tv[0] + tv[1]) + (tv[2] + tv[3])) + ((tv[4] + tv[5]) + (tv[6] + tv[7]));
+            const double p = (c > j && m >= J) ? tj * sum : 0.0;
+            ps[c] = p;
+            const double pv = wave_sum(p * vs[c]);
+            if (l == 0) pvp[w] = pv;
+        }
+        lds_barrier();   // B2
+        S32_STAMP(2);
+        // ---- 4. w = p + alpha2 v; A -= v w' + w v' on the live tiles
+        const double alpha2 = -0.5 * tj * (((pvp[0] + pvp[1]) + pvp[2]) + pvp[3]);
+#pragma unroll
+        for (int s = 0; s < S32_SL; ++s) {
+            if (s * S32_W + w < nlive) {
+                const int r0 = 32 * S32_I(s) + 4 * ra, c0 = 32 * S32_K(s) + 4 * cb;
+                double vr[4], vc[4], wr[4], wc[4];
+                {
+                    const double2 a0 = *(const double2 *)&vs[r0], a1 = *(const double2 *)&vs[r0 + 2];
+                    const double2 b0 = *(const double2 *)&vs[c0], b1 = *(const double2 *)&vs[c0 + 2];
+                    const double2 p0 = *(const double2 *)&ps[r0], p1 = *(const double2 *)&ps[r0 + 2];
+                    const double2 q0 = *(const double2 *)&ps[c0], q1 = *(const double2 *)&ps[c0 + 2];
+                    vr[0] = a0.x; vr[1] = a0.y; vr[2] = a1.x; vr[3] = a1.y;
+                    vc[0] = b0.x; vc[1] = b0.y; vc[2] = b1.x; vc[3] = b1.y;
+                    wr[0] = fma(alpha2, vr[0], p0.x); wr[1] = fma(alpha2, vr[1], p0.y);
+                    wr[2] = fma(alpha2, vr[2], p1.x); wr[3] = fma(alpha2, vr[3], p1.y);
+                    wc[0] = fma(alpha2, vc[0], q0.x); wc[1] = fma(alpha2, vc[1], q0.y);
+                    wc[2] = fma(alpha2, vc[2], q1.x); wc[3] = fma(alpha2, vc[3], q1.y);
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) x[s][i][k] = fma(-vr[i], wc[k], fma(-wr[i], vc[k], x[s][i][k]));
+            }
+        }
+        // ---- publish row j + 1 (its tile row's owners)
+        {
+            const int j1 = j + 1, J1 = j1 >> 5, rr = j1 & 31;
+#pragma unroll
+            for (int s = 0; s < S32_SL; ++s) {
+                if (S32_I(s) == J1 && ra == (rr >> 2)) {
+                    const int c0 = 32 * S32_K(s) + 4 * cb;
+                    double y[4];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) y[k] = (rr & 3) == 0 ? x[s][0][k] : ((rr & 3) == 1 ? x[s][1][k] : ((rr & 3) == 2 ? x[s][2][k] : x[s][3][k]));
+                    *(double2 *)&xrow[c0] = make_double2(y[0], y[1]);
+                    *(double2 *)&xrow[c0 + 2] = make_double2(y[2], y[3]);
+                }
+            }
+        }
+        lds_barrier();   // B0
+        S32_STAMP(3);
+    }
+    // ---- the last 2 x 2 block: row b-2 is in LDS, A[b-1][b-1] from its owner
+    {
+        const int rl = b - 1, I = rl >> 5, rr = rl & 31;
+#pragma unroll
+        for (int s = 0; s < S32_SL; ++s)
+            if (tI[s] == I && tK[s] == I && ra == (rr >> 2) && cb == (rr >> 2))
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (i == (rr & 3)) fin[0] = x[s][i][i];
+    }
+    __syncthreads();
+    if (t == 0) {
+        if (b >= 2) {
+            d[b - 2] = xrow[b - 2];
+            d[b - 1] = fin[0];
+            e[b - 2] = xrow[b - 1];
+            tau[b - 2] = 0.0;
+        } else {
+            d[0] = xrow[0];
+        }
+    }
+    if (ST && t == 0)
+        for (int q = 0; q < 4; ++q) stamps[q] = sacc[q];
+#undef S32_STAMP
+#undef S32_I
+#undef S32_K
+}
+bool sytrd32_supported(int b) { return b >= 3 && b <= 256; }
+int g_sytrd32 = 1;   // knob 37: 0 = k_sytrd_reg (16 x 16 tiles)
+
 // C <- Q_H C, Q_H = H_0 H_1 ... H_{b-3}: one wave per column of C (b x b, ldc = b)
 template <int QM>
 __global__ void __launch_bounds__(256) k_ormtr_l(const double *A, const double *tau, int b, double *C) {
@@ -776,7 +1082,9 @@ int g_sytrd_reg = 1;   // diagnostics switch: 0 = the L2-resident k_sytrd_l
 void eig_sym(double *A, int b, double *theta, double *work, hipStream_t s) {
     if (!eig_sym_supported(b)) fail(TP_ERR_UNSUPPORTED, "eig_sym: b > 1280 (EIG_BMAX)");
     double *C = work, *e = C + (size_t)b * b, *tau = e + b, *dg = tau + b, *lam = dg + b;   // lam: b + 1
-    if (sytrd_reg_supported(b) && g_sytrd_reg)
+    if (g_sytrd32 && sytrd32_supported(b))
+        hipLaunchKernelGGL((k_sytrd32<false>), dim3(1), dim3(64 * S32_W), 0, s, A, b, dg, e, tau, (long long *)nullptr);
+    else if (sytrd_reg_supported(b) && g_sytrd_reg)
         hipLaunchKernelGGL(k_sytrd_reg, dim3(1), dim3(1024), 0, s, A, b, dg, e, tau);
     else if (b <= 256)
         hipLaunchKernelGGL((k_sytrd_l<4, false>), dim3(1), dim3(1024), 0, s, A, b, dg, e, tau, (long long *)nullptr);
@@ -808,11 +1116,14 @@ void eig_sym(double *A, int b, double *theta, double *work, hipStream_t s) {
     TP_HIP(hipMemcpyAsync(A, C, (size_t)b * b * sizeof(double), hipMemcpyDeviceToDevice, s));
 }
 
-// diagnostic: one tridiagonalisation by either kernel (which: 0 k_sytrd_l, 1 k_sytrd_reg)
+// diagnostic: one tridiagonalisation by either kernel (which: 0 k_sytrd_l, 1 k_sytrd_reg, 2 k_sytrd32)
 void sytrd_which(double *A, int b, double *work, int which, hipStream_t s, long long *d_stamps) {
     double *e = work, *tau = e + b, *dg = tau + b;
     (void)d_stamps;
-    if (which == 1) {
+    if (which == 2) {
+        if (!sytrd32_supported(b)) fail(TP_ERR_ARG, "k_sytrd32: b must be 3..256");
+        hipLaunchKernelGGL((k_sytrd32<false>), dim3(1), dim3(64 * S32_W), 0, s, A, b, dg, e, tau, (long long *)nullptr);
+    } else if (which == 1) {
         if (!sytrd_reg_supported(b)) fail(TP_ERR_ARG, "k_sytrd_reg: b must be 16..256, a multiple of 16");
         hipLaunchKernelGGL(k_sytrd_reg, dim3(1), dim3(1024), 0, s, A, b, dg, e, tau);
     } else if (b <= 256) {
@@ -825,10 +1136,13 @@ void sytrd_which(double *A, int b, double *work, int which, hipStream_t s, long 
     TP_HIP(hipGetLastError());
 }
 // diagnostic: the tridiagonalisation alone with per-phase cycle stamps
-// (0 reflector, 1 trailing pass, 2 p/w combine), in a separate build of the kernel
+// (k_sytrd32 for b <= 256: 0 reflector, 1 partials + B1, 2 p + B2, 3 update +
+// publish + B0; k_sytrd_l above: 0 reflector, 1 trailing pass, 2 p/w combine)
 void sytrd_stamped(double *A, int b, double *work, long long *d_stamps, hipStream_t s) {
     double *e = work, *tau = e + b, *dg = tau + b;
-    if (b <= 256)
+    if (sytrd32_supported(b))
+        hipLaunchKernelGGL((k_sytrd32<true>), dim3(1), dim3(64 * S32_W), 0, s, A, b, dg, e, tau, d_stamps);
+    else if (b <= 256)
         hipLaunchKernelGGL((k_sytrd_l<4, true>), dim3(1), dim3(1024), 0, s, A, b, dg, e, tau, d_stamps);
     else
         hipLaunchKernelGGL((k_sytrd_l<8, true>), dim3(1), dim3(1024), 0, s, A, b, dg, e, tau, d_stamps);

@@ -292,6 +292,7 @@ void launch_transpose(const double *d_A, int rows, int cols, int lda, double *d_
 // triangle) <- eigenvectors, theta <- ascending eigenvalues.  work >= b*b + 4b + 8.
 bool eig_sym_supported(int b);
 extern int g_sytrd_reg;
+extern int g_sytrd32;
 void sytrd_stamped(double *A, int b, double *work, long long *d_stamps, hipStream_t s);
 void sytrd_which(double *A, int b, double *work, int which, hipStream_t s,
                  long long *d_stamps = nullptr);   // work: 3b (e, tau, d)

@@ -202,11 +202,14 @@ def _q_from_reflectors(A, tau, b):
     return Q
 
 
-@pytest.mark.parametrize("b,which", [(16, 1), (48, 1), (208, 1), (240, 1), (256, 1), (256, 0), (96, 1)])
+@pytest.mark.parametrize("b,which", [(16, 1), (48, 1), (208, 1), (240, 1), (256, 1), (256, 0), (96, 1),
+                                     (256, 2), (240, 2), (208, 2), (200, 2), (96, 2), (48, 2), (33, 2),
+                                     (16, 2), (5, 2), (3, 2)])
 def test_sytrd_kernels(gpu, b, which):
     """Tridiagonalisation kernels of the Rayleigh-Ritz eigensolver: Q'HQ = T
     with Q from the stored reflectors (bar ~ b eps |H|) and Q orthogonal;
-    which = 1: the register-resident kernel, 0: the L2-resident one."""
+    which = 2: the 32 x 32-tile register kernel (the product path for b <=
+    256), 1: the 16 x 16-tile one, 0: the L2-resident one."""
     import ctypes
     rng = np.random.default_rng(b)
     h = rng.standard_normal((b, b))
@@ -224,7 +227,7 @@ def test_sytrd_kernels(gpu, b, which):
     Q = _q_from_reflectors(A, tau, b)
     Tm = np.diag(d) + np.diag(e[:b - 1], 1) + np.diag(e[:b - 1], -1)
     scale = np.abs(h).max()
-    print(f"sytrd b={b} kernel={'reg' if which else 'l2'}: {ms[0] * 1e3:.1f} us")
+    print(f"sytrd b={b} kernel={['l2', 'reg16', 'reg32'][which]}: {ms[0] * 1e3:.1f} us")
     # run-to-run determinism (three more calls, identical bits)
     for _ in range(3):
         d2 = np.zeros(b); e2 = np.zeros(b); t2 = np.zeros(b); A2 = np.zeros((b, b), order="F")

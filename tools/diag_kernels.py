@@ -99,12 +99,15 @@ def sytrd(b=256):
     rng = np.random.default_rng(2)
     h = rng.standard_normal((b, b))
     h = np.asfortranarray(h + h.T)
-    ms = ctypes.c_double(0); st = ctypes.c_int(0); stamps = np.zeros(3, np.int64)
+    ms = ctypes.c_double(0); st = ctypes.c_int(0); stamps = np.zeros(4, np.int64)
     L.tp_debug_sytrd(h.ctypes.data_as(D), B(ctypes.c_int(b)), B(ms),
                      stamps.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)), B(st))
     _lib.check(st)
-    print(f"sytrd b={b}: {ms.value:.3f} ms (stamped build); cycles reflector {stamps[0]}, pass {stamps[1]}, "
-          f"combine {stamps[2]}; per step {stamps.sum() / max(1, b - 2):.0f}", flush=True)
+    names = (["reflector", "partials+B1", "p+B2", "update+B0"] if b <= 256 else
+             ["reflector", "pass", "combine", "-"])
+    per = ", ".join(f"{n} {v / max(1, b - 2):.0f}" for n, v in zip(names, stamps))
+    print(f"sytrd b={b}: {ms.value:.3f} ms (stamped build); cycles a step: {per}; "
+          f"total {stamps.sum() / max(1, b - 2):.0f}", flush=True)
 
 
 if __name__ == "__main__":
