@@ -314,63 +314,65 @@ C5_BINS = 49851
 C5_CHUNK_ROWS = 4096
 
 
+def matrix_checksum_dev(dm):
+    """``synth.matrix_checksum`` of a device-resident count matrix: exact int64
+    row sums on the GPU (< 2^43 a row at counts < 2^13, n < 2^16), the two
+    integers accumulated on the host in Python ints."""
+    import torch
+    n = dm.shape[0]
+    P = (1 << 61) - 1
+    w = torch.arange(1, n + 1, dtype=torch.int64, device=dm.device)
+    total, acc = 0, 0
+    for r0 in range(0, n, 1024):
+        blk = dm[r0:r0 + 1024].to(torch.int64)
+        total += int(blk.sum().item())
+        rows = (blk * w[None, :]).sum(dim=1).cpu().numpy()
+        acc += sum(int(v) * (r0 + q + 1) for q, v in enumerate(rows))
+    return np.array([total, acc % P], np.int64)
+
+
 def _c5_resident(world, rank, local):
     """BASELINE config 5's matrix (chr1 @5kb: synth_hic_par(49 851, seed
     20261015+5, centromere=True), the input of tests/golden/c5full.npz) resident
-    in HBM on every rank.  Rank 0 draws it on the host and checks its checksum
-    against the fixture; with several ranks it travels to the others over the
-    gloo control group in row chunks (4096 rows = 1.6 GB at a time: a rank
-    other than 0 never holds more than one chunk on the host, and no GPU
-    collective is involved).  Setup, outside every timing."""
+    in HBM on every rank.  Every rank draws it itself, block by block straight
+    into its device copy (``synth_hic_par_stream``: the same bits, no n0 x n0
+    host array, no broadcast between ranks), and checks its checksum against
+    the fixture on the device.  Setup, outside every timing."""
     import torch
-    import torch.distributed as dist
-    from tadpole_amd.synth import SEED_BASE, matrix_checksum, synth_hic_par
+    from tadpole_amd.synth import SEED_BASE, place_upper_block, synth_hic_par_stream
     n0 = C5_BINS
     info = {}
     dm = torch.empty((n0, n0), dtype=torch.float64, device=f"cuda:{local}")
-    host = None
-    if rank == 0:
-        t0 = time.perf_counter()
-        host = synth_hic_par(n0, SEED_BASE + 5, centromere=True)
-        info["matrix_build_s"] = round(time.perf_counter() - t0, 2)
-        gold = os.path.join(HERE, "tests", "golden", "c5full.npz")
-        if os.path.exists(gold):
-            info["matrix_checksum_match"] = bool(np.array_equal(matrix_checksum(host),
-                                                                np.load(gold)["matrix_checksum"]))
     t0 = time.perf_counter()
-    distribute_rows(host, n0, world, rank, lambda r0, r1, t: dm[r0:r1].copy_(t))
+    zero = synth_hic_par_stream(n0, SEED_BASE + 5, lambda r0, r1, U: place_upper_block(
+        dm, r0, r1, torch.from_numpy(U).to(dm.device, non_blocking=False)), centromere=True)
+    zi = torch.as_tensor(zero, device=dm.device)
+    dm.index_fill_(0, zi, 0.0)
+    dm.index_fill_(1, zi, 0.0)
     torch.cuda.synchronize()
-    info["distribute_s"] = round(time.perf_counter() - t0, 2)
-    del host
-    return dm, info
-
-
-def distribute_rows(host, n0, world, rank, sink, chunk_rows=C5_CHUNK_ROWS):
-    """Rank 0's n0 x n0 host matrix to every rank, row chunk by row chunk:
-    sink(r0, r1, rows) receives rows [r0, r1) as a CPU tensor on each rank
-    (broadcast over the default -- gloo -- group when world > 1)."""
-    import torch
-    import torch.distributed as dist
-    for r0 in range(0, n0, chunk_rows):
-        r1 = min(n0, r0 + chunk_rows)
+    info["matrix_build_s"] = round(time.perf_counter() - t0, 2)
+    gold = os.path.join(HERE, "tests", "golden", "c5full.npz")
+    if os.path.exists(gold):
+        ok = bool(np.array_equal(matrix_checksum_dev(dm), np.load(gold)["matrix_checksum"]))
         if world > 1:
-            buf = (torch.from_numpy(np.ascontiguousarray(host[r0:r1])) if rank == 0
-                   else torch.empty((r1 - r0, n0), dtype=torch.float64))
-            dist.broadcast(buf, src=0)
-        else:
-            buf = torch.from_numpy(np.ascontiguousarray(host[r0:r1]))
-        sink(r0, r1, buf)
+            import torch.distributed as dist
+            t = torch.tensor([0 if ok else 1], dtype=torch.int64)
+            dist.all_reduce(t)
+            ok = int(t.item()) == 0
+        info["matrix_checksum_match"] = ok
+    return dm, info
 
 
 def c5_mode(world):
     """How the c5_full line runs at this rank count: one GPU unsharded (plus a
-    one-rank RCCL check), every arm sharded over all ranks, or skipped when
-    ranks share a GPU (a rehearsal with more ranks than devices: RCCL needs
-    one device per rank)."""
+    one-rank RCCL check); N ranks in two groups, the p arm sharded over ranks
+    [0, ceil(N/2)) and the q arm over the rest at the same time
+    (``multi.init_arm_comms``); or skipped when ranks share a GPU (a rehearsal
+    with more ranks than devices: RCCL needs one device per rank)."""
     if world == 1:
         return "one_gpu"
     import torch
-    return "sharded" if torch.cuda.device_count() >= world else "skipped"
+    return "arm_groups" if torch.cuda.device_count() >= world else "skipped"
 
 
 def run_c5_full(world, rank, local, max_pcs, reps):
@@ -390,13 +392,15 @@ def run_c5_full(world, rank, local, max_pcs, reps):
     from tadpole_amd import multi
     from tadpole_amd.api import TADpole
     dm, info = _c5_resident(world, rank, local)
-    sharded = c5_mode(world) == "sharded"
-    comm_size = None
+    sharded = c5_mode(world) == "arm_groups"
+    comm_size = groups = None
     if sharded:
-        comm_size = multi.init_comm(device=local)[1]
+        groups = multi.init_arm_comms(device=local)
+        comm_size = {"p": len(groups.p_ranks), "q": len(groups.q_ranks)}
 
     def once():
-        return TADpole(dm, max_pcs=max_pcs, centromere_search=True, sharded=sharded, inplace=True)
+        return TADpole(dm, max_pcs=max_pcs, centromere_search=True, sharded=sharded, inplace=True,
+                       arm_groups=groups)
 
     try:
         once()                                     # warm-up (scratch of these sizes)
@@ -443,11 +447,12 @@ def run_c5_full(world, rank, local, max_pcs, reps):
            "workload": ("C5: chr1 @5kb shape, synthetic 49851x49851 Hi-C (synth_hic_par, seed 20261015+5, "
                         "centromere run at [0.4875, 0.572) N0), TADpole(centromere_search=TRUE) bug-compatible, "
                         "max_pcs=%d, resident in HBM, " % max_pcs +
-                        (f"every arm sharded over {world} GPUs (RCCL)" if sharded else "one GPU")),
+                        (f"p arm sharded over GPUs {groups.p_ranks}, q arm over {groups.q_ranks} at the same "
+                         f"time (RCCL, one communicator a group)" if sharded else "one GPU")),
            "arms": {}}
     out.update(info)
     if comm_size is not None:
-        out["rccl_comm_size"] = comm_size
+        out["rccl_comm_size"] = comm_size   # ranks of each arm's group
     if one_rank is not None:
         out["sharded_1rank_bit_identical"] = one_rank
     for a in ("p", "q"):

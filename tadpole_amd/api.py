@@ -539,7 +539,7 @@ def _assemble_rle(t, dendro, levels, good1, bad_idx1) -> Tadpole:
 def TADpole(mat_file, max_pcs: int = 200, min_clusters: int = 2, bad_frac: float = 0.01,
             chr=None, start=None, end=None, resol=None, centromere_search: bool = False,
             device: int = 0, sharded: bool = False, stream=None, fixed_centromere: bool = False,
-            verbose: bool = False, inplace: bool = False) -> Tadpole:
+            verbose: bool = False, inplace: bool = False, arm_groups=None) -> Tadpole:
     """``TADpole()`` (R/TADpole.R:344-501).  ``mat_file`` may be a path to a
     tab-separated matrix or an in-memory square array.  ``sharded``: split this
     matrix over the ranks of the communicator made by
@@ -554,7 +554,11 @@ def TADpole(mat_file, max_pcs: int = 200, min_clusters: int = 2, bad_frac: float
     pipeline cleans (NA -> 0, forceSymmetric, R/TADpole.R:19-20) a device copy.
     ``inplace=True`` skips that copy (N0^2 doubles of HBM) and cleans the
     caller's float64 tensor in place.  ``stream`` contexts: see
-    ``tadpole_amd.release_stream``."""
+    ``tadpole_amd.release_stream``.  ``arm_groups`` (from
+    ``tadpole_amd.multi.init_arm_comms``, with ``centromere_search`` and
+    ``sharded``): each rank computes only its group's arm, sharded over that
+    group, and the arms' results are exchanged -- the two arms on disjoint
+    GPUs at the same time."""
     if _is_device(mat_file):
         raw = mat_file
         if not inplace:
@@ -572,6 +576,8 @@ def TADpole(mat_file, max_pcs: int = 200, min_clusters: int = 2, bad_frac: float
     else:
         raw = _as_matrix(mat_file)
     shard_flag = _lib.TP_FLAG_SHARDED if sharded else 0
+    if arm_groups is not None and not (centromere_search and sharded):
+        raise ValueError("arm_groups: the two-group schedule is for centromere_search=True, sharded=True")
     if not centromere_search:
         res = _pipeline(raw, max_pcs, min_clusters, bad_frac, shard_flag, device, stream)
         bad_idx1 = np.flatnonzero(res["bad"]) + 1
@@ -596,9 +602,11 @@ def TADpole(mat_file, max_pcs: int = 200, min_clusters: int = 2, bad_frac: float
             # R/TADpole.R:356: `mat$centromer` on a matrix is an error in R
             raise TypeError("$ operator is invalid for atomic vectors (no centromere split: no bad bin, or the "
                             "longest bad run touches an end of the matrix; R/TADpole.R:66-70,87-90,356)")
+        if arm_groups is not None:
+            raise ValueError("arm_groups: no centromere split (the group communicators cover one arm each)")
         return TADpole(raw, max_pcs, min_clusters, bad_frac, device=device, sharded=sharded, stream=stream,
                        verbose=verbose, inplace=True)
-    return _tadpole_arms(raw, plan, max_pcs, min_clusters, device, shard_flag, stream, verbose)
+    return _tadpole_arms(raw, plan, max_pcs, min_clusters, device, shard_flag, stream, verbose, arm_groups)
 
 
 _ARM_STREAMS: Dict[int, tuple] = {}
@@ -631,36 +639,68 @@ def _arms_concurrent(raw, shard_flag: int, stream) -> bool:
     return torch.cuda.is_available()
 
 
-def _tadpole_arms(raw, plan, max_pcs, min_clusters, device, shard_flag: int = 0, stream=None,
-                  verbose: bool = False) -> Tadpole:
-    """R/TADpole.R:351-442 (arm loop and arm merge).  Each arm is the raw
-    principal submatrix of its kept bins; NA->0 and forceSymmetric(uplo='U')
-    commute with taking it, so the device cleans it (TP_FLAG_NO_MASK: the arm
-    matrices are correlated as given, R/TADpole.R:362).  On one GPU the two
-    arms run concurrently on two streams (``_arms_concurrent``); results and
-    R's message() lines are those of the sequential loop, in its order."""
+def _run_arm(raw, plan, arm, max_pcs, min_clusters, device, shard_flag: int = 0, stream=None) -> Tadpole:
+    """One centromere arm (R/TADpole.R:362-408): the raw principal submatrix
+    of its kept bins; NA->0 and forceSymmetric(uplo='U') commute with taking
+    it, so the device cleans it (TP_FLAG_NO_MASK: the arm matrices are
+    correlated as given, R/TADpole.R:362)."""
+    names, bad_cols = plan[arm]
+    if _is_device(raw):   # already cleaned by tp_mask_dev
+        import torch
+        sel = torch.as_tensor(names - 1, device=raw.device)
+        sub = raw.index_select(0, sel).index_select(1, sel)
+        clean = _lib.TP_FLAG_CLEAN
+    else:
+        sub = raw[np.ix_(names - 1, names - 1)]
+        clean = 0
+    res = _pipeline(sub, max_pcs, min_clusters, 0.0, _lib.TP_FLAG_NO_MASK | clean | shard_flag, device, stream)
+    del sub
+    res["good"] = names.astype(np.int32)   # rownames inherited from the full matrix
+    return _assemble(res, np.asarray(bad_cols))
+
+
+def _merge_arms(plan, subs, verbose: bool = False) -> Tadpole:
+    """R/TADpole.R:404-442: the per-arm objects, R's message() lines in the
+    sequential loop's order, and merging_arms (p labels, a zero pad of the
+    centromere's length after each arm, the trailing pad dropped, RLE)."""
     tad = Tadpole()
     centromer = plan["centromere"]
+    fixed_arms: List[np.ndarray] = []
+    for arm in ("p", "q"):
+        names, bad_cols = plan[arm]
+        sub_t = subs[arm]
+        _message(f"Processing arm {arm}", verbose)
+        _message(f"Optimal number of PCs: {sub_t.n_pcs}", verbose)
+        _message(f"Optimal number of clusters: {sub_t.optimal_n_clusters}", verbose)
+        setattr(tad, arm, sub_t)
+        lab = sub_t.dendro.cutree(sub_t.optimal_n_clusters)
+        fixed, _ = _fixed_clusters(lab, names, np.asarray(bad_cols))
+        fixed_arms.append(fixed)
+        fixed_arms.append(np.zeros(len(centromer)))
+    allv = np.concatenate(fixed_arms)
+    allv = allv[: len(allv) - len(centromer)]
+    tad.merging_arms = _coords(allv)
+    return tad
+
+
+def _tadpole_arms(raw, plan, max_pcs, min_clusters, device, shard_flag: int = 0, stream=None,
+                  verbose: bool = False, arm_groups=None) -> Tadpole:
+    """R/TADpole.R:351-442 (arm loop and arm merge).  On one GPU the two arms
+    run concurrently on two streams (``_arms_concurrent``); with ``arm_groups``
+    each rank runs its group's arm sharded over the group and the results are
+    exchanged (``multi.exchange_arms``); results and R's message() lines are
+    those of the sequential loop, in its order."""
     if _is_device(raw):
         device = raw.device.index if raw.device.index is not None else device
 
     def run_arm(arm, arm_stream):
-        names, bad_cols = plan[arm]
-        if _is_device(raw):   # already cleaned by tp_mask_dev
-            import torch
-            sel = torch.as_tensor(names - 1, device=raw.device)
-            sub = raw.index_select(0, sel).index_select(1, sel)
-            clean = _lib.TP_FLAG_CLEAN
-        else:
-            sub = raw[np.ix_(names - 1, names - 1)]
-            clean = 0
-        res = _pipeline(sub, max_pcs, min_clusters, 0.0, _lib.TP_FLAG_NO_MASK | clean | shard_flag, device,
-                        arm_stream)
-        del sub
-        res["good"] = names.astype(np.int32)   # rownames inherited from the full matrix
-        return _assemble(res, np.asarray(bad_cols))
+        return _run_arm(raw, plan, arm, max_pcs, min_clusters, device, shard_flag, arm_stream)
 
-    if _arms_concurrent(raw, shard_flag, stream):
+    if arm_groups is not None:
+        from . import multi
+        mine = run_arm(arm_groups.arm, stream)
+        subs = multi.exchange_arms(arm_groups, mine)
+    elif _arms_concurrent(raw, shard_flag, stream):
         # both arms start at once (0.305 s for C5 on one MI355X, 0.33 s one
         # after the other).  TADPOLE_ARMS_Q_AT=s (1..3) holds q back until p's
         # progress word reaches stage s (2: p's correlation queued, 3: p's
@@ -696,22 +736,7 @@ def _tadpole_arms(raw, plan, max_pcs, min_clusters, device, shard_flag: int = 0,
         subs = {}
         for arm in ("p", "q"):
             subs[arm] = run_arm(arm, stream)
-    fixed_arms: List[np.ndarray] = []
-    for arm in ("p", "q"):
-        names, bad_cols = plan[arm]
-        sub_t = subs[arm]
-        _message(f"Processing arm {arm}", verbose)
-        _message(f"Optimal number of PCs: {sub_t.n_pcs}", verbose)
-        _message(f"Optimal number of clusters: {sub_t.optimal_n_clusters}", verbose)
-        setattr(tad, arm, sub_t)
-        lab = sub_t.dendro.cutree(sub_t.optimal_n_clusters)
-        fixed, _ = _fixed_clusters(lab, names, np.asarray(bad_cols))
-        fixed_arms.append(fixed)
-        fixed_arms.append(np.zeros(len(centromer)))
-    allv = np.concatenate(fixed_arms)
-    allv = allv[: len(allv) - len(centromer)]
-    tad.merging_arms = _coords(allv)
-    return tad
+    return _merge_arms(plan, subs, verbose)
 
 
 # ------------------------------------------------------------------ diffT

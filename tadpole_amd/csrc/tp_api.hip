@@ -1314,6 +1314,33 @@ void tp_debug_prod_i8(const double *A, const int *K, const int *M, const double 
     });
 }
 
+/* int8-digit product rows (test hook): the digit image of columns [col0, M)
+ * of A (K x M, the column slab a rank keeps), then rows [r0, r0 + rows) of
+ * A'B, no rank-1 epilogue, into O (rows x N, column-major): a shard's rows
+ * must carry the whole product's bits.  *which: the product kernel (knob 36). */
+void tp_debug_prod_i8_rows(const double *A, const int *K, const int *M, const double *B, const int *N,
+                           const int *col0, const int *r0, const int *rows, double *O, int *status) {
+    guarded(status, [&] {
+        Ctx &c = ctx_for(0);
+        hipStream_t s = c.cur;
+        const int k = *K, m = *M, nn = *N, c0 = *col0, q0 = *r0, nr = *rows;
+        if (!prod_i8_ok(k, nn) || c0 < 0 || c0 % 64 || c0 >= m || q0 < c0 || nr < 1 || q0 + nr > m)
+            fail(TP_ERR_ARG, "prod_i8_rows: N must be 64, col0 a multiple of 64, rows inside [col0, M)");
+        double *dA = c.buf[S_C].as<double>((size_t)k * (m - c0));
+        double *dB = c.buf[S_Q].as<double>((size_t)k * nn);
+        double *dO = c.buf[S_Z].as<double>((size_t)nr * nn);
+        TP_HIP(hipMemcpyAsync(dA, A + (size_t)c0 * k, (size_t)k * (m - c0) * 8, hipMemcpyHostToDevice, s));
+        TP_HIP(hipMemcpyAsync(dB, B, (size_t)k * nn * 8, hipMemcpyHostToDevice, s));
+        ProdDigits pd;
+        prod_digits_build(c, dA, k, k, m - c0, c0, pd);
+        double *part = nullptr;
+        const int S = prod_i8_partials(c, pd, q0, nr, dB, k, nn, k, c.buf[S_PARTIAL], &part);
+        launch_splitk_reduce(part, (size_t)nr * nn, S, nr, nn, dO, nr, 0, s);
+        TP_HIP(hipMemcpyAsync(O, dO, (size_t)nr * nn * 8, hipMemcpyDeviceToHost, s));
+        TP_HIP(hipStreamSynchronize(s));
+    });
+}
+
 /* CholQR kernels for b <= 256 on Z = I: k_chol_inv + k_trsm_frag give
  * Y = U^{-1} (W = U'U, S-scaled, + rel on the scaled diagonal); diag[b] =
  * diag(U).  ms[0] chol kernel (the product's choice of waves), ms[1] info,

@@ -342,6 +342,125 @@ __global__ void __launch_bounds__(256, 3 - NB) k_pd_prod(const int8_t *__restric
             }
 }
 
+// k_pd_dma: the same products (same pairs, same int32 sums, same combine: the
+// bits of k_pd_prod), built for the HBM stream (round 5).  k_pd_prod moved 52
+// KB a k step per workgroup through registers and ds_write_b128, one step in
+// flight, two barriers a step.  Here both operands' digit blocks of a step go
+// straight to LDS by LDS-DMA (global_load_lds_dwordx4) into a ring of
+// PD_RING stages, PD_RING - 1 steps in flight (no VGPR round trip, no store
+// pass, one raw barrier a step; counted vmcnt, never 0 in the loop):
+//   * wave w owns output columns 16 w .. 16 w + 15 of all 64 rows (four row
+//     tiles), so it DMAs exactly the seven B chunks it reads (its 16
+//     columns, seven digits) plus A's six digit chunks of row tile w, which
+//     every wave reads;
+//   * a 1 KB chunk is 16 columns x 64 k bytes; each DMA carries the bank
+//     swizzle of k_xtx_i8_glds on its source address (lane p loads column
+//     p >> 2, k quarter (p & 3) ^ ((p >> 4) & 2)), so every ds_read_b128
+//     fragment read (column fr, quarter kq at slot 4 fr + (kq ^ ((fr >> 2) &
+//     2))) is conflict-free.
+// Every step issues the same 13 DMAs a wave (a step past the chunk re-reads
+// its last step into a slot no later step reads), so the wait is one fixed
+// count.  One workgroup a CU (3 x 52 KB of LDS).
+#ifndef TP_PD_RING
+#define TP_PD_RING 3
+#endif
+constexpr int PD_RING = TP_PD_RING;
+constexpr int PD_BOFF = PD_ADIG * 4 * 1024;                 // B's chunks after A's in a stage
+constexpr int PD_STAGE = PD_BOFF + PD_DIG * 4 * 1024;       // 52 KB
+static_assert(PD_RING * PD_STAGE <= 160 * 1024, "LDS ring");
+__device__ __forceinline__ void pd_glds16(const void *g, void *l) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)g,
+                                     (__attribute__((address_space(3))) void *)l, 16, 0, 0);
+}
+template <int N>
+__device__ __forceinline__ void pd_wait_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__global__ void __launch_bounds__(256, 1) k_pd_dma(const int8_t *__restrict__ Da, int Kp, int M,
+                                                   const int8_t *__restrict__ Db, const double *__restrict__ rs,
+                                                   const double *__restrict__ cs, double *__restrict__ part,
+                                                   size_t pstride, int kchunk) {
+    __shared__ __attribute__((aligned(16))) int8_t L[PD_RING * PD_STAGE];   // the only LDS object (DMA waits)
+    const int tm = (M + 63) / 64;
+    const int total = (int)gridDim.x;
+    const int xcd = (int)blockIdx.x & 7, slot = (int)blockIdx.x >> 3;
+    const int Lg = xcd * (total >> 3) + min(xcd, total & 7) + slot;
+    const int bm = Lg % tm, z = Lg / tm;
+    const int t = threadIdx.x, lane = t & 63;
+    const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int fr = lane & 15, kq = lane >> 4;
+    const int kbeg = z * kchunk, kend = min(Kp, kbeg + kchunk);
+    const int nsteps = Kp / 64;
+    const int T = (kend - kbeg) / 64, st0 = kbeg / 64;
+    TP_DASSERT(Kp % 64 == 0 && kchunk % 64 == 0 && T >= 1);
+    // DMA sources: column 16 w + (lane >> 2) of this wave's A row tile and B
+    // column tile, k quarter swizzled
+    const int pc = lane >> 2, pk = (lane & 3) ^ ((lane >> 4) & 2);
+    const int8_t *asrc = Da + (size_t)bm * nsteps * (PD_DIG * PD_BLK) + (size_t)(16 * w + pc) * 64 + 16 * pk;
+    const int8_t *bsrc = Db + (size_t)(16 * w + pc) * 64 + 16 * pk;
+    const int roff = (4 * fr + (kq ^ ((fr >> 2) & 2))) * 16;   // fragment (fr, kq) in a chunk
+    auto issue = [&](int k) {   // step k (clamped) into ring slot k % PD_RING: A digits, then B digits
+        const size_t o = (size_t)(st0 + min(k, T - 1)) * (PD_DIG * PD_BLK);
+        int8_t *dst = L + (k % PD_RING) * PD_STAGE + w * 1024;
+#pragma unroll
+        for (int s = 0; s < PD_ADIG; ++s) pd_glds16(asrc + o + s * PD_BLK, dst + s * 4096);
+#pragma unroll
+        for (int s = 0; s < PD_DIG; ++s) pd_glds16(bsrc + o + s * PD_BLK, dst + PD_BOFF + s * 4096);
+    };
+    pd_i32x4 acc[PD_DIG][4];
+#pragma unroll
+    for (int u = 0; u < PD_DIG; ++u)
+#pragma unroll
+        for (int a = 0; a < 4; ++a) acc[u][a] = pd_i32x4{0, 0, 0, 0};
+    auto mstep = [&](int k) {
+        const int8_t *Ls = L + (k % PD_RING) * PD_STAGE + roff;
+        pd_i32x4 fb[PD_DIG], fa[2][4];
+#pragma unroll
+        for (int s = 0; s < PD_DIG; ++s) fb[s] = *(const pd_i32x4 *)(Ls + PD_BOFF + s * 4096 + w * 1024);
+#pragma unroll
+        for (int a = 0; a < 4; ++a) fa[0][a] = *(const pd_i32x4 *)(Ls + a * 1024);
+#pragma unroll
+        for (int s0 = 0; s0 < PD_ADIG; ++s0) {
+            if (s0 + 1 < PD_ADIG) {
+#pragma unroll
+                for (int a = 0; a < 4; ++a) fa[(s0 + 1) & 1][a] = *(const pd_i32x4 *)(Ls + (s0 + 1) * 4096 + a * 1024);
+            }
+#pragma unroll
+            for (int tt = 0; tt + s0 < PD_DIG; ++tt)
+#pragma unroll
+                for (int a = 0; a < 4; ++a)
+                    acc[s0 + tt][a] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[s0 & 1][a], fb[tt], acc[s0 + tt][a], 0, 0, 0);
+        }
+    };
+#pragma unroll
+    for (int k = 0; k < PD_RING - 1; ++k) issue(k);
+    for (int k = 0; k < T; ++k) {
+        // step k landed: this wave's DMAs by the count (the RING - 2 later
+        // steps' 13 each stay in flight), the others' by the barrier, after
+        // which step k - 1's slot is free for step k + RING - 1
+        pd_wait_vm<(PD_RING - 2) * (PD_DIG + PD_ADIG)>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        issue(k + PD_RING - 1);
+        mstep(k);
+    }
+    pd_wait_vm<0>();   // the clamped re-reads of the tail: nothing in flight at exit
+    const int i0 = bm * 64, j = 16 * w + fr;
+    double *P = part + pstride * z;
+    const double csj = cs[j];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = i0 + 16 * a + kq * 4 + r;
+            if (i >= M) continue;
+            double v = 0.0;
+#pragma unroll
+            for (int u = PD_DIG - 1; u >= 0; --u) v += (double)acc[u][a][r] * ldexp(1.0, 96 - 8 * u);
+            P[(size_t)i + (size_t)j * M] = (v * rs[i]) * csj;
+        }
+}
+
 // k chunks from K alone (shards agree); <= 16384 rows a chunk (accumulator range)
 #ifndef TP_PD_KDIV
 #define TP_PD_KDIV 960   // C3: 8 k chunks, 984 workgroups (~4 full rounds of one a CU; 1024: 7, 861)
@@ -414,7 +533,10 @@ int prod_i8_partials(Ctx &c, const ProdDigits &pd, int r0, int M, const double *
     const int tm = (M + 63) / 64;
     // one LDS buffer, two workgroups a CU: the 32 C3 products 4.57 ms against
     // 5.35 for the double-buffered one-workgroup form (knob 36 = 2, A/B)
-    if (g_prod_i8 == 2)
+    if (g_prod_i8 == 3)
+        hipLaunchKernelGGL(k_pd_dma, dim3((unsigned)(tm * S)), dim3(256), 0, s, Da, pd.Kp, M, Db, rs, cs, *part,
+                           pstride, kc);
+    else if (g_prod_i8 == 2)
         hipLaunchKernelGGL(k_pd_prod<2>, dim3((unsigned)(tm * S)), dim3(256), (size_t)2 * PD_BUF, s, Da, pd.Kp, M, Db,
                            rs, cs, *part, pstride, kc);
     else

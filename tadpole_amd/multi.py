@@ -15,7 +15,7 @@ host, R/TADpole.R:104).
 from __future__ import annotations
 
 import ctypes
-from typing import Callable, Optional, Tuple
+from typing import Callable, List, NamedTuple, Optional, Tuple
 
 import numpy as np
 
@@ -57,6 +57,58 @@ def init_comm(device: int, group=None, uid_fn: Optional[Callable[[], bytes]] = N
         raise RuntimeError("bad RCCL unique id from rank 0")
     (init_fn or _lib_init)(bytes(uid), world, rank, device)
     return rank, world
+
+
+class ArmGroups(NamedTuple):
+    """The C5 schedule over R >= 2 ranks (``init_arm_comms``): the p arm on
+    ``p_ranks``, the q arm on ``q_ranks``, each group one communicator."""
+    arm: str              # this rank's arm, "p" or "q"
+    p_ranks: List[int]    # global ranks of the p group (its root first)
+    q_ranks: List[int]
+    rank: int             # global rank
+    world: int
+
+
+def arm_group_ranks(world: int) -> Tuple[List[int], List[int]]:
+    """p on ranks [0, ceil(R/2)), q on the rest: the two centromere arms are
+    independent matrices (R/TADpole.R:357-436) of similar size (C5: ~24.3k and
+    ~21.3k bins), so each group takes one and their unshardable CONISS merge
+    chains run at the same time instead of one after the other."""
+    if world < 2:
+        raise ValueError("arm groups need at least two ranks")
+    npr = (world + 1) // 2
+    return list(range(npr)), list(range(npr, world))
+
+
+def init_arm_comms(device: int, uid_fn: Optional[Callable[[], bytes]] = None,
+                   init_fn: Optional[Callable[[bytes, int, int, int], None]] = None) -> ArmGroups:
+    """Split the default process group into the p and q arm groups
+    (``arm_group_ranks``) and bind this rank's library communicator over its
+    group: ``TADpole(..., centromere_search=True, sharded=True,
+    arm_groups=<this>)`` then shards each arm over its own group only.  Every
+    rank calls this (``new_group`` is collective)."""
+    import torch.distributed as dist
+
+    world, rank = dist.get_world_size(), dist.get_rank()
+    p_ranks, q_ranks = arm_group_ranks(world)
+    gp = dist.new_group(p_ranks)
+    gq = dist.new_group(q_ranks)
+    arm = "p" if rank in p_ranks else "q"
+    init_comm(device, group=gp if arm == "p" else gq, uid_fn=uid_fn, init_fn=init_fn)
+    return ArmGroups(arm, p_ranks, q_ranks, rank, world)
+
+
+def exchange_arms(groups: ArmGroups, mine) -> dict:
+    """Every rank gets both arms' results: each group's root broadcasts its
+    arm's ``tadpole`` object over the default (control) group."""
+    import torch.distributed as dist
+
+    out = {}
+    for arm, ranks in (("p", groups.p_ranks), ("q", groups.q_ranks)):
+        obj = [mine if (groups.arm == arm and groups.rank == ranks[0]) else None]
+        dist.broadcast_object_list(obj, src=ranks[0])
+        out[arm] = obj[0]
+    return out
 
 
 def destroy_comm(device: int = 0) -> None:

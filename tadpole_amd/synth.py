@@ -140,6 +140,69 @@ def synth_hic_par(n0: int, seed: int, zero_frac: float = 0.005, centromere: bool
     return out
 
 
+def synth_hic_par_stream(n0: int, seed: int, put, zero_frac: float = 0.005, centromere: bool = False,
+                         threads: int = 0) -> np.ndarray:
+    """``synth_hic_par`` without its n0 x n0 host array: the same draws (bit
+    for bit), handed to ``put(r0, r1, U)`` block by block in row order, U = the
+    block's upper rows ``[r0, r1) x [r0, n0)`` (zero below the diagonal; the
+    consumer mirrors them, e.g. with ``place_upper_block``).  Blocks are drawn
+    in parallel threads, at most one per thread ahead of the consumer.  Returns
+    the bins the caller zeroes afterwards (rows and columns): the random bad
+    bins and the centromere run.  Every rank of a multi-GPU run can fill its
+    own device copy of the C5 matrix this way (no broadcast)."""
+    from concurrent.futures import ThreadPoolExecutor
+    import os
+
+    rng = np.random.default_rng(seed)
+    tad, meta = tad_layout(n0, rng)
+    idx = np.arange(n0)
+    nblk = -(-n0 // PAR_BLOCK)
+
+    def draw(b):
+        r0, r1 = b * PAR_BLOCK, min(n0, (b + 1) * PAR_BLOCK)
+        i = idx[r0:r1, None]
+        c = idx[None, r0:]
+        e = 1000.0 / (1.0 + np.abs(c - i))
+        e = e * (1.0 + 2.0 * (tad[r0:r1, None] == tad[None, r0:])
+                 + 1.0 * (meta[r0:r1, None] == meta[None, r0:]))
+        e[c < i] = 0.0
+        return np.random.default_rng([seed, 1, b]).poisson(e).astype(np.float64)
+
+    nt = threads or min(16, os.cpu_count() or 1)
+    with ThreadPoolExecutor(max_workers=nt) as ex:
+        pend = {}
+        nxt = 0
+        for b in range(nblk):
+            while nxt < nblk and nxt < b + nt + 1:
+                pend[nxt] = ex.submit(draw, nxt)
+                nxt += 1
+            U = pend.pop(b).result()
+            put(b * PAR_BLOCK, min(n0, (b + 1) * PAR_BLOCK), U)
+    zero = []
+    nz = max(1, int(round(zero_frac * n0))) if zero_frac > 0 else 0
+    if nz:
+        zero.append(rng.choice(n0, nz, replace=False))
+    if centromere:
+        zero.append(np.arange(int(0.4875 * n0), int(0.572 * n0)))
+    return np.unique(np.concatenate(zero)) if zero else np.zeros(0, np.int64)
+
+
+def place_upper_block(M, r0: int, r1: int, U) -> None:
+    """Write one block of ``synth_hic_par_stream`` into the symmetric M (numpy
+    or torch, either device): rows [r0, r1) from column r1 on, their mirror
+    below, and the diagonal block symmetrised (upper wins, as the generators
+    mirror)."""
+    w = r1 - r0
+    R = U[:, w:]
+    M[r0:r1, r1:] = R
+    M[r1:, r0:r1] = R.T
+    D = U[:, :w]
+    if hasattr(D, "triu"):            # torch
+        M[r0:r1, r0:r1] = D.triu() + D.triu(1).T
+    else:
+        M[r0:r1, r0:r1] = np.triu(D) + np.triu(D, 1).T
+
+
 def config_matrix(config: int, **kw) -> np.ndarray:
     return synth_hic(CONFIG_BINS[config], SEED_BASE + config,
                      centromere=(config == 5), **kw)

@@ -71,44 +71,86 @@ def _dist_worker(rank, world, port, out):
     import torch
     import torch.distributed as dist
     sys.path.insert(0, ROOT)
-    import bench
+    from tadpole_amd import multi
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    n0 = 37
-    host = np.arange(n0 * n0, dtype=np.float64).reshape(n0, n0) if rank == 0 else None
-    got = torch.full((n0, n0), -1.0, dtype=torch.float64)
-    bench.distribute_rows(host, n0, world, rank, lambda r0, r1, t: got[r0:r1].copy_(t), chunk_rows=8)
-    want = torch.arange(n0 * n0, dtype=torch.float64).reshape(n0, n0)
-    out.put((rank, bool(torch.equal(got, want)), bench.c5_mode(world)))
+    seen = []
+    g = multi.init_arm_comms(0, uid_fn=lambda: bytes(range(128)),
+                             init_fn=lambda uid, n, r, dev: seen.append((len(uid), n, r)))
+    # each rank computes only its arm; every rank ends with both
+    mine = {"arm": g.arm, "by": rank, "data": np.arange(3) + (0 if g.arm == "p" else 10)}
+    got = multi.exchange_arms(g, mine)
+    out.put((rank, g.arm, g.p_ranks, g.q_ranks, seen, got["p"]["by"], got["q"]["by"],
+             int(got["p"]["data"][0]), int(got["q"]["data"][0])))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_c5_full_multi_rank_path_gloo(monkeypatch):
-    """The c5_full line at world 2 (what `bench.py --gpus 2` selects): the
-    sharded mode with a device per rank (skipped when ranks would share a
-    GPU), and the C5 matrix reaching every rank intact through the chunked
-    gloo broadcast (rank 0 holds the only host copy)."""
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_c5_arm_groups_gloo(world, monkeypatch):
+    """The c5_full line at N > 1 ranks (what `bench.py --gpus N` selects with a
+    device per rank): the p arm on ranks [0, ceil(N/2)), the q arm on the rest,
+    each group binding one communicator of its own size (rank within the
+    group), and every rank receiving both arms' results from the group roots
+    (SURVEY §8(e)2, R/TADpole.R:357-442)."""
     import socket
     import torch
     import torch.multiprocessing as mp
     import bench
     monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
-    assert bench.c5_mode(1) == "one_gpu" and bench.c5_mode(8) == "sharded"
+    assert bench.c5_mode(1) == "one_gpu" and bench.c5_mode(8) == "arm_groups"
     monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
     assert bench.c5_mode(2) == "skipped"
     monkeypatch.undo()
-    want_mode = "sharded" if torch.cuda.device_count() >= 2 else "skipped"
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_dist_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_dist_worker, args=(r, world, port, q)) for r in range(world)]
     for p in ps:
         p.start()
     res = sorted(q.get(timeout=120) for _ in ps)
     for p in ps:
         p.join(60)
-    assert res == [(0, True, want_mode), (1, True, want_mode)]
+    npr = (world + 1) // 2
+    for rank, arm, pr, qr, seen, by_p, by_q, d_p, d_q in res:
+        assert pr == list(range(npr)) and qr == list(range(npr, world))
+        assert arm == ("p" if rank < npr else "q")
+        grp = pr if arm == "p" else qr
+        assert seen == [(128, len(grp), grp.index(rank))]
+        assert (by_p, by_q, d_p, d_q) == (0, npr, 0, 10)
+
+
+def test_matrix_checksum_dev_matches_host():
+    """The on-device checksum every rank takes of its own C5 copy equals the
+    fixture's host checksum (synth.matrix_checksum)."""
+    import numpy as np
+    import torch
+    import bench
+    from tadpole_amd.synth import matrix_checksum, synth_hic_par
+    m = synth_hic_par(1500, 7, centromere=True)
+    assert np.array_equal(bench.matrix_checksum_dev(torch.from_numpy(m)), matrix_checksum(m))
+
+
+@pytest.mark.parametrize("n0,cen", [(700, True), (513, False), (256, True)])
+def test_synth_stream_equals_synth_hic_par(n0, cen):
+    """synth_hic_par_stream + place_upper_block (numpy and torch sinks) give
+    synth_hic_par's matrix bit for bit (the C5 input each rank draws itself)."""
+    import numpy as np
+    import torch
+    from tadpole_amd.synth import place_upper_block, synth_hic_par, synth_hic_par_stream
+    ref = synth_hic_par(n0, 99, centromere=cen)
+    M = np.full((n0, n0), -1.0)
+    z = synth_hic_par_stream(n0, 99, lambda r0, r1, U: place_upper_block(M, r0, r1, U), centromere=cen)
+    M[z, :] = 0
+    M[:, z] = 0
+    assert np.array_equal(M, ref)
+    T = torch.full((n0, n0), -1.0, dtype=torch.float64)
+    z = synth_hic_par_stream(n0, 99, lambda r0, r1, U: place_upper_block(T, r0, r1, torch.from_numpy(U)),
+                             centromere=cen, threads=3)
+    zi = torch.as_tensor(z)
+    T.index_fill_(0, zi, 0.0)
+    T.index_fill_(1, zi, 0.0)
+    assert np.array_equal(T.numpy(), ref)

@@ -363,6 +363,8 @@ def _nested(clusters):
 
 
 def test_c5_full_golden_and_sharded_bit_identical(gpu):
+    # (also: the arm-group schedule -- p and q each sharded over its own rank
+    # group, tadpole_amd.multi.init_arm_comms -- gives the same bits)
     """BASELINE config 5 at full size (chr1 @5kb shape: synth_hic_par(49 851,
     SEED_BASE + 5, centromere=True), the CPU-generated matrix of
     tests/golden/c5full.npz): TADpole(centromere_search=TRUE), bug-compatible
@@ -397,15 +399,30 @@ def test_c5_full_golden_and_sharded_bit_identical(gpu):
         g8 = tp.TADpole(dm, max_pcs=200, centromere_search=True, sharded=True, inplace=True)
     finally:
         multi.set_virtual_shards(1)
+    # the arm-group schedule of N = 5 ranks (bench.py --gpus 5: p over 3, q
+    # over 2): each arm sharded over its own group, merged after
+    from tadpole_amd import api
+    p_r, q_r = multi.arm_group_ranks(5)
+    bad, _, _ = api.mask_dev(dm, 0.01)
+    plan = api._arm_plan(bad)
+    subs = {}
+    for arm, nv in (("p", len(p_r)), ("q", len(q_r))):
+        multi.set_virtual_shards(nv)
+        try:
+            subs[arm] = api._run_arm(dm, plan, arm, 200, 2, 0, api._lib.TP_FLAG_SHARDED)
+        finally:
+            multi.set_virtual_shards(1)
+    g5 = api._merge_arms(plan, subs)
     del dm
     torch.cuda.empty_cache()
-    assert np.array_equal(g8.merging_arms, got.merging_arms)
-    for arm in ("p", "q"):
-        x, y = getattr(got, arm), getattr(g8, arm)
-        assert (x.n_pcs, x.optimal_n_clusters) == (y.n_pcs, y.optimal_n_clusters)
-        assert np.array_equal(x.scores.view(np.uint64), y.scores.view(np.uint64))
-        assert np.array_equal(x.dendro.boundary, y.dendro.boundary)
-        assert np.array_equal(x.dendro.height.view(np.uint64), y.dendro.height.view(np.uint64))
+    for g in (g8, g5):
+        assert np.array_equal(g.merging_arms, got.merging_arms)
+        for arm in ("p", "q"):
+            x, y = getattr(got, arm), getattr(g, arm)
+            assert (x.n_pcs, x.optimal_n_clusters) == (y.n_pcs, y.optimal_n_clusters)
+            assert np.array_equal(x.scores.view(np.uint64), y.scores.view(np.uint64))
+            assert np.array_equal(x.dendro.boundary, y.dendro.boundary)
+            assert np.array_equal(x.dendro.height.view(np.uint64), y.dendro.height.view(np.uint64))
 
 
 def test_gemm_ts_two_stage_prefetch_same_bits(gpu):

@@ -666,7 +666,7 @@ def test_gemm_rows_kernel_row_independent(gpu, M, N, K):
     print(f"rows gemm {M}x{N}x{K}: {t * 1e3:.1f} us, {2.0 * M * N * K / t / 1e9:.1f} TF/s")
 
 
-@pytest.mark.parametrize("K,M,N", [(4100, 302, 64), (7808, 130, 64), (4160, 9, 64)])
+@pytest.mark.parametrize("K,M,N", [(4100, 302, 64), (7808, 130, 64), (4160, 9, 64), (9000, 200, 64)])
 def test_prod_i8_digit_product(gpu, K, M, N):
     """The Krylov products on the int8 MFMA (digit images, knob 36) against
     an 80-bit reference of the same A'B with the rank-1 epilogue: within
@@ -701,3 +701,39 @@ def test_prod_i8_digit_product(gpu, K, M, N):
     e64 = float(np.max(np.abs(O64 - ref) / bound))
     print(f"prod_i8 K={K} M={M} N={N}: int8 {ms[0] * 1e3:.1f} us err {e8:.2e} | fp64 {ms[1] * 1e3:.1f} us err {e64:.2e}")
     assert e8 < 1e-14
+
+
+@pytest.mark.parametrize("K,M,col0,r0", [(4100, 330, 64, 64), (9000, 300, 128, 192), (7729, 400, 0, 128)])
+@pytest.mark.parametrize("kernel", [1, 3])
+def test_prod_i8_rows_slab_same_bits(gpu, K, M, col0, r0, kernel):
+    """A rank's row shard of an int8-digit product, from the digit image of
+    its own column slab [col0, M) (the C5 schedule: tp_shard.hip), carries
+    the bits of the same rows of the whole product; K > 8192 takes the
+    two-pass digitizers of the block (k_pd_colmax + k_pd_digits_sl) and of
+    A (k_pd_digits).  kernel: the product kernel (knob 36: 1 = k_pd_prod,
+    3 = k_pd_dma), which must agree bit for bit."""
+    import ctypes
+    rng = np.random.default_rng(K + M + col0)
+    A = np.asfortranarray(rng.uniform(-1, 1, size=(K, M)))
+    A[:, 70] *= 1e-7
+    B = np.asfortranarray(rng.standard_normal((K, 64)) / np.sqrt(K))
+    D = ctypes.POINTER(ctypes.c_double)
+    I = lambda v: ctypes.byref(ctypes.c_int(v))  # noqa: E731
+
+    def rows(c0, q0, nr):
+        O = np.zeros((nr, 64), order="F")
+        st = ctypes.c_int(0)
+        gpu.tp_debug_prod_i8_rows(A.ctypes.data_as(D), I(K), I(M), B.ctypes.data_as(D), I(64), I(c0), I(q0),
+                                  I(nr), O.ctypes.data_as(D), ctypes.byref(st))
+        assert st.value == 0
+        return O
+
+    old = G.knob(36, kernel)
+    try:
+        full = rows(0, 0, M)
+        part = rows(col0, r0, M - r0)
+    finally:
+        G.knob(36, old)
+    assert np.array_equal(part.view(np.uint64), full[r0:].view(np.uint64))
+    ref = A.T @ B
+    assert np.abs(full - ref).max() <= 1e-14 * (np.abs(A).T @ np.abs(B)).max()

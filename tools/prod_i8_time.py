@@ -1,6 +1,8 @@
-"""Device time of one C3-size int8-digit product (tp_debug_prod_i8 at K = 7808,
-M = 7810, N = 64) against the fp64 path; no reference check (diagnostic builds
-give wrong results by design)."""
+"""Device time of one C3-size int8-digit product (tp_debug_prod_i8 at K = 7729,
+M = 7731, N = 64: B's digits + the product + the split-K reduce) for each
+product kernel (knob 36: 1 = k_pd_prod<1>, 2 = k_pd_prod<2>, 3 = k_pd_dma)
+against the fp64 path, and whether the kernels give the same bits.
+python tools/prod_i8_time.py [K]"""
 import ctypes
 import os
 import sys
@@ -12,14 +14,23 @@ from tadpole_amd import _lib  # noqa: E402
 
 L = _lib.load()
 D = ctypes.POINTER(ctypes.c_double)
-K, M, N = 7808, 7810, 64
+I = lambda v: ctypes.byref(ctypes.c_int(v))  # noqa: E731
+K = int(sys.argv[1]) if len(sys.argv) > 1 else 7729
+M, N = K + 2, 64
 rng = np.random.default_rng(1)
 A = np.asfortranarray(rng.uniform(-1, 1, size=(K, M)))
 B = np.asfortranarray(rng.standard_normal((K, N)) / np.sqrt(K))
-O8 = np.zeros((M - 1, N), order="F"); O64 = np.zeros((M - 1, N), order="F"); ms = np.zeros(2); st = ctypes.c_int(0)
-I = lambda v: ctypes.byref(ctypes.c_int(v))  # noqa: E731
-L.tp_debug_prod_i8(A.ctypes.data_as(D), I(K), I(M), B.ctypes.data_as(D), I(N), O8.ctypes.data_as(D),
-                   O64.ctypes.data_as(D), ms.ctypes.data_as(D), ctypes.byref(st))
-_lib.check(st)
-print(f"{os.path.basename(os.environ.get('TADPOLE_LIB', 'default'))}: int8 product {ms[0] * 1e3:.1f} us, "
-      f"fp64 {ms[1] * 1e3:.1f} us, max |diff| {np.max(np.abs(O8 - O64)):.2e}", flush=True)
+outs = {}
+for kn in (1, 3, 2):
+    old = ctypes.c_int(0); st = ctypes.c_int(0)
+    L.tp_debug_knob(I(36), I(kn), ctypes.byref(old), ctypes.byref(st))
+    _lib.check(st)
+    O8 = np.zeros((M - 1, N), order="F"); O64 = np.zeros((M - 1, N), order="F"); ms = np.zeros(2)
+    L.tp_debug_prod_i8(A.ctypes.data_as(D), I(K), I(M), B.ctypes.data_as(D), I(N), O8.ctypes.data_as(D),
+                       O64.ctypes.data_as(D), ms.ctypes.data_as(D), ctypes.byref(st))
+    _lib.check(st)
+    outs[kn] = O8
+    same = np.array_equal(O8.view(np.uint64), outs[1].view(np.uint64))
+    print(f"K={K} knob36={kn}: int8 product {ms[0] * 1e3:.1f} us, fp64 {ms[1] * 1e3:.1f} us, "
+          f"max |int8 - fp64| {np.max(np.abs(O8 - O64)):.2e}, bits == knob 1: {same}", flush=True)
+L.tp_debug_knob(I(36), I(1), ctypes.byref(ctypes.c_int(0)), ctypes.byref(ctypes.c_int(0)))
