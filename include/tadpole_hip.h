@@ -45,7 +45,9 @@ enum {
                                rep(NA, n_cluster) at R/TADpole.R:115            */
     TP_ERR_CAPACITY = 4,    /* an output array is too small (see *_cap args)     */
     TP_ERR_NUMERIC = 5,     /* PCA did not converge / non-finite scores          */
-    TP_ERR_UNSUPPORTED = 6  /* size beyond what this build handles               */
+    TP_ERR_UNSUPPORTED = 6, /* size beyond what this build handles               */
+    TP_ERR_INTERNAL = 7     /* an internal invariant failed (a library bug); in
+                               a sharded call it aborts the communicator        */
 };
 
 /* flags for tp_pipeline / tp_mask */

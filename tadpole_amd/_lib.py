@@ -14,7 +14,8 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TADPOLE_LIB") or os.path.join(_HERE, "libtadpole_hip.so")   # override: debugging builds
 
-TP_OK, TP_ERR_ARG, TP_ERR_HIP, TP_ERR_NO_BSTICK, TP_ERR_CAPACITY, TP_ERR_NUMERIC, TP_ERR_UNSUPPORTED = range(7)
+TP_OK, TP_ERR_ARG, TP_ERR_HIP, TP_ERR_NO_BSTICK, TP_ERR_CAPACITY, TP_ERR_NUMERIC, TP_ERR_UNSUPPORTED, TP_ERR_INTERNAL = \
+    range(8)
 TP_FLAG_ROW_MAJOR = 1
 TP_FLAG_CLEAN = 2
 TP_FLAG_NO_MASK = 4

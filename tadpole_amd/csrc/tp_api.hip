@@ -629,7 +629,10 @@ static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_cl
     // their collectives through their deadline (see stream_sync).  Data errors
     // (bad arguments, no broken-stick level, capacity, no convergence) come
     // from the replicated inputs and hit every rank at the same point, so the
-    // communicator stays usable.
+    // communicator stays usable.  Checks of rank-local state (a shard's rows
+    // against its slab or digit image) fail with TP_ERR_INTERNAL, which
+    // aborts: its peers would otherwise wait in their collectives until the
+    // deadline.
     struct ShardScope {
         Ctx &c;
         int pending;

@@ -40,20 +40,43 @@ namespace tp {
 int g_prod_i8 = 1;
 
 constexpr int PD_DIG = 7;   // digits per value
+#ifndef TP_PD_ADIG
+// digits of A the product reads, and the digits A's image stores.  6: the
+// (6, 0) pair and A's least significant digit dropped.  Dropping a balanced
+// digit (|d_6| <= 128 at weight 2^(e - 54)) leaves A's image within 2^(e - 47)
+// of A, 2^-46..2^-47 of the column's largest |x| -- a fixed perturbation of C
+// shared by every product of the PCA, not per-product rounding (~7e-15 on C's
+// entries; errors 3e-17 -> 5e-16..9e-16 of sum |A||B|; C3 products 6.63 ->
+// 6.12 ms with the first layout)
+#define TP_PD_ADIG 6
+#endif
+constexpr int PD_ADIG = TP_PD_ADIG;
 typedef int pd_i32x4 __attribute__((ext_vector_type(4)));
 
 // Digit image layout (both operands): 64 columns x 64 k bytes per block, the
-// PD_DIG digit blocks of one (column tile, k step) contiguous --
-//   ((c / 64) nsteps + k / 64) PD_DIG 4096 + s 4096 + (c % 64) 64 + k % 64
+// ND digit blocks of one (column tile, k step) contiguous (ND = PD_ADIG for
+// A, whose last digit the product never reads; PD_DIG for the blocks) --
+//   ((c / 64) nsteps + k / 64) ND 4096 + s 4096 + (c % 64) 64 + k % 64
 // -- so a workgroup's k step of A (64 rows, six digits) is one contiguous 24 KB
 // read (DRAM pages streamed, not 64-byte pieces of 384 columns).
 constexpr int PD_BLK = 4096;
+template <int ND>
 __device__ __forceinline__ size_t pd_off(int c, int k, int nsteps) {
-    return ((size_t)(c >> 6) * nsteps + (k >> 6)) * (PD_DIG * PD_BLK) + (size_t)(c & 63) * 64 + (k & 63);
+    return ((size_t)(c >> 6) * nsteps + (k >> 6)) * (ND * PD_BLK) + (size_t)(c & 63) * 64 + (k & 63);
+}
+
+// 2^(54 - e) and 2^(e - 54) for a column with largest |x| < 2^e, e clamped
+// at -968 so the scale stays finite (columns below 2^-968 lose their low bits)
+__device__ __forceinline__ int pd_exp(double mx) {
+    int e = 0;
+    if (mx > 0.0 && isfinite(mx)) (void)frexp(mx, &e);
+    return max(e, -968);
 }
 
 // Digits of x[k0..k0+3] (zero past K or when !ok): one 4-byte word per digit,
-// digit s at d + s PD_BLK (d = the image at pd_off(c, k0))
+// digit s < ND at d + s PD_BLK (d = the image at pd_off<ND>(c, k0)); all seven
+// are formed (the carries), the first ND stored
+template <int ND>
 __device__ __forceinline__ void pd_digits4(const double *__restrict__ x, int K, int k0, bool ok, double sc,
                                            int8_t *__restrict__ d) {
     long long q[4];
@@ -78,13 +101,14 @@ __device__ __forceinline__ void pd_digits4(const double *__restrict__ x, int K, 
         w[0] |= ((unsigned)(r & 0xFF)) << (8 * u);   // |r| <= 64
     }
 #pragma unroll
-    for (int s = 0; s < PD_DIG; ++s) *(unsigned *)(d + (size_t)s * PD_BLK) = w[s];
+    for (int s = 0; s < ND; ++s) *(unsigned *)(d + (size_t)s * PD_BLK) = w[s];
 }
 
 // Digits of one column per workgroup: column c of X (K values, ld ldx) ->
 // the image at pd_off(c, k) (k < Kp; zero past K and for c >= cols), the column
 // scale 2^(e - 54) into scale[c] (NaN for a non-finite column, so the product
 // is NaN as the fp64 one would be).
+template <int ND>
 __global__ void __launch_bounds__(256) k_pd_digits(const double *__restrict__ X, int ldx, int K, int cols, int Kp,
                                                    int8_t *__restrict__ D, double *__restrict__ scale) {
     __shared__ double red[4];
@@ -105,19 +129,19 @@ __global__ void __launch_bounds__(256) k_pd_digits(const double *__restrict__ X,
     if ((t & 63) == 0) red[t >> 6] = mx;
     __syncthreads();
     mx = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
-    int e = 0;
-    if (mx > 0.0 && isfinite(mx)) (void)frexp(mx, &e);   // mx < 2^e
+    const int e = pd_exp(mx);   // mx < 2^e
     const double sc = ldexp(1.0, 54 - e);
     if (t == 0) scale[c] = !live ? 0.0 : (isfinite(mx) ? ldexp(1.0, e - 54) : NAN);
     const int nsteps = Kp / 64;
-    for (int k0 = 4 * t; k0 < Kp; k0 += 1024) pd_digits4(x, K, k0, live && isfinite(mx), sc, D + pd_off(c, k0, nsteps));
+    for (int k0 = 4 * t; k0 < Kp; k0 += 1024)
+        pd_digits4<ND>(x, K, k0, live && isfinite(mx), sc, D + pd_off<ND>(c, k0, nsteps));
 }
 
 // The same, for K <= 1024 IT: the column is read once (values kept in
 // registers across the max and the digits), thread t holding k = 1024 i + 4 t
 // .. + 3 -- one HBM pass over C instead of two (the second pass of k_pd_digits
 // misses L2 at C3: 1.87 GB moved for 0.9 GB of data)
-template <int IT>
+template <int IT, int ND>
 __global__ void __launch_bounds__(256) k_pd_digits_reg(const double *__restrict__ X, int ldx, int K, int cols, int Kp,
                                                        int8_t *__restrict__ D, double *__restrict__ scale) {
     __shared__ double red[4];
@@ -146,8 +170,7 @@ __global__ void __launch_bounds__(256) k_pd_digits_reg(const double *__restrict_
     if ((t & 63) == 0) red[t >> 6] = mx;
     __syncthreads();
     mx = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
-    int e = 0;
-    if (mx > 0.0 && isfinite(mx)) (void)frexp(mx, &e);   // mx < 2^e
+    const int e = pd_exp(mx);   // mx < 2^e
     const double sc = ldexp(1.0, 54 - e);
     if (t == 0) scale[c] = !live ? 0.0 : (isfinite(mx) ? ldexp(1.0, e - 54) : NAN);
     const bool ok = live && isfinite(mx);
@@ -155,7 +178,7 @@ __global__ void __launch_bounds__(256) k_pd_digits_reg(const double *__restrict_
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
         const int k0 = 1024 * i + 4 * t;
-        if (k0 < Kp) pd_digits4(v[i], 4, 0, ok, sc, D + pd_off(c, k0, nsteps));
+        if (k0 < Kp) pd_digits4<ND>(v[i], 4, 0, ok, sc, D + pd_off<ND>(c, k0, nsteps));
     }
 }
 constexpr int PD_REG_IT = 8;   // register path up to K = 8192
@@ -194,11 +217,11 @@ __global__ void __launch_bounds__(256) k_pd_digits_sl(const double *__restrict__
     const int t = threadIdx.x;
     double mx = 0.0;
     for (int q = 0; q < SL; ++q) mx = fmax(mx, pmax[c * SL + q]);
-    int e = 0;
-    if (mx > 0.0 && isfinite(mx)) (void)frexp(mx, &e);
+    const int e = pd_exp(mx);
     if (sl == 0 && t == 0) scale[c] = isfinite(mx) ? ldexp(1.0, e - 54) : NAN;
     const int k0 = sl * 1024 + 4 * t;
-    if (k0 < Kp) pd_digits4(X + (size_t)c * ldx, K, k0, isfinite(mx), ldexp(1.0, 54 - e), D + pd_off(c, k0, Kp / 64));
+    if (k0 < Kp)
+        pd_digits4<PD_DIG>(X + (size_t)c * ldx, K, k0, isfinite(mx), ldexp(1.0, 54 - e), D + pd_off<PD_DIG>(c, k0, Kp / 64));
 }
 
 // Out partials: rows [0, M) of A'B from the digit images Da (A's column tiles
@@ -207,18 +230,15 @@ __global__ void __launch_bounds__(256) k_pd_digits_sl(const double *__restrict__
 // seven accumulators each): 64 rows x 64 columns a workgroup; blockIdx ->
 // (row tile, k chunk) dealt XCD-contiguously.  Each 64-byte k step of both
 // images (PD_ADIG x 4 KB of A, 7 x 4 KB of B, each a contiguous run) is
-// staged through LDS (80-byte rows: the 16-lane b128 fragment reads spread
-// over the banks), double-buffered, with two k steps of loads in flight in two
-// register sets (one barrier a step; ~143 KB of LDS: one workgroup a CU).
+// staged through registers into LDS (80-byte rows: the 16-lane b128 fragment
+// reads spread over the banks).
+// NB = 1 (the default): one LDS buffer of 62 KB (PD_BUF), the next step's
+// loads in registers while this step's MFMAs run, two barriers a step, two
+// workgroups a CU (each one's MFMAs run under the other's waits).
+// NB = 2 (knob 36 = 2): two LDS buffers (124 KB, one workgroup a CU), two k
+// steps of loads in flight in two register sets, one barrier a step.
 constexpr int PD_LD = 80;                        // LDS row stride (bytes)
-#ifndef TP_PD_ADIG
-#define TP_PD_ADIG 6   // digits of A read by the product (6: without the (6, 0) pair, A to 2^-49 of its column
-                       // maximum: C3 products 6.63 -> 6.12 ms, errors 3e-17 -> 5e-16..9e-16 of sum |A||B|)
-#endif
-constexpr int PD_ADIG = TP_PD_ADIG;
 constexpr int PD_ASZ = PD_ADIG * 64 * PD_LD, PD_BUF = PD_ASZ + PD_DIG * 64 * PD_LD;
-// NB = 1: one LDS buffer (66.5 KB), one step of loads ahead, two workgroups a
-// CU (each one's MFMAs run under the other's waits)
 template <int NB>
 __global__ void __launch_bounds__(256, 3 - NB) k_pd_prod(const int8_t *__restrict__ Da, int Kp, int M,
                                                     const int8_t *__restrict__ Db, const double *__restrict__ rs,
@@ -246,18 +266,19 @@ __global__ void __launch_bounds__(256, 3 - NB) k_pd_prod(const int8_t *__restric
     // staging: thread t moves bytes 16 t .. 16 t + 15 of every 4 KB digit block
     // (row t / 4, k quarter t % 4) of the step
     const int sr = t >> 2, sk = (t & 3) * 16;
-    const int8_t *ga = Da + (size_t)bm * nsteps * (PD_DIG * PD_BLK) + 16 * t;
+    const int8_t *ga = Da + (size_t)bm * nsteps * (PD_ADIG * PD_BLK) + 16 * t;
     const int8_t *gb = Db + 16 * t;
     const int T = (kend - kbeg) / 64, st0 = kbeg / 64;
     pd_i32x4 ra[PD_DIG], rb[PD_DIG], xa[PD_DIG], xb[PD_DIG];
     // loads past the chunk re-read its last step (clamped, unconditional: the
     // compiler counts them) and land in the buffer no later step reads
     auto gload = [&](pd_i32x4 (&ta)[PD_DIG], pd_i32x4 (&tb)[PD_DIG], int st) {
-        const size_t o = (size_t)(st0 + min(st, T - 1)) * (PD_DIG * PD_BLK);
+        const int sk = st0 + min(st, T - 1);
+        const size_t oa = (size_t)sk * (PD_ADIG * PD_BLK), ob = (size_t)sk * (PD_DIG * PD_BLK);
 #pragma unroll
         for (int s = 0; s < PD_DIG; ++s) {
-            if (s < PD_ADIG) ta[s] = *(const pd_i32x4 *)(ga + o + s * PD_BLK);
-            tb[s] = *(const pd_i32x4 *)(gb + o + s * PD_BLK);
+            if (s < PD_ADIG) ta[s] = *(const pd_i32x4 *)(ga + oa + s * PD_BLK);
+            tb[s] = *(const pd_i32x4 *)(gb + ob + s * PD_BLK);
         }
     };
     auto lstore = [&](const pd_i32x4 (&ta)[PD_DIG], const pd_i32x4 (&tb)[PD_DIG], int bf) {
@@ -396,16 +417,17 @@ __global__ void __launch_bounds__(256, 1) k_pd_dma(const int8_t *__restrict__ Da
     // DMA sources: column 16 w + (lane >> 2) of this wave's A row tile and B
     // column tile, k quarter swizzled
     const int pc = lane >> 2, pk = (lane & 3) ^ ((lane >> 4) & 2);
-    const int8_t *asrc = Da + (size_t)bm * nsteps * (PD_DIG * PD_BLK) + (size_t)(16 * w + pc) * 64 + 16 * pk;
+    const int8_t *asrc = Da + (size_t)bm * nsteps * (PD_ADIG * PD_BLK) + (size_t)(16 * w + pc) * 64 + 16 * pk;
     const int8_t *bsrc = Db + (size_t)(16 * w + pc) * 64 + 16 * pk;
     const int roff = (4 * fr + (kq ^ ((fr >> 2) & 2))) * 16;   // fragment (fr, kq) in a chunk
     auto issue = [&](int k) {   // step k (clamped) into ring slot k % PD_RING: A digits, then B digits
-        const size_t o = (size_t)(st0 + min(k, T - 1)) * (PD_DIG * PD_BLK);
+        const int sk = st0 + min(k, T - 1);
+        const size_t oa = (size_t)sk * (PD_ADIG * PD_BLK), ob = (size_t)sk * (PD_DIG * PD_BLK);
         int8_t *dst = L + (k % PD_RING) * PD_STAGE + w * 1024;
 #pragma unroll
-        for (int s = 0; s < PD_ADIG; ++s) pd_glds16(asrc + o + s * PD_BLK, dst + s * 4096);
+        for (int s = 0; s < PD_ADIG; ++s) pd_glds16(asrc + oa + s * PD_BLK, dst + s * 4096);
 #pragma unroll
-        for (int s = 0; s < PD_DIG; ++s) pd_glds16(bsrc + o + s * PD_BLK, dst + PD_BOFF + s * 4096);
+        for (int s = 0; s < PD_DIG; ++s) pd_glds16(bsrc + ob + s * PD_BLK, dst + PD_BOFF + s * 4096);
     };
     pd_i32x4 acc[PD_DIG][4];
 #pragma unroll
@@ -489,15 +511,17 @@ void prod_digits_build(Ctx &c, const double *A, int lda, int K, int cols, int co
     // tile (prod_i8_partials)
     const int cp = (cols + 63) / 64 * 64;
     pd.slice = (size_t)cp * pd.Kp;   // bytes of one digit over the image
-    char *base = c.buf[S_PDIGA].as<char>(PD_DIG * pd.slice + (size_t)cp * sizeof(double) + 256);
+    // A's image keeps the PD_ADIG digits the product reads (the
+    // seventh was written and never read, n^2 bytes a PCA)
+    char *base = c.buf[S_PDIGA].as<char>(PD_ADIG * pd.slice + (size_t)cp * sizeof(double) + 256);
     pd.d = (int8_t *)base;
-    pd.rs = (double *)(base + (PD_DIG * pd.slice + 255) / 256 * 256);
+    pd.rs = (double *)(base + (PD_ADIG * pd.slice + 255) / 256 * 256);
     if (pd.Kp <= 1024 * PD_REG_IT)
-        hipLaunchKernelGGL(k_pd_digits_reg<PD_REG_IT>, dim3((unsigned)cp), dim3(256), 0, s, A, lda, K, cols, pd.Kp,
-                           (int8_t *)pd.d, (double *)pd.rs);
+        hipLaunchKernelGGL((k_pd_digits_reg<PD_REG_IT, PD_ADIG>), dim3((unsigned)cp), dim3(256), 0, s, A, lda, K, cols,
+                           pd.Kp, (int8_t *)pd.d, (double *)pd.rs);
     else
-        hipLaunchKernelGGL(k_pd_digits, dim3((unsigned)cp), dim3(256), 0, s, A, lda, K, cols, pd.Kp, (int8_t *)pd.d,
-                           (double *)pd.rs);
+        hipLaunchKernelGGL(k_pd_digits<PD_ADIG>, dim3((unsigned)cp), dim3(256), 0, s, A, lda, K, cols, pd.Kp,
+                           (int8_t *)pd.d, (double *)pd.rs);
     TP_HIP(hipGetLastError());
 }
 
@@ -508,7 +532,7 @@ int prod_i8_partials(Ctx &c, const ProdDigits &pd, int r0, int M, const double *
     hipStream_t s = c.cur;
     if (!prod_i8_ok(K, N) || (K + 63) / 64 * 64 != pd.Kp || r0 < pd.col0 || r0 + M > pd.col0 + pd.cols ||
         (r0 - pd.col0) % 64)
-        fail(TP_ERR_ARG, "prod_i8: rows outside the digit image or off its 64-column tiles, or an unsupported block");
+        fail(TP_ERR_INTERNAL, "prod_i8: rows outside the digit image or off its 64-column tiles, or an unsupported block");
     const size_t slb = (size_t)N * pd.Kp;
     char *bb = c.buf[S_PDIGB].as<char>(PD_DIG * slb + 256 + 512 * sizeof(double) +
                                         (size_t)N * ((pd.Kp + 1023) / 1024) * sizeof(double));
@@ -517,8 +541,8 @@ int prod_i8_partials(Ctx &c, const ProdDigits &pd, int r0, int M, const double *
     const int SL = (pd.Kp + 1023) / 1024;
     double *pmax = (double *)(bb + (PD_DIG * slb + 255) / 256 * 256 + 512 * sizeof(double));
     if (pd.Kp <= 1024 * PD_REG_IT) {   // one launch, the block read once
-        hipLaunchKernelGGL(k_pd_digits_reg<PD_REG_IT>, dim3((unsigned)N), dim3(256), 0, s, B, ldb, K, N, pd.Kp, Db,
-                           cs);
+        hipLaunchKernelGGL((k_pd_digits_reg<PD_REG_IT, PD_DIG>), dim3((unsigned)N), dim3(256), 0, s, B, ldb, K, N, pd.Kp,
+                           Db, cs);
     } else {
         hipLaunchKernelGGL(k_pd_colmax, dim3((unsigned)(N * SL)), dim3(256), 0, s, B, ldb, K, SL, pmax);
         hipLaunchKernelGGL(k_pd_digits_sl, dim3((unsigned)(N * SL)), dim3(256), 0, s, B, ldb, K, pd.Kp, SL, pmax, Db,
@@ -528,7 +552,7 @@ int prod_i8_partials(Ctx &c, const ProdDigits &pd, int r0, int M, const double *
     const int S = (pd.Kp + kc - 1) / kc;
     const size_t pstride = (size_t)M * N;
     *part = work.as<double>(pstride * S);
-    const int8_t *Da = pd.d + (size_t)(r0 - pd.col0) * pd.Kp * PD_DIG;   // whole tiles: 64 columns x Kp x PD_DIG
+    const int8_t *Da = pd.d + (size_t)(r0 - pd.col0) * pd.Kp * PD_ADIG;   // whole tiles: 64 columns x Kp x PD_ADIG
     const double *rs = pd.rs + (r0 - pd.col0);
     const int tm = (M + 63) / 64;
     // one LDS buffer, two workgroups a CU: the 32 C3 products 4.57 ms against

@@ -461,7 +461,7 @@ void rows_gemm_sharded(Ctx &c, const double *A, int lda, int M, const double *B,
     double *T = c.buf[S_SHARD].as<double>((size_t)M * N);
     for (int r = 0; r < R; ++r) {
         if (!shard_mine(c, r) || rb[r + 1] <= rb[r]) continue;
-        if (rb[r] < a_col0) fail(TP_ERR_ARG, "rows_gemm_sharded: shard rows outside this rank's slab");
+        if (rb[r] < a_col0) fail(TP_ERR_INTERNAL, "rows_gemm_sharded: shard rows outside this rank's slab");
         if (i8) {   // the same k chunks as unsharded: the same element bits
             const int Mr = rb[r + 1] - rb[r];
             double *part = nullptr;

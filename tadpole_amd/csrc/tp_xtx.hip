@@ -764,7 +764,7 @@ static void launch_xtx128_t(Ctx &c, unsigned nb, const int8_t *sl, int n, int Kp
         unsigned *nzw = nullptr;
         const int NW = (Kp / 64 + 31) / 32;
         if (NS == 2 && g_xtx_nz) {
-            if (NW > 64) fail(TP_ERR_ARG, "xtx_int8: k blocks past the 64-word nonzero map");
+            if (NW > 64) fail(TP_ERR_INTERNAL, "xtx_int8: k blocks past the 64-word nonzero map");
             nzw = c.buf[S_XNZ].as<unsigned>((size_t)(Np / 128) * NW);
             hipLaunchKernelGGL(k_slice_nz, dim3((unsigned)(Np / 128), (unsigned)NW), dim3(256), 0, c.cur,
                                sl + (size_t)Np * Kp, Kp, NW, nzw);

@@ -31,7 +31,8 @@ def test_version_and_status_codes():
     L = _lib.load()
     assert L.tp_version() == 2
     txt = open(os.path.join(ROOT, "include", "tadpole_hip.h")).read()
-    for name, val in [("TP_OK", 0), ("TP_ERR_ARG", 1), ("TP_ERR_HIP", 2), ("TP_ERR_NO_BSTICK", 3)]:
+    for name, val in [("TP_OK", 0), ("TP_ERR_ARG", 1), ("TP_ERR_HIP", 2), ("TP_ERR_NO_BSTICK", 3),
+                      ("TP_ERR_CAPACITY", 4), ("TP_ERR_NUMERIC", 5), ("TP_ERR_UNSUPPORTED", 6), ("TP_ERR_INTERNAL", 7)]:
         assert re.search(rf"{name}\s*=\s*{val}\b", txt)
         assert getattr(_lib, name) == val
 

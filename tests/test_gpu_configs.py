@@ -101,7 +101,7 @@ def test_pca_krylov_path_vs_lapack(gpu, forced, space):
     or of C: knob 20; G with the first CGS pass against every block instead of
     the last two: knob 28; C with the first PIP pass against every block
     instead of K_0 and the last two: knob 33; G with the products on the int8
-    MFMA from 7-digit images: knob 36) against LAPACK's SVD on a matrix below its default
+    MFMA from digit images -- six digits of C, seven of each block: knob 36) against LAPACK's SVD on a matrix below its default
     size threshold (forced) and the G-formed path on the same matrix: every
     prefix subspace the sweep uses agrees."""
     n0 = 2600
