@@ -363,6 +363,112 @@ __global__ void __launch_bounds__(256, 3 - NB) k_pd_prod(const int8_t *__restric
             }
 }
 
+// k_pd_prod128: the k_pd_prod<1> schedule (same pairs, sums, combine and k
+// chunks: the same bits) with 128-row tiles -- 8 waves in 4 x 2, each a 32 x
+// 32 output block, one workgroup a CU (97 KB of LDS, 2 waves a SIMD).  The
+// block's digits (28 KB a step) are re-read by every row tile, more than half
+// of what a 64-row workgroup loads; two row tiles per workgroup halve that
+// share (76 KB a step for the MFMAs of two 64-row workgroups' 104 KB).
+// Threads 0..255 stage row tile 2 bm and the block, 256..511 row tile 2 bm + 1.
+constexpr int PD_ASZ2 = PD_ADIG * 128 * PD_LD, PD_BUF2 = PD_ASZ2 + PD_DIG * 64 * PD_LD;
+__global__ void __launch_bounds__(512, 1) k_pd_prod128(const int8_t *__restrict__ Da, int Kp, int M,
+                                                       const int8_t *__restrict__ Db, const double *__restrict__ rs,
+                                                       const double *__restrict__ cs, double *__restrict__ part,
+                                                       size_t pstride, int kchunk) {
+    extern __shared__ __attribute__((aligned(16))) int8_t pd_lds[];
+    const int tm = (M + 127) / 128, tm64 = (M + 63) / 64;
+    const int total = (int)gridDim.x;
+    const int xcd = (int)blockIdx.x & 7, slot = (int)blockIdx.x >> 3;
+    const int Lg = xcd * (total >> 3) + min(xcd, total & 7) + slot;
+    const int bm = Lg % tm, z = Lg / tm;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int wr = w & 3, wc = w >> 2;
+    const int fr = lane & 15, fk = (lane >> 4) * 16;
+    const int kbeg = z * kchunk, kend = min(Kp, kbeg + kchunk);
+    const int nsteps = Kp / 64;
+    TP_DASSERT(Kp % 64 == 0 && kchunk % 64 == 0 && kend - kbeg >= 64);
+    pd_i32x4 acc[PD_DIG][2][2];
+#pragma unroll
+    for (int u = 0; u < PD_DIG; ++u)
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b) acc[u][a][b] = pd_i32x4{0, 0, 0, 0};
+    const int h = t >> 8, tt = t & 255;
+    const int sr = tt >> 2, sk = (tt & 3) * 16;
+    // a second row tile past the image (odd tile count) re-reads the last one:
+    // its rows are past M and never stored
+    const int8_t *ga = Da + (size_t)min(2 * bm + h, tm64 - 1) * nsteps * (PD_ADIG * PD_BLK) + 16 * tt;
+    const int8_t *gb = Db + 16 * tt;
+    const int T = (kend - kbeg) / 64, st0 = kbeg / 64;
+    pd_i32x4 ra[PD_ADIG], rb[PD_DIG];
+    auto gload = [&](int st) {
+        const int sk2 = st0 + min(st, T - 1);
+        const size_t oa = (size_t)sk2 * (PD_ADIG * PD_BLK), ob = (size_t)sk2 * (PD_DIG * PD_BLK);
+#pragma unroll
+        for (int s = 0; s < PD_ADIG; ++s) ra[s] = *(const pd_i32x4 *)(ga + oa + s * PD_BLK);
+        if (h == 0) {
+#pragma unroll
+            for (int s = 0; s < PD_DIG; ++s) rb[s] = *(const pd_i32x4 *)(gb + ob + s * PD_BLK);
+        }
+    };
+    auto lstore = [&]() {
+#pragma unroll
+        for (int s = 0; s < PD_ADIG; ++s) *(pd_i32x4 *)(pd_lds + (s * 128 + 64 * h + sr) * PD_LD + sk) = ra[s];
+        if (h == 0) {
+#pragma unroll
+            for (int s = 0; s < PD_DIG; ++s) *(pd_i32x4 *)(pd_lds + PD_ASZ2 + (s * 64 + sr) * PD_LD + sk) = rb[s];
+        }
+    };
+    auto mstep = [&]() {
+        pd_i32x4 fb[PD_DIG][2];
+#pragma unroll
+        for (int q = 0; q < PD_DIG; ++q)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+                fb[q][b] = *(const pd_i32x4 *)(pd_lds + PD_ASZ2 + (q * 64 + 32 * wc + 16 * b + fr) * PD_LD + fk);
+#pragma unroll
+        for (int s0 = 0; s0 < PD_ADIG; ++s0) {
+            pd_i32x4 fa[2];
+#pragma unroll
+            for (int a = 0; a < 2; ++a) fa[a] = *(const pd_i32x4 *)(pd_lds + (s0 * 128 + 32 * wr + 16 * a + fr) * PD_LD + fk);
+#pragma unroll
+            for (int q = 0; q + s0 < PD_DIG; ++q)
+#pragma unroll
+                for (int a = 0; a < 2; ++a)
+#pragma unroll
+                    for (int b = 0; b < 2; ++b)
+                        acc[s0 + q][a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[a], fb[q][b], acc[s0 + q][a][b], 0, 0, 0);
+        }
+    };
+    gload(0);
+    lstore();
+    __syncthreads();
+    for (int st = 0; st < T; ++st) {
+        gload(st + 1);
+        mstep();
+        __syncthreads();
+        lstore();
+        __syncthreads();
+    }
+    const int i0 = bm * 128 + 32 * wr, j0 = 32 * wc;
+    double *P = part + pstride * z;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = i0 + 16 * a + (lane >> 4) * 4 + r;
+                const int j = j0 + 16 * b + fr;
+                if (i >= M) continue;
+                double v = 0.0;
+#pragma unroll
+                for (int u = PD_DIG - 1; u >= 0; --u) v += (double)acc[u][a][b][r] * ldexp(1.0, 96 - 8 * u);
+                P[(size_t)i + (size_t)j * M] = (v * rs[i]) * cs[j];
+            }
+}
+
 // k_pd_dma: the same products (same pairs, same int32 sums, same combine: the
 // bits of k_pd_prod), built for the HBM stream (round 5).  k_pd_prod moved 52
 // KB a k step per workgroup through registers and ds_write_b128, one step in
@@ -557,7 +663,10 @@ int prod_i8_partials(Ctx &c, const ProdDigits &pd, int r0, int M, const double *
     const int tm = (M + 63) / 64;
     // one LDS buffer, two workgroups a CU: the 32 C3 products 4.57 ms against
     // 5.35 for the double-buffered one-workgroup form (knob 36 = 2, A/B)
-    if (g_prod_i8 == 3)
+    if (g_prod_i8 == 4)
+        hipLaunchKernelGGL(k_pd_prod128, dim3((unsigned)((M + 127) / 128 * S)), dim3(512), (size_t)PD_BUF2, s, Da, pd.Kp,
+                           M, Db, rs, cs, *part, pstride, kc);
+    else if (g_prod_i8 == 3)
         hipLaunchKernelGGL(k_pd_dma, dim3((unsigned)(tm * S)), dim3(256), 0, s, Da, pd.Kp, M, Db, rs, cs, *part,
                            pstride, kc);
     else if (g_prod_i8 == 2)
