@@ -258,6 +258,18 @@ def run_c5_arm(device, max_pcs, reps):
 C4_GOLDEN = ("chr21", "chr22", "chr19", "chr1")
 
 
+def _phase_summary(ph):
+    tot = {}
+    for d in ph.values():
+        for k, v in d.items():
+            tot[k] = tot.get(k, 0.0) + v
+    out = {k: round(v, 4) for k, v in sorted(tot.items())}
+    if ph:
+        c = max(ph, key=lambda q: sum(v for k, v in ph[q].items() if k != "wait"))
+        out["slowest"] = {"chrom": c, **{k: round(v, 4) for k, v in sorted(ph[c].items())}}
+    return out
+
+
 def run_c4_genome(world, rank, max_pcs, reps, streams=8):
     """C4: the 23 hg19 chromosomes @25 kb (synthetic counts of the real bin
     numbers) through run_genome over every rank of the default process group:
@@ -276,15 +288,18 @@ def run_c4_genome(world, rank, max_pcs, reps, streams=8):
     run_genome(mats, sizes=sizes, streams=streams, max_pcs=max_pcs)     # warm-up (contexts, code objects)
     walls, res, rep_secs = [], None, []
     ctx0 = _lib.context_stats(torch_device())[1]
+    rep_phases = []
     for _ in range(max(1, reps)):
         if world > 1:
             dist.barrier()
+        ph = {}
         t0 = time.perf_counter()
-        res, secs = run_genome(mats, sizes=sizes, streams=streams, max_pcs=max_pcs)
+        res, secs = run_genome(mats, sizes=sizes, streams=streams, max_pcs=max_pcs, phases=ph)
         if world > 1:
             dist.barrier()
         walls.append(time.perf_counter() - t0)
         rep_secs.append(secs)
+        rep_phases.append(ph)
     ctx_new = _lib.context_stats(torch_device())[1] - ctx0
     if rank != 0:
         return None
@@ -297,6 +312,10 @@ def run_c4_genome(world, rank, max_pcs, reps, streams=8):
            # and the library contexts rank 0 created during the timed reps (0: the stream pool reuses them)
            "chrom_s_per_rep": [{c: round(v, 4) for c, v in sorted(sc.items())} for sc in rep_secs],
            "contexts_created_in_timed_reps_rank0": ctx_new,
+           # rank 0's chromosomes, per timed rep: summed seconds of each phase (queue wait for a
+           # stream worker, upload through the pinned staging, library call, Python assembly)
+           # and the slowest chromosome's split
+           "phases_rank0": [_phase_summary(ph) for ph in rep_phases],
            "workload": "C4: 23 hg19 chromosomes @25 kb (synthetic, synth_hic_par), max_pcs=%d, one run_genome "
                        "call; host-resident matrices (H2D copies and host assembly included)" % max_pcs}
     par = {}

@@ -132,6 +132,16 @@ void tp_read_tsv_dev(const char **path, const int *nrow, const int *ncol,
                      const int *nthreads, const int *device, void *stream,
                      double *d_out, int *status);
 
+/* Host -> device copy of `bytes` bytes of a pageable host buffer into d_dst
+ * (device memory of `device`), queued on `stream` (hipStream_t, NULL: the
+ * library's) through that stream's context's pinned staging: 16 MB blocks in
+ * a ring of three, each block's host copy (nthreads threads, 0 = 1) overlapped
+ * with the previous blocks' DMAs; returns when the data is on the device.
+ * Stands where R's .C/ctypes caller would hand tp_pipeline a host matrix but
+ * wants tp_pipeline_dev's stream (concurrent pipelines per GPU). */
+void tp_upload_dev(const void *host, const long long *bytes, void *d_dst, const int *nthreads,
+                   const int *device, void *stream, int *status);
+
 /* ------------------------------------------------------------------- mask */
 /* R/TADpole.R:19-20 (NA->0, forceSymmetric(uplo='U')), :35-37 (rowMeans, diag==0,
  * quantile type 7 at bad_frac), :88-89 (subset).  M: n0 x n0.  Outputs:

@@ -12,6 +12,7 @@ out of scope: they draw, they do not compute.
 from __future__ import annotations
 
 import ctypes
+import time
 import logging
 import os
 import struct
@@ -96,6 +97,9 @@ class Tadpole:
     q: Optional["Tadpole"] = None
     bad_columns: Optional[np.ndarray] = None                        # 1-based original indices
     timings_ms: Optional[np.ndarray] = None
+    # host seconds of this call's phases (upload through the pinned staging,
+    # the library call, the Python assembly); not part of R's object
+    host_s: Dict[str, float] = field(default_factory=dict)
 
     def __getitem__(self, key):
         return getattr(self, key)
@@ -327,6 +331,8 @@ def _pipeline(m, max_pcs: int, min_clusters: int, bad_frac: float, flags: int,
         m, lay = _layout(m)
         flags |= lay
     n0 = m.shape[0]
+    t0 = time.perf_counter()
+    t_up = 0.0
     k_cap = max(1, min(max_pcs, n0))
     w_cap = max(1, n0)
     bad = np.zeros(n0, np.int32)
@@ -360,9 +366,18 @@ def _pipeline(m, max_pcs: int, min_clusters: int, bad_frac: float, flags: int,
                 stream.wait_stream(torch.cuda.current_stream(device))
         else:
             host = m if m.flags["C_CONTIGUOUS"] else np.ascontiguousarray(m.T)   # same buffer order as `lay`
+            host = np.ascontiguousarray(host, dtype=np.float64)
             with torch.cuda.stream(stream):
-                dm = torch.from_numpy(host).to(f"cuda:{device}", non_blocking=False)
-            stream.synchronize()
+                dm = torch.empty(host.shape, dtype=torch.float64, device=f"cuda:{device}")
+            # through this stream's context's pinned staging (tp_upload_dev): a
+            # pageable .to(device) shares the runtime's one staging path with
+            # every other stream of the process
+            ust = cint(0)
+            L.tp_upload_dev(ctypes.c_void_p(host.ctypes.data), ctypes.byref(ctypes.c_longlong(host.nbytes)),
+                            ctypes.c_void_p(dm.data_ptr()), ctypes.byref(cint(_upload_threads(host.nbytes))),
+                            ctypes.byref(cint(device)), ctypes.c_void_p(stream.cuda_stream), ctypes.byref(ust))
+            _lib.check(ust)
+            t_up = time.perf_counter() - t0
         L.tp_pipeline_dev(ctypes.c_void_p(dm.data_ptr()), ctypes.byref(cint(n0)), ctypes.byref(cint(max_pcs)),
                           ctypes.byref(cint(min_clusters)), ctypes.byref(cdbl(bad_frac)), ctypes.byref(cint(flags)),
                           ctypes.byref(cint(device)), ctypes.c_void_p(stream.cuda_stream),
@@ -372,13 +387,21 @@ def _pipeline(m, max_pcs: int, min_clusters: int, bad_frac: float, flags: int,
                           ctypes.byref(st))
         del dm
     _lib.check(st)
+    t_call = time.perf_counter() - t0 - t_up
     n = n_good.value
     kk, ww = k.value, w.value
     sc = scores[:kk * ww].reshape(ww, kk).T.copy()
     return dict(bad=bad.astype(bool), good=good[:n].copy(), k=kk, w=ww, n_cluster=nclu[:kk].copy(),
                 scores=sc, n_pcs=n_pcs.value, n_clusters=n_clusters.value,
                 merge=merge[:2 * (n - 1)].reshape(2, n - 1).T.copy(), height=height[:n - 1].copy(),
-                boundary=boundary[:n - 1].copy(), timings=timings)
+                boundary=boundary[:n - 1].copy(), timings=timings,
+                host_s={"upload": t_up, "call": t_call})
+
+
+def _upload_threads(nbytes: int) -> int:
+    """Host threads for one tp_upload_dev copy: one for small matrices (the
+    genome driver runs several uploads at once), a few for large ones."""
+    return 1 if nbytes < (256 << 20) else 4
 
 
 def mask_dev(dm, bad_frac: float = 0.01, stream=None):
@@ -583,7 +606,9 @@ def TADpole(mat_file, max_pcs: int = 200, min_clusters: int = 2, bad_frac: float
         bad_idx1 = np.flatnonzero(res["bad"]) + 1
         _message(f"{len(bad_idx1)} bad columns found at position(s):", verbose)
         _message(" ".join(str(int(b)) for b in bad_idx1), verbose)
+        ta = time.perf_counter()
         t = _assemble(res, bad_idx1)
+        t.host_s = dict(res["host_s"], assemble=time.perf_counter() - ta)
         _message(f"Optimal number of PCs: {t.n_pcs}", verbose)
         _message(f"Optimal number of clusters: {t.optimal_n_clusters}", verbose)
         return t

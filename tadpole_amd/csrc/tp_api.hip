@@ -754,8 +754,9 @@ static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_cl
     // C's column means, for prcomp (C's tail, or the [m | 1] buffer of a slab)
     double *cmean = use_slab ? c.buf[S_MEXT].as<double>(2 * (size_t)n) : (g_cor_fused ? C + (size_t)n * n : nullptr);
     trace_mark(s, "cor: start");
+    bool cm_defer = !use_slab;   // C's means in the PCA's digit pass when C comes from the int8 X'X
     cor_product(c, X, n, m, prep ? &gs : nullptr, nullptr, C, c.buf[S_DIAG].as<double>(n), cmean,
-                use_slab ? &slab : nullptr);
+                use_slab ? &slab : nullptr, &cm_defer);
     trace_mark(s, "cor");
     tm.mark();
     progress.set(2);
@@ -764,7 +765,7 @@ static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_cl
     if (k > k_cap) fail(TP_ERR_CAPACITY, "k_cap smaller than min(max_pcs, n_good)");
     double *P = c.buf[S_P].as<double>((size_t)n * k);
     double *Pt = c.buf[S_PT].as<double>(pt_doubles(n, k));
-    PcaStats ps = pca_dev(c, C, n, k, P, Pt, nullptr, cmean, sc0, sc1);
+    PcaStats ps = pca_dev(c, C, n, k, P, Pt, nullptr, cmean, sc0, sc1, cm_defer);
     trace_mark(s, "pca");
     tm.mark();
     // ---- find_params + final tree (R/TADpole.R:456-460)
@@ -1344,6 +1345,40 @@ void tp_debug_prod_i8_rows(const double *A, const int *K, const int *M, const do
     });
 }
 
+/* A's int8 digit image (test hook): columns of A (K x M) digitised as the
+ * PCA does -- fused = 1: the first M - 2 columns with their means in one pass
+ * (k_pd_digits_cm), then the last two; 0: k_pd_digits_reg / k_pd_digits.
+ * img: ND x ceil(M / 64) 64 x Kp bytes in the pd_off layout (ND = *nd on
+ * return), scale[ceil(M/64) 64], cm[M - 2] (fused only) and cm_ref[M - 2]
+ * (k_colmean on the same columns). */
+void tp_debug_pd_image(const double *A, const int *K, const int *M, const int *fused, int8_t *img, double *scale,
+                       double *cm, double *cm_ref, int *nd, int *status) {
+    guarded(status, [&] {
+        Ctx &c = ctx_for(0);
+        hipStream_t s = c.cur;
+        const int k = *K, m = *M;
+        if (k < 64 || m < 3) fail(TP_ERR_ARG, "pd_image: K >= 64, M >= 3");
+        double *dA = c.buf[S_C].as<double>((size_t)k * m);
+        double *dm = c.buf[S_Q].as<double>(2 * (size_t)m);
+        TP_HIP(hipMemcpyAsync(dA, A, (size_t)k * m * 8, hipMemcpyHostToDevice, s));
+        ProdDigits pd;
+        if (*fused) {
+            prod_digits_build(c, dA, k, k, m, 0, pd, dm, m - 2);
+            prod_digits_finish(c, dA, k, k, pd);
+        } else {
+            prod_digits_build(c, dA, k, k, m, 0, pd);
+        }
+        launch_colmean_cols(dA, k, m - 2, k, dm + m, s);
+        const int cp = (m + 63) / 64 * 64;
+        *nd = prod_i8_adig();
+        TP_HIP(hipMemcpyAsync(img, pd.d, (size_t)prod_i8_adig() * pd.slice, hipMemcpyDeviceToHost, s));
+        TP_HIP(hipMemcpyAsync(scale, pd.rs, (size_t)cp * 8, hipMemcpyDeviceToHost, s));
+        if (*fused) TP_HIP(hipMemcpyAsync(cm, dm, (size_t)(m - 2) * 8, hipMemcpyDeviceToHost, s));
+        TP_HIP(hipMemcpyAsync(cm_ref, dm + m, (size_t)(m - 2) * 8, hipMemcpyDeviceToHost, s));
+        TP_HIP(hipStreamSynchronize(s));
+    });
+}
+
 /* CholQR kernels for b <= 256 on Z = I: k_chol_inv + k_trsm_frag give
  * Y = U^{-1} (W = U'U, S-scaled, + rel on the scaled diagonal); diag[b] =
  * diag(U).  ms[0] chol kernel (the product's choice of waves), ms[1] info,
@@ -1506,6 +1541,55 @@ void tp_read_tsv(const char **path, const int *nrow, const int *ncol, const int 
         if (!path || !*path || !nrow || !ncol || !out) fail(TP_ERR_ARG, "null argument");
         const int th = (nthreads && *nthreads > 0) ? *nthreads : (int)std::max(1u, std::thread::hardware_concurrency());
         tp::tsv_read(*path, *nrow, *ncol, th, flags && (*flags & TP_FLAG_ROW_MAJOR), out);
+    });
+}
+
+// host -> device copy of a pageable buffer through this stream's context's
+// pinned staging: a ring of 3 x 16 MB slots, each block's memcpy into a slot
+// (nthreads host threads) overlapped with the previous blocks' DMAs.  A plain
+// pageable hipMemcpy goes through the runtime's one staging path, which the 8
+// streams of a genome run shared (C4: ~6 GB of matrices).
+void tp_upload_dev(const void *host, const long long *bytes, void *d_dst, const int *nthreads, const int *device,
+                   void *stream, int *status) {
+    guarded(status, [&] {
+        if (!host || !bytes || !d_dst || *bytes < 0) fail(TP_ERR_ARG, "null argument");
+        Ctx &c = ctx_for(dev_of(device), (hipStream_t)stream);
+        const size_t total = (size_t)*bytes;
+        if (total == 0) return;
+        constexpr int kSlots = 3;
+        constexpr size_t kBlock = (size_t)16 << 20;
+        for (int q = 0; q < kSlots; ++q)
+            if (!c.ring_ev[q]) TP_HIP(hipEventCreateWithFlags(&c.ring_ev[q], hipEventDisableTiming));
+        const size_t nb = (total + kBlock - 1) / kBlock;
+        const size_t slot_bytes = std::min(total, kBlock);
+        char *ring = (char *)c.pinned(kSlots * slot_bytes);
+        const int th = std::max(1, std::min(nthreads && *nthreads > 0 ? *nthreads : 1, 16));
+        for (size_t b = 0; b < nb; ++b) {
+            const int slot = (int)(b % kSlots);
+            if (b >= (size_t)kSlots) {   // the slot's previous DMA (a 16 MB copy, < 1 ms)
+                hipError_t q;
+                while ((q = hipEventQuery(c.ring_ev[slot])) == hipErrorNotReady) std::this_thread::yield();
+                TP_HIP(q);
+            }
+            const size_t off = b * kBlock, len = std::min(kBlock, total - off);
+            char *dst = ring + (size_t)slot * slot_bytes;
+            const char *src = (const char *)host + off;
+            if (th == 1 || len < ((size_t)1 << 20)) {
+                memcpy(dst, src, len);
+            } else {
+                std::vector<std::thread> ts;
+                const size_t part = (len / th + 63) & ~(size_t)63;
+                for (int t = 0; t < th; ++t) {
+                    const size_t o = (size_t)t * part;
+                    if (o >= len) break;
+                    ts.emplace_back([=] { memcpy(dst + o, src + o, std::min(part, len - o)); });
+                }
+                for (auto &x : ts) x.join();
+            }
+            TP_HIP(hipMemcpyAsync((char *)d_dst + off, dst, len, hipMemcpyHostToDevice, c.cur));
+            TP_HIP(hipEventRecord(c.ring_ev[slot], c.cur));
+        }
+        stream_sync(c, c.cur);   // the staging is reused by the next call on this context
     });
 }
 
@@ -1715,6 +1799,9 @@ void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
         case 35: p = &g_gemm_ts_pf2; break;
         case 36: p = &g_prod_i8; break;
         case 37: p = &g_sytrd32; break;
+        case 38: p = &g_pd_digits_blk; break;
+        case 39: p = &g_pd_cm; break;
+        case 40: p = &g_sync_spin_us; break;
         default: fail(TP_ERR_ARG, "unknown knob");
         }
         if (*which == 3 && *value != 16 && *value != 32) fail(TP_ERR_ARG, "stage depth must be 16 or 32");

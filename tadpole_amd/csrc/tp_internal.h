@@ -293,6 +293,7 @@ void launch_transpose(const double *d_A, int rows, int cols, int lda, double *d_
 bool eig_sym_supported(int b);
 extern int g_sytrd_reg;
 extern int g_sytrd32;
+extern int g_pd_digits_blk;
 void sytrd_stamped(double *A, int b, double *work, long long *d_stamps, hipStream_t s);
 void sytrd_which(double *A, int b, double *work, int which, hipStream_t s,
                  long long *d_stamps = nullptr);   // work: 3b (e, tau, d)
@@ -348,11 +349,20 @@ struct ProdDigits {
     const double *rs = nullptr;
     size_t slice = 0;
     int Kp = 0, col0 = 0, cols = 0;
+    int pending = 0;   // > 0: columns [pending, cols) not digitised yet (prod_digits_finish)
 };
 extern int g_prod_i8;
 bool prod_i8_ok(int K, int N);
 int prod_i8_pairs();   // digit pairs one int8 product sums (27 with six digits of A)
-void prod_digits_build(Ctx &c, const double *A, int lda, int K, int cols, int col0, ProdDigits &pd);
+int prod_i8_adig();    // digits of A the image stores
+// cm != nullptr: only columns [0, ncm) now, with their means (k_colmean's bits)
+// into cm; the rest after the caller has written them, by prod_digits_finish
+void prod_digits_build(Ctx &c, const double *A, int lda, int K, int cols, int col0, ProdDigits &pd,
+                       double *cm = nullptr, int ncm = 0);
+void prod_digits_finish(Ctx &c, const double *A, int lda, int K, ProdDigits &pd);
+bool prod_digits_means_ok(int K);
+extern int g_pd_cm;
+extern int g_sync_spin_us;
 int prod_i8_partials(Ctx &c, const ProdDigits &pd, int r0, int M, const double *B, int ldb, int N, int K,
                      DevBuf &work, double **part);
 // pd (optional): A's digit image; the product then runs on the int8 MFMA
@@ -402,8 +412,11 @@ struct CorSlab {
     std::vector<int> rb;
     bool narrow = false;
 };
+// cm_defer (in/out): true asks to leave d_cmean for the PCA's digit pass
+// (pca_dev's cm_pending) where C comes from the int8 X'X epilogue; it stays
+// true only if the means were left out
 void cor_product(Ctx &c, const double *d_X, int n, const double *d_m, const GatherStats *gs, double *d_S,
-                 double *d_C, double *d_sd, double *d_cmean, const CorSlab *slab = nullptr);
+                 double *d_C, double *d_sd, double *d_cmean, const CorSlab *slab = nullptr, bool *cm_defer = nullptr);
 // S = X'X by the exact int8 path when possible, sharded like sym_gemm_sharded
 void xtx_product(Ctx &c, const double *d_X, int n, double *d_S);
 
@@ -436,8 +449,11 @@ bool krylov_c_topk(Ctx &c, double *C, int c_col0, const double *mext, int n, int
 // caller already has them (may be d_C + n n), else computed here
 inline size_t pca_c_doubles(int n) { return (size_t)n * n + 2 * (size_t)n; }
 // c_col0 / c_col1: d_C holds only columns [c_col0, c_col1) of [C | m | 1] (a
-// C5 rank's slab, Krylov path; -1: all of them, with room for the two extra)
+// C5 rank's slab, Krylov path; -1: all of them, with room for the two extra).
+// cm_pending: d_cmean is the buffer for C's means, not filled yet (formed in
+// A's digit pass on the int8 Krylov path, else by k_colmean: the same bits)
 PcaStats pca_dev(Ctx &c, double *d_C, int n, int k, double *d_P, double *d_Pt,
-                 double *h_sdev, const double *d_cmean = nullptr, int c_col0 = 0, int c_col1 = -1);
+                 double *h_sdev, const double *d_cmean = nullptr, int c_col0 = 0, int c_col1 = -1,
+                 bool cm_pending = false);
 
 }  // namespace tp

@@ -669,10 +669,20 @@ static void krylov_topk(Ctx &c, double *C, int c_col0, const double *mext, int n
 }
 
 PcaStats pca_dev(Ctx &c, double *d_C, int n, int k, double *d_P, double *d_Pt, double *h_sdev,
-                 const double *d_cmean, int c_col0, int c_col1) {
+                 const double *d_cmean, int c_col0, int c_col1, bool cm_pending) {
     PcaStats st;
     hipStream_t s = c.cur;
     const double *mean = d_cmean;
+    const int b_est = std::min(n, ((k + std::max(32, k / 4) + 31) / 32) * 32);
+    const bool krylov = n >= g_pca_krylov_min && b_est < n;
+    const bool cspace = g_pca_ckrylov > 0 || (g_pca_ckrylov < 0 && n >= g_ckry_min);
+    const int cend = c_col1 < 0 ? n + 2 : c_col1;
+    const bool i8 = krylov && g_prod_i8 > 0 && !cspace && prod_i8_ok(n, krylov_block(k));
+    // cm_pending: d_cmean is where C's column means go; with the int8 products
+    // over all of [C | m | 1] they come out of A's digit pass (k_colmean's bits)
+    const bool cm_fused = cm_pending && i8 && c_col0 == 0 && cend == n + 2 && prod_digits_means_ok(n);
+    if (cm_pending && !d_cmean) fail(TP_ERR_INTERNAL, "pca_dev: pending means need their buffer");
+    if (cm_pending && !cm_fused) launch_colmean(d_C, n, n, const_cast<double *>(d_cmean), s);
     if (!mean) {
         double *cm = c.buf[S_COLMEAN].as<double>(n);
         launch_colmean(d_C, n, n, cm, s);
@@ -680,11 +690,15 @@ PcaStats pca_dev(Ctx &c, double *d_C, int n, int k, double *d_P, double *d_Pt, d
     }
     double *V = c.buf[S_W].as<double>((size_t)n * k);       // n x k, descending
     std::vector<double> h_theta;
-    const int b_est = std::min(n, ((k + std::max(32, k / 4) + 31) / 32) * 32);
-    const bool krylov = n >= g_pca_krylov_min && b_est < n;
     double *Xc = nullptr, *XcT = nullptr;
     if (c_col0 != 0 && !krylov) fail(TP_ERR_ARG, "pca_dev: a column slab of C needs the Krylov path");
     if (krylov) {
+        // the int8-digit image of this rank's columns of [C | m | 1] for the
+        // ~32 products with it (tp_prod_i8.hip); with fused means its first n
+        // columns now, m and 1 once they are written below
+        ProdDigits pdg;
+        const ProdDigits *pd = nullptr;
+        if (cm_fused) prod_digits_build(c, d_C, n, n, n + 2, 0, pdg, const_cast<double *>(d_cmean), n);
         // [m | 1] (the centring's rank-1 terms) for every rank, and as columns
         // n, n + 1 of [C | m | 1] (the products' extra rows m'B, 1'B) where
         // this rank holds them (all of C, or the last rank's slab)
@@ -692,18 +706,15 @@ PcaStats pca_dev(Ctx &c, double *d_C, int n, int k, double *d_P, double *d_Pt, d
         if (mean != mext) TP_HIP(hipMemcpyAsync(mext, mean, (size_t)n * sizeof(double), hipMemcpyDeviceToDevice, s));
         hipLaunchKernelGGL(k_fill_const, dim3((n + 255) / 256), dim3(256), 0, s, mext + n, n, 1.0);
         TP_HIP(hipGetLastError());
-        const int cend = c_col1 < 0 ? n + 2 : c_col1;
         if (c_col0 <= n && cend >= n + 2)
             TP_HIP(hipMemcpyAsync(d_C + (size_t)(n - c_col0) * n, mext, 2 * (size_t)n * sizeof(double),
                                   hipMemcpyDeviceToDevice, s));
         // neither Xc nor XcT is formed; the Krylov space of C (tp_krylov.hip),
         // or of G when an orthogonalisation pass of that path breaks down
-        // the int8-digit image of this rank's columns of [C | m | 1] for the
-        // ~32 products with it (tp_prod_i8.hip)
-        const bool cspace = g_pca_ckrylov > 0 || (g_pca_ckrylov < 0 && n >= g_ckry_min);
-        ProdDigits pdg;
-        const ProdDigits *pd = nullptr;
-        if (g_prod_i8 > 0 && !cspace && prod_i8_ok(n, krylov_block(k))) {
+        if (cm_fused) {
+            prod_digits_finish(c, d_C, n, n, pdg);
+            pd = &pdg;
+        } else if (i8) {
             prod_digits_build(c, d_C, n, n, cend - c_col0, c_col0, pdg);
             pd = &pdg;
         }

@@ -109,16 +109,40 @@ __device__ uint64_t radix_select(const double *r, int n, int rank, unsigned *his
             if ((key & pmask) == prefix) atomicAdd(&hist[(key >> shift) & 255], 1u);
         }
         __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned cum = 0;
-            int d = 0;
-            for (; d < 256; ++d) {
-                if (cum + hist[d] > (unsigned)rank) break;
-                cum += hist[d];
+        if (threadIdx.x < 64) {
+            // the digit d holding rank: wave 0 scans the histogram, four bins a
+            // lane (a serial 256-bin loop on one thread was ~10 us a pass)
+            const int l = threadIdx.x;
+            const unsigned h0 = hist[4 * l], h1 = hist[4 * l + 1], h2 = hist[4 * l + 2], h3 = hist[4 * l + 3];
+            unsigned incl = h0 + h1 + h2 + h3;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const unsigned y = __shfl_up(incl, o, 64);
+                if (l >= o) incl += y;
             }
-            rank -= (int)cum;
-            bcast[0] = prefix | ((uint64_t)d << shift);
-            bcast[1] = (uint64_t)rank;
+            const unsigned ex = incl - (h0 + h1 + h2 + h3);   // bins below 4 l
+            const unsigned rk = (unsigned)rank;
+            // the bin holding rank lies in the first lane whose inclusive sum exceeds it
+            const unsigned long long m = __ballot(incl > rk);
+            const int L = (int)__builtin_ctzll(m);   // m != 0: rank < the count of matching keys
+            if (l == L) {
+                unsigned cum = ex;
+                int d = 4 * l;
+                if (cum + h0 <= rk) {
+                    cum += h0;
+                    ++d;
+                    if (cum + h1 <= rk) {
+                        cum += h1;
+                        ++d;
+                        if (cum + h2 <= rk) {
+                            cum += h2;
+                            ++d;
+                        }
+                    }
+                }
+                bcast[0] = prefix | ((uint64_t)d << shift);
+                bcast[1] = (uint64_t)(rank - (int)cum);
+            }
         }
         __syncthreads();
         prefix = bcast[0];

@@ -38,6 +38,7 @@ namespace tp {
 // (test_prod_i8_digit_product); the 32 C3 products 4.6 ms against 6.3
 // 
 int g_prod_i8 = 1;
+int g_pd_digits_blk = 1;   // knob 38: the block's digits by (column, slice) workgroups (0: one per column); same bits
 
 constexpr int PD_DIG = 7;   // digits per value
 #ifndef TP_PD_ADIG
@@ -75,31 +76,33 @@ __device__ __forceinline__ int pd_exp(double mx) {
 
 // Digits of x[k0..k0+3] (zero past K or when !ok): one 4-byte word per digit,
 // digit s < ND at d + s PD_BLK (d = the image at pd_off<ND>(c, k0)); all seven
-// are formed (the carries), the first ND stored
+// are formed, the first ND stored.  The balanced digits (least significant
+// first: d = the signed low byte of r, r = (r - d) / 256) are the bytes of
+// u = q + 0x808080808080 -- the six low digits offset by 128 (xor 0x80), the
+// top digit byte 6 as is -- so no carry loop: one 64-bit add, then byte
+// permutes gather digit s of the four values into one word.
 template <int ND>
 __device__ __forceinline__ void pd_digits4(const double *__restrict__ x, int K, int k0, bool ok, double sc,
                                            int8_t *__restrict__ d) {
-    long long q[4];
+    unsigned lo[4], hi[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const int k = k0 + u;
         const double v = (ok && k < K) ? x[k] : 0.0;
-        q[u] = llrint(v * sc);   // |q| <= 2^54
+        const unsigned long long uq = (unsigned long long)llrint(v * sc) + 0x808080808080ULL;   // |q| <= 2^54
+        lo[u] = (unsigned)uq ^ 0x80808080u;
+        hi[u] = (unsigned)(uq >> 32) ^ 0x8080u;
     }
-    unsigned w[PD_DIG];
-#pragma unroll
-    for (int s = 0; s < PD_DIG; ++s) w[s] = 0u;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        long long r = q[u];
-#pragma unroll
-        for (int s = PD_DIG - 1; s >= 1; --s) {   // least significant first, balanced
-            const long long dd = (long long)(int8_t)(r & 0xFF);
-            w[s] |= ((unsigned)(dd & 0xFF)) << (8 * u);
-            r = (r - dd) >> 8;
-        }
-        w[0] |= ((unsigned)(r & 0xFF)) << (8 * u);   // |r| <= 64
-    }
+    // byte b of a[0..3] -> bytes 0..3 of one word (v_perm_b32: selector 0..3 the
+    // second operand's bytes, 4..7 the first's, 12 a zero byte)
+    auto gather = [](const unsigned (&a)[4], unsigned b) {
+        const unsigned sel = 0x0C0C0000u | ((4u + b) << 8) | b;
+        const unsigned t01 = __builtin_amdgcn_perm(a[1], a[0], sel);
+        const unsigned t23 = __builtin_amdgcn_perm(a[3], a[2], sel);
+        return __builtin_amdgcn_perm(t23, t01, 0x05040100u);
+    };
+    const unsigned w[PD_DIG] = {gather(hi, 2), gather(hi, 1), gather(hi, 0), gather(lo, 3),
+                                gather(lo, 2), gather(lo, 1), gather(lo, 0)};
 #pragma unroll
     for (int s = 0; s < ND; ++s) *(unsigned *)(d + (size_t)s * PD_BLK) = w[s];
 }
@@ -182,6 +185,139 @@ __global__ void __launch_bounds__(256) k_pd_digits_reg(const double *__restrict_
     }
 }
 constexpr int PD_REG_IT = 8;   // register path up to K = 8192
+
+// A's digit image and C's column means in one pass over C: two adjacent
+// columns (c0, c0 + 1) a workgroup of ten waves.
+//   waves 0..7 (digits): thread t = 32 g + 16 h + j holds column c0 + h, rows
+//     64 (g + 16 i) + 4 j .. + 3 (i < 8, K <= 8192) in registers; column maxima
+//     by a 16-lane-row butterfly and LDS (fmax: k_pd_digits_reg's scale bits);
+//     then each digit word store of a wave covers whole 128-byte lines of the
+//     image (the two columns' 64-byte halves side by side: one workgroup per
+//     column wrote half lines, ~3 TB/s);
+//   waves 8, 9 (means, c < ncm): column c0 + w - 8 streamed in k_colmean's
+//     order -- lane l sums rows l, l + 64, ... in double-double, then the wave
+//     butterfly -- from L2 (the digit waves read the same lines at the same
+//     time), so the means carry k_colmean's bits.
+// Columns [c_begin, c_end) (live below `cols`, zero digits above).  Replaces
+// k_colmean (124 us at C3) and the digit pass (~315 us).
+constexpr int PD_CM_W = 10;
+template <int ND>
+__global__ void __launch_bounds__(64 * PD_CM_W) k_pd_digits_cm(const double *__restrict__ X, int ldx, int K, int c_begin,
+                                                             int c_end, int cols, int Kp, int8_t *__restrict__ D,
+                                                             double *__restrict__ scale, double *__restrict__ cm,
+                                                             int ncm) {
+    __shared__ double red[8][2];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int c0 = c_begin + 2 * (int)blockIdx.x;
+    if (w >= 8) {   // ---- means
+        const int c = c0 + (w - 8);
+        __syncthreads();   // the digit waves' one barrier
+        if (c >= c_end || c >= ncm || c >= cols) return;
+        const double *x = X + (size_t)c * ldx;
+        double hs = 0.0, ls = 0.0;
+        constexpr int U = 16;   // two batches of U loads a lane in flight around the chain
+        double va[U], vb[U];
+        auto load = [&](double (&v)[U], int r) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = r + 64 * u < K ? x[r + 64 * u] : 0.0;
+        };
+        auto take = [&](const double (&v)[U], int r) {
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (r + 64 * u < K) dd_add_d(hs, ls, v[u]);
+        };
+        int r = lane;
+        load(va, r);
+        for (; r < K; r += 128 * U) {
+            load(vb, r + 64 * U);
+            take(va, r);
+            load(va, r + 128 * U);
+            take(vb, r + 64 * U);
+        }
+        wave_dd_sum(hs, ls);
+        if (lane == 0) cm[c] = dd_div_d(hs, ls, (double)K);
+        return;
+    }
+    // ---- digits
+    const int g = t >> 5, h = (t >> 4) & 1, j = t & 15;
+    const int c = c0 + h;
+    const bool inr = c < c_end;                 // this launch writes column c
+    const bool live = inr && c < cols;
+    const double *x = X + (size_t)min(c, c_end - 1) * ldx;
+    double v[8][4];
+    double mx = 0.0;
+    bool bad = false;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int k = 64 * (g + 16 * i) + 4 * j + u;
+            v[i][u] = (live && k < K) ? x[k] : 0.0;
+            mx = fmax(mx, fabs(v[i][u]));
+            bad |= !isfinite(v[i][u]);
+        }
+    mx = bad ? INFINITY : mx;
+#pragma unroll
+    for (int o = 1; o <= 32; o <<= 1)   // lanes of the same column: bit 4 (16) fixed
+        if (o != 16) mx = fmax(mx, __shfl_xor(mx, o, 64));
+    if ((lane & 47) == 0) red[w][h] = mx;   // lanes 0 and 16
+    __syncthreads();
+    mx = red[0][h];
+#pragma unroll
+    for (int q = 1; q < 8; ++q) mx = fmax(mx, red[q][h]);
+    if (!inr) return;
+    const int e = pd_exp(mx);   // mx < 2^e
+    const double sc = ldexp(1.0, 54 - e);
+    if (g == 0 && j == 0) scale[c] = !live ? 0.0 : (isfinite(mx) ? ldexp(1.0, e - 54) : NAN);
+    const bool ok = live && isfinite(mx);
+    const int nsteps = Kp / 64;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int k0 = 64 * (g + 16 * i) + 4 * j;
+        if (k0 < Kp) pd_digits4<ND>(v[i], 4, 0, ok, sc, D + pd_off<ND>(c, k0, nsteps));
+    }
+}
+
+// A Krylov block's digits (N = 64 columns): one workgroup per (column, 1024-row
+// slice), N x Kp / 1024 of them instead of N.  Each forms its column's largest
+// |x| from the whole column (the same loads and fmax as k_pd_digits_reg, so
+// the same scale bits) and digitises only its slice: the 64-workgroup form ran
+// its 32 k-rows of digit work a thread on a quarter of the chip.  Work item q
+// = slice * N + column, dealt XCD-contiguously so columns c and c + 1 of a
+// slice (the two halves of each 128-byte line of the image) share an L2.
+template <int IT>
+__global__ void __launch_bounds__(256) k_pd_digits_blk(const double *__restrict__ X, int ldx, int K, int N, int Kp,
+                                                       int8_t *__restrict__ D, double *__restrict__ scale) {
+    __shared__ double red[4];
+    const int G = (int)gridDim.x;
+    const int q = (int)(blockIdx.x & 7) * (G >> 3) + (int)(blockIdx.x >> 3);
+    const int c = q % N, sl = q / N;
+    const int t = threadIdx.x;
+    const double *x = X + (size_t)c * ldx;
+    double mx = 0.0;
+    bool bad = false;
+    double v[4];
+#pragma unroll
+    for (int i = 0; i < IT; ++i)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int k = 1024 * i + 4 * t + u;
+            const double y = k < K ? x[k] : 0.0;
+            mx = fmax(mx, fabs(y));
+            bad |= !isfinite(y);
+            if (i == sl) v[u] = y;
+        }
+    mx = bad ? INFINITY : mx;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
+    if ((t & 63) == 0) red[t >> 6] = mx;
+    __syncthreads();
+    mx = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+    const int e = pd_exp(mx);   // mx < 2^e
+    if (sl == 0 && t == 0) scale[c] = isfinite(mx) ? ldexp(1.0, e - 54) : NAN;
+    const int k0 = 1024 * sl + 4 * t;
+    if (k0 < Kp) pd_digits4<PD_DIG>(v, 4, 0, isfinite(mx), ldexp(1.0, 54 - e), D + pd_off<PD_DIG>(c, k0, Kp / 64));
+}
 
 // The same digits for a few columns (a Krylov block, N = 64): the column's
 // largest |x| from per-1024-row partial maxima (k_pd_colmax), one workgroup
@@ -599,6 +735,8 @@ static int pd_kchunk(int Kp) {
     return std::min(kc, 16384);
 }
 
+int prod_i8_adig() { return PD_ADIG; }
+
 int prod_i8_pairs() {
     int n = 0;
     for (int a = 0; a < PD_ADIG; ++a) n += PD_DIG - a;
@@ -608,7 +746,20 @@ int prod_i8_pairs() {
 // N = 64 (the G-space Krylov blocks; the kernel's workgroup is 64 x 64)
 bool prod_i8_ok(int K, int N) { return N == 64 && K >= 64; }
 
-void prod_digits_build(Ctx &c, const double *A, int lda, int K, int cols, int col0, ProdDigits &pd) {
+static void launch_digits_cm(const double *A, int lda, int K, int c_begin, int c_end, int cols, ProdDigits &pd,
+                             double *cm, int ncm, hipStream_t s) {
+    if (c_end <= c_begin) return;
+    hipLaunchKernelGGL(k_pd_digits_cm<PD_ADIG>, dim3((unsigned)((c_end - c_begin + 1) / 2)), dim3(64 * PD_CM_W), 0, s,
+                       A, lda, K, c_begin, c_end, cols, pd.Kp, (int8_t *)pd.d, (double *)pd.rs, cm, ncm);
+    TP_HIP(hipGetLastError());
+}
+
+int g_pd_cm = 1;   // knob 39: C's column means in A's digit pass (0: the separate k_colmean pass); same bits
+
+bool prod_digits_means_ok(int K) { return g_pd_cm && K >= 64 && (K + 63) / 64 * 64 <= 8192; }
+
+void prod_digits_build(Ctx &c, const double *A, int lda, int K, int cols, int col0, ProdDigits &pd, double *cm,
+                       int ncm) {
     hipStream_t s = c.cur;
     pd.Kp = (K + 63) / 64 * 64;
     pd.col0 = col0;
@@ -622,6 +773,16 @@ void prod_digits_build(Ctx &c, const double *A, int lda, int K, int cols, int co
     char *base = c.buf[S_PDIGA].as<char>(PD_ADIG * pd.slice + (size_t)cp * sizeof(double) + 256);
     pd.d = (int8_t *)base;
     pd.rs = (double *)(base + (PD_ADIG * pd.slice + 255) / 256 * 256);
+    pd.pending = 0;
+    if (cm) {
+        // columns [0, ncm) with their means now; [ncm, cp) by prod_digits_finish
+        // once the caller has written those columns (m and 1 come from the means)
+        if (!prod_digits_means_ok(K) || ncm < 1 || ncm > cols || col0 != 0)
+            fail(TP_ERR_INTERNAL, "prod_digits_build: means only over the leading columns of a whole image (K >= 64)");
+        launch_digits_cm(A, lda, K, 0, ncm, cols, pd, cm, ncm, s);
+        pd.pending = ncm;
+        return;
+    }
     if (pd.Kp <= 1024 * PD_REG_IT)
         hipLaunchKernelGGL((k_pd_digits_reg<PD_REG_IT, PD_ADIG>), dim3((unsigned)cp), dim3(256), 0, s, A, lda, K, cols,
                            pd.Kp, (int8_t *)pd.d, (double *)pd.rs);
@@ -631,13 +792,20 @@ void prod_digits_build(Ctx &c, const double *A, int lda, int K, int cols, int co
     TP_HIP(hipGetLastError());
 }
 
+void prod_digits_finish(Ctx &c, const double *A, int lda, int K, ProdDigits &pd) {
+    if (pd.pending <= 0) return;
+    const int cp = (pd.cols + 63) / 64 * 64;
+    launch_digits_cm(A, lda, K, pd.pending, cp, pd.cols, pd, nullptr, 0, c.cur);
+    pd.pending = 0;
+}
+
 // partials of rows [r0, r0 + M) (global column indices of A) of A'B into
 // `work`: returns the chunk count; pstride = M N
 int prod_i8_partials(Ctx &c, const ProdDigits &pd, int r0, int M, const double *B, int ldb, int N, int K,
                      DevBuf &work, double **part) {
     hipStream_t s = c.cur;
     if (!prod_i8_ok(K, N) || (K + 63) / 64 * 64 != pd.Kp || r0 < pd.col0 || r0 + M > pd.col0 + pd.cols ||
-        (r0 - pd.col0) % 64)
+        (r0 - pd.col0) % 64 || pd.pending)
         fail(TP_ERR_INTERNAL, "prod_i8: rows outside the digit image or off its 64-column tiles, or an unsupported block");
     const size_t slb = (size_t)N * pd.Kp;
     char *bb = c.buf[S_PDIGB].as<char>(PD_DIG * slb + 256 + 512 * sizeof(double) +
@@ -646,7 +814,10 @@ int prod_i8_partials(Ctx &c, const ProdDigits &pd, int r0, int M, const double *
     double *cs = (double *)(bb + (PD_DIG * slb + 255) / 256 * 256);
     const int SL = (pd.Kp + 1023) / 1024;
     double *pmax = (double *)(bb + (PD_DIG * slb + 255) / 256 * 256 + 512 * sizeof(double));
-    if (pd.Kp <= 1024 * PD_REG_IT) {   // one launch, the block read once
+    if (pd.Kp <= 1024 * PD_REG_IT && g_pd_digits_blk) {   // one launch, a workgroup per (column, slice)
+        hipLaunchKernelGGL((k_pd_digits_blk<PD_REG_IT>), dim3((unsigned)(N * SL)), dim3(256), 0, s, B, ldb, K, N, pd.Kp,
+                           Db, cs);
+    } else if (pd.Kp <= 1024 * PD_REG_IT) {   // one launch, the block read once
         hipLaunchKernelGGL((k_pd_digits_reg<PD_REG_IT, PD_DIG>), dim3((unsigned)N), dim3(256), 0, s, B, ldb, K, N, pd.Kp,
                            Db, cs);
     } else {

@@ -148,9 +148,32 @@ void comm_abort(Ctx &c) {
 
 int g_shard_inject = 0;   // test hook (knob 30): the next N sharded waits fail as a device error
 
+// Unsharded waits poll the stream (yielding the core) before blocking: the
+// pipeline's read-backs are short waits, and hipStreamSynchronize's blocking
+// wake-up put ~45 us between a copy and the next command (rocprof trace, four
+// such host round trips after the sweep, two in the mask).  Waits longer than
+// g_sync_spin_us block as before.
+int g_sync_spin_us = 20000;   // knob 40 (0: always block)
+template <typename Query, typename Block>
+static void poll_then_block(Query query, Block block) {
+    if (g_sync_spin_us > 0) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (;;) {
+            const hipError_t e = query();
+            if (e == hipSuccess) return;
+            if (e != hipErrorNotReady) TP_HIP(e);
+            if (std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() >
+                g_sync_spin_us)
+                break;
+            std::this_thread::yield();
+        }
+    }
+    TP_HIP(block());
+}
+
 void stream_sync(Ctx &c, hipStream_t s) {
     if (!(c.shard.active && c.shard.comm)) {
-        TP_HIP(hipStreamSynchronize(s));
+        poll_then_block([&] { return hipStreamQuery(s); }, [&] { return hipStreamSynchronize(s); });
         return;
     }
     if (g_shard_inject > 0) {
@@ -188,7 +211,7 @@ void event_mark(Ctx &c, hipStream_t s) {
 
 void event_sync(Ctx &c) {
     if (!(c.shard.active && c.shard.comm)) {
-        TP_HIP(hipEventSynchronize(c.sync_ev));
+        poll_then_block([&] { return hipEventQuery(c.sync_ev); }, [&] { return hipEventSynchronize(c.sync_ev); });
         return;
     }
     const auto t0 = std::chrono::steady_clock::now();
@@ -359,8 +382,10 @@ int g_xtx_fused = 1;
 int g_shard_slab = 1;   // 0: X'X into S, then the separate correlation epilogue (A/B, tests)
 
 void cor_product(Ctx &c, const double *X, int n, const double *m, const GatherStats *gs, double *S, double *C,
-                 double *sd, double *cmean, const CorSlab *slab) {
+                 double *sd, double *cmean, const CorSlab *slab, bool *cm_defer) {
     hipStream_t s = c.cur;
+    const bool defer = cm_defer && *cm_defer && cmean;
+    if (cm_defer) *cm_defer = false;   // set again where the means are left out
     if (slab) {
         // C5 row-sharded C: each shard computes only its columns (the tiles of
         // xtx_int8_slab128: same tiles and arithmetic, so the same bits) and
@@ -422,7 +447,8 @@ void cor_product(Ctx &c, const double *X, int n, const double *m, const GatherSt
         launch_clean_symmetrize(C, n, true, s);   // lower <- upper (cor is finite: NaN -> 0 done)
     }
     kprof_end(c, K_COR_GEMM);
-    if (cmean) launch_colmean(C, n, n, cmean, s);   // k_cor_epilogue_mean's bits
+    if (defer) *cm_defer = true;                         // the PCA's digit pass forms them
+    else if (cmean) launch_colmean(C, n, n, cmean, s);   // k_cor_epilogue_mean's bits
 }
 
 // Out (M x N col-major, ld M) = A' B with A stored K x M (col-major, lda) and

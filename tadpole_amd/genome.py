@@ -62,7 +62,8 @@ def matrix_cost(n_bins: int) -> float:
 
 def run_genome(matrices: Mapping[str, object], sizes: Optional[Mapping[str, int]] = None,
                runner: Optional[Callable[[str, object, int], object]] = None, streams: int = 8,
-               retries: int = 1, **tadpole_kwargs) -> Tuple[Dict[str, object], Dict[str, float]]:
+               retries: int = 1, phases: Optional[Dict[str, Dict[str, float]]] = None,
+               **tadpole_kwargs) -> Tuple[Dict[str, object], Dict[str, float]]:
     """Process every chromosome once across the ranks of the default process
     group (or locally when torch.distributed is not initialised).
 
@@ -77,6 +78,9 @@ def run_genome(matrices: Mapping[str, object], sizes: Optional[Mapping[str, int]
     a time.  What still fails afterwards raises a RuntimeError on every rank,
     naming the chromosomes and their last errors.
     Returns (results, seconds per chromosome) on rank 0 (empty dicts elsewhere).
+    ``phases`` (optional, filled on this rank): per chromosome the seconds it
+    waited for a stream worker (``wait``), then the result's ``host_s``
+    (``upload``, ``call``, ``assemble``) when the runner reports them.
     """
     import torch.distributed as dist
 
@@ -103,6 +107,8 @@ def run_genome(matrices: Mapping[str, object], sizes: Optional[Mapping[str, int]
     secs: Dict[str, float] = {}
     failed: Dict[str, str] = {}
 
+    t_submit = time.perf_counter()
+
     def one(name, run):
         m = matrices[name]
         try:
@@ -111,6 +117,8 @@ def run_genome(matrices: Mapping[str, object], sizes: Optional[Mapping[str, int]
             t0 = time.perf_counter()
             mine[name] = run(name, m, local)
             secs[name] = time.perf_counter() - t0
+            if phases is not None:
+                phases[name] = dict(wait=t0 - t_submit, **dict(getattr(mine[name], "host_s", {}) or {}))
             failed.pop(name, None)
         except Exception as e:   # noqa: BLE001 -- recorded, re-queued below
             failed[name] = f"{type(e).__name__}: {e}"

@@ -703,6 +703,114 @@ def test_prod_i8_digit_product(gpu, K, M, N):
     assert e8 < 1e-14
 
 
+def _digits_ref(x, nd):
+    """The digit image's restatement for one column: e from the largest |x|
+    (frexp, clamped at -968), q = rint(x 2^(54 - e)), balanced base-256 digits
+    least significant first (d = the signed low byte of r, r = (r - d) / 256),
+    the top digit last; the first nd digits, most significant first."""
+    mx = np.max(np.abs(x)) if x.size else 0.0
+    e = max(int(np.frexp(mx)[1]) if mx > 0 else 0, -968)
+    q = np.rint(x * np.ldexp(1.0, 54 - e)).astype(np.int64)
+    r = q.copy()
+    dig = [None] * 7
+    for s in range(6, 0, -1):
+        d = ((r & 0xFF) ^ 0x80) - 0x80
+        dig[s] = d
+        r = (r - d) >> 8
+    dig[0] = r
+    return np.stack(dig[:nd]).astype(np.int8), np.ldexp(1.0, e - 54)
+
+
+@pytest.mark.parametrize("K,M", [(7729, 260), (1000, 67), (4160, 130)])
+@pytest.mark.parametrize("fused", [1, 0])
+def test_pd_image_digits_and_fused_means(gpu, K, M, fused):
+    """A's int8 digit image against the restated digitisation (every byte, the
+    pd_off layout: ((c / 64) Kp / 64 + k / 64) ND 4096 + s 4096 + (c % 64) 64 +
+    k % 64), the per-column scales, zero digits past K and past M; with fused
+    = 1 (k_pd_digits_cm, the PCA's default) the column means of the first
+    M - 2 columns carry k_colmean's bits -- a zero column, tiny and huge
+    columns and a column of integers ride along."""
+    import ctypes
+    rng = np.random.default_rng(K + M)
+    A = rng.uniform(-1, 1, size=(K, M))
+    A[:, 1] = 0.0
+    A[:, 4] *= 1e-9
+    A[:, 6] *= 3.7e12
+    A[:, 9] = np.rint(A[:, 9] * 1000)
+    A[:, M - 2] = A[:, :M - 2].mean(axis=0)[:K] if K <= M - 2 else rng.uniform(-1, 1, K)
+    A[:, M - 1] = 1.0
+    A = np.asfortranarray(A)
+    cp = (M + 63) // 64 * 64
+    Kp = (K + 63) // 64 * 64
+    img = np.zeros(7 * cp * Kp, dtype=np.int8)
+    scale = np.zeros(cp)
+    cm = np.zeros(M - 2)
+    cm_ref = np.zeros(M - 2)
+    nd = ctypes.c_int(0)
+    st = ctypes.c_int(0)
+    D = ctypes.POINTER(ctypes.c_double)
+    I = lambda v: ctypes.byref(ctypes.c_int(v))  # noqa: E731
+    gpu.tp_debug_pd_image(A.ctypes.data_as(D), I(K), I(M), I(fused), img.ctypes.data_as(ctypes.POINTER(ctypes.c_int8)),
+                          scale.ctypes.data_as(D), cm.ctypes.data_as(D), cm_ref.ctypes.data_as(D), ctypes.byref(nd),
+                          ctypes.byref(st))
+    assert st.value == 0
+    ND = nd.value
+    nsteps = Kp // 64
+    # image[tile, kstep, s, col % 64, k % 64]
+    im = img[:ND * cp * Kp].reshape(cp // 64, nsteps, ND, 64, 64)
+    for c in range(cp):
+        got = im[c // 64, :, :, c % 64, :].transpose(1, 0, 2).reshape(ND, Kp)
+        if c >= M:
+            assert not got.any() and scale[c] == 0.0, c
+            continue
+        ref, sc = _digits_ref(A[:, c], ND)
+        assert scale[c] == sc, c
+        assert np.array_equal(got[:, :K], ref), c
+        assert not got[:, K:].any(), c
+    if fused:
+        assert np.array_equal(cm.view(np.uint64), cm_ref.view(np.uint64))
+    import math
+    exact = np.array([math.fsum(A[:, j]) / K for j in range(M - 2)])   # double-double: within an ulp or two
+    np.testing.assert_allclose(cm_ref, exact, rtol=5e-16, atol=0)
+
+
+@pytest.mark.parametrize("K", [64, 1000, 4100, 7729, 8192])
+def test_prod_i8_block_digitizers_same_bits(gpu, K):
+    """The block's digit image by (column, 1024-row slice) workgroups
+    (k_pd_digits_blk, knob 38 = 1, the default) against one workgroup per
+    column (k_pd_digits_reg, knob 38 = 0): the same column maxima, so the same
+    scales and digits -- the products agree bit for bit, a NaN column (NaN
+    products), a zero column and a huge column included."""
+    import ctypes
+    M = 200
+    rng = np.random.default_rng(K)
+    A = np.asfortranarray(rng.uniform(-1, 1, size=(K, M)))
+    B = rng.standard_normal((K, 64)) / np.sqrt(K)
+    B[:, 2] = 0.0
+    B[:, 9] *= 1e200
+    B[K // 2, 11] = np.nan
+    B = np.asfortranarray(B)
+    D = ctypes.POINTER(ctypes.c_double)
+    I = lambda v: ctypes.byref(ctypes.c_int(v))  # noqa: E731
+    outs = []
+    for kn in (1, 0):
+        old = G.knob(38, kn)
+        try:
+            O = np.zeros((M, 64), order="F")
+            st = ctypes.c_int(0)
+            gpu.tp_debug_prod_i8_rows(A.ctypes.data_as(D), I(K), I(M), B.ctypes.data_as(D), I(64), I(0), I(0),
+                                      I(M), O.ctypes.data_as(D), ctypes.byref(st))
+            assert st.value == 0
+        finally:
+            G.knob(38, old)
+        outs.append(O)
+    assert np.array_equal(outs[0].view(np.uint64), outs[1].view(np.uint64))
+    assert np.all(np.isnan(outs[0][:, 11])) and np.all(outs[0][:, 2] == 0.0)
+    ok = [j for j in range(64) if j != 11]
+    ref = A.T @ B[:, ok]
+    assert np.abs(outs[0][:, ok] - ref).max() <= 1e-14 * (np.abs(A).T @ np.abs(B[:, ok])).max(axis=0).max()
+
+
 @pytest.mark.parametrize("K,M,col0,r0", [(4100, 330, 64, 64), (9000, 300, 128, 192), (7729, 400, 0, 128)])
 @pytest.mark.parametrize("kernel", [1, 3, 4])
 def test_prod_i8_rows_slab_same_bits(gpu, K, M, col0, r0, kernel):

@@ -34,3 +34,13 @@ for kn in (1, 4, 3, 2):
     print(f"K={K} knob36={kn}: int8 product {ms[0] * 1e3:.1f} us, fp64 {ms[1] * 1e3:.1f} us, "
           f"max |int8 - fp64| {np.max(np.abs(O8 - O64)):.2e}, bits == knob 1: {same}", flush=True)
 L.tp_debug_knob(I(36), I(1), ctypes.byref(ctypes.c_int(0)), ctypes.byref(ctypes.c_int(0)))
+# the block digitizer: (column, slice) workgroups (knob 38 = 1) vs one per column
+for kn in (0, 1):
+    L.tp_debug_knob(I(38), I(kn), ctypes.byref(ctypes.c_int(0)), ctypes.byref(ctypes.c_int(0)))
+    O8 = np.zeros((M - 1, N), order="F"); O64 = np.zeros((M - 1, N), order="F"); ms = np.zeros(2)
+    st = ctypes.c_int(0)
+    L.tp_debug_prod_i8(A.ctypes.data_as(D), I(K), I(M), B.ctypes.data_as(D), I(N), O8.ctypes.data_as(D),
+                       O64.ctypes.data_as(D), ms.ctypes.data_as(D), ctypes.byref(st))
+    _lib.check(st)
+    same = np.array_equal(O8.view(np.uint64), outs[1].view(np.uint64))
+    print(f"K={K} knob38={kn}: digits + product + reduce {ms[0] * 1e3:.1f} us, bits == default: {same}", flush=True)
