@@ -289,6 +289,7 @@ def run_c4_genome(world, rank, max_pcs, reps, streams=8):
     walls, res, rep_secs = [], None, []
     ctx0 = _lib.context_stats(torch_device())[1]
     rep_phases = []
+    grows0 = _lib.debug_knob(41, 0)
     for _ in range(max(1, reps)):
         if world > 1:
             dist.barrier()
@@ -301,6 +302,7 @@ def run_c4_genome(world, rank, max_pcs, reps, streams=8):
         rep_secs.append(secs)
         rep_phases.append(ph)
     ctx_new = _lib.context_stats(torch_device())[1] - ctx0
+    grows = _lib.debug_knob(41, 0)   # scratch regrowths (each a device-wide sync) during the timed reps
     if rank != 0:
         return None
     bins = sum(sizes.values())
@@ -312,6 +314,8 @@ def run_c4_genome(world, rank, max_pcs, reps, streams=8):
            # and the library contexts rank 0 created during the timed reps (0: the stream pool reuses them)
            "chrom_s_per_rep": [{c: round(v, 4) for c, v in sorted(sc.items())} for sc in rep_secs],
            "contexts_created_in_timed_reps_rank0": ctx_new,
+           "scratch_regrowths_in_timed_reps_rank0": grows,
+           "scratch_regrowths_before_rank0": grows0,
            # rank 0's chromosomes, per timed rep: summed seconds of each phase (queue wait for a
            # stream worker, upload through the pinned staging, library call, Python assembly)
            # and the slowest chromosome's split

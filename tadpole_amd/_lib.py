@@ -167,3 +167,14 @@ def context_stats(device: int = 0):
                        ctypes.byref(st))
     check(st)
     return live.value, created.value
+
+
+def debug_knob(which: int, value: int) -> int:
+    """tp_debug_knob: set a library tuning switch (or, for 41, read and reset
+    the scratch-regrowth counter); returns the previous value."""
+    L = load()
+    old, st = ctypes.c_int(0), ctypes.c_int(0)
+    L.tp_debug_knob(ctypes.byref(ctypes.c_int(int(which))), ctypes.byref(ctypes.c_int(int(value))), ctypes.byref(old),
+                    ctypes.byref(st))
+    check(st)
+    return old.value

@@ -398,10 +398,17 @@ def _pipeline(m, max_pcs: int, min_clusters: int, bad_frac: float, flags: int,
                 host_s={"upload": t_up, "call": t_call})
 
 
+_UPLOAD_THREADS = int(os.environ.get("TP_UPLOAD_THREADS", "0"))
+
+
 def _upload_threads(nbytes: int) -> int:
-    """Host threads for one tp_upload_dev copy: one for small matrices (the
-    genome driver runs several uploads at once), a few for large ones."""
-    return 1 if nbytes < (256 << 20) else 4
+    """Host threads for one tp_upload_dev copy (TP_UPLOAD_THREADS overrides):
+    one for small matrices (the genome driver runs several uploads at once),
+    more for large ones -- the largest chromosome's upload is on a genome
+    run's critical path."""
+    if _UPLOAD_THREADS > 0:
+        return _UPLOAD_THREADS
+    return 1 if nbytes < (64 << 20) else (4 if nbytes < (256 << 20) else 8)
 
 
 def mask_dev(dm, bad_frac: float = 0.01, stream=None):

@@ -2,6 +2,7 @@
 // orchestration, and the host-side tail of find_params (R/TADpole.R:125-135:
 // NA-padded score matrix, rowMeans(na.rm=TRUE) in long double as R does, first
 // which.max) plus the hclust merge encoding of the chosen tree.
+#include <atomic>
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -47,23 +48,66 @@ void hip_check(hipError_t e, const char *what, const char *file, int line) {
     }
 }
 
+std::atomic<int> g_devbuf_grows{0};   // knob 41 (read / reset): scratch regrowths so far
+// knob 42: scratch grows in stream order (hipFreeAsync / hipMallocAsync on the
+// context's stream, the device pool keeping what is freed) instead of a
+// device-wide sync + hipFree + hipMalloc, which stalled every stream of a
+// genome run (C4: ~35 regrowths a run while contexts meet larger chromosomes)
+int g_devbuf_async = 1;
+
 void *DevBuf::get(size_t b) {
     if (b == 0) b = 8;
     if (b > bytes) {
-        // work queued on any stream may still read the old block
-        if (p) TP_HIP(hipDeviceSynchronize());
-        if (p) TP_HIP(hipFree(p));
-        p = nullptr;
-        size_t nb = std::max(b, bytes + bytes / 4);
-        TP_HIP(hipMalloc(&p, nb));
+        if (p) g_devbuf_grows.fetch_add(1, std::memory_order_relaxed);
+        const size_t nb = std::max(b, bytes + bytes / 4);
+        if (g_devbuf_async && owner && owner->cur) {
+            hipStream_t s = owner->cur;
+            if (p) {
+                // the old block's readers: this context's stream and its side
+                // stream (joined into it first); no other stream uses it
+                if (owner->side) {
+                    TP_HIP(hipEventRecord(owner->join_ev, owner->side));
+                    TP_HIP(hipStreamWaitEvent(s, owner->join_ev, 0));
+                }
+                if (pooled) {
+                    TP_HIP(hipFreeAsync(p, s));
+                } else {
+                    TP_HIP(hipDeviceSynchronize());
+                    TP_HIP(hipFree(p));
+                }
+                p = nullptr;
+            }
+            TP_HIP(hipMallocAsync(&p, nb, s));
+            pooled = true;
+        } else {
+            // work queued on any stream may still read the old block
+            if (p) TP_HIP(hipDeviceSynchronize());
+            if (p) {
+                if (pooled) TP_HIP(hipFreeAsync(p, nullptr));
+                else TP_HIP(hipFree(p));
+                if (pooled) TP_HIP(hipDeviceSynchronize());
+            }
+            p = nullptr;
+            TP_HIP(hipMalloc(&p, nb));
+            pooled = false;
+        }
         bytes = nb;
     }
     return p;
 }
 void DevBuf::release() {
-    if (p) (void)hipFree(p);
+    if (p) {
+        if (pooled) {   // every call that queued work on the context synchronised before returning
+            (void)hipDeviceSynchronize();
+            (void)hipFreeAsync(p, nullptr);
+            (void)hipDeviceSynchronize();
+        } else {
+            (void)hipFree(p);
+        }
+    }
     p = nullptr;
     bytes = 0;
+    pooled = false;
 }
 
 void *Ctx::pinned(size_t b) {
@@ -159,7 +203,18 @@ static int g_created[64];   // contexts made per device (under g_mu)
 static std::shared_ptr<Ctx> new_ctx(int device) {
     auto c = std::make_shared<Ctx>();
     c->device = device;
+    for (auto &b : c->buf) b.owner = c.get();
+    c->pinned_flag.owner = c.get();
     ++g_created[device];
+    static bool pool_set[64];
+    if (!pool_set[device]) {   // (under g_mu) the pool keeps what scratch regrowth frees, for reuse
+        hipMemPool_t pool;
+        if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
+            uint64_t keep = UINT64_MAX;
+            (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+        }
+        pool_set[device] = true;
+    }
     return c;
 }
 
@@ -1760,6 +1815,10 @@ extern "C" {
  * double-buffered one-workgroup kernel; 0: the fp64 k_gemm_ts). */
 void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
     guarded(status, [&] {
+        if (*which == 41) {   // a counter, not a switch: returns it and sets it to *value
+            *old = g_devbuf_grows.exchange(*value);
+            return;
+        }
         int *p = nullptr;
         switch (*which) {
         case 0: p = &g_ch_dedup; break;
@@ -1802,6 +1861,7 @@ void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
         case 38: p = &g_pd_digits_blk; break;
         case 39: p = &g_pd_cm; break;
         case 40: p = &g_sync_spin_us; break;
+        case 42: p = &g_devbuf_async; break;
         default: fail(TP_ERR_ARG, "unknown knob");
         }
         if (*which == 3 && *value != 16 && *value != 32) fail(TP_ERR_ARG, "stage depth must be 16 or 32");

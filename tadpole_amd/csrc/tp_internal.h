@@ -27,9 +27,12 @@ void hip_check(hipError_t e, const char *what, const char *file, int line);
 #define TP_HIP(x) ::tp::hip_check((x), #x, __FILE__, __LINE__)
 
 // Growable device scratch buffer.
+struct Ctx;
 struct DevBuf {
     void *p = nullptr;
     size_t bytes = 0;
+    Ctx *owner = nullptr;   // the context whose streams use the block
+    bool pooled = false;    // from the device's stream-ordered pool (hipMallocAsync)
     void *get(size_t b);
     template <class T> T *as(size_t count) { return static_cast<T *>(get(count * sizeof(T))); }
     void release();
@@ -363,6 +366,7 @@ void prod_digits_finish(Ctx &c, const double *A, int lda, int K, ProdDigits &pd)
 bool prod_digits_means_ok(int K);
 extern int g_pd_cm;
 extern int g_sync_spin_us;
+extern int g_devbuf_async;
 int prod_i8_partials(Ctx &c, const ProdDigits &pd, int r0, int M, const double *B, int ldb, int N, int K,
                      DevBuf &work, double **part);
 // pd (optional): A's digit image; the product then runs on the int8 MFMA
