@@ -142,6 +142,14 @@ void tp_read_tsv_dev(const char **path, const int *nrow, const int *ncol,
 void tp_upload_dev(const void *host, const long long *bytes, void *d_dst, const int *nthreads,
                    const int *device, void *stream, int *status);
 
+/* The same for a float64 matrix of `count` values: 16 MB blocks whose every
+ * value is an exact integer in [0, 65535] (Hi-C counts; no -0.0, NaN or
+ * fraction) travel as 16-bit integers and are widened on the device to the
+ * same doubles, any other block as float64.  *packed (may be NULL): bytes of
+ * float64 that travelled packed.  tp_pipeline's host matrix takes this path. */
+void tp_upload_counts_dev(const double *host, const long long *count, double *d_dst, const int *nthreads,
+                          const int *device, void *stream, long long *packed, int *status);
+
 /* ------------------------------------------------------------------- mask */
 /* R/TADpole.R:19-20 (NA->0, forceSymmetric(uplo='U')), :35-37 (rowMeans, diag==0,
  * quantile type 7 at bad_frac), :88-89 (subset).  M: n0 x n0.  Outputs:

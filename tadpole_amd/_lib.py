@@ -29,6 +29,7 @@ EXPORTS = (
     "tp_pipeline", "tp_pipeline_dev", "tp_sweep_dev", "tp_tsv_dims", "tp_read_tsv",
     "tp_comm_unique_id", "tp_comm_init", "tp_comm_destroy", "tp_set_virtual_shards", "tp_shard_plan",
     "tp_level_coords", "tp_read_tsv_dev", "tp_context_stats", "tp_progress_attach", "tp_upload_dev",
+    "tp_upload_counts_dev",
 )
 
 
@@ -96,6 +97,8 @@ def load() -> ctypes.CDLL:
     L.tp_context_stats.argtypes = [_I, _I, _I, _I]
     L.tp_progress_attach.argtypes = [_I, _V, _V, _I]
     L.tp_upload_dev.argtypes = [_V, ctypes.POINTER(ctypes.c_longlong), _V, _I, _I, _V, _I]
+    L.tp_upload_counts_dev.argtypes = [_V, ctypes.POINTER(ctypes.c_longlong), _V, _I, _I, _V,
+                                       ctypes.POINTER(ctypes.c_longlong), _I]
     if L.tp_version() != ABI_VERSION:
         raise ImportError(f"{LIB_PATH}: ABI version {L.tp_version()}, this binding needs {ABI_VERSION} (rebuild)")
     _lib = L

@@ -372,10 +372,12 @@ def _pipeline(m, max_pcs: int, min_clusters: int, bad_frac: float, flags: int,
             # through this stream's context's pinned staging (tp_upload_dev): a
             # pageable .to(device) shares the runtime's one staging path with
             # every other stream of the process
+            # (tp_upload_counts_dev): blocks of exact 16-bit counts travel packed
             ust = cint(0)
-            L.tp_upload_dev(ctypes.c_void_p(host.ctypes.data), ctypes.byref(ctypes.c_longlong(host.nbytes)),
-                            ctypes.c_void_p(dm.data_ptr()), ctypes.byref(cint(_upload_threads(host.nbytes))),
-                            ctypes.byref(cint(device)), ctypes.c_void_p(stream.cuda_stream), ctypes.byref(ust))
+            L.tp_upload_counts_dev(ctypes.c_void_p(host.ctypes.data), ctypes.byref(ctypes.c_longlong(host.size)),
+                                   ctypes.c_void_p(dm.data_ptr()), ctypes.byref(cint(_upload_threads(host.nbytes))),
+                                   ctypes.byref(cint(device)), ctypes.c_void_p(stream.cuda_stream), None,
+                                   ctypes.byref(ust))
             _lib.check(ust)
             t_up = time.perf_counter() - t0
         L.tp_pipeline_dev(ctypes.c_void_p(dm.data_ptr()), ctypes.byref(cint(n0)), ctypes.byref(cint(max_pcs)),
@@ -403,12 +405,11 @@ _UPLOAD_THREADS = int(os.environ.get("TP_UPLOAD_THREADS", "0"))
 
 def _upload_threads(nbytes: int) -> int:
     """Host threads for one tp_upload_dev copy (TP_UPLOAD_THREADS overrides):
-    one for small matrices (the genome driver runs several uploads at once),
-    more for large ones -- the largest chromosome's upload is on a genome
-    run's critical path."""
+    the library runs one upload at a time per device (FIFO), and four threads
+    of host copy keep up with the PCIe link (~52 of ~56 GB/s measured)."""
     if _UPLOAD_THREADS > 0:
         return _UPLOAD_THREADS
-    return 1 if nbytes < (64 << 20) else (4 if nbytes < (256 << 20) else 8)
+    return 1 if nbytes < (16 << 20) else 4
 
 
 def mask_dev(dm, bad_frac: float = 0.01, stream=None):

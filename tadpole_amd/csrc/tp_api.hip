@@ -1205,7 +1205,8 @@ void tp_pipeline(const double *M, const int *n0, const int *max_pcs, const int *
         Ctx &c = ctx_for(dev_of(device));
         const size_t bytes = (size_t)(*n0) * (*n0) * 8;
         double *dM = c.buf[S_M].as<double>((size_t)(*n0) * (*n0));
-        TP_HIP(hipMemcpyAsync(dM, M, bytes, hipMemcpyHostToDevice, c.cur));
+        // through the context's pinned ring, count blocks packed to 16 bits
+        upload_host(c, M, bytes, dM, bytes >= ((size_t)256 << 20) ? 8 : (bytes >= ((size_t)64 << 20) ? 4 : 1), true);
         pipeline_common(dM, n0, max_pcs, min_clusters, bad_frac, flags, c, k_cap, w_cap, bad, n_good, good_idx, k,
                         n_cluster, scores, w, n_pcs, n_clusters, merge, height, boundary, timings_ms);
     });
@@ -1600,51 +1601,29 @@ void tp_read_tsv(const char **path, const int *nrow, const int *ncol, const int 
 }
 
 // host -> device copy of a pageable buffer through this stream's context's
-// pinned staging: a ring of 3 x 16 MB slots, each block's memcpy into a slot
-// (nthreads host threads) overlapped with the previous blocks' DMAs.  A plain
-// pageable hipMemcpy goes through the runtime's one staging path, which the 8
-// streams of a genome run shared (C4: ~6 GB of matrices).
+// pinned staging (tp_upload.hip): a pageable hipMemcpy goes through the
+// runtime's one staging path, which the 8 streams of a genome run shared
 void tp_upload_dev(const void *host, const long long *bytes, void *d_dst, const int *nthreads, const int *device,
                    void *stream, int *status) {
     guarded(status, [&] {
         if (!host || !bytes || !d_dst || *bytes < 0) fail(TP_ERR_ARG, "null argument");
         Ctx &c = ctx_for(dev_of(device), (hipStream_t)stream);
-        const size_t total = (size_t)*bytes;
-        if (total == 0) return;
-        constexpr int kSlots = 3;
-        constexpr size_t kBlock = (size_t)16 << 20;
-        for (int q = 0; q < kSlots; ++q)
-            if (!c.ring_ev[q]) TP_HIP(hipEventCreateWithFlags(&c.ring_ev[q], hipEventDisableTiming));
-        const size_t nb = (total + kBlock - 1) / kBlock;
-        const size_t slot_bytes = std::min(total, kBlock);
-        char *ring = (char *)c.pinned(kSlots * slot_bytes);
-        const int th = std::max(1, std::min(nthreads && *nthreads > 0 ? *nthreads : 1, 16));
-        for (size_t b = 0; b < nb; ++b) {
-            const int slot = (int)(b % kSlots);
-            if (b >= (size_t)kSlots) {   // the slot's previous DMA (a 16 MB copy, < 1 ms)
-                hipError_t q;
-                while ((q = hipEventQuery(c.ring_ev[slot])) == hipErrorNotReady) std::this_thread::yield();
-                TP_HIP(q);
-            }
-            const size_t off = b * kBlock, len = std::min(kBlock, total - off);
-            char *dst = ring + (size_t)slot * slot_bytes;
-            const char *src = (const char *)host + off;
-            if (th == 1 || len < ((size_t)1 << 20)) {
-                memcpy(dst, src, len);
-            } else {
-                std::vector<std::thread> ts;
-                const size_t part = (len / th + 63) & ~(size_t)63;
-                for (int t = 0; t < th; ++t) {
-                    const size_t o = (size_t)t * part;
-                    if (o >= len) break;
-                    ts.emplace_back([=] { memcpy(dst + o, src + o, std::min(part, len - o)); });
-                }
-                for (auto &x : ts) x.join();
-            }
-            TP_HIP(hipMemcpyAsync((char *)d_dst + off, dst, len, hipMemcpyHostToDevice, c.cur));
-            TP_HIP(hipEventRecord(c.ring_ev[slot], c.cur));
-        }
-        stream_sync(c, c.cur);   // the staging is reused by the next call on this context
+        upload_host(c, host, (size_t)*bytes, d_dst, nthreads && *nthreads > 0 ? *nthreads : 1, false);
+    });
+}
+
+// the same for a float64 matrix of counts: blocks whose values are all exact
+// integers in [0, 65535] travel as 16-bit integers (widened on the device to
+// the same doubles), any other block as float64; *packed = bytes of float64
+// that travelled packed (may be NULL)
+void tp_upload_counts_dev(const double *host, const long long *count, double *d_dst, const int *nthreads,
+                          const int *device, void *stream, long long *packed, int *status) {
+    guarded(status, [&] {
+        if (!host || !count || !d_dst || *count < 0) fail(TP_ERR_ARG, "null argument");
+        Ctx &c = ctx_for(dev_of(device), (hipStream_t)stream);
+        const size_t pk = upload_host(c, host, (size_t)*count * sizeof(double), d_dst,
+                                      nthreads && *nthreads > 0 ? *nthreads : 1, true);
+        if (packed) *packed = (long long)pk;
     });
 }
 
@@ -1862,6 +1841,7 @@ void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
         case 39: p = &g_pd_cm; break;
         case 40: p = &g_sync_spin_us; break;
         case 42: p = &g_devbuf_async; break;
+        case 43: p = &g_upload_mode; break;
         default: fail(TP_ERR_ARG, "unknown knob");
         }
         if (*which == 3 && *value != 16 && *value != 32) fail(TP_ERR_ARG, "stage depth must be 16 or 32");

@@ -113,7 +113,7 @@ enum Slot {
     S_S, S_C, S_XC, S_XCT, S_G, S_Q, S_Z, S_W, S_SMALL, S_P, S_PT,
     S_SWEEP, S_SWEEP2, S_SCORES, S_PARTIAL, S_MISC, S_SHARD, S_SHARD2, S_DEDUP,
     S_KRY, S_KRYG, S_KRYT, S_KRYV, S_KRYX, S_CMEAN, S_CHBIG, S_CHOLP, S_SMALL2, S_GSTAT, S_XTXT, S_MEXT, S_KRYA,
-    S_KRYH, S_XNZ, S_PDIGA, S_PDIGB,
+    S_KRYH, S_XNZ, S_PDIGA, S_PDIGB, S_UPLD,
     S_NSLOT
 };
 static_assert(S_NSLOT <= (int)(sizeof(Ctx::buf) / sizeof(Ctx::buf[0])), "Ctx::buf too small for the slots");
@@ -367,6 +367,10 @@ bool prod_digits_means_ok(int K);
 extern int g_pd_cm;
 extern int g_sync_spin_us;
 extern int g_devbuf_async;
+// host -> device through the context's pinned ring (tp_upload.hip); counts:
+// blocks of exact 16-bit counts travel packed.  Returns the bytes sent packed.
+size_t upload_host(Ctx &c, const void *host, size_t bytes, void *d_dst, int nthreads, bool counts);
+extern int g_upload_mode;
 int prod_i8_partials(Ctx &c, const ProdDigits &pd, int r0, int M, const double *B, int ldb, int N, int K,
                      DevBuf &work, double **part);
 // pd (optional): A's digit image; the product then runs on the int8 MFMA

@@ -845,3 +845,61 @@ def test_prod_i8_rows_slab_same_bits(gpu, K, M, col0, r0, kernel):
     assert np.array_equal(part.view(np.uint64), full[r0:].view(np.uint64))
     ref = A.T @ B
     assert np.abs(full - ref).max() <= 1e-14 * (np.abs(A).T @ np.abs(B)).max()
+
+
+# ------------------------------------------------------------------- upload
+
+def test_upload_counts_bit_exact(gpu):
+    """tp_upload_counts_dev (tp_pipeline's host path, and the stream path of
+    TADpole() on a host matrix): 16 MB blocks of exact 16-bit counts travel
+    packed and are widened on the device; every other block (a fraction, NaN
+    with a payload, -0.0, 65536, a negative count) travels as float64 -- the
+    device copy equals the host matrix bit for bit either way; tp_upload_dev
+    copies raw bytes."""
+    import ctypes
+    import torch
+    blk = (16 << 20) // 8                       # values a block
+    n = 5 * blk + 12345                         # ragged last block
+    rng = np.random.default_rng(3)
+    h = rng.integers(0, 65536, n).astype(np.float64)
+    specials = {1: 0.5, 2: np.frombuffer(np.uint64(0x7FF8000000000123).tobytes(), np.float64)[0],
+                3: -0.0, 4: 65536.0}
+    for b, v in specials.items():
+        h[b * blk + 777] = v
+    h[5 * blk + 5] = -1.0                       # the ragged block
+    d = torch.empty(n, dtype=torch.float64, device="cuda:0")
+    packed = ctypes.c_longlong(0)
+    st = ctypes.c_int(0)
+    s = torch.cuda.Stream()
+    old = G.knob(43, 3)   # packed count blocks, uploads in turn (both paths of the switch)
+    try:
+        _upload_checks(gpu, h, d, n, blk, packed, st, s, rng)
+    finally:
+        G.knob(43, old)
+
+
+def _upload_checks(gpu, h, d, n, blk, packed, st, s, rng):
+    import ctypes
+    import torch
+    gpu.tp_upload_counts_dev(ctypes.c_void_p(h.ctypes.data), ctypes.byref(ctypes.c_longlong(n)),
+                             ctypes.c_void_p(d.data_ptr()), ctypes.byref(ctypes.c_int(4)), ctypes.byref(ctypes.c_int(0)),
+                             ctypes.c_void_p(s.cuda_stream), ctypes.byref(packed), ctypes.byref(st))
+    assert st.value == 0
+    out = d.cpu().numpy()
+    assert np.array_equal(out.view(np.uint64), h.view(np.uint64))
+    assert packed.value == 16 << 20             # only block 0 is all counts
+    # all counts: everything packed; raw copy of arbitrary bytes
+    h2 = rng.integers(0, 1000, 3 * blk).astype(np.float64)
+    d2 = torch.empty(3 * blk, dtype=torch.float64, device="cuda:0")
+    gpu.tp_upload_counts_dev(ctypes.c_void_p(h2.ctypes.data), ctypes.byref(ctypes.c_longlong(h2.size)),
+                             ctypes.c_void_p(d2.data_ptr()), ctypes.byref(ctypes.c_int(1)), ctypes.byref(ctypes.c_int(0)),
+                             ctypes.c_void_p(s.cuda_stream), ctypes.byref(packed), ctypes.byref(st))
+    assert st.value == 0 and packed.value == h2.nbytes
+    assert np.array_equal(d2.cpu().numpy(), h2)
+    raw = rng.standard_normal(blk + 3)
+    d3 = torch.empty(blk + 3, dtype=torch.float64, device="cuda:0")
+    gpu.tp_upload_dev(ctypes.c_void_p(raw.ctypes.data), ctypes.byref(ctypes.c_longlong(raw.nbytes)),
+                      ctypes.c_void_p(d3.data_ptr()), ctypes.byref(ctypes.c_int(2)), ctypes.byref(ctypes.c_int(0)),
+                      ctypes.c_void_p(s.cuda_stream), ctypes.byref(st))
+    assert st.value == 0
+    assert np.array_equal(d3.cpu().numpy().view(np.uint64), raw.view(np.uint64))
