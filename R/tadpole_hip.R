@@ -106,8 +106,17 @@ read_matrix_hip <- function(mat_file, nthreads = 0L) {
 
 # TADpole() (R/TADpole.R:344-501) on the GPU.  `mat_file`: a path (native
 # reader) or an in-memory matrix.  Plots of load_mat are not drawn.
+# Limit: min(max_pcs, number of good bins) <= 1024 -- the sweep's kernels hold
+# at most 1024 PC columns per tree (16 column slots of 64) and the PCA's own
+# eigensolver blocks up to 1280; R itself has no cap (R/TADpole.R:344,452).
+# Larger values stop with the library's TP_ERR_UNSUPPORTED message.
 TADpole_hip <- function(mat_file, max_pcs = 200, min_clusters = 2, bad_frac = 0.01,
                         chr, start, end, resol, centromere_search = FALSE, device = 0L) {
+  if (max_pcs > 1024) {
+    nb <- if (is.character(mat_file)) NA else nrow(as.matrix(mat_file))
+    if (is.na(nb) || nb > 1024)
+      warning("max_pcs > 1024: supported only while the matrix keeps <= 1024 good bins (sweep limit)")
+  }
   mat <- if (is.character(mat_file)) read_matrix_hip(mat_file) else as.matrix(mat_file)
   if (!centromere_search) {
     r <- .tp_pipeline(mat, max_pcs, min_clusters, bad_frac, 0L, device)

@@ -794,6 +794,12 @@ def main():
                "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
                "higher_is_better": True, "scaling": "strong" if args.sharded else "weak", "vs_baseline": None,
                "dtype": "f64",
+               # what "f64" covers: every result is fp64; two products run on integer matrix cores
+               # without changing that (exact, or within fp64 rounding of the fp64 product)
+               "dtype_detail": ("f64 results; X'X of integer counts exact on the int8 MFMA (7-bit slices, "
+                                "int32 accumulation, one rounding); the G-space Krylov products with C on the "
+                                "int8 MFMA from base-256 digit images (6 digits of C, 7 of each block, 27 digit "
+                                "pairs, within ~1e-15 of sum |A||B|); everything else fp64 VALU / MFMA"),
                "data": "synthetic (SURVEY.md §8(d) Hi-C generator, seed 20261015+%d" % cfg +
                        ("" if args.sharded else "+1000*rank") + ")",
                "ranks_seen": len(seen), "devices_seen": sorted({d for _, d in seen}),
