@@ -8,8 +8,8 @@
 //
 // Tile: 64x64 per workgroup, BK = 16, 256 threads = 4 waves in a 2x2 grid, each
 // wave 32x32 = 2x2 MFMA tiles.  Operands are staged k-contiguous in LDS
-// ([row][BK+2]: the +2 pad makes the 16-row x 2-k fragment read of ds_read_b64
-// conflict-free), next tile prefetched into registers during the MFMAs.
+// ([row][BK+1]: GPAD below), next tile prefetched into registers during the
+// MFMAs.
 // fp64 MFMA layout (cdna_hip_programming.md §3): A lane l = A[l&15][k=l>>4],
 // B lane l = B[k=l>>4][l&15], D lane l reg r = D[(l>>4) + 4r][l&15].
 #include "tp_common.cuh"
@@ -22,9 +22,20 @@ namespace tp {
 typedef double d4 __attribute__((ext_vector_type(4)));
 
 constexpr int BM = 64, BN = 64, BK = 16;
+// LDS row pad (doubles) of every operand tile here.  The fragment reads fuse
+// into ds_read2_b64 (two k steps a read), which serves 16 contiguous lanes a
+// cycle on banks (a/4) mod 32: rows fr = 0..15 of a 2-word span must land on
+// distinct banks, i.e. a row stride of 2 mod 4 words.  A +2 pad (18 or 34
+// doubles = 36 / 68 words) put two rows on each bank pair (rocprof: 40-45 % of
+// the LDS cycles of k_gemm_f64 / _panel were conflict cycles); +1 (17 / 33
+// doubles) is conflict-free for those reads and for the i-contiguous A stores.
+#ifndef TP_GEMM_PAD
+#define TP_GEMM_PAD 1
+#endif
+constexpr int GPAD = TP_GEMM_PAD;
 
 // KB = k depth of one LDS stage (16 or 32): per thread KB/4 elements of each
-// operand; rows stored k-contiguous with a +2 pad (conflict-free fragment reads)
+// operand; rows stored k-contiguous with a GPAD pad (conflict-free fragment reads)
 template <bool TA, int KB>
 __device__ __forceinline__ void load_a(double (&ra)[KB / 4], const double *A, int lda, int M, int K, int i0, int k0) {
     const int t = threadIdx.x;
@@ -39,7 +50,7 @@ __device__ __forceinline__ void load_a(double (&ra)[KB / 4], const double *A, in
     }
 }
 template <bool TA, int KB>
-__device__ __forceinline__ void store_a(double (*As)[KB + 2], const double (&ra)[KB / 4]) {
+__device__ __forceinline__ void store_a(double (*As)[KB + GPAD], const double (&ra)[KB / 4]) {
     const int t = threadIdx.x;
 #pragma unroll
     for (int p = 0; p < KB / 4; ++p) {
@@ -62,7 +73,7 @@ __device__ __forceinline__ void load_b(double (&rb)[KB / 4], const double *B, in
     }
 }
 template <int KB>
-__device__ __forceinline__ void store_b(double (*Bs)[KB + 2], const double (&rb)[KB / 4]) {
+__device__ __forceinline__ void store_b(double (*Bs)[KB + GPAD], const double (&rb)[KB / 4]) {
     const int t = threadIdx.x;
 #pragma unroll
     for (int p = 0; p < KB / 4; ++p) {
@@ -79,8 +90,8 @@ __global__ void __launch_bounds__(256) k_gemm_f64(int M, int N, int K, const dou
                                                   int ldc, int store_t, int sym, int tcol0, int kchunk,
                                                   size_t part_stride, int g_xcd_order,
                                                   const double *C0 = nullptr) {   // C0 may alias C (no restrict)
-    __shared__ double As[2][BM][KB + 2];
-    __shared__ double Bs[2][BN][KB + 2];
+    __shared__ double As[2][BM][KB + GPAD];
+    __shared__ double Bs[2][BN][KB + GPAD];
     // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs (each
     // with its own L2), so the logical tile index Lg makes consecutive
     // workgroups of one XCD neighbours -- the tiles of one A row panel (all
@@ -187,7 +198,7 @@ int g_gemm_kb = 16;   // k depth of the 64 x 64 kernel's LDS stages (16 / 32; sa
 // 64 x 64 kernel and 4x the MFMAs per LDS fragment read.  Every output element
 // sees the same k order (blocks of 16, steps of 4) as k_gemm_f64, so the two
 // kernels give identical bits and can be mixed freely (also across shards).
-constexpr int GB = 128, GBK = 16, GLD = GBK + 2;
+constexpr int GB = 128, GBK = 16, GLD = GBK + GPAD;
 template <bool TA>
 __global__ void __launch_bounds__(256, 2) k_gemm_f64_big(int M, int N, int K, const double *__restrict__ A, int lda,
                                                          const double *__restrict__ B, int ldb,
@@ -298,7 +309,7 @@ __global__ void __launch_bounds__(256, 2) k_gemm_f64_big(int M, int N, int K, co
 // k order of every output element is that of k_gemm_f64 (steps of 4 within
 // blocks of 16; a 32-block is two 16-blocks back to back), so all three
 // kernels give identical bits.
-constexpr int PM = 32, PN = 64, PK = 32, PLD = PK + 2, PSETS = 3;
+constexpr int PM = 32, PN = 64, PK = 32, PLD = PK + GPAD, PSETS = 3;
 // Global loads run PSETS - 1 stages ahead of the MFMAs (register sets rotate):
 // a stage is only ~1k MFMA cycles a wave, less than an HBM/MALL round trip.
 template <bool TA>
@@ -408,7 +419,7 @@ int g_gemm_panel = 1;   // 0: tall-skinny products take the split-K 64 x 64 path
 // same chunking the bits are those of the 64 x 64 kernel.
 // TN = 32 (the C-Krylov blocks): a 128 x 32 tile, each wave 32 x 32 (2 x 2
 // accumulators); same k order, so the bits of a column do not depend on TN.
-constexpr int TSM = 128, TSN = 64, TSK = 16, TSLD = TSK + 2;
+constexpr int TSM = 128, TSN = 64, TSK = 16, TSLD = TSK + GPAD;
 template <int TAG, int TN = TSN, bool PF2 = false>
 __global__ void __launch_bounds__(256, 2) k_gemm_ts(int M, int N, int K, const double *__restrict__ A, int lda,
                                                     const double *__restrict__ B, int ldb, double *__restrict__ C,

@@ -366,15 +366,34 @@ __global__ void __launch_bounds__(256) k_pd_digits_sl(const double *__restrict__
 // seven accumulators each): 64 rows x 64 columns a workgroup; blockIdx ->
 // (row tile, k chunk) dealt XCD-contiguously.  Each 64-byte k step of both
 // images (PD_ADIG x 4 KB of A, 7 x 4 KB of B, each a contiguous run) is
-// staged through registers into LDS (80-byte rows: the 16-lane b128 fragment
-// reads spread over the banks).
-// NB = 1 (the default): one LDS buffer of 62 KB (PD_BUF), the next step's
+// staged through registers into LDS (96-byte rows: conflict-free b128 fragment
+// reads and staging writes, PD_LD).
+// NB = 1 (the default): one LDS buffer of 78 KB (PD_BUF), the next step's
 // loads in registers while this step's MFMAs run, two barriers a step, two
 // workgroups a CU (each one's MFMAs run under the other's waits).
-// NB = 2 (knob 36 = 2): two LDS buffers (124 KB, one workgroup a CU), two k
+// NB = 2 (knob 36 = 2): two LDS buffers (156 KB, one workgroup a CU), two k
 // steps of loads in flight in two register sets, one barrier a step.
-constexpr int PD_LD = 80;                        // LDS row stride (bytes)
+// LDS row stride (bytes).  The 16-lane groups of ds_read_b128 ({0-3,12-15,
+// 20-27}, ...: banks (a/4) mod 64) read fragment rows l & 15 at byte 16 (l >> 4):
+// with 96-byte rows the 16 lanes of every group land on 16 distinct 4-bank
+// blocks ((6 m + q) mod 16 all distinct); the 80-byte rows of round 4 put two
+// lanes on each busy block (rocprof: SQ_LDS_BANK_CONFLICT = 50 % of the LDS
+// cycles of k_pd_prod<1>).  Two 78 KB buffers still fit one CU (two
+// workgroups of NB = 1, one of NB = 2).
+#ifndef TP_PD_LD
+#define TP_PD_LD 96
+#endif
+constexpr int PD_LD = TP_PD_LD;
 constexpr int PD_ASZ = PD_ADIG * 64 * PD_LD, PD_BUF = PD_ASZ + PD_DIG * 64 * PD_LD;
+static_assert(2 * PD_BUF <= 160 * 1024, "two k_pd_prod buffers must fit the CU's LDS");
+// Staging: thread t moves one 16-byte piece of every 4 KB digit block -- row
+// pd_srow(t), k quarter t % 4.  The 8-lane groups of ds_write_b128 (banks
+// (a/4) mod 32) then hold rows r and r + 2 ((6 r + j) mod 8 distinct at 96-byte
+// rows); a wave's global load is still one contiguous 1 KB (rows 16 w ..
+// 16 w + 15, permuted within it).
+__device__ __forceinline__ int pd_srow(int t) {
+    return PD_LD == 96 ? 4 * (t >> 4) + ((t >> 3) & 1) + 2 * ((t >> 2) & 1) : t >> 2;
+}
 template <int NB>
 __global__ void __launch_bounds__(256, 3 - NB) k_pd_prod(const int8_t *__restrict__ Da, int Kp, int M,
                                                     const int8_t *__restrict__ Db, const double *__restrict__ rs,
@@ -399,11 +418,11 @@ __global__ void __launch_bounds__(256, 3 - NB) k_pd_prod(const int8_t *__restric
         for (int a = 0; a < 2; ++a)
 #pragma unroll
             for (int b = 0; b < 2; ++b) acc[u][a][b] = pd_i32x4{0, 0, 0, 0};
-    // staging: thread t moves bytes 16 t .. 16 t + 15 of every 4 KB digit block
-    // (row t / 4, k quarter t % 4) of the step
-    const int sr = t >> 2, sk = (t & 3) * 16;
-    const int8_t *ga = Da + (size_t)bm * nsteps * (PD_ADIG * PD_BLK) + 16 * t;
-    const int8_t *gb = Db + 16 * t;
+    // staging: thread t moves row sr, k quarter t % 4 of every 4 KB digit block
+    // of the step (pd_srow)
+    const int sr = pd_srow(t), sk = (t & 3) * 16;
+    const int8_t *ga = Da + (size_t)bm * nsteps * (PD_ADIG * PD_BLK) + 64 * sr + sk;
+    const int8_t *gb = Db + 64 * sr + sk;
     const int T = (kend - kbeg) / 64, st0 = kbeg / 64;
     pd_i32x4 ra[PD_DIG], rb[PD_DIG], xa[PD_DIG], xb[PD_DIG];
     // loads past the chunk re-read its last step (clamped, unconditional: the
@@ -531,11 +550,11 @@ __global__ void __launch_bounds__(512, 1) k_pd_prod128(const int8_t *__restrict_
 #pragma unroll
             for (int b = 0; b < 2; ++b) acc[u][a][b] = pd_i32x4{0, 0, 0, 0};
     const int h = t >> 8, tt = t & 255;
-    const int sr = tt >> 2, sk = (tt & 3) * 16;
+    const int sr = pd_srow(tt), sk = (tt & 3) * 16;
     // a second row tile past the image (odd tile count) re-reads the last one:
     // its rows are past M and never stored
-    const int8_t *ga = Da + (size_t)min(2 * bm + h, tm64 - 1) * nsteps * (PD_ADIG * PD_BLK) + 16 * tt;
-    const int8_t *gb = Db + 16 * tt;
+    const int8_t *ga = Da + (size_t)min(2 * bm + h, tm64 - 1) * nsteps * (PD_ADIG * PD_BLK) + 64 * sr + sk;
+    const int8_t *gb = Db + 64 * sr + sk;
     const int T = (kend - kbeg) / 64, st0 = kbeg / 64;
     pd_i32x4 ra[PD_ADIG], rb[PD_DIG];
     auto gload = [&](int st) {
