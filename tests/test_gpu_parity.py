@@ -819,7 +819,8 @@ def test_prod_i8_rows_slab_same_bits(gpu, K, M, col0, r0, kernel):
     the bits of the same rows of the whole product; K > 8192 takes the
     two-pass digitizers of the block (k_pd_colmax + k_pd_digits_sl) and of
     A (k_pd_digits).  kernel: the product kernel (knob 36: 1 = k_pd_prod,
-    3 = k_pd_dma, 4 = k_pd_prod128), which must agree bit for bit."""
+    3 = k_pd_dma, 4 = k_pd_prod128), which must agree bit for bit with each
+    other."""
     import ctypes
     rng = np.random.default_rng(K + M + col0)
     A = np.asfortranarray(rng.uniform(-1, 1, size=(K, M)))
@@ -836,12 +837,15 @@ def test_prod_i8_rows_slab_same_bits(gpu, K, M, col0, r0, kernel):
         assert st.value == 0
         return O
 
-    old = G.knob(36, kernel)
+    old = G.knob(36, 1)
     try:
+        base = rows(0, 0, M)
+        G.knob(36, kernel)
         full = rows(0, 0, M)
         part = rows(col0, r0, M - r0)
     finally:
         G.knob(36, old)
+    assert np.array_equal(full.view(np.uint64), base.view(np.uint64))
     assert np.array_equal(part.view(np.uint64), full[r0:].view(np.uint64))
     ref = A.T @ B
     assert np.abs(full - ref).max() <= 1e-14 * (np.abs(A).T @ np.abs(B)).max()
