@@ -1842,6 +1842,7 @@ void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
         case 40: p = &g_sync_spin_us; break;
         case 42: p = &g_devbuf_async; break;
         case 43: p = &g_upload_mode; break;
+        case 44: p = &g_xtx_w; break;
         default: fail(TP_ERR_ARG, "unknown knob");
         }
         if (*which == 3 && *value != 16 && *value != 32) fail(TP_ERR_ARG, "stage depth must be 16 or 32");

@@ -402,6 +402,10 @@ __device__ __forceinline__ void wait_vm_dyn(int n) {
         default: wait_vm<16>(); break;
     }
 }
+// lgkmcnt(0) as an instruction the compiler's wait insertion sees (an asm
+// wait is opaque to it: it then re-waits, lgkmcnt(0) after the next step's
+// fragment reads are issued, before the MFMAs on the current ones)
+__device__ __forceinline__ void wait_lgkm0() { __builtin_amdgcn_s_waitcnt(0xC07F); }
 // wait until at most `later` (<= MAXL) stages of CPW DMAs each are outstanding
 template <int CPW, int MAXL>
 __device__ __forceinline__ void wait_stages(int later) {
@@ -638,6 +642,283 @@ __global__ void __launch_bounds__(512) k_xtx_i8_glds(const int8_t *__restrict__ 
             }
 }
 
+// k_xtx_i8_w: the whole upper triangle in 256 x 128 tiles -- rows 256 P ..,
+// columns 128 Q .., every (P, Q) with 2 P <= Q -- by 8 waves of 64 x 64 (4 x 4
+// MFMA tiles each; waves 4 x 2).  Why: the 128-tiles are bound by the per-CU
+// LDS-DMA fill rate (~25 GB/s a CU: k_xtx_i8_glds's DMA-only build takes 17.8 of
+// its 23.6 ms at 24 300 bins, a one-slice ring of twice the depth no less), and
+// a 256 x 128 tile stages 24 KiB a 64-deep k step for twice the MACs (12 KiB
+// per 128 x 128 instead of 16).  Its compute side is also leaner: the main
+// loop stages slice 0 only (a 6-stage ring, 4 stages in flight, one constant
+// counted wait a step where the 128-tiles chose among 17 by the high slice's
+// map), and reads step k + 1's fragments while step k's 16 MFMAs run.
+//
+// The high slice (counts >= 128: a band around the diagonal for raw Hi-C) goes
+// in a second phase over the k-blocks where either panel's X1 is nonzero
+// (k_slice_nz's map; every block when the map is off): A0 A1 B0 B1 of each such
+// block are staged (3-slot ring of 48 KiB) and t01 += A1'B0 + A0'B1,
+// t11 += A1'B1 in int32 -- the products k_xtx_i8_glds takes inline, exact in
+// separate accumulators (|t01| <= 2 * 64 * 127^2 a block: nk <= 1040), so
+// S = acc + 2^7 t01 + 2^14 t11 is the same integer and the same double.
+// The epilogue is k_xtx_i8_glds's (COR: the sparse_cor epilogue in the store).
+constexpr int XW_ST = 6;                 // main-loop ring stages
+constexpr int XW_STAGE = 24 * 1024;      // A0 (256 columns) + B0 (128 columns) x 64 k bytes
+constexpr int XW_HSTAGE = 48 * 1024;     // phase 2: A0 A1 B0 B1
+constexpr int XW_LIST = XW_ST * XW_STAGE;   // hi-block list (u16) + its count, after the ring
+constexpr int XW_LDS = XW_LIST + 4096;
+static_assert(3 * XW_HSTAGE <= XW_LIST && XW_LDS <= 160 * 1024, "k_xtx_i8_w LDS");
+constexpr int XW_MAXNK = 1040;           // k blocks: t01 stays below 2^31
+
+// tile L of the order below -> (P, Q).  Column panels in chunks of 8, row
+// panels in chunks of 4 inside: a chunk pair is 32 tiles sharing 12 panels --
+// one XCD's 32 CUs at a time (workgroups are dealt to XCDs round-robin and
+// each XCD takes a contiguous run of L).  A full column chunk qc holds
+// 32 qc + 20 tiles: qc full row chunks of 4 x 8, then the diagonal one.
+__device__ __forceinline__ void xtx_w_tile(int L, int tnc, int &P, int &Q) {
+    int qc = 0;
+    while (true) {
+        const int q0 = 8 * qc, wq = min(8, tnc - q0);
+        int cnt = 0;
+        if (wq == 8) cnt = 32 * qc + 20;
+        else
+            for (int q = q0; q < q0 + wq; ++q) cnt += q / 2 + 1;
+        if (L < cnt) {
+            if (L < 4 * wq * qc) {   // a full row chunk: Q-major inside
+                const int pc = L / (4 * wq), r = L % (4 * wq);
+                Q = q0 + r / 4;
+                P = 4 * pc + (r & 3);
+                return;
+            }
+            L -= 4 * wq * qc;
+            for (int q = q0; q < q0 + wq; ++q)
+                for (int p = 4 * qc; p <= q / 2; ++p)
+                    if (L-- == 0) {
+                        P = p;
+                        Q = q;
+                        return;
+                    }
+        }
+        L -= cnt;
+        ++qc;
+        if (q0 + 8 >= tnc) break;   // not reached for L < the tile count
+    }
+    P = Q = 0;
+}
+static long xtx_w_tiles(int tnc) {
+    long t = 0;
+    for (int q = 0; q < tnc; ++q) t += q / 2 + 1;
+    return t;
+}
+
+template <int NS, bool COR>
+__global__ void __launch_bounds__(512) k_xtx_i8_w(const int8_t *__restrict__ S, int n, int Kp, int Np,
+                                                  double *__restrict__ C, int ntiles,
+                                                  const double *__restrict__ cm, const double *__restrict__ csd,
+                                                  const unsigned *__restrict__ nzw, int NW) {
+    static_assert(NS == 1 || NS == 2, "1 or 2 slices");
+    __shared__ __attribute__((aligned(16))) int8_t L[XW_LDS];
+    const int tnc = Np / 128;
+    int P, Q;
+    {
+        const int xcd = (int)blockIdx.x & 7, slot = (int)blockIdx.x >> 3;
+        xtx_w_tile(xcd * (ntiles >> 3) + min(xcd, ntiles & 7) + slot, tnc, P, Q);
+    }
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int wr = w & 3, wc = w >> 2;
+    const size_t slice = (size_t)Np * Kp;
+    const int ia = 256 * P, jb = 128 * Q;
+    // DMA sources (k_xtx_i8_glds's swizzle): lane p of a 1 KiB chunk loads
+    // column p >> 2, k bytes 16 ((p & 3) ^ ((p >> 4) & 2)) .. + 15.  Chunks of
+    // wave w: A columns 16 w .. (slot w), A 128 + 16 w .. (slot 8 + w), B 16 w ..
+    // (slot 16 + w).  A's second half may lie past the padded columns (last row
+    // panel): it then reads the first half (its rows are >= n, never stored).
+    const int pc = lane >> 2, pk = (lane & 3) ^ ((lane >> 4) & 2);
+    const int8_t *vA0 = S + (size_t)(ia + 16 * w + pc) * Kp + 16 * pk;
+    const int8_t *vA1 = ia + 128 < Np ? vA0 + (size_t)128 * Kp : vA0;
+    const int8_t *vB = S + (size_t)(jb + 16 * w + pc) * Kp + 16 * pk;
+    TP_DASSERT(ia + 16 * w + pc < Np && jb + 16 * w + pc < Np);
+    const int nk = Kp / 64;
+    auto issue = [&](int k) {
+        int8_t *dst = L + (k % XW_ST) * XW_STAGE + w * 1024;
+        const size_t o = (size_t)64 * k;
+        glds16(vA0 + o, dst);
+        glds16(vA1 + o, dst + 8 * 1024);
+        glds16(vB + o, dst + 16 * 1024);
+    };
+    i32x4 acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = i32x4{0, 0, 0, 0};
+    const int fr = lane & 15, kc = lane >> 4;
+    const int roff = (4 * fr + (kc ^ ((fr >> 2) & 2))) * 16;
+    struct Frag {
+        i32x4 a[4], b[4];
+    };
+    auto read_frags = [&](Frag &f, int k) {
+        const int8_t *Lb = L + (k % XW_ST) * XW_STAGE + roff;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) f.a[i] = *(const i32x4 *)(Lb + (4 * wr + i) * 1024);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) f.b[i] = *(const i32x4 *)(Lb + (16 + 4 * wc + i) * 1024);
+    };
+    auto prod = [&](i32x4 (&ac)[4][4], const i32x4 (&fa)[4], const i32x4 (&fb)[4]) {
+#ifdef TP_XG_DIAG_NOMFMA   // diagnostic builds only (timing of the load side alone; wrong results)
+        return;
+#endif
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) ac[a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[a], fb[b], ac[a][b], 0, 0, 0);
+    };
+#pragma unroll
+    for (int k = 0; k < XW_ST - 1; ++k)
+        if (k < nk) issue(k);
+    // step k: stage k + 1 has landed everywhere (this wave's DMAs by the
+    // counted wait -- stages k + 2 .. k + XW_ST - 2 may stay in flight -- the
+    // others' by the barrier); stage k - 1's slot, read at step k - 2, takes
+    // stage k + XW_ST - 1
+    auto sync_issue = [&](int k) {
+        wait_stages<3, XW_ST - 3>(nk - 2 - k);
+        wait_lgkm0();
+        __builtin_amdgcn_s_barrier();
+#ifdef TP_XG_DIAG_NODMA   // diagnostic builds only (timing of the MFMA side alone; wrong results)
+        if (k + XW_ST - 1 < XW_ST)
+#endif
+        if (k + XW_ST - 1 < nk) issue(k + XW_ST - 1);
+    };
+    wait_stages<3, XW_ST - 2>(nk - 1);
+    __builtin_amdgcn_s_barrier();
+    {
+        Frag f0, f1;
+        read_frags(f0, 0);
+        auto step = [&](int k, Frag &cur, Frag &nxt) {
+            sync_issue(k);
+            if (k + 1 < nk) read_frags(nxt, k + 1);
+            prod(acc, cur.a, cur.b);
+        };
+        int k = 0;
+        for (; k + 1 < nk; k += 2) {
+            step(k, f0, f1);
+            step(k + 1, f1, f0);
+        }
+        if (k < nk) step(k, f0, f1);
+    }
+    // every DMA landed (the last steps waited vmcnt(0)); all reads done
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    i32x4 t01[4][4], t11[4][4];
+    if constexpr (NS == 2) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) t01[a][b] = t11[a][b] = i32x4{0, 0, 0, 0};
+        // the k-blocks where A's (two 128-column panels) or B's X1 is nonzero,
+        // ascending, into LDS by wave 0 (lane j: word j of the maps)
+        unsigned short *hl = (unsigned short *)(L + XW_LIST);
+        int *hcount = (int *)(L + XW_LIST + 4096 - 16);
+        int nh = nk;
+        if (nzw != nullptr) {
+            if (w == 0) {
+                unsigned u = 0;
+                if (lane < NW) {
+                    u = nzw[(size_t)(2 * P) * NW + lane] | nzw[(size_t)Q * NW + lane];
+                    if (2 * P + 1 < tnc) u |= nzw[(size_t)(2 * P + 1) * NW + lane];
+                }
+                const int cnt = __popc(u);
+                int incl = cnt;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int y = __shfl_up(incl, o, 64);
+                    if (lane >= o) incl += y;
+                }
+                int pos = incl - cnt;
+                while (u) {
+                    hl[pos++] = (unsigned short)(32 * lane + __ffs(u) - 1);
+                    u &= u - 1;
+                }
+                if (lane == 63) *hcount = incl;
+            }
+            wait_lgkm0();
+            __builtin_amdgcn_s_barrier();
+            nh = __builtin_amdgcn_readfirstlane(*hcount);
+        }
+        auto blk = [&](int h) -> int {
+            return nzw != nullptr ? __builtin_amdgcn_readfirstlane((int)hl[h]) : h;
+        };
+        // stage h: wave w's chunks A0 (slots w, 8 + w), A1 (16 + w, 24 + w),
+        // B0 (32 + w), B1 (40 + w)
+        auto issue2 = [&](int h) {
+            int8_t *dst = L + (h % 3) * XW_HSTAGE + w * 1024;
+            const size_t o = (size_t)64 * blk(h);
+            glds16(vA0 + o, dst);
+            glds16(vA1 + o, dst + 8 * 1024);
+            glds16(vA0 + slice + o, dst + 16 * 1024);
+            glds16(vA1 + slice + o, dst + 24 * 1024);
+            glds16(vB + o, dst + 32 * 1024);
+            glds16(vB + slice + o, dst + 40 * 1024);
+        };
+        if (nh > 0) issue2(0);
+        if (nh > 1) issue2(1);
+        for (int h = 0; h < nh; ++h) {
+            if (h + 1 < nh) wait_vm<6>();
+            else wait_vm<0>();
+            wait_lgkm0();
+            __builtin_amdgcn_s_barrier();
+            if (h + 2 < nh) issue2(h + 2);   // the slot of stage h - 1, read before this barrier
+            const int8_t *Lb = L + (h % 3) * XW_HSTAGE + roff;
+            i32x4 fa[4], fb[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) fa[i] = *(const i32x4 *)(Lb + (16 + 4 * wr + i) * 1024);   // A1
+#pragma unroll
+            for (int i = 0; i < 4; ++i) fb[i] = *(const i32x4 *)(Lb + (32 + 4 * wc + i) * 1024);   // B0
+            prod(t01, fa, fb);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) fb[i] = *(const i32x4 *)(Lb + (40 + 4 * wc + i) * 1024);   // B1
+            prod(t11, fa, fb);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) fa[i] = *(const i32x4 *)(Lb + (4 * wr + i) * 1024);   // A0
+            prod(t01, fa, fb);
+        }
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+    }
+    double *pm = (double *)L;   // [0,256) m rows, [256,384) m cols, [384,640) sd rows, [640,768) sd cols
+    if constexpr (COR) {
+        if (t < 256) {
+            const int i = min(ia + t, n - 1);
+            pm[t] = cm[i];
+            pm[384 + t] = csd[i];
+        } else if (t < 384) {
+            const int j = min(jb + t - 256, n - 1);
+            pm[t] = cm[j];
+            pm[384 + t] = csd[j];
+        }
+        __syncthreads();
+    }
+    const double fn = (double)n, fn1 = (double)(n - 1);
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int il = 64 * wr + 16 * a + 4 * kc + r, jl = 64 * wc + 16 * b + fr;
+                const int i = ia + il, j = jb + jl;
+                if (i >= n || j >= n || i > j) continue;
+                long long v = (long long)acc[a][b][r];
+                if constexpr (NS == 2) v += ((long long)t01[a][b][r] << 7) + ((long long)t11[a][b][r] << 14);
+                double d = (double)v;
+                if constexpr (COR) {
+                    const double cij = (d - fn * (pm[il] * pm[256 + jl])) / fn1;
+                    d = cij / (pm[384 + il] * pm[640 + jl]);
+                    if (isnan(d)) d = 0.0;
+                }
+                C[(size_t)i + (size_t)j * n] = d;
+                C[(size_t)j + (size_t)i * n] = d;
+            }
+}
+
 // the gather's per-column maxima / flags -> the k_int_scan result format
 __global__ void __launch_bounds__(256) k_colflags(const double *cmax, const int *cbad, int n,
                                                   unsigned long long *maxbits, int *notint) {
@@ -786,9 +1067,40 @@ static void launch_xtx128(Ctx &c, int ns, unsigned nb, const int8_t *sl, int n, 
     else fail(TP_ERR_ARG, "xtx_int8 (128-tiles): 1..2 slices");
 }
 
+int g_xtx_w = 1;   // knob 44: the whole upper triangle by k_xtx_i8_w (256 x 128 tiles; 0: 128-tiles)
+
+template <int NS, bool COR>
+static void launch_xtx_w_t(Ctx &c, const int8_t *sl, int n, int Kp, int Np, double *d_S, const double *cm,
+                           const double *csd) {
+    const long nt = xtx_w_tiles(Np / 128);
+    unsigned *nzw = nullptr;
+    const int NW = (Kp / 64 + 31) / 32;
+    if (NS == 2 && g_xtx_nz) {
+        nzw = c.buf[S_XNZ].as<unsigned>((size_t)(Np / 128) * NW);
+        hipLaunchKernelGGL(k_slice_nz, dim3((unsigned)(Np / 128), (unsigned)NW), dim3(256), 0, c.cur,
+                           sl + (size_t)Np * Kp, Kp, NW, nzw);
+    }
+    hipLaunchKernelGGL((k_xtx_i8_w<NS, COR>), dim3((unsigned)nt), dim3(512), 0, c.cur, sl, n, Kp, Np, d_S, (int)nt,
+                       cm, csd, nzw, NW);
+}
+// the whole upper triangle by k_xtx_i8_w when it applies
+static bool launch_xtx_w(Ctx &c, int ns, const int8_t *sl, int n, int Kp, int Np, double *d_S, const double *cm,
+                         const double *csd) {
+    if (!g_xtx_w || !g_xtx_glds || !g_xtx_supertile || (ns != 1 && ns != 2)) return false;
+    if (ns == 2 && Kp / 64 > XW_MAXNK) return false;   // t01's int32 bound
+    const bool cor = cm != nullptr;
+    if (ns == 1 && !cor) launch_xtx_w_t<1, false>(c, sl, n, Kp, Np, d_S, cm, csd);
+    else if (ns == 2 && !cor) launch_xtx_w_t<2, false>(c, sl, n, Kp, Np, d_S, cm, csd);
+    else if (ns == 1) launch_xtx_w_t<1, true>(c, sl, n, Kp, Np, d_S, cm, csd);
+    else launch_xtx_w_t<2, true>(c, sl, n, Kp, Np, d_S, cm, csd);
+    TP_HIP(hipGetLastError());
+    return true;
+}
+
 // S (n x n) = X'X exactly on the upper tiles of tile columns [tc0, tc1) and
 // their mirrors, from ns slices.
 // 128-column tiles [tc0, tc1) (tile units of 128) by the LDS-staged kernel
+// (the whole triangle by k_xtx_i8_w's 256 x 128 tiles: same products, same bits)
 void xtx_int8_tiles128(Ctx &c, const int8_t *sl, int n, int ns, double *d_S, int tc0, int tc1, const double *cm,
                        const double *csd) {
     const int Kp = xtx_kp(n), Np = (n + 127) / 128 * 128;
@@ -796,6 +1108,7 @@ void xtx_int8_tiles128(Ctx &c, const int8_t *sl, int n, int ns, double *d_S, int
     tc0 = std::max(0, tc0);
     tc1 = tc1 < 0 ? tn : std::min(tn, tc1);
     if (tc1 <= tc0) return;
+    if (tc0 == 0 && tc1 == tn && launch_xtx_w(c, ns, sl, n, Kp, Np, d_S, cm, csd)) return;
     const unsigned nb = (unsigned)((long)tc1 * (tc1 + 1) / 2 - (long)tc0 * (tc0 + 1) / 2);
     const int tn_all = (tc0 == 0 && tc1 == tn && g_xtx_supertile) ? tn : 0;
     launch_xtx128(c, ns, nb, sl, n, Kp, Np, d_S, tc0, tn_all, cm, csd, nullptr, 0, 0x7fffffff);

@@ -239,6 +239,28 @@ def test_cor_in_xtx_store_same_bits(gpu, case):
     assert np.array_equal(a.dendro.height.view(np.uint64), b.dendro.height.view(np.uint64))
 
 
+@pytest.mark.parametrize("n", [2100, 4500])
+def test_cor_wide_tiles_same_bits(gpu, n):
+    """The correlation in k_xtx_i8_w's 256 x 128 tile store (knob 44, default)
+    against the 128-tile kernel: the same exact X'X and epilogue, so the same
+    pipeline bits (ragged n with an odd tile-column count; 4500 bins: the
+    block Krylov path)."""
+    import tadpole_amd as tp
+    m = synth_hic(n, SEED_BASE + 82)
+    runs = []
+    for wide in (1, 0):
+        old = G.knob(44, wide)
+        try:
+            runs.append(tp.TADpole(m, max_pcs=150))
+        finally:
+            G.knob(44, old)
+    a, b = runs
+    assert (a.n_pcs, a.optimal_n_clusters) == (b.n_pcs, b.optimal_n_clusters)
+    assert np.array_equal(np.asarray(a.scores).view(np.uint64), np.asarray(b.scores).view(np.uint64))
+    for q in a.clusters:
+        assert np.array_equal(a.clusters[q], b.clusters[q]), q
+
+
 def test_cheb_in_product_reduction_same_bits(gpu):
     """The Chebyshev three-term step applied in the split-K reduction of the
     Krylov small problem's T Y product (knob 19, default) gives the bits of the

@@ -503,31 +503,36 @@ def test_xtx_int8_exact(gpu, n, maxv, slices):
     print(f"xtx n={n} slices={ns}: int8 {ms * 1e3:.1f} us, fp64 {ms64 * 1e3:.1f} us")
 
 
-@pytest.mark.parametrize("glds", [1, 0])
+@pytest.mark.parametrize("glds,wide", [(1, 1), (1, 0), (0, 0)])
 @pytest.mark.parametrize("n,maxv,slices", [(1100, 120, 1), (1500, 16000, 2), (2000, 127, 1), (4100, 9000, 2),
-                                           (1025, 300, 2)])
-def test_xtx_int8_tiles128_exact(gpu, n, maxv, slices, glds):
-    """The pipeline's 128-column tile kernels (the LDS-DMA ring, knob 32 = 1,
-    and the register-staged one): exact X'X at ragged n, both slice counts."""
+                                           (1025, 300, 2), (300, 9000, 2), (130, 50, 1)])
+def test_xtx_int8_tiles128_exact(gpu, n, maxv, slices, glds, wide):
+    """The pipeline's whole-triangle int8 X'X kernels -- k_xtx_i8_w's 256 x 128
+    tiles (knob 44 = 1), the 128-tile LDS-DMA ring (knob 32 = 1) and the
+    register-staged 128-tiles: exact X'X at ragged n (odd tile-column counts:
+    the last 256-row panel past the padded columns), both slice counts."""
     rng = np.random.default_rng(n * 3 + maxv)
     x = rng.integers(0, maxv, size=(n, n)).astype(np.float64)
     x[0, 0] = maxv - 1
-    old = G.knob(32, glds)
+    old, oldw = G.knob(32, glds), G.knob(44, wide)
     try:
         S, ns, ms, st = _xtx(gpu, x, 2)
     finally:
         G.knob(32, old)
+        G.knob(44, oldw)
     assert st == 0 and ns == slices
     assert np.array_equal(S, _exact_xtx(x))
-    print(f"xtx128 n={n} slices={ns} glds={glds}: {ms * 1e3:.1f} us")
+    print(f"xtx128 n={n} slices={ns} glds={glds} wide={wide}: {ms * 1e3:.1f} us")
 
 
+@pytest.mark.parametrize("wide", [1, 0])
 @pytest.mark.parametrize("nzmap", [1, 0])
 @pytest.mark.parametrize("n", [1100, 3000, 4100])
-def test_xtx_int8_tiles128_sparse_high_slice(gpu, n, nzmap):
+def test_xtx_int8_tiles128_sparse_high_slice(gpu, n, nzmap, wide):
     """Counts >= 128 only in a band around the diagonal and at a few scattered
-    entries (raw Hi-C): the LDS-DMA kernel skips the high slice's all-zero
-    128 x 64 blocks (knob 34) and the product stays exact."""
+    entries (raw Hi-C): the LDS-DMA kernels skip the high slice's all-zero
+    128 x 64 blocks (knob 34; k_xtx_i8_w, knob 44, takes the nonzero ones in
+    its second phase) and the product stays exact."""
     rng = np.random.default_rng(n)
     x = rng.integers(0, 128, size=(n, n)).astype(np.float64)
     i = np.arange(n)
@@ -537,15 +542,16 @@ def test_xtx_int8_tiles128_sparse_high_slice(gpu, n, nzmap):
         x[i[ok], j[ok]] = rng.integers(128, 16000, size=int(ok.sum()))
     r, c = rng.integers(0, n, 40), rng.integers(0, n, 40)
     x[r, c] = 15000
-    old32, old34 = G.knob(32, 1), G.knob(34, nzmap)
+    old32, old34, old44 = G.knob(32, 1), G.knob(34, nzmap), G.knob(44, wide)
     try:
         S, ns, ms, st = _xtx(gpu, x, 2)
     finally:
         G.knob(32, old32)
         G.knob(34, old34)
+        G.knob(44, old44)
     assert st == 0 and ns == 2
     assert np.array_equal(S, _exact_xtx(x))
-    print(f"xtx128 sparse-high n={n} nzmap={nzmap}: {ms * 1e3:.1f} us")
+    print(f"xtx128 sparse-high n={n} nzmap={nzmap} wide={wide}: {ms * 1e3:.1f} us")
 
 
 @pytest.mark.parametrize("n,maxv", [(515, 16000), (1100, 9000), (1100, 120)])
