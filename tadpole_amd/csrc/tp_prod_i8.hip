@@ -475,6 +475,12 @@ __global__ void __launch_bounds__(256, 3 - NB) k_pd_prod(const int8_t *__restric
         __syncthreads();
         for (int st = 0; st < T; ++st) {
             gload(ra, rb, st + 1);
+#ifndef TP_PD_NO_SCHED_PIN
+            // the next step's loads issue before this step's MFMAs (left alone,
+            // the scheduler sinks them three quarters of the way down the MFMA
+            // block and their HBM latency is exposed every step)
+            __builtin_amdgcn_sched_barrier(0);
+#endif
             mstep(0);
             __syncthreads();
             lstore(ra, rb, 0);
