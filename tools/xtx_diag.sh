@@ -17,7 +17,7 @@ cat $O/time.log
 [ -n "$TIME_ONLY" ] && exit 0
 pass() {   # name counters...
   local nm=$1; shift
-  timeout -s KILL 300 rocprofv3 --pmc "$@" --kernel-include-regex k_xtx_i8_glds --output-format csv -d $O/pmc_$nm -o run -- python3 tools/xtx_time.py $N 1 > $O/pmc_$nm.log 2>&1
+  timeout -s KILL 300 rocprofv3 --pmc "$@" --kernel-include-regex "${KRX:-k_xtx_i8}" --output-format csv -d $O/pmc_$nm -o run -- python3 tools/xtx_time.py $N 1 > $O/pmc_$nm.log 2>&1
   local rc=$?; echo "pmc $nm rc=$rc"; return $rc
 }
 pass sq SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE &&
