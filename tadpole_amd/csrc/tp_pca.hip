@@ -677,7 +677,10 @@ PcaStats pca_dev(Ctx &c, double *d_C, int n, int k, double *d_P, double *d_Pt, d
     const bool krylov = n >= g_pca_krylov_min && b_est < n;
     const bool cspace = g_pca_ckrylov > 0 || (g_pca_ckrylov < 0 && n >= g_ckry_min);
     const int cend = c_col1 < 0 ? n + 2 : c_col1;
-    const bool i8 = krylov && g_prod_i8 > 0 && !cspace && prod_i8_ok(n, krylov_block(k));
+    // the int8-digit products: the G-space blocks of krylov_block(k) columns, the
+    // C-space blocks of 32 (knob 45)
+    const bool i8 = krylov && g_prod_i8 > 0 &&
+                    (cspace ? g_pd_cspace != 0 && prod_i8_ok(n, 32) : prod_i8_ok(n, krylov_block(k)));
     // cm_pending: d_cmean is where C's column means go; with the int8 products
     // over all of [C | m | 1] they come out of A's digit pass (k_colmean's bits)
     const bool cm_fused = cm_pending && i8 && c_col0 == 0 && cend == n + 2 && prod_digits_means_ok(n);

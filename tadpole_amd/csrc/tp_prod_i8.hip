@@ -38,6 +38,7 @@ namespace tp {
 // (test_prod_i8_digit_product); the 32 C3 products 4.6 ms against 6.3
 // 
 int g_prod_i8 = 1;
+int g_pd_cspace = 0;   // knob 45: C-space blocks (32 columns) on the int8 digits
 int g_pd_digits_blk = 1;   // knob 38: the block's digits by (column, slice) workgroups (0: one per column); same bits
 
 constexpr int PD_DIG = 7;   // digits per value
@@ -630,6 +631,151 @@ __global__ void __launch_bounds__(512, 1) k_pd_prod128(const int8_t *__restrict_
             }
 }
 
+// k_pd_prodA (knob 36 = 5): the same products, pairs, int32 sums and combine
+// (the bits of k_pd_prod) for 128-row tiles, built on the per-CU fill rate
+// (tools/ubench_fill.hip: ~20 GB/s a CU from HBM, ~35 from L2, registers and
+// LDS-DMA alike).  k_pd_prod moves A's 48 KB (HBM) and the block's 56 KB (L2,
+// re-read by every 64-row workgroup) per two workgroups a step: 4.0 us
+// predicted, 4.06 measured.  Here each of 8 waves owns 16 rows x 64 columns
+// (seven int32 sums x 4 tiles, 112 registers), so A's fragments are
+// wave-private: loaded straight into registers (1 KiB per digit, 2 steps
+// ahead in 3 register sets), never through LDS; only the block (28 KB a step)
+// is staged, by LDS-DMA into a 3-stage ring with the bank swizzle on the
+// source (k_xtx_i8_glds's).  A step moves 76 KB for 128 x 64 outputs.
+constexpr int PA_ST = 3;   // block ring stages
+__device__ __forceinline__ void pd_glds16(const void *g, void *l) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)g,
+                                     (__attribute__((address_space(3))) void *)l, 16, 0, 0);
+}
+// s_waitcnt vmcnt(N) as an instruction the compiler's wait insertion sees
+template <int N>
+__device__ __forceinline__ void pd_wait_vm() {
+    static_assert(N >= 0 && N < 64, "vmcnt");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x70 | 0xF00);
+}
+__device__ __forceinline__ void pd_wait_lgkm0() { __builtin_amdgcn_s_waitcnt(0xC07F); }
+
+// RB 16-row A fragments and CB 16-column block fragments a wave (seven int32
+// sums x RB x CB tiles: 112 registers for 1 x 4); 8 waves, so a workgroup
+// covers 128 RB rows of A and N = 16 CB columns (1 x 4: the G-space blocks of
+// 64 columns; 1 x 2: the C-space blocks of 32).
+template <int RB, int CB>
+__global__ void __launch_bounds__(512, 1) k_pd_prodA(const int8_t *__restrict__ Da, int Kp, int M,
+                                                     const int8_t *__restrict__ Db, const double *__restrict__ rs,
+                                                     const double *__restrict__ cs, double *__restrict__ part,
+                                                     size_t pstride, int kchunk) {
+    static_assert(RB * CB <= 4, "tile shapes");
+    constexpr int NCH = PD_DIG * CB;            // block chunks (1 KiB) a stage
+    constexpr int DW = (NCH + 7) / 8;           // DMAs a wave a stage
+    constexpr int ROWS = 128 * RB;
+    __shared__ __attribute__((aligned(16))) int8_t L[PA_ST * NCH * 1024];
+    const int tm = (M + ROWS - 1) / ROWS, tm64 = (M + 63) / 64;
+    const int total = (int)gridDim.x;
+    const int xcd = (int)blockIdx.x & 7, slot = (int)blockIdx.x >> 3;
+    const int Lg = xcd * (total >> 3) + min(xcd, total & 7) + slot;
+    const int bm = Lg % tm, z = Lg / tm;
+    const int t = threadIdx.x, lane = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int fr = lane & 15, kc = lane >> 4;
+    const int kbeg = z * kchunk, kend = min(Kp, kbeg + kchunk);
+    const int nsteps = Kp / 64;
+    TP_DASSERT(Kp % 64 == 0 && kchunk % 64 == 0 && kend - kbeg >= 64);
+    const int T = (kend - kbeg) / 64, st0 = kbeg / 64;
+    // A: wave w's 16 RB rows start at row0 (inside one 64-column tile of the
+    // image; a tile past the image -- odd tile count -- re-reads the last one:
+    // its rows are past M and never stored); lane (fr, kc) of fragment a loads
+    // row 16 a + fr, k bytes 16 kc ..
+    const int row0 = bm * ROWS + 16 * RB * w;
+    const int8_t *ga = Da + (size_t)min(row0 >> 6, tm64 - 1) * nsteps * (PD_ADIG * PD_BLK) +
+                       ((row0 & 63) + fr) * 64 + 16 * kc;
+    // the block: chunk c (< NCH) = digit c / CB, columns 16 (c % CB) ..; lane p
+    // loads column p >> 2, k quarter (p & 3) ^ ((p >> 4) & 2)
+    const int8_t *gb = Db + ((lane >> 2) * 64 + 16 * ((lane & 3) ^ ((lane >> 4) & 2)));
+    auto aload = [&](pd_i32x4 (&ra)[PD_ADIG][RB], int st) {
+        const size_t o = (size_t)(st0 + min(st, T - 1)) * (PD_ADIG * PD_BLK);
+#pragma unroll
+        for (int s = 0; s < PD_ADIG; ++s)
+#pragma unroll
+            for (int a = 0; a < RB; ++a) ra[s][a] = *(const pd_i32x4 *)(ga + o + s * PD_BLK + a * 1024);
+    };
+    auto bissue = [&](int st) {   // stage st of the block into ring slot st % PA_ST
+        const size_t o = (size_t)(st0 + min(st, T - 1)) * (PD_DIG * PD_BLK);
+        int8_t *dst = L + (st % PA_ST) * (NCH * 1024);
+#pragma unroll
+        for (int i = 0; i < DW; ++i) {
+            // past the last chunk a wave repeats its previous one (same bytes to
+            // the same LDS place): DW DMAs a wave, one wait count, no branch
+            const int c = w + 8 * i < NCH ? w + 8 * i : w + 8 * (i - 1);
+            pd_glds16(gb + o + (c / CB) * PD_BLK + (c % CB) * 1024, dst + c * 1024);
+        }
+    };
+    pd_i32x4 acc[PD_DIG][RB][CB];
+#pragma unroll
+    for (int u = 0; u < PD_DIG; ++u)
+#pragma unroll
+        for (int a = 0; a < RB; ++a)
+#pragma unroll
+            for (int b = 0; b < CB; ++b) acc[u][a][b] = pd_i32x4{0, 0, 0, 0};
+    const int roff = (4 * fr + (kc ^ ((fr >> 2) & 2))) * 16;
+    auto mstep = [&](const pd_i32x4 (&ra)[PD_ADIG][RB], int st) {
+        const int8_t *Lb = L + (st % PA_ST) * (NCH * 1024) + roff;
+#pragma unroll
+        for (int q = 0; q < PD_DIG; ++q) {
+            pd_i32x4 fb[CB];
+#pragma unroll
+            for (int b = 0; b < CB; ++b) fb[b] = *(const pd_i32x4 *)(Lb + (CB * q + b) * 1024);
+#pragma unroll
+            for (int s0 = 0; s0 + q < PD_DIG && s0 < PD_ADIG; ++s0)
+#pragma unroll
+                for (int a = 0; a < RB; ++a)
+#pragma unroll
+                    for (int b = 0; b < CB; ++b)
+                        acc[s0 + q][a][b] =
+                            __builtin_amdgcn_mfma_i32_16x16x64_i8(ra[s0][a], fb[b], acc[s0 + q][a][b], 0, 0, 0);
+        }
+    };
+    // step st, after the wait and the barrier: block stage st everywhere and
+    // stage st - 1's slot free; A(st + 2) loaded into the set step st - 1 used
+    // and block stage st + 2 issued (ring of 3).  (A one-step form with two
+    // register sets gets compiler waits of vmcnt(0) before its MFMAs: the
+    // compiler's count ignores the DMAs issued after the A loads.)
+    pd_i32x4 r0[PD_ADIG][RB], r1[PD_ADIG][RB], r2[PD_ADIG][RB];
+    aload(r0, 0);
+    bissue(0);
+    aload(r1, 1);
+    bissue(1);
+    auto step = [&](pd_i32x4 (&cur)[PD_ADIG][RB], pd_i32x4 (&nxt)[PD_ADIG][RB], int st) {
+        pd_wait_vm<PD_ADIG * RB + DW>();   // A(st + 1) and stage st + 1 may stay in flight
+        pd_wait_lgkm0();
+        __builtin_amdgcn_s_barrier();
+        aload(nxt, st + 2);
+        bissue(st + 2);
+        mstep(cur, st);
+    };
+    int st = 0;
+    for (; st + 2 < T; st += 3) {
+        step(r0, r2, st);
+        step(r1, r0, st + 1);
+        step(r2, r1, st + 2);
+    }
+    if (st < T) step(r0, r2, st);
+    if (st + 1 < T) step(r1, r0, st + 1);
+    pd_wait_vm<0>();   // the redundant tail loads and DMAs land before the workgroup ends
+#pragma unroll
+    for (int a = 0; a < RB; ++a)
+#pragma unroll
+        for (int b = 0; b < CB; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = row0 + 16 * a + 4 * kc + r;
+                const int j = 16 * b + fr;
+                if (i >= M) continue;
+                double v = 0.0;
+#pragma unroll
+                for (int u = PD_DIG - 1; u >= 0; --u) v += (double)acc[u][a][b][r] * ldexp(1.0, 96 - 8 * u);
+                (part + pstride * z)[(size_t)i + (size_t)j * M] = (v * rs[i]) * cs[j];
+            }
+}
+
 // k_pd_dma: the same products (same pairs, same int32 sums, same combine: the
 // bits of k_pd_prod), built for the HBM stream (round 5).  k_pd_prod moved 52
 // KB a k step per workgroup through registers and ds_write_b128, one step in
@@ -656,14 +802,6 @@ constexpr int PD_RING = TP_PD_RING;
 constexpr int PD_BOFF = PD_ADIG * 4 * 1024;                 // B's chunks after A's in a stage
 constexpr int PD_STAGE = PD_BOFF + PD_DIG * 4 * 1024;       // 52 KB
 static_assert(PD_RING * PD_STAGE <= 160 * 1024, "LDS ring");
-__device__ __forceinline__ void pd_glds16(const void *g, void *l) {
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)g,
-                                     (__attribute__((address_space(3))) void *)l, 16, 0, 0);
-}
-template <int N>
-__device__ __forceinline__ void pd_wait_vm() {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
 __global__ void __launch_bounds__(256, 1) k_pd_dma(const int8_t *__restrict__ Da, int Kp, int M,
                                                    const int8_t *__restrict__ Db, const double *__restrict__ rs,
                                                    const double *__restrict__ cs, double *__restrict__ part,
@@ -769,7 +907,9 @@ int prod_i8_pairs() {
 }
 
 // N = 64 (the G-space Krylov blocks; the kernel's workgroup is 64 x 64)
-bool prod_i8_ok(int K, int N) { return N == 64 && K >= 64; }
+// N = 64: the G-space blocks (knob 36's kernel); N = 32: the C-space blocks
+// (k_pd_prodA<1, 2>, knob 45)
+bool prod_i8_ok(int K, int N) { return (N == 64 || N == 32) && K >= 64; }
 
 static void launch_digits_cm(const double *A, int lda, int K, int c_begin, int c_end, int cols, ProdDigits &pd,
                              double *cm, int ncm, hipStream_t s) {
@@ -832,7 +972,7 @@ int prod_i8_partials(Ctx &c, const ProdDigits &pd, int r0, int M, const double *
     if (!prod_i8_ok(K, N) || (K + 63) / 64 * 64 != pd.Kp || r0 < pd.col0 || r0 + M > pd.col0 + pd.cols ||
         (r0 - pd.col0) % 64 || pd.pending)
         fail(TP_ERR_INTERNAL, "prod_i8: rows outside the digit image or off its 64-column tiles, or an unsupported block");
-    const size_t slb = (size_t)N * pd.Kp;
+    const size_t slb = (size_t)64 * pd.Kp;   // the image spaces k steps by whole 64-column tiles
     char *bb = c.buf[S_PDIGB].as<char>(PD_DIG * slb + 256 + 512 * sizeof(double) +
                                         (size_t)N * ((pd.Kp + 1023) / 1024) * sizeof(double));
     int8_t *Db = (int8_t *)bb;
@@ -859,7 +999,13 @@ int prod_i8_partials(Ctx &c, const ProdDigits &pd, int r0, int M, const double *
     const int tm = (M + 63) / 64;
     // one LDS buffer, two workgroups a CU: the 32 C3 products 4.57 ms against
     // 5.35 for the double-buffered one-workgroup form (knob 36 = 2, A/B)
-    if (g_prod_i8 == 4)
+    if (N == 32)
+        hipLaunchKernelGGL((k_pd_prodA<1, 2>), dim3((unsigned)((M + 127) / 128 * S)), dim3(512), 0, s, Da, pd.Kp, M, Db,
+                           rs, cs, *part, pstride, kc);
+    else if (g_prod_i8 == 5)
+        hipLaunchKernelGGL((k_pd_prodA<1, 4>), dim3((unsigned)((M + 127) / 128 * S)), dim3(512), 0, s, Da, pd.Kp, M, Db,
+                           rs, cs, *part, pstride, kc);
+    else if (g_prod_i8 == 4)
         hipLaunchKernelGGL(k_pd_prod128, dim3((unsigned)((M + 127) / 128 * S)), dim3(512), (size_t)PD_BUF2, s, Da, pd.Kp,
                            M, Db, rs, cs, *part, pstride, kc);
     else if (g_prod_i8 == 3)

@@ -714,12 +714,18 @@ template <int NS, bool COR>
 __global__ void __launch_bounds__(512) k_xtx_i8_w(const int8_t *__restrict__ S, int n, int Kp, int Np,
                                                   double *__restrict__ C, int ntiles,
                                                   const double *__restrict__ cm, const double *__restrict__ csd,
-                                                  const unsigned *__restrict__ nzw, int NW) {
+                                                  const unsigned *__restrict__ nzw, int NW,
+                                                  const int2 *__restrict__ tiles = nullptr, int c0 = 0,
+                                                  int c1 = 0x7fffffff) {
     static_assert(NS == 1 || NS == 2, "1 or 2 slices");
     __shared__ __attribute__((aligned(16))) int8_t L[XW_LDS];
     const int tnc = Np / 128;
     int P, Q;
-    {
+    if (tiles) {   // column slab (C5 row-sharded C): the listed tiles, stores filtered to [c0, c1)
+        const int2 tl = tiles[blockIdx.x];
+        P = tl.x;
+        Q = tl.y;
+    } else {
         const int xcd = (int)blockIdx.x & 7, slot = (int)blockIdx.x >> 3;
         xtx_w_tile(xcd * (ntiles >> 3) + min(xcd, ntiles & 7) + slot, tnc, P, Q);
     }
@@ -914,8 +920,8 @@ __global__ void __launch_bounds__(512) k_xtx_i8_w(const int8_t *__restrict__ S, 
                     d = cij / (pm[384 + il] * pm[640 + jl]);
                     if (isnan(d)) d = 0.0;
                 }
-                C[(size_t)i + (size_t)j * n] = d;
-                C[(size_t)j + (size_t)i * n] = d;
+                if (j >= c0 && j < c1) C[(size_t)i + (size_t)(j - c0) * n] = d;
+                if (i >= c0 && i < c1) C[(size_t)j + (size_t)(i - c0) * n] = d;
             }
 }
 
@@ -1071,8 +1077,8 @@ int g_xtx_w = 1;   // knob 44: the whole upper triangle by k_xtx_i8_w (256 x 128
 
 template <int NS, bool COR>
 static void launch_xtx_w_t(Ctx &c, const int8_t *sl, int n, int Kp, int Np, double *d_S, const double *cm,
-                           const double *csd) {
-    const long nt = xtx_w_tiles(Np / 128);
+                           const double *csd, const int2 *d_tl, long ntl, int c0, int c1) {
+    const long nt = d_tl ? ntl : xtx_w_tiles(Np / 128);
     unsigned *nzw = nullptr;
     const int NW = (Kp / 64 + 31) / 32;
     if (NS == 2 && g_xtx_nz) {
@@ -1080,21 +1086,24 @@ static void launch_xtx_w_t(Ctx &c, const int8_t *sl, int n, int Kp, int Np, doub
         hipLaunchKernelGGL(k_slice_nz, dim3((unsigned)(Np / 128), (unsigned)NW), dim3(256), 0, c.cur,
                            sl + (size_t)Np * Kp, Kp, NW, nzw);
     }
-    hipLaunchKernelGGL((k_xtx_i8_w<NS, COR>), dim3((unsigned)nt), dim3(512), 0, c.cur, sl, n, Kp, Np, d_S, (int)nt,
-                       cm, csd, nzw, NW);
+    if (nt > 0)
+        hipLaunchKernelGGL((k_xtx_i8_w<NS, COR>), dim3((unsigned)nt), dim3(512), 0, c.cur, sl, n, Kp, Np, d_S,
+                           (int)nt, cm, csd, nzw, NW, d_tl, c0, c1);
 }
-// the whole upper triangle by k_xtx_i8_w when it applies
-static bool launch_xtx_w(Ctx &c, int ns, const int8_t *sl, int n, int Kp, int Np, double *d_S, const double *cm,
-                         const double *csd) {
-    if (!g_xtx_w || !g_xtx_glds || !g_xtx_supertile || (ns != 1 && ns != 2)) return false;
-    if (ns == 2 && Kp / 64 > XW_MAXNK) return false;   // t01's int32 bound
+static bool xtx_w_applies(int ns, int Kp) {
+    if (!g_xtx_w || !g_xtx_glds || (ns != 1 && ns != 2)) return false;
+    return ns == 1 || Kp / 64 <= XW_MAXNK;   // t01's int32 bound
+}
+// the whole upper triangle (d_tl null) or a column slab's tiles by k_xtx_i8_w
+static void launch_xtx_w(Ctx &c, int ns, const int8_t *sl, int n, int Kp, int Np, double *d_S, const double *cm,
+                         const double *csd, const int2 *d_tl = nullptr, long ntl = 0, int c0 = 0,
+                         int c1 = 0x7fffffff) {
     const bool cor = cm != nullptr;
-    if (ns == 1 && !cor) launch_xtx_w_t<1, false>(c, sl, n, Kp, Np, d_S, cm, csd);
-    else if (ns == 2 && !cor) launch_xtx_w_t<2, false>(c, sl, n, Kp, Np, d_S, cm, csd);
-    else if (ns == 1) launch_xtx_w_t<1, true>(c, sl, n, Kp, Np, d_S, cm, csd);
-    else launch_xtx_w_t<2, true>(c, sl, n, Kp, Np, d_S, cm, csd);
+    if (ns == 1 && !cor) launch_xtx_w_t<1, false>(c, sl, n, Kp, Np, d_S, cm, csd, d_tl, ntl, c0, c1);
+    else if (ns == 2 && !cor) launch_xtx_w_t<2, false>(c, sl, n, Kp, Np, d_S, cm, csd, d_tl, ntl, c0, c1);
+    else if (ns == 1) launch_xtx_w_t<1, true>(c, sl, n, Kp, Np, d_S, cm, csd, d_tl, ntl, c0, c1);
+    else launch_xtx_w_t<2, true>(c, sl, n, Kp, Np, d_S, cm, csd, d_tl, ntl, c0, c1);
     TP_HIP(hipGetLastError());
-    return true;
 }
 
 // S (n x n) = X'X exactly on the upper tiles of tile columns [tc0, tc1) and
@@ -1108,7 +1117,10 @@ void xtx_int8_tiles128(Ctx &c, const int8_t *sl, int n, int ns, double *d_S, int
     tc0 = std::max(0, tc0);
     tc1 = tc1 < 0 ? tn : std::min(tn, tc1);
     if (tc1 <= tc0) return;
-    if (tc0 == 0 && tc1 == tn && launch_xtx_w(c, ns, sl, n, Kp, Np, d_S, cm, csd)) return;
+    if (tc0 == 0 && tc1 == tn && g_xtx_supertile && xtx_w_applies(ns, Kp)) {
+        launch_xtx_w(c, ns, sl, n, Kp, Np, d_S, cm, csd);
+        return;
+    }
     const unsigned nb = (unsigned)((long)tc1 * (tc1 + 1) / 2 - (long)tc0 * (tc0 + 1) / 2);
     const int tn_all = (tc0 == 0 && tc1 == tn && g_xtx_supertile) ? tn : 0;
     launch_xtx128(c, ns, nb, sl, n, Kp, Np, d_S, tc0, tn_all, cm, csd, nullptr, 0, 0x7fffffff);
@@ -1124,15 +1136,23 @@ void xtx_int8_slab128(Ctx &c, const int8_t *sl, int n, int ns, double *d_slab, i
     if (c1 <= c0) return;
     const int Kp = xtx_kp(n), Np = (n + 127) / 128 * 128;
     const int tn = Np / 128, T0 = c0 / 128, T1 = (c1 + 127) / 128;
+    const bool wide = xtx_w_applies(ns, Kp);
     std::vector<int2> tl;
-    for (int q = T0; q < T1; ++q)
-        for (int p = 0; p <= q; ++p) tl.push_back(make_int2(p, q));
-    for (int p = T0; p < T1; ++p)
-        for (int q = T1; q < tn; ++q) tl.push_back(make_int2(p, q));
+    if (wide) {   // k_xtx_i8_w tiles (256-row panel P, 128-column panel Q, 2P <= Q)
+        for (int q = T0; q < T1; ++q)   // the slab's columns, upper part
+            for (int p = 0; 2 * p <= q; ++p) tl.push_back(make_int2(p, q));
+        for (int p = c0 / 256; p <= (c1 - 1) / 256; ++p)   // its rows' mirrors past the slab
+            for (int q = std::max(T1, 2 * p); q < tn; ++q) tl.push_back(make_int2(p, q));
+    } else {
+        for (int q = T0; q < T1; ++q)
+            for (int p = 0; p <= q; ++p) tl.push_back(make_int2(p, q));
+        for (int p = T0; p < T1; ++p)
+            for (int q = T1; q < tn; ++q) tl.push_back(make_int2(p, q));
+    }
     int2 *d_tl = c.buf[S_XTXT].as<int2>(tl.size());
     TP_HIP(hipMemcpyAsync(d_tl, tl.data(), tl.size() * sizeof(int2), hipMemcpyHostToDevice, c.cur));
-    const unsigned nb = (unsigned)tl.size();
-    launch_xtx128(c, ns, nb, sl, n, Kp, Np, d_slab, 0, 0, cm, csd, d_tl, c0, c1);
+    if (wide) launch_xtx_w(c, ns, sl, n, Kp, Np, d_slab, cm, csd, d_tl, (long)tl.size(), c0, c1);
+    else launch_xtx128(c, ns, (unsigned)tl.size(), sl, n, Kp, Np, d_slab, 0, 0, cm, csd, d_tl, c0, c1);
     TP_HIP(hipGetLastError());
     // the host tile list must outlive the asynchronous copy
     stream_sync(c, c.cur);

@@ -280,6 +280,35 @@ def test_cheb_in_product_reduction_same_bits(gpu):
     assert np.array_equal(a.dendro.height.view(np.uint64), b.dendro.height.view(np.uint64))   # PC-score bits
 
 
+@pytest.mark.parametrize("n", [4500, 10500])
+def test_cspace_int8_products(gpu, n):
+    """The C-space Krylov path (knob 20 = 1 forces it at 4500 bins; the default
+    from 10 000) with its 32-column products on the int8 digits of C (knob 45,
+    k_pd_prodA<1, 2>) against the fp64 products: the same PC count, cluster
+    count and clusters at every level, dendrogram heights within 1e-9 (the
+    digit products are within ~1e-15 of sum |A||B|, not bit-equal)."""
+    import tadpole_amd as tp
+    m = synth_hic(n, SEED_BASE + 83)
+    runs = []
+    old20 = G.knob(20, 1)
+    try:
+        for i8 in (1, 0):
+            old = G.knob(45, i8)
+            try:
+                runs.append(tp.TADpole(m, max_pcs=150))
+            finally:
+                G.knob(45, old)
+    finally:
+        G.knob(20, old20)
+    a, b = runs
+    assert a.timings_ms[16] > 0                       # the Krylov path ran
+    assert (a.n_pcs, a.optimal_n_clusters) == (b.n_pcs, b.optimal_n_clusters)
+    assert a.clusters.keys() == b.clusters.keys()
+    for q in a.clusters:
+        assert np.array_equal(a.clusters[q], b.clusters[q]), q
+    np.testing.assert_allclose(a.dendro.height, b.dendro.height, rtol=1e-9, atol=0)
+
+
 # ------------------------------------------------------------ arm path (C5)
 
 @pytest.mark.parametrize("name", ["arm_c5layout", "arm_early"])

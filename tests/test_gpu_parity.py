@@ -818,15 +818,15 @@ def test_prod_i8_block_digitizers_same_bits(gpu, K):
 
 
 @pytest.mark.parametrize("K,M,col0,r0", [(4100, 330, 64, 64), (9000, 300, 128, 192), (7729, 400, 0, 128)])
-@pytest.mark.parametrize("kernel", [1, 3, 4])
+@pytest.mark.parametrize("kernel", [1, 3, 4, 5])
 def test_prod_i8_rows_slab_same_bits(gpu, K, M, col0, r0, kernel):
     """A rank's row shard of an int8-digit product, from the digit image of
     its own column slab [col0, M) (the C5 schedule: tp_shard.hip), carries
     the bits of the same rows of the whole product; K > 8192 takes the
     two-pass digitizers of the block (k_pd_colmax + k_pd_digits_sl) and of
     A (k_pd_digits).  kernel: the product kernel (knob 36: 1 = k_pd_prod,
-    3 = k_pd_dma, 4 = k_pd_prod128), which must agree bit for bit with each
-    other."""
+    3 = k_pd_dma, 4 = k_pd_prod128, 5 = k_pd_prodA), which must agree bit for
+    bit with each other."""
     import ctypes
     rng = np.random.default_rng(K + M + col0)
     A = np.asfortranarray(rng.uniform(-1, 1, size=(K, M)))

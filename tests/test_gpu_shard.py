@@ -50,7 +50,8 @@ def test_virtual_shards_row_sharded_c(gpu):
     computes only its columns of C (the int8 X'X tiles that touch them) and
     their means, and the Krylov products read only those columns -- C is never
     gathered.  Bit-identical to the gathered schedule (knob 24 = 0) and to one
-    shard, for both Krylov spaces (knob 20)."""
+    shard, for both Krylov spaces (knob 20) and both X'X tile kernels (knob 44:
+    k_xtx_i8_w's 256 x 128 slab tiles or the 128-tiles)."""
     import gpu_helpers as G
     m = synth_hic(2600, 35)
     old8 = G.knob(8, 0)            # the Krylov path at this size
@@ -61,13 +62,14 @@ def test_virtual_shards_row_sharded_c(gpu):
                 multi.set_virtual_shards(1)
                 ref = tp.TADpole(m, max_pcs=160, sharded=True)
                 assert ref.timings_ms[16] > 0
-                for slab in (1, 0):
-                    old24 = G.knob(24, slab)
+                for slab, wide in ((1, 1), (1, 0), (0, 1)):
+                    old24, old44 = G.knob(24, slab), G.knob(44, wide)
                     try:
                         multi.set_virtual_shards(3)
                         _same(tp.TADpole(m, max_pcs=160, sharded=True), ref)
                     finally:
                         G.knob(24, old24)
+                        G.knob(44, old44)
             finally:
                 G.knob(20, old20)
                 multi.set_virtual_shards(1)

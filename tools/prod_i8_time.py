@@ -1,6 +1,7 @@
 """Device time of one C3-size int8-digit product (tp_debug_prod_i8 at K = 7729,
 M = 7731, N = 64: B's digits + the product + the split-K reduce) for each
-product kernel (knob 36: 1 = k_pd_prod<1>, 2 = k_pd_prod<2>, 3 = k_pd_dma, 4 = k_pd_prod128)
+product kernel (knob 36: 1 = k_pd_prod<1>, 2 = k_pd_prod<2>, 3 = k_pd_dma, 4 = k_pd_prod128,
+5 = k_pd_prodA)
 against the fp64 path, and whether the kernels give the same bits.
 python tools/prod_i8_time.py [K]"""
 import ctypes
@@ -21,7 +22,7 @@ rng = np.random.default_rng(1)
 A = np.asfortranarray(rng.uniform(-1, 1, size=(K, M)))
 B = np.asfortranarray(rng.standard_normal((K, N)) / np.sqrt(K))
 outs = {}
-for kn in (1, 4, 3, 2):
+for kn in (1, 5, 1, 5, 4, 3, 2):
     old = ctypes.c_int(0); st = ctypes.c_int(0)
     L.tp_debug_knob(I(36), I(kn), ctypes.byref(old), ctypes.byref(st))
     _lib.check(st)
