@@ -1334,7 +1334,7 @@ void tp_debug_prod_i8(const double *A, const int *K, const int *M, const double 
         Ctx &c = ctx_for(0);
         hipStream_t s = c.cur;
         const int k = *K, m = *M, nn = *N;
-        if (!prod_i8_ok(k, nn) || m < 2) fail(TP_ERR_ARG, "prod_i8: N must be 64 and K >= 64");
+        if (!prod_i8_ok(k, nn) || m < 2) fail(TP_ERR_ARG, "prod_i8: N must be 32 or 64 and K >= 64");
         double *dA = c.buf[S_C].as<double>((size_t)k * m);
         double *dB = c.buf[S_Q].as<double>((size_t)k * nn);
         double *dO = c.buf[S_Z].as<double>(2 * (size_t)(m - 1) * nn);

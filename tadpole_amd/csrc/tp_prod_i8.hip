@@ -37,8 +37,8 @@ namespace tp {
 // k_gemm_ts; 2: the double-buffered kernel).  Within ~1e-15 of sum |A||B|
 // (test_prod_i8_digit_product); the 32 C3 products 4.6 ms against 6.3
 // 
-int g_prod_i8 = 1;
-int g_pd_cspace = 0;   // knob 45: C-space blocks (32 columns) on the int8 digits
+int g_prod_i8 = 5;
+int g_pd_cspace = 1;   // knob 45: C-space blocks (32 columns) on the int8 digits (0: k_gemm_ts)
 int g_pd_digits_blk = 1;   // knob 38: the block's digits by (column, slice) workgroups (0: one per column); same bits
 
 constexpr int PD_DIG = 7;   // digits per value

@@ -672,7 +672,8 @@ def test_gemm_rows_kernel_row_independent(gpu, M, N, K):
     print(f"rows gemm {M}x{N}x{K}: {t * 1e3:.1f} us, {2.0 * M * N * K / t / 1e9:.1f} TF/s")
 
 
-@pytest.mark.parametrize("K,M,N", [(4100, 302, 64), (7808, 130, 64), (4160, 9, 64), (9000, 200, 64)])
+@pytest.mark.parametrize("K,M,N", [(4100, 302, 64), (7808, 130, 64), (4160, 9, 64), (9000, 200, 64),
+                                   (4100, 302, 32), (9000, 330, 32), (4160, 9, 32)])
 def test_prod_i8_digit_product(gpu, K, M, N):
     """The Krylov products on the int8 MFMA (digit images, knob 36) against
     an 80-bit reference of the same A'B with the rank-1 epilogue: within

@@ -3,7 +3,7 @@ M = 7731, N = 64: B's digits + the product + the split-K reduce) for each
 product kernel (knob 36: 1 = k_pd_prod<1>, 2 = k_pd_prod<2>, 3 = k_pd_dma, 4 = k_pd_prod128,
 5 = k_pd_prodA)
 against the fp64 path, and whether the kernels give the same bits.
-python tools/prod_i8_time.py [K]"""
+python tools/prod_i8_time.py [K]   (env N=32: the C-space block width; KNOBS="1 5")"""
 import ctypes
 import os
 import sys
@@ -17,12 +17,13 @@ L = _lib.load()
 D = ctypes.POINTER(ctypes.c_double)
 I = lambda v: ctypes.byref(ctypes.c_int(v))  # noqa: E731
 K = int(sys.argv[1]) if len(sys.argv) > 1 else 7729
-M, N = K + 2, 64
+N = int(os.environ.get("N", "64"))   # 32: the C-space blocks (k_pd_prodA<1, 2> whatever knob 36 says)
+M = K + 2
 rng = np.random.default_rng(1)
 A = np.asfortranarray(rng.uniform(-1, 1, size=(K, M)))
 B = np.asfortranarray(rng.standard_normal((K, N)) / np.sqrt(K))
 outs = {}
-for kn in (1, 5, 1, 5, 4, 3, 2):
+for kn in [int(v) for v in os.environ.get("KNOBS", "1 5 1 5 4 3 2").split()]:
     old = ctypes.c_int(0); st = ctypes.c_int(0)
     L.tp_debug_knob(I(36), I(kn), ctypes.byref(old), ctypes.byref(st))
     _lib.check(st)
