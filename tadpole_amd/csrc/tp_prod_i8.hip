@@ -703,7 +703,9 @@ __global__ void __launch_bounds__(512, 1) k_pd_prodA(const int8_t *__restrict__ 
 #pragma unroll
         for (int i = 0; i < DW; ++i) {
             // past the last chunk a wave repeats its previous one (same bytes to
-            // the same LDS place): DW DMAs a wave, one wait count, no branch
+            // the same LDS place): DW DMAs a wave, one wait count, no branch (a
+            // branch around a DMA -- e.g. a small dummy one -- makes the
+            // compiler wait vmcnt(0) before the next MFMAs)
             const int c = w + 8 * i < NCH ? w + 8 * i : w + 8 * (i - 1);
             pd_glds16(gb + o + (c / CB) * PD_BLK + (c % CB) * 1024, dst + c * 1024);
         }
@@ -999,12 +1001,11 @@ int prod_i8_partials(Ctx &c, const ProdDigits &pd, int r0, int M, const double *
     const int tm = (M + 63) / 64;
     // one LDS buffer, two workgroups a CU: the 32 C3 products 4.57 ms against
     // 5.35 for the double-buffered one-workgroup form (knob 36 = 2, A/B)
+    const dim3 ga((unsigned)((M + 127) / 128 * S));
     if (N == 32)
-        hipLaunchKernelGGL((k_pd_prodA<1, 2>), dim3((unsigned)((M + 127) / 128 * S)), dim3(512), 0, s, Da, pd.Kp, M, Db,
-                           rs, cs, *part, pstride, kc);
+        hipLaunchKernelGGL((k_pd_prodA<1, 2>), ga, dim3(512), 0, s, Da, pd.Kp, M, Db, rs, cs, *part, pstride, kc);
     else if (g_prod_i8 == 5)
-        hipLaunchKernelGGL((k_pd_prodA<1, 4>), dim3((unsigned)((M + 127) / 128 * S)), dim3(512), 0, s, Da, pd.Kp, M, Db,
-                           rs, cs, *part, pstride, kc);
+        hipLaunchKernelGGL((k_pd_prodA<1, 4>), ga, dim3(512), 0, s, Da, pd.Kp, M, Db, rs, cs, *part, pstride, kc);
     else if (g_prod_i8 == 4)
         hipLaunchKernelGGL(k_pd_prod128, dim3((unsigned)((M + 127) / 128 * S)), dim3(512), (size_t)PD_BUF2, s, Da, pd.Kp,
                            M, Db, rs, cs, *part, pstride, kc);

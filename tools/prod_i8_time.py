@@ -32,9 +32,10 @@ for kn in [int(v) for v in os.environ.get("KNOBS", "1 5 1 5 4 3 2").split()]:
                        O64.ctypes.data_as(D), ms.ctypes.data_as(D), ctypes.byref(st))
     _lib.check(st)
     outs[kn] = O8
-    same = np.array_equal(O8.view(np.uint64), outs[1].view(np.uint64))
-    print(f"K={K} knob36={kn}: int8 product {ms[0] * 1e3:.1f} us, fp64 {ms[1] * 1e3:.1f} us, "
-          f"max |int8 - fp64| {np.max(np.abs(O8 - O64)):.2e}, bits == knob 1: {same}", flush=True)
+    first = next(iter(outs.values()))
+    same = np.array_equal(O8.view(np.uint64), first.view(np.uint64))
+    print(f"K={K} N={N} knob36={kn}: int8 product {ms[0] * 1e3:.1f} us, fp64 {ms[1] * 1e3:.1f} us, "
+          f"max |int8 - fp64| {np.max(np.abs(O8 - O64)):.2e}, bits == the first: {same}", flush=True)
 L.tp_debug_knob(I(36), I(1), ctypes.byref(ctypes.c_int(0)), ctypes.byref(ctypes.c_int(0)))
 # the block digitizer: (column, slice) workgroups (knob 38 = 1) vs one per column
 for kn in (0, 1):
@@ -44,5 +45,5 @@ for kn in (0, 1):
     L.tp_debug_prod_i8(A.ctypes.data_as(D), I(K), I(M), B.ctypes.data_as(D), I(N), O8.ctypes.data_as(D),
                        O64.ctypes.data_as(D), ms.ctypes.data_as(D), ctypes.byref(st))
     _lib.check(st)
-    same = np.array_equal(O8.view(np.uint64), outs[1].view(np.uint64))
+    same = np.array_equal(O8.view(np.uint64), next(iter(outs.values())).view(np.uint64))
     print(f"K={K} knob38={kn}: digits + product + reduce {ms[0] * 1e3:.1f} us, bits == default: {same}", flush=True)
