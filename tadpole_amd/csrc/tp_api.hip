@@ -1844,6 +1844,7 @@ void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
         case 43: p = &g_upload_mode; break;
         case 44: p = &g_xtx_w; break;
         case 45: p = &g_pd_cspace; break;
+        case 46: p = &g_pd_digits_big; break;
         default: fail(TP_ERR_ARG, "unknown knob");
         }
         if (*which == 3 && *value != 16 && *value != 32) fail(TP_ERR_ARG, "stage depth must be 16 or 32");

@@ -371,6 +371,7 @@ extern int g_devbuf_async;
 // blocks of exact 16-bit counts travel packed.  Returns the bytes sent packed.
 size_t upload_host(Ctx &c, const void *host, size_t bytes, void *d_dst, int nthreads, bool counts);
 extern int g_upload_mode;
+extern int g_pd_digits_big;   // knob 46
 extern int g_pd_cspace;   // knob 45: the C-space Krylov products on the int8 digits
 extern int g_xtx_w;   // knob 44: whole-triangle X'X by 256 x 128 tiles
 int prod_i8_partials(Ctx &c, const ProdDigits &pd, int r0, int M, const double *B, int ldb, int N, int K,

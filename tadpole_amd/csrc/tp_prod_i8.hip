@@ -38,6 +38,7 @@ namespace tp {
 // (test_prod_i8_digit_product); the 32 C3 products 4.6 ms against 6.3
 // 
 int g_prod_i8 = 5;
+int g_pd_digits_big = 1;   // knob 46: long columns' image in one read (0: k_pd_digits, three passes)
 int g_pd_cspace = 1;   // knob 45: C-space blocks (32 columns) on the int8 digits (0: k_gemm_ts)
 int g_pd_digits_blk = 1;   // knob 38: the block's digits by (column, slice) workgroups (0: one per column); same bits
 
@@ -145,10 +146,13 @@ __global__ void __launch_bounds__(256) k_pd_digits(const double *__restrict__ X,
 // registers across the max and the digits), thread t holding k = 1024 i + 4 t
 // .. + 3 -- one HBM pass over C instead of two (the second pass of k_pd_digits
 // misses L2 at C3: 1.87 GB moved for 0.9 GB of data)
-template <int IT, int ND>
-__global__ void __launch_bounds__(256) k_pd_digits_reg(const double *__restrict__ X, int ldx, int K, int cols, int Kp,
-                                                       int8_t *__restrict__ D, double *__restrict__ scale) {
-    __shared__ double red[4];
+// TB threads a column (256; 1024 for the long columns of the C-space path:
+// 24 300 bins with IT = 6 instead of k_pd_digits' three passes over C)
+template <int IT, int ND, int TB = 256>
+__global__ void __launch_bounds__(TB) k_pd_digits_reg(const double *__restrict__ X, int ldx, int K, int cols, int Kp,
+                                                      int8_t *__restrict__ D, double *__restrict__ scale) {
+    constexpr int NW = TB / 64;
+    __shared__ double red[NW];
     // adjacent columns on one XCD (workgroups are dealt round-robin over the 8):
     // columns c and c + 1 fill the two halves of each 128-byte line of the image
     // in the same L2 (gridDim.x is a multiple of 64)
@@ -163,7 +167,7 @@ __global__ void __launch_bounds__(256) k_pd_digits_reg(const double *__restrict_
     for (int i = 0; i < IT; ++i)
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            const int k = 1024 * i + 4 * t + u;
+            const int k = 4 * TB * i + 4 * t + u;
             v[i][u] = (live && k < K) ? x[k] : 0.0;
             mx = fmax(mx, fabs(v[i][u]));
             bad |= !isfinite(v[i][u]);
@@ -173,7 +177,9 @@ __global__ void __launch_bounds__(256) k_pd_digits_reg(const double *__restrict_
     for (int o = 32; o >= 1; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
     if ((t & 63) == 0) red[t >> 6] = mx;
     __syncthreads();
-    mx = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+    mx = red[0];
+#pragma unroll
+    for (int q = 1; q < NW; ++q) mx = fmax(mx, red[q]);
     const int e = pd_exp(mx);   // mx < 2^e
     const double sc = ldexp(1.0, 54 - e);
     if (t == 0) scale[c] = !live ? 0.0 : (isfinite(mx) ? ldexp(1.0, e - 54) : NAN);
@@ -181,7 +187,7 @@ __global__ void __launch_bounds__(256) k_pd_digits_reg(const double *__restrict_
     const int nsteps = Kp / 64;
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
-        const int k0 = 1024 * i + 4 * t;
+        const int k0 = 4 * TB * i + 4 * t;
         if (k0 < Kp) pd_digits4<ND>(v[i], 4, 0, ok, sc, D + pd_off<ND>(c, k0, nsteps));
     }
 }
@@ -952,6 +958,9 @@ void prod_digits_build(Ctx &c, const double *A, int lda, int K, int cols, int co
     }
     if (pd.Kp <= 1024 * PD_REG_IT)
         hipLaunchKernelGGL((k_pd_digits_reg<PD_REG_IT, PD_ADIG>), dim3((unsigned)cp), dim3(256), 0, s, A, lda, K, cols,
+                           pd.Kp, (int8_t *)pd.d, (double *)pd.rs);
+    else if (pd.Kp <= 4096 * 6 && g_pd_digits_big)   // one read of each long column (1024 threads)
+        hipLaunchKernelGGL((k_pd_digits_reg<6, PD_ADIG, 1024>), dim3((unsigned)cp), dim3(1024), 0, s, A, lda, K, cols,
                            pd.Kp, (int8_t *)pd.d, (double *)pd.rs);
     else
         hipLaunchKernelGGL(k_pd_digits<PD_ADIG>, dim3((unsigned)cp), dim3(256), 0, s, A, lda, K, cols, pd.Kp,
