@@ -117,7 +117,7 @@ static void pip_pass(Ctx &c, double *Kb, int n, int D, const double *W0, const P
     hipLaunchKernelGGL(k_pipz, dim3((unsigned)(dt * S)), dim3(256), 0, s, Kb, D, W0, n, chunk, ps.part, pstride, Kt,
                        Dh);
     const int nsl = (ldz + PR - 1) / PR, nh = (D + PR - 1) / PR;
-    hipLaunchKernelGGL(k_pipr, dim3((unsigned)nsl), dim3(256), 0, s, ps.part, pstride, S, D, ps.Z, ps.hh);
+    hipLaunchKernelGGL(k_pipr, dim3((unsigned)nsl), dim3(PR_TB), 0, s, ps.part, pstride, S, D, ps.Z, ps.hh);
     hipLaunchKernelGGL(k_pips<3>, dim3(1), dim3(512), 0, s, ps.Z, D, ps.hh, nh, shift, ps.Ri, ps.info, lowdin);
     const int tiles = (n + PA_ROWS - 1) / PA_ROWS;
     if (D > 0)

@@ -98,36 +98,38 @@ __global__ void __launch_bounds__(256) k_pipz(const double *__restrict__ K, int 
 // ---- reduce the Z partials (ascending chunk order) for a 64-row slice, and
 // the slice's share of H'H (H = rows < D of Z): hh[s] (32 x 32, col-major)
 constexpr int PR = 64;   // rows per reduce slice
-__global__ void __launch_bounds__(256) k_pipr(const double *__restrict__ part, size_t pstride, int S, int D,
-                                              double *__restrict__ Z, double *__restrict__ hh) {
+constexpr int PR_TB = 1024;   // threads: two entries each, 16 partials of each in flight
+__global__ void __launch_bounds__(PR_TB) k_pipr(const double *__restrict__ part, size_t pstride, int S, int D,
+                                                double *__restrict__ Z, double *__restrict__ hh) {
     __shared__ double Hs[PR][KP + 1];
     const int ldz = D + KP;
     const int r0 = blockIdx.x * PR;
     const int t = threadIdx.x;
-    constexpr int NE = PR * KP / 256;   // entries per thread
+    constexpr int NE = PR * KP / PR_TB;   // entries per thread
+    constexpr int G = 16;                 // partials of an entry in flight
     size_t idx[NE];
     bool in[NE];
     double v[NE];
 #pragma unroll
     for (int h = 0; h < NE; ++h) {
-        const int e = t + 256 * h;
+        const int e = t + PR_TB * h;
         const int row = r0 + (e & (PR - 1)), col = e / PR;
         in[h] = row < ldz;
         idx[h] = in[h] ? (size_t)row + (size_t)col * ldz : 0;
         v[h] = part[idx[h]];
     }
-    // the partials of every entry in flight together, summed in ascending order
+    // summed in ascending chunk order (the bits of a sequential sum)
     int z = 1;
-    for (; z + 4 <= S; z += 4) {
-        double q[NE][4];
+    for (; z + G <= S; z += G) {
+        double q[NE][G];
 #pragma unroll
         for (int h = 0; h < NE; ++h)
 #pragma unroll
-            for (int u = 0; u < 4; ++u) q[h][u] = part[idx[h] + (size_t)(z + u) * pstride];
+            for (int u = 0; u < G; ++u) q[h][u] = part[idx[h] + (size_t)(z + u) * pstride];
 #pragma unroll
         for (int h = 0; h < NE; ++h)
 #pragma unroll
-            for (int u = 0; u < 4; ++u) v[h] = v[h] + q[h][u];
+            for (int u = 0; u < G; ++u) v[h] = v[h] + q[h][u];
     }
     for (; z < S; ++z) {
 #pragma unroll
@@ -135,7 +137,7 @@ __global__ void __launch_bounds__(256) k_pipr(const double *__restrict__ part, s
     }
 #pragma unroll
     for (int h = 0; h < NE; ++h) {
-        const int e = t + 256 * h;
+        const int e = t + PR_TB * h;
         const int row = r0 + (e & (PR - 1)), col = e / PR;
         if (in[h]) Z[idx[h]] = v[h];
         Hs[e & (PR - 1)][col] = row < D ? v[h] : 0.0;
@@ -144,8 +146,8 @@ __global__ void __launch_bounds__(256) k_pipr(const double *__restrict__ part, s
     __syncthreads();
     double *o = hh + (size_t)blockIdx.x * KP * KP;
 #pragma unroll
-    for (int h = 0; h < 4; ++h) {
-        const int e = t + 256 * h;
+    for (int h = 0; h < KP * KP / PR_TB; ++h) {
+        const int e = t + PR_TB * h;
         const int a = e & 31, b = e >> 5;
         double acc = 0.0;
 #pragma unroll 16
@@ -364,12 +366,20 @@ __global__ void __launch_bounds__(256) k_pipc(const double *__restrict__ part, c
     const int lane = t & 63, w = t >> 6, fr = lane & 15, fk = lane >> 4;
     for (int e = t; e < KP * KP; e += 256) Rs[e >> 5][e & 31] = Ri[e];
     const double *pt = part + (size_t)tile * PA_SPLIT * PA_ROWS * KP;
+    // the splits' sums read along their rows (row-major 64 x 32: consecutive
+    // lanes, consecutive columns -- the earlier row-fastest order put each lane
+    // on its own 256-byte row), then W0 down its columns; the same kh and W0 - kh
+#pragma unroll
+    for (int h = 0; h < PA_ROWS * KP / 256; ++h) {
+        const int e = t + 256 * h, il = e >> 5, j = e & 31;
+        const size_t o = (size_t)il * KP + j;
+        Us[il][j] = ((pt[o] + pt[o + PA_ROWS * KP]) + pt[o + 2 * PA_ROWS * KP]) + pt[o + 3 * PA_ROWS * KP];
+    }
+    __syncthreads();
 #pragma unroll
     for (int h = 0; h < PA_ROWS * KP / 256; ++h) {
         const int e = t + 256 * h, il = e & 63, j = e >> 6, i = i0 + il;
-        const size_t o = (size_t)il * KP + j;
-        const double kh = ((pt[o] + pt[o + PA_ROWS * KP]) + pt[o + 2 * PA_ROWS * KP]) + pt[o + 3 * PA_ROWS * KP];
-        Us[il][j] = i < n ? W0[(size_t)i + (size_t)j * n] - kh : 0.0;
+        Us[il][j] = i < n ? W0[(size_t)i + (size_t)j * n] - Us[il][j] : 0.0;
     }
     __syncthreads();
     d4k acc[2];

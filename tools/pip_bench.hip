@@ -75,7 +75,7 @@ int main(int argc, char **argv) {
             timeit(nm, [&] { hipLaunchKernelGGL(k_pipz, dim3((unsigned)(dt * S)), dim3(256), 0, 0, K, D, W, n, chunk, part, pstride); });
             const int nsl = (ldz + PR - 1) / PR;
             snprintf(nm, sizeof nm, "D=%d k_pipr S=%d (%d wg)", D, S, nsl);
-            timeit(nm, [&] { hipLaunchKernelGGL(k_pipr, dim3((unsigned)nsl), dim3(256), 0, 0, part, pstride, S, D, Z, hh); });
+            timeit(nm, [&] { hipLaunchKernelGGL(k_pipr, dim3((unsigned)nsl), dim3(PR_TB), 0, 0, part, pstride, S, D, Z, hh); });
         }
         const int nh = (D + PR - 1) / PR;
         // a well-conditioned Zw: Z rows D.. = 64 I-ish via the hh = 0 path
