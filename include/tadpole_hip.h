@@ -59,6 +59,18 @@ enum {
                                    over the ranks of the device's communicator
                                    (tp_comm_init); every rank passes the same
                                    matrix and gets the same results            */
+#define TP_FLAG_SUBSET     16   /* tp_pipeline(_dev): run on the principal
+                                   submatrix good_idx[0 .. *n_good) names (input:
+                                   1-based, strictly ascending; implies NO_MASK;
+                                   bad[] is not written).  The centromere arms
+                                   (R/TADpole.R:362) read straight from the
+                                   cleaned whole matrix, never copied out      */
+#define TP_FLAG_LDS_LEAN   32   /* tuning hint: another pipeline runs on this
+                                   device at the same time; the CONISS sweep of
+                                   a matrix too large for LDS keeps its links in
+                                   global memory (slower alone) so its trees fit
+                                   on CUs beside the other pipeline's.  Results
+                                   are the same bits either way                */
 
 /* ---------------------------------------------------------------- runtime */
 int  tp_version(void);                          /* ABI version, 2 (see below)    */

@@ -20,6 +20,8 @@ TP_FLAG_ROW_MAJOR = 1
 TP_FLAG_CLEAN = 2
 TP_FLAG_NO_MASK = 4
 TP_FLAG_SHARDED = 8
+TP_FLAG_SUBSET = 16
+TP_FLAG_LDS_LEAN = 32
 ABI_VERSION = 2   # tp_version() this binding is written for (timings_ms: 32 doubles)
 
 #: every symbol include/tadpole_hip.h declares

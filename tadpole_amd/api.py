@@ -311,12 +311,14 @@ def _is_device(m) -> bool:
 
 
 def _pipeline(m, max_pcs: int, min_clusters: int, bad_frac: float, flags: int,
-              device: int, stream=None):
+              device: int, stream=None, subset=None):
     """One tp_pipeline call.  ``m``: a host array, or a square float64 torch
     tensor on the GPU (tp_pipeline_dev on it: no host staging; unless
     TP_FLAG_CLEAN it is cleaned in place).  ``stream`` (a torch.cuda.Stream):
     the pipeline is queued on that stream with its own library context, so
-    several pipelines can run concurrently on one GPU."""
+    several pipelines can run concurrently on one GPU.  ``subset`` (1-based,
+    strictly ascending bin indices): TP_FLAG_SUBSET, the pipeline runs on that
+    principal submatrix of ``m``, read in place (no copy of it is made)."""
     L = _lib.load()
     dev_in = _is_device(m)
     if dev_in:
@@ -333,10 +335,18 @@ def _pipeline(m, max_pcs: int, min_clusters: int, bad_frac: float, flags: int,
     n0 = m.shape[0]
     t0 = time.perf_counter()
     t_up = 0.0
-    k_cap = max(1, min(max_pcs, n0))
-    w_cap = max(1, n0)
-    bad = np.zeros(n0, np.int32)
     good = np.zeros(n0, np.int32)
+    nsub = n0
+    if subset is not None:
+        subset = np.asarray(subset, np.int64)
+        nsub = int(subset.size)
+        if nsub < 1 or nsub > n0:
+            raise ValueError("subset: 1..n0 bin indices")
+        good[:nsub] = subset
+        flags |= _lib.TP_FLAG_SUBSET
+    k_cap = max(1, min(max_pcs, nsub))
+    w_cap = max(1, nsub)
+    bad = np.zeros(n0, np.int32)
     nclu = np.zeros(k_cap, np.int32)
     scores = np.zeros(k_cap * w_cap)
     merge = np.zeros(2 * max(1, n0 - 1), np.int32)
@@ -345,6 +355,7 @@ def _pipeline(m, max_pcs: int, min_clusters: int, bad_frac: float, flags: int,
     timings = np.zeros(32)
     out = [cint(0) for _ in range(6)]
     n_good, k, w, n_pcs, n_clusters, st = out
+    n_good.value = nsub if subset is not None else 0
     if stream is None and not dev_in:
         L.tp_pipeline(dp(m), ctypes.byref(cint(n0)), ctypes.byref(cint(max_pcs)), ctypes.byref(cint(min_clusters)),
                       ctypes.byref(cdbl(bad_frac)), ctypes.byref(cint(flags)), ctypes.byref(cint(device)),
@@ -393,7 +404,7 @@ def _pipeline(m, max_pcs: int, min_clusters: int, bad_frac: float, flags: int,
     n = n_good.value
     kk, ww = k.value, w.value
     sc = scores[:kk * ww].reshape(ww, kk).T.copy()
-    return dict(bad=bad.astype(bool), good=good[:n].copy(), k=kk, w=ww, n_cluster=nclu[:kk].copy(),
+    return dict(bad=bad[:n].astype(bool) if subset is not None else bad.astype(bool), good=good[:n].copy(), k=kk, w=ww, n_cluster=nclu[:kk].copy(),
                 scores=sc, n_pcs=n_pcs.value, n_clusters=n_clusters.value,
                 merge=merge[:2 * (n - 1)].reshape(2, n - 1).T.copy(), height=height[:n - 1].copy(),
                 boundary=boundary[:n - 1].copy(), timings=timings,
@@ -678,16 +689,16 @@ def _run_arm(raw, plan, arm, max_pcs, min_clusters, device, shard_flag: int = 0,
     it, so the device cleans it (TP_FLAG_NO_MASK: the arm matrices are
     correlated as given, R/TADpole.R:362)."""
     names, bad_cols = plan[arm]
-    if _is_device(raw):   # already cleaned by tp_mask_dev
-        import torch
-        sel = torch.as_tensor(names - 1, device=raw.device)
-        sub = raw.index_select(0, sel).index_select(1, sel)
-        clean = _lib.TP_FLAG_CLEAN
+    if _is_device(raw):
+        # already cleaned by tp_mask_dev: the pipeline reads the arm's rows and
+        # columns straight from it (TP_FLAG_SUBSET; an index_select copy of the
+        # two C5 arms cost 16.5 ms of HBM traffic before either could start)
+        res = _pipeline(raw, max_pcs, min_clusters, 0.0, _lib.TP_FLAG_CLEAN | shard_flag, device, stream,
+                        subset=names)
     else:
         sub = raw[np.ix_(names - 1, names - 1)]
-        clean = 0
-    res = _pipeline(sub, max_pcs, min_clusters, 0.0, _lib.TP_FLAG_NO_MASK | clean | shard_flag, device, stream)
-    del sub
+        res = _pipeline(sub, max_pcs, min_clusters, 0.0, _lib.TP_FLAG_NO_MASK | shard_flag, device, stream)
+        del sub
     res["good"] = names.astype(np.int32)   # rownames inherited from the full matrix
     return _assemble(res, np.asarray(bad_cols))
 
@@ -726,8 +737,8 @@ def _tadpole_arms(raw, plan, max_pcs, min_clusters, device, shard_flag: int = 0,
     if _is_device(raw):
         device = raw.device.index if raw.device.index is not None else device
 
-    def run_arm(arm, arm_stream):
-        return _run_arm(raw, plan, arm, max_pcs, min_clusters, device, shard_flag, arm_stream)
+    def run_arm(arm, arm_stream, hint=0):
+        return _run_arm(raw, plan, arm, max_pcs, min_clusters, device, shard_flag | hint, arm_stream)
 
     if arm_groups is not None:
         from . import multi
@@ -735,7 +746,10 @@ def _tadpole_arms(raw, plan, max_pcs, min_clusters, device, shard_flag: int = 0,
         subs = multi.exchange_arms(arm_groups, mine)
     elif _arms_concurrent(raw, shard_flag, stream):
         # both arms start at once (0.305 s for C5 on one MI355X, 0.33 s one
-        # after the other).  TADPOLE_ARMS_Q_AT=s (1..3) holds q back until p's
+        # after the other).  The smaller arm's CONISS keeps its links out of
+        # LDS (TP_FLAG_LDS_LEAN, TADPOLE_ARMS_LEAN=0 turns it off): its trees
+        # then fit beside the larger arm's on the same CUs instead of waiting
+        # for them.  TADPOLE_ARMS_Q_AT=s (1..3) holds q back until p's
         # progress word reaches stage s (2: p's correlation queued, 3: p's
         # sweep): measured slower (0.32-0.34 s at s = 3: q's int8 X'X, 160 KiB
         # of LDS a workgroup, cannot share a CU with p's CONISS trees).
@@ -752,12 +766,15 @@ def _tadpole_arms(raw, plan, max_pcs, min_clusters, device, shard_flag: int = 0,
             _lib.check(st)
         try:
             with ThreadPoolExecutor(max_workers=2) as ex:
-                fp = ex.submit(run_arm, "p", sp)
+                lean = {"p": 0, "q": 0}
+                if os.environ.get("TADPOLE_ARMS_LEAN", "1") != "0":
+                    lean["q" if len(plan["q"][0]) <= len(plan["p"][0]) else "p"] = _lib.TP_FLAG_LDS_LEAN
+                fp = ex.submit(run_arm, "p", sp, lean["p"])
 
                 def run_q():
                     while q_at > 0 and prog[0] < q_at and not fp.done():
                         time.sleep(2e-4)
-                    return run_arm("q", sq)
+                    return run_arm("q", sq, lean["q"])
 
                 fq = ex.submit(run_q)
                 subs = {"p": fp.result(), "q": fq.result()}

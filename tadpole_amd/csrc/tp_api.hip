@@ -508,6 +508,7 @@ static SweepOut run_sweep(Ctx &c, const double *d_Pt, int n, int k, int min_clus
     sd.ldp = k;
     sd.k = k;
     sd.min_clusters = min_clusters;
+    sd.lds_lean = c.lds_lean;
     double *sums = c.buf[S_SWEEP].as<double>(sweep_sums_doubles(n, 0, k));
     const size_t rec = (size_t)k * (n - 1);
     char *recbuf = c.buf[S_SWEEP2].as<char>(rec * (4 + 4 + 8 + 8) + 256);
@@ -670,7 +671,7 @@ struct PipeOut {
 
 static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_clusters, double bad_frac, int flags,
                             int k_cap, int w_cap, int *bad, int *good_idx, int *n_cluster, double *scores,
-                            int *merge, double *height, int *boundary, double *timings) {
+                            int *merge, double *height, int *boundary, double *timings, int n_sub = 0) {
     hipStream_t s = c.cur;
     if (n0 < 1) fail(TP_ERR_ARG, "empty matrix");
     if (max_pcs < 1) fail(TP_ERR_ARG, "max_pcs must be >= 1");
@@ -707,6 +708,7 @@ static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_cl
         }
     } shard_scope(c, (flags & TP_FLAG_SHARDED) != 0);
     c.prof = timings != nullptr;
+    c.lds_lean = (flags & TP_FLAG_LDS_LEAN) != 0;
     c.recs.clear();
     c.evnext = 0;
     // the caller's progress word (tp_progress_attach): 0 started, 1 mask read
@@ -729,7 +731,22 @@ static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_cl
     int *d_good = c.buf[S_GOOD].as<int>(n0);
     int *d_ng = (int *)c.buf[S_NGOOD].as<char>(64);
     int n = 0;
-    if (flags & TP_FLAG_NO_MASK) {
+    if (flags & TP_FLAG_SUBSET) {
+        // the principal submatrix the caller names (a centromere arm's kept
+        // bins, R/TADpole.R:362): the gather below reads only its rows and
+        // columns, so the submatrix is never formed
+        if (!good_idx || n_sub < 1 || n_sub > n0) fail(TP_ERR_ARG, "TP_FLAG_SUBSET: *n_good must be in 1..n0");
+        std::vector<int> g(n_sub);
+        for (int q = 0; q < n_sub; ++q) {
+            g[q] = good_idx[q] - 1;
+            if (g[q] < 0 || g[q] >= n0 || (q > 0 && g[q] <= g[q - 1]))
+                fail(TP_ERR_ARG, "TP_FLAG_SUBSET: good_idx must hold strictly ascending 1-based indices into the matrix");
+        }
+        TP_HIP(hipMemcpyAsync(d_good, g.data(), n_sub * sizeof(int), hipMemcpyHostToDevice, s));
+        TP_HIP(hipMemsetAsync(d_bad, 0, n0 * sizeof(int), s));
+        stream_sync(c, s);
+        n = n_sub;
+    } else if (flags & TP_FLAG_NO_MASK) {
         std::vector<int> iota(n0);
         for (int q = 0; q < n0; ++q) iota[q] = q;
         TP_HIP(hipMemcpyAsync(d_good, iota.data(), n0 * sizeof(int), hipMemcpyHostToDevice, s));
@@ -749,8 +766,8 @@ static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_cl
         if (bad) TP_HIP(hipMemcpyAsync(pi, d_bad, n0 * sizeof(int), hipMemcpyDeviceToHost, s));
         if (good_idx) TP_HIP(hipMemcpyAsync(pi + n0, d_good, n0 * sizeof(int), hipMemcpyDeviceToHost, s));
         stream_sync(c, s);
-        if (!(flags & TP_FLAG_NO_MASK)) n = pi[2 * n0];
-        if (bad) memcpy(bad, pi, n0 * sizeof(int));
+        if (!(flags & (TP_FLAG_NO_MASK | TP_FLAG_SUBSET))) n = pi[2 * n0];
+        if (bad && !(flags & TP_FLAG_SUBSET)) memcpy(bad, pi, n0 * sizeof(int));
         if (good_idx) memcpy(good_idx, pi + n0, (size_t)n * sizeof(int));
     }
     PipeOut o;
@@ -1188,7 +1205,7 @@ static void pipeline_common(double *dM, const int *n0, const int *max_pcs, const
     PipeOut o = pipeline_dev(c, dM, *n0, max_pcs ? *max_pcs : 200, min_clusters ? *min_clusters : 2,
                              bad_frac ? *bad_frac : 0.01, flags ? *flags : 0, k_cap ? *k_cap : 0,
                              w_cap ? *w_cap : 0, bad, good_idx, n_cluster, scores, merge, height, boundary,
-                             timings_ms);
+                             timings_ms, flags && (*flags & TP_FLAG_SUBSET) && n_good ? *n_good : 0);
     if (n_good) *n_good = o.n_good;
     if (k) *k = o.k;
     if (w) *w = o.sw.w;

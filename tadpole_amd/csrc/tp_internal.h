@@ -61,6 +61,7 @@ struct Ctx {
     std::recursive_mutex mu;
     Shard shard;
     bool prof = false;                  // record per-kernel events this call
+    bool lds_lean = false;              // TP_FLAG_LDS_LEAN this call: CONISS links in global memory
     std::vector<hipEvent_t> evpool;
     size_t evnext = 0;
     struct Rec { int cls; hipEvent_t a, b; };
@@ -251,6 +252,7 @@ struct SweepDev {
     double *ustore = nullptr;             // ucap x (k + 1)
     int ucap = 0;
     int *ucount = nullptr;                // distinct segments inserted (may exceed ucap)
+    bool lds_lean = false;                // CONISS: links in global memory (a few bytes of LDS a tree)
 };
 // scratch of the shared CH segment statistics for ntrees trees
 extern int g_ch_dedup;        // 0: every tree computes its own segment statistics

@@ -1439,7 +1439,10 @@ static void run_coniss(const SweepDev &sd_in, hipStream_t s, bool stamped, Ctx *
     // global variant: 16-bit links in LDS when they fit (costs stay global)
     const size_t lu_bytes = coniss_link_stride(sd.n) * 4;
     const int bs = (nbk + 63) / 64;   // block-minimum slots per lane
-    const bool lu = !in_lds && g_coniss_lu && sd.n + 64 < 0xFFFF && lu_bytes <= 150 * 1024 && bs <= 11;
+    // lds_lean (TP_FLAG_LDS_LEAN: another pipeline runs beside this one): the
+    // links stay global too, so these trees fit on CUs whose LDS the other
+    // pipeline's LU trees hold (24.3k bins alone: ~1.4x slower a tree)
+    const bool lu = !in_lds && g_coniss_lu && !sd.lds_lean && sd.n + 64 < 0xFFFF && lu_bytes <= 150 * 1024 && bs <= 11;
     const size_t lds = in_lds ? coniss_lds_bytes(sd.n) : (lu ? lu_bytes : kConissGlbLds);
     if (!stamped && prof) kprof_begin(*prof, K_CONISS);
     // global variant: as few block-minimum slots as the size needs (every

@@ -332,6 +332,51 @@ def test_arms_golden(gpu, name, mode):
         assert sub.cluster is sub.clusters        # R's `$cluster` slot on the arm branch
 
 
+@pytest.mark.parametrize("mode", ["bug", "fixed"])
+def test_arms_golden_device_input(gpu, mode):
+    """The same golden arms from a GPU-resident matrix: each arm's pipeline
+    reads its rows and columns from the cleaned whole matrix (TP_FLAG_SUBSET)
+    instead of a copied submatrix."""
+    import torch
+    import tadpole_amd as tp
+    z = np.load(os.path.join(GOLD, "arm_c5layout.npz"))
+    m = synth_hic(int(z["n0"]), int(z["seed"]), centromere=True)
+    got = tp.TADpole(torch.from_numpy(m).cuda(), max_pcs=200, centromere_search=True,
+                     fixed_centromere=(mode == "fixed"))
+    assert np.array_equal(got.merging_arms, z[f"{mode}_merging_arms"])
+    for arm in ("p", "q"):
+        sub = getattr(got, arm)
+        assert np.array_equal(sub.dendro.labels, z[f"{mode}_{arm}_names"].astype(str).tolist())
+        _check(sub, z, f"{mode}_{arm}_", bad=False)
+
+
+@pytest.mark.parametrize("n0,take", [(400, 300), (2600, 2100)])
+def test_subset_pipeline_same_bits(gpu, n0, take):
+    """TP_FLAG_SUBSET on a ragged index list (gaps, both ends dropped) gives
+    the bits of the pipeline on the copied principal submatrix; bad lists
+    (descending, repeated, out of range) are TP_ERR_ARG."""
+    import torch
+    from tadpole_amd import _lib
+    from tadpole_amd.api import _pipeline
+    rng = np.random.default_rng(7)
+    m = synth_hic(n0, SEED_BASE + 91)
+    names = np.sort(rng.choice(np.arange(2, n0), take, replace=False)) + 1     # 1-based, ragged
+    dm = torch.from_numpy(m).cuda()
+    a = _pipeline(dm, 200, 2, 0.0, _lib.TP_FLAG_CLEAN, 0, subset=names)
+    sel = torch.as_tensor(names - 1, device=dm.device)
+    sub = dm.index_select(0, sel).index_select(1, sel).contiguous()
+    b = _pipeline(sub, 200, 2, 0.0, _lib.TP_FLAG_NO_MASK | _lib.TP_FLAG_CLEAN, 0)
+    assert np.array_equal(a["good"], names)
+    assert not a["bad"].any() and a["bad"].size == take
+    for key in ("k", "w", "n_pcs", "n_clusters"):
+        assert a[key] == b[key], key
+    for key in ("n_cluster", "scores", "merge", "height", "boundary"):
+        assert np.array_equal(a[key], b[key], equal_nan=key in ("scores", "height")), key
+    for bad in (names[::-1].copy(), np.r_[names[:5], names[4:10]], np.r_[0, names[1:]], np.r_[names[:-1], n0 + 1]):
+        with pytest.raises(RuntimeError, match="TP_FLAG_SUBSET"):
+            _pipeline(dm, 200, 2, 0.0, _lib.TP_FLAG_CLEAN, 0, subset=bad)
+
+
 def test_arms_bug_mode_errors_like_r(gpu):
     import tadpole_amd as tp
     m = synth_hic(300, 5)
