@@ -67,10 +67,10 @@ enum {
                                    cleaned whole matrix, never copied out      */
 #define TP_FLAG_LDS_LEAN   32   /* tuning hint: another pipeline runs on this
                                    device at the same time; the CONISS sweep of
-                                   a matrix too large for LDS keeps its links in
-                                   global memory (slower alone) so its trees fit
-                                   on CUs beside the other pipeline's.  Results
-                                   are the same bits either way                */
+                                   a matrix too large for LDS keeps half its
+                                   link data there (2 bytes a bin) so a tree of
+                                   each pipeline fits on one CU.  Results are
+                                   the same bits either way                    */
 
 /* ---------------------------------------------------------------- runtime */
 int  tp_version(void);                          /* ABI version, 2 (see below)    */

@@ -746,10 +746,15 @@ def _tadpole_arms(raw, plan, max_pcs, min_clusters, device, shard_flag: int = 0,
         subs = multi.exchange_arms(arm_groups, mine)
     elif _arms_concurrent(raw, shard_flag, stream):
         # both arms start at once (0.305 s for C5 on one MI355X, 0.33 s one
-        # after the other).  The smaller arm's CONISS keeps its links out of
-        # LDS (TP_FLAG_LDS_LEAN, TADPOLE_ARMS_LEAN=0 turns it off): its trees
-        # then fit beside the larger arm's on the same CUs instead of waiting
-        # for them.  TADPOLE_ARMS_Q_AT=s (1..3) holds q back until p's
+        # after the other).  Both arms' CONISS trees keep only their link
+        # array in LDS (TP_FLAG_LDS_LEAN: 48.6 + 43 KB a tree instead of 97 +
+        # 86) so a tree of each arm fits on one CU: c5_full 0.207 -> 0.190 s.
+        # With only the smaller arm lean ("smaller") it was 0.182 or 0.216 s
+        # run to run: a CU's LDS is allocated contiguously, and a lean tree
+        # placed mid-LDS (above a workgroup still resident when it started)
+        # leaves no 97 KB gap for the other arm's full tree, which then waits
+        # for a CU; with both lean any placement leaves a >= 58 KB gap.
+        # TADPOLE_ARMS_LEAN=0 turns it off.  TADPOLE_ARMS_Q_AT=s (1..3) holds q back until p's
         # progress word reaches stage s (2: p's correlation queued, 3: p's
         # sweep): measured slower (0.32-0.34 s at s = 3: q's int8 X'X, 160 KiB
         # of LDS a workgroup, cannot share a CU with p's CONISS trees).
@@ -766,9 +771,12 @@ def _tadpole_arms(raw, plan, max_pcs, min_clusters, device, shard_flag: int = 0,
             _lib.check(st)
         try:
             with ThreadPoolExecutor(max_workers=2) as ex:
-                lean = {"p": 0, "q": 0}
-                if os.environ.get("TADPOLE_ARMS_LEAN", "1") != "0":
-                    lean["q" if len(plan["q"][0]) <= len(plan["p"][0]) else "p"] = _lib.TP_FLAG_LDS_LEAN
+                lmode = os.environ.get("TADPOLE_ARMS_LEAN", "both")
+                lean = {"p": _lib.TP_FLAG_LDS_LEAN, "q": _lib.TP_FLAG_LDS_LEAN}
+                if lmode == "0":
+                    lean = {"p": 0, "q": 0}
+                elif lmode == "smaller":
+                    lean["p" if len(plan["q"][0]) <= len(plan["p"][0]) else "q"] = 0
                 fp = ex.submit(run_arm, "p", sp, lean["p"])
 
                 def run_q():

@@ -258,6 +258,21 @@ template <> struct LinkArr<true> {
     }
     __device__ __forceinline__ void set(int i, int v) const { p[i] = (unsigned short)v; }
 };
+// LU = 2 (link-only): rn is not stored.  rn is only read at a cluster start a
+// (or the dummy slot DL, whose link is -1), where it is the end of the next
+// cluster, link[link[a] + 1] (link[n] = -1 ends the chain), and every rn store
+// restates exactly that value -- half the LDS a tree for one dependent LDS
+// read more on some merge-chain steps
+struct RnDerived {
+    LinkArr<true> link;
+    __device__ __forceinline__ int get(int i) const {
+        const int e = link.get(i);
+        return e < 0 ? -1 : link.get(e + 1);
+    }
+    __device__ __forceinline__ void set(int, int) const {}
+};
+template <int LU> struct RnOf { using T = LinkArr<LU != 0>; };
+template <> struct RnOf<2> { using T = RnDerived; };
 
 // Columns i..ld-1 of a row hold whatever the row was read from (later PCs of
 // Pt, or their sums): the last slot's term is selected to 0 there, which adds
@@ -309,7 +324,7 @@ __device__ __forceinline__ double ward_part(const double (&sa)[NS], double fa, c
 #ifndef TP_CONISS_RECB
 #define TP_CONISS_RECB 1
 #endif
-template <bool STAMPS, int NS, int BS, bool GLB, bool LU = false>
+template <bool STAMPS, int NS, int BS, bool GLB, int LU = 0>
 __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, double *lds, double *mb_d,
                                              int4 *mb_i) {
     long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -337,13 +352,17 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
     const size_t cst = coniss_cost_stride(n), lst = coniss_link_stride(n);
     // LU (with GLB): the links are 16-bit indices in LDS, the costs stay global
     double *cost = GLB ? cost0 + (size_t)ti * cst : lds;
-    LinkArr<LU> link, rn;
-    if constexpr (LU) {
+    LinkArr<LU != 0> link;
+    typename RnOf<LU>::T rn;
+    if constexpr (LU != 0) {
         link.p = (unsigned short *)lds;
     } else {
         link.p = GLB ? (int *)(cost0 + (size_t)sd.ntrees * cst) + (size_t)ti * 2 * lst : (int *)(cost + cst);
     }
-    rn.p = link.p + lst;
+    if constexpr (LU == 2)
+        rn.link = link;
+    else
+        rn.p = link.p + lst;
     // dummy slots: branch-free code writes absent positions there (an exec-
     // masked `if` costs ~55 cycles on the merge chain, a select ~14)
     const int DC = nbk * 64, DL = n;
@@ -776,7 +795,7 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
 // STAMPS: diagnostic build (see coniss_tree2).  BS: block-minimum slots (n <= 4096 BS).
 // LU: the global variant with its links as 16-bit indices in LDS.
 // KS: the most column slots a tree of this launch has (4: k <= 256; 8: k <= 512)
-template <bool STAMPS, int BS, bool GLB, bool LU = false, int KS = 4>
+template <bool STAMPS, int BS, bool GLB, int LU = 0, int KS = 4>
 __global__ void __launch_bounds__(128) k_coniss_t(SweepDev sd, double *cost0) {
     extern __shared__ double lds[];
     __shared__ double mb_d[4];
@@ -1380,7 +1399,7 @@ static bool coniss_in_lds(int n) { return coniss_lds_bytes(n) <= 160 * 1024 - 25
 
 // seed kernel + CONISS (cost0 = initial adjacent costs, ntrees x nbk*64, then
 // the global-variant link scratch: see sweep_cost0_doubles)
-template <bool STAMPS, int BS, bool GLB, bool LU = false>
+template <bool STAMPS, int BS, bool GLB, int LU = 0>
 static void launch_coniss_bs(const SweepDev &sd, double *cost0, size_t lds, hipStream_t s) {
     if (sd.tree0 + sd.ntrees > 512) {   // trees of 9..16 column slots
         if constexpr (!STAMPS) {
@@ -1439,11 +1458,13 @@ static void run_coniss(const SweepDev &sd_in, hipStream_t s, bool stamped, Ctx *
     // global variant: 16-bit links in LDS when they fit (costs stay global)
     const size_t lu_bytes = coniss_link_stride(sd.n) * 4;
     const int bs = (nbk + 63) / 64;   // block-minimum slots per lane
-    // lds_lean (TP_FLAG_LDS_LEAN: another pipeline runs beside this one): the
-    // links stay global too, so these trees fit on CUs whose LDS the other
-    // pipeline's LU trees hold (24.3k bins alone: ~1.4x slower a tree)
-    const bool lu = !in_lds && g_coniss_lu && !sd.lds_lean && sd.n + 64 < 0xFFFF && lu_bytes <= 150 * 1024 && bs <= 11;
-    const size_t lds = in_lds ? coniss_lds_bytes(sd.n) : (lu ? lu_bytes : kConissGlbLds);
+    // lds_lean (TP_FLAG_LDS_LEAN: another pipeline runs beside this one): only
+    // the link array in LDS, rn derived from it (LU = 2, half the bytes), so
+    // these trees fit on CUs whose LDS the other pipeline's trees hold
+    const bool lu_ok = !in_lds && g_coniss_lu && sd.n + 64 < 0xFFFF && bs <= 11;
+    const bool lu2 = lu_ok && sd.lds_lean;
+    const bool lu = lu_ok && !lu2 && lu_bytes <= 150 * 1024;
+    const size_t lds = in_lds ? coniss_lds_bytes(sd.n) : (lu ? lu_bytes : (lu2 ? lu_bytes / 2 : kConissGlbLds));
     if (!stamped && prof) kprof_begin(*prof, K_CONISS);
     // global variant: as few block-minimum slots as the size needs (every
     // per-slot loop of the merge chain -- the untouched minimum, the argmin
@@ -1456,7 +1477,10 @@ static void run_coniss(const SweepDev &sd_in, hipStream_t s, bool stamped, Ctx *
         else if (bs == 2) launch_coniss_bs<true, 2, false>(sd, cost0, lds, s);
         else launch_coniss_bs<true, 3, false>(sd, cost0, lds, s);
     } else {
-        if (lu && bs <= 6) launch_coniss_bs<false, 6, true, true>(sd, cost0, lds, s);
+        if (lu2 && bs <= 6) launch_coniss_bs<false, 6, true, 2>(sd, cost0, lds, s);
+        else if (lu2 && bs <= 8) launch_coniss_bs<false, 8, true, 2>(sd, cost0, lds, s);
+        else if (lu2) launch_coniss_bs<false, 11, true, 2>(sd, cost0, lds, s);
+        else if (lu && bs <= 6) launch_coniss_bs<false, 6, true, true>(sd, cost0, lds, s);
         else if (lu && bs <= 8) launch_coniss_bs<false, 8, true, true>(sd, cost0, lds, s);
         else if (lu) launch_coniss_bs<false, 11, true, true>(sd, cost0, lds, s);
         else if (!in_lds && bs <= 11) launch_coniss_bs<false, 11, true>(sd, cost0, lds, s);

@@ -377,6 +377,22 @@ def test_subset_pipeline_same_bits(gpu, n0, take):
             _pipeline(dm, 200, 2, 0.0, _lib.TP_FLAG_CLEAN, 0, subset=bad)
 
 
+@pytest.mark.parametrize("n", [10500, 16000])
+def test_lds_lean_coniss_same_bits(gpu, n):
+    """TP_FLAG_LDS_LEAN (the smaller centromere arm beside the larger one):
+    CONISS keeps only its link array in LDS and derives each next cluster's
+    end from it; every merge, height and score is the default sweep's."""
+    from tadpole_amd import _lib
+    from tadpole_amd.api import _pipeline
+    m = synth_hic(n, SEED_BASE + 97)
+    a = _pipeline(m, 60, 2, 0.01, 0, 0)
+    b = _pipeline(m, 60, 2, 0.01, _lib.TP_FLAG_LDS_LEAN, 0)
+    for key in ("k", "w", "n_pcs", "n_clusters"):
+        assert a[key] == b[key], key
+    for key in ("good", "n_cluster", "scores", "merge", "height", "boundary"):
+        assert np.array_equal(a[key], b[key], equal_nan=key in ("scores", "height")), key
+
+
 def test_arms_bug_mode_errors_like_r(gpu):
     import tadpole_amd as tp
     m = synth_hic(300, 5)

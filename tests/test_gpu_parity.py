@@ -52,6 +52,22 @@ def test_mask_real_values_nan_and_asymmetric(gpu, frac):
     assert np.array_equal(bad2, obad)
 
 
+@pytest.mark.parametrize("n0", [64, 257, 1000])
+def test_clean_symmetrize_in_place(gpu, n0):
+    """tp_mask_dev's in-place NA -> 0 and forceSymmetric(uplo='U')
+    (R/TADpole.R:19-20) leave exactly the oracle's matrix in the buffer: NaNs on
+    both sides of the diagonal and on it, the lower triangle overwritten."""
+    import torch
+    from tadpole_amd.api import mask_dev
+    rng = np.random.default_rng(n0)
+    m = rng.gamma(2.0, 3.0, (n0, n0))
+    m[rng.random((n0, n0)) < 0.02] = np.nan
+    m[3, 3] = np.nan
+    dm = torch.from_numpy(m).cuda()
+    mask_dev(dm, 0.01)
+    assert np.array_equal(dm.cpu().numpy(), O.clean_symmetrize(m))
+
+
 def test_mask_ties_and_all_equal(gpu):
     m = np.ones((64, 64))
     bad, _, _ = G.mask(m, 0.01)
