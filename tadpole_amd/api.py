@@ -753,8 +753,9 @@ def _tadpole_arms(raw, plan, max_pcs, min_clusters, device, shard_flag: int = 0,
         # run to run: a CU's LDS is allocated contiguously, and a lean tree
         # placed mid-LDS (above a workgroup still resident when it started)
         # leaves no 97 KB gap for the other arm's full tree, which then waits
-        # for a CU; with both lean any placement leaves a >= 58 KB gap.
-        # TADPOLE_ARMS_LEAN=0 turns it off.  TADPOLE_ARMS_Q_AT=s (1..3) holds q back until p's
+        # for a CU; with both lean any placement leaves a >= 58 KB gap.  (The
+        # library also makes a sweep lean by itself while another pipeline is
+        # in flight on the device, knob 47.)  TADPOLE_ARMS_Q_AT=s (1..3) holds q back until p's
         # progress word reaches stage s (2: p's correlation queued, 3: p's
         # sweep): measured slower (0.32-0.34 s at s = 3: q's int8 X'X, 160 KiB
         # of LDS a workgroup, cannot share a CU with p's CONISS trees).
@@ -771,12 +772,7 @@ def _tadpole_arms(raw, plan, max_pcs, min_clusters, device, shard_flag: int = 0,
             _lib.check(st)
         try:
             with ThreadPoolExecutor(max_workers=2) as ex:
-                lmode = os.environ.get("TADPOLE_ARMS_LEAN", "both")
                 lean = {"p": _lib.TP_FLAG_LDS_LEAN, "q": _lib.TP_FLAG_LDS_LEAN}
-                if lmode == "0":
-                    lean = {"p": 0, "q": 0}
-                elif lmode == "smaller":
-                    lean["p" if len(plan["q"][0]) <= len(plan["p"][0]) else "q"] = 0
                 fp = ex.submit(run_arm, "p", sp, lean["p"])
 
                 def run_q():

@@ -508,7 +508,9 @@ static SweepOut run_sweep(Ctx &c, const double *d_Pt, int n, int k, int min_clus
     sd.ldp = k;
     sd.k = k;
     sd.min_clusters = min_clusters;
-    sd.lds_lean = c.lds_lean;
+    // lean: asked for, or another pipeline is in flight on this device now
+    // (concurrent streams: a tree of each fits on one CU; the same bits)
+    sd.lds_lean = c.lds_lean || (g_lean_auto && pipelines_in_flight(c.device) > 1);
     double *sums = c.buf[S_SWEEP].as<double>(sweep_sums_doubles(n, 0, k));
     const size_t rec = (size_t)k * (n - 1);
     char *recbuf = c.buf[S_SWEEP2].as<char>(rec * (4 + 4 + 8 + 8) + 256);
@@ -664,6 +666,10 @@ static SweepOut run_sweep(Ctx &c, const double *d_Pt, int n, int k, int min_clus
 }
 
 // ------------------------------------------------------------ pipeline
+static std::atomic<int> g_in_flight[64];
+int pipelines_in_flight(int device) { return g_in_flight[device & 63].load(); }
+int g_lean_auto = 1;
+
 struct PipeOut {
     int n_good = 0, k = 0;
     SweepOut sw;
@@ -709,6 +715,11 @@ static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_cl
     } shard_scope(c, (flags & TP_FLAG_SHARDED) != 0);
     c.prof = timings != nullptr;
     c.lds_lean = (flags & TP_FLAG_LDS_LEAN) != 0;
+    struct InFlight {   // this device's pipelines in flight (the sweep's lean choice)
+        int d;
+        explicit InFlight(int dev) : d(dev & 63) { g_in_flight[d].fetch_add(1); }
+        ~InFlight() { g_in_flight[d].fetch_sub(1); }
+    } in_flight(c.device);
     c.recs.clear();
     c.evnext = 0;
     // the caller's progress word (tp_progress_attach): 0 started, 1 mask read
@@ -1808,7 +1819,9 @@ extern "C" {
  * sharded waits with a live communicator fail as device errors (failure-containment tests), 31 the
  * bins from which knob 20 = -1 (default) takes the Krylov space of C, ..., 36 the Krylov products with
  * C on the int8 MFMA from digit images (1, default: one LDS buffer, two workgroups a CU; 2: the
- * double-buffered one-workgroup kernel; 0: the fp64 k_gemm_ts). */
+ * double-buffered one-workgroup kernel; 0: the fp64 k_gemm_ts), ..., 47 sweeps lean (CONISS link-only
+ * in LDS) while another pipeline is in flight on the device (1, default), 48 the bins from which a
+ * lean sweep of a matrix that fits LDS takes the global link-only variant (0: never). */
 void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
     guarded(status, [&] {
         if (*which == 41) {   // a counter, not a switch: returns it and sets it to *value
@@ -1862,6 +1875,8 @@ void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
         case 44: p = &g_xtx_w; break;
         case 45: p = &g_pd_cspace; break;
         case 46: p = &g_pd_digits_big; break;
+        case 47: p = &g_lean_auto; break;
+        case 48: p = &g_coniss_lean_min; break;
         default: fail(TP_ERR_ARG, "unknown knob");
         }
         if (*which == 3 && *value != 16 && *value != 32) fail(TP_ERR_ARG, "stage depth must be 16 or 32");

@@ -61,7 +61,7 @@ struct Ctx {
     std::recursive_mutex mu;
     Shard shard;
     bool prof = false;                  // record per-kernel events this call
-    bool lds_lean = false;              // TP_FLAG_LDS_LEAN this call: CONISS links in global memory
+    bool lds_lean = false;              // TP_FLAG_LDS_LEAN this call (or another pipeline in flight on the device)
     std::vector<hipEvent_t> evpool;
     size_t evnext = 0;
     struct Rec { int cls; hipEvent_t a, b; };
@@ -258,6 +258,9 @@ struct SweepDev {
 extern int g_ch_dedup;        // 0: every tree computes its own segment statistics
 extern int g_cor_fused;        // 0: prcomp's column means by a separate pass over C
 extern int g_coniss_lu;       // 0: the global CONISS variant keeps its links in global memory
+extern int g_coniss_lean_min; // lean sweeps of matrices that fit LDS from this many bins take the link-only variant (0: never)
+extern int g_lean_auto;       // 1: a sweep is lean whenever another pipeline is in flight on its device
+int pipelines_in_flight(int device);
 extern int g_ch_dedup_ucap;   // > 0: cap on the shared store (tests of the overflow path)
 size_t sweep_dedup_bytes(int n, int k, int ntrees, int seg_cap, int *hcap, int *ucap);
 void sweep_dedup_bind(SweepDev &sd, void *base, int hcap, int ucap);

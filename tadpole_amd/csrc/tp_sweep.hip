@@ -1424,6 +1424,14 @@ static void launch_coniss_bs(const SweepDev &sd, double *cost0, size_t lds, hipS
     hipLaunchKernelGGL((k_coniss_t<STAMPS, BS, GLB, LU>), dim3(sd.ntrees), dim3(128), lds, s, sd, cost0);
 }
 int g_coniss_lu = 1;   // 0: the global variant keeps its links in global memory too
+// lean sweeps (another pipeline in flight on the device) of matrices that fit
+// LDS, from this many bins (knob 48; 0: never): costs global and only the
+// links in LDS (2 bytes a bin) so several trees share a CU -- the LDS
+// variant's 16 bytes a bin hold a whole CU from ~5k bins while the tree's two
+// waves use two of its SIMDs.  Measured on C4 (8 streams): 0.27-0.29 s at
+// 4096 or 2048 vs 0.26 s off -- the global costs slow each tree more than
+// the sharing gains -- so off
+int g_coniss_lean_min = 0;
 
 static void run_coniss(const SweepDev &sd_in, hipStream_t s, bool stamped, Ctx *prof) {
     SweepDev sd = sd_in;
@@ -1454,7 +1462,8 @@ static void run_coniss(const SweepDev &sd_in, hipStream_t s, bool stamped, Ctx *
     else
         hipLaunchKernelGGL(k_seed<16>, dim3(sd.ntrees, nbk), dim3(64), 0, s, sd, cost0);
     TP_HIP(hipGetLastError());
-    const bool in_lds = coniss_in_lds(sd.n);
+    const bool lean_small = sd.lds_lean && g_coniss_lean_min > 0 && sd.n >= g_coniss_lean_min;
+    const bool in_lds = coniss_in_lds(sd.n) && !lean_small;
     // global variant: 16-bit links in LDS when they fit (costs stay global)
     const size_t lu_bytes = coniss_link_stride(sd.n) * 4;
     const int bs = (nbk + 63) / 64;   // block-minimum slots per lane
@@ -1477,7 +1486,9 @@ static void run_coniss(const SweepDev &sd_in, hipStream_t s, bool stamped, Ctx *
         else if (bs == 2) launch_coniss_bs<true, 2, false>(sd, cost0, lds, s);
         else launch_coniss_bs<true, 3, false>(sd, cost0, lds, s);
     } else {
-        if (lu2 && bs <= 6) launch_coniss_bs<false, 6, true, 2>(sd, cost0, lds, s);
+        if (lu2 && bs <= 2) launch_coniss_bs<false, 2, true, 2>(sd, cost0, lds, s);
+        else if (lu2 && bs <= 3) launch_coniss_bs<false, 3, true, 2>(sd, cost0, lds, s);
+        else if (lu2 && bs <= 6) launch_coniss_bs<false, 6, true, 2>(sd, cost0, lds, s);
         else if (lu2 && bs <= 8) launch_coniss_bs<false, 8, true, 2>(sd, cost0, lds, s);
         else if (lu2) launch_coniss_bs<false, 11, true, 2>(sd, cost0, lds, s);
         else if (lu && bs <= 6) launch_coniss_bs<false, 6, true, true>(sd, cost0, lds, s);

@@ -377,16 +377,21 @@ def test_subset_pipeline_same_bits(gpu, n0, take):
             _pipeline(dm, 200, 2, 0.0, _lib.TP_FLAG_CLEAN, 0, subset=bad)
 
 
-@pytest.mark.parametrize("n", [10500, 16000])
+@pytest.mark.parametrize("n", [2100, 5000, 10500, 16000])
 def test_lds_lean_coniss_same_bits(gpu, n):
-    """TP_FLAG_LDS_LEAN (the smaller centromere arm beside the larger one):
-    CONISS keeps only its link array in LDS and derives each next cluster's
-    end from it; every merge, height and score is the default sweep's."""
+    """TP_FLAG_LDS_LEAN (pipelines sharing a GPU: the C5 arms, run_genome's
+    streams): CONISS keeps only its link array in LDS and derives each next
+    cluster's end from it (from 4096 bins also for matrices whose costs would
+    fit LDS); every merge, height and score is the default sweep's."""
     from tadpole_amd import _lib
     from tadpole_amd.api import _pipeline
     m = synth_hic(n, SEED_BASE + 97)
     a = _pipeline(m, 60, 2, 0.01, 0, 0)
-    b = _pipeline(m, 60, 2, 0.01, _lib.TP_FLAG_LDS_LEAN, 0)
+    old = G.knob(48, 4096)          # the in-LDS sizes' lean variant is opt-in
+    try:
+        b = _pipeline(m, 60, 2, 0.01, _lib.TP_FLAG_LDS_LEAN, 0)
+    finally:
+        G.knob(48, old)
     for key in ("k", "w", "n_pcs", "n_clusters"):
         assert a[key] == b[key], key
     for key in ("good", "n_cluster", "scores", "merge", "height", "boundary"):
