@@ -354,8 +354,8 @@ __device__ __forceinline__ void coniss_tree2(const SweepDev &sd, double *cost0, 
     double *cost = GLB ? cost0 + (size_t)ti * cst : lds;
     LinkArr<LU != 0> link;
     typename RnOf<LU>::T rn;
-    if constexpr (LU != 0) {
-        link.p = (unsigned short *)lds;
+    if constexpr (LU != 0) {   // global variant: LDS holds only links; LDS variant: after the costs
+        link.p = (unsigned short *)(GLB ? lds : lds + cst);
     } else {
         link.p = GLB ? (int *)(cost0 + (size_t)sd.ntrees * cst) + (size_t)ti * 2 * lst : (int *)(cost + cst);
     }
@@ -1396,6 +1396,14 @@ static size_t coniss_lds_bytes(int n) {   // costs, links, right ends (the mailb
 constexpr size_t kConissGlbLds = 16;   // nothing: the mailbox is static LDS
 constexpr int kConissMaxN = 64 * 64 * 32;             // global variant: up to 32 block-minimum slots
 static bool coniss_in_lds(int n) { return coniss_lds_bytes(n) <= 160 * 1024 - 256 && n <= 64 * 64 * 3; }   // 256: static mailbox
+// the LDS variant with one 16-bit link array (LU = 2): 10 bytes a bin instead of 16
+static size_t coniss_lds2_bytes(int n) { return coniss_cost_stride(n) * 8 + coniss_link_stride(n) * 2; }
+static bool coniss_in_lds2(int n) { return coniss_lds2_bytes(n) <= 160 * 1024 - 256 && n <= 64 * 64 * 3; }
+// knob 49: the LDS variant link-only -- 3 (default): where the 16-byte variant
+// does not fit (~10.2k-12.3k bins; 11 000 bins: sweep 21.5 -> 18.8 ms against the
+// global variant), 2: every sweep, 1: lean sweeps, 0: never.  Not below: at C3
+// the extra dependent LDS read on the merge chain costs 10.9 -> 12.8 ms
+int g_coniss_lds2 = 3;
 
 // seed kernel + CONISS (cost0 = initial adjacent costs, ntrees x nbk*64, then
 // the global-variant link scratch: see sweep_cost0_doubles)
@@ -1463,7 +1471,10 @@ static void run_coniss(const SweepDev &sd_in, hipStream_t s, bool stamped, Ctx *
         hipLaunchKernelGGL(k_seed<16>, dim3(sd.ntrees, nbk), dim3(64), 0, s, sd, cost0);
     TP_HIP(hipGetLastError());
     const bool lean_small = sd.lds_lean && g_coniss_lean_min > 0 && sd.n >= g_coniss_lean_min;
-    const bool in_lds = coniss_in_lds(sd.n) && !lean_small;
+    const bool in_lds2 = !lean_small && coniss_in_lds2(sd.n) &&
+                         (g_coniss_lds2 == 2 || (g_coniss_lds2 == 1 && sd.lds_lean) ||
+                          (g_coniss_lds2 == 3 && !coniss_in_lds(sd.n)));
+    const bool in_lds = (coniss_in_lds(sd.n) || in_lds2) && !lean_small;
     // global variant: 16-bit links in LDS when they fit (costs stay global)
     const size_t lu_bytes = coniss_link_stride(sd.n) * 4;
     const int bs = (nbk + 63) / 64;   // block-minimum slots per lane
@@ -1473,7 +1484,8 @@ static void run_coniss(const SweepDev &sd_in, hipStream_t s, bool stamped, Ctx *
     const bool lu_ok = !in_lds && g_coniss_lu && sd.n + 64 < 0xFFFF && bs <= 11;
     const bool lu2 = lu_ok && sd.lds_lean;
     const bool lu = lu_ok && !lu2 && lu_bytes <= 150 * 1024;
-    const size_t lds = in_lds ? coniss_lds_bytes(sd.n) : (lu ? lu_bytes : (lu2 ? lu_bytes / 2 : kConissGlbLds));
+    const size_t lds = in_lds2 ? coniss_lds2_bytes(sd.n)
+                               : (in_lds ? coniss_lds_bytes(sd.n) : (lu ? lu_bytes : (lu2 ? lu_bytes / 2 : kConissGlbLds)));
     if (!stamped && prof) kprof_begin(*prof, K_CONISS);
     // global variant: as few block-minimum slots as the size needs (every
     // per-slot loop of the merge chain -- the untouched minimum, the argmin
@@ -1486,7 +1498,10 @@ static void run_coniss(const SweepDev &sd_in, hipStream_t s, bool stamped, Ctx *
         else if (bs == 2) launch_coniss_bs<true, 2, false>(sd, cost0, lds, s);
         else launch_coniss_bs<true, 3, false>(sd, cost0, lds, s);
     } else {
-        if (lu2 && bs <= 2) launch_coniss_bs<false, 2, true, 2>(sd, cost0, lds, s);
+        if (in_lds2 && bs == 1) launch_coniss_bs<false, 1, false, 2>(sd, cost0, lds, s);
+        else if (in_lds2 && bs == 2) launch_coniss_bs<false, 2, false, 2>(sd, cost0, lds, s);
+        else if (in_lds2) launch_coniss_bs<false, 3, false, 2>(sd, cost0, lds, s);
+        else if (lu2 && bs <= 2) launch_coniss_bs<false, 2, true, 2>(sd, cost0, lds, s);
         else if (lu2 && bs <= 3) launch_coniss_bs<false, 3, true, 2>(sd, cost0, lds, s);
         else if (lu2 && bs <= 6) launch_coniss_bs<false, 6, true, 2>(sd, cost0, lds, s);
         else if (lu2 && bs <= 8) launch_coniss_bs<false, 8, true, 2>(sd, cost0, lds, s);

@@ -398,6 +398,31 @@ def test_lds_lean_coniss_same_bits(gpu, n):
         assert np.array_equal(a[key], b[key], equal_nan=key in ("scores", "height")), key
 
 
+@pytest.mark.parametrize("n", [700, 2100, 7808, 11000])
+def test_lds_link_only_coniss_same_bits(gpu, n):
+    """Knob 49: the LDS variant keeps one 16-bit link array after the costs (10
+    bytes a bin instead of 16; by default only where the 16-byte variant does not
+    fit, so 11 000 bins fit LDS instead of taking the global variant).  Every
+    size on it (2) against the 16-byte and global variants (0): same merges,
+    heights and scores."""
+    from tadpole_amd.api import _pipeline
+    m = synth_hic(n, SEED_BASE + 98)
+    old = G.knob(49, 0)
+    try:
+        a = _pipeline(m, 60, 2, 0.01, 0, 0)
+    finally:
+        G.knob(49, old)
+    old = G.knob(49, 2)
+    try:
+        b = _pipeline(m, 60, 2, 0.01, 0, 0)
+    finally:
+        G.knob(49, old)
+    for key in ("k", "w", "n_pcs", "n_clusters"):
+        assert a[key] == b[key], key
+    for key in ("good", "n_cluster", "scores", "merge", "height", "boundary"):
+        assert np.array_equal(a[key], b[key], equal_nan=key in ("scores", "height")), key
+
+
 def test_arms_bug_mode_errors_like_r(gpu):
     import tadpole_amd as tp
     m = synth_hic(300, 5)
