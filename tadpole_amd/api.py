@@ -658,11 +658,14 @@ _ARM_STREAMS: Dict[int, tuple] = {}
 
 def _arm_streams(device: int):
     """Two persistent HIP streams per device for the concurrent arms (the
-    library keeps one context per stream: reusing them reuses its scratch)."""
+    library keeps one context per stream: reusing them reuses its scratch):
+    (high priority, normal) -- the larger arm takes the first (see
+    _tadpole_arms); TADPOLE_ARMS_PRIO=0 makes both normal."""
     s = _ARM_STREAMS.get(device)
     if s is None:
         import torch
-        s = _ARM_STREAMS[device] = (torch.cuda.Stream(device=f"cuda:{device}"),
+        hi = -1 if os.environ.get("TADPOLE_ARMS_PRIO", "1") != "0" else 0
+        s = _ARM_STREAMS[device] = (torch.cuda.Stream(device=f"cuda:{device}", priority=hi),
                                     torch.cuda.Stream(device=f"cuda:{device}"))
     return s
 
@@ -761,7 +764,10 @@ def _tadpole_arms(raw, plan, max_pcs, min_clusters, device, shard_flag: int = 0,
         # of LDS a workgroup, cannot share a CU with p's CONISS trees).
         import time
         from concurrent.futures import ThreadPoolExecutor
-        sp, sq = _arm_streams(device)
+        # the larger arm's sweep ends last: its stream goes first when both
+        # arms' correlation and PCA kernels compete for the CUs
+        s_hi, s_lo = _arm_streams(device)
+        sp, sq = (s_hi, s_lo) if len(plan["p"][0]) >= len(plan["q"][0]) else (s_lo, s_hi)
         q_at = int(os.environ.get("TADPOLE_ARMS_Q_AT", "0"))
         L = _lib.load() if q_at > 0 else None
         prog = np.zeros(1, np.int32)
