@@ -1823,7 +1823,8 @@ extern "C" {
  * in LDS) while another pipeline is in flight on the device (1, default), 48 the bins from which a
  * lean sweep of a matrix that fits LDS takes the global link-only variant (0: never), 49 the LDS
  * variant with one 16-bit link array, 10 bytes a bin (3, default: where the 16-byte one does not fit;
- * 1: lean sweeps, 2: every sweep, 0: never). */
+ * 1: lean sweeps, 2: every sweep, 0: never), 50 the NA -> 0 / symmetrise pass's tile edge (0, default: 128 from 16 384 bins, else 64;
+ * 64 or 128 force one). */
 void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
     guarded(status, [&] {
         if (*which == 41) {   // a counter, not a switch: returns it and sets it to *value
@@ -1880,6 +1881,7 @@ void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
         case 47: p = &g_lean_auto; break;
         case 48: p = &g_coniss_lean_min; break;
         case 49: p = &g_coniss_lds2; break;
+        case 50: p = &g_clean_tile; break;
         default: fail(TP_ERR_ARG, "unknown knob");
         }
         if (*which == 3 && *value != 16 && *value != 32) fail(TP_ERR_ARG, "stage depth must be 16 or 32");

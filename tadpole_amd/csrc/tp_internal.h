@@ -261,6 +261,7 @@ extern int g_coniss_lu;       // 0: the global CONISS variant keeps its links in
 extern int g_coniss_lean_min; // lean sweeps of matrices that fit LDS from this many bins take the link-only variant (0: never)
 extern int g_lean_auto;       // 1: a sweep is lean whenever another pipeline is in flight on its device
 extern int g_coniss_lds2;     // the LDS variant with one 16-bit link array (1: lean sweeps, 2: every sweep)
+extern int g_clean_tile;      // k_clean_symmetrize tile edge (0: by size, 64 or 128)
 int pipelines_in_flight(int device);
 extern int g_ch_dedup_ucap;   // > 0: cap on the shared store (tests of the overflow path)
 size_t sweep_dedup_bytes(int n, int k, int ntrees, int seg_cap, int *hcap, int *ucap);

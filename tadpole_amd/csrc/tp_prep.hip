@@ -14,8 +14,13 @@ namespace tp {
 // source tile is read once, its mirror written whole, and the source itself
 // written back only where it held a NaN (was: rewritten whole, 30 of the 20
 // necessary GB at the 49 851-bin C5 matrix, 9.2 ms).
-__global__ void __launch_bounds__(256) k_clean_symmetrize(double *M, int n0, int nb, bool src_upper) {
-    __shared__ double t[64][65];
+// T x T tiles, T * T / 16 threads (16 elements each): T = 64 (256 threads, 33 KB
+// of LDS) or 128 (1024 threads, 132 KB: 1 KB contiguous runs on both the read
+// and the mirrored write instead of 512 B)
+template <int T>
+__global__ void __launch_bounds__(T * T / 16) k_clean_symmetrize(double *M, int n0, int nb, bool src_upper) {
+    constexpr int NT = T / 16;   // rows of threads
+    __shared__ double t[T][T + 1];
     // linear block id -> (bi <= bj): row bi starts at S(bi) = bi nb - bi (bi - 1) / 2
     // (closed form, then an exact integer fix-up; was a loop over up to nb rows)
     const long long id = blockIdx.x;
@@ -26,28 +31,28 @@ __global__ void __launch_bounds__(256) k_clean_symmetrize(double *M, int n0, int
     while (bi > 0 && row_start(bi) > id) --bi;
     while (bi + 1 < nb && row_start(bi + 1) <= id) ++bi;
     const int bj = bi + (int)(id - row_start(bi));
-    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    const int tx = threadIdx.x % T, ty = threadIdx.x / T;
     // source tile rows/cols (buffer coordinates)
-    int sr0 = src_upper ? bi * 64 : bj * 64;
-    int sc0 = src_upper ? bj * 64 : bi * 64;
-    unsigned nanm = 0;   // bit y / 4: this thread's element (tx, y) was NaN
+    int sr0 = src_upper ? bi * T : bj * T;
+    int sc0 = src_upper ? bj * T : bi * T;
+    unsigned nanm = 0;   // bit u: this thread's element (tx, ty + NT u) was NaN
     double v[16];
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
-        const int r = sr0 + tx, c = sc0 + ty + 4 * u;
+        const int r = sr0 + tx, c = sc0 + ty + NT * u;
         v[u] = (r < n0 && c < n0) ? M[(size_t)r + (size_t)c * n0] : 0.0;
     }
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
         const bool bad = isnan(v[u]);
         nanm |= bad ? 1u << u : 0u;
-        t[tx][ty + 4 * u] = bad ? 0.0 : v[u];
+        t[tx][ty + NT * u] = bad ? 0.0 : v[u];
     }
     __syncthreads();
     if (bi != bj) {
 #pragma unroll
         for (int u = 0; u < 16; ++u) {
-            const int y = ty + 4 * u;
+            const int y = ty + NT * u;
             int r = sr0 + tx, c = sc0 + y;
             if ((nanm >> u & 1u) && r < n0 && c < n0) M[(size_t)r + (size_t)c * n0] = 0.0;
             // mirrored tile: B(sc0 + tx, sr0 + y) = t[y][tx]
@@ -57,7 +62,7 @@ __global__ void __launch_bounds__(256) k_clean_symmetrize(double *M, int n0, int
     } else {
 #pragma unroll
         for (int u = 0; u < 16; ++u) {
-            const int y = ty + 4 * u;
+            const int y = ty + NT * u;
             int r = sr0 + tx, c = sc0 + y;
             bool from_here = src_upper ? (tx <= y) : (tx >= y);
             if (r < n0 && c < n0 && (!from_here || (nanm >> u & 1u)))
@@ -66,10 +71,21 @@ __global__ void __launch_bounds__(256) k_clean_symmetrize(double *M, int n0, int
     }
 }
 
+// knob 50: k_clean_symmetrize tile edge -- 0 (default): 128 from 16 384 bins
+// (49 851: 6.18 -> 5.36 ms), 64 below (7 808, Infinity-Cache resident: 93 vs
+// 100 us); 64 / 128 force one
+int g_clean_tile = 0;
+
 void launch_clean_symmetrize(double *d_M, int n0, bool src_upper, hipStream_t s) {
-    int nb = (n0 + 63) / 64;
-    long nblk = (long)nb * (nb + 1) / 2;
-    hipLaunchKernelGGL(k_clean_symmetrize, dim3((unsigned)nblk), dim3(256), 0, s, d_M, n0, nb, src_upper);
+    if (g_clean_tile == 128 || (g_clean_tile == 0 && n0 >= 16384)) {
+        int nb = (n0 + 127) / 128;
+        long nblk = (long)nb * (nb + 1) / 2;
+        hipLaunchKernelGGL(k_clean_symmetrize<128>, dim3((unsigned)nblk), dim3(1024), 0, s, d_M, n0, nb, src_upper);
+    } else {
+        int nb = (n0 + 63) / 64;
+        long nblk = (long)nb * (nb + 1) / 2;
+        hipLaunchKernelGGL(k_clean_symmetrize<64>, dim3((unsigned)nblk), dim3(256), 0, s, d_M, n0, nb, src_upper);
+    }
     TP_HIP(hipGetLastError());
 }
 

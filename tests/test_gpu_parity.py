@@ -52,8 +52,9 @@ def test_mask_real_values_nan_and_asymmetric(gpu, frac):
     assert np.array_equal(bad2, obad)
 
 
+@pytest.mark.parametrize("tile", [64, 128])
 @pytest.mark.parametrize("n0", [64, 257, 1000])
-def test_clean_symmetrize_in_place(gpu, n0):
+def test_clean_symmetrize_in_place(gpu, n0, tile):
     """tp_mask_dev's in-place NA -> 0 and forceSymmetric(uplo='U')
     (R/TADpole.R:19-20) leave exactly the oracle's matrix in the buffer: NaNs on
     both sides of the diagonal and on it, the lower triangle overwritten."""
@@ -64,7 +65,11 @@ def test_clean_symmetrize_in_place(gpu, n0):
     m[rng.random((n0, n0)) < 0.02] = np.nan
     m[3, 3] = np.nan
     dm = torch.from_numpy(m).cuda()
-    mask_dev(dm, 0.01)
+    old = G.knob(50, tile)
+    try:
+        mask_dev(dm, 0.01)
+    finally:
+        G.knob(50, old)
     assert np.array_equal(dm.cpu().numpy(), O.clean_symmetrize(m))
 
 
