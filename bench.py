@@ -61,6 +61,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
 FP64_MFMA_PEAK_TFLOPS = 78.6     # MI355X FP64 matrix, dense (AMD spec)
+FP32_MFMA_PEAK_TFLOPS = 157.3    # MI355X FP32 matrix, dense (MI355X_MICROARCH.md: 155 TF measured)
 INT8_MFMA_PEAK_TOPS = 5000.0     # MI355X I8 MFMA, dense: 2x the BF16 rate per clock (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0            # MI355X HBM3E (MI355X_MICROARCH.md)
 METRIC = "bins/sec (NxN matrix) at 1/2/4/8 GPUs; TAD boundary bit-match vs R ref"
@@ -252,6 +253,66 @@ def run_c5_arm(device, max_pcs, reps):
     if os.path.exists(gold) and max_pcs == 200:
         ok, rel = _golden_check(res, np.load(gold))
         out["parity"] = {"golden_fixture": "tests/golden/c5arm.npz", "match": ok, "ch_max_rel_err": rel}
+    return out
+
+
+def pipeline_roofline(n, k, ms):
+    """SURVEY.md §8(d)'s whole-pipeline roofline time of one n-bin, k-PC
+    pipeline, T_roof = (N^3 + 2 N^2 k) / P_mfma + (3 * 8 N^2 + 4 N k^2 + 3000 * 8 N k)
+    / BW_hbm, against the fp32 and the fp64 MFMA peaks (north_star asks for
+    the fp32 one) and 8 TB/s of HBM, and the measured ms_per_step's fraction of
+    it (T_roof / T_measured: 1.0 = at the roofline)."""
+    flops = float(n) ** 3 + 2.0 * float(n) ** 2 * k
+    bytes_ = 3 * 8.0 * float(n) ** 2 + 4.0 * n * k * k + 3000 * 8.0 * n * k
+    t_hbm = bytes_ / (HBM_PEAK_GBS * 1e9) * 1e3
+    out = {"formula": "T_roof = (N^3 + 2N^2k)/P_mfma + (3*8N^2 + 4Nk^2 + 3000*8Nk)/BW_hbm (SURVEY.md §8(d))",
+           "n": n, "k": k, "flops": flops, "hbm_bytes": bytes_, "hbm_ms": round(t_hbm, 4)}
+    for name, peak in (("fp32_mfma", FP32_MFMA_PEAK_TFLOPS), ("fp64_mfma", FP64_MFMA_PEAK_TFLOPS)):
+        t = flops / (peak * 1e12) * 1e3 + t_hbm
+        out[name] = {"peak_tflops": peak, "t_roof_ms": round(t, 4),
+                     "frac_of_roofline": round(t / ms, 4) if ms > 0 else None}
+    return out
+
+
+def run_c2(device, max_pcs, steps, warmup):
+    """BASELINE.json configs[1], C2: one synthetic 2000 x 2000 Hi-C matrix
+    (synth_hic, seed 20261015+2, the input of tests/golden/c2.npz) resident in
+    HBM, pipelines one after another on one stream, TADpole()'s whole call with
+    the host assembly; stage times from the library's events; parity against
+    the golden fixture; the whole-pipeline roofline fraction."""
+    import torch
+    from tadpole_amd.api import TADpole
+    from tadpole_amd.synth import SEED_BASE, synth_hic
+    n0 = 2000
+    dm = torch.from_numpy(synth_hic(n0, SEED_BASE + 2)).to(f"cuda:{device}")
+    for _ in range(max(1, warmup)):
+        TADpole(dm, max_pcs=max_pcs, inplace=True)   # symmetric, NaN-free: cleaning in place is idempotent
+    ts, tms, res = [], [], None
+    torch.cuda.synchronize()
+    for _ in range(max(1, steps)):
+        t0 = time.perf_counter()
+        res = TADpole(dm, max_pcs=max_pcs, inplace=True)
+        ts.append(time.perf_counter() - t0)
+        tms.append(res.timings_ms)
+    torch.cuda.synchronize()
+    del dm
+    tm = np.mean(np.stack(tms), axis=0)
+    ms = float(np.sum(ts)) / len(ts) * 1e3
+    n, k = int(tm[14]), int(tm[15])
+    out = {"n0": n0, "n_good": n, "k": k, "steps": len(ts), "ms_per_step": round(ms, 3),
+           "ms_median": round(float(np.median(ts)) * 1e3, 3), "bins_per_s": round(n0 / (ms * 1e-3), 1),
+           "stages_ms": _stages(tm), "coniss_ms": round(float(tm[9]), 3), "ch_ms": round(float(tm[10]), 3),
+           "pca": {"path": "block Krylov" if int(tm[16]) else "G = Xc'Xc + subspace iteration",
+                   "chebyshev_degrees": int(tm[11]), "block": int(tm[12]), "resid": float(tm[13])},
+           "pipeline_roofline": pipeline_roofline(n, k, ms),
+           "workload": "C2 (BASELINE configs[1]): synthetic 2000x2000 Hi-C (synth_hic, seed 20261015+2), "
+                       "max_pcs=%d, one GPU, resident in HBM, TADpole() incl. host assembly" % max_pcs}
+    gold = os.path.join(HERE, "tests", "golden", "c2.npz")
+    if os.path.exists(gold) and max_pcs == 200:
+        z = np.load(gold)
+        ok, rel = _golden_check(res, z)
+        ok = ok and np.array_equal(res.dendro.merge, z["merge"])
+        out["parity"] = {"golden_fixture": "tests/golden/c2.npz", "match": bool(ok), "ch_max_rel_err": rel}
     return out
 
 
@@ -657,6 +718,13 @@ def main():
     torch.cuda.synchronize()
     tm[7], tm[8] = tmf[7], tmf[8]
     n, k = int(tm[14]), int(tm[15])
+    # the int8 MACs the last whole-triangle X'X executed (its high slice runs only
+    # on the k-blocks the block-nonzero map lists): read back after the timing
+    xexec = np.zeros(5)
+    st_x = I(0)
+    L.tp_debug_xtx_exec(ctypes.byref(I(local)), ctypes.c_void_p(lane0.stream.cuda_stream), _lib.dp(xexec),
+                        ctypes.byref(st_x))
+    _lib.check(st_x)
     nh = max(1, host_call["n"])
     host_ms = {"c_call": round(host_call["call"] / nh * 1e3, 3), "device_stages": round(float(tm[4]), 3),
                "c_call_minus_device": round(host_call["call"] / nh * 1e3 - float(tm[4]), 3),
@@ -706,6 +774,7 @@ def main():
     extras = {}
     if not args.no_extras and not args.sharded:
         if world == 1:
+            extras["c2"] = run_c2(local, args.max_pcs, max(5, args.steps), 2)
             extras["e2e_10k"] = run_e2e_tsv(10000, args.max_pcs, args.extras_reps)
             extras["c5_arm"] = run_c5_arm(local, args.max_pcs, args.extras_reps)
         c4 = run_c4_genome(world, rank, args.max_pcs, args.extras_reps)
@@ -735,8 +804,11 @@ def main():
         ns = int(tm[18])   # int8 slices of the exact X'X (0: fp64 product)
         pairs = int(tm[19])   # int8 digit pairs of each product with C (0: fp64 products)
         kern = {   # class: (ms per pipeline, bound, launches per pipeline, algorithmic work per launch, peak)
-            # X'X: ns^2 slice products of N^3 int8 ops each (upper tiles: N^2/2 outputs x N MACs x 2)
-            "xtx_gemm": ((tm[5], "mfma", 1, share * ns * ns * float(n) ** 3, INT8_MFMA_PEAK_TOPS) if ns else
+            # X'X on the int8 MFMA: the int8 ops the kernel executed (2 x MACs: slice 0 over every
+            # upper 256 x 128 tile and k-block, the three high-slice products on the k-blocks the
+            # map lists; tp_debug_xtx_exec); the dense-equivalent ns^2 N^3 figure is a labelled extra
+            "xtx_gemm": ((tm[5], "mfma", 1, share * 2.0 * xexec[0] if xexec[0] > 0 else share * ns * ns * float(n) ** 3,
+                          INT8_MFMA_PEAK_TOPS) if ns else
                          (tm[5], "mfma", 1, share * float(n) ** 3, FP64_MFMA_PEAK_TFLOPS)),
             "xcxc_gemm": (tm[6], "mfma", 1, share * float(n) ** 3, FP64_MFMA_PEAK_TFLOPS),
             # products with C on the int8 MFMA: `pairs` digit products of 2 N^2 p int8 ops each
@@ -772,9 +844,17 @@ def main():
                 "xtx": {"int8_slices": ns,
                         "fp64_equivalent_tflops": (round(share * float(n) ** 3 / (tm[5] * 1e-3) / 1e12, 2)
                                                    if tm[5] > 0 else None),
-                        "note": ("xtx_gemm counts the ns^2 slice products whole (dense-equivalent int8 ops); "
-                                 "the kernel skips the high slice's all-zero 128x64 blocks (raw counts >= 128 "
-                                 "sit near the diagonal), so it executes fewer") if ns == 2 else None},
+                        "executed_int8_macs": xexec[0] if xexec[0] > 0 else None,
+                        "slice0_macs": xexec[1] if xexec[0] > 0 else None,
+                        "high_slice_blocks_executed": int(xexec[2]) if xexec[0] > 0 else None,
+                        "high_slice_blocks_dense": int(xexec[3] * xexec[4]) if xexec[0] > 0 else None,
+                        "dense_equivalent_tops": (round(share * ns * ns * float(n) ** 3 / (tm[5] * 1e-3) / 1e12, 2)
+                                                  if tm[5] > 0 and ns else None),
+                        "note": ("xtx_gemm.achieved counts the int8 ops k_xtx_i8_w executed (2 x MACs over its "
+                                 "256x128 upper tiles: slice 0 on every 64-deep k-block, the three high-slice "
+                                 "products only on the blocks the nonzero map lists); dense_equivalent_tops "
+                                 "counts all ns^2 slice products whole (a labelled extra, not the roofline)")
+                        if ns == 2 else None},
                 "gq": {"int8_digit_pairs": pairs,
                        "fp64_equivalent_tflops": (round(gq_flops * gq_launches / (tm[7] * 1e-3) / 1e12, 2)
                                                   if tm[7] > 0 else None),
@@ -799,7 +879,10 @@ def main():
                "dtype_detail": ("f64 results; X'X of integer counts exact on the int8 MFMA (7-bit slices, "
                                 "int32 accumulation, one rounding); the G-space Krylov products with C on the "
                                 "int8 MFMA from base-256 digit images (6 digits of C, 7 of each block, 27 digit "
-                                "pairs, within ~1e-15 of sum |A||B|); everything else fp64 VALU / MFMA"),
+                                "pairs, within ~1e-15 of sum |A||B|), and from 10 000 bins (the c5 lines) the "
+                                "C-space Krylov products of 32 columns on the same 6-digit image of C (not "
+                                "bit-equal to the fp64 products: heights within 1e-9, same TADs); everything "
+                                "else fp64 VALU / MFMA"),
                "data": "synthetic (SURVEY.md §8(d) Hi-C generator, seed 20261015+%d" % cfg +
                        ("" if args.sharded else "+1000*rank") + ")",
                "ranks_seen": len(seen), "devices_seen": sorted({d for _, d in seen}),
@@ -809,7 +892,8 @@ def main():
                           "n0": n0, "n_good": n, "k": k, "max_pcs": args.max_pcs,
                           "parallelism": (f"one matrix over {world} GPU(s): column/row-split products, "
                                           "RCCL all-gather" if args.sharded else f"one matrix per GPU x{world}")},
-               "roofline": roof, "host_ms_per_step": host_ms}
+               "roofline": roof, "host_ms_per_step": host_ms,
+               "pipeline_roofline": pipeline_roofline(n, k, elapsed / args.steps * 1e3)}
         if comm_size is not None:
             out["rccl_comm_size"] = comm_size
         if thr:

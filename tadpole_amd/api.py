@@ -745,8 +745,14 @@ def _tadpole_arms(raw, plan, max_pcs, min_clusters, device, shard_flag: int = 0,
 
     if arm_groups is not None:
         from . import multi
-        mine = run_arm(arm_groups.arm, stream)
-        subs = multi.exchange_arms(arm_groups, mine)
+        # a failing arm (a data error, or a communicator abort) must not leave
+        # the other group blocked in the result exchange: the status goes to
+        # every rank first and all of them raise together
+        try:
+            mine, err = run_arm(arm_groups.arm, stream), None
+        except Exception as e:   # noqa: BLE001 -- re-raised by exchange_arms on every rank
+            mine, err = None, e
+        subs = multi.exchange_arms(arm_groups, mine, err)
     elif _arms_concurrent(raw, shard_flag, stream):
         # both arms start at once (0.305 s for C5 on one MI355X, 0.33 s one
         # after the other).  Both arms' CONISS trees keep only their link

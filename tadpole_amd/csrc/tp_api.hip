@@ -55,12 +55,63 @@ std::atomic<int> g_devbuf_grows{0};   // knob 41 (read / reset): scratch regrowt
 // genome run (C4: ~35 regrowths a run while contexts meet larger chromosomes)
 int g_devbuf_async = 1;
 
+// The library's own stream-ordered pool per device (hipMemPoolCreate): scratch
+// regrowth frees into it and takes from it without a device sync, and it keeps
+// what is freed for reuse (release threshold: unlimited) -- but only this
+// library's blocks: the device's default pool, which torch and other
+// hipMallocAsync users share, is left as it was.  Retiring a context trims the
+// pool (hipMemPoolTrimTo), so freed scratch goes back to the device.
+static hipMemPool_t g_pool[64];
+static std::mutex g_pool_mu;
+static hipMemPool_t lib_pool(int device) {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    if (device < 0 || device >= 64) return nullptr;
+    if (!g_pool[device]) {
+        hipMemPoolProps pp;
+        memset(&pp, 0, sizeof pp);
+        pp.allocType = hipMemAllocationTypePinned;
+        pp.handleTypes = hipMemHandleTypeNone;
+        pp.location.type = hipMemLocationTypeDevice;
+        pp.location.id = device;
+        hipMemPool_t pool = nullptr;
+        if (hipMemPoolCreate(&pool, &pp) != hipSuccess) return nullptr;
+        uint64_t keep = UINT64_MAX;
+        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+        g_pool[device] = pool;
+    }
+    return g_pool[device];
+}
+// give the pool's unused blocks back to the device (after a context's scratch went)
+static void lib_pool_trim(int device) {
+    hipMemPool_t pool = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        if (device >= 0 && device < 64) pool = g_pool[device];
+    }
+    if (pool) (void)hipMemPoolTrimTo(pool, 0);
+}
+
+// knob 51 (test hook): the next N scratch allocations fail as out-of-memory
+// (after the old block is gone, where a real hipMalloc failure would strike)
+int g_devbuf_fail_inject = 0;
+static void devbuf_inject_failure() {
+    if (g_devbuf_fail_inject > 0) {
+        --g_devbuf_fail_inject;
+        fail(TP_ERR_HIP, "scratch allocation failed (injected out-of-memory, knob 51)");
+    }
+}
+
 void *DevBuf::get(size_t b) {
     if (b == 0) b = 8;
     if (b > bytes) {
         if (p) g_devbuf_grows.fetch_add(1, std::memory_order_relaxed);
         const size_t nb = std::max(b, bytes + bytes / 4);
-        if (g_devbuf_async && owner && owner->cur) {
+        hipMemPool_t pool = (g_devbuf_async && owner && owner->cur) ? lib_pool(owner->device) : nullptr;
+        // the old block goes first; bytes / pooled describe what p holds at every
+        // point, so a failed allocation below leaves an empty buffer (p null,
+        // bytes 0) that the next get() allocates again -- never a null block that
+        // claims a size
+        if (pool) {
             hipStream_t s = owner->cur;
             if (p) {
                 // the old block's readers: this context's stream and its side
@@ -69,26 +120,43 @@ void *DevBuf::get(size_t b) {
                     TP_HIP(hipEventRecord(owner->join_ev, owner->side));
                     TP_HIP(hipStreamWaitEvent(s, owner->join_ev, 0));
                 }
-                if (pooled) {
-                    TP_HIP(hipFreeAsync(p, s));
+                void *old = p;
+                const bool was_pooled = pooled;
+                p = nullptr;
+                bytes = 0;
+                pooled = false;
+                if (was_pooled) {
+                    TP_HIP(hipFreeAsync(old, s));
                 } else {
                     TP_HIP(hipDeviceSynchronize());
-                    TP_HIP(hipFree(p));
+                    TP_HIP(hipFree(old));
                 }
-                p = nullptr;
             }
-            TP_HIP(hipMallocAsync(&p, nb, s));
+            void *np = nullptr;
+            devbuf_inject_failure();
+            TP_HIP(hipMallocFromPoolAsync(&np, nb, pool, s));
+            p = np;
             pooled = true;
         } else {
             // work queued on any stream may still read the old block
-            if (p) TP_HIP(hipDeviceSynchronize());
             if (p) {
-                if (pooled) TP_HIP(hipFreeAsync(p, nullptr));
-                else TP_HIP(hipFree(p));
-                if (pooled) TP_HIP(hipDeviceSynchronize());
+                TP_HIP(hipDeviceSynchronize());
+                void *old = p;
+                const bool was_pooled = pooled;
+                p = nullptr;
+                bytes = 0;
+                pooled = false;
+                if (was_pooled) {
+                    TP_HIP(hipFreeAsync(old, nullptr));
+                    TP_HIP(hipDeviceSynchronize());
+                } else {
+                    TP_HIP(hipFree(old));
+                }
             }
-            p = nullptr;
-            TP_HIP(hipMalloc(&p, nb));
+            void *np = nullptr;
+            devbuf_inject_failure();
+            TP_HIP(hipMalloc(&np, nb));
+            p = np;
             pooled = false;
         }
         bytes = nb;
@@ -351,6 +419,7 @@ Ctx::~Ctx() {
     for (auto e : ring_ev)
         if (e) (void)hipEventDestroy(e);
     if (owns_stream) (void)hipStreamDestroy(stream);
+    lib_pool_trim(device);   // the freed scratch goes back to the device
 }
 
 void ctx_shutdown_all() {
@@ -1882,6 +1951,7 @@ void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
         case 48: p = &g_coniss_lean_min; break;
         case 49: p = &g_coniss_lds2; break;
         case 50: p = &g_clean_tile; break;
+        case 51: p = &g_devbuf_fail_inject; break;
         default: fail(TP_ERR_ARG, "unknown knob");
         }
         if (*which == 3 && *value != 16 && *value != 32) fail(TP_ERR_ARG, "stage depth must be 16 or 32");
@@ -1889,6 +1959,19 @@ void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
             fail(TP_ERR_ARG, "Krylov block must be 0 or a multiple of 16 up to 256");
         *old = *p;
         *p = *value;
+    });
+}
+
+/* The int8 MACs the last whole-triangle X'X (k_xtx_i8_w) of this stream's
+ * context executed (out[0]), its slice-0 MACs (out[1]), high-slice k-blocks
+ * over all tiles (out[2]), tiles (out[3]), k-blocks a tile (out[4]); out[0] = -1
+ * when the context ran none.  Reads the high slice's block map back (a sync):
+ * call it outside timed regions. */
+void tp_debug_xtx_exec(const int *device, void *stream, double *out, int *status) {
+    guarded(status, [&] {
+        Ctx &c = ctx_for(dev_of(device), (hipStream_t)stream);
+        for (int q = 0; q < 5; ++q) out[q] = 0.0;
+        if (!xtx_w_exec(c, out)) out[0] = -1.0;
     });
 }
 

@@ -71,6 +71,10 @@ struct Ctx {
     int device = 0;
     unsigned long long last_use = 0;   // registry tick of the last lookup (LRU retirement)
     int last_xtx_ns = 0;            // int8 slices of the last X'X product (0: fp64 MFMA product)
+    // the last whole-triangle k_xtx_i8_w launch (tp_debug_xtx_exec: its executed
+    // int8 MACs from the high slice's block map, still in S_XNZ)
+    int xtx_w_n = 0, xtx_w_kp = 0, xtx_w_np = 0, xtx_w_ns = 0;
+    bool xtx_w_map = false;
     hipStream_t stream = nullptr;   // library stream (or the caller's, owns_stream = false)
     bool owns_stream = false;
     hipStream_t cur = nullptr;      // stream used by the current call
@@ -404,6 +408,10 @@ void xtx_int8_tiles128(Ctx &c, const int8_t *sl, int n, int ns, double *d_S, int
 void xtx_int8_slab128(Ctx &c, const int8_t *sl, int n, int ns, double *d_slab, int c0, int c1,
                       const double *cm = nullptr, const double *csd = nullptr);
 int xtx_kp(int n);
+// executed MACs of the context's last whole-triangle k_xtx_i8_w launch: out[0]
+// executed int8 MACs, out[1] the slice-0 MACs, out[2] high-slice k-blocks
+// summed over the tiles, out[3] tiles, out[4] k-blocks a tile (false: none)
+bool xtx_w_exec(Ctx &c, double *out);
 int8_t *xtx_slice_buf(Ctx &c, int n, int ns);
 int xtx_int_slices_cols(Ctx &c, const double *d_cmax, const int *d_cbad, int n);
 // sparse_cor in one call (R/TADpole.R:94-100,449): C = cor(X) with NaN -> 0, and

@@ -155,7 +155,12 @@ __device__ uint64_t radix_select(const double *r, int n, int rank, unsigned *his
             const unsigned rk = (unsigned)rank;
             // the bin holding rank lies in the first lane whose inclusive sum exceeds it
             const unsigned long long m = __ballot(incl > rk);
-            const int L = (int)__builtin_ctzll(m);   // m != 0: rank < the count of matching keys
+            // m != 0 while rank < the count of matching keys; if that invariant
+            // ever broke, lane 63 (the last bin) answers, so the pass writes a
+            // defined prefix instead of leaving stale values (TP_DASSERT traps
+            // it in checked builds)
+            TP_DASSERT(m != 0ull);
+            const int L = m ? (int)__builtin_ctzll(m) : 63;
             if (l == L) {
                 unsigned cum = ex;
                 int d = 4 * l;

@@ -1089,6 +1089,50 @@ static void launch_xtx_w_t(Ctx &c, const int8_t *sl, int n, int Kp, int Np, doub
     if (nt > 0)
         hipLaunchKernelGGL((k_xtx_i8_w<NS, COR>), dim3((unsigned)nt), dim3(512), 0, c.cur, sl, n, Kp, Np, d_S,
                            (int)nt, cm, csd, nzw, NW, d_tl, c0, c1);
+    if (!d_tl) {
+        c.xtx_w_n = n;
+        c.xtx_w_kp = Kp;
+        c.xtx_w_np = Np;
+        c.xtx_w_ns = NS;
+        c.xtx_w_map = nzw != nullptr;
+    }
+}
+
+// The MACs k_xtx_i8_w executed (host, after the fact): every tile (P, Q), 2P <=
+// Q, runs slice 0 over all nk k-blocks (256 x 128 x 64 MACs a block) and, with
+// two slices, three products (A1'B0, A0'B1, A1'B1) over the k-blocks where its
+// panels' map words have a bit -- the same union the kernel lists.
+bool xtx_w_exec(Ctx &c, double *out) {
+    if (!c.xtx_w_n) return false;
+    const int Kp = c.xtx_w_kp, Np = c.xtx_w_np, tnc = Np / 128, nk = Kp / 64, NW = (nk + 31) / 32;
+    std::vector<unsigned> map;
+    if (c.xtx_w_ns == 2 && c.xtx_w_map) {
+        map.resize((size_t)tnc * NW);
+        TP_HIP(hipStreamSynchronize(c.cur));
+        TP_HIP(hipMemcpy(map.data(), c.buf[S_XNZ].p, map.size() * 4, hipMemcpyDeviceToHost));
+    }
+    double tiles = 0, hi = 0;
+    for (int Q = 0; Q < tnc; ++Q)
+        for (int P = 0; 2 * P <= Q; ++P) {
+            tiles += 1;
+            if (c.xtx_w_ns != 2) continue;
+            if (map.empty()) {
+                hi += nk;
+                continue;
+            }
+            for (int w = 0; w < NW; ++w) {
+                unsigned u = map[(size_t)(2 * P) * NW + w] | map[(size_t)Q * NW + w];
+                if (2 * P + 1 < tnc) u |= map[(size_t)(2 * P + 1) * NW + w];
+                hi += __builtin_popcount(u);
+            }
+        }
+    const double blk = 256.0 * 128.0 * 64.0;
+    out[1] = tiles * nk * blk;
+    out[0] = out[1] + 3.0 * hi * blk;
+    out[2] = hi;
+    out[3] = tiles;
+    out[4] = nk;
+    return true;
 }
 static bool xtx_w_applies(int ns, int Kp) {
     if (!g_xtx_w || !g_xtx_glds || (ns != 1 && ns != 2)) return false;

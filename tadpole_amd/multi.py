@@ -98,11 +98,31 @@ def init_arm_comms(device: int, uid_fn: Optional[Callable[[], bytes]] = None,
     return ArmGroups(arm, p_ranks, q_ranks, rank, world)
 
 
-def exchange_arms(groups: ArmGroups, mine) -> dict:
+class ArmGroupError(RuntimeError):
+    """An arm failed on another rank's group (raised on every rank that did
+    not fail itself, so no rank is left waiting for that arm's result)."""
+
+
+def exchange_arms(groups: ArmGroups, mine, error: Optional[BaseException] = None) -> dict:
     """Every rank gets both arms' results: each group's root broadcasts its
-    arm's ``tadpole`` object over the default (control) group."""
+    arm's ``tadpole`` object over the default (control) group.
+
+    ``error``: this rank's arm raised (``mine`` is then ignored).  Every rank
+    first all-gathers its status, so when any arm failed all ranks raise at once
+    -- the failing ranks their own exception, the others ``ArmGroupError``
+    naming the first failing rank -- instead of the healthy group blocking in
+    the result broadcast until the process-group timeout."""
     import torch.distributed as dist
 
+    status: List[Optional[str]] = [None] * groups.world
+    msg = None if error is None else f"{type(error).__name__}: {error}"
+    dist.all_gather_object(status, msg)
+    failed = [(r, m) for r, m in enumerate(status) if m is not None]
+    if failed:
+        if error is not None:
+            raise error
+        r, m = failed[0]
+        raise ArmGroupError(f"the {'p' if r in groups.p_ranks else 'q'} arm failed on rank {r}: {m}")
     out = {}
     for arm, ranks in (("p", groups.p_ranks), ("q", groups.q_ranks)):
         obj = [mine if (groups.arm == arm and groups.rank == ranks[0]) else None]

@@ -123,6 +123,59 @@ def test_c5_arm_groups_gloo(world, monkeypatch):
         assert (by_p, by_q, d_p, d_q) == (0, npr, 0, 10)
 
 
+def _fail_worker(rank, world, port, out, bad_arm):
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    from tadpole_amd import multi
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = multi.init_arm_comms(0, uid_fn=lambda: bytes(range(128)), init_fn=lambda uid, n, r, dev: None)
+    try:
+        if g.arm == bad_arm:
+            raise ValueError("TP_ERR_NO_BSTICK on this arm")
+        mine, err = {"arm": g.arm}, None
+    except ValueError as e:
+        mine, err = None, e
+    try:
+        multi.exchange_arms(g, mine, err)
+        out.put((rank, "ok", ""))
+    except multi.ArmGroupError as e:
+        out.put((rank, "group", str(e)))
+    except ValueError as e:
+        out.put((rank, "own", str(e)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,bad_arm", [(2, "q"), (3, "p")])
+def test_c5_arm_group_failure_reaches_every_rank(world, bad_arm):
+    """an arm that raises on its group (a data error or a
+    communicator abort) makes every rank raise at once -- its own ranks their
+    exception, the other group's ranks ArmGroupError naming the failing rank --
+    instead of the healthy group blocking in the result broadcast until the
+    process-group timeout."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_fail_worker, args=(r, world, port, q, bad_arm)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(60)
+    npr = (world + 1) // 2
+    bad = list(range(npr)) if bad_arm == "p" else list(range(npr, world))
+    for rank, kind, msg in res:
+        if rank in bad:
+            assert kind == "own" and "NO_BSTICK" in msg
+        else:
+            assert kind == "group" and f"rank {bad[0]}" in msg and "NO_BSTICK" in msg
+
+
 def test_matrix_checksum_dev_matches_host():
     """The on-device checksum every rank takes of its own C5 copy equals the
     fixture's host checksum (synth.matrix_checksum)."""

@@ -54,6 +54,73 @@ def test_fresh_streams_keep_device_memory_bounded(gpu):
     assert _used() - base <= (256 << 20)
 
 
+def test_failed_scratch_allocation_then_smaller_call(gpu):
+    """a scratch regrowth whose allocation fails (injected
+    out-of-memory, knob 51) leaves that buffer empty, not a null block that
+    still claims its old size: a smaller call on the same stream context then
+    allocates it again and gives the same result (before the fix it wrote
+    through a null pointer)."""
+    import torch
+    import tadpole_amd as tp
+    import gpu_helpers as G
+    small, large = synth_hic(900, 67), synth_hic(2200, 68)
+    s = torch.cuda.Stream()
+    ref = tp.TADpole(small, max_pcs=60, stream=s)
+    old = G.knob(51, 1)
+    try:
+        with pytest.raises(Exception, match="injected out-of-memory"):
+            tp.TADpole(large, max_pcs=60, stream=s)
+    finally:
+        G.knob(51, 0)
+    assert _same(tp.TADpole(small, max_pcs=60, stream=s), ref)
+    assert _same(tp.TADpole(large, max_pcs=60, stream=s), tp.TADpole(large, max_pcs=60))
+    tp.release_stream(s)
+    assert old == 0
+
+
+_POOL_SCRIPT = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, sys.argv[1])
+import tadpole_amd as tp
+from tadpole_amd import _lib
+from tadpole_amd.synth import synth_hic
+def used():
+    torch.cuda.synchronize(); torch.cuda.empty_cache()
+    f, t = torch.cuda.mem_get_info(0)
+    return t - f
+m = synth_hic(4000, 69)
+torch.zeros(1, device="cuda")
+base = used()                       # before the library's first allocation
+s = torch.cuda.Stream()
+tp.TADpole(m, max_pcs=60, stream=s)
+tp.TADpole(m, max_pcs=60)
+peak = used()
+tp.release_stream(s)
+_lib.load().tp_shutdown()
+after = used()
+print("POOL", base, peak, after)
+"""
+
+
+def test_library_pool_returns_memory(gpu, tmp_path):
+    """scratch comes from the library's own stream-ordered pool (not
+    the device's default pool with its release threshold raised), and retiring
+    the contexts trims it: in a fresh process, device memory after
+    release_stream + tp_shutdown is back to its level before the library's
+    first allocation (code objects aside)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "-c", _POOL_SCRIPT, root], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = [x for x in p.stdout.splitlines() if x.startswith("POOL")][-1]
+    base, peak, after = (int(v) for v in line.split()[1:])
+    print(f"device memory: before {base >> 20} MB, two contexts {peak >> 20} MB, after shutdown {after >> 20} MB")
+    assert peak - base > (512 << 20)                  # the scratch was really there
+    assert after - base <= (96 << 20), (base, peak, after)
+
+
 def test_default_stream_callers_serialise(gpu):
     """Two host threads on the library stream of one device (no stream given)
     get the same results as one caller: the context lock serialises them."""
