@@ -1952,6 +1952,7 @@ void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
         case 49: p = &g_coniss_lds2; break;
         case 50: p = &g_clean_tile; break;
         case 51: p = &g_devbuf_fail_inject; break;
+        case 52: p = &g_coniss_batch; break;
         default: fail(TP_ERR_ARG, "unknown knob");
         }
         if (*which == 3 && *value != 16 && *value != 32) fail(TP_ERR_ARG, "stage depth must be 16 or 32");

@@ -262,6 +262,7 @@ struct SweepDev {
 extern int g_ch_dedup;        // 0: every tree computes its own segment statistics
 extern int g_cor_fused;        // 0: prcomp's column means by a separate pass over C
 extern int g_coniss_lu;       // 0: the global CONISS variant keeps its links in global memory
+extern int g_coniss_batch;    // the batched CONISS kernel (1 default, 2 also for lean sweeps, 0 never)
 extern int g_coniss_lean_min; // lean sweeps of matrices that fit LDS from this many bins take the link-only variant (0: never)
 extern int g_lean_auto;       // 1: a sweep is lean whenever another pipeline is in flight on its device
 extern int g_coniss_lds2;     // the LDS variant with one 16-bit link array (1: lean sweeps, 2: every sweep)

@@ -867,6 +867,461 @@ template __global__ void k_coniss_t<false, 11, true, false, 16>(SweepDev, double
 template __global__ void k_coniss_t<false, 16, true, false, 16>(SweepDev, double *);
 template __global__ void k_coniss_t<false, 32, true, false, 16>(SweepDev, double *);
 
+// ------------------------------------------------ batched CONISS (round 6)
+// The same merges, costs, heights and records as coniss_tree2, produced in
+// batches by one workgroup of CB_W waves per tree.  Greedy adjacency-
+// constrained Ward merging is sequential, but a run of merges can be taken at
+// once when it provably equals the next merges of the sequential order
+// (tools/coniss_batch_model.py checks the rule against the oracle):
+//   1. candidates: every position whose cost is <= T = g r (g the smallest
+//      cost, r an adaptive ratio >= 1), taken from the blocks whose minimum is
+//      <= T -- a COMPLETE prefix of the (cost, position) order -- sorted, the
+//      first CB_W kept;
+//   2. windows: each candidate's clusters LS, A, B, R (starts ls, a, b, r); the
+//      candidates are kept up to the first whose window overlaps an earlier
+//      one's, so every kept merge reads clusters no other kept merge changes;
+//   3. new costs: wave j merges candidate j's A and B from the pre-batch rows
+//      (the rows the sequential order would read: nothing earlier in the batch
+//      touched them) and forms cl = Ward(LS, M), cr = Ward(M, R) in the
+//      canonical arithmetic of coniss_tree2;
+//   4. the leading run: candidate i is the next sequential merge unless a new
+//      cost of a kept candidate before it, (cl_j, ls_j) or (cr_j, a_j), is
+//      lexicographically smaller than (cost_i, a_i) -- the batch stops there;
+//   5. the run is applied (costs, links, records, heights summed in merge
+//      order, the merged clusters' sums rows), the touched blocks' minima are
+//      refreshed, and the next batch starts.
+// Typical runs: ~3 merges for trees of 1-3 PCs, 5-7 for wider trees, against
+// one merge per ~2 800-cycle step of coniss_tree2.  The overflow case (more
+// than CB_CAP positions <= T, or ties at g) takes one merge, the exact argmin.
+constexpr int CB_W = 8;      // waves a tree = most candidates a batch
+constexpr int CB_CAP = 16;   // positions <= T ranked a batch (16 x 16 lane pairs)
+constexpr int CB_FMAX = 16;  // flagged blocks a batch (two a wave)
+constexpr int CB_SEG = 8;    // positions <= T a wave may contribute
+static_assert(CB_W * CB_SEG == 64, "one segment entry a lane");
+struct CbShared {
+    double sgc[CB_W * CB_SEG];   // the waves' segments: positions <= T and their costs
+    int sgp[CB_W * CB_SEG];
+    int segn[CB_W];
+    double ccost[CB_CAP];
+    int cpos[CB_CAP];
+    double key[CB_W], cl[CB_W], cr[CB_W], hgt[CB_W];
+    int spos[CB_W], ka[CB_W];
+    int4 win[CB_W];   // (lo, hi, ls, r): positions covered by LS..R, the neighbours (-1: none)
+    int4 w2[CB_W];    // (b, eb, er, -)
+    int kc, cnt;
+};
+__device__ __forceinline__ int mbcnt64(unsigned long long m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
+// lexicographic (cost, position) order of the merge choice
+__device__ __forceinline__ bool key_lt(double c1, int p1, double c2, int p2) {
+    return c1 < c2 || (c1 == c2 && p1 < p2);
+}
+
+template <int NS, int BS, bool STAMPS>
+__device__ __forceinline__ void coniss_tree_b(const SweepDev &sd, double *cost0, double *lds, CbShared &sh) {
+    const int n = sd.n;
+    const int ti = blockIdx.x;
+    const int i = sd.tree0 + ti + 1;
+    constexpr int ld = NS * 64;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int nbk = (n + 63) / 64;
+    const double QNAN = __longlong_as_double(0x7FF8000000000000LL);
+    // STAMPS (diagnostic builds): wave 0's cycles per phase, summed over the
+    // batches, into sd.stamps[tree * 16 + 0..9]; 13: merges, 14: batches,
+    // 15: retries of the candidate pass (too many positions <= T)
+    long long st_acc[16] = {};
+    long long st_t0 = STAMPS ? (long long)__builtin_amdgcn_s_memtime() : 0;
+#define TP_BSTAMP(ph)                                                     \
+    if (STAMPS && w == 0) {                                               \
+        long long _t = (long long)__builtin_amdgcn_s_memtime();           \
+        st_acc[ph] += _t - st_t0;                                         \
+        st_t0 = _t;                                                       \
+    }
+    const size_t cst = coniss_cost_stride(n), lst = coniss_link_stride(n);
+    double *cost = lds;
+    int *link = (int *)(cost + cst);
+    int *rn = link + lst;
+    double *bmin = (double *)(rn + lst);   // 8-byte aligned: 8 cst + 8 lst bytes before it
+    const int DC = nbk * 64, DL = n;
+    constexpr bool P4 = NS == 4;
+    double *S = sd.sums + sums_off(n, sd.tree0, i);
+    const double *PP = P4 ? sd.pt4 : (NS >= 2 ? sd.pt2 : sd.Pt);
+    const size_t ldpp = P4 ? (size_t)256 : (NS >= 2 ? (size_t)sd.pt2_ld : (size_t)sd.ldp);
+    const bool last_in = lane + 64 * (NS - 1) < i;
+    int *mrg_a = sd.mrg_a + (size_t)ti * (n - 1);
+    int *mrg_b = sd.mrg_b + (size_t)ti * (n - 1);
+    double *mcost = sd.cost + (size_t)ti * (n - 1);
+    double *height = sd.height + (size_t)ti * (n - 1);
+    const double *c0 = cost0 + (size_t)ti * cst;
+
+    auto load_row = [&](double (&dst)[NS], int code) {
+        code = __builtin_amdgcn_readfirstlane(code);
+        const int p = code & (ROW_PT - 1);
+        const double *pr = (code & ROW_PT) ? PP + (size_t)p * ldpp : S + (size_t)p * ld;
+        if (NS >= 2) {
+            const double2 v = *(const double2 *)(pr + 2 * lane);
+            dst[0] = v.x;
+            dst[1] = v.y;
+        } else {
+            dst[0] = pr[lane];
+        }
+        if (P4) {
+            const double2 v = *(const double2 *)(pr + 128 + 2 * lane);
+            dst[2] = v.x;
+            dst[3] = v.y;
+        } else {
+#pragma unroll
+            for (int t = 2; t < NS; ++t) dst[t] = pr[64 * t + lane];
+        }
+    };
+    auto rowc = [](int start, bool single) { return start | (single ? ROW_PT : 0); };
+
+    // ---- initial costs, links, block minima (all waves)
+    for (int bk = w; bk < nbk; bk += CB_W) {
+        const int p = bk * 64 + lane;
+        const double cp = c0[p];
+        cost[p] = cp;
+        if (p < n) {
+            link[p] = p;
+            rn[p] = p + 1 < n ? p + 1 : -1;
+        }
+        const double m = wave_min(cp);
+        if (lane == 0) bmin[bk] = m;
+    }
+    if (w == 0) {
+        cost[DC + lane] = QNAN;
+        link[DL + lane] = -1;
+        rn[DL + lane] = -1;
+    }
+    __syncthreads();
+
+    double h = 0.0;      // wave 0: the height so far
+    double gap = -1.0;   // T = g + gap (every wave the same), adapted to about 6..10 positions <= T
+    // waves j < kc: candidate j's window, merged sums, key and new costs
+    int a = 0, ea = 0, b = 0, eb = 0, ls = -1, r = -1, er = -1;
+    double sm[NS];
+    double key = 0.0, cl = 0.0, cr = 0.0;
+    int s = 0;
+    while (s < n - 1) {
+        // ---- A1 (every wave): g and T = g + gap from the block minima (every
+        // wave computes the same); wave w scans the flagged blocks (minimum <=
+        // T) of flagged index w and w + CB_W and writes its positions with cost
+        // <= T to its segment; after B0 every wave reads the segment counts and
+        // retries with a smaller gap if they overflow (the same decision in
+        // every wave; try 6 takes only the ties at g, try 7 the exact argmin)
+        double gq = 0.0;
+        bool single = false;
+        int C = 0;
+        {
+            double bm[BS];
+#pragma unroll
+            for (int q = 0; q < BS; ++q) bm[q] = 64 * q + lane < nbk ? bmin[64 * q + lane] : QNAN;
+            double x = bm[0];
+#pragma unroll
+            for (int q = 1; q < BS; ++q) x = vmin(x, bm[q]);
+            gq = wave_min(x);
+            if (!(gap > 0.0)) gap = gq > 0.0 && gq < 1e300 ? 0.5 * gq : 1e-300;
+            for (int tries = 0;; ++tries) {
+                double T = gq + gap;
+                if (!(T >= gq) || tries >= 6) T = gq;
+                int F = 0, mb0 = -1, mb1 = -1;   // this wave's flagged blocks (at most 2)
+#pragma unroll
+                for (int q = 0; q < BS; ++q) {
+                    const bool f = bm[q] <= T;
+                    const unsigned long long m = __ballot(f);
+                    const int idx = F + mbcnt64(m);
+                    const unsigned long long mine = __ballot(f && (idx & (CB_W - 1)) == w);
+                    const int i0 = mine ? 64 * q + (int)__builtin_ctzll(mine) : -1;
+                    const unsigned long long rest = mine & (mine - 1);
+                    const int i1 = rest ? 64 * q + (int)__builtin_ctzll(rest) : -1;
+                    if (i0 >= 0) {
+                        if (mb0 < 0) mb0 = i0;
+                        else if (mb1 < 0) mb1 = i0;
+                    }
+                    if (i1 >= 0 && mb1 < 0) mb1 = i1;
+                    F += __popcll(m);
+                }
+                int cw = CB_CAP + 1;
+                if (F <= CB_FMAX) {
+                    const double v0 = cost[(mb0 >= 0 ? mb0 : 0) * 64 + lane];
+                    const double v1 = cost[(mb1 >= 0 ? mb1 : 0) * 64 + lane];
+                    const bool s0 = (mb0 >= 0) & (v0 <= T), s1 = (mb1 >= 0) & (v1 <= T);
+                    const unsigned long long m0 = __ballot(s0), m1 = __ballot(s1);
+                    const int i0 = mbcnt64(m0), i1 = __popcll(m0) + mbcnt64(m1);
+                    if (s0 && i0 < CB_SEG) {
+                        sh.sgc[w * CB_SEG + i0] = v0;
+                        sh.sgp[w * CB_SEG + i0] = mb0 * 64 + lane;
+                    }
+                    if (s1 && i1 < CB_SEG) {
+                        sh.sgc[w * CB_SEG + i1] = v1;
+                        sh.sgp[w * CB_SEG + i1] = mb1 * 64 + lane;
+                    }
+                    cw = __popcll(m0) + __popcll(m1);
+                }
+                if (lane == 0) sh.segn[w] = cw;
+                lds_barrier();   // B0
+                // the eight counts (two broadcast reads): every wave takes the same decision
+                const int4 n0 = *(const int4 *)&sh.segn[0], n1 = *(const int4 *)&sh.segn[4];
+                const int c0_ = __builtin_amdgcn_readfirstlane(n0.x), c1_ = __builtin_amdgcn_readfirstlane(n0.y),
+                          c2_ = __builtin_amdgcn_readfirstlane(n0.z), c3_ = __builtin_amdgcn_readfirstlane(n0.w),
+                          c4_ = __builtin_amdgcn_readfirstlane(n1.x), c5_ = __builtin_amdgcn_readfirstlane(n1.y),
+                          c6_ = __builtin_amdgcn_readfirstlane(n1.z), c7_ = __builtin_amdgcn_readfirstlane(n1.w);
+                const int tot = c0_ + c1_ + c2_ + c3_ + c4_ + c5_ + c6_ + c7_;
+                const int mx = max(max(max(c0_, c1_), max(c2_, c3_)), max(max(c4_, c5_), max(c6_, c7_)));
+                if (tot <= CB_CAP && mx <= CB_SEG && tot >= 1) {
+                    C = tot;
+                    if (tries <= 5) gap *= C < 6 ? 1.3 : (C > 10 ? 0.8 : 1.0);   // next batch: ~6..10 positions <= T
+                    break;
+                }
+                if (tries >= 6) {
+                    single = true;
+                    break;
+                }
+                lds_barrier();   // every wave has read the counts before a retry rewrites them
+                gap *= 0.5;
+                if (STAMPS) st_acc[15] += 1;
+            }
+        }
+        TP_BSTAMP(10);
+        // ---- A1b (wave 0): gather the segments, rank, the first CB_W into the slots
+        if (w == 0) {
+            int Kc;
+            if (!single) {
+                // the segments compacted: lane l holds entry l & 7 of wave l >> 3
+                const bool valid = (lane & (CB_SEG - 1)) < sh.segn[lane >> 3];
+                const double cv = sh.sgc[lane];
+                const int cp = sh.sgp[lane];
+                const unsigned long long mv = __ballot(valid);
+                const int idx = mbcnt64(mv);
+                if (valid) {
+                    sh.ccost[idx] = cv;
+                    sh.cpos[idx] = cp;
+                }
+                // ranks: lane l compares candidate i = 4 p + (l >> 4) with j = l & 15
+                const int j = lane & 15;
+                const double kj = sh.ccost[j];
+                const int pj = sh.cpos[j];
+                double ki[4];
+                int pi[4];
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+                    ki[p] = sh.ccost[4 * p + (lane >> 4)];
+                    pi[p] = sh.cpos[4 * p + (lane >> 4)];
+                }
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+                    const int ii = 4 * p + (lane >> 4);
+                    const unsigned long long mm = __ballot((j < C) & key_lt(kj, pj, ki[p], pi[p]));
+                    const int rank = __popc((unsigned)(mm >> (16 * (lane >> 4))) & 0xFFFFu);
+                    if ((j == 0) & (ii < C) & (rank < CB_W)) {
+                        sh.key[rank] = ki[p];
+                        sh.spos[rank] = pi[p];
+                    }
+                }
+                Kc = C < CB_W ? C : CB_W;
+            } else {
+                // too many positions tie at g: the exact argmin, one merge
+                double bm[BS];
+#pragma unroll
+                for (int q = 0; q < BS; ++q) bm[q] = 64 * q + lane < nbk ? bmin[64 * q + lane] : QNAN;
+                int bk = 0;
+#pragma unroll
+                for (int q = BS - 1; q >= 0; --q) {
+                    const unsigned long long m = __ballot(bm[q] == gq);
+                    bk = m ? 64 * q + (int)__builtin_ctzll(m) : bk;
+                }
+                const unsigned long long mv = __ballot(cost[bk * 64 + lane] == gq);
+                TP_DASSERT(mv != 0ull);
+                if (lane == 0) {
+                    sh.key[0] = gq;
+                    sh.spos[0] = bk * 64 + (int)__builtin_ctzll(mv);
+                }
+                Kc = 1;
+            }
+            if (lane == 0) sh.kc = Kc;
+        }
+        TP_BSTAMP(0);
+        lds_barrier();   // B1
+        TP_BSTAMP(1);
+        // ---- A2 (wave j < kc): candidate j's window, rows, merged sums, new costs
+        const int kc = __builtin_amdgcn_readfirstlane(sh.kc);
+        if (w < kc) {
+            a = __builtin_amdgcn_readfirstlane(sh.spos[w]);
+            key = sh.key[w];
+            TP_DASSERT(a >= 0 && a < n - 1);
+            int lsv = link[a > 0 ? a - 1 : DL];
+            ea = link[a];
+            eb = rn[a];
+            pin3(lsv, ea, eb);
+            ea = __builtin_amdgcn_readfirstlane(ea);
+            eb = __builtin_amdgcn_readfirstlane(eb);
+            b = ea + 1;
+            ls = a > 0 ? __builtin_amdgcn_readfirstlane(lsv) : -1;
+            r = eb + 1 < n ? eb + 1 : -1;
+            er = r >= 0 ? __builtin_amdgcn_readfirstlane(rn[b]) : -1;
+            const int ac = rowc(a, ea == a);
+            double sa[NS], sb[NS], sl[NS], sr[NS];
+            load_row(sa, ac);
+            load_row(sb, rowc(b, eb == b));
+            load_row(sl, ls >= 0 ? rowc(ls, ls == a - 1) : ac);
+            load_row(sr, r >= 0 ? rowc(r, er == r) : ac);
+            if (lane == 0) {
+                sh.win[w] = make_int4(ls >= 0 ? ls : a, r >= 0 ? er : eb, ls, r);
+                sh.w2[w] = make_int4(b, eb, er, 0);
+                sh.ka[w] = a;
+            }
+#pragma unroll
+            for (int t = 0; t < NS; ++t) sm[t] = sa[t] + sb[t];
+            const double fm = (double)(eb - a + 1), fl = (double)(a - ls), fr = (double)(er - r + 1);
+            double ul = ward_part<NS>(sl, fl, sm, fm, last_in);
+            double ur = ward_part<NS>(sm, fm, sr, fr, last_in);
+            wave_sum2(ul, ur);
+            const double ql = pin_d(ul / (fl * fm * (fl + fm)));
+            const double qr = pin_d(ur / (fm * fr * (fm + fr)));
+            cl = ls >= 0 ? nan2inf(ql) : QNAN;
+            cr = r >= 0 ? nan2inf(qr) : QNAN;
+            if (lane == 0) {
+                sh.cl[w] = cl;
+                sh.cr[w] = cr;
+            }
+        }
+        TP_BSTAMP(2);
+        lds_barrier();   // B2
+        TP_BSTAMP(3);
+        // ---- A3 (wave 0): the conflict-free prefix and the leading run, lane
+        // l comparing slot i = l >> 3 with an earlier slot j = l & 7; the
+        // run's heights, costs and links
+        if (w == 0) {
+            const int si = lane >> 3, sj = lane & 7;
+            const int4 wi = sh.win[si], wj = sh.win[sj];
+            const double ki = sh.key[si];
+            const int ai = sh.ka[si], aj = sh.ka[sj];
+            const double clj = sh.cl[sj], crj = sh.cr[sj];
+            const int4 x2 = sh.w2[sj];
+            const bool pair = sj < si && si < kc;
+            const unsigned long long cm = __ballot(pair && !(wi.y < wj.x || wj.y < wi.x));
+            const int kacc = cm ? (int)(__builtin_ctzll(cm) >> 3) : kc;
+            const bool und = (wj.z >= 0 && key_lt(clj, wj.z, ki, ai)) || (wj.w >= 0 && key_lt(crj, aj, ki, ai));
+            const unsigned long long pm = __ballot(pair && si < kacc && und);
+            const int cnt = pm ? (int)(__builtin_ctzll(pm) >> 3) : kacc;
+            // heights in merge order (lane j < 8 holds slot j's key)
+            const double kl = sh.key[sj];
+            double hh = h, myh = 0.0;
+            for (int q = 0; q < cnt; ++q) {
+                hh = hh + readlane_d(kl, q);
+                myh = lane == q ? hh : myh;
+            }
+            h = hh;
+            // the run's costs and links, lane q < cnt for merge s + q (the
+            // windows are disjoint: no two lanes write one word)
+            if (lane < cnt) {
+                sh.hgt[lane] = myh;
+                cost[x2.x] = QNAN;
+                cost[aj] = crj;   // QNAN without a right neighbour
+                link[aj] = x2.y;
+                link[x2.y] = aj;
+                rn[aj] = x2.z;
+                if (wj.z >= 0) {
+                    cost[wj.z] = clj;
+                    rn[wj.z] = x2.y;
+                }
+            }
+            if (lane == 0) sh.cnt = cnt;
+            if (STAMPS) st_acc[13] += cnt;
+        }
+        TP_BSTAMP(4);
+        lds_barrier();   // B3
+        TP_BSTAMP(5);
+        // ---- A4 (wave j < cnt): merge s + j's sums row and record, the touched
+        // blocks' minima (every cost of the run is in place); the stores
+        // complete before B4 (the next batch's rows may be these)
+        const int cnt = __builtin_amdgcn_readfirstlane(sh.cnt);
+        if (w < cnt) {
+            if (NS >= 2)
+                *(double2 *)(S + (size_t)a * ld + 2 * lane) = make_double2(sm[0], sm[1]);
+            else
+                S[(size_t)a * ld + lane] = sm[0];
+            if (P4) {
+                *(double2 *)(S + (size_t)a * ld + 128 + 2 * lane) = make_double2(sm[2], sm[3]);
+            } else {
+#pragma unroll
+                for (int t = 2; t < NS; ++t) S[(size_t)a * ld + 64 * t + lane] = sm[t];
+            }
+            if (lane == 0) {
+                mrg_a[s + w] = a;
+                mrg_b[s + w] = b;
+                mcost[s + w] = key;
+                height[s + w] = sh.hgt[w];
+            }
+            TP_BSTAMP(6);
+            const int ba = a >> 6, bb = b >> 6, bl = ls >= 0 ? (ls >> 6) : ba;
+            double ma = cost[ba * 64 + lane], mb = cost[bb * 64 + lane], ml = cost[bl * 64 + lane], mx = QNAN;
+            wave_min4(ma, mb, ml, mx);
+            if (lane == 0) {
+                bmin[ba] = ma;
+                bmin[bb] = mb;
+                bmin[bl] = ml;
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        s += cnt;
+        TP_BSTAMP(8);
+        lds_barrier();   // B4
+        TP_BSTAMP(9);
+        if (STAMPS) st_acc[14] += 1;
+    }
+    __syncthreads();
+    // ---- broken stick (rioja bstick.chclust, vegan bstick.default) on heights
+    if (threadIdx.x == 0) {
+        const int nobj = n - 1;
+        int ncl = -1;
+        if (nobj >= 2) {
+            const double tot = height[nobj - 1];
+            double *cs = cost;
+            double hi = 0.0, lo = 0.0;
+            for (int t = 1; t <= nobj; ++t) {
+                dd_add_d(hi, lo, tot / (double)(nobj - t + 1));
+                cs[t - 1] = hi + lo;
+            }
+            int run = 0;
+            bool started = false;
+            for (int j = 1; j <= nobj - 1; ++j) {
+                double disp = fabs(height[nobj - 1 - j] - height[nobj - j]);
+                double bs = cs[nobj - j] / (double)nobj;
+                if (disp > bs) { started = true; ++run; }
+                else if (started) break;
+            }
+            ncl = started ? run : -1;
+        }
+        sd.n_cluster[ti] = ncl;
+    }
+    if (STAMPS && threadIdx.x == 0)
+        for (int q = 0; q < 16; ++q) sd.stamps[(size_t)ti * 16 + q] = st_acc[q];
+#undef TP_BSTAMP
+}
+
+// trees of up to 4 column slots (k <= 256), costs and links in LDS
+template <int BS, bool STAMPS = false>
+__global__ void __launch_bounds__(64 * CB_W) k_coniss_b(SweepDev sd, double *cost0) {
+    extern __shared__ double lds[];
+    __shared__ CbShared sh;
+    const int i = sd.tree0 + blockIdx.x + 1;
+    switch ((i + 63) / 64) {
+        case 1: coniss_tree_b<1, BS, STAMPS>(sd, cost0, lds, sh); break;
+        case 2: coniss_tree_b<2, BS, STAMPS>(sd, cost0, lds, sh); break;
+        case 3: coniss_tree_b<3, BS, STAMPS>(sd, cost0, lds, sh); break;
+        default: coniss_tree_b<4, BS, STAMPS>(sd, cost0, lds, sh); break;
+    }
+}
+template __global__ void k_coniss_b<1>(SweepDev, double *);
+template __global__ void k_coniss_b<2>(SweepDev, double *);
+template __global__ void k_coniss_b<3>(SweepDev, double *);
+template __global__ void k_coniss_b<1, true>(SweepDev, double *);
+template __global__ void k_coniss_b<2, true>(SweepDev, double *);
+template __global__ void k_coniss_b<3, true>(SweepDev, double *);
+
 // ------------------------------------------------------------ CH over cuts
 // canonical segment statistics of rows s..e, by one wave (see tpo_seg_ss)
 // RB rows per batch (RB x KS loads in flight); the order of the sums is
@@ -1432,6 +1887,10 @@ static void launch_coniss_bs(const SweepDev &sd, double *cost0, size_t lds, hipS
     hipLaunchKernelGGL((k_coniss_t<STAMPS, BS, GLB, LU>), dim3(sd.ntrees), dim3(128), lds, s, sd, cost0);
 }
 int g_coniss_lu = 1;   // 0: the global variant keeps its links in global memory too
+// knob 52: the batched CONISS kernel (k_coniss_b) where it applies -- 1: not for
+// lean sweeps (a tree holds a whole CU: 8 waves, ~130 KB of LDS), 2: also for
+// them, 0: never (the two-wave k_coniss_t)
+int g_coniss_batch = 1;
 // lean sweeps (another pipeline in flight on the device) of matrices that fit
 // LDS, from this many bins (knob 48; 0: never): costs global and only the
 // links in LDS (2 bytes a bin) so several trees share a CU -- the LDS
@@ -1487,6 +1946,26 @@ static void run_coniss(const SweepDev &sd_in, hipStream_t s, bool stamped, Ctx *
     const size_t lds = in_lds2 ? coniss_lds2_bytes(sd.n)
                                : (in_lds ? coniss_lds_bytes(sd.n) : (lu ? lu_bytes : (lu2 ? lu_bytes / 2 : kConissGlbLds)));
     if (!stamped && prof) kprof_begin(*prof, K_CONISS);
+    // the batched kernel (round 6): costs, links and the block minima in LDS,
+    // trees of up to 4 column slots
+    const size_t lds_b = coniss_lds_bytes(sd.n) + (size_t)nbk * 8;
+    if (g_coniss_batch && sd.tree0 + sd.ntrees <= 256 && bs <= 3 && !lean_small &&
+        lds_b + sizeof(CbShared) <= 160 * 1024 - 64 && !(sd.lds_lean && g_coniss_batch < 2)) {
+        auto go = [&](auto kern) {
+            TP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_b));
+            hipLaunchKernelGGL(kern, dim3(sd.ntrees), dim3(64 * CB_W), lds_b, s, sd, cost0);
+        };
+        if (stamped) {
+            if (bs == 1) go(k_coniss_b<1, true>);
+            else if (bs == 2) go(k_coniss_b<2, true>);
+            else go(k_coniss_b<3, true>);
+        } else if (bs == 1) go(k_coniss_b<1>);
+        else if (bs == 2) go(k_coniss_b<2>);
+        else go(k_coniss_b<3>);
+        if (!stamped && prof) kprof_end(*prof, K_CONISS);
+        TP_HIP(hipGetLastError());
+        return;
+    }
     // global variant: as few block-minimum slots as the size needs (every
     // per-slot loop of the merge chain -- the untouched minimum, the argmin
     // ballots, the block-minimum updates -- runs over all of them)

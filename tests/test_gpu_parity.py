@@ -938,3 +938,25 @@ def _upload_checks(gpu, h, d, n, blk, packed, st, s, rng):
                       ctypes.c_void_p(s.cuda_stream), ctypes.byref(st))
     assert st.value == 0
     assert np.array_equal(d3.cpu().numpy().view(np.uint64), raw.view(np.uint64))
+
+
+@pytest.mark.parametrize("n,k,seed", [(150, 5, 31), (1999, 70, 32), (4100, 200, 33), (7729, 200, 34),
+                                      (9500, 24, 35), (3000, 256, 36)])
+def test_coniss_batched_same_bits(gpu, n, k, seed):
+    """The batched CONISS (k_coniss_b, knob 52: candidate runs taken several
+    merges at a time by 8 waves a tree) gives every tree's merge order, costs,
+    heights, broken-stick count and CH scores of the two-wave kernel bit for
+    bit (the run rule of tools/coniss_batch_model.py), on TAD-like scores with
+    1..256 PCs (1..4 column slots, 1..3 block-minimum slots)."""
+    p = _structured_pcs(n, k, seed)
+    old = G.knob(52, 0)
+    try:
+        ref = G.sweep_dev(p)
+        G.knob(52, 1)
+        got = G.sweep_dev(p)
+    finally:
+        G.knob(52, old)
+    for f in ("n_cluster", "mrg_a", "mrg_b"):
+        assert np.array_equal(got[f], ref[f]), f
+    for f in ("cost", "height", "scores"):
+        assert np.array_equal(got[f].view(np.uint64), ref[f].view(np.uint64)), f

@@ -160,3 +160,20 @@ def test_read_matrix_na(tmp_path):
     assert m.shape == (3, 3) and np.isnan(m[0, 2]) and np.isnan(m[1, 1])
     c = api.clean_symmetrize(m)
     assert c[2, 0] == 0.0 and c[1, 1] == 0.0 and np.array_equal(c, c.T)
+
+
+@pytest.mark.parametrize("n,k,seed", [(150, 5, 31), (300, 1, 7), (65, 2, 4), (3, 1, 1)])
+def test_coniss_batch_emulation(n, k, seed):
+    """The batched CONISS kernel's control flow (tools/coniss_batch_emu.py: the
+    candidate scan over the waves' segments, slot_of, ranks, windows,
+    conflicts, runs), emulated with range checks on every index, makes the
+    sequential CONISS's merges on TAD-like scores."""
+    import importlib.util
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("coniss_batch_emu", os.path.join(root, "tools", "coniss_batch_emu.py"))
+    E = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(E)
+    p = E.structured(n, k, seed)
+    got, _ = E.kernel(p)
+    ref = E.seq_coniss(p)
+    assert [(a, b) for a, b, _ in got] == [(a, b) for a, b, _ in ref]
