@@ -92,6 +92,12 @@ void tp_release_stream(const int *device, void *stream, int *status);
  * was loaded.  A caller that reuses its streams creates none after the first
  * call on each (tadpole_amd.genome's persistent stream pool is tested so). */
 void tp_context_stats(const int *device, int *live, int *created, int *status);
+/* Size the contexts of `nstreams` caller streams alike: each of their scratch
+ * buffers grows to the largest size that buffer has in any of them (no data
+ * kept; stream-ordered, synchronised before returning).  For a pool of streams
+ * that any matrix of a workload may land on (tadpole_amd.genome): once every
+ * matrix has run on one stream of the pool, no call regrows scratch. */
+void tp_reserve_streams(const int *device, void *const *streams, const int *nstreams, int *status);
 /* Attach a host word to the context of (device, stream) (NULL detaches):
  * every later tp_pipeline / tp_pipeline_dev on that context stores its stage
  * there as it goes -- 0 started, 1 mask read back, 2 correlation queued,

@@ -31,7 +31,7 @@ EXPORTS = (
     "tp_pipeline", "tp_pipeline_dev", "tp_sweep_dev", "tp_tsv_dims", "tp_read_tsv",
     "tp_comm_unique_id", "tp_comm_init", "tp_comm_destroy", "tp_set_virtual_shards", "tp_shard_plan",
     "tp_level_coords", "tp_read_tsv_dev", "tp_context_stats", "tp_progress_attach", "tp_upload_dev",
-    "tp_upload_counts_dev",
+    "tp_upload_counts_dev", "tp_reserve_streams",
 )
 
 
@@ -160,6 +160,19 @@ def release_stream(stream, device: int = None) -> None:
     L = load()
     st = ctypes.c_int(0)
     L.tp_release_stream(ctypes.byref(ctypes.c_int(int(device))), ctypes.c_void_p(int(handle)), ctypes.byref(st))
+    check(st)
+
+
+def reserve_streams(streams, device: int = 0) -> None:
+    """tp_reserve_streams: size the library contexts of these caller streams
+    (torch.cuda.Stream or raw handles) alike -- every scratch buffer of each
+    grows to that buffer's largest size over the set."""
+    hs = [int(getattr(x, "cuda_stream", x)) for x in streams]
+    arr = (ctypes.c_void_p * len(hs))(*hs)
+    L = load()
+    st = ctypes.c_int(0)
+    L.tp_reserve_streams(ctypes.byref(ctypes.c_int(int(device))), arr, ctypes.byref(ctypes.c_int(len(hs))),
+                         ctypes.byref(st))
     check(st)
 
 

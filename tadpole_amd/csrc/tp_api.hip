@@ -101,11 +101,11 @@ static void devbuf_inject_failure() {
     }
 }
 
-void *DevBuf::get(size_t b) {
+void *DevBuf::get(size_t b, bool exact) {
     if (b == 0) b = 8;
     if (b > bytes) {
         if (p) g_devbuf_grows.fetch_add(1, std::memory_order_relaxed);
-        const size_t nb = std::max(b, bytes + bytes / 4);
+        const size_t nb = exact ? b : std::max(b, bytes + bytes / 4);
         hipMemPool_t pool = (g_devbuf_async && owner && owner->cur) ? lib_pool(owner->device) : nullptr;
         // the old block goes first; bytes / pooled describe what p holds at every
         // point, so a failed allocation below leaves an empty buffer (p null,
@@ -995,6 +995,34 @@ void tp_release_stream(const int *device, void *stream, int *status) {
     guarded(status, [&] {
         if (!stream) fail(TP_ERR_ARG, "tp_release_stream: NULL stream (the library stream is freed by tp_shutdown)");
         (void)ctx_release_stream(dev_of(device), (hipStream_t)stream);
+    });
+}
+
+/* Size the scratch of the contexts of `nstreams` caller streams alike: every
+ * scratch buffer of each becomes at least as large as the largest of that
+ * buffer over the set (stream-ordered allocation on each stream, no data
+ * kept).  A pool of streams that any matrix of a workload may land on (genome
+ * runs) then regrows no scratch once each matrix has run on one of them. */
+void tp_reserve_streams(const int *device, void *const *streams, const int *nstreams, int *status) {
+    guarded(status, [&] {
+        const int ns = *nstreams;
+        if (ns < 1 || !streams) fail(TP_ERR_ARG, "tp_reserve_streams: no streams");
+        std::vector<Ctx *> cs;
+        for (int q = 0; q < ns; ++q) {
+            if (!streams[q]) fail(TP_ERR_ARG, "tp_reserve_streams: NULL stream");
+            cs.push_back(&ctx_for(dev_of(device), (hipStream_t)streams[q]));   // locked until the call ends
+        }
+        for (int b = 0; b < S_NSLOT; ++b) {
+            size_t mx = 0;
+            for (Ctx *c : cs) mx = std::max(mx, c->buf[b].bytes);
+            if (!mx) continue;
+            for (Ctx *c : cs) {
+                if (c->buf[b].bytes >= mx) continue;
+                c->cur = c->stream;
+                (void)c->buf[b].get(mx, true);   // exactly the largest: no headroom to leapfrog it
+            }
+        }
+        for (Ctx *c : cs) TP_HIP(hipStreamSynchronize(c->stream));
     });
 }
 

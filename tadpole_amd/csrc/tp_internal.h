@@ -33,7 +33,7 @@ struct DevBuf {
     size_t bytes = 0;
     Ctx *owner = nullptr;   // the context whose streams use the block
     bool pooled = false;    // from the device's stream-ordered pool (hipMallocAsync)
-    void *get(size_t b);
+    void *get(size_t b, bool exact = false);   // exact: grow to b, not b or 1.25x the old size
     template <class T> T *as(size_t count) { return static_cast<T *>(get(count * sizeof(T))); }
     void release();
 };

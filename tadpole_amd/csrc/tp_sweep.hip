@@ -897,13 +897,16 @@ constexpr int CB_W = 8;      // waves a tree = most candidates a batch
 constexpr int CB_CAP = 16;   // positions <= T ranked a batch (16 x 16 lane pairs)
 constexpr int CB_FMAX = 16;  // flagged blocks a batch (two a wave)
 constexpr int CB_SEG = 8;    // positions <= T a wave may contribute
+constexpr int CB_NMIN = 3;   // rescan when the maintained candidate set holds fewer
 static_assert(CB_W * CB_SEG == 64, "one segment entry a lane");
 struct CbShared {
     double sgc[CB_W * CB_SEG];   // the waves' segments: positions <= T and their costs
     int sgp[CB_W * CB_SEG];
     int segn[CB_W];
-    double ccost[CB_CAP];
+    double ccost[CB_CAP];   // the candidate set: every position with cost <= sT (sN of them; -1: rescan)
     int cpos[CB_CAP];
+    double sT;
+    int sN;
     double key[CB_W], cl[CB_W], cr[CB_W], hgt[CB_W];
     int spos[CB_W], ka[CB_W];
     int4 win[CB_W];   // (lo, hi, ls, r): positions covered by LS..R, the neighbours (-1: none)
@@ -997,6 +1000,8 @@ __device__ __forceinline__ void coniss_tree_b(const SweepDev &sd, double *cost0,
     }
     __syncthreads();
 
+    if (threadIdx.x == 0) sh.sN = -1;   // (read after the barrier below the initial costs' one)
+    __syncthreads();
     double h = 0.0;      // wave 0: the height so far
     double gap = -1.0;   // T = g + gap (every wave the same), adapted to about 6..10 positions <= T
     // waves j < kc: candidate j's window, merged sums, key and new costs
@@ -1013,8 +1018,10 @@ __device__ __forceinline__ void coniss_tree_b(const SweepDev &sd, double *cost0,
         // every wave; try 6 takes only the ties at g, try 7 the exact argmin)
         double gq = 0.0;
         bool single = false;
-        int C = 0;
-        {
+        int C = __builtin_amdgcn_readfirstlane(sh.sN);
+        double Tu = 0.0;   // the T of a successful scan
+        const bool rescan = C < CB_NMIN;
+        if (rescan) {
             double bm[BS];
 #pragma unroll
             for (int q = 0; q < BS; ++q) bm[q] = 64 * q + lane < nbk ? bmin[64 * q + lane] : QNAN;
@@ -1072,6 +1079,7 @@ __device__ __forceinline__ void coniss_tree_b(const SweepDev &sd, double *cost0,
                 const int mx = max(max(max(c0_, c1_), max(c2_, c3_)), max(max(c4_, c5_), max(c6_, c7_)));
                 if (tot <= CB_CAP && mx <= CB_SEG && tot >= 1) {
                     C = tot;
+                    Tu = T;
                     if (tries <= 5) gap *= C < 6 ? 1.3 : (C > 10 ? 0.8 : 1.0);   // next batch: ~6..10 positions <= T
                     break;
                 }
@@ -1089,15 +1097,18 @@ __device__ __forceinline__ void coniss_tree_b(const SweepDev &sd, double *cost0,
         if (w == 0) {
             int Kc;
             if (!single) {
-                // the segments compacted: lane l holds entry l & 7 of wave l >> 3
-                const bool valid = (lane & (CB_SEG - 1)) < sh.segn[lane >> 3];
-                const double cv = sh.sgc[lane];
-                const int cp = sh.sgp[lane];
-                const unsigned long long mv = __ballot(valid);
-                const int idx = mbcnt64(mv);
-                if (valid) {
-                    sh.ccost[idx] = cv;
-                    sh.cpos[idx] = cp;
+                if (rescan) {
+                    // the segments compacted into the set: lane l holds entry l & 7 of wave l >> 3
+                    const bool valid = (lane & (CB_SEG - 1)) < sh.segn[lane >> 3];
+                    const double cv = sh.sgc[lane];
+                    const int cp = sh.sgp[lane];
+                    const unsigned long long mv = __ballot(valid);
+                    const int idx = mbcnt64(mv);
+                    if (valid) {
+                        sh.ccost[idx] = cv;
+                        sh.cpos[idx] = cp;
+                    }
+                    if (lane == 0) sh.sT = Tu;
                 }
                 // ranks: lane l compares candidate i = 4 p + (l >> 4) with j = l & 15
                 const int j = lane & 15;
@@ -1230,6 +1241,45 @@ __device__ __forceinline__ void coniss_tree_b(const SweepDev &sd, double *cost0,
             }
             if (lane == 0) sh.cnt = cnt;
             if (STAMPS) st_acc[13] += cnt;
+            // the candidate set after the run: drop the changed positions (a, b
+            // and ls of every merge), add the new costs <= T -- still every
+            // position with cost <= T (costs change only there)
+            if (single) {
+                if (lane == 0) sh.sN = -1;
+            } else {
+                const double sT = sh.sT;
+                const double ce = sh.ccost[lane & (CB_CAP - 1)];
+                const int pe = sh.cpos[lane & (CB_CAP - 1)];
+                // lane pairs (entry e = 8 h + (l >> 3), merge q = l & 7 -- this
+                // lane's slot sj): does merge q change entry e's position?
+                const int pe0 = sh.cpos[lane >> 3], pe1 = sh.cpos[8 + (lane >> 3)];
+                const bool onq = sj < cnt;
+                const unsigned long long r0 = __ballot(onq && (pe0 == aj || pe0 == x2.x || pe0 == wj.z));
+                const unsigned long long r1 = __ballot(onq && (pe1 == aj || pe1 == x2.x || pe1 == wj.z));
+                const int le = lane & (CB_CAP - 1);
+                const bool rm = ((le < 8 ? r0 : r1) >> (8 * (le & 7))) & 0xFFull;
+                const bool keep = lane < C && !rm;
+                const bool addl = lane < cnt && wj.z >= 0 && clj <= sT;
+                const bool addr = lane < cnt && wj.w >= 0 && crj <= sT;
+                const unsigned long long mk = __ballot(keep), ml = __ballot(addl), mr = __ballot(addr);
+                const int nk = __popcll(mk), nl = __popcll(ml), nr = __popcll(mr);
+                if (nk + nl + nr <= CB_CAP) {
+                    // (every lane read the old set above: in-order LDS, the writes come after)
+                    if (keep) {
+                        sh.ccost[mbcnt64(mk)] = ce;
+                        sh.cpos[mbcnt64(mk)] = pe;
+                    }
+                    if (addl) {
+                        sh.ccost[nk + mbcnt64(ml)] = clj;
+                        sh.cpos[nk + mbcnt64(ml)] = wj.z;
+                    }
+                    if (addr) {
+                        sh.ccost[nk + nl + mbcnt64(mr)] = crj;
+                        sh.cpos[nk + nl + mbcnt64(mr)] = aj;
+                    }
+                }
+                if (lane == 0) sh.sN = nk + nl + nr <= CB_CAP ? nk + nl + nr : -1;
+            }
         }
         TP_BSTAMP(4);
         lds_barrier();   // B3
@@ -1887,10 +1937,10 @@ static void launch_coniss_bs(const SweepDev &sd, double *cost0, size_t lds, hipS
     hipLaunchKernelGGL((k_coniss_t<STAMPS, BS, GLB, LU>), dim3(sd.ntrees), dim3(128), lds, s, sd, cost0);
 }
 int g_coniss_lu = 1;   // 0: the global variant keeps its links in global memory too
-// knob 52: the batched CONISS kernel (k_coniss_b) where it applies -- 1: not for
-// lean sweeps (a tree holds a whole CU: 8 waves, ~130 KB of LDS), 2: also for
-// them, 0: never (the two-wave k_coniss_t)
-int g_coniss_batch = 1;
+// knob 52: the batched CONISS kernel (k_coniss_b) where it applies (costs and
+// links in LDS, k <= 256) -- 2 (default): also for lean sweeps (C4, 8 streams:
+// 0.265 -> 0.229 s), 1: not for them, 0: never (the two-wave k_coniss_t)
+int g_coniss_batch = 2;
 // lean sweeps (another pipeline in flight on the device) of matrices that fit
 // LDS, from this many bins (knob 48; 0: never): costs global and only the
 // links in LDS (2 bytes a bin) so several trees share a CU -- the LDS

@@ -63,7 +63,7 @@ def matrix_cost(n_bins: int) -> float:
 def run_genome(matrices: Mapping[str, object], sizes: Optional[Mapping[str, int]] = None,
                runner: Optional[Callable[[str, object, int], object]] = None, streams: int = 8,
                retries: int = 1, phases: Optional[Dict[str, Dict[str, float]]] = None,
-               **tadpole_kwargs) -> Tuple[Dict[str, object], Dict[str, float]]:
+               presize: bool = True, **tadpole_kwargs) -> Tuple[Dict[str, object], Dict[str, float]]:
     """Process every chromosome once across the ranks of the default process
     group (or locally when torch.distributed is not initialised).
 
@@ -81,6 +81,12 @@ def run_genome(matrices: Mapping[str, object], sizes: Optional[Mapping[str, int]
     ``phases`` (optional, filled on this rank): per chromosome the seconds it
     waited for a stream worker (``wait``), then the result's ``host_s``
     (``upload``, ``call``, ``assemble``) when the runner reports them.
+    ``presize``: with several streams any stream may receive any chromosome,
+    so after the chromosomes have run, every context of the pool is sized
+    like the largest (``_lib.reserve_streams``: each scratch buffer to its
+    largest size over the pool, allocation only): later calls on the same
+    genome regrow no scratch whichever stream receives which chromosome (each
+    regrowth re-allocates a buffer on the stream).
     """
     import torch.distributed as dist
 
@@ -145,6 +151,18 @@ def run_genome(matrices: Mapping[str, object], sizes: Optional[Mapping[str, int]
 
             for f in [ex.submit(one, name, run_stream) for name in plan[rank]]:
                 f.result()
+            if presize:
+                # every chromosome has now run on some stream of the pool: size
+                # all of its contexts alike (each buffer to its largest size
+                # over the pool), so later calls regrow no scratch whichever
+                # stream receives which chromosome
+                from . import _lib
+                held = [free.get() for _ in range(streams)]
+                try:
+                    _lib.reserve_streams(held, device=local)
+                finally:
+                    for st in held:
+                        free.put(st)
         else:
             for name in plan[rank]:
                 one(name, runner)

@@ -241,3 +241,20 @@ def test_progress_word_reports_stages(gpu):
     assert vals == sorted(vals) and vals[-1] == 4 and 3 in vals, seen
     import tadpole_amd as tp
     tp.release_stream(s)
+
+
+def test_run_genome_presized_contexts_do_not_regrow(gpu):
+    """Verdict r5 item 7: run_genome sizes its pool's stream contexts for the
+    largest chromosome once (presize), so later calls regrow no scratch
+    whichever stream receives which chromosome (knob 41 counts regrowths)."""
+    from tadpole_amd import _lib
+    from tadpole_amd.genome import run_genome
+    mats = {f"c{i}": synth_hic(500 + 150 * i, 80 + i) for i in range(6)}
+    a, _ = run_genome(mats, streams=3, max_pcs=60)
+    _lib.debug_knob(41, 0)
+    for _ in range(2):
+        b, _ = run_genome(mats, streams=3, max_pcs=60)
+    grows = _lib.debug_knob(41, 0)
+    assert grows == 0, grows
+    for c in mats:
+        assert _same(a[c], b[c]), c

@@ -8,6 +8,7 @@ tools/coniss_batch_emu.py"""
 import sys, numpy as np
 NAN = float('nan')
 W, CAP, FMAX, SEG = 8, 16, 16, 8   # SEG: positions <= T a wave may contribute (CB_SEG)
+NMIN = 3                           # rescan when the maintained set holds fewer (CB_NMIN)
 
 def ward(sa, na, sb, nb):
     e = sa * nb - sb * na
@@ -52,7 +53,7 @@ def kernel(p):
         assert 0 <= i < lst, ("link index", i); return int(link[i])
     def lds_rn(i):
         assert 0 <= i < lst, ("rn index", i); return int(rn[i])
-    merges = []; s = 0; gap = -1.0; h = 0.0; nbatch = 0
+    merges = []; s = 0; gap = -1.0; h = 0.0; nbatch = 0; Sset = None; Tset = None; nscan = 0
     sgc = [NAN] * (W * SEG); sgp = [-(10**9)] * (W * SEG)
     while s < n - 1:
         nbatch += 1
@@ -61,7 +62,11 @@ def kernel(p):
         gq = min(allv)
         if not (gap > 0.0): gap = 0.5 * gq if (gq > 0.0 and gq < 1e300) else 1e-300
         tries = 0; C = 0; cands = None
-        while True:
+        rescan = Sset is None or len(Sset) < NMIN
+        if not rescan:
+            cands = list(Sset); C = len(cands); T = Tset
+        nscan += rescan
+        while rescan:
             T = gq + gap
             if not (T >= gq) or tries >= 6: T = gq
             segn = [0] * W
@@ -97,12 +102,12 @@ def kernel(p):
                 else:
                     segn[w] = SEG + 1
             if max(segn) <= SEG and CAP >= sum(segn) >= 1:
-                C = sum(segn); cands = ent
+                C = sum(segn); cands = ent; Tset = T
                 if tries <= 5: gap *= 1.3 if C < 6 else (0.8 if C > 10 else 1.0)
                 break
             if tries >= 6:                                 # the exact argmin alone
                 pos = min([q_ for q_ in range(n) if cost[q_] == gq])
-                cands = [(gq, pos)]; C = 1; T = None
+                cands = [(gq, pos)]; C = 1; T = None; Tset = None
                 break
             gap *= 0.5; tries += 1
         for (cc, pp) in cands: assert 0 <= pp < n and cost[pp] == cc, ("cand", pp, cc)
@@ -149,6 +154,22 @@ def kernel(p):
             x = rec[j]
             cost[x['b']] = NAN; cost[x['a']] = x['cr']; link[x['a']] = x['eb']; link[x['eb']] = x['a']; rn[x['a']] = x['er']
             if x['ls'] >= 0: cost[x['ls']] = x['cl']; rn[x['ls']] = x['eb']
+        # the maintained set: drop the changed positions, add the new costs <= T
+        if T is None:
+            Sset = None
+        else:
+            chg = set()
+            for j in range(cnt):
+                chg |= {rec[j]['a'], rec[j]['b']} | ({rec[j]['ls']} if rec[j]['ls'] >= 0 else set())
+            ns = [(cc, pp) for (cc, pp) in cands if pp not in chg]
+            for j in range(cnt):
+                x = rec[j]
+                if x['ls'] >= 0 and x['cl'] <= Tset: ns.append((x['cl'], x['ls']))
+                if x['r'] >= 0 and x['cr'] <= Tset: ns.append((x['cr'], x['a']))
+            Sset = ns if len(ns) <= CAP else None
+            if Sset is not None:
+                exact = sorted([q_ for q_ in range(n) if cost[q_] <= Tset])
+                assert sorted(pp for _, pp in Sset) == exact, "maintained set not exact"
         for j in range(cnt):
             x = rec[j]
             rows[x['a']] = x['sm']
@@ -157,7 +178,7 @@ def kernel(p):
                 seg = cost[blk*64:blk*64+64]
                 bmin[blk] = NAN if np.all(np.isnan(seg)) else np.nanmin(seg)
         s += cnt
-    return merges, nbatch
+    return merges, (nbatch, nscan)
 
 def structured(n, k, seed):
     r = np.random.default_rng(seed)
@@ -173,7 +194,7 @@ if __name__ == "__main__":
         ref = seq_coniss(p)
         got, nb = kernel(p)
         ok = [(a, b) for a, b, _ in got] == [(a, b) for a, b, _ in ref]
-        print(f"n={n} k={k}: same merges {ok}, batches {nb} ({(n-1)/nb:.2f} merges each)", flush=True)
+        print(f"n={n} k={k}: same merges {ok}, batches {nb[0]} ({(n-1)/nb[0]:.2f} merges each), scans {nb[1]}", flush=True)
         assert ok
     # ties: duplicate rows
     p = np.repeat(structured(40, 2, 3), 5, axis=0)

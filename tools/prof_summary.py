@@ -21,7 +21,7 @@ OUT = os.path.join(ROOT, "gpurun_out")
 # bench.py kernel class -> name prefixes of the kernels one launch of that class
 # runs; per prefix the variant with the largest total time in the trace is taken
 # (the CONISS block size and the GEMM tile are chosen per problem size)
-CLASSES = {"coniss": ["tp::k_coniss_t<false,"],
+CLASSES = {"coniss": ["tp::k_coniss_"],   # k_coniss_b (batched, round 6) or k_coniss_t
            "ch": ["tp::k_ch_cut", "tp::k_ch_segstat", "tp::k_ch<"],
            "xtx_gemm": ["tp::k_xtx_i8_"]}
 
