@@ -53,7 +53,6 @@ std::atomic<int> g_devbuf_grows{0};   // knob 41 (read / reset): scratch regrowt
 // context's stream, the device pool keeping what is freed) instead of a
 // device-wide sync + hipFree + hipMalloc, which stalled every stream of a
 // genome run (C4: ~35 regrowths a run while contexts meet larger chromosomes)
-int g_devbuf_async = 1;
 
 // The library's own stream-ordered pool per device (hipMemPoolCreate): scratch
 // regrowth frees into it and takes from it without a device sync, and it keeps
@@ -93,10 +92,12 @@ static void lib_pool_trim(int device) {
 
 // knob 51 (test hook): the next N scratch allocations fail as out-of-memory
 // (after the old block is gone, where a real hipMalloc failure would strike)
-int g_devbuf_fail_inject = 0;
+std::atomic<int> g_devbuf_fail_inject{0};   // hook 51: the next N allocations fail
 static void devbuf_inject_failure() {
-    if (g_devbuf_fail_inject > 0) {
-        --g_devbuf_fail_inject;
+    int inj = g_devbuf_fail_inject.load();
+    while (inj > 0 && !g_devbuf_fail_inject.compare_exchange_weak(inj, inj - 1)) {
+    }
+    if (inj > 0) {
         fail(TP_ERR_HIP, "scratch allocation failed (injected out-of-memory, knob 51)");
     }
 }
@@ -106,7 +107,7 @@ void *DevBuf::get(size_t b, bool exact) {
     if (b > bytes) {
         if (p) g_devbuf_grows.fetch_add(1, std::memory_order_relaxed);
         const size_t nb = exact ? b : std::max(b, bytes + bytes / 4);
-        hipMemPool_t pool = (g_devbuf_async && owner && owner->cur) ? lib_pool(owner->device) : nullptr;
+        hipMemPool_t pool = (cfg_devbuf_async && owner && owner->cur) ? lib_pool(owner->device) : nullptr;
         // the old block goes first; bytes / pooled describe what p holds at every
         // point, so a failed allocation below leaves an empty buffer (p null,
         // bytes 0) that the next get() allocates again -- never a null block that
@@ -211,7 +212,7 @@ static hipEvent_t next_event(Ctx &c) {
     }
     return c.evpool[c.evnext++];
 }
-int g_kprof_fine = 1;
+std::atomic<int> g_kprof_fine{1};
 void kprof_begin(Ctx &c, int cls) {
     if (!c.prof || (cls == K_GQ_GEMM && !g_kprof_fine)) return;
     c.open_cls = cls;
@@ -579,7 +580,7 @@ static SweepOut run_sweep(Ctx &c, const double *d_Pt, int n, int k, int min_clus
     sd.min_clusters = min_clusters;
     // lean: asked for, or another pipeline is in flight on this device now
     // (concurrent streams: a tree of each fits on one CU; the same bits)
-    sd.lds_lean = c.lds_lean || (g_lean_auto && pipelines_in_flight(c.device) > 1);
+    sd.lds_lean = c.lds_lean || (cfg_lean_auto && pipelines_in_flight(c.device) > 1);
     double *sums = c.buf[S_SWEEP].as<double>(sweep_sums_doubles(n, 0, k));
     const size_t rec = (size_t)k * (n - 1);
     char *recbuf = c.buf[S_SWEEP2].as<char>(rec * (4 + 4 + 8 + 8) + 256);
@@ -597,7 +598,7 @@ static SweepOut run_sweep(Ctx &c, const double *d_Pt, int n, int k, int min_clus
     sd.iseg = c.buf[S_MISC].as<int>((size_t)k * (2 * sd.seg_cap + 2) + 64) + 64;
     sd.trS = (double *)(c.buf[S_NGOOD].as<char>(64)) + 2;
     sd.cost0 = c.buf[S_SMALL].as<double>(sweep_cost0_doubles(n, k, k));
-    if (g_ch_dedup) {   // CH segment statistics shared across trees
+    if (cfg_ch_dedup) {   // CH segment statistics shared across trees
         int hcap = 0, ucap = 0;
         const size_t bytes = sweep_dedup_bytes(n, k, k, sd.seg_cap, &hcap, &ucap);
         sweep_dedup_bind(sd, c.buf[S_DEDUP].as<char>(bytes), hcap, ucap);
@@ -737,7 +738,6 @@ static SweepOut run_sweep(Ctx &c, const double *d_Pt, int n, int k, int min_clus
 // ------------------------------------------------------------ pipeline
 static std::atomic<int> g_in_flight[64];
 int pipelines_in_flight(int device) { return g_in_flight[device & 63].load(); }
-int g_lean_auto = 1;
 
 struct PipeOut {
     int n_good = 0, k = 0;
@@ -859,7 +859,7 @@ static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_cl
     // S_jj) and builds its 2-slice image: no separate passes over X for them,
     // and X itself is written only if the fp64 product turns out to be needed
     // (non-integer counts: cor_product gathers it then)
-    const bool prep = g_xtx_fused && g_xtx_int8 && n >= 1024 && n <= 130000;
+    const bool prep = t_knob.xtx_fused && t_knob.xtx_int8 && n >= 1024 && n <= 130000;
     GatherStats gs{};
     double *X = nullptr;
     if (prep) {
@@ -888,7 +888,7 @@ static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_cl
     {
         const int R = shard_count(c);
         const int b_est = std::min(n, ((k + std::max(32, k / 4) + 31) / 32) * 32);
-        if (g_shard_slab && c.shard.active && R > 1 && prep && n >= g_pca_krylov_min && b_est < n) {
+        if (t_knob.shard_slab && c.shard.active && R > 1 && prep && n >= t_knob.pca_krylov_min && b_est < n) {
             const int ns = xtx_int_slices_cols(c, gs.cmax, gs.cbad, n);
             if (ns == 1 || ns == 2) {
                 use_slab = true;
@@ -904,7 +904,7 @@ static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_cl
     double *C = use_slab && slab.narrow ? c.buf[S_C].as<double>((size_t)n * (sc1 - sc0) + 64)
                                         : c.buf[S_C].as<double>(pca_c_doubles(n));
     // C's column means, for prcomp (C's tail, or the [m | 1] buffer of a slab)
-    double *cmean = use_slab ? c.buf[S_MEXT].as<double>(2 * (size_t)n) : (g_cor_fused ? C + (size_t)n * n : nullptr);
+    double *cmean = use_slab ? c.buf[S_MEXT].as<double>(2 * (size_t)n) : (cfg_cor_fused ? C + (size_t)n * n : nullptr);
     trace_mark(s, "cor: start");
     bool cm_defer = !use_slab;   // C's means in the PCA's digit pass when C comes from the int8 X'X
     cor_product(c, X, n, m, prep ? &gs : nullptr, nullptr, C, c.buf[S_DIAG].as<double>(n), cmean,
@@ -954,10 +954,24 @@ static PipeOut pipeline_dev(Ctx &c, double *d_M, int n0, int max_pcs, int min_cl
     return o;
 }
 
+thread_local Knobs t_knob;
+static std::mutex &knob_mu() {
+    static std::mutex m;
+    return m;
+}
+static Knobs &knob_set() {   // the process-wide values tp_debug_knob sets
+    static Knobs k;
+    return k;
+}
+
 template <class F> static void guarded(int *status, F &&f) {
     struct Unlock {
         ~Unlock() { ctx_unlock_held(); }
     } unlock;
+    {
+        std::lock_guard<std::mutex> lk(knob_mu());
+        t_knob = knob_set();   // this call's switches
+    }
     try {
         f();
         if (status) *status = TP_OK;
@@ -1815,7 +1829,7 @@ void tp_debug_sytrd(const double *H, const int *b, double *ms, long long *stamps
     });
 }
 /* one tridiagonalisation of H (b x b, lower triangle used) by k_sytrd_l
- * (which 0) or k_sytrd_reg (which 1): d[b], e[b-1], tau[b-1], Aout = A with
+ * (which 0) or k_sytrd32 (which 2): d[b], e[b-1], tau[b-1], Aout = A with
  * the reflectors below the subdiagonal; ms[0] = kernel time (mean of 3). */
 void tp_debug_sytrd2(const double *H, const int *b, const int *which, double *ms, double *d, double *e, double *tau,
                      double *Aout, int *status) {
@@ -1853,8 +1867,8 @@ void tp_debug_sytrd2(const double *H, const int *b, const int *which, double *ms
 extern "C" {
 /* S = X'X (n x n, column-major in and out) by mode 0 = fp64 MFMA GEMM, 1 = the
  * int8-exact path with 64-column tiles, 2 = the 128-column tile kernels of the
- * pipeline (knob 32 picks the LDS-DMA or the register-staged one; counts below
- * 16384) (fails with TP_ERR_ARG when X is not non-negative integer
+ * pipeline (k_xtx_i8_w, or with knob 44 = 0 the 128-tile LDS-DMA kernel;
+ * counts below 16384) (fails with TP_ERR_ARG when X is not non-negative integer
  * counts below 2^21); *slices = slices used (0 for fp64); ms = mean of 3. */
 void tp_debug_xtx(const double *X, const int *n, const int *mode, double *S, int *slices, double *ms,
                   int *status) {
@@ -1902,90 +1916,69 @@ void tp_debug_xtx(const double *X, const int *n, const int *mode, double *S, int
 }  // extern "C"
 
 extern "C" {
-/* Test hook: set a tuning switch, *old = its previous value.  which: 0 CH
- * segment statistics shared across trees, 1 cap on their store (0 = automatic),
- * 2 short-K panel GEMM, 3 GEMM LDS stage depth (16 / 32), 4 register-resident
- * tridiagonalisation, 5 int8 X'X, 6 PCA degree margin, 7 XCD-aware GEMM order, ..., 14 supertile
- * order of the int8 X'X tiles, ..., 17 C's column means formed by the correlation epilogue, 18 the
- * correlation epilogue in the int8 X'X store (with the gather's statistics), ..., 20 the PCA's block
- * Krylov space: 1 of C, 0 of G, -1 (default) of C from knob 31's bin count on, ..., 25 events around
- * every Krylov product when timings are requested (0: stage and one-launch classes only), 26 products
- * with the block-tridiagonal Krylov projection T skip its zero blocks (0: dense GEMM), 28 the
- * Krylov CGS2's first pass against the last two blocks only (0: against every block), 29 CholQR
- * Gram matrices of 64-column blocks by k_gram64 (0: the split-K GEMM; same bits), 30 the next N
- * sharded waits with a live communicator fail as device errors (failure-containment tests), 31 the
- * bins from which knob 20 = -1 (default) takes the Krylov space of C, ..., 36 the Krylov products with
- * C on the int8 MFMA from digit images (1, default: one LDS buffer, two workgroups a CU; 2: the
- * double-buffered one-workgroup kernel; 0: the fp64 k_gemm_ts), ..., 47 sweeps lean (CONISS link-only
- * in LDS) while another pipeline is in flight on the device (1, default), 48 the bins from which a
- * lean sweep of a matrix that fits LDS takes the global link-only variant (0: never), 49 the LDS
- * variant with one 16-bit link array, 10 bytes a bin (3, default: where the 16-byte one does not fit;
- * 1: lean sweeps, 2: every sweep, 0: never), 50 the NA -> 0 / symmetrise pass's tile edge (0, default: 128 from 16 384 bins, else 64;
- * 64 or 128 force one). */
+/* Test hook: set a run-time switch, *old = its previous value.  Switches (the
+ * process-wide values each C-ABI entry copies into its calling thread's set
+ * when it starts, so a call in flight keeps the set it started with):
+ *   1 cap on the shared CH segment store (0 = automatic; > 0 tests its
+ *     overflow path),
+ *   5 exact int8 X'X for integer counts (0: the fp64 MFMA product),
+ *   8 bins from which the block Krylov PCA replaces forming G,
+ *  18 the correlation epilogue in the int8 X'X store (0: X'X into S, then the
+ *     separate epilogue -- the path of counts past two slices and real data),
+ *  20 the PCA's Krylov space: 1 of C, 0 of G, -1 (default) of C from 10 000 bins,
+ *  24 C5 shards keep C row-sharded (0: C gathered whole),
+ *  36 the G-space Krylov products on int8 digit images (0: the fp64
+ *     k_gemm_ts; 1: k_pd_prod's 64-row tiles; 5, default: k_pd_prodA),
+ *  43 host uploads (bit 1: exact 16-bit count blocks travel packed, bit 0:
+ *     one block at a time),
+ *  44 the whole-triangle int8 X'X by k_xtx_i8_w's 256 x 128 tiles (0: 128-tiles),
+ *  45 the C-space Krylov products on int8 digit images (0: fp64),
+ *  48 the bins from which a lean sweep of a matrix that fits LDS takes the
+ *     global link-only CONISS (0: never),
+ *  49 the LDS CONISS with one 16-bit link array (3, default: where the 16-byte
+ *     variant does not fit; 1: lean sweeps; 2: every sweep; 0: never),
+ *  52 the batched CONISS (2, default: every sweep; 1: not lean ones; 0: never).
+ * Process-wide hooks (not path choices):
+ *  25 events around every Krylov product when timings are requested,
+ *  30 the next N sharded waits with a live communicator fail as device errors,
+ *  41 scratch regrowths so far (a counter: returned, then set to *value),
+ *  51 the next N scratch allocations fail as out-of-memory.
+ * Every other switch of earlier rounds is a compile-time constant now
+ * (tp_internal.h, cfg_*). */
 void tp_debug_knob(const int *which, const int *value, int *old, int *status) {
     guarded(status, [&] {
-        if (*which == 41) {   // a counter, not a switch: returns it and sets it to *value
-            *old = g_devbuf_grows.exchange(*value);
+        std::atomic<int> *h = nullptr;
+        switch (*which) {
+        case 25: h = &g_kprof_fine; break;
+        case 30: h = &g_shard_inject; break;
+        case 41: h = &g_devbuf_grows; break;
+        case 51: h = &g_devbuf_fail_inject; break;
+        default: break;
+        }
+        if (h) {
+            *old = h->exchange(*value);
             return;
         }
+        std::lock_guard<std::mutex> lk(knob_mu());
+        Knobs &k = knob_set();
         int *p = nullptr;
         switch (*which) {
-        case 0: p = &g_ch_dedup; break;
-        case 1: p = &g_ch_dedup_ucap; break;
-        case 2: p = &g_gemm_panel; break;
-        case 3: p = &g_gemm_kb; break;
-        case 4: p = &g_sytrd_reg; break;
-        case 5: p = &g_xtx_int8; break;
-        case 6: p = &g_pca_margin; break;
-        case 7: p = &g_gemm_xcd; break;
-        case 8: p = &g_pca_krylov_min; break;
-        case 9: p = &g_pca_krylov_block; break;
-        case 10: p = &g_pca_krylov_steps; break;
-        case 11: p = &g_chol_inv_waves; break;
-        case 12: p = &g_gemm_splitk; break;
-        case 13: p = &g_gemm_ts; break;
-        case 14: p = &g_xtx_supertile; break;
-        case 15: p = &g_pca_over; break;
-        case 16: p = &g_coniss_lu; break;
-        case 17: p = &g_cor_fused; break;
-        case 18: p = &g_xtx_fused; break;
-        case 19: p = &g_pca_cheb_fused; break;
-        case 20: p = &g_pca_ckrylov; break;
-        case 21: p = &g_ckry_chunk; break;
-        case 22: p = &g_ckry_steps; break;
-        case 23: p = &g_gemm_ts32; break;
-        case 24: p = &g_shard_slab; break;
-        case 25: p = &g_kprof_fine; break;
-        case 26: p = &g_pca_band; break;
-        case 28: p = &g_krylov_local; break;
-        case 29: p = &g_gram64; break;
-        case 30: p = &g_shard_inject; break;
-        case 31: p = &g_ckry_min; break;
-        case 32: p = &g_xtx_glds; break;
-        case 33: p = &g_ckry_local; break;
-        case 34: p = &g_xtx_nz; break;
-        case 35: p = &g_gemm_ts_pf2; break;
-        case 36: p = &g_prod_i8; break;
-        case 37: p = &g_sytrd32; break;
-        case 38: p = &g_pd_digits_blk; break;
-        case 39: p = &g_pd_cm; break;
-        case 40: p = &g_sync_spin_us; break;
-        case 42: p = &g_devbuf_async; break;
-        case 43: p = &g_upload_mode; break;
-        case 44: p = &g_xtx_w; break;
-        case 45: p = &g_pd_cspace; break;
-        case 46: p = &g_pd_digits_big; break;
-        case 47: p = &g_lean_auto; break;
-        case 48: p = &g_coniss_lean_min; break;
-        case 49: p = &g_coniss_lds2; break;
-        case 50: p = &g_clean_tile; break;
-        case 51: p = &g_devbuf_fail_inject; break;
-        case 52: p = &g_coniss_batch; break;
+        case 1: p = &k.ch_dedup_ucap; break;
+        case 5: p = &k.xtx_int8; break;
+        case 8: p = &k.pca_krylov_min; break;
+        case 18: p = &k.xtx_fused; break;
+        case 20: p = &k.pca_ckrylov; break;
+        case 24: p = &k.shard_slab; break;
+        case 36: p = &k.prod_i8; break;
+        case 43: p = &k.upload_mode; break;
+        case 44: p = &k.xtx_w; break;
+        case 45: p = &k.pd_cspace; break;
+        case 48: p = &k.coniss_lean_min; break;
+        case 49: p = &k.coniss_lds2; break;
+        case 52: p = &k.coniss_batch; break;
         default: fail(TP_ERR_ARG, "unknown knob");
         }
-        if (*which == 3 && *value != 16 && *value != 32) fail(TP_ERR_ARG, "stage depth must be 16 or 32");
-        if (*which == 9 && *value != 0 && (*value % 16 != 0 || *value > 256))
-            fail(TP_ERR_ARG, "Krylov block must be 0 or a multiple of 16 up to 256");
+        if (*which == 36 && *value != 0 && *value != 1 && *value != 5) fail(TP_ERR_ARG, "knob 36 takes 0, 1 or 5");
         *old = *p;
         *p = *value;
     });

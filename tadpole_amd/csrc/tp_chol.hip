@@ -620,7 +620,7 @@ template __global__ void k_chol_inv<8, 16>(double *, double *, double *, double 
 template __global__ void k_chol_inv<16, 16>(double *, double *, double *, double *, int, double, int *, long long *);
 template __global__ void k_chol_inv<4, 4>(double *, double *, double *, double *, int, double, int *, long long *);
 
-int g_chol_inv_waves = 0;   // 0: 4 waves for b <= 64, else 16; 4 / 8 / 16 force (diagnostics switch)
+thread_local int g_chol_inv_waves = 0;   // 0: 4 waves for b <= 64, else 16; 4 / 8 / 16 force (diagnostics switch)
 
 // ---------------------------------------------------------------------------
 // k_trsm_frag: Q = Z U^-1 = (Z S) U'^-1 from k_chol_inv's fragments, one

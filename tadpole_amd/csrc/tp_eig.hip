@@ -10,7 +10,7 @@
 //               p = A22 v of step j+1: one read + one write of the trailing
 //               matrix per step (L2-resident), column dots by wave reductions,
 //               row dots in per-lane registers (lane owns rows r = 64q + lane).
-//   k_sytrd_reg the same with the matrix in registers (b <= 256).
+//   k_sytrd32   the same with the matrix in registers as 32 x 32 tiles (b <= 256).
 //   k_bisect / k_invit  eigenpairs of T (Sturm bisection, inverse iteration).
 //   k_ormtr_l   C <- Q_H C: one wave per column of C, reflectors applied in
 //               reverse order with the column held in registers.
@@ -241,25 +241,7 @@ __global__ void __launch_bounds__(1024) k_sytrd_l(double *A, int b, double *d, d
 }
 
 // ---------------------------------------------------------------------------
-// k_sytrd_reg: the same reduction (same outputs and reflector storage as
-// k_sytrd_l) with the matrix resident in registers, for b = 16T <= 256.
-//
-// The upper triangle is cut into 16 x 16 tiles held in MFMA accumulator
-// layout (lane l, reg q = element (16I + (l>>4) + 4q, 16K + (l&15))).  Tile
-// rows are paired (p, T-1-p) -- T+1 tiles per pair -- and each pair is split
-// over two waves (<= 9 tiles, 72 VGPRs each), so every step's trailing tiles
-// spread evenly over 16 waves.  Step j (J = j / 16):
-//   1. the owners of tile row J publish row j (= column j) to LDS;
-//   2. wave 0 forms the reflector (dlarfg) -> v, tau, d[j], e[j];
-//   3. p = A22 v: per tile, row partials (lane products accumulated over the
-//      wave's tiles of one row, then a 16-lane DPP sum) and column partials
-//      (a 4-row-group sum by permlane16/32 swaps); off-diagonal tiles give
-//      both, diagonal tiles (full symmetric blocks) the row partial only;
-//   4. wave 0 assembles p in a fixed order, p'v, w = p - (tau/2)(p'v) v;
-//   5. every trailing tile applies A -= v w' + w v' in registers.
-// Four LDS-only barriers per step (the reflector's global store is never read
-// back by the kernel, so no barrier waits for it).
-// ---------------------------------------------------------------------------
+// Lane-exchange helpers of the register-resident tridiagonalisation (k_sytrd32).
 __device__ __forceinline__ double xor16_sum(double v) {   // v[l] + v[l ^ 16]
     int lo = __double2loint(v), hi = __double2hiint(v);
     auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
@@ -288,208 +270,12 @@ __device__ __forceinline__ int sy_opaque(int v) {
 }
 
 typedef double sy_d4 __attribute__((ext_vector_type(4)));
-constexpr int SR_SLOTS = 9;
 
-__global__ void __launch_bounds__(1024) k_sytrd_reg(double *A, int b, double *d, double *e, double *tau) {
-    __shared__ double xrow[256], vb[256], wb[256];
-    __shared__ double rowp[16][2][16];   // [wave][row slot][row in tile]
-    __shared__ double colp[16][16][16];  // [tile row I][tile col K][col in tile]
-    __shared__ double sc[4];
-    const int t = threadIdx.x, l = t & 63, lr = l >> 4, lc = l & 15;
-    const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-    const int T = b >> 4;
-    // ---- this wave's tiles: pair p = w / 2, rows p and T-1-p
-    const int p = w >> 1;
-    const bool pair_live = p < (T + 1) / 2;
-    const int r1 = p, r2 = T - 1 - p;
-    const int len = !pair_live ? 0 : (r1 == r2 ? T - p : T + 1);
-    const int half = (len + 1) / 2;
-    const int first = (w & 1) ? half : 0;
-    const int cnt = (w & 1) ? len - half : half;
-    int tc[SR_SLOTS];
-#pragma unroll
-    for (int s = 0; s < SR_SLOTS; ++s) {
-        int v = 255 << 8;
-        if (s < cnt) {
-            const int idx = first + s;
-            v = idx < T - p ? ((r1 << 8) | (r1 + idx)) : ((r2 << 8) | (r2 + idx - (T - p)));
-        }
-        tc[s] = __builtin_amdgcn_readfirstlane(v);
-    }
-#define TI(s) (sy_opaque(tc[s]) >> 8)
-#define TJ(s) (sy_opaque(tc[s]) & 255)
-#define LIVE(s) (TI(s) != 255)
-#define RSLOT(s) (TI(s) == r1 ? 0 : 1)
-    sy_d4 a[SR_SLOTS];
-#pragma unroll
-    for (int s = 0; s < SR_SLOTS; ++s) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            // element (R, C) from the lower triangle (A[max][min], col-major):
-            // contiguous along the 16 lanes of a row for off-diagonal tiles
-            const int R = 16 * TI(s) + lr + 4 * q, C = 16 * TJ(s) + lc;
-            a[s][q] = LIVE(s) ? A[(size_t)min(R, C) * b + max(R, C)] : 0.0;
-        }
-    }
-    __syncthreads();   // all loads done before reflectors are written into A
-    for (int j = 0; j + 2 < b; ++j) {
-        const int J = j >> 4, jj = j & 15;
-        // ---- 1. row j
-#pragma unroll
-        for (int s = 0; s < SR_SLOTS; ++s) {
-            if (TI(s) == J && lr == (jj & 3)) {
-                const int C = 16 * TJ(s) + lc;
-                xrow[C] = a[s][jj >> 2];
-            }
-        }
-        lds_barrier();
-        // ---- 2. reflector (LAPACK dlarfg conventions, as k_sytrd_l)
-        if (w == 0) {
-            double xs = 0.0;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int c = l + 64 * q;
-                if (c >= j + 2 && c < b) {
-                    const double x = xrow[c];
-                    xs = fma(x, x, xs);
-                }
-            }
-            const double xnorm2 = wave_sum(xs);
-            const double alpha = xrow[j + 1];
-            double beta, tj, scale;
-            if (xnorm2 == 0.0) {
-                beta = alpha;
-                tj = 0.0;
-                scale = 0.0;
-            } else {
-                beta = -copysign(sqrt(fma(alpha, alpha, xnorm2)), alpha);
-                tj = (beta - alpha) / beta;
-                scale = 1.0 / (alpha - beta);
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int c = l + 64 * q;
-                double v = 0.0;
-                if (c == j + 1) v = 1.0;
-                else if (c >= j + 2 && c < b) {
-                    v = xrow[c] * scale;
-                    A[(size_t)j * b + c] = v;
-                }
-                vb[c] = v;
-            }
-            if (l == 0) {
-                d[j] = xrow[j];
-                e[j] = beta;
-                tau[j] = tj;
-                sc[0] = tj;
-            }
-        }
-        lds_barrier();
-        // ---- 3. partials of p = A22 v over the trailing tiles (tile row >= J)
-        {
-            double acc[2][4] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
-#pragma unroll
-            for (int s = 0; s < SR_SLOTS; ++s) {
-                if (LIVE(s) && TI(s) >= J) {
-                    const int I = TI(s), K = TJ(s);
-                    const double vK = vb[16 * K + lc];
-                    double cp = 0.0;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const double x = a[s][q];
-                        if (RSLOT(s) == 0) acc[0][q] = fma(x, vK, acc[0][q]);
-                        else acc[1][q] = fma(x, vK, acc[1][q]);
-                        cp = fma(x, vb[16 * I + lr + 4 * q], cp);
-                    }
-                    if (I != K) {
-                        cp = xor16_sum(cp);
-                        cp = xor32_sum(cp);
-                        if (l < 16) colp[I][K][lc] = cp;
-                    }
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
-#pragma unroll
-            for (int rs = 0; rs < 2; ++rs)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const double v = row16_sum(acc[rs][q]);
-                    if (lc == 0) rowp[w][rs][lr + 4 * q] = v;
-                }
-        }
-        lds_barrier();
-        // ---- 4. p (fixed order), p'v, w
-        if (w == 0) {
-            const double tj = sc[0];
-            double pv = 0.0, pc[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int c = l + 64 * q;
-                pc[q] = 0.0;
-                if (c > j && c < b) {
-                    const int I = c >> 4, cc = c & 15;
-                    const int pp = min(I, T - 1 - I);
-                    const int rs = I == pp ? 0 : 1;
-                    double sum = rowp[2 * pp][rs][cc] + rowp[2 * pp + 1][rs][cc];
-                    for (int I2 = J; I2 < I; ++I2) sum = sum + colp[I2][I][cc];
-                    pc[q] = tj * sum;
-                    pv = fma(pc[q], vb[c], pv);
-                }
-            }
-            const double dot = wave_sum(pv);
-            const double alpha2 = -0.5 * tj * dot;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int c = l + 64 * q;
-                wb[c] = (c > j && c < b) ? fma(alpha2, vb[c], pc[q]) : 0.0;
-            }
-        }
-        lds_barrier();
-        // ---- 5. A -= v w' + w v' on the trailing tiles
-#pragma unroll
-        for (int s = 0; s < SR_SLOTS; ++s) {
-            if (LIVE(s) && TI(s) >= J) {
-                const int I = TI(s), K = TJ(s);
-                const double vC = vb[16 * K + lc], wC = wb[16 * K + lc];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int R = 16 * I + lr + 4 * q;
-                    a[s][q] = fma(-vb[R], wC, fma(-wb[R], vC, a[s][q]));
-                }
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    }
-    // ---- last 2 x 2 block (rows b-2, b-1 of tile (T-1, T-1))
-#pragma unroll
-    for (int s = 0; s < SR_SLOTS; ++s) {
-        if (TI(s) == T - 1 && TJ(s) == T - 1) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int rl = lr + 4 * q;
-                if (rl >= 14) rowp[0][rl - 14][lc] = a[s][q];   // rows 14, 15 of the tile
-            }
-        }
-    }
-    __syncthreads();
-    if (t == 0) {
-        const int j = b - 2;
-        d[j] = rowp[0][0][14];
-        d[j + 1] = rowp[0][1][15];
-        e[j] = rowp[0][1][14];
-        tau[j] = 0.0;
-    }
-#undef TI
-#undef TJ
-#undef LIVE
-#undef RSLOT
-}
-bool sytrd_reg_supported(int b) { return b >= 16 && b <= 256 && b % 16 == 0; }
 
 // ---------------------------------------------------------------------------
 // k_sytrd32: the same reduction and outputs (LAPACK dsytd2 'L'), b <= 256,
 // with the upper triangle in registers as 32 x 32 tiles and three barriers a
-// step.  Built to cut the per-step cost of k_sytrd_reg (~14 k cycles: the
+// step.  Built to cut the per-step cost of k_sytrd_reg (removed in round 6; ~14 k cycles: the
 // 16 x 16 tiles need a 16-lane reduction per tile row, and wave 0 alone forms
 // the reflector and assembles p in long LDS chains while 15 waves wait).
 //
@@ -790,7 +576,6 @@ __global__ void __launch_bounds__(64 * S32_W) k_sytrd32(double *A, int b, double
 #undef S32_K
 }
 bool sytrd32_supported(int b) { return b >= 3 && b <= 256; }
-int g_sytrd32 = 1;   // knob 37: 0 = k_sytrd_reg (16 x 16 tiles)
 
 // C <- Q_H C, Q_H = H_0 H_1 ... H_{b-3}: one wave per column of C (b x b, ldc = b)
 template <int QM>
@@ -1072,7 +857,6 @@ __global__ void __launch_bounds__(64 * NV) k_invit(const double *d, const double
 }
 
 bool eig_sym_supported(int b) { return b >= 1 && b <= EIG_BMAX; }
-int g_sytrd_reg = 1;   // diagnostics switch: 0 = the L2-resident k_sytrd_l
 
 // In place: A (b x b, lower triangle of a symmetric matrix) <- eigenvectors,
 // theta <- eigenvalues ascending, b <= EIG_BMAX (1280: k <= 1024).  work: >=
@@ -1082,10 +866,8 @@ int g_sytrd_reg = 1;   // diagnostics switch: 0 = the L2-resident k_sytrd_l
 void eig_sym(double *A, int b, double *theta, double *work, hipStream_t s) {
     if (!eig_sym_supported(b)) fail(TP_ERR_UNSUPPORTED, "eig_sym: b > 1280 (EIG_BMAX)");
     double *C = work, *e = C + (size_t)b * b, *tau = e + b, *dg = tau + b, *lam = dg + b;   // lam: b + 1
-    if (g_sytrd32 && sytrd32_supported(b))
+    if (sytrd32_supported(b))
         hipLaunchKernelGGL((k_sytrd32<false>), dim3(1), dim3(64 * S32_W), 0, s, A, b, dg, e, tau, (long long *)nullptr);
-    else if (sytrd_reg_supported(b) && g_sytrd_reg)
-        hipLaunchKernelGGL(k_sytrd_reg, dim3(1), dim3(1024), 0, s, A, b, dg, e, tau);
     else if (b <= 256)
         hipLaunchKernelGGL((k_sytrd_l<4, false>), dim3(1), dim3(1024), 0, s, A, b, dg, e, tau, (long long *)nullptr);
     else if (b <= 512)
@@ -1116,7 +898,7 @@ void eig_sym(double *A, int b, double *theta, double *work, hipStream_t s) {
     TP_HIP(hipMemcpyAsync(A, C, (size_t)b * b * sizeof(double), hipMemcpyDeviceToDevice, s));
 }
 
-// diagnostic: one tridiagonalisation by either kernel (which: 0 k_sytrd_l, 1 k_sytrd_reg, 2 k_sytrd32)
+// diagnostic: one tridiagonalisation by either kernel (which: 0 k_sytrd_l, 2 k_sytrd32)
 void sytrd_which(double *A, int b, double *work, int which, hipStream_t s, long long *d_stamps) {
     double *e = work, *tau = e + b, *dg = tau + b;
     (void)d_stamps;
@@ -1124,8 +906,7 @@ void sytrd_which(double *A, int b, double *work, int which, hipStream_t s, long 
         if (!sytrd32_supported(b)) fail(TP_ERR_ARG, "k_sytrd32: b must be 3..256");
         hipLaunchKernelGGL((k_sytrd32<false>), dim3(1), dim3(64 * S32_W), 0, s, A, b, dg, e, tau, (long long *)nullptr);
     } else if (which == 1) {
-        if (!sytrd_reg_supported(b)) fail(TP_ERR_ARG, "k_sytrd_reg: b must be 16..256, a multiple of 16");
-        hipLaunchKernelGGL(k_sytrd_reg, dim3(1), dim3(1024), 0, s, A, b, dg, e, tau);
+        fail(TP_ERR_ARG, "k_sytrd_reg (which 1) was removed in round 6 (k_sytrd32 replaced it)");
     } else if (b <= 256) {
         hipLaunchKernelGGL((k_sytrd_l<4, false>), dim3(1), dim3(1024), 0, s, A, b, dg, e, tau, (long long *)nullptr);
     } else if (b <= 512) {

@@ -187,8 +187,7 @@ __global__ void __launch_bounds__(256) k_gemm_f64(int M, int N, int K, const dou
                 }
             }
 }
-int g_gemm_xcd = 1;   // XCD-aware workgroup order (0: linear; A/B tests)
-int g_gemm_kb = 16;   // k depth of the 64 x 64 kernel's LDS stages (16 / 32; same bits; 32 measured no faster)
+thread_local int g_gemm_kb = 16;   // k depth of the 64 x 64 kernel's LDS stages (16 / 32; same bits; 32 measured no faster)
 
 // ---------------------------------------------------------------------------
 // Large products: 128 x 128 output tile per 256-thread workgroup, each wave a
@@ -405,7 +404,7 @@ __global__ void __launch_bounds__(256) k_gemm_f64_panel(int M, int N, int K, con
             }
         }
 }
-int g_gemm_panel = 1;   // 0: tall-skinny products take the split-K 64 x 64 path (A/B tests)
+thread_local int g_gemm_panel = 1;   // 0: tall-skinny products take the split-K 64 x 64 path (A/B tests)
 
 // ---------------------------------------------------------------------------
 // Long-K tall-skinny products C = A'B with A k-contiguous (the PCA's Xc K_t,
@@ -420,7 +419,7 @@ int g_gemm_panel = 1;   // 0: tall-skinny products take the split-K 64 x 64 path
 // TN = 32 (the C-Krylov blocks): a 128 x 32 tile, each wave 32 x 32 (2 x 2
 // accumulators); same k order, so the bits of a column do not depend on TN.
 constexpr int TSM = 128, TSN = 64, TSK = 16, TSLD = TSK + GPAD;
-template <int TAG, int TN = TSN, bool PF2 = false>
+template <int TAG, int TN = TSN>
 __global__ void __launch_bounds__(256, 2) k_gemm_ts(int M, int N, int K, const double *__restrict__ A, int lda,
                                                     const double *__restrict__ B, int ldb, double *__restrict__ C,
                                                     int ldc, int store_t, int kchunk, size_t part_stride) {
@@ -484,74 +483,19 @@ __global__ void __launch_bounds__(256, 2) k_gemm_ts(int M, int N, int K, const d
                     acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[a], bf[b], acc[a][b], 0, 0, 0);
         }
     };
-    if constexpr (PF2) {
-        // two stages of register prefetch in two register sets used in turn
-        // (twice the loads in flight: the 32-column products stream C at
-        // ~4.5 TB/s with 8 flop a byte); same k order, same bits
-        double xa[2][8], xb[2][NB];
-        // branch-free loads (clamped addresses; out-of-range values times a 0/1
-        // factor -- finite operands, so exactly +-0, which adds nothing: a select
-        // on the loaded value makes hipcc branch around each load and drain
-        // vmcnt per element), issued every step: the compiler then counts them
-        // instead of draining the queue at each LDS store
-        auto load_to = [&](double (&ta)[8], double (&tb)[NB], int k0) {
-            const int k = k0 + lk;
-            const bool kin = k < kend;
-            const size_t kc = (size_t)min(k, K - 1);
-#pragma unroll
-            for (int p = 0; p < 8; ++p) {
-                const int i = i0 + lr + 16 * p;
-                const double f = (kin && i < M) ? 1.0 : 0.0;
-                ta[p] = A[kc + (size_t)min(i, M - 1) * lda] * f;
-            }
-#pragma unroll
-            for (int p = 0; p < NB; ++p) {
-                const int j = j0 + lr + 16 * p;
-                const double f = (kin && j < N) ? 1.0 : 0.0;
-                tb[p] = B[kc + (size_t)min(j, N - 1) * ldb] * f;
-            }
-        };
-        auto store_from = [&](const double (&ta)[8], const double (&tb)[NB], int buf) {
-#pragma unroll
-            for (int p = 0; p < 8; ++p) As[buf][lr + 16 * p][lk] = ta[p];
-#pragma unroll
-            for (int p = 0; p < NB; ++p) Bs[buf][lr + 16 * p][lk] = tb[p];
-        };
-        load_to(xa[0], xb[0], kbeg);
-        store_from(xa[0], xb[0], 0);
-        load_to(xa[1], xb[1], kbeg + TSK);
+    if (kbeg < kend) {
+        load(kbeg);
+        store(0);
+    }
+    __syncthreads();
+    int buf = 0;
+    for (int k0 = kbeg; k0 < kend; k0 += TSK) {
+        const bool more = k0 + TSK < kend;
+        if (more) load(k0 + TSK);
+        mfma_stage(buf);
+        if (more) store(buf ^ 1);
         __syncthreads();
-        int buf = 0;
-        // stage k (in LDS buf) computes while set `nxt` holds stage k + TSK and
-        // set `cur` (stage k, already stored) takes stage k + 2 TSK
-        auto step = [&](int k0, double (&ca)[8], double (&cb)[NB], double (&na)[8], double (&nb)[NB]) {
-            load_to(ca, cb, k0 + 2 * TSK);   // past kend: zeros, never stored
-            mfma_stage(buf);
-            store_from(na, nb, buf ^ 1);     // past kend: zeros into the buffer no later stage reads
-            lds_barrier();   // LDS-only: the loads of stage k0 + 2 TSK stay in flight across it
-            buf ^= 1;
-        };
-        int k0 = kbeg;
-        for (; k0 + TSK < kend; k0 += 2 * TSK) {
-            step(k0, xa[0], xb[0], xa[1], xb[1]);
-            step(k0 + TSK, xa[1], xb[1], xa[0], xb[0]);
-        }
-        if (k0 < kend) step(k0, xa[0], xb[0], xa[1], xb[1]);
-    } else {
-        if (kbeg < kend) {
-            load(kbeg);
-            store(0);
-        }
-        __syncthreads();
-        int buf = 0;
-        for (int k0 = kbeg; k0 < kend; k0 += TSK) {
-            const bool more = k0 + TSK < kend;
-            if (more) load(k0 + TSK);
-            mfma_stage(buf);
-            if (more) store(buf ^ 1);
-            __syncthreads();
-            buf ^= 1;
-        }
+        buf ^= 1;
     }
 #pragma unroll
     for (int a = 0; a < 2; ++a)
@@ -566,9 +510,6 @@ __global__ void __launch_bounds__(256, 2) k_gemm_ts(int M, int N, int K, const d
                 else C[(size_t)i + (size_t)j * ldc] = acc[a][b][r];
             }
 }
-int g_gemm_ts = 8;   // k_gemm_ts: most k chunks (0: off -> the 64 x 64 split-K kernel)
-int g_gemm_ts32 = 8;   // the same for the 32-column tile (a function of K alone: shards agree)
-int g_gemm_ts_pf2 = 0;   // 32-column tile: two stages of register prefetch (same bits; knob 35)
 
 // Fixed-order split-K reduction: C = sum_{z=0..S-1} part[z] (column-major M x N),
 // z ascending; loads issued 8 at a time (S is a runtime count: one dependent
@@ -729,10 +670,8 @@ __global__ void __launch_bounds__(256) k_splitk_reduce4(const double *part, size
         }
     }
 }
-int g_gemm_splitk = 1;   // auto split-K policy: 1 = deep splits for few-tile long-K products, 0 = round-1 policy
 
-// Split-K plan of the 64 x 64 kernel (shared with k_gram64, which must chunk
-// K exactly as that kernel would to give the same bits).
+// Split-K plan of the 64 x 64 kernel.
 static void split_plan(const GemmArgs &g, long nblk, int &S, int &kchunk) {
     S = g.splitk;
     if (S < 1) {
@@ -740,7 +679,7 @@ static void split_plan(const GemmArgs &g, long nblk, int &S, int &kchunk) {
         S = 1;
         if (nblk < 192 && g.K >= 512) S = (int)std::min<long>(8, std::max<long>(1, (384 + nblk - 1) / nblk));
         S = std::min(S, std::max(1, g.K / 128));
-        if (g_gemm_splitk && nblk <= 64 && g.K >= 512) {
+        if (cfg_gemm_splitk && nblk <= 64 && g.K >= 512) {
             // few output tiles, long K (Gram matrices Z'Z, the Krylov K'W, T Y):
             // one k-chunk is otherwise a long chain of dependent stages on a
             // quarter of the chip.  ~1024 workgroups, chunks of >= 8 stages
@@ -786,7 +725,7 @@ void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s) {
         // the k chunks depend on K alone (not on M): a row shard of the
         // product (tp_shard.hip) then sums every element in the same order
         int S = 1;
-        if (g.splitk <= 0) S = std::max(1, std::min(tnw == 32 ? g_gemm_ts32 : g_gemm_ts, g.K / 256));
+        if (g.splitk <= 0) S = std::max(1, std::min(tnw == 32 ? cfg_gemm_ts32 : cfg_gemm_ts, g.K / 256));
         int kchunk = ((g.K + S - 1) / S + TSK - 1) / TSK * TSK;
         S = (g.K + kchunk - 1) / kchunk;
         double *out = g.C;
@@ -800,10 +739,7 @@ void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s) {
             st = 0;
         }
         const dim3 grid((unsigned)(tiles * S));
-        if (tnw == 32 && g_gemm_ts_pf2)
-            hipLaunchKernelGGL((k_gemm_ts<1, 32, true>), grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb,
-                               out, ldo, st, kchunk, pstride);
-        else if (tnw == 32)
+        if (tnw == 32)
             hipLaunchKernelGGL((k_gemm_ts<1, 32>), grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb, out,
                                ldo, st, kchunk, pstride);
         else if (g.tag == 1)
@@ -893,19 +829,19 @@ void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s) {
     if (g_gemm_kb == 32) {
         if (g.trans_a)
             hipLaunchKernelGGL((k_gemm_f64<true, 32>), grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb,
-                               out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride, g_gemm_xcd, S == 1 ? g.sub_from : nullptr);
+                               out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride, cfg_gemm_xcd, S == 1 ? g.sub_from : nullptr);
         else
             hipLaunchKernelGGL((k_gemm_f64<false, 32>), grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb,
-                               out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride, g_gemm_xcd, S == 1 ? g.sub_from : nullptr);
+                               out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride, cfg_gemm_xcd, S == 1 ? g.sub_from : nullptr);
     } else if (g.trans_a && g.tag == 1) {
         hipLaunchKernelGGL((k_gemm_f64<true, 16, 1>), grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb,
-                           out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride, g_gemm_xcd, S == 1 ? g.sub_from : nullptr);
+                           out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride, cfg_gemm_xcd, S == 1 ? g.sub_from : nullptr);
     } else if (g.trans_a) {
         hipLaunchKernelGGL((k_gemm_f64<true, 16>), grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb,
-                           out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride, g_gemm_xcd, S == 1 ? g.sub_from : nullptr);
+                           out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride, cfg_gemm_xcd, S == 1 ? g.sub_from : nullptr);
     } else {
         hipLaunchKernelGGL((k_gemm_f64<false, 16>), grid, dim3(256), 0, s, g.M, g.N, g.K, g.A, g.lda, g.B, g.ldb,
-                           out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride, g_gemm_xcd, S == 1 ? g.sub_from : nullptr);
+                           out, ldo, st, (int)g.sym_upper, tc0, kchunk, pstride, cfg_gemm_xcd, S == 1 ? g.sub_from : nullptr);
     }
     TP_HIP(hipGetLastError());
     if (g.affine) {
@@ -934,81 +870,6 @@ void gemm_f64(const GemmArgs &g, DevBuf &work, hipStream_t s) {
     }
 }
 
-// ---------------------------------------------------------------------------
-// Gram matrix Z'Z of a tall 64-column block (the Krylov CholQR Gram matrices):
-// the 64 x 64 kernel's split-K chunks, but each workgroup stages its whole
-// chunk of rows in LDS once (both operands read from it, one load latency, no
-// stage barriers) and computes all 16 tiles.  Same chunks as split_plan gives
-// the 64 x 64 kernel, k ascending in steps of 4 from the chunk start with the
-// last stage zero-padded to 16 rows, and the same partial layout: the partials
-// -- and after the same reduction, the Gram matrix -- are bit-identical.
-constexpr int GRM = 128;   // most rows of a chunk
-__global__ void __launch_bounds__(256) k_gram64(const double *__restrict__ Z, int n, int ldz, int kchunk,
-                                                double *__restrict__ part, size_t pstride) {
-    __shared__ double Zs[GRM][65];
-    const int z = blockIdx.x;
-    const int k0 = z * kchunk, k1 = min(n, k0 + kchunk);
-    const int rows16 = ((k1 - k0) + 15) & ~15;
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    // lane = row (64 consecutive doubles of a column per load), wave w =
-    // columns w, w + 4, ...
-#pragma unroll 4
-    for (int c = w; c < 64; c += 4) {
-        const double *zc = Z + (size_t)c * ldz;
-        for (int r = lane; r < rows16; r += 64) {
-            const int k = k0 + r;
-            Zs[r][c] = k < k1 ? zc[k] : 0.0;
-        }
-    }
-    __syncthreads();
-    const int fr = lane & 15, fk = lane >> 4;
-    d4 acc[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[j] = (d4){0.0, 0.0, 0.0, 0.0};
-    for (int k = 0; k < rows16; k += 4) {
-        const double af = Zs[k + fk][16 * w + fr];   // A[i][k] = Z[k][i]
-        double bf[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) bf[j] = Zs[k + fk][16 * j + fr];   // B[k][j] = Z[k][j]
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af, bf[j], acc[j], 0, 0, 0);
-    }
-    double *P = part + pstride * z;
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) P[(size_t)(16 * w + fk + 4 * r) + (size_t)(16 * j + fr) * 64] = acc[j][r];
-}
-int g_gram64 = 0;   // CholQR Gram of 64-column blocks by k_gram64 (0: the 64 x 64 split-K kernel; same bits)
-
-bool gram64(const double *Z, int n, int ldz, double *W, DevBuf &work, hipStream_t s) {
-    if (!g_gram64 || n < 1) return false;
-    GemmArgs g{64, 64, n, Z, ldz, true, Z, ldz, W, 64};
-    g.sym_upper = true;
-    g.splitk = 0;
-    int S = 0, kchunk = 0;
-    split_plan(g, 1, S, kchunk);
-    if (kchunk > GRM) return false;
-    double *out = W;
-    size_t pstride = 0;
-    if (S > 1) {
-        pstride = (size_t)64 * 64;
-        out = work.as<double>(pstride * S);
-    }
-    hipLaunchKernelGGL(k_gram64, dim3((unsigned)S), dim3(256), 0, s, Z, n, ldz, kchunk, out, pstride);
-    TP_HIP(hipGetLastError());
-    if (S > 1) {   // the reduction gemm_f64 would run
-        const size_t tot = (size_t)64 * 64;
-        if (S >= 16)
-            hipLaunchKernelGGL(k_splitk_reduce4, dim3((unsigned)((tot + 63) / 64)), dim3(256), 0, s, out, pstride, S, 64,
-                               64, W, 64, 0, (const double *)nullptr);
-        else
-            hipLaunchKernelGGL(k_splitk_reduce<0>, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, out, pstride,
-                               S, 64, 64, W, 64, 0, (const double *)nullptr);
-        TP_HIP(hipGetLastError());
-    }
-    return true;
-}
 
 
 }  // namespace tp

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <cstddef>
 #include <cstdint>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <functional>
@@ -12,6 +13,57 @@
 #include "../../include/tadpole_hip.h"
 
 namespace tp {
+
+// Run-time switches (tp_debug_knob, tp_api.hip).  tp_debug_knob sets the
+// process-wide values; every C-ABI entry copies them into its calling
+// thread's t_knob when it starts (guarded), so a call runs on the one set it
+// started with whatever another thread sets meanwhile.
+struct Knobs {
+    int ch_dedup_ucap = 0;       // 1: cap on the shared CH segment store (> 0: tests of its overflow path)
+    int xtx_int8 = 1;            // 5: exact int8 X'X for integer counts (0: the fp64 MFMA product)
+    int pca_krylov_min = 4096;   // 8: bins from which the block Krylov PCA replaces forming G
+    int xtx_fused = 1;           // 18: the correlation epilogue in the int8 X'X store
+    int pca_ckrylov = -1;        // 20: Krylov space of C (1), of G (0), of C from cfg_ckry_min bins (-1)
+    int shard_slab = 1;          // 24: C5 shards keep C row-sharded (0: C gathered whole)
+    int prod_i8 = 5;             // 36: G-space Krylov products on int8 digits (0: fp64; 1: k_pd_prod; 5: k_pd_prodA)
+    int upload_mode = 2;         // 43: bit 1: exact count blocks travel packed; bit 0: one block at a time
+    int xtx_w = 1;               // 44: whole-triangle X'X by 256 x 128 tiles
+    int pd_cspace = 1;           // 45: C-space Krylov products on int8 digits
+    int coniss_lean_min = 0;     // 48: lean sweeps from this many bins take the global link-only CONISS
+    int coniss_lds2 = 3;         // 49: LDS CONISS with one 16-bit link array (3: where 16 bytes a bin do not fit)
+    int coniss_batch = 2;        // 52: batched CONISS (2: every sweep; 1: not lean ones; 0: never)
+};
+extern thread_local Knobs t_knob;
+
+// Former A/B switches, now compile-time constants at their measured settings
+// (the alternatives were measured slower or equal; git history has them).
+constexpr int cfg_ch_dedup = 1;          // CH segment statistics shared across trees
+constexpr int cfg_pca_margin = 0;        // extra Chebyshev degrees over the planned count
+constexpr int cfg_gemm_xcd = 1;          // XCD-aware workgroup order of the 64 x 64 GEMM
+constexpr int cfg_pca_krylov_block = 0;  // Krylov block p (0: 64 for k >= 128, else 32)
+constexpr int cfg_pca_krylov_steps = 0;  // Krylov steps before the first check (0: ceil(5 k / p))
+constexpr int cfg_gemm_splitk = 1;       // deep split-K for few-tile long-K products
+constexpr int cfg_gemm_ts = 8;           // k_gemm_ts: most k chunks (64-column tile)
+constexpr int cfg_gemm_ts32 = 8;         // the same for the 32-column tile
+constexpr int cfg_xtx_supertile = 1;     // int8 X'X: XCD-contiguous supertile order
+constexpr int cfg_pca_over = 0;          // subspace oversampling (0: max(32, k / 4), b rounded to 32)
+constexpr int cfg_coniss_lu = 1;         // the global CONISS keeps its links as 16-bit indices in LDS
+constexpr int cfg_cor_fused = 1;         // C's column means in the correlation epilogue
+constexpr int cfg_pca_cheb_fused = 1;    // Chebyshev step in the T Y product's reduction
+constexpr int cfg_ckry_chunk = 0;        // rows per Z partial of the PIP passes (0: from n and D)
+constexpr int cfg_ckry_steps = 0;        // C-Krylov blocks before the first check (0: from k and n)
+constexpr int cfg_pca_band = 1;          // products with the block-tridiagonal T skip its zero blocks
+constexpr int cfg_krylov_local = 1;      // G-space CGS pass 0 against the last two blocks only
+constexpr int cfg_ckry_min = 10000;      // bins from which pca_ckrylov = -1 takes the Krylov space of C
+constexpr int cfg_ckry_local = 1;        // C-space first PIP pass against K_0 and the last two blocks
+constexpr int cfg_xtx_nz = 1;            // int8 X'X skips the high slice's all-zero blocks
+constexpr int cfg_pd_digits_blk = 1;     // the block's digits by (column, slice) workgroups
+constexpr int cfg_pd_cm = 1;             // C's column means in A's digit pass
+constexpr int cfg_sync_spin_us = 20000;  // sharded waits spin this long before blocking
+constexpr int cfg_devbuf_async = 1;      // scratch from the library's stream-ordered pool
+constexpr int cfg_pd_digits_big = 1;     // long columns' digit image in one read
+constexpr int cfg_lean_auto = 1;         // sweeps lean while another pipeline is in flight on the device
+constexpr int cfg_clean_tile = 0;        // NA -> 0 / symmetrise tile edge (0: 128 from 16 384 bins, else 64)
 
 constexpr uint64_t kRNaBits = 0x7FF00000000007A2ULL;  // R NA_real_
 constexpr uint64_t kRNanBits = 0x7FF8000000000000ULL; // R NaN
@@ -185,9 +237,9 @@ void launch_splitk_reduce_r1(const double *part, size_t stride, int S, int M, in
                              const double *u, double *C, int ldc, hipStream_t s);
 void launch_splitk_reduce(const double *part, size_t stride, int S, int M, int N, double *C, int ldc, int store_t,
                           hipStream_t s);
-extern int g_gemm_panel;   // short-K tall-skinny 32 x 64 kernel enabled (default 1)
-extern int g_gemm_kb;      // LDS stage depth of the 64 x 64 kernel (16 / 32)
-extern int g_gemm_xcd;     // XCD-aware workgroup order of the 64 x 64 kernel (default 1)
+// set only by the tp_debug_gemm hook around its own call (this thread)
+extern thread_local int g_gemm_panel;   // short-K tall-skinny 32 x 64 kernel enabled (default 1)
+extern thread_local int g_gemm_kb;      // LDS stage depth of the 64 x 64 kernel (16 / 32)
 // b <= 1280 (a multiple of 32); b > 480 needs chol_panel_doubles(b) of scratch
 size_t chol_panel_doubles(int b);
 void launch_chol(double *d_W, double *d_rdiag, int b, double rel, int *d_info, hipStream_t s,
@@ -202,21 +254,10 @@ void launch_trsm_ru(const double *d_Z, int n, int b, const double *d_U, const do
 // in F (b x b doubles), S in sc (b), 1/diag(U) in rdiag (b), diag(U) on W's
 // diagonal; k_trsm_frag then forms Q = Z U^-1 (U = U' S^-1), n/16 waves.
 constexpr int kCholInvMax = 256;
-extern int g_chol_inv_waves;
-extern int g_gemm_splitk;
-extern int g_gemm_ts_pf2;   // 32-column long-K product: two stages of register prefetch
-extern int g_gemm_ts;
-extern int g_gemm_ts32;
-extern int g_gram64;
-// Z'Z (64 x 64, ld 64) of an n x 64 block by k_gram64, bit-identical to the
-// symmetric split-K GEMM; false: not applicable (the caller runs gemm_f64)
-bool gram64(const double *Z, int n, int ldz, double *W, DevBuf &work, hipStream_t s);
-extern int g_xtx_nz;          // int8 X'X (LDS-DMA kernel): skip the high slice's zero blocks
-extern int g_xtx_glds;        // int8 X'X: LDS-DMA ring kernel (0: register-staged k_xtx_i8_big)
-extern int g_xtx_supertile;   // int8 X'X: XCD-contiguous supertile order of the 128 x 128 tiles (0: columns)
+extern thread_local int g_chol_inv_waves;   // set only by the CholQR debug hook (this thread)
 // row-shardable products that take the 128 x 64 kernel with k chunks fixed by K
 // (tp_gemm.hip); shards and the unsharded call must agree on it
-inline bool rows_ts(int K, int N) { return g_gemm_ts > 0 && K >= 4096 && N <= 256; }
+inline bool rows_ts(int K, int N) { return cfg_gemm_ts > 0 && K >= 4096 && N <= 256; }
 void launch_chol_inv(double *d_W, double *d_F, double *d_sc, double *d_rdiag, int b, double rel, int *d_info,
                      hipStream_t s, long long *d_stamps = nullptr);
 void launch_trsm_frag(const double *d_Z, int n, int b, const double *d_F, const double *d_sc, double *d_Q,
@@ -259,16 +300,7 @@ struct SweepDev {
     bool lds_lean = false;                // CONISS: links in global memory (a few bytes of LDS a tree)
 };
 // scratch of the shared CH segment statistics for ntrees trees
-extern int g_ch_dedup;        // 0: every tree computes its own segment statistics
-extern int g_cor_fused;        // 0: prcomp's column means by a separate pass over C
-extern int g_coniss_lu;       // 0: the global CONISS variant keeps its links in global memory
-extern int g_coniss_batch;    // the batched CONISS kernel (1 default, 2 also for lean sweeps, 0 never)
-extern int g_coniss_lean_min; // lean sweeps of matrices that fit LDS from this many bins take the link-only variant (0: never)
-extern int g_lean_auto;       // 1: a sweep is lean whenever another pipeline is in flight on its device
-extern int g_coniss_lds2;     // the LDS variant with one 16-bit link array (1: lean sweeps, 2: every sweep)
-extern int g_clean_tile;      // k_clean_symmetrize tile edge (0: by size, 64 or 128)
 int pipelines_in_flight(int device);
-extern int g_ch_dedup_ucap;   // > 0: cap on the shared store (tests of the overflow path)
 size_t sweep_dedup_bytes(int n, int k, int ntrees, int seg_cap, int *hcap, int *ucap);
 void sweep_dedup_bind(SweepDev &sd, void *base, int hcap, int ucap);
 // CONISS per-tree rows: roundup(n, 64) costs + 64 (a dummy slot, index
@@ -306,9 +338,6 @@ void launch_transpose(const double *d_A, int rows, int cols, int lda, double *d_
 // Symmetric eigendecomposition for b <= 1280 (tp_eig.hip): A (b x b, lower
 // triangle) <- eigenvectors, theta <- ascending eigenvalues.  work >= b*b + 4b + 8.
 bool eig_sym_supported(int b);
-extern int g_sytrd_reg;
-extern int g_sytrd32;
-extern int g_pd_digits_blk;
 void sytrd_stamped(double *A, int b, double *work, long long *d_stamps, hipStream_t s);
 void sytrd_which(double *A, int b, double *work, int which, hipStream_t s,
                  long long *d_stamps = nullptr);   // work: 3b (e, tau, d)
@@ -340,7 +369,7 @@ void stream_sync(Ctx &c, hipStream_t s);
 void event_mark(Ctx &c, hipStream_t s);
 void event_sync(Ctx &c);
 void comm_abort(Ctx &c);
-extern int g_shard_inject;   // test hook: the next N sharded waits fail as device errors
+extern std::atomic<int> g_shard_inject;   // test hook: the next N sharded waits fail as device errors
 int shard_count(const Ctx &c);
 bool shard_mine(const Ctx &c, int r);
 void shard_plan(int n, int R, int kind, int *bounds);
@@ -366,7 +395,6 @@ struct ProdDigits {
     int Kp = 0, col0 = 0, cols = 0;
     int pending = 0;   // > 0: columns [pending, cols) not digitised yet (prod_digits_finish)
 };
-extern int g_prod_i8;
 bool prod_i8_ok(int K, int N);
 int prod_i8_pairs();   // digit pairs one int8 product sums (27 with six digits of A)
 int prod_i8_adig();    // digits of A the image stores
@@ -376,16 +404,9 @@ void prod_digits_build(Ctx &c, const double *A, int lda, int K, int cols, int co
                        double *cm = nullptr, int ncm = 0);
 void prod_digits_finish(Ctx &c, const double *A, int lda, int K, ProdDigits &pd);
 bool prod_digits_means_ok(int K);
-extern int g_pd_cm;
-extern int g_sync_spin_us;
-extern int g_devbuf_async;
 // host -> device through the context's pinned ring (tp_upload.hip); counts:
 // blocks of exact 16-bit counts travel packed.  Returns the bytes sent packed.
 size_t upload_host(Ctx &c, const void *host, size_t bytes, void *d_dst, int nthreads, bool counts);
-extern int g_upload_mode;
-extern int g_pd_digits_big;   // knob 46
-extern int g_pd_cspace;   // knob 45: the C-space Krylov products on the int8 digits
-extern int g_xtx_w;   // knob 44: whole-triangle X'X by 256 x 128 tiles
 int prod_i8_partials(Ctx &c, const ProdDigits &pd, int r0, int M, const double *B, int ldb, int N, int K,
                      DevBuf &work, double **part);
 // pd (optional): A's digit image; the product then runs on the int8 MFMA
@@ -395,10 +416,7 @@ void rows_gemm_sharded(Ctx &c, const double *A, int lda, int M, const double *B,
                        const ProdDigits *pd = nullptr);
 
 // exact X'X on int8 matrix cores for integer counts (tp_xtx.hip)
-extern int g_xtx_int8;
-extern int g_xtx_fused;
-extern int g_kprof_fine;   // 0: no per-launch Krylov product events (they open gaps on the stream)
-extern int g_shard_slab;   // 1: C5 shards keep C row-sharded (column slabs), 0: C gathered whole
+extern std::atomic<int> g_kprof_fine;   // 0: no per-launch Krylov product events (they open gaps on the stream)
 int xtx_int_slices(Ctx &c, const double *d_X, int n);   // 0 = not integer counts (fp64 path)
 const int8_t *xtx_slices(Ctx &c, const double *d_X, int n, int ns);
 void xtx_int8_tiles(Ctx &c, const int8_t *sl, int n, int ns, double *d_S, int tc0, int tc1);   // 64-col tiles
@@ -447,27 +465,17 @@ void cor_product(Ctx &c, const double *d_X, int n, const double *d_m, const Gath
 // S = X'X by the exact int8 path when possible, sharded like sym_gemm_sharded
 void xtx_product(Ctx &c, const double *d_X, int n, double *d_S);
 
-extern int g_pca_margin;   // extra Chebyshev degrees over the planned count (default 0)
 struct PcaStats {
     int iters = 0; double resid = 0; double rate = 0; int block = 0; int blocks = 0;
     int krylov_steps = 0, krylov_dim = 0;   // block Krylov path (0: G formed)
     int prod_pairs = 0;                     // int8 digit pairs of the products with C (0: fp64 products)
     const double *d_theta = nullptr;        // device copy of h_theta (valid until the next small problem)
 };
-extern int g_pca_krylov_min, g_pca_krylov_block, g_pca_krylov_steps, g_pca_over;
-extern int g_pca_cheb_fused;   // Krylov small problem: Chebyshev step in the T Y reduction (default 1)
-extern int g_pca_ckrylov;      // 1: block Krylov in C (tp_krylov.hip), 0: in G (tp_pca.hip), -1: C from g_ckry_min
-extern int g_ckry_min;         // bins from which the automatic choice takes the Krylov space of C
-extern int g_ckry_local;   // C-space Krylov: local first orthogonalisation pass (knob 33)
-extern int g_ckry_chunk;       // rows per Z partial of the C-Krylov orthogonalisation
-extern int g_ckry_steps;       // C-Krylov blocks before the first check (0: from k and n)
 // the top k eigenpairs of a D x D projected matrix (tp_pca.hip)
 // band_p > 0: T is block tridiagonal with band_p x band_p blocks (products
-// with it skip the zero blocks when g_pca_band)
+// with it skip the zero blocks when cfg_pca_band)
 void small_topk_T(Ctx &c, double *Tm, int D, int k, double *Vs, std::vector<double> &h_theta, PcaStats &sst,
                   int band_p = 0);
-extern int g_pca_band;
-extern int g_krylov_local;   // Krylov CGS pass 0 against the last two blocks (1) or all (0)
 // false: an orthogonalisation pass broke down (the caller takes the G path)
 bool krylov_c_topk(Ctx &c, double *C, int c_col0, const double *mext, int n, int k, double *V, double *P,
                    std::vector<double> &h_theta, PcaStats &st, const ProdDigits *pd = nullptr);

@@ -70,15 +70,10 @@ __global__ void k_start_block(double *Q, int n, uint64_t seed) {
 // latency-bound) cost 5.1 ms against the G path's 3.3 ms: PCA 14.9 vs 14.1 ms
 // (profiles/r03b_*).  Kept, tested, behind knob 20.
 // 1: Krylov in C (this file), 0: Krylov in G (tp_pca.hip), -1: C from
-// g_ckry_min bins on.  Measured (round 4, MI355X, PCA ms G vs C): 10k bins
+// cfg_ckry_min bins on.  Measured (round 4, MI355X, PCA ms G vs C): 10k bins
 // 18.3 vs 18.1, 24.3k bins 96.0 vs 77.3 -- the C space halves the product
 // flops, and above ~10k bins that outweighs its costlier orthogonalisation
 // (at C3, 7.7k bins, the G space is ~0.8 ms faster)
-int g_pca_ckrylov = -1;
-int g_ckry_min = 10000;
-int g_ckry_chunk = 0;         // rows per Z partial of the PIP passes (0: from n and D, see pip_chunk)
-int g_ckry_steps = 0;         // blocks s before the first check (0: from k and n)
-int g_ckry_local = 1;         // first BCGS-PIP pass against K_0, K_{t-2}, K_{t-1} only (knob 33)
 
 // One BCGS-PIP pass of block slot `D / KP` (columns D..D+KP-1 of Kb, n x KP):
 // W0 is the block to orthonormalise against Kb's first D columns (W0 may be
@@ -94,7 +89,7 @@ struct PipScratch {
 // chunk row chunks), 512 to 1024 rows (fewer partials for k_pipr to sum; 24.3k
 // bins, PCA: fixed 256 rows 74.5 ms, 512 73.4, 768 73.3, 1024 73.7)
 static int pip_chunk(int n, int dt) {
-    if (g_ckry_chunk > 0) return std::max(64, g_ckry_chunk);
+    if (cfg_ckry_chunk > 0) return std::max(64, cfg_ckry_chunk);
     const long want = ((long)n * dt / 1024 + 63) / 64 * 64;
     return (int)std::max<long>(512, std::min<long>(1024, want));
 }
@@ -131,7 +126,7 @@ static void pip_pass(Ctx &c, double *Kb, int n, int D, const double *W0, const P
 
 size_t ckry_partial_doubles(int n, int dmax) {
     // the most partials any pass needs: the smallest chunk is the floor's
-    const int chunk = g_ckry_chunk > 0 ? std::max(64, g_ckry_chunk) : 512;
+    const int chunk = cfg_ckry_chunk > 0 ? std::max(64, cfg_ckry_chunk) : 512;
     return (size_t)((n + chunk - 1) / chunk) * (size_t)(dmax + KP) * KP;
 }
 
@@ -144,13 +139,13 @@ bool krylov_c_topk(Ctx &c, double *C, int c_col0, const double *mext, int n, int
     // k = 200), more for the denser spectra of larger matrices
     int steps = (int)std::ceil(5.28 * k / KP);
     if (n > 12000) steps += (int)std::ceil(12.0 * std::log2((double)n / 12000.0));   // 24k: 45 (44 measured)
-    if (g_ckry_steps > 0) steps = g_ckry_steps;
+    if (cfg_ckry_steps > 0) steps = cfg_ckry_steps;
     steps = std::max(1, steps);
     // T = K'GK is block pentadiagonal in the 32-column blocks (G = C Pc C,
     // C K_t in span K_{t-1..t+1}, the rank-1 centring term in K_0, K_1): with
     // an even block count it is block TRIdiagonal in 64-column blocks, so the
     // small problem's products with T are banded (k_band_ty, as the G path)
-    if (g_pca_band) steps += steps & 1;
+    if (cfg_pca_band) steps += steps & 1;
     const int smax = std::max(steps, std::min(steps + 48, (n / 2) / KP));
     steps = std::min(steps, smax);
     const size_t np = (size_t)n * KP;
@@ -188,7 +183,7 @@ bool krylov_c_topk(Ctx &c, double *C, int c_col0, const double *mext, int n, int
                 // Lanczos recurrence; 1 is in span K_0), so the first pass runs
                 // against those blocks only and the second, against every block,
                 // removes the rounding-level rest (knob 33)
-                pip_pass(c, K, n, D, Pb + (size_t)(t - 1) * np, ps, 1e-14, 0, g_ckry_local ? t : 0);
+                pip_pass(c, K, n, D, Pb + (size_t)(t - 1) * np, ps, 1e-14, 0, cfg_ckry_local ? t : 0);
                 pip_pass(c, K, n, D, K + (size_t)D * n, ps, 0.0, 1);   // Gram ~ I + 1e-13: Lowdin
             }
             double *Kt = K + (size_t)t * np, *Pt = Pb + (size_t)t * np;
@@ -220,7 +215,7 @@ bool krylov_c_topk(Ctx &c, double *C, int c_col0, const double *mext, int n, int
         PcaStats sst;
         // banded products when T is block tridiagonal in 64-column blocks (its
         // entries off the band are rounding-level and are not read)
-        small_topk_T(c, Tm, D, k, Vs, h_theta, sst, (g_pca_band && D % 64 == 0) ? 64 : 0);
+        small_topk_T(c, Tm, D, k, Vs, h_theta, sst, (cfg_pca_band && D % 64 == 0) ? 64 : 0);
         // V = K Y, scores Xc V = P Y
         GemmArgs vg{n, k, D, K, n, false, Vs, D, V, n};
         vg.splitk = 0;

@@ -6,7 +6,7 @@
 // Two ways to the same eigenvectors (only span(V_1..V_i) matters downstream:
 // distances and CH are invariant to sign and to rotations inside a prefix):
 //
-//  * small N (N < g_pca_krylov_min): G = Xc'Xc on the fp64 MFMA (N^3), then
+//  * small N (N < t_knob.pca_krylov_min): G = Xc'Xc on the fp64 MFMA (N^3), then
 //    Chebyshev-filtered block subspace iteration on G (block b = k +
 //    oversampling, CholQR orthonormalisation, Rayleigh-Ritz at the end);
 //  * large N: G is never formed.  A block Krylov space of G (block p, s steps,
@@ -97,7 +97,7 @@ static void orth_cholqr(Ctx &c, double *Z, double *Qout, double *Tmp, int n, int
         GemmArgs g{b, b, n, src, n, true, src, n, W, b};
         g.sym_upper = true;
         g.splitk = 0;   // auto: deep split for few-tile Gram matrices (tp_gemm.hip)
-        if (!(b == 64 && gram64(src, n, n, W, c.buf[S_PARTIAL], c.cur))) gemm_f64(g, c.buf[S_PARTIAL], c.cur);
+        gemm_f64(g, c.buf[S_PARTIAL], c.cur);
         double *dst = ((passes - 1 - p) % 2 == 0) ? Qout : Tmp;   // last pass lands in Qout
         if (b <= kCholInvMax && b % 16 == 0) {
             launch_chol_inv(W, Y, X + b, X, b, p == 0 ? shift : 0.0, d_info, c.cur);
@@ -203,12 +203,6 @@ __global__ void k_diag(const double *W, int b, double *d) {
     if (j < b) d[j] = fabs(W[(size_t)j * b + j]);
 }
 
-int g_pca_margin = 0;     // extra Chebyshev degrees over the planned count (the residual check adds more when needed; tools/pca_margin.py)
-int g_pca_krylov_min = 4096;   // N at which the block Krylov path replaces forming G (0: always, huge: never)
-int g_pca_krylov_block = 0;    // Krylov block p (0: 64 for k >= 128, else 32)
-int g_pca_over = 0;            // subspace oversampling b - k (0: max(32, k / 4), b rounded to 32; else rounded to 16)
-int g_pca_cheb_fused = 1;     // Krylov small problem: the Chebyshev step in the T Y product's reduction (0: k_cheb)
-int g_pca_krylov_steps = 0;    // Krylov steps s before the first check (0: ceil(5 k / p))
 
 using Prod = std::function<void(const double *, double *)>;
 // Out = a (A Y) + b Yc [+ c Yp]: the product with the Chebyshev step in its
@@ -225,8 +219,8 @@ static void subspace_topk(Ctx &c, const double *A, int n, int k, const Prod &pro
                           std::vector<double> &h_theta, PcaStats &st, uint64_t seed, int margin = 0,
                           const ProdAff *paff = nullptr) {
     hipStream_t s = c.cur;
-    const int over = g_pca_over > 0 ? g_pca_over : std::max(32, k / 4);
-    const int rnd = g_pca_over > 0 ? 16 : 32;
+    const int over = cfg_pca_over > 0 ? cfg_pca_over : std::max(32, k / 4);
+    const int rnd = cfg_pca_over > 0 ? 16 : 32;
     int b = std::min(n, ((k + over + rnd - 1) / rnd) * rnd);
     st.block = b;
     if (b >= n) {
@@ -346,7 +340,7 @@ static void subspace_topk(Ctx &c, const double *A, int n, int k, const Prod &pro
             cut = 0.0;
         }
         st.rate = gk > 1 ? 1.0 / gk : 0.9;
-        int need = (int)std::ceil(std::log(1.0 / target) / std::log(std::max(gk, 1.0005))) + g_pca_margin + margin;
+        int need = (int)std::ceil(std::log(1.0 / target) / std::log(std::max(gk, 1.0005))) + cfg_pca_margin + margin;
         need = std::min(need, max_deg);
         if (cut > 0) {
             // Block degrees double: after total degree D the j-th column's
@@ -455,8 +449,6 @@ static void subspace_topk(Ctx &c, const double *A, int n, int k, const Prod &pro
 // The projected problem of the Krylov paths: the top k eigenpairs of T (D x
 // D, symmetric, ld D) by the subspace iteration above (products with T are
 // D x D GEMMs, the Chebyshev step in their split-K reduction).  Vs: D x k.
-int g_pca_band = 1;
-int g_krylov_local = 1;   // CGS pass 0 against the last two Krylov blocks only (0: every block)
 
 static void band_ty(const double *T, const double *Y, double *Out, int D, int b, int p, bool aff, double a, double bc,
                     const double *Yc, double cc, const double *Yp, hipStream_t s) {
@@ -474,7 +466,7 @@ static void band_ty(const double *T, const double *Y, double *Out, int D, int b,
 
 void small_topk_T(Ctx &c, double *Tm, int D, int k, double *Vs, std::vector<double> &h_theta, PcaStats &sst, int band_p) {
     hipStream_t s = c.cur;
-    const bool band = band_p > 0 && g_pca_band;
+    const bool band = band_p > 0 && cfg_pca_band;
     Prod tprod = [&](const double *Y, double *Out) {
         if (band) {
             band_ty(Tm, Y, Out, D, sst.block, band_p, false, 0, 0, nullptr, 0, nullptr, s);
@@ -503,7 +495,7 @@ void small_topk_T(Ctx &c, double *Tm, int D, int k, double *Vs, std::vector<doub
     // +2 planned degrees: a product with T costs ~1.5 % of a Rayleigh-Ritz
     // round (one-workgroup tridiagonalisation) that a near miss of the
     // residual check would add
-    subspace_topk(c, Tm, D, k, tprod, Vs, h_theta, sst, 0x5EEDULL + (uint64_t)D, 2, g_pca_cheb_fused ? &taff : nullptr);
+    subspace_topk(c, Tm, D, k, tprod, Vs, h_theta, sst, 0x5EEDULL + (uint64_t)D, 2, cfg_pca_cheb_fused ? &taff : nullptr);
 }
 
 // Block Krylov path (see the file comment): V (n x k) = top-k eigenvectors of
@@ -512,7 +504,7 @@ void small_topk_T(Ctx &c, double *Tm, int D, int k, double *Vs, std::vector<doub
 // itself and the centring is two rank-1 corrections of an n x p block.
 // Blocks K_t (n x p) in S_KRY, G K_t in S_KRYG, T = K'GK in S_KRYT, the small
 // problem's vectors in S_KRYV.
-static int krylov_block(int k) { return g_pca_krylov_block > 0 ? g_pca_krylov_block : (k >= 128 ? 64 : 32); }
+static int krylov_block(int k) { return cfg_pca_krylov_block > 0 ? cfg_pca_krylov_block : (k >= 128 ? 64 : 32); }
 
 static void krylov_topk(Ctx &c, double *C, int c_col0, const double *mext, int n, int k, double *V, double *P,
                         std::vector<double> &h_theta, PcaStats &st, const ProdDigits *pd) {
@@ -522,7 +514,7 @@ static void krylov_topk(Ctx &c, double *C, int c_col0, const double *mext, int n
     // +4 steps at 24k bins)
     int steps = (5 * k + p - 1) / p;
     if (n > 12000) steps += 2 * (int)std::ceil(std::log2((double)n / 12000.0));
-    if (g_pca_krylov_steps > 0) steps = g_pca_krylov_steps;
+    if (cfg_pca_krylov_steps > 0) steps = cfg_pca_krylov_steps;
     const int smax = std::max(steps, std::min(steps + 24, (n / 2) / p));
     steps = std::min(steps, smax);
     double *K = c.buf[S_KRY].as<double>((size_t)n * p * smax);
@@ -571,7 +563,7 @@ static void krylov_topk(Ctx &c, double *C, int c_col0, const double *mext, int n
                 // streaming of K.  T's band needs only those two blocks of H1.
                 for (int pass = 0; pass < 2; ++pass) {
                     const double *src = pass == 0 ? GK + (size_t)(t - 1) * np : W;
-                    const int D0 = (pass == 0 && g_krylov_local) ? std::max(0, (t - 2) * p) : 0;
+                    const int D0 = (pass == 0 && cfg_krylov_local) ? std::max(0, (t - 2) * p) : 0;
                     double *Hc = (pass == 0 ? H1 : H2) + (size_t)(t - 1) * p * Dm + D0;   // column block t - 1
                     const double *Kc = K + (size_t)D0 * n;
                     GemmArgs pr{D - D0, p, n, Kc, n, true, src, n, Hc, Dm};   // K'src
@@ -674,13 +666,13 @@ PcaStats pca_dev(Ctx &c, double *d_C, int n, int k, double *d_P, double *d_Pt, d
     hipStream_t s = c.cur;
     const double *mean = d_cmean;
     const int b_est = std::min(n, ((k + std::max(32, k / 4) + 31) / 32) * 32);
-    const bool krylov = n >= g_pca_krylov_min && b_est < n;
-    const bool cspace = g_pca_ckrylov > 0 || (g_pca_ckrylov < 0 && n >= g_ckry_min);
+    const bool krylov = n >= t_knob.pca_krylov_min && b_est < n;
+    const bool cspace = t_knob.pca_ckrylov > 0 || (t_knob.pca_ckrylov < 0 && n >= cfg_ckry_min);
     const int cend = c_col1 < 0 ? n + 2 : c_col1;
     // the int8-digit products: the G-space blocks of krylov_block(k) columns, the
     // C-space blocks of 32 (knob 45)
-    const bool i8 = krylov && g_prod_i8 > 0 &&
-                    (cspace ? g_pd_cspace != 0 && prod_i8_ok(n, 32) : prod_i8_ok(n, krylov_block(k)));
+    const bool i8 = krylov && t_knob.prod_i8 > 0 &&
+                    (cspace ? t_knob.pd_cspace != 0 && prod_i8_ok(n, 32) : prod_i8_ok(n, krylov_block(k)));
     // cm_pending: d_cmean is where C's column means go; with the int8 products
     // over all of [C | m | 1] they come out of A's digit pass (k_colmean's bits)
     const bool cm_fused = cm_pending && i8 && c_col0 == 0 && cend == n + 2 && prod_digits_means_ok(n);

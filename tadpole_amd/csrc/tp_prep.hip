@@ -74,10 +74,9 @@ __global__ void __launch_bounds__(T * T / 16) k_clean_symmetrize(double *M, int 
 // knob 50: k_clean_symmetrize tile edge -- 0 (default): 128 from 16 384 bins
 // (49 851: 6.18 -> 5.36 ms), 64 below (7 808, Infinity-Cache resident: 93 vs
 // 100 us); 64 / 128 force one
-int g_clean_tile = 0;
 
 void launch_clean_symmetrize(double *d_M, int n0, bool src_upper, hipStream_t s) {
-    if (g_clean_tile == 128 || (g_clean_tile == 0 && n0 >= 16384)) {
+    if (cfg_clean_tile == 128 || (cfg_clean_tile == 0 && n0 >= 16384)) {
         int nb = (n0 + 127) / 128;
         long nblk = (long)nb * (nb + 1) / 2;
         hipLaunchKernelGGL(k_clean_symmetrize<128>, dim3((unsigned)nblk), dim3(1024), 0, s, d_M, n0, nb, src_upper);
@@ -437,7 +436,6 @@ __global__ void __launch_bounds__(256) k_cor_epilogue(const double *S, const dou
     }
 }
 
-int g_cor_fused = 1;
 
 // The same elements, one wave per column j, with C's column mean formed in the same
 // pass: the lane-strided double-double order of k_colmean (rows lane, lane + 64, ...,

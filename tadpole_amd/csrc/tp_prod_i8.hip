@@ -34,13 +34,9 @@
 namespace tp {
 
 // knob 36: the int8-digit products in the G-space Krylov path (0: the fp64
-// k_gemm_ts; 2: the double-buffered kernel).  Within ~1e-15 of sum |A||B|
+// k_gemm_ts; 1: k_pd_prod, 64-row tiles; 5: k_pd_prodA, 128-row tiles).  Within ~1e-15 of sum |A||B|
 // (test_prod_i8_digit_product); the 32 C3 products 4.6 ms against 6.3
 // 
-int g_prod_i8 = 5;
-int g_pd_digits_big = 1;   // knob 46: long columns' image in one read (0: k_pd_digits, three passes)
-int g_pd_cspace = 1;   // knob 45: C-space blocks (32 columns) on the int8 digits (0: k_gemm_ts)
-int g_pd_digits_blk = 1;   // knob 38: the block's digits by (column, slice) workgroups (0: one per column); same bits
 
 constexpr int PD_DIG = 7;   // digits per value
 #ifndef TP_PD_ADIG
@@ -378,8 +374,9 @@ __global__ void __launch_bounds__(256) k_pd_digits_sl(const double *__restrict__
 // NB = 1 (the default): one LDS buffer of 78 KB (PD_BUF), the next step's
 // loads in registers while this step's MFMAs run, two barriers a step, two
 // workgroups a CU (each one's MFMAs run under the other's waits).
-// NB = 2 (knob 36 = 2): two LDS buffers (156 KB, one workgroup a CU), two k
-// steps of loads in flight in two register sets, one barrier a step.
+// NB = 2: two LDS buffers (156 KB, one workgroup a CU), two k steps of loads
+// in flight in two register sets, one barrier a step (measured slower; no
+// longer dispatched since round 6, kept as the template's second form).
 // LDS row stride (bytes).  The 16-lane groups of ds_read_b128 ({0-3,12-15,
 // 20-27}, ...: banks (a/4) mod 64) read fragment rows l & 15 at byte 16 (l >> 4):
 // with 96-byte rows the 16 lanes of every group land on 16 distinct 4-bank
@@ -524,112 +521,6 @@ __global__ void __launch_bounds__(256, 3 - NB) k_pd_prod(const int8_t *__restric
                 const int j = j0 + 16 * b + fr;
                 if (i >= M) continue;
                 // weight of u: 256^(12 - u) 2^-108 -> 2^(-12 - 8u), times the scales
-                double v = 0.0;
-#pragma unroll
-                for (int u = PD_DIG - 1; u >= 0; --u) v += (double)acc[u][a][b][r] * ldexp(1.0, 96 - 8 * u);
-                P[(size_t)i + (size_t)j * M] = (v * rs[i]) * cs[j];
-            }
-}
-
-// k_pd_prod128: the k_pd_prod<1> schedule (same pairs, sums, combine and k
-// chunks: the same bits) with 128-row tiles -- 8 waves in 4 x 2, each a 32 x
-// 32 output block, one workgroup a CU (97 KB of LDS, 2 waves a SIMD).  The
-// block's digits (28 KB a step) are re-read by every row tile, more than half
-// of what a 64-row workgroup loads; two row tiles per workgroup halve that
-// share (76 KB a step for the MFMAs of two 64-row workgroups' 104 KB).
-// Threads 0..255 stage row tile 2 bm and the block, 256..511 row tile 2 bm + 1.
-constexpr int PD_ASZ2 = PD_ADIG * 128 * PD_LD, PD_BUF2 = PD_ASZ2 + PD_DIG * 64 * PD_LD;
-__global__ void __launch_bounds__(512, 1) k_pd_prod128(const int8_t *__restrict__ Da, int Kp, int M,
-                                                       const int8_t *__restrict__ Db, const double *__restrict__ rs,
-                                                       const double *__restrict__ cs, double *__restrict__ part,
-                                                       size_t pstride, int kchunk) {
-    extern __shared__ __attribute__((aligned(16))) int8_t pd_lds[];
-    const int tm = (M + 127) / 128, tm64 = (M + 63) / 64;
-    const int total = (int)gridDim.x;
-    const int xcd = (int)blockIdx.x & 7, slot = (int)blockIdx.x >> 3;
-    const int Lg = xcd * (total >> 3) + min(xcd, total & 7) + slot;
-    const int bm = Lg % tm, z = Lg / tm;
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const int wr = w & 3, wc = w >> 2;
-    const int fr = lane & 15, fk = (lane >> 4) * 16;
-    const int kbeg = z * kchunk, kend = min(Kp, kbeg + kchunk);
-    const int nsteps = Kp / 64;
-    TP_DASSERT(Kp % 64 == 0 && kchunk % 64 == 0 && kend - kbeg >= 64);
-    pd_i32x4 acc[PD_DIG][2][2];
-#pragma unroll
-    for (int u = 0; u < PD_DIG; ++u)
-#pragma unroll
-        for (int a = 0; a < 2; ++a)
-#pragma unroll
-            for (int b = 0; b < 2; ++b) acc[u][a][b] = pd_i32x4{0, 0, 0, 0};
-    const int h = t >> 8, tt = t & 255;
-    const int sr = pd_srow(tt), sk = (tt & 3) * 16;
-    // a second row tile past the image (odd tile count) re-reads the last one:
-    // its rows are past M and never stored
-    const int8_t *ga = Da + (size_t)min(2 * bm + h, tm64 - 1) * nsteps * (PD_ADIG * PD_BLK) + 64 * sr + sk;
-    const int8_t *gb = Db + 64 * sr + sk;
-    const int T = (kend - kbeg) / 64, st0 = kbeg / 64;
-    pd_i32x4 ra[PD_ADIG], rb[PD_DIG];
-    auto gload = [&](int st) {
-        const int sk2 = st0 + min(st, T - 1);
-        const size_t oa = (size_t)sk2 * (PD_ADIG * PD_BLK), ob = (size_t)sk2 * (PD_DIG * PD_BLK);
-#pragma unroll
-        for (int s = 0; s < PD_ADIG; ++s) ra[s] = *(const pd_i32x4 *)(ga + oa + s * PD_BLK);
-        if (h == 0) {
-#pragma unroll
-            for (int s = 0; s < PD_DIG; ++s) rb[s] = *(const pd_i32x4 *)(gb + ob + s * PD_BLK);
-        }
-    };
-    auto lstore = [&]() {
-#pragma unroll
-        for (int s = 0; s < PD_ADIG; ++s) *(pd_i32x4 *)(pd_lds + (s * 128 + 64 * h + sr) * PD_LD + sk) = ra[s];
-        if (h == 0) {
-#pragma unroll
-            for (int s = 0; s < PD_DIG; ++s) *(pd_i32x4 *)(pd_lds + PD_ASZ2 + (s * 64 + sr) * PD_LD + sk) = rb[s];
-        }
-    };
-    auto mstep = [&]() {
-        pd_i32x4 fb[PD_DIG][2];
-#pragma unroll
-        for (int q = 0; q < PD_DIG; ++q)
-#pragma unroll
-            for (int b = 0; b < 2; ++b)
-                fb[q][b] = *(const pd_i32x4 *)(pd_lds + PD_ASZ2 + (q * 64 + 32 * wc + 16 * b + fr) * PD_LD + fk);
-#pragma unroll
-        for (int s0 = 0; s0 < PD_ADIG; ++s0) {
-            pd_i32x4 fa[2];
-#pragma unroll
-            for (int a = 0; a < 2; ++a) fa[a] = *(const pd_i32x4 *)(pd_lds + (s0 * 128 + 32 * wr + 16 * a + fr) * PD_LD + fk);
-#pragma unroll
-            for (int q = 0; q + s0 < PD_DIG; ++q)
-#pragma unroll
-                for (int a = 0; a < 2; ++a)
-#pragma unroll
-                    for (int b = 0; b < 2; ++b)
-                        acc[s0 + q][a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[a], fb[q][b], acc[s0 + q][a][b], 0, 0, 0);
-        }
-    };
-    gload(0);
-    lstore();
-    __syncthreads();
-    for (int st = 0; st < T; ++st) {
-        gload(st + 1);
-        mstep();
-        __syncthreads();
-        lstore();
-        __syncthreads();
-    }
-    const int i0 = bm * 128 + 32 * wr, j0 = 32 * wc;
-    double *P = part + pstride * z;
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int b = 0; b < 2; ++b)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int i = i0 + 16 * a + (lane >> 4) * 4 + r;
-                const int j = j0 + 16 * b + fr;
-                if (i >= M) continue;
                 double v = 0.0;
 #pragma unroll
                 for (int u = PD_DIG - 1; u >= 0; --u) v += (double)acc[u][a][b][r] * ldexp(1.0, 96 - 8 * u);
@@ -784,118 +675,6 @@ __global__ void __launch_bounds__(512, 1) k_pd_prodA(const int8_t *__restrict__ 
             }
 }
 
-// k_pd_dma: the same products (same pairs, same int32 sums, same combine: the
-// bits of k_pd_prod), built for the HBM stream (round 5).  k_pd_prod moved 52
-// KB a k step per workgroup through registers and ds_write_b128, one step in
-// flight, two barriers a step.  Here both operands' digit blocks of a step go
-// straight to LDS by LDS-DMA (global_load_lds_dwordx4) into a ring of
-// PD_RING stages, PD_RING - 1 steps in flight (no VGPR round trip, no store
-// pass, one raw barrier a step; counted vmcnt, never 0 in the loop):
-//   * wave w owns output columns 16 w .. 16 w + 15 of all 64 rows (four row
-//     tiles), so it DMAs exactly the seven B chunks it reads (its 16
-//     columns, seven digits) plus A's six digit chunks of row tile w, which
-//     every wave reads;
-//   * a 1 KB chunk is 16 columns x 64 k bytes; each DMA carries the bank
-//     swizzle of k_xtx_i8_glds on its source address (lane p loads column
-//     p >> 2, k quarter (p & 3) ^ ((p >> 4) & 2)), so every ds_read_b128
-//     fragment read (column fr, quarter kq at slot 4 fr + (kq ^ ((fr >> 2) &
-//     2))) is conflict-free.
-// Every step issues the same 13 DMAs a wave (a step past the chunk re-reads
-// its last step into a slot no later step reads), so the wait is one fixed
-// count.  One workgroup a CU (3 x 52 KB of LDS).
-#ifndef TP_PD_RING
-#define TP_PD_RING 3
-#endif
-constexpr int PD_RING = TP_PD_RING;
-constexpr int PD_BOFF = PD_ADIG * 4 * 1024;                 // B's chunks after A's in a stage
-constexpr int PD_STAGE = PD_BOFF + PD_DIG * 4 * 1024;       // 52 KB
-static_assert(PD_RING * PD_STAGE <= 160 * 1024, "LDS ring");
-__global__ void __launch_bounds__(256, 1) k_pd_dma(const int8_t *__restrict__ Da, int Kp, int M,
-                                                   const int8_t *__restrict__ Db, const double *__restrict__ rs,
-                                                   const double *__restrict__ cs, double *__restrict__ part,
-                                                   size_t pstride, int kchunk) {
-    __shared__ __attribute__((aligned(16))) int8_t L[PD_RING * PD_STAGE];   // the only LDS object (DMA waits)
-    const int tm = (M + 63) / 64;
-    const int total = (int)gridDim.x;
-    const int xcd = (int)blockIdx.x & 7, slot = (int)blockIdx.x >> 3;
-    const int Lg = xcd * (total >> 3) + min(xcd, total & 7) + slot;
-    const int bm = Lg % tm, z = Lg / tm;
-    const int t = threadIdx.x, lane = t & 63;
-    const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-    const int fr = lane & 15, kq = lane >> 4;
-    const int kbeg = z * kchunk, kend = min(Kp, kbeg + kchunk);
-    const int nsteps = Kp / 64;
-    const int T = (kend - kbeg) / 64, st0 = kbeg / 64;
-    TP_DASSERT(Kp % 64 == 0 && kchunk % 64 == 0 && T >= 1);
-    // DMA sources: column 16 w + (lane >> 2) of this wave's A row tile and B
-    // column tile, k quarter swizzled
-    const int pc = lane >> 2, pk = (lane & 3) ^ ((lane >> 4) & 2);
-    const int8_t *asrc = Da + (size_t)bm * nsteps * (PD_ADIG * PD_BLK) + (size_t)(16 * w + pc) * 64 + 16 * pk;
-    const int8_t *bsrc = Db + (size_t)(16 * w + pc) * 64 + 16 * pk;
-    const int roff = (4 * fr + (kq ^ ((fr >> 2) & 2))) * 16;   // fragment (fr, kq) in a chunk
-    auto issue = [&](int k) {   // step k (clamped) into ring slot k % PD_RING: A digits, then B digits
-        const int sk = st0 + min(k, T - 1);
-        const size_t oa = (size_t)sk * (PD_ADIG * PD_BLK), ob = (size_t)sk * (PD_DIG * PD_BLK);
-        int8_t *dst = L + (k % PD_RING) * PD_STAGE + w * 1024;
-#pragma unroll
-        for (int s = 0; s < PD_ADIG; ++s) pd_glds16(asrc + oa + s * PD_BLK, dst + s * 4096);
-#pragma unroll
-        for (int s = 0; s < PD_DIG; ++s) pd_glds16(bsrc + ob + s * PD_BLK, dst + PD_BOFF + s * 4096);
-    };
-    pd_i32x4 acc[PD_DIG][4];
-#pragma unroll
-    for (int u = 0; u < PD_DIG; ++u)
-#pragma unroll
-        for (int a = 0; a < 4; ++a) acc[u][a] = pd_i32x4{0, 0, 0, 0};
-    auto mstep = [&](int k) {
-        const int8_t *Ls = L + (k % PD_RING) * PD_STAGE + roff;
-        pd_i32x4 fb[PD_DIG], fa[2][4];
-#pragma unroll
-        for (int s = 0; s < PD_DIG; ++s) fb[s] = *(const pd_i32x4 *)(Ls + PD_BOFF + s * 4096 + w * 1024);
-#pragma unroll
-        for (int a = 0; a < 4; ++a) fa[0][a] = *(const pd_i32x4 *)(Ls + a * 1024);
-#pragma unroll
-        for (int s0 = 0; s0 < PD_ADIG; ++s0) {
-            if (s0 + 1 < PD_ADIG) {
-#pragma unroll
-                for (int a = 0; a < 4; ++a) fa[(s0 + 1) & 1][a] = *(const pd_i32x4 *)(Ls + (s0 + 1) * 4096 + a * 1024);
-            }
-#pragma unroll
-            for (int tt = 0; tt + s0 < PD_DIG; ++tt)
-#pragma unroll
-                for (int a = 0; a < 4; ++a)
-                    acc[s0 + tt][a] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[s0 & 1][a], fb[tt], acc[s0 + tt][a], 0, 0, 0);
-        }
-    };
-#pragma unroll
-    for (int k = 0; k < PD_RING - 1; ++k) issue(k);
-    for (int k = 0; k < T; ++k) {
-        // step k landed: this wave's DMAs by the count (the RING - 2 later
-        // steps' 13 each stay in flight), the others' by the barrier, after
-        // which step k - 1's slot is free for step k + RING - 1
-        pd_wait_vm<(PD_RING - 2) * (PD_DIG + PD_ADIG)>();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        issue(k + PD_RING - 1);
-        mstep(k);
-    }
-    pd_wait_vm<0>();   // the clamped re-reads of the tail: nothing in flight at exit
-    const int i0 = bm * 64, j = 16 * w + fr;
-    double *P = part + pstride * z;
-    const double csj = cs[j];
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int i = i0 + 16 * a + kq * 4 + r;
-            if (i >= M) continue;
-            double v = 0.0;
-#pragma unroll
-            for (int u = PD_DIG - 1; u >= 0; --u) v += (double)acc[u][a][r] * ldexp(1.0, 96 - 8 * u);
-            P[(size_t)i + (size_t)j * M] = (v * rs[i]) * csj;
-        }
-}
-
 // k chunks from K alone (shards agree); <= 16384 rows a chunk (accumulator range)
 #ifndef TP_PD_KDIV
 #define TP_PD_KDIV 960   // C3: 8 k chunks, 984 workgroups (~4 full rounds of one a CU; 1024: 7, 861)
@@ -927,9 +706,8 @@ static void launch_digits_cm(const double *A, int lda, int K, int c_begin, int c
     TP_HIP(hipGetLastError());
 }
 
-int g_pd_cm = 1;   // knob 39: C's column means in A's digit pass (0: the separate k_colmean pass); same bits
 
-bool prod_digits_means_ok(int K) { return g_pd_cm && K >= 64 && (K + 63) / 64 * 64 <= 8192; }
+bool prod_digits_means_ok(int K) { return cfg_pd_cm && K >= 64 && (K + 63) / 64 * 64 <= 8192; }
 
 void prod_digits_build(Ctx &c, const double *A, int lda, int K, int cols, int col0, ProdDigits &pd, double *cm,
                        int ncm) {
@@ -959,7 +737,7 @@ void prod_digits_build(Ctx &c, const double *A, int lda, int K, int cols, int co
     if (pd.Kp <= 1024 * PD_REG_IT)
         hipLaunchKernelGGL((k_pd_digits_reg<PD_REG_IT, PD_ADIG>), dim3((unsigned)cp), dim3(256), 0, s, A, lda, K, cols,
                            pd.Kp, (int8_t *)pd.d, (double *)pd.rs);
-    else if (pd.Kp <= 4096 * 6 && g_pd_digits_big)   // one read of each long column (1024 threads)
+    else if (pd.Kp <= 4096 * 6 && cfg_pd_digits_big)   // one read of each long column (1024 threads)
         hipLaunchKernelGGL((k_pd_digits_reg<6, PD_ADIG, 1024>), dim3((unsigned)cp), dim3(1024), 0, s, A, lda, K, cols,
                            pd.Kp, (int8_t *)pd.d, (double *)pd.rs);
     else
@@ -990,7 +768,7 @@ int prod_i8_partials(Ctx &c, const ProdDigits &pd, int r0, int M, const double *
     double *cs = (double *)(bb + (PD_DIG * slb + 255) / 256 * 256);
     const int SL = (pd.Kp + 1023) / 1024;
     double *pmax = (double *)(bb + (PD_DIG * slb + 255) / 256 * 256 + 512 * sizeof(double));
-    if (pd.Kp <= 1024 * PD_REG_IT && g_pd_digits_blk) {   // one launch, a workgroup per (column, slice)
+    if (pd.Kp <= 1024 * PD_REG_IT && cfg_pd_digits_blk) {   // one launch, a workgroup per (column, slice)
         hipLaunchKernelGGL((k_pd_digits_blk<PD_REG_IT>), dim3((unsigned)(N * SL)), dim3(256), 0, s, B, ldb, K, N, pd.Kp,
                            Db, cs);
     } else if (pd.Kp <= 1024 * PD_REG_IT) {   // one launch, the block read once
@@ -1008,22 +786,14 @@ int prod_i8_partials(Ctx &c, const ProdDigits &pd, int r0, int M, const double *
     const int8_t *Da = pd.d + (size_t)(r0 - pd.col0) * pd.Kp * PD_ADIG;   // whole tiles: 64 columns x Kp x PD_ADIG
     const double *rs = pd.rs + (r0 - pd.col0);
     const int tm = (M + 63) / 64;
-    // one LDS buffer, two workgroups a CU: the 32 C3 products 4.57 ms against
-    // 5.35 for the double-buffered one-workgroup form (knob 36 = 2, A/B)
+    // one LDS buffer, two workgroups a CU (the double-buffered one-workgroup
+    // form, the 128-row tiles and the LDS-DMA ring measured slower and were
+    // removed in round 6)
     const dim3 ga((unsigned)((M + 127) / 128 * S));
     if (N == 32)
         hipLaunchKernelGGL((k_pd_prodA<1, 2>), ga, dim3(512), 0, s, Da, pd.Kp, M, Db, rs, cs, *part, pstride, kc);
-    else if (g_prod_i8 == 5)
+    else if (t_knob.prod_i8 == 5)
         hipLaunchKernelGGL((k_pd_prodA<1, 4>), ga, dim3(512), 0, s, Da, pd.Kp, M, Db, rs, cs, *part, pstride, kc);
-    else if (g_prod_i8 == 4)
-        hipLaunchKernelGGL(k_pd_prod128, dim3((unsigned)((M + 127) / 128 * S)), dim3(512), (size_t)PD_BUF2, s, Da, pd.Kp,
-                           M, Db, rs, cs, *part, pstride, kc);
-    else if (g_prod_i8 == 3)
-        hipLaunchKernelGGL(k_pd_dma, dim3((unsigned)(tm * S)), dim3(256), 0, s, Da, pd.Kp, M, Db, rs, cs, *part,
-                           pstride, kc);
-    else if (g_prod_i8 == 2)
-        hipLaunchKernelGGL(k_pd_prod<2>, dim3((unsigned)(tm * S)), dim3(256), (size_t)2 * PD_BUF, s, Da, pd.Kp, M, Db,
-                           rs, cs, *part, pstride, kc);
     else
         hipLaunchKernelGGL(k_pd_prod<1>, dim3((unsigned)(tm * S)), dim3(256), (size_t)PD_BUF, s, Da, pd.Kp, M, Db, rs,
                            cs, *part, pstride, kc);

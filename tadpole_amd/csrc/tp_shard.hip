@@ -146,24 +146,23 @@ void comm_abort(Ctx &c) {
     if (owner) (void)rccl().abort((ncclComm_t)comm);
 }
 
-int g_shard_inject = 0;   // test hook (knob 30): the next N sharded waits fail as a device error
+std::atomic<int> g_shard_inject{0};   // test hook (knob 30): the next N sharded waits fail as a device error
 
 // Unsharded waits poll the stream (yielding the core) before blocking: the
 // pipeline's read-backs are short waits, and hipStreamSynchronize's blocking
 // wake-up put ~45 us between a copy and the next command (rocprof trace, four
 // such host round trips after the sweep, two in the mask).  Waits longer than
-// g_sync_spin_us block as before.
-int g_sync_spin_us = 20000;   // knob 40 (0: always block)
+// cfg_sync_spin_us block as before.
 template <typename Query, typename Block>
 static void poll_then_block(Query query, Block block) {
-    if (g_sync_spin_us > 0) {
+    if (cfg_sync_spin_us > 0) {
         const auto t0 = std::chrono::steady_clock::now();
         for (;;) {
             const hipError_t e = query();
             if (e == hipSuccess) return;
             if (e != hipErrorNotReady) TP_HIP(e);
             if (std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() >
-                g_sync_spin_us)
+                cfg_sync_spin_us)
                 break;
             std::this_thread::yield();
         }
@@ -176,8 +175,10 @@ void stream_sync(Ctx &c, hipStream_t s) {
         poll_then_block([&] { return hipStreamQuery(s); }, [&] { return hipStreamSynchronize(s); });
         return;
     }
-    if (g_shard_inject > 0) {
-        --g_shard_inject;
+    int inj = g_shard_inject.load();
+    while (inj > 0 && !g_shard_inject.compare_exchange_weak(inj, inj - 1)) {
+    }
+    if (inj > 0) {
         TP_HIP(hipStreamSynchronize(s));
         comm_abort(c);
         fail(TP_ERR_HIP, "injected device failure in a sharded call (knob 30); communicator aborted");
@@ -378,8 +379,6 @@ void xtx_product(Ctx &c, const double *X, int n, double *S) {
     launch_clean_symmetrize(S, n, true, c.cur);
 }
 
-int g_xtx_fused = 1;
-int g_shard_slab = 1;   // 0: X'X into S, then the separate correlation epilogue (A/B, tests)
 
 void cor_product(Ctx &c, const double *X, int n, const double *m, const GatherStats *gs, double *S, double *C,
                  double *sd, double *cmean, const CorSlab *slab, bool *cm_defer) {
@@ -411,7 +410,7 @@ void cor_product(Ctx &c, const double *X, int n, const double *m, const GatherSt
         return;
     }
     int ns = -1;
-    if (gs && g_xtx_fused && n >= 1024) ns = xtx_int_slices_cols(c, gs->cmax, gs->cbad, n);
+    if (gs && t_knob.xtx_fused && n >= 1024) ns = xtx_int_slices_cols(c, gs->cmax, gs->cbad, n);
     if (!(ns == 1 || ns == 2)) {
         if (!X) {   // the gather skipped X (int8 path expected): gather it now, same means
             if (!gs || !gs->M) fail(TP_ERR_ARG, "cor_product: no X and no gather source");

@@ -1592,15 +1592,13 @@ __global__ void __launch_bounds__(256) k_ch_segstat(SweepDev sd) {
     }
 }
 
-int g_ch_dedup = 1;
-int g_ch_dedup_ucap = 0;
 static size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
 size_t sweep_dedup_bytes(int n, int k, int ntrees, int seg_cap, int *hcap, int *ucap) {
     const long ins = (long)ntrees * (long)std::max(1, std::min(seg_cap, n));
     long h = 1024;
     while (h < 2 * ins) h <<= 1;
     long u = std::min<long>(ins, std::max<long>(4096, 2L * n));
-    if (g_ch_dedup_ucap > 0) u = std::min<long>(u, g_ch_dedup_ucap);
+    if (t_knob.ch_dedup_ucap > 0) u = std::min<long>(u, t_knob.ch_dedup_ucap);
     *hcap = (int)h;
     *ucap = (int)u;
     return al256((size_t)h * 8) + al256((size_t)h * 4) + al256((size_t)u * 8) + al256((size_t)u * (k + 1) * 8) + 256;
@@ -1908,7 +1906,6 @@ static bool coniss_in_lds2(int n) { return coniss_lds2_bytes(n) <= 160 * 1024 - 
 // does not fit (~10.2k-12.3k bins; 11 000 bins: sweep 21.5 -> 18.8 ms against the
 // global variant), 2: every sweep, 1: lean sweeps, 0: never.  Not below: at C3
 // the extra dependent LDS read on the merge chain costs 10.9 -> 12.8 ms
-int g_coniss_lds2 = 3;
 
 // seed kernel + CONISS (cost0 = initial adjacent costs, ntrees x nbk*64, then
 // the global-variant link scratch: see sweep_cost0_doubles)
@@ -1936,11 +1933,9 @@ static void launch_coniss_bs(const SweepDev &sd, double *cost0, size_t lds, hipS
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL((k_coniss_t<STAMPS, BS, GLB, LU>), dim3(sd.ntrees), dim3(128), lds, s, sd, cost0);
 }
-int g_coniss_lu = 1;   // 0: the global variant keeps its links in global memory too
 // knob 52: the batched CONISS kernel (k_coniss_b) where it applies (costs and
 // links in LDS, k <= 256) -- 2 (default): also for lean sweeps (C4, 8 streams:
 // 0.265 -> 0.229 s), 1: not for them, 0: never (the two-wave k_coniss_t)
-int g_coniss_batch = 2;
 // lean sweeps (another pipeline in flight on the device) of matrices that fit
 // LDS, from this many bins (knob 48; 0: never): costs global and only the
 // links in LDS (2 bytes a bin) so several trees share a CU -- the LDS
@@ -1948,7 +1943,6 @@ int g_coniss_batch = 2;
 // waves use two of its SIMDs.  Measured on C4 (8 streams): 0.27-0.29 s at
 // 4096 or 2048 vs 0.26 s off -- the global costs slow each tree more than
 // the sharing gains -- so off
-int g_coniss_lean_min = 0;
 
 static void run_coniss(const SweepDev &sd_in, hipStream_t s, bool stamped, Ctx *prof) {
     SweepDev sd = sd_in;
@@ -1979,10 +1973,10 @@ static void run_coniss(const SweepDev &sd_in, hipStream_t s, bool stamped, Ctx *
     else
         hipLaunchKernelGGL(k_seed<16>, dim3(sd.ntrees, nbk), dim3(64), 0, s, sd, cost0);
     TP_HIP(hipGetLastError());
-    const bool lean_small = sd.lds_lean && g_coniss_lean_min > 0 && sd.n >= g_coniss_lean_min;
+    const bool lean_small = sd.lds_lean && t_knob.coniss_lean_min > 0 && sd.n >= t_knob.coniss_lean_min;
     const bool in_lds2 = !lean_small && coniss_in_lds2(sd.n) &&
-                         (g_coniss_lds2 == 2 || (g_coniss_lds2 == 1 && sd.lds_lean) ||
-                          (g_coniss_lds2 == 3 && !coniss_in_lds(sd.n)));
+                         (t_knob.coniss_lds2 == 2 || (t_knob.coniss_lds2 == 1 && sd.lds_lean) ||
+                          (t_knob.coniss_lds2 == 3 && !coniss_in_lds(sd.n)));
     const bool in_lds = (coniss_in_lds(sd.n) || in_lds2) && !lean_small;
     // global variant: 16-bit links in LDS when they fit (costs stay global)
     const size_t lu_bytes = coniss_link_stride(sd.n) * 4;
@@ -1990,7 +1984,7 @@ static void run_coniss(const SweepDev &sd_in, hipStream_t s, bool stamped, Ctx *
     // lds_lean (TP_FLAG_LDS_LEAN: another pipeline runs beside this one): only
     // the link array in LDS, rn derived from it (LU = 2, half the bytes), so
     // these trees fit on CUs whose LDS the other pipeline's trees hold
-    const bool lu_ok = !in_lds && g_coniss_lu && sd.n + 64 < 0xFFFF && bs <= 11;
+    const bool lu_ok = !in_lds && cfg_coniss_lu && sd.n + 64 < 0xFFFF && bs <= 11;
     const bool lu2 = lu_ok && sd.lds_lean;
     const bool lu = lu_ok && !lu2 && lu_bytes <= 150 * 1024;
     const size_t lds = in_lds2 ? coniss_lds2_bytes(sd.n)
@@ -1999,8 +1993,8 @@ static void run_coniss(const SweepDev &sd_in, hipStream_t s, bool stamped, Ctx *
     // the batched kernel (round 6): costs, links and the block minima in LDS,
     // trees of up to 4 column slots
     const size_t lds_b = coniss_lds_bytes(sd.n) + (size_t)nbk * 8;
-    if (g_coniss_batch && sd.tree0 + sd.ntrees <= 256 && bs <= 3 && !lean_small &&
-        lds_b + sizeof(CbShared) <= 160 * 1024 - 64 && !(sd.lds_lean && g_coniss_batch < 2)) {
+    if (t_knob.coniss_batch && sd.tree0 + sd.ntrees <= 256 && bs <= 3 && !lean_small &&
+        lds_b + sizeof(CbShared) <= 160 * 1024 - 64 && !(sd.lds_lean && t_knob.coniss_batch < 2)) {
         auto go = [&](auto kern) {
             TP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_b));
             hipLaunchKernelGGL(kern, dim3(sd.ntrees), dim3(64 * CB_W), lds_b, s, sd, cost0);

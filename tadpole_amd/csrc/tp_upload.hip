@@ -63,7 +63,7 @@ static bool pack_u16(const double *src, size_t n, uint16_t *dst) {
 // Optionally one upload at a time per device, first come first served
 // (concurrent uploads split the PCIe link, ~56 GB/s on the MI355X box, evenly;
 // in turn the largest matrix of a genome run, submitted first, gets it whole --
-// measured no faster, see g_upload_mode).
+// measured no faster, see t_knob.upload_mode).
 struct UploadTurn {
     std::mutex mu;
     std::condition_variable cv;
@@ -75,7 +75,6 @@ static UploadTurn g_turn[64];
 // median (4.5 % spread), raw 0.299, in turn 0.279-0.284 with runs up to 0.32,
 // in turn + packed 0.319 -- staggering the uploads staggers the pipelines
 // behind them more than it helps the first one
-int g_upload_mode = 2;
 
 template <typename F>
 static void split_run(size_t n, int th, F f) {   // f(offset, count) over th contiguous parts
@@ -95,9 +94,9 @@ static void split_run(size_t n, int th, F f) {   // f(offset, count) over th con
 
 size_t upload_host(Ctx &c, const void *host, size_t bytes, void *d_dst, int nthreads, bool counts) {
     if (bytes == 0) return 0;
-    if (!(g_upload_mode & 2)) counts = false;
+    if (!(t_knob.upload_mode & 2)) counts = false;
     UploadTurn &turn = g_turn[c.device & 63];
-    const bool in_turn = (g_upload_mode & 1) != 0;
+    const bool in_turn = (t_knob.upload_mode & 1) != 0;
     unsigned long long ticket = 0;
     if (in_turn) {
         std::unique_lock<std::mutex> lk(turn.mu);

@@ -178,7 +178,7 @@ __global__ void __launch_bounds__(256) k_xtx_i8(const int8_t *__restrict__ S, in
 // column inside each), so the ~32-64 tiles one XCD holds at a time share 16
 // slice panels instead of one B panel and ~40 A panels (same tiles, same bits).
 // Sharded calls (tcol0 > 0) keep the column order.
-constexpr int XB = 128, XK = 128, XLD = 160, XST = 8;   // 160-B column stride: conflict-free b128 fragments and stores
+constexpr int XB = 128, XST = 8;
 __device__ __forceinline__ void xtx_supertile(int L, int tn, int &bm, int &bn) {
     const int U = (tn + XST - 1) / XST;
     for (int Q = 0; Q < U; ++Q) {
@@ -213,149 +213,9 @@ __device__ __forceinline__ void xtx_supertile(int L, int tn, int &bm, int &bn) {
 // upper tile tiles[b] and stores only the elements whose column lies in
 // [c0, c1), at C[row + (col - c0) n] -- the same tiles and arithmetic as the
 // whole matrix, so a slab holds exactly those columns' bits.
-template <int NS, bool COR = false>
-__global__ void __launch_bounds__(512) k_xtx_i8_big(const int8_t *__restrict__ S, int n, int Kp, int Np,
-                                                    double *__restrict__ C, int tcol0, int tn_all,
-                                                    const double *__restrict__ cm = nullptr,
-                                                    const double *__restrict__ csd = nullptr,
-                                                    const int2 *__restrict__ tiles = nullptr, int c0 = 0,
-                                                    int c1 = 0x7fffffff) {
-    __shared__ __attribute__((aligned(16))) int8_t Ls[2][2][NS][XB * XLD];   // [buf][A/B][slice]
-    int bm, bn;
-    if (tiles) {
-        const int2 tl = tiles[blockIdx.x];
-        bm = tl.x;
-        bn = tl.y;
-    } else if (tn_all > 0) {
-        const int total = tn_all * (tn_all + 1) / 2;
-        const int xcd = (int)blockIdx.x & 7, slot = (int)blockIdx.x >> 3;
-        xtx_supertile(xcd * (total >> 3) + min(xcd, total & 7) + slot, tn_all, bm, bn);
-    } else {
-        int id = blockIdx.x;
-        bn = tcol0;
-        while (id > bn) {
-            id -= bn + 1;
-            ++bn;
-        }
-        bm = id;
-    }
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const int wm = (w & 1) * 64, wn = (w >> 1) * 32;
-    const size_t slice = (size_t)Np * Kp;
-    const int ia = bm * XB, jb = bn * XB;
-    // global -> LDS: per (operand, slice) 128 columns x 128 bytes of k, two
-    // 16-byte loads per thread (k bytes lk and lk + 64).  Kp is an odd multiple
-    // of 64, so the second half of the last k-block lies past it: it is read
-    // as zeros, which add nothing to the exact int32 sums.
-    const int lc = t >> 2, lk = (t & 3) * 16;
-    auto gload = [&](i32x4 (&r)[2][NS][2], int kb) {
-        const int ca = min(ia + lc, Np - 1), cb = min(jb + lc, Np - 1);
-#pragma unroll
-        for (int s = 0; s < NS; ++s)
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int k0 = kb + 64 * h + lk;
-                const bool in = kb + 64 * h < Kp;
-                TP_DASSERT(!in || (k0 + 16 <= Kp && ca >= 0 && cb >= 0));
-                r[0][s][h] = in ? *(const i32x4 *)(S + s * slice + (size_t)ca * Kp + k0) : i32x4{0, 0, 0, 0};
-                r[1][s][h] = in ? *(const i32x4 *)(S + s * slice + (size_t)cb * Kp + k0) : i32x4{0, 0, 0, 0};
-            }
-    };
-    auto lstore = [&](int buf, const i32x4 (&r)[2][NS][2]) {
-#pragma unroll
-        for (int o = 0; o < 2; ++o)
-#pragma unroll
-            for (int s = 0; s < NS; ++s)
-#pragma unroll
-                for (int h = 0; h < 2; ++h) *(i32x4 *)(&Ls[buf][o][s][lc * XLD + 64 * h + lk]) = r[o][s][h];
-    };
-    i32x4 acc[NS][NS][4][2];
-#pragma unroll
-    for (int s = 0; s < NS; ++s)
-#pragma unroll
-        for (int u = 0; u < NS; ++u)
-#pragma unroll
-            for (int a = 0; a < 4; ++a)
-#pragma unroll
-                for (int b = 0; b < 2; ++b) acc[s][u][a][b] = i32x4{0, 0, 0, 0};
-    i32x4 rg[2][NS][2];
-    gload(rg, 0);
-    lstore(0, rg);
-    __syncthreads();
-    const int fr = lane & 15, fk = (lane >> 4) * 16;
-    int buf = 0;
-    for (int kb = 0; kb < Kp; kb += XK) {
-        const bool more = kb + XK < Kp;
-        if (more) gload(rg, kb + XK);
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {   // two MFMA k-steps of 64 per barrier
-            i32x4 fa[NS][4], fb[NS][2];
-#pragma unroll
-            for (int s = 0; s < NS; ++s) {
-#pragma unroll
-                for (int a = 0; a < 4; ++a)
-                    fa[s][a] = *(const i32x4 *)(&Ls[buf][0][s][(wm + 16 * a + fr) * XLD + 64 * h + fk]);
-#pragma unroll
-                for (int b = 0; b < 2; ++b)
-                    fb[s][b] = *(const i32x4 *)(&Ls[buf][1][s][(wn + 16 * b + fr) * XLD + 64 * h + fk]);
-            }
-#pragma unroll
-            for (int s = 0; s < NS; ++s)
-#pragma unroll
-                for (int u = 0; u < NS; ++u)
-#pragma unroll
-                    for (int a = 0; a < 4; ++a)
-#pragma unroll
-                        for (int b = 0; b < 2; ++b)
-                            acc[s][u][a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[s][a], fb[u][b],
-                                                                                    acc[s][u][a][b], 0, 0, 0);
-        }
-        if (more) lstore(buf ^ 1, rg);
-        __syncthreads();
-        buf ^= 1;
-    }
-    // COR: the tile's column means and sds (128 rows, 128 columns) into LDS
-    // (the staging buffers are free after the last barrier)
-    double *pm = (double *)&Ls[0][0][0][0];   // [0,128) m rows, [128,256) m cols, [256,384) sd rows, [384,512) sd cols
-    if constexpr (COR) {
-        if (t < 128) {
-            const int i = min(ia + t, n - 1), j = min(jb + t, n - 1);
-            pm[t] = cm[i];
-            pm[128 + t] = cm[j];
-            pm[256 + t] = csd[i];
-            pm[384 + t] = csd[j];
-        }
-        __syncthreads();
-    }
-    const double fn = (double)n, fn1 = (double)(n - 1);
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 2; ++b)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int il = wm + 16 * a + (lane >> 4) * 4 + r, jl = wn + 16 * b + fr;
-                const int i = ia + il;
-                const int j = jb + jl;
-                if (i >= n || j >= n || i > j) continue;
-                long long v = 0;
-#pragma unroll
-                for (int s = 0; s < NS; ++s)
-#pragma unroll
-                    for (int u = 0; u < NS; ++u) v += (long long)acc[s][u][a][b][r] << (7 * (s + u));
-                double d = (double)v;
-                if constexpr (COR) {   // k_cor_epilogue's expression, element (i, j); (j, i) is the same value
-                    const double cij = (d - fn * (pm[il] * pm[128 + jl])) / fn1;
-                    d = cij / (pm[256 + il] * pm[384 + jl]);
-                    if (isnan(d)) d = 0.0;
-                }
-                if (j >= c0 && j < c1) C[(size_t)i + (size_t)(j - c0) * n] = d;
-                if (i >= c0 && i < c1) C[(size_t)j + (size_t)(i - c0) * n] = d;
-            }
-}
-
-// k_xtx_i8_glds: the same tiles, tile order, waves and exact arithmetic as
-// k_xtx_i8_big, with the slices staged by LDS-DMA (global_load_lds_dwordx4)
+// k_xtx_i8_glds: 128 x 128 upper tiles, the supertile order above, 8 waves and
+// exact arithmetic (the register-staged k_xtx_i8_big before it, removed in
+// round 6), with the slices staged by LDS-DMA (global_load_lds_dwordx4)
 // into a ring of 64-deep k-blocks (5 stages of 32 KiB for 2 slices): no VGPR round trip and no
 // ds_write pass (k_xtx_i8_big's 64 KiB of b128 stores per k-block ran
 // between its MFMA blocks), all but two stages in flight across each raw barrier
@@ -968,7 +828,7 @@ static int slices_for(Ctx &c, unsigned long long *mb) {
 
 // Decide the path for X (n x n, col-major, device): 0 = fp64, else the slice count.
 int xtx_int_slices(Ctx &c, const double *d_X, int n) {
-    if (g_xtx_int8 == 0 || n > 130000) return 0;
+    if (t_knob.xtx_int8 == 0 || n > 130000) return 0;
     unsigned long long *mb = (unsigned long long *)c.buf[S_SHARD2].as<char>(64);
     int *flag = (int *)(mb + 1);
     TP_HIP(hipMemsetAsync(mb, 0, 16, c.cur));
@@ -982,7 +842,7 @@ int xtx_int_slices(Ctx &c, const double *d_X, int n) {
 int xtx_kp(int n);
 // The same decision from the gather's per-column statistics (k_gather_prep)
 int xtx_int_slices_cols(Ctx &c, const double *d_cmax, const int *d_cbad, int n) {
-    if (g_xtx_int8 == 0 || n > 130000) return 0;
+    if (t_knob.xtx_int8 == 0 || n > 130000) return 0;
     unsigned long long *mb = (unsigned long long *)c.buf[S_SMALL2].as<char>(64);
     int *flag = (int *)(mb + 1);
     hipLaunchKernelGGL(k_colflags, dim3(1), dim3(256), 0, c.cur, d_cmax, d_cbad, n, mb, flag);
@@ -1014,9 +874,6 @@ const int8_t *xtx_slices(Ctx &c, const double *d_X, int n, int ns) {
     return sl;
 }
 
-int g_xtx_supertile = 1;
-int g_xtx_glds = 1;   // 0: k_xtx_i8_big (register-staged), 1: k_xtx_i8_glds (knob 32)
-int g_xtx_nz = 1;     // 1: k_xtx_i8_glds skips the high slice's zero blocks (knob 34)
 
 // Block-nonzero map of the high slice (slice 1): bit kb & 31 of word
 // nzw[cb * NW + kb / 32] is set when any byte of columns 128 cb .. + 127, k
@@ -1047,21 +904,16 @@ __global__ void __launch_bounds__(256) k_slice_nz(const int8_t *__restrict__ S1,
 template <int NS, bool COR>
 static void launch_xtx128_t(Ctx &c, unsigned nb, const int8_t *sl, int n, int Kp, int Np, double *d_S, int tc0,
                             int tn_all, const double *cm, const double *csd, const int2 *d_tl, int c0, int c1) {
-    if (g_xtx_glds) {
-        unsigned *nzw = nullptr;
-        const int NW = (Kp / 64 + 31) / 32;
-        if (NS == 2 && g_xtx_nz) {
-            if (NW > 64) fail(TP_ERR_INTERNAL, "xtx_int8: k blocks past the 64-word nonzero map");
-            nzw = c.buf[S_XNZ].as<unsigned>((size_t)(Np / 128) * NW);
-            hipLaunchKernelGGL(k_slice_nz, dim3((unsigned)(Np / 128), (unsigned)NW), dim3(256), 0, c.cur,
-                               sl + (size_t)Np * Kp, Kp, NW, nzw);
-        }
-        hipLaunchKernelGGL((k_xtx_i8_glds<NS, COR>), dim3(nb), dim3(512), 0, c.cur, sl, n, Kp, Np, d_S, tc0, tn_all,
-                           cm, csd, d_tl, c0, c1, nzw, NW);
+    unsigned *nzw = nullptr;
+    const int NW = (Kp / 64 + 31) / 32;
+    if (NS == 2 && cfg_xtx_nz) {
+        if (NW > 64) fail(TP_ERR_INTERNAL, "xtx_int8: k blocks past the 64-word nonzero map");
+        nzw = c.buf[S_XNZ].as<unsigned>((size_t)(Np / 128) * NW);
+        hipLaunchKernelGGL(k_slice_nz, dim3((unsigned)(Np / 128), (unsigned)NW), dim3(256), 0, c.cur,
+                           sl + (size_t)Np * Kp, Kp, NW, nzw);
     }
-    else
-        hipLaunchKernelGGL((k_xtx_i8_big<NS, COR>), dim3(nb), dim3(512), 0, c.cur, sl, n, Kp, Np, d_S, tc0, tn_all,
-                           cm, csd, d_tl, c0, c1);
+    hipLaunchKernelGGL((k_xtx_i8_glds<NS, COR>), dim3(nb), dim3(512), 0, c.cur, sl, n, Kp, Np, d_S, tc0, tn_all,
+                       cm, csd, d_tl, c0, c1, nzw, NW);
 }
 static void launch_xtx128(Ctx &c, int ns, unsigned nb, const int8_t *sl, int n, int Kp, int Np, double *d_S, int tc0,
                           int tn_all, const double *cm, const double *csd, const int2 *d_tl, int c0, int c1) {
@@ -1073,7 +925,6 @@ static void launch_xtx128(Ctx &c, int ns, unsigned nb, const int8_t *sl, int n, 
     else fail(TP_ERR_ARG, "xtx_int8 (128-tiles): 1..2 slices");
 }
 
-int g_xtx_w = 1;   // knob 44: the whole upper triangle by k_xtx_i8_w (256 x 128 tiles; 0: 128-tiles)
 
 template <int NS, bool COR>
 static void launch_xtx_w_t(Ctx &c, const int8_t *sl, int n, int Kp, int Np, double *d_S, const double *cm,
@@ -1081,7 +932,7 @@ static void launch_xtx_w_t(Ctx &c, const int8_t *sl, int n, int Kp, int Np, doub
     const long nt = d_tl ? ntl : xtx_w_tiles(Np / 128);
     unsigned *nzw = nullptr;
     const int NW = (Kp / 64 + 31) / 32;
-    if (NS == 2 && g_xtx_nz) {
+    if (NS == 2 && cfg_xtx_nz) {
         nzw = c.buf[S_XNZ].as<unsigned>((size_t)(Np / 128) * NW);
         hipLaunchKernelGGL(k_slice_nz, dim3((unsigned)(Np / 128), (unsigned)NW), dim3(256), 0, c.cur,
                            sl + (size_t)Np * Kp, Kp, NW, nzw);
@@ -1135,7 +986,7 @@ bool xtx_w_exec(Ctx &c, double *out) {
     return true;
 }
 static bool xtx_w_applies(int ns, int Kp) {
-    if (!g_xtx_w || !g_xtx_glds || (ns != 1 && ns != 2)) return false;
+    if (!t_knob.xtx_w || (ns != 1 && ns != 2)) return false;
     return ns == 1 || Kp / 64 <= XW_MAXNK;   // t01's int32 bound
 }
 // the whole upper triangle (d_tl null) or a column slab's tiles by k_xtx_i8_w
@@ -1161,12 +1012,12 @@ void xtx_int8_tiles128(Ctx &c, const int8_t *sl, int n, int ns, double *d_S, int
     tc0 = std::max(0, tc0);
     tc1 = tc1 < 0 ? tn : std::min(tn, tc1);
     if (tc1 <= tc0) return;
-    if (tc0 == 0 && tc1 == tn && g_xtx_supertile && xtx_w_applies(ns, Kp)) {
+    if (tc0 == 0 && tc1 == tn && cfg_xtx_supertile && xtx_w_applies(ns, Kp)) {
         launch_xtx_w(c, ns, sl, n, Kp, Np, d_S, cm, csd);
         return;
     }
     const unsigned nb = (unsigned)((long)tc1 * (tc1 + 1) / 2 - (long)tc0 * (tc0 + 1) / 2);
-    const int tn_all = (tc0 == 0 && tc1 == tn && g_xtx_supertile) ? tn : 0;
+    const int tn_all = (tc0 == 0 && tc1 == tn && cfg_xtx_supertile) ? tn : 0;
     launch_xtx128(c, ns, nb, sl, n, Kp, Np, d_S, tc0, tn_all, cm, csd, nullptr, 0, 0x7fffffff);
     TP_HIP(hipGetLastError());
 }
@@ -1218,6 +1069,5 @@ void xtx_int8_tiles(Ctx &c, const int8_t *sl, int n, int ns, double *d_S, int tc
     TP_HIP(hipGetLastError());
 }
 
-int g_xtx_int8 = 1;   // 0: always the fp64 MFMA product (diagnostics / tests)
 
 }  // namespace tp

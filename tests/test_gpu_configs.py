@@ -66,11 +66,11 @@ def test_config_golden(gpu, name):
     assert got.timings_ms[13] <= 1e-11
 
 
-@pytest.mark.parametrize("prod", [0, 2])
+@pytest.mark.parametrize("prod", [0, 1])
 def test_config_c3_golden_product_paths(gpu, prod):
     """C3 with the Krylov products on the paths the default does not take
-    (knob 36: 0 the fp64 k_gemm_ts, 2 the double-buffered int8-digit kernel;
-    the default, the one-buffer int8 kernel, is test_config_golden): the
+    (knob 36: 0 the fp64 k_gemm_ts, 1 the 64-row-tile int8-digit kernel
+    k_pd_prod; the default, k_pd_prodA, is test_config_golden): the
     golden's n_pcs, clusters, merge order and every level, CH within 1e-6."""
     import tadpole_amd as tp
     z = np.load(os.path.join(GOLD, "c3.npz"))
@@ -94,13 +94,10 @@ def test_config_c3_from_hbm(gpu):
     _check(got, z)
 
 
-@pytest.mark.parametrize("forced,space", [(True, "C"), (True, "C-full-pip"), (True, "G"), (True, "G-full-cgs"),
-                                          (True, "G-int8"), (False, "G")])
+@pytest.mark.parametrize("forced,space", [(True, "C"), (True, "G"), (True, "G-int8"), (False, "G")])
 def test_pca_krylov_path_vs_lapack(gpu, forced, space):
     """The block Krylov PCA (G never formed; Krylov space of G, the default,
-    or of C: knob 20; G with the first CGS pass against every block instead of
-    the last two: knob 28; C with the first PIP pass against every block
-    instead of K_0 and the last two: knob 33; G with the products on the int8
+    or of C: knob 20; G with the products on the int8
     MFMA from digit images -- six digits of C, seven of each block: knob 36) against LAPACK's SVD on a matrix below its default
     size threshold (forced) and the G-formed path on the same matrix: every
     prefix subspace the sweep uses agrees."""
@@ -112,16 +109,12 @@ def test_pca_krylov_path_vs_lapack(gpu, forced, space):
     c = O.sparse_cor(cm[np.ix_(g, g)])
     old = G.knob(8, 0 if forced else 1 << 30)
     old20 = G.knob(20, 1 if space.startswith("C") else 0)
-    old28 = G.knob(28, 0 if space == "G-full-cgs" else 1)
-    old33 = G.knob(33, 0 if space == "C-full-pip" else 1)
     old36 = G.knob(36, 1 if space == "G-int8" else 0)   # the other spaces on the fp64 products
     try:
         p, _ = G.pca(c, 200)
     finally:
         G.knob(8, old)
         G.knob(20, old20)
-        G.knob(28, old28)
-        G.knob(33, old33)
         G.knob(36, old36)
     op = O.prcomp_x(c, 200)
     s = np.sign(np.sum(p * op, axis=0))
@@ -137,28 +130,6 @@ def test_pca_krylov_path_vs_lapack(gpu, forced, space):
         if i < 200 and sv[i - 1] / max(sv[i], 1e-300) < 1.0 + 1e-6:
             continue
         assert np.abs(proj(p, i) - proj(op, i)).max() < 1e-7, i
-
-
-def test_gram64_same_bits_as_split_k_gemm(gpu):
-    """The CholQR Gram matrices of the Krylov blocks by k_gram64 (knob 29) and
-    by the 64 x 64 split-K GEMM give the same bits: the whole Krylov PCA's
-    scores are identical."""
-    n0 = 2600
-    m = synth_hic(n0, SEED_BASE + 79)
-    cm = O.clean_symmetrize(m)
-    obad, _, _ = O.bad_mask(cm, 0.01)
-    g = np.flatnonzero(~obad)
-    c = O.sparse_cor(cm[np.ix_(g, g)])
-    old8 = G.knob(8, 0)
-    old29 = G.knob(29, 1)
-    try:
-        p1, _ = G.pca(c, 200)
-        G.knob(29, 0)
-        p0, _ = G.pca(c, 200)
-    finally:
-        G.knob(8, old8)
-        G.knob(29, old29)
-    assert np.array_equal(p1.view(np.uint64), p0.view(np.uint64))
 
 
 @pytest.mark.parametrize("space", ["C", "G"])
@@ -183,32 +154,6 @@ def test_pipeline_krylov_forced_end_to_end(gpu, space):
     fin = ~np.isnan(b)
     assert np.array_equal(np.isnan(a), ~fin)
     assert np.max(np.abs(a[fin] - b[fin]) / np.abs(b[fin])) < 1e-6
-
-
-@pytest.mark.parametrize("krylov", [True, False])
-def test_cor_epilogue_fused_colmean_same_bits(gpu, krylov):
-    """C's column means formed inside the correlation epilogue (knob 17, default)
-    carry k_colmean's bits: the whole pipeline's output is bit-identical to the
-    separate pass, on both PCA paths."""
-    import tadpole_amd as tp
-    m = synth_hic(2400, SEED_BASE + 79)
-    old8 = G.knob(8, 0 if krylov else 1 << 30)
-    try:
-        runs = []
-        for fused in (1, 0):
-            old = G.knob(17, fused)
-            try:
-                runs.append(tp.TADpole(m, max_pcs=200))
-            finally:
-                G.knob(17, old)
-    finally:
-        G.knob(8, old8)
-    a, b = runs
-    assert (a.n_pcs, a.optimal_n_clusters) == (b.n_pcs, b.optimal_n_clusters)
-    assert np.array_equal(np.asarray(a.scores).view(np.uint64), np.asarray(b.scores).view(np.uint64))
-    assert a.clusters.keys() == b.clusters.keys()
-    for q in a.clusters:
-        assert np.array_equal(a.clusters[q], b.clusters[q]), q
 
 
 @pytest.mark.parametrize("case", ["counts", "large_counts", "real"])
@@ -259,25 +204,6 @@ def test_cor_wide_tiles_same_bits(gpu, n):
     assert np.array_equal(np.asarray(a.scores).view(np.uint64), np.asarray(b.scores).view(np.uint64))
     for q in a.clusters:
         assert np.array_equal(a.clusters[q], b.clusters[q]), q
-
-
-def test_cheb_in_product_reduction_same_bits(gpu):
-    """The Chebyshev three-term step applied in the split-K reduction of the
-    Krylov small problem's T Y product (knob 19, default) gives the bits of the
-    stored product plus k_cheb: the same arithmetic on the same reduced value."""
-    import tadpole_amd as tp
-    m = synth_hic(4200, SEED_BASE + 81)      # n >= 4096: the block Krylov path
-    runs = []
-    for fused in (1, 0):
-        old = G.knob(19, fused)
-        try:
-            runs.append(tp.TADpole(m, max_pcs=120))
-        finally:
-            G.knob(19, old)
-    a, b = runs
-    assert a.timings_ms[16] > 0                       # the Krylov path ran
-    assert np.array_equal(np.asarray(a.scores).view(np.uint64), np.asarray(b.scores).view(np.uint64))
-    assert np.array_equal(a.dendro.height.view(np.uint64), b.dendro.height.view(np.uint64))   # PC-score bits
 
 
 @pytest.mark.parametrize("n", [4500, 10500])
@@ -565,25 +491,6 @@ def test_c5_full_golden_and_sharded_bit_identical(gpu):
             assert np.array_equal(x.scores.view(np.uint64), y.scores.view(np.uint64))
             assert np.array_equal(x.dendro.boundary, y.dendro.boundary)
             assert np.array_equal(x.dendro.height.view(np.uint64), y.dendro.height.view(np.uint64))
-
-
-def test_gemm_ts_two_stage_prefetch_same_bits(gpu):
-    """The 32-column long-K product with two register prefetch stages (knob
-    35) keeps the k order: the whole C-space Krylov PCA (10 400 bins) gives the
-    same bits."""
-    import tadpole_amd as tp
-    from tadpole_amd.synth import synth_hic_par
-    m = synth_hic_par(10400, SEED_BASE + 81)
-    old = G.knob(35, 0)
-    try:
-        a = tp.TADpole(m, max_pcs=200)
-        G.knob(35, 1)
-        b = tp.TADpole(m, max_pcs=200)
-    finally:
-        G.knob(35, old)
-    assert a.timings_ms[16] > 0          # the Krylov path ran
-    assert np.array_equal(a.scores.view(np.uint64), b.scores.view(np.uint64))
-    assert np.array_equal(a.dendro.height.view(np.uint64), b.dendro.height.view(np.uint64))
 
 
 def test_non_integer_counts_gather_x_on_demand(gpu):

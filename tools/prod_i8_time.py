@@ -1,7 +1,6 @@
 """Device time of one C3-size int8-digit product (tp_debug_prod_i8 at K = 7729,
 M = 7731, N = 64: B's digits + the product + the split-K reduce) for each
-product kernel (knob 36: 1 = k_pd_prod<1>, 2 = k_pd_prod<2>, 3 = k_pd_dma, 4 = k_pd_prod128,
-5 = k_pd_prodA)
+product kernel (knob 36: 1 = k_pd_prod<1>, 5 = k_pd_prodA)
 against the fp64 path, and whether the kernels give the same bits.
 python tools/prod_i8_time.py [K]   (env N=32: the C-space block width; KNOBS="1 5")"""
 import ctypes
@@ -23,7 +22,7 @@ rng = np.random.default_rng(1)
 A = np.asfortranarray(rng.uniform(-1, 1, size=(K, M)))
 B = np.asfortranarray(rng.standard_normal((K, N)) / np.sqrt(K))
 outs = {}
-for kn in [int(v) for v in os.environ.get("KNOBS", "1 5 1 5 4 3 2").split()]:
+for kn in [int(v) for v in os.environ.get("KNOBS", "1 5 1 5").split()]:
     old = ctypes.c_int(0); st = ctypes.c_int(0)
     L.tp_debug_knob(I(36), I(kn), ctypes.byref(old), ctypes.byref(st))
     _lib.check(st)
@@ -36,14 +35,4 @@ for kn in [int(v) for v in os.environ.get("KNOBS", "1 5 1 5 4 3 2").split()]:
     same = np.array_equal(O8.view(np.uint64), first.view(np.uint64))
     print(f"K={K} N={N} knob36={kn}: int8 product {ms[0] * 1e3:.1f} us, fp64 {ms[1] * 1e3:.1f} us, "
           f"max |int8 - fp64| {np.max(np.abs(O8 - O64)):.2e}, bits == the first: {same}", flush=True)
-L.tp_debug_knob(I(36), I(1), ctypes.byref(ctypes.c_int(0)), ctypes.byref(ctypes.c_int(0)))
-# the block digitizer: (column, slice) workgroups (knob 38 = 1) vs one per column
-for kn in (0, 1):
-    L.tp_debug_knob(I(38), I(kn), ctypes.byref(ctypes.c_int(0)), ctypes.byref(ctypes.c_int(0)))
-    O8 = np.zeros((M - 1, N), order="F"); O64 = np.zeros((M - 1, N), order="F"); ms = np.zeros(2)
-    st = ctypes.c_int(0)
-    L.tp_debug_prod_i8(A.ctypes.data_as(D), I(K), I(M), B.ctypes.data_as(D), I(N), O8.ctypes.data_as(D),
-                       O64.ctypes.data_as(D), ms.ctypes.data_as(D), ctypes.byref(st))
-    _lib.check(st)
-    same = np.array_equal(O8.view(np.uint64), next(iter(outs.values())).view(np.uint64))
-    print(f"K={K} knob38={kn}: digits + product + reduce {ms[0] * 1e3:.1f} us, bits == default: {same}", flush=True)
+L.tp_debug_knob(I(36), I(5), ctypes.byref(ctypes.c_int(0)), ctypes.byref(ctypes.c_int(0)))
