@@ -893,6 +893,13 @@ template __global__ void k_coniss_t<false, 32, true, false, 16>(SweepDev, double
 // Typical runs: ~3 merges for trees of 1-3 PCs, 5-7 for wider trees, against
 // one merge per ~2 800-cycle step of coniss_tree2.  The overflow case (more
 // than CB_CAP positions <= T, or ties at g) takes one merge, the exact argmin.
+// Storage modes M: 0 costs and int links / right ends in LDS (16 bytes a bin,
+// to ~9.8k bins); 1 costs in LDS, 16-bit links only (10 bytes a bin, rn
+// derived as in coniss_tree2's LU = 2, to 12.3k bins); 2 costs in the tree's
+// slice of cost0 (global, L2/MALL), 16-bit links only in LDS (2 bytes a bin,
+// the C5 arms).  In mode 2 the run's waves read the cost blocks they refresh
+// in A2 (with the rows, before the run is known) and apply the run's changes
+// in registers, so no global read follows A3's cost stores.
 constexpr int CB_W = 8;      // waves a tree = most candidates a batch
 constexpr int CB_CAP = 16;   // positions <= T ranked a batch (16 x 16 lane pairs)
 constexpr int CB_FMAX = 16;  // flagged blocks a batch (two a wave)
@@ -921,8 +928,9 @@ __device__ __forceinline__ bool key_lt(double c1, int p1, double c2, int p2) {
     return c1 < c2 || (c1 == c2 && p1 < p2);
 }
 
-template <int NS, int BS, bool STAMPS>
+template <int NS, int BS, int M, bool STAMPS>
 __device__ __forceinline__ void coniss_tree_b(const SweepDev &sd, double *cost0, double *lds, CbShared &sh) {
+    constexpr bool GL = M == 2, L16 = M >= 1;
     const int n = sd.n;
     const int ti = blockIdx.x;
     const int i = sd.tree0 + ti + 1;
@@ -943,10 +951,19 @@ __device__ __forceinline__ void coniss_tree_b(const SweepDev &sd, double *cost0,
         st_t0 = _t;                                                       \
     }
     const size_t cst = coniss_cost_stride(n), lst = coniss_link_stride(n);
-    double *cost = lds;
-    int *link = (int *)(cost + cst);
-    int *rn = link + lst;
-    double *bmin = (double *)(rn + lst);   // 8-byte aligned: 8 cst + 8 lst bytes before it
+    double *cost = GL ? cost0 + (size_t)ti * cst : lds;
+    LinkArr<L16> link;
+    typename RnOf<L16 ? 2 : 0>::T rn;
+    double *bmin;
+    if constexpr (L16) {
+        link.p = (unsigned short *)(GL ? lds : lds + cst);
+        rn.link = link;
+        bmin = (double *)((char *)link.p + ((lst * 2 + 7) & ~(size_t)7));
+    } else {
+        link.p = (int *)(cost + cst);
+        rn.p = link.p + lst;
+        bmin = (double *)(rn.p + lst);   // 8-byte aligned: 8 cst + 8 lst bytes before it
+    }
     const int DC = nbk * 64, DL = n;
     constexpr bool P4 = NS == 4;
     double *S = sd.sums + sums_off(n, sd.tree0, i);
@@ -985,18 +1002,19 @@ __device__ __forceinline__ void coniss_tree_b(const SweepDev &sd, double *cost0,
     for (int bk = w; bk < nbk; bk += CB_W) {
         const int p = bk * 64 + lane;
         const double cp = c0[p];
-        cost[p] = cp;
+        if (!GL) cost[p] = cp;   // (mode 2: the costs stay where k_seed wrote them)
         if (p < n) {
-            link[p] = p;
-            rn[p] = p + 1 < n ? p + 1 : -1;
+            link.set(p, p);
+            rn.set(p, p + 1 < n ? p + 1 : -1);
         }
         const double m = wave_min(cp);
         if (lane == 0) bmin[bk] = m;
     }
     if (w == 0) {
         cost[DC + lane] = QNAN;
-        link[DL + lane] = -1;
-        rn[DL + lane] = -1;
+        link.set(DL + lane, -1);
+        rn.set(DL + lane, -1);
+        if (GL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
 
@@ -1008,6 +1026,7 @@ __device__ __forceinline__ void coniss_tree_b(const SweepDev &sd, double *cost0,
     int a = 0, ea = 0, b = 0, eb = 0, ls = -1, r = -1, er = -1;
     double sm[NS];
     double key = 0.0, cl = 0.0, cr = 0.0;
+    double pba = 0.0, pbb = 0.0, pbl = 0.0;   // mode 2: the cost blocks of a, b and ls before the batch
     int s = 0;
     while (s < n - 1) {
         // ---- A1 (every wave): g and T = g + gap from the block minima (every
@@ -1162,22 +1181,29 @@ __device__ __forceinline__ void coniss_tree_b(const SweepDev &sd, double *cost0,
             a = __builtin_amdgcn_readfirstlane(sh.spos[w]);
             key = sh.key[w];
             TP_DASSERT(a >= 0 && a < n - 1);
-            int lsv = link[a > 0 ? a - 1 : DL];
-            ea = link[a];
-            eb = rn[a];
+            int lsv = link.get(a > 0 ? a - 1 : DL);
+            ea = link.get(a);
+            eb = rn.get(a);
             pin3(lsv, ea, eb);
             ea = __builtin_amdgcn_readfirstlane(ea);
             eb = __builtin_amdgcn_readfirstlane(eb);
             b = ea + 1;
             ls = a > 0 ? __builtin_amdgcn_readfirstlane(lsv) : -1;
             r = eb + 1 < n ? eb + 1 : -1;
-            er = r >= 0 ? __builtin_amdgcn_readfirstlane(rn[b]) : -1;
+            er = r >= 0 ? __builtin_amdgcn_readfirstlane(rn.get(b)) : -1;
             const int ac = rowc(a, ea == a);
             double sa[NS], sb[NS], sl[NS], sr[NS];
             load_row(sa, ac);
             load_row(sb, rowc(b, eb == b));
             load_row(sl, ls >= 0 ? rowc(ls, ls == a - 1) : ac);
             load_row(sr, r >= 0 ? rowc(r, er == r) : ac);
+            if (GL) {
+                // the blocks A4 refreshes, issued after the rows so the rows'
+                // waits leave them in flight (used only after A3)
+                pba = cost[(a >> 6) * 64 + lane];
+                pbb = cost[(b >> 6) * 64 + lane];
+                pbl = cost[((ls >= 0 ? ls : a) >> 6) * 64 + lane];
+            }
             if (lane == 0) {
                 sh.win[w] = make_int4(ls >= 0 ? ls : a, r >= 0 ? er : eb, ls, r);
                 sh.w2[w] = make_int4(b, eb, er, 0);
@@ -1231,12 +1257,12 @@ __device__ __forceinline__ void coniss_tree_b(const SweepDev &sd, double *cost0,
                 sh.hgt[lane] = myh;
                 cost[x2.x] = QNAN;
                 cost[aj] = crj;   // QNAN without a right neighbour
-                link[aj] = x2.y;
-                link[x2.y] = aj;
-                rn[aj] = x2.z;
+                link.set(aj, x2.y);
+                link.set(x2.y, aj);
+                rn.set(aj, x2.z);
                 if (wj.z >= 0) {
                     cost[wj.z] = clj;
-                    rn[wj.z] = x2.y;
+                    rn.set(wj.z, x2.y);
                 }
             }
             if (lane == 0) sh.cnt = cnt;
@@ -1307,7 +1333,40 @@ __device__ __forceinline__ void coniss_tree_b(const SweepDev &sd, double *cost0,
             }
             TP_BSTAMP(6);
             const int ba = a >> 6, bb = b >> 6, bl = ls >= 0 ? (ls >> 6) : ba;
-            double ma = cost[ba * 64 + lane], mb = cost[bb * 64 + lane], ml = cost[bl * 64 + lane], mx = QNAN;
+            double ma, mb, ml, mx = QNAN;
+            if constexpr (GL) {
+                // the blocks read in A2 with the run's changes (A3's stores):
+                // merge q sets b_q's cost to NaN, a_q's to cr_q, ls_q's to cl_q
+                int qb = -1, qa = -1, ql = -1;
+                double qcl = 0.0, qcr = 0.0;
+                if (lane < cnt) {
+                    qb = sh.w2[lane].x;
+                    qa = sh.ka[lane];
+                    ql = sh.win[lane].z;
+                    qcl = sh.cl[lane];
+                    qcr = sh.cr[lane];
+                }
+                ma = pba;
+                mb = pbb;
+                ml = pbl;
+                const int Pa = ba * 64 + lane, Pb = bb * 64 + lane, Pl = bl * 64 + lane;
+                for (int q = 0; q < cnt; ++q) {
+                    const int xb = __builtin_amdgcn_readlane(qb, q), xa = __builtin_amdgcn_readlane(qa, q),
+                              xl = __builtin_amdgcn_readlane(ql, q);
+                    const int kb = xb >> 6, ka_ = xa >> 6, kl = xl >> 6;   // xl = -1: no block
+                    const bool hit = kb == ba || kb == bb || kb == bl || ka_ == ba || ka_ == bb || ka_ == bl ||
+                                     kl == ba || kl == bb || kl == bl;
+                    if (!hit) continue;
+                    const double vl = readlane_d(qcl, q), vr = readlane_d(qcr, q);
+                    ma = Pa == xb ? QNAN : (Pa == xa ? vr : (Pa == xl ? vl : ma));
+                    mb = Pb == xb ? QNAN : (Pb == xa ? vr : (Pb == xl ? vl : mb));
+                    ml = Pl == xb ? QNAN : (Pl == xa ? vr : (Pl == xl ? vl : ml));
+                }
+            } else {
+                ma = cost[ba * 64 + lane];
+                mb = cost[bb * 64 + lane];
+                ml = cost[bl * 64 + lane];
+            }
             wave_min4(ma, mb, ml, mx);
             if (lane == 0) {
                 bmin[ba] = ma;
@@ -1352,25 +1411,30 @@ __device__ __forceinline__ void coniss_tree_b(const SweepDev &sd, double *cost0,
 #undef TP_BSTAMP
 }
 
-// trees of up to 4 column slots (k <= 256), costs and links in LDS
-template <int BS, bool STAMPS = false>
+// trees of up to 4 column slots (k <= 256); M: the storage mode above
+template <int BS, int M, bool STAMPS = false>
 __global__ void __launch_bounds__(64 * CB_W) k_coniss_b(SweepDev sd, double *cost0) {
     extern __shared__ double lds[];
     __shared__ CbShared sh;
     const int i = sd.tree0 + blockIdx.x + 1;
     switch ((i + 63) / 64) {
-        case 1: coniss_tree_b<1, BS, STAMPS>(sd, cost0, lds, sh); break;
-        case 2: coniss_tree_b<2, BS, STAMPS>(sd, cost0, lds, sh); break;
-        case 3: coniss_tree_b<3, BS, STAMPS>(sd, cost0, lds, sh); break;
-        default: coniss_tree_b<4, BS, STAMPS>(sd, cost0, lds, sh); break;
+        case 1: coniss_tree_b<1, BS, M, STAMPS>(sd, cost0, lds, sh); break;
+        case 2: coniss_tree_b<2, BS, M, STAMPS>(sd, cost0, lds, sh); break;
+        case 3: coniss_tree_b<3, BS, M, STAMPS>(sd, cost0, lds, sh); break;
+        default: coniss_tree_b<4, BS, M, STAMPS>(sd, cost0, lds, sh); break;
     }
 }
-template __global__ void k_coniss_b<1>(SweepDev, double *);
-template __global__ void k_coniss_b<2>(SweepDev, double *);
-template __global__ void k_coniss_b<3>(SweepDev, double *);
-template __global__ void k_coniss_b<1, true>(SweepDev, double *);
-template __global__ void k_coniss_b<2, true>(SweepDev, double *);
-template __global__ void k_coniss_b<3, true>(SweepDev, double *);
+template __global__ void k_coniss_b<1, 0>(SweepDev, double *);
+template __global__ void k_coniss_b<2, 0>(SweepDev, double *);
+template __global__ void k_coniss_b<3, 0>(SweepDev, double *);
+template __global__ void k_coniss_b<3, 1>(SweepDev, double *);
+template __global__ void k_coniss_b<6, 2>(SweepDev, double *);
+template __global__ void k_coniss_b<11, 2>(SweepDev, double *);
+template __global__ void k_coniss_b<1, 0, true>(SweepDev, double *);
+template __global__ void k_coniss_b<2, 0, true>(SweepDev, double *);
+template __global__ void k_coniss_b<3, 0, true>(SweepDev, double *);
+template __global__ void k_coniss_b<3, 1, true>(SweepDev, double *);
+template __global__ void k_coniss_b<6, 2, true>(SweepDev, double *);
 
 // ------------------------------------------------------------ CH over cuts
 // canonical segment statistics of rows s..e, by one wave (see tpo_seg_ss)
@@ -1933,8 +1997,8 @@ static void launch_coniss_bs(const SweepDev &sd, double *cost0, size_t lds, hipS
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL((k_coniss_t<STAMPS, BS, GLB, LU>), dim3(sd.ntrees), dim3(128), lds, s, sd, cost0);
 }
-// knob 52: the batched CONISS kernel (k_coniss_b) where it applies (costs and
-// links in LDS, k <= 256) -- 2 (default): also for lean sweeps (C4, 8 streams:
+// knob 52: the batched CONISS kernel (k_coniss_b) where it applies (k <= 256,
+// up to ~38k bins) -- 2 (default): also for lean sweeps (C4, 8 streams:
 // 0.265 -> 0.229 s), 1: not for them, 0: never (the two-wave k_coniss_t)
 // lean sweeps (another pipeline in flight on the device) of matrices that fit
 // LDS, from this many bins (knob 48; 0: never): costs global and only the
@@ -1990,22 +2054,36 @@ static void run_coniss(const SweepDev &sd_in, hipStream_t s, bool stamped, Ctx *
     const size_t lds = in_lds2 ? coniss_lds2_bytes(sd.n)
                                : (in_lds ? coniss_lds_bytes(sd.n) : (lu ? lu_bytes : (lu2 ? lu_bytes / 2 : kConissGlbLds)));
     if (!stamped && prof) kprof_begin(*prof, K_CONISS);
-    // the batched kernel (round 6): costs, links and the block minima in LDS,
-    // trees of up to 4 column slots
-    const size_t lds_b = coniss_lds_bytes(sd.n) + (size_t)nbk * 8;
-    if (t_knob.coniss_batch && sd.tree0 + sd.ntrees <= 256 && bs <= 3 && !lean_small &&
-        lds_b + sizeof(CbShared) <= 160 * 1024 - 64 && !(sd.lds_lean && t_knob.coniss_batch < 2)) {
+    // the batched kernel (round 6), trees of up to 4 column slots: mode 0
+    // (costs, int links and the block minima in LDS) where it fits, else mode 1
+    // (16-bit links only) up to 3 block-minimum slots, else mode 2 (costs global)
+    const size_t l16 = (coniss_link_stride(sd.n) * 2 + 7) & ~(size_t)7;
+    const size_t cap_b = 160 * 1024 - 64 - sizeof(CbShared);
+    const size_t lds_b0 = coniss_lds_bytes(sd.n) + (size_t)nbk * 8;
+    const size_t lds_b1 = coniss_cost_stride(sd.n) * 8 + l16 + (size_t)nbk * 8;
+    const size_t lds_b2 = l16 + (size_t)nbk * 8;
+    const int mode = (bs <= 3 && lds_b0 <= cap_b) ? 0 : (bs <= 3 && lds_b1 <= cap_b) ? 1
+                     : (bs <= 11 && sd.n + 64 < 0xFFFF && lds_b2 <= cap_b) ? 2 : -1;
+    if (t_knob.coniss_batch && sd.tree0 + sd.ntrees <= 256 && mode >= 0 && !lean_small &&
+        !(sd.lds_lean && t_knob.coniss_batch < 2)) {
+        const size_t lds_b = mode == 0 ? lds_b0 : (mode == 1 ? lds_b1 : lds_b2);
         auto go = [&](auto kern) {
             TP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_b));
             hipLaunchKernelGGL(kern, dim3(sd.ntrees), dim3(64 * CB_W), lds_b, s, sd, cost0);
         };
         if (stamped) {
-            if (bs == 1) go(k_coniss_b<1, true>);
-            else if (bs == 2) go(k_coniss_b<2, true>);
-            else go(k_coniss_b<3, true>);
-        } else if (bs == 1) go(k_coniss_b<1>);
-        else if (bs == 2) go(k_coniss_b<2>);
-        else go(k_coniss_b<3>);
+            if (mode == 2 && bs <= 6) go(k_coniss_b<6, 2, true>);
+            else if (mode == 2) fail(TP_ERR_UNSUPPORTED, "stamped batched CONISS: at most 24 576 bins in mode 2");
+            else if (mode == 1) go(k_coniss_b<3, 1, true>);
+            else if (bs == 1) go(k_coniss_b<1, 0, true>);
+            else if (bs == 2) go(k_coniss_b<2, 0, true>);
+            else go(k_coniss_b<3, 0, true>);
+        } else if (mode == 2 && bs <= 6) go(k_coniss_b<6, 2>);
+        else if (mode == 2) go(k_coniss_b<11, 2>);
+        else if (mode == 1) go(k_coniss_b<3, 1>);
+        else if (bs == 1) go(k_coniss_b<1, 0>);
+        else if (bs == 2) go(k_coniss_b<2, 0>);
+        else go(k_coniss_b<3, 0>);
         if (!stamped && prof) kprof_end(*prof, K_CONISS);
         TP_HIP(hipGetLastError());
         return;

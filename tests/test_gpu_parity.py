@@ -908,13 +908,16 @@ def _upload_checks(gpu, h, d, n, blk, packed, st, s, rng):
 
 
 @pytest.mark.parametrize("n,k,seed", [(150, 5, 31), (1999, 70, 32), (4100, 200, 33), (7729, 200, 34),
-                                      (9500, 24, 35), (3000, 256, 36)])
+                                      (9500, 24, 35), (3000, 256, 36), (11000, 12, 37), (24300, 66, 38),
+                                      (40000, 3, 39)])
 def test_coniss_batched_same_bits(gpu, n, k, seed):
     """The batched CONISS (k_coniss_b, knob 52: candidate runs taken several
     merges at a time by 8 waves a tree) gives every tree's merge order, costs,
     heights, broken-stick count and CH scores of the two-wave kernel bit for
     bit (the run rule of tools/coniss_batch_model.py), on TAD-like scores with
-    1..256 PCs (1..4 column slots, 1..3 block-minimum slots)."""
+    1..256 PCs (1..4 column slots, 1..3 block-minimum slots) -- storage mode 0
+    (everything in LDS), 11 000 bins mode 1 (16-bit links), 24 300 and 40 000
+    bins mode 2 (costs in global memory, 6 and 11 block-minimum slots)."""
     p = _structured_pcs(n, k, seed)
     old = G.knob(52, 0)
     try:

@@ -12,10 +12,10 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
 import gpu_helpers as G  # noqa: E402
 import tadpole_amd as tp  # noqa: E402
 from tadpole_amd import _lib  # noqa: E402
-from tadpole_amd.synth import synth_hic  # noqa: E402
+from tadpole_amd.synth import synth_hic, synth_hic_par  # noqa: E402
 
 n0 = int(sys.argv[1]) if len(sys.argv) > 1 else 7808
-res = tp.TADpole(synth_hic(n0, 20261018))
+res = tp.TADpole(synth_hic(n0, 20261018) if n0 < 8000 else synth_hic_par(n0, 20261018))
 L = _lib.load()
 n, k = int(res.timings_ms[14]), int(res.timings_ms[15])
 P = np.zeros((n, k), order="F")
