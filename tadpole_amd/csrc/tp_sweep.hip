@@ -841,11 +841,13 @@ template __global__ void k_coniss_t<false, 11, true, true>(SweepDev, double *);
 template __global__ void k_coniss_t<false, 11, true>(SweepDev, double *);
 template __global__ void k_coniss_t<false, 16, true>(SweepDev, double *);
 template __global__ void k_coniss_t<false, 32, true>(SweepDev, double *);
+#ifdef TP_STAMPS_BUILD   // stamped (diagnostic) kernels: make STAMPS=1
 template __global__ void k_coniss_t<true, 1, false>(SweepDev, double *);
 template __global__ void k_coniss_t<true, 2, false>(SweepDev, double *);
 template __global__ void k_coniss_t<true, 3, false>(SweepDev, double *);
 template __global__ void k_coniss_t<true, 6, true, true>(SweepDev, double *);
 template __global__ void k_coniss_t<true, 16, true>(SweepDev, double *);
+#endif
 // k in 257..512 (R accepts any max_pcs, R/TADpole.R:344,452): trees of up to 8 slots
 template __global__ void k_coniss_t<false, 1, false, false, 8>(SweepDev, double *);
 template __global__ void k_coniss_t<false, 2, false, false, 8>(SweepDev, double *);
@@ -1430,11 +1432,13 @@ template __global__ void k_coniss_b<3, 0>(SweepDev, double *);
 template __global__ void k_coniss_b<3, 1>(SweepDev, double *);
 template __global__ void k_coniss_b<6, 2>(SweepDev, double *);
 template __global__ void k_coniss_b<11, 2>(SweepDev, double *);
+#ifdef TP_STAMPS_BUILD
 template __global__ void k_coniss_b<1, 0, true>(SweepDev, double *);
 template __global__ void k_coniss_b<2, 0, true>(SweepDev, double *);
 template __global__ void k_coniss_b<3, 0, true>(SweepDev, double *);
 template __global__ void k_coniss_b<3, 1, true>(SweepDev, double *);
 template __global__ void k_coniss_b<6, 2, true>(SweepDev, double *);
+#endif
 
 // ------------------------------------------------------------ CH over cuts
 // canonical segment statistics of rows s..e, by one wave (see tpo_seg_ss)
@@ -2072,12 +2076,16 @@ static void run_coniss(const SweepDev &sd_in, hipStream_t s, bool stamped, Ctx *
             hipLaunchKernelGGL(kern, dim3(sd.ntrees), dim3(64 * CB_W), lds_b, s, sd, cost0);
         };
         if (stamped) {
+#ifdef TP_STAMPS_BUILD
             if (mode == 2 && bs <= 6) go(k_coniss_b<6, 2, true>);
             else if (mode == 2) fail(TP_ERR_UNSUPPORTED, "stamped batched CONISS: at most 24 576 bins in mode 2");
             else if (mode == 1) go(k_coniss_b<3, 1, true>);
             else if (bs == 1) go(k_coniss_b<1, 0, true>);
             else if (bs == 2) go(k_coniss_b<2, 0, true>);
             else go(k_coniss_b<3, 0, true>);
+#else
+            fail(TP_ERR_UNSUPPORTED, "stamped CONISS kernels are in the diagnostic build only (make STAMPS=1)");
+#endif
         } else if (mode == 2 && bs <= 6) go(k_coniss_b<6, 2>);
         else if (mode == 2) go(k_coniss_b<11, 2>);
         else if (mode == 1) go(k_coniss_b<3, 1>);
@@ -2092,12 +2100,16 @@ static void run_coniss(const SweepDev &sd_in, hipStream_t s, bool stamped, Ctx *
     // per-slot loop of the merge chain -- the untouched minimum, the argmin
     // ballots, the block-minimum updates -- runs over all of them)
     if (stamped) {
+#ifdef TP_STAMPS_BUILD
         if (lu && bs <= 6) launch_coniss_bs<true, 6, true, true>(sd, cost0, lds, s);
         else if (!in_lds && bs <= 16) launch_coniss_bs<true, 16, true>(sd, cost0, lds, s);
         else if (!in_lds) fail(TP_ERR_UNSUPPORTED, "stamped CONISS: at most 65 536 bins");
         else if (bs == 1) launch_coniss_bs<true, 1, false>(sd, cost0, lds, s);
         else if (bs == 2) launch_coniss_bs<true, 2, false>(sd, cost0, lds, s);
         else launch_coniss_bs<true, 3, false>(sd, cost0, lds, s);
+#else
+        fail(TP_ERR_UNSUPPORTED, "stamped CONISS kernels are in the diagnostic build only (make STAMPS=1)");
+#endif
     } else {
         if (in_lds2 && bs == 1) launch_coniss_bs<false, 1, false, 2>(sd, cost0, lds, s);
         else if (in_lds2 && bs == 2) launch_coniss_bs<false, 2, false, 2>(sd, cost0, lds, s);

@@ -1,6 +1,7 @@
 """Per-phase cycles of the batched CONISS (k_coniss_b, STAMPS build of the same
 source) on the PC scores of a synthetic matrix: python tools/coniss_b_stamps.py
-[N0]"""
+[N0].  Needs the diagnostic build (`make -C tadpole_amd/csrc STAMPS=1`: the
+product build leaves the stamped kernels out)."""
 import ctypes
 import os
 import sys
