@@ -1029,6 +1029,31 @@ __device__ __forceinline__ void coniss_tree_b(const SweepDev &sd, double *cost0,
     double sm[NS];
     double key = 0.0, cl = 0.0, cr = 0.0;
     double pba = 0.0, pbb = 0.0, pbl = 0.0;   // mode 2: the cost blocks of a, b and ls before the batch
+    // rank the candidate set (C entries) by (cost, position) and write the
+    // first CB_W to the slots: lane l compares candidate i = 4 p + (l >> 4)
+    // with j = l & 15 (in-order LDS: reads the set after this wave's writes)
+    auto rank_set = [&](int C) {
+        const int j = lane & 15;
+        const double kj = sh.ccost[j];
+        const int pj = sh.cpos[j];
+        double ki[4];
+        int pi[4];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            ki[p] = sh.ccost[4 * p + (lane >> 4)];
+            pi[p] = sh.cpos[4 * p + (lane >> 4)];
+        }
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int ii = 4 * p + (lane >> 4);
+            const unsigned long long mm = __ballot((j < C) & key_lt(kj, pj, ki[p], pi[p]));
+            const int rank = __popc((unsigned)(mm >> (16 * (lane >> 4))) & 0xFFFFu);
+            if ((j == 0) & (ii < C) & (rank < CB_W)) {
+                sh.key[rank] = ki[p];
+                sh.spos[rank] = pi[p];
+            }
+        }
+    };
     int s = 0;
     while (s < n - 1) {
         // ---- A1 (every wave): g and T = g + gap from the block minima (every
@@ -1114,44 +1139,25 @@ __device__ __forceinline__ void coniss_tree_b(const SweepDev &sd, double *cost0,
             }
         }
         TP_BSTAMP(10);
-        // ---- A1b (wave 0): gather the segments, rank, the first CB_W into the slots
-        if (w == 0) {
+        // ---- A1b (wave 0, after a rescan): gather the segments, rank, the
+        // first CB_W into the slots.  Without a rescan the slots were filled
+        // during the previous batch's A4 by wave CB_W - 1 (rank_set below), so
+        // the batch goes straight to A2
+        if (rescan && w == 0) {
             int Kc;
             if (!single) {
-                if (rescan) {
-                    // the segments compacted into the set: lane l holds entry l & 7 of wave l >> 3
-                    const bool valid = (lane & (CB_SEG - 1)) < sh.segn[lane >> 3];
-                    const double cv = sh.sgc[lane];
-                    const int cp = sh.sgp[lane];
-                    const unsigned long long mv = __ballot(valid);
-                    const int idx = mbcnt64(mv);
-                    if (valid) {
-                        sh.ccost[idx] = cv;
-                        sh.cpos[idx] = cp;
-                    }
-                    if (lane == 0) sh.sT = Tu;
+                // the segments compacted into the set: lane l holds entry l & 7 of wave l >> 3
+                const bool valid = (lane & (CB_SEG - 1)) < sh.segn[lane >> 3];
+                const double cv = sh.sgc[lane];
+                const int cp = sh.sgp[lane];
+                const unsigned long long mv = __ballot(valid);
+                const int idx = mbcnt64(mv);
+                if (valid) {
+                    sh.ccost[idx] = cv;
+                    sh.cpos[idx] = cp;
                 }
-                // ranks: lane l compares candidate i = 4 p + (l >> 4) with j = l & 15
-                const int j = lane & 15;
-                const double kj = sh.ccost[j];
-                const int pj = sh.cpos[j];
-                double ki[4];
-                int pi[4];
-#pragma unroll
-                for (int p = 0; p < 4; ++p) {
-                    ki[p] = sh.ccost[4 * p + (lane >> 4)];
-                    pi[p] = sh.cpos[4 * p + (lane >> 4)];
-                }
-#pragma unroll
-                for (int p = 0; p < 4; ++p) {
-                    const int ii = 4 * p + (lane >> 4);
-                    const unsigned long long mm = __ballot((j < C) & key_lt(kj, pj, ki[p], pi[p]));
-                    const int rank = __popc((unsigned)(mm >> (16 * (lane >> 4))) & 0xFFFFu);
-                    if ((j == 0) & (ii < C) & (rank < CB_W)) {
-                        sh.key[rank] = ki[p];
-                        sh.spos[rank] = pi[p];
-                    }
-                }
+                if (lane == 0) sh.sT = Tu;
+                rank_set(C);
                 Kc = C < CB_W ? C : CB_W;
             } else {
                 // too many positions tie at g: the exact argmin, one merge
@@ -1175,7 +1181,7 @@ __device__ __forceinline__ void coniss_tree_b(const SweepDev &sd, double *cost0,
             if (lane == 0) sh.kc = Kc;
         }
         TP_BSTAMP(0);
-        lds_barrier();   // B1
+        if (rescan) lds_barrier();   // B1
         TP_BSTAMP(1);
         // ---- A2 (wave j < kc): candidate j's window, rows, merged sums, new costs
         const int kc = __builtin_amdgcn_readfirstlane(sh.kc);
@@ -1376,6 +1382,16 @@ __device__ __forceinline__ void coniss_tree_b(const SweepDev &sd, double *cost0,
                 bmin[bl] = ml;
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        if (w == CB_W - 1) {
+            // the next batch's slots from the kept set (every cost of the run is
+            // in place: A3 updated the set before B3); a set that ran low is
+            // rescanned and ranked in the next A1 / A1b instead
+            const int Cn = __builtin_amdgcn_readfirstlane(sh.sN);
+            if (Cn >= CB_NMIN) {
+                rank_set(Cn);
+                if (lane == 0) sh.kc = Cn < CB_W ? Cn : CB_W;
+            }
         }
         s += cnt;
         TP_BSTAMP(8);
