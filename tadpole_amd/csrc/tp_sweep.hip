@@ -907,6 +907,12 @@ constexpr int CB_CAP = 16;   // positions <= T ranked a batch (16 x 16 lane pair
 constexpr int CB_FMAX = 16;  // flagged blocks a batch (two a wave)
 constexpr int CB_SEG = 8;    // positions <= T a wave may contribute
 constexpr int CB_NMIN = 3;   // rescan when the maintained candidate set holds fewer
+#ifndef TP_CB_LO             // the gap adapts so a scan finds about LO..HI positions <= T
+#define TP_CB_LO 10          // (6..10: C3 7.0 ms; 8..12: 6.8; 10..14: 6.67; 12..15: 6.66)
+#endif
+#ifndef TP_CB_HI
+#define TP_CB_HI 14
+#endif
 static_assert(CB_W * CB_SEG == 64, "one segment entry a lane");
 struct CbShared {
     double sgc[CB_W * CB_SEG];   // the waves' segments: positions <= T and their costs
@@ -1126,7 +1132,7 @@ __device__ __forceinline__ void coniss_tree_b(const SweepDev &sd, double *cost0,
                 if (tot <= CB_CAP && mx <= CB_SEG && tot >= 1) {
                     C = tot;
                     Tu = T;
-                    if (tries <= 5) gap *= C < 6 ? 1.3 : (C > 10 ? 0.8 : 1.0);   // next batch: ~6..10 positions <= T
+                    if (tries <= 5) gap *= C < TP_CB_LO ? 1.3 : (C > TP_CB_HI ? 0.8 : 1.0);   // next scan: ~LO..HI positions <= T
                     break;
                 }
                 if (tries >= 6) {
@@ -1390,7 +1396,8 @@ __device__ __forceinline__ void coniss_tree_b(const SweepDev &sd, double *cost0,
             const int Cn = __builtin_amdgcn_readfirstlane(sh.sN);
             if (Cn >= CB_NMIN) {
                 rank_set(Cn);
-                if (lane == 0) sh.kc = Cn < CB_W ? Cn : CB_W;
+                const int K8 = Cn < CB_W ? Cn : CB_W;
+                if (lane == 0) sh.kc = K8;
             }
         }
         s += cnt;
