@@ -1060,6 +1060,52 @@ __device__ __forceinline__ void coniss_tree_b(const SweepDev &sd, double *cost0,
             }
         }
     };
+    // the candidate set after a run of cnt merges: drop the changed positions
+    // (a, b and ls of every merge), add the new costs <= T -- still every
+    // position with cost <= T (costs change only there).  Lane pairs (entry
+    // e = 8 h + (l >> 3), merge q = l & 7): does merge q change entry e's
+    // position?  Run by the ranking wave during A4 (the slots' windows and new
+    // costs stay in LDS until the next A2).
+    auto update_set = [&](int C, int cnt, bool single) {
+        if (single) {
+            if (lane == 0) sh.sN = -1;
+            return;
+        }
+        const int sj = lane & 7;
+        const int4 wj = sh.win[sj], x2 = sh.w2[sj];
+        const int aj = sh.ka[sj];
+        const double clj = sh.cl[sj], crj = sh.cr[sj];
+        const double sT = sh.sT;
+        const double ce = sh.ccost[lane & (CB_CAP - 1)];
+        const int pe = sh.cpos[lane & (CB_CAP - 1)];
+        const int pe0 = sh.cpos[lane >> 3], pe1 = sh.cpos[8 + (lane >> 3)];
+        const bool onq = sj < cnt;
+        const unsigned long long r0 = __ballot(onq && (pe0 == aj || pe0 == x2.x || pe0 == wj.z));
+        const unsigned long long r1 = __ballot(onq && (pe1 == aj || pe1 == x2.x || pe1 == wj.z));
+        const int le = lane & (CB_CAP - 1);
+        const bool rm = ((le < 8 ? r0 : r1) >> (8 * (le & 7))) & 0xFFull;
+        const bool keep = lane < C && !rm;
+        const bool addl = lane < cnt && wj.z >= 0 && clj <= sT;
+        const bool addr = lane < cnt && wj.w >= 0 && crj <= sT;
+        const unsigned long long mk = __ballot(keep), ml = __ballot(addl), mr = __ballot(addr);
+        const int nk = __popcll(mk), nl = __popcll(ml), nr = __popcll(mr);
+        if (nk + nl + nr <= CB_CAP) {
+            // (every lane read the old set above: in-order LDS, the writes come after)
+            if (keep) {
+                sh.ccost[mbcnt64(mk)] = ce;
+                sh.cpos[mbcnt64(mk)] = pe;
+            }
+            if (addl) {
+                sh.ccost[nk + mbcnt64(ml)] = clj;
+                sh.cpos[nk + mbcnt64(ml)] = wj.z;
+            }
+            if (addr) {
+                sh.ccost[nk + nl + mbcnt64(mr)] = crj;
+                sh.cpos[nk + nl + mbcnt64(mr)] = aj;
+            }
+        }
+        if (lane == 0) sh.sN = nk + nl + nr <= CB_CAP ? nk + nl + nr : -1;
+    };
     int s = 0;
     while (s < n - 1) {
         // ---- A1 (every wave): g and T = g + gap from the block minima (every
@@ -1281,45 +1327,6 @@ __device__ __forceinline__ void coniss_tree_b(const SweepDev &sd, double *cost0,
             }
             if (lane == 0) sh.cnt = cnt;
             if (STAMPS) st_acc[13] += cnt;
-            // the candidate set after the run: drop the changed positions (a, b
-            // and ls of every merge), add the new costs <= T -- still every
-            // position with cost <= T (costs change only there)
-            if (single) {
-                if (lane == 0) sh.sN = -1;
-            } else {
-                const double sT = sh.sT;
-                const double ce = sh.ccost[lane & (CB_CAP - 1)];
-                const int pe = sh.cpos[lane & (CB_CAP - 1)];
-                // lane pairs (entry e = 8 h + (l >> 3), merge q = l & 7 -- this
-                // lane's slot sj): does merge q change entry e's position?
-                const int pe0 = sh.cpos[lane >> 3], pe1 = sh.cpos[8 + (lane >> 3)];
-                const bool onq = sj < cnt;
-                const unsigned long long r0 = __ballot(onq && (pe0 == aj || pe0 == x2.x || pe0 == wj.z));
-                const unsigned long long r1 = __ballot(onq && (pe1 == aj || pe1 == x2.x || pe1 == wj.z));
-                const int le = lane & (CB_CAP - 1);
-                const bool rm = ((le < 8 ? r0 : r1) >> (8 * (le & 7))) & 0xFFull;
-                const bool keep = lane < C && !rm;
-                const bool addl = lane < cnt && wj.z >= 0 && clj <= sT;
-                const bool addr = lane < cnt && wj.w >= 0 && crj <= sT;
-                const unsigned long long mk = __ballot(keep), ml = __ballot(addl), mr = __ballot(addr);
-                const int nk = __popcll(mk), nl = __popcll(ml), nr = __popcll(mr);
-                if (nk + nl + nr <= CB_CAP) {
-                    // (every lane read the old set above: in-order LDS, the writes come after)
-                    if (keep) {
-                        sh.ccost[mbcnt64(mk)] = ce;
-                        sh.cpos[mbcnt64(mk)] = pe;
-                    }
-                    if (addl) {
-                        sh.ccost[nk + mbcnt64(ml)] = clj;
-                        sh.cpos[nk + mbcnt64(ml)] = wj.z;
-                    }
-                    if (addr) {
-                        sh.ccost[nk + nl + mbcnt64(mr)] = crj;
-                        sh.cpos[nk + nl + mbcnt64(mr)] = aj;
-                    }
-                }
-                if (lane == 0) sh.sN = nk + nl + nr <= CB_CAP ? nk + nl + nr : -1;
-            }
         }
         TP_BSTAMP(4);
         lds_barrier();   // B3
@@ -1390,10 +1397,10 @@ __device__ __forceinline__ void coniss_tree_b(const SweepDev &sd, double *cost0,
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         if (w == CB_W - 1) {
-            // the next batch's slots from the kept set (every cost of the run is
-            // in place: A3 updated the set before B3); a set that ran low is
-            // rescanned and ranked in the next A1 / A1b instead
-            const int Cn = __builtin_amdgcn_readfirstlane(sh.sN);
+            // the set after the run and the next batch's slots from it; a set
+            // that ran low is rescanned and ranked in the next A1 / A1b instead
+            update_set(C, cnt, single);
+            const int Cn = __builtin_amdgcn_readfirstlane(sh.sN);   // (in-order LDS: this wave's write)
             if (Cn >= CB_NMIN) {
                 rank_set(Cn);
                 const int K8 = Cn < CB_W ? Cn : CB_W;
