@@ -1064,8 +1064,8 @@ __device__ __forceinline__ void coniss_tree_b(const SweepDev &sd, double *cost0,
     // (a, b and ls of every merge), add the new costs <= T -- still every
     // position with cost <= T (costs change only there).  Lane pairs (entry
     // e = 8 h + (l >> 3), merge q = l & 7): does merge q change entry e's
-    // position?  Run by the ranking wave during A4 (the slots' windows and new
-    // costs stay in LDS until the next A2).
+    // position?  Run by the ranking wave during wave 0's A3 (the slots'
+    // windows and new costs stay in LDS until the next A2).
     auto update_set = [&](int C, int cnt, bool single) {
         if (single) {
             if (lane == 0) sh.sN = -1;
@@ -1274,6 +1274,7 @@ __device__ __forceinline__ void coniss_tree_b(const SweepDev &sd, double *cost0,
             const double fm = (double)(eb - a + 1), fl = (double)(a - ls), fr = (double)(er - r + 1);
             double ul = ward_part<NS>(sl, fl, sm, fm, last_in);
             double ur = ward_part<NS>(sm, fm, sr, fr, last_in);
+            TP_BSTAMP(7);   // (stamps build: window + rows landed)
             wave_sum2(ul, ur);
             const double ql = pin_d(ul / (fl * fm * (fl + fm)));
             const double qr = pin_d(ur / (fm * fr * (fm + fr)));
@@ -1287,6 +1288,22 @@ __device__ __forceinline__ void coniss_tree_b(const SweepDev &sd, double *cost0,
         TP_BSTAMP(2);
         lds_barrier();   // B2
         TP_BSTAMP(3);
+        if (w == CB_W - 1) {
+            // the ranking wave: the run's length as wave 0 finds it below (the
+            // same slots, the same ballots), then the candidate set after the
+            // run, beside wave 0's A3 (which reads neither the set nor sN)
+            const int si = lane >> 3, sj = lane & 7;
+            const int4 wi = sh.win[si], wj = sh.win[sj];
+            const double ki = sh.key[si];
+            const int ai = sh.ka[si], aj = sh.ka[sj];
+            const double clj = sh.cl[sj], crj = sh.cr[sj];
+            const bool pair = sj < si && si < kc;
+            const unsigned long long cm = __ballot(pair && !(wi.y < wj.x || wj.y < wi.x));
+            const int kacc = cm ? (int)(__builtin_ctzll(cm) >> 3) : kc;
+            const bool und = (wj.z >= 0 && key_lt(clj, wj.z, ki, ai)) || (wj.w >= 0 && key_lt(crj, aj, ki, ai));
+            const unsigned long long pm = __ballot(pair && si < kacc && und);
+            update_set(C, pm ? (int)(__builtin_ctzll(pm) >> 3) : kacc, single);
+        }
         // ---- A3 (wave 0): the conflict-free prefix and the leading run, lane
         // l comparing slot i = l >> 3 with an earlier slot j = l & 7; the
         // run's heights, costs and links
@@ -1397,9 +1414,9 @@ __device__ __forceinline__ void coniss_tree_b(const SweepDev &sd, double *cost0,
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         if (w == CB_W - 1) {
-            // the set after the run and the next batch's slots from it; a set
-            // that ran low is rescanned and ranked in the next A1 / A1b instead
-            update_set(C, cnt, single);
+            // the next batch's slots from the set after the run (updated by
+            // this wave during A3); a set that ran low is rescanned and ranked
+            // in the next A1 / A1b instead
             const int Cn = __builtin_amdgcn_readfirstlane(sh.sN);   // (in-order LDS: this wave's write)
             if (Cn >= CB_NMIN) {
                 rank_set(Cn);

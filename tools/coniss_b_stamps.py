@@ -24,8 +24,8 @@ st = ctypes.c_int(0)
 L.tp_debug_last_scores(ctypes.byref(ctypes.c_int(n)), ctypes.byref(ctypes.c_int(k)),
                        P.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), ctypes.byref(st))
 _lib.check(st)
-names = ["A1b rank", "B1", "A2 win+rows+ward", "B2", "A3 run+costs", "B3", "A4 stores", "-", "A4 blkmin", "B4",
-         "A1 scan+B0"]
+names = ["A1b rank", "B1", "A2 ward+writes", "B2", "A3 run+costs", "B3", "A4 stores", "A2 window+rows", "A4 blkmin",
+         "B4", "A1 scan+B0"]
 
 for kb in (1, 0):
     G.knob(52, kb)
