@@ -1937,7 +1937,8 @@ extern "C" {
  *     global link-only CONISS (0: never),
  *  49 the LDS CONISS with one 16-bit link array (3, default: where the 16-byte
  *     variant does not fit; 1: lean sweeps; 2: every sweep; 0: never),
- *  52 the batched CONISS (2, default: every sweep; 1: not lean ones; 0: never).
+ *  52 the batched CONISS (3, default: every sweep, lean ones in storage mode 1
+ *     where it fits; 2: every sweep; 1: not lean ones; 0: never).
  * Process-wide hooks (not path choices):
  *  25 events around every Krylov product when timings are requested,
  *  30 the next N sharded waits with a live communicator fail as device errors,

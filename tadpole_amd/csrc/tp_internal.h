@@ -31,7 +31,8 @@ struct Knobs {
     int pd_cspace = 1;           // 45: C-space Krylov products on int8 digits
     int coniss_lean_min = 0;     // 48: lean sweeps from this many bins take the global link-only CONISS
     int coniss_lds2 = 3;         // 49: LDS CONISS with one 16-bit link array (3: where 16 bytes a bin do not fit)
-    int coniss_batch = 2;        // 52: batched CONISS (2: every sweep; 1: not lean ones; 0: never)
+    int coniss_batch = 3;        // 52: batched CONISS (3: every sweep, lean ones in mode 1 where it fits;
+                                 // 2: every sweep; 1: not lean ones; 0: never)
 };
 extern thread_local Knobs t_knob;
 

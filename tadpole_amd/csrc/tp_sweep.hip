@@ -2049,8 +2049,10 @@ static void launch_coniss_bs(const SweepDev &sd, double *cost0, size_t lds, hipS
     hipLaunchKernelGGL((k_coniss_t<STAMPS, BS, GLB, LU>), dim3(sd.ntrees), dim3(128), lds, s, sd, cost0);
 }
 // knob 52: the batched CONISS kernel (k_coniss_b) where it applies (k <= 256,
-// up to ~38k bins) -- 2 (default): also for lean sweeps (C4, 8 streams:
-// 0.265 -> 0.229 s), 1: not for them, 0: never (the two-wave k_coniss_t)
+// up to ~38k bins) -- 3 (default): also for lean sweeps, which take storage
+// mode 1 where mode 0 would fit (10 bytes a bin: two trees share a CU; C4, 8
+// streams: 0.224 -> 0.214 s), 2: lean sweeps in mode 0 (C4 0.265 -> 0.229 s
+// against the two-wave kernel), 1: not for lean sweeps, 0: never (k_coniss_t)
 // lean sweeps (another pipeline in flight on the device) of matrices that fit
 // LDS, from this many bins (knob 48; 0: never): costs global and only the
 // links in LDS (2 bytes a bin) so several trees share a CU -- the LDS
@@ -2113,7 +2115,10 @@ static void run_coniss(const SweepDev &sd_in, hipStream_t s, bool stamped, Ctx *
     const size_t lds_b0 = coniss_lds_bytes(sd.n) + (size_t)nbk * 8;
     const size_t lds_b1 = coniss_cost_stride(sd.n) * 8 + l16 + (size_t)nbk * 8;
     const size_t lds_b2 = l16 + (size_t)nbk * 8;
-    const int mode = (bs <= 3 && lds_b0 <= cap_b) ? 0 : (bs <= 3 && lds_b1 <= cap_b) ? 1
+    // knob 52 = 3: lean sweeps (another pipeline in flight) take mode 1 where
+    // mode 0 would fit, so two trees share a CU's LDS
+    const bool lean1 = sd.lds_lean && t_knob.coniss_batch == 3;
+    const int mode = (bs <= 3 && lds_b0 <= cap_b && !lean1) ? 0 : (bs <= 3 && lds_b1 <= cap_b) ? 1
                      : (bs <= 11 && sd.n + 64 < 0xFFFF && lds_b2 <= cap_b) ? 2 : -1;
     if (t_knob.coniss_batch && sd.tree0 + sd.ntrees <= 256 && mode >= 0 && !lean_small &&
         !(sd.lds_lean && t_knob.coniss_batch < 2)) {
