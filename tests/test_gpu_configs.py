@@ -324,6 +324,23 @@ def test_lds_lean_coniss_same_bits(gpu, n):
         assert np.array_equal(a[key], b[key], equal_nan=key in ("scores", "height")), key
 
 
+@pytest.mark.parametrize("n", [2100, 7808, 16000])
+def test_lds_lean_batched_coniss_same_bits(gpu, n):
+    """The default lean sweep (TP_FLAG_LDS_LEAN, knob 52 = 3): the batched CONISS
+    in storage mode 1 (costs in LDS, 16-bit links: two trees a CU) where the
+    default sweep takes mode 0, mode 2 at 16 000 bins -- every merge, height and
+    score is the default sweep's."""
+    from tadpole_amd import _lib
+    from tadpole_amd.api import _pipeline
+    m = synth_hic(n, SEED_BASE + 96)
+    a = _pipeline(m, 60, 2, 0.01, 0, 0)
+    b = _pipeline(m, 60, 2, 0.01, _lib.TP_FLAG_LDS_LEAN, 0)
+    for key in ("k", "w", "n_pcs", "n_clusters"):
+        assert a[key] == b[key], key
+    for key in ("good", "n_cluster", "scores", "merge", "height", "boundary"):
+        assert np.array_equal(a[key], b[key], equal_nan=key in ("scores", "height")), key
+
+
 @pytest.mark.parametrize("n", [700, 2100, 7808, 11000])
 def test_lds_link_only_coniss_same_bits(gpu, n):
     """Knob 49: the LDS variant keeps one 16-bit link array after the costs (10
