@@ -906,7 +906,10 @@ constexpr int CB_W = 8;      // waves a tree = most candidates a batch
 constexpr int CB_CAP = 16;   // positions <= T ranked a batch (16 x 16 lane pairs)
 constexpr int CB_FMAX = 16;  // flagged blocks a batch (two a wave)
 constexpr int CB_SEG = 8;    // positions <= T a wave may contribute
-constexpr int CB_NMIN = 3;   // rescan when the maintained candidate set holds fewer
+#ifndef TP_CB_NMIN
+#define TP_CB_NMIN 2   // (3: C3 6.30 ms, 24.3k 27.5; 2: 6.22, 26.8; 5: 6.53, 28.5)
+#endif
+constexpr int CB_NMIN = TP_CB_NMIN;   // rescan when the maintained candidate set holds fewer
 #ifndef TP_CB_LO             // the gap adapts so a scan finds about LO..HI positions <= T
 #define TP_CB_LO 10          // (6..10: C3 7.0 ms; 8..12: 6.8; 10..14: 6.67; 12..15: 6.66)
 #endif

@@ -8,7 +8,7 @@ tools/coniss_batch_emu.py"""
 import sys, numpy as np
 NAN = float('nan')
 W, CAP, FMAX, SEG = 8, 16, 16, 8   # SEG: positions <= T a wave may contribute (CB_SEG)
-NMIN = 3                           # rescan when the maintained set holds fewer (CB_NMIN)
+NMIN = 2                           # rescan when the maintained set holds fewer (CB_NMIN)
 
 def ward(sa, na, sb, nb):
     e = sa * nb - sb * na
