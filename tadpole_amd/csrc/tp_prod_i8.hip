@@ -677,7 +677,10 @@ __global__ void __launch_bounds__(512, 1) k_pd_prodA(const int8_t *__restrict__ 
 
 // k chunks from K alone (shards agree); <= 16384 rows a chunk (accumulator range)
 #ifndef TP_PD_KDIV
-#define TP_PD_KDIV 960   // C3: 8 k chunks, 984 workgroups (~4 full rounds of one a CU; 1024: 7, 861)
+#define TP_PD_KDIV 1920  // C3: 4 k chunks, 244 k_pd_prodA workgroups (one round of one a CU): the 32
+                         // products with digits and reductions 3.97 -> 3.45 ms against 8 chunks
+                         // (3 chunks: 3.94, 2: 4.97 -- fewer workgroups than CUs); 24.3k (C space,
+                         // 12 chunks): 33.2 -> ~31 ms
 #endif
 static int pd_kchunk(int Kp) {
     const int S = std::max(1, std::min(16, Kp / TP_PD_KDIV));
