@@ -288,18 +288,22 @@ __global__ void __launch_bounds__(64 * PD_CM_W) k_pd_digits_cm(const double *__r
 // its 32 k-rows of digit work a thread on a quarter of the chip.  Work item q
 // = slice * N + column, dealt XCD-contiguously so columns c and c + 1 of a
 // slice (the two halves of each 128-byte line of the image) share an L2.
-template <int IT>
+#ifndef TP_PD_SPW
+#define TP_PD_SPW 4   // 1024-row slices a k_pd_digits_blk workgroup digitises (each reads its whole column
+                      // for the scale): C3 products with digits 3.49 -> 3.35 ms against 1 (2: 3.39)
+#endif
+template <int IT, int SPW = 1>
 __global__ void __launch_bounds__(256) k_pd_digits_blk(const double *__restrict__ X, int ldx, int K, int N, int Kp,
                                                        int8_t *__restrict__ D, double *__restrict__ scale) {
     __shared__ double red[4];
     const int G = (int)gridDim.x;
     const int q = (int)(blockIdx.x & 7) * (G >> 3) + (int)(blockIdx.x >> 3);
-    const int c = q % N, sl = q / N;
+    const int c = q % N, sg = q / N;   // slices SPW sg .. SPW sg + SPW - 1
     const int t = threadIdx.x;
     const double *x = X + (size_t)c * ldx;
     double mx = 0.0;
     bool bad = false;
-    double v[4];
+    double v[SPW][4];
 #pragma unroll
     for (int i = 0; i < IT; ++i)
 #pragma unroll
@@ -308,7 +312,7 @@ __global__ void __launch_bounds__(256) k_pd_digits_blk(const double *__restrict_
             const double y = k < K ? x[k] : 0.0;
             mx = fmax(mx, fabs(y));
             bad |= !isfinite(y);
-            if (i == sl) v[u] = y;
+            if (i / SPW == sg) v[i % SPW][u] = y;
         }
     mx = bad ? INFINITY : mx;
 #pragma unroll
@@ -317,9 +321,13 @@ __global__ void __launch_bounds__(256) k_pd_digits_blk(const double *__restrict_
     __syncthreads();
     mx = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
     const int e = pd_exp(mx);   // mx < 2^e
-    if (sl == 0 && t == 0) scale[c] = isfinite(mx) ? ldexp(1.0, e - 54) : NAN;
-    const int k0 = 1024 * sl + 4 * t;
-    if (k0 < Kp) pd_digits4<PD_DIG>(v, 4, 0, isfinite(mx), ldexp(1.0, 54 - e), D + pd_off<PD_DIG>(c, k0, Kp / 64));
+    if (sg == 0 && t == 0) scale[c] = isfinite(mx) ? ldexp(1.0, e - 54) : NAN;
+#pragma unroll
+    for (int h = 0; h < SPW; ++h) {
+        const int k0 = 1024 * (SPW * sg + h) + 4 * t;
+        if (k0 < Kp)
+            pd_digits4<PD_DIG>(v[h], 4, 0, isfinite(mx), ldexp(1.0, 54 - e), D + pd_off<PD_DIG>(c, k0, Kp / 64));
+    }
 }
 
 // The same digits for a few columns (a Krylov block, N = 64): the column's
@@ -772,8 +780,8 @@ int prod_i8_partials(Ctx &c, const ProdDigits &pd, int r0, int M, const double *
     const int SL = (pd.Kp + 1023) / 1024;
     double *pmax = (double *)(bb + (PD_DIG * slb + 255) / 256 * 256 + 512 * sizeof(double));
     if (pd.Kp <= 1024 * PD_REG_IT && cfg_pd_digits_blk) {   // one launch, a workgroup per (column, slice)
-        hipLaunchKernelGGL((k_pd_digits_blk<PD_REG_IT>), dim3((unsigned)(N * SL)), dim3(256), 0, s, B, ldb, K, N, pd.Kp,
-                           Db, cs);
+        hipLaunchKernelGGL((k_pd_digits_blk<PD_REG_IT, TP_PD_SPW>), dim3((unsigned)(N * ((SL + TP_PD_SPW - 1) / TP_PD_SPW))),
+                           dim3(256), 0, s, B, ldb, K, N, pd.Kp, Db, cs);
     } else if (pd.Kp <= 1024 * PD_REG_IT) {   // one launch, the block read once
         hipLaunchKernelGGL((k_pd_digits_reg<PD_REG_IT, PD_DIG>), dim3((unsigned)N), dim3(256), 0, s, B, ldb, K, N, pd.Kp,
                            Db, cs);
