@@ -54,3 +54,22 @@ def test_r_error_message_entry():
     arr = (ctypes.c_char_p * 1)(ctypes.cast(buf, ctypes.c_char_p))
     n = ctypes.c_int(64)
     L.tp_last_error_r(arr, ctypes.byref(n))   # must not crash; fills a caller buffer
+
+
+def test_run_time_switch_table():
+    """tp_debug_knob (no GPU work): the 13 run-time switches and the four test
+    hooks are accepted and return their previous value; the switches of
+    earlier rounds, now compile-time constants (round 6), are refused with
+    TP_ERR_ARG; knob 36 takes only the product kernels that remain."""
+    switches = {1: 0, 5: 1, 8: 4096, 18: 1, 20: -1, 24: 1, 36: 5, 43: 2, 44: 1, 45: 1, 48: 0, 49: 3, 52: 3}
+    for which, default in switches.items():
+        assert _lib.debug_knob(which, default) == default, which
+    for hook in (25, 30, 41, 51):
+        old = _lib.debug_knob(hook, 0)
+        _lib.debug_knob(hook, old)
+    for gone in (0, 2, 3, 4, 6, 7, 9, 16, 17, 19, 28, 29, 32, 33, 34, 35, 37, 38, 39, 40, 46, 47, 50):
+        with pytest.raises(Exception, match="unknown knob"):
+            _lib.debug_knob(gone, 0)
+    with pytest.raises(Exception, match="knob 36"):
+        _lib.debug_knob(36, 2)
+    assert _lib.debug_knob(36, 5) == 5
