@@ -911,10 +911,11 @@ constexpr int CB_SEG = 8;    // positions <= T a wave may contribute
 #endif
 constexpr int CB_NMIN = TP_CB_NMIN;   // rescan when the maintained candidate set holds fewer
 #ifndef TP_CB_LO             // the gap adapts so a scan finds about LO..HI positions <= T
-#define TP_CB_LO 10          // (6..10: C3 7.0 ms; 8..12: 6.8; 10..14: 6.67; 12..15: 6.66)
+#define TP_CB_LO 12          // (6..10: C3 7.0 ms; 8..12: 6.8; 10..14: 6.67; 12..15: 6.66; with a
+                             // rescan below 2 kept: 8..12 6.38, 10..14 6.33, 12..15 6.26)
 #endif
 #ifndef TP_CB_HI
-#define TP_CB_HI 14
+#define TP_CB_HI 15
 #endif
 static_assert(CB_W * CB_SEG == 64, "one segment entry a lane");
 struct CbShared {

@@ -103,7 +103,7 @@ def kernel(p):
                     segn[w] = SEG + 1
             if max(segn) <= SEG and CAP >= sum(segn) >= 1:
                 C = sum(segn); cands = ent; Tset = T
-                if tries <= 5: gap *= 1.3 if C < 10 else (0.8 if C > 14 else 1.0)   # TP_CB_LO / TP_CB_HI
+                if tries <= 5: gap *= 1.3 if C < 12 else (0.8 if C > 15 else 1.0)   # TP_CB_LO / TP_CB_HI
                 break
             if tries >= 6:                                 # the exact argmin alone
                 pos = min([q_ for q_ in range(n) if cost[q_] == gq])
